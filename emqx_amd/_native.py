@@ -1,0 +1,134 @@
+"""ctypes binding of libemqx_tm.so (include/emqx_tm.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module
+raises at import, and match calls on an engine without a device fail with
+TM_ENODEV.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libemqx_tm.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "emqx_tm.h")
+
+TM_OK = 0
+TM_ENOENT = -2
+TM_EIO = -5
+TM_ENOMEM = -12
+TM_ENODEV = -19
+TM_EINVAL = -22
+TM_EOVERFLOW = -75
+TM_EABORT = -125
+TM_NONE = 0xFFFFFFFF
+TM_MAX_TOPIC_LEN = 4096
+
+_ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
+             TM_EINVAL: "EINVAL", TM_EOVERFLOW: "EOVERFLOW", TM_EABORT: "EABORT"}
+
+
+class TmError(RuntimeError):
+    def __init__(self, rc, what=""):
+        self.rc = rc
+        super().__init__(f"{what}: {_ERRNAMES.get(rc, rc)}")
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("init_slots", C.c_uint32), ("host_threads", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+class TrieNode(C.Structure):
+    _fields_ = [("edge_count", C.c_uint32), ("has_topic", C.c_uint32), ("filter_id", C.c_uint32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_matches", C.c_uint64),
+                ("row_offsets", C.POINTER(C.c_uint32)), ("filter_ids", C.POINTER(C.c_uint32))]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("topics", C.c_uint64), ("visits", C.c_uint64), ("hash_hits", C.c_uint64),
+                ("words", C.c_uint64), ("matches", C.c_uint64), ("slow_topics", C.c_uint64),
+                ("overflow_tiles", C.c_uint64), ("ms_match", C.c_float), ("ms_total", C.c_float)]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class EngineStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("version", "nodes", "edges", "filters", "words", "slots",
+                                          "device_bytes", "uploads_full", "uploads_delta", "delta_slots")]
+
+    def asdict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+# exported symbol -> (restype, argtypes); must cover every declaration in include/emqx_tm.h
+P = C.c_void_p
+SZ = C.c_size_t
+U8P = C.c_char_p
+SIGNATURES = {
+    "tm_create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+    "tm_destroy": (None, [P]),
+    "tm_version": (C.c_uint64, [P]),
+    "tm_stats": (C.c_int, [P, C.POINTER(EngineStats)]),
+    "tm_sync": (C.c_int, [P]),
+    "tm_trie_insert": (C.c_int, [P, U8P, SZ]),
+    "tm_trie_delete": (C.c_int, [P, U8P, SZ]),
+    "tm_trie_lookup": (C.c_int, [P, U8P, SZ, C.c_int, C.POINTER(TrieNode)]),
+    "tm_trie_empty": (C.c_int, [P]),
+    "tm_trie_match": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "tm_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_batch_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
+    "tm_batch_launch": (C.c_int, [P, P]),
+    "tm_batch_wait": (C.c_int, [P, P]),
+    "tm_batch_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
+    "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
+    "tm_batch_free": (None, [P, P]),
+    "tm_filter_bytes": (C.POINTER(C.c_uint8), [P, C.c_uint32, C.POINTER(SZ)]),
+    "tm_filter_id": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32)]),
+    "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),
+    "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
+    "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),
+    "tm_last_error": (C.c_char_p, []),
+    "tm_build_info": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built (run __graft_entry__.build()); "
+                              "the HIP engine is required -- there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc < 0:
+        detail = ""
+        if rc == TM_EIO and _lib is not None:
+            detail = " [" + (_lib.tm_last_error() or b"").decode(errors="replace") + "]"
+        raise TmError(rc, what + detail)
+    return rc
+
+
+def gpu_available() -> bool:
+    """True when a HIP device is visible (checked without initialising HIP twice)."""
+    try:
+        import torch
+        return torch.cuda.is_available() and torch.cuda.device_count() > 0
+    except Exception:
+        return False

@@ -1,0 +1,60 @@
+"""In-tree build of the native libraries (no cmake/ninja, no JIT cache).
+
+    python -m emqx_amd.build          # libemqx_tm.so (gfx950) + libemqx_gen.so
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+TM_SOURCES = ["tm_engine.cpp", "tm_kernels.hip"]
+TM_HEADERS = ["tm_internal.hpp", os.path.join("..", "..", "include", "emqx_tm.h")]
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_tm(force=False):
+    out = os.path.join(HERE, "libemqx_tm.so")
+    deps = [os.path.join(CSRC, f) for f in TM_SOURCES + TM_HEADERS]
+    if force or _stale(out, deps):
+        tmp = out + ".tmp"
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-fvisibility=hidden", "-Wall", "-o", tmp] + [os.path.join(CSRC, f) for f in TM_SOURCES]
+             + ["-lpthread"])
+        os.replace(tmp, out)
+    return out
+
+
+def build_gen(force=False):
+    out = os.path.join(HERE, "libemqx_gen.so")
+    src = os.path.join(CSRC, "tm_gen.c")
+    if force or _stale(out, [src]):
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall", "-o", out, src, "-lm"])
+    return out
+
+
+def build_all(force=False):
+    return [build_tm(force), build_gen(force)]
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

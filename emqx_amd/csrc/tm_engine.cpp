@@ -1,0 +1,1297 @@
+// tm_engine.cpp -- host side of the MI355X topic-matching engine + C ABI.
+//
+// Owns: the word interner (emqx_topic:words/1 tokens -> u32 ids), the host
+// mirror of the compiled trie (node table + the open-addressed edge hash that is
+// byte-identical to the HBM replica), the delta log that keeps the replica in
+// sync (read-your-writes: deltas are applied on the engine stream before every
+// match launch), batch tokenisation, and the orchestration of the device
+// pipeline in tm_kernels.hip.
+//
+// Trie semantics follow src/emqx_trie.erl exactly (insert/1 :81-93, add_path/1
+// :145-158, delete/1 :107-116, delete_path/1 :190-204, lookup/1, empty/0); the
+// node record's edge_count is kept so that emqx_trie:lookup/1 answers match
+// the reference's tests (test/emqx_trie_SUITE.erl:49-142).
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/emqx_tm.h"
+#include "tm_internal.hpp"
+
+using namespace etm;
+
+namespace {
+
+#define HIP_OK(expr)                                                        \
+    do {                                                                    \
+        hipError_t _e = (expr);                                             \
+        if (_e != hipSuccess) {                                             \
+            snprintf(last_error(), 512, "%s at tm_engine.cpp:%d (%s)",      \
+                     hipGetErrorString(_e), __LINE__, #expr);               \
+            return TM_EIO;                                                  \
+        }                                                                   \
+    } while (0)
+
+char* last_error() {
+    static thread_local char buf[512] = "";
+    return buf;
+}
+
+inline uint64_t hash_bytes(const uint8_t* p, size_t n) {
+    uint64_t h = 0xcbf29ce484222325ull ^ (n * 0x9E3779B97F4A7C15ull);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t v;
+        memcpy(&v, p + i, 8);
+        h = (h ^ (v * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+        h ^= h >> 29;
+    }
+    uint64_t t = 0;
+    for (size_t k = 0; i < n; ++i, ++k) t |= (uint64_t)p[i] << (8 * k);
+    h = (h ^ (t * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+    h ^= h >> 31;
+    return h | 1;  // 0 = empty slot
+}
+
+// ------------------------------------------------------------- word interner
+// Open-addressed string -> id map; bytes live in an append-only arena.
+class WordDict {
+  public:
+    WordDict() { rehash(1024); }
+
+    uint32_t find(const uint8_t* p, size_t n) const {
+        const uint64_t h = hash_bytes(p, n);
+        size_t i = h & mask_;
+        for (;;) {
+            const Ent& e = tab_[i];
+            if (e.h == 0) return W_UNKNOWN;
+            if (e.h == h && e.len == n && memcmp(arena_.data() + e.off, p, n) == 0) return e.id;
+            i = (i + 1) & mask_;
+        }
+    }
+
+    uint32_t intern(const uint8_t* p, size_t n) {
+        uint32_t id = find(p, n);
+        if (id != W_UNKNOWN) return id;
+        if ((count_ + 1) * 2 > tab_.size()) rehash(tab_.size() * 2);
+        id = next_id_++;
+        const uint64_t h = hash_bytes(p, n);
+        size_t i = h & mask_;
+        while (tab_[i].h) i = (i + 1) & mask_;
+        tab_[i] = Ent{h, arena_.size(), (uint32_t)n, id};
+        arena_.insert(arena_.end(), p, p + n);
+        ++count_;
+        return id;
+    }
+
+    size_t size() const { return count_; }
+
+  private:
+    struct Ent {
+        uint64_t h;
+        uint64_t off;
+        uint32_t len;
+        uint32_t id;
+    };
+    void rehash(size_t cap) {
+        std::vector<Ent> old;
+        old.swap(tab_);
+        tab_.assign(cap, Ent{0, 0, 0, 0});
+        mask_ = cap - 1;
+        for (const Ent& e : old)
+            if (e.h) {
+                size_t i = e.h & mask_;
+                while (tab_[i].h) i = (i + 1) & mask_;
+                tab_[i] = e;
+            }
+    }
+    std::vector<Ent> tab_;
+    std::vector<uint8_t> arena_;
+    size_t mask_ = 0, count_ = 0;
+    uint32_t next_id_ = W_FIRST;
+};
+
+struct TWord {
+    const uint8_t* p;
+    uint32_t n;
+};
+
+// binary:split(T, <<"/">>, [global]) (src/emqx_topic.erl:153-154)
+inline void split_words(const uint8_t* t, size_t len, std::vector<TWord>& out) {
+    out.clear();
+    size_t start = 0;
+    for (size_t i = 0; i <= len; ++i) {
+        if (i == len || t[i] == '/') {
+            out.push_back(TWord{t + start, (uint32_t)(i - start)});
+            start = i + 1;
+        }
+    }
+}
+
+inline bool is_plus(const TWord& w) { return w.n == 1 && w.p[0] == '+'; }
+inline bool is_hash(const TWord& w) { return w.n == 1 && w.p[0] == '#'; }
+
+// word class for the path-code digits (tm_internal.hpp C_*), and whether the
+// word makes the topic irregular (starts with '+' but is not '+').
+inline uint32_t word_class(const TWord& w, bool& irregular) {
+    if (w.n == 0) return C_EMPTY;
+    const uint8_t c = w.p[0];
+    if (w.n == 1 && c == '+') return C_ABOVE;
+    if (c == '+') { irregular = true; return C_ABOVE; }
+    if (c < '#') return C_BELOW;
+    if (c < '+') return C_BETWEEN;
+    return C_ABOVE;
+}
+
+template <class T>
+void dev_free(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+template <class T>
+int dev_reserve(T*& p, size_t& cap, size_t n, bool keep = false, size_t keep_n = 0) {
+    if (n <= cap && p) return TM_OK;
+    size_t nc = std::max<size_t>(n + n / 4, 1024);
+    T* np = nullptr;
+    HIP_OK(hipMalloc((void**)&np, nc * sizeof(T)));
+    if (keep && p && keep_n) HIP_OK(hipMemcpy(np, p, keep_n * sizeof(T), hipMemcpyDeviceToDevice));
+    dev_free(p);
+    p = np;
+    cap = nc;
+    return TM_OK;
+}
+
+template <class T>
+int host_reserve(T*& p, size_t& cap, size_t n) {
+    if (n <= cap && p) return TM_OK;
+    size_t nc = std::max<size_t>(n + n / 4, 1024);
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    HIP_OK(hipHostMalloc((void**)&p, nc * sizeof(T), hipHostMallocDefault));
+    cap = nc;
+    return TM_OK;
+}
+
+unsigned default_threads() {
+    unsigned h = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(h ? h : 1u, 16u));
+}
+
+}  // namespace
+
+// ===================================================================== batch
+
+struct tm_batch {
+    uint32_t n = 0;
+    uint64_t nwords = 0;
+    uint64_t dict_size = 0;     // interner size at tokenisation (re-tokenise if it grew)
+    // host copy of the input (to re-tokenise after concurrent subscribes)
+    std::vector<uint8_t> bytes;
+    std::vector<uint64_t> offs;
+    // host tokens
+    std::vector<uint32_t> h_words, h_toff, h_slow;
+    std::vector<uint8_t> h_tflags;
+    // device inputs
+    uint32_t *d_words = nullptr, *d_toff = nullptr, *d_slow = nullptr;
+    uint8_t* d_tflags = nullptr;
+    size_t c_words = 0, c_toff = 0, c_slow = 0, c_tflags = 0;
+    // device outputs
+    uint32_t *d_count = nullptr, *d_fids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
+    unsigned long long *d_src = nullptr, *d_rkeys = nullptr;
+    uint32_t *d_bsums = nullptr, *d_ctrl = nullptr, *d_ovf = nullptr, *d_total = nullptr;
+    unsigned long long* d_stats = nullptr;
+    size_t c_count = 0, c_src = 0, c_fids = 0, c_rkeys = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
+    uint64_t slow_cap = 0;      // slow-path region of fids[] (after the n * K fast rows)
+    size_t c_ctrl = 0, c_stats = 0, c_total = 0;
+    // pinned host results
+    uint32_t* h_rowoff = nullptr;
+    uint32_t* h_ids = nullptr;
+    uint32_t* h_ctrl = nullptr;
+    unsigned long long* h_stats = nullptr;
+    size_t ch_rowoff = 0, ch_ids = 0, ch_ctrl = 0, ch_stats = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    bool launched = false, done = false;
+    uint64_t total = 0;
+    tm_batch_stats st{};
+
+    void release() {
+        dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
+        dev_free(d_count); dev_free(d_src); dev_free(d_fids); dev_free(d_rkeys); dev_free(d_rowoff); dev_free(d_ids);
+        dev_free(d_bsums); dev_free(d_ctrl); dev_free(d_ovf); dev_free(d_total); dev_free(d_stats);
+        if (h_rowoff) (void)hipHostFree(h_rowoff);
+        if (h_ids) (void)hipHostFree(h_ids);
+        if (h_ctrl) (void)hipHostFree(h_ctrl);
+        if (h_stats) (void)hipHostFree(h_stats);
+        h_rowoff = h_ids = h_ctrl = nullptr;
+        h_stats = nullptr;
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (ev2) (void)hipEventDestroy(ev2);
+        ev0 = ev1 = ev2 = nullptr;
+    }
+};
+
+// ==================================================================== engine
+
+struct tm_engine {
+    std::recursive_mutex mu;
+    int device = -1;
+    unsigned threads = 1;
+    hipStream_t stream = nullptr;
+
+    WordDict dict;
+
+    // node table (host)
+    std::vector<uint32_t> n_parent, n_word, n_ec, n_plus, n_hash, n_bloom, n_inslot, n_flen;
+    std::vector<uint64_t> n_foff;
+    std::vector<uint8_t> n_live, n_topic;
+    std::vector<uint32_t> free_nodes;
+    uint64_t live_nodes = 0, live_edges = 0, n_filters = 0;
+    std::vector<uint8_t> fbytes;
+
+    // edge hash (host mirror of the HBM replica)
+    std::vector<Slot> slots;
+    uint64_t used_slots = 0;   // live + tombstones
+    uint32_t max_disp = 0;
+
+    // delta log
+    std::vector<uint32_t> dirty;
+    std::vector<uint8_t> dirty_mark;
+    std::vector<uint32_t> dirty_f;
+    std::vector<uint8_t> dirty_f_mark;
+    bool full_dirty = true;
+    bool full_f_dirty = true;
+    uint64_t fbytes_uploaded = 0;
+
+    // device replica
+    Slot* d_slots = nullptr;
+    size_t d_nslots = 0;
+    uint64_t* d_foff = nullptr;
+    uint32_t* d_flen = nullptr;
+    size_t c_foff = 0, c_flen = 0;
+    uint8_t* d_fbytes = nullptr;
+    size_t c_fbytes = 0;
+    // delta staging
+    uint32_t* h_didx = nullptr;
+    Slot* h_dval = nullptr;
+    uint32_t* d_didx = nullptr;
+    Slot* d_dval = nullptr;
+    size_t ch_didx = 0, ch_dval = 0, cd_didx = 0, cd_dval = 0;
+    uint32_t* h_fidx = nullptr;
+    uint64_t* h_foffv = nullptr;
+    uint32_t* h_flenv = nullptr;
+    uint32_t* d_fidx = nullptr;
+    uint64_t* d_foffv = nullptr;
+    uint32_t* d_flenv = nullptr;
+    size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0, cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
+    hipEvent_t ev_delta = nullptr;
+    bool delta_inflight = false;
+
+    // slow-path scratch
+    uint32_t s_waves = 128, s_qcap = 1u << 14, s_ocap = 1u << 15;
+    uint32_t *d_sqpar = nullptr, *d_sqpw = nullptr, *d_sqmeta = nullptr, *d_sofid = nullptr;
+    unsigned long long *d_sqkey = nullptr, *d_sokey = nullptr;
+    size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
+
+    uint64_t version = 1;
+    uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
+    bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
+    uint32_t row_cap = 64;         // K: fast-path row slots per topic (TM_ROWCAP)
+    uint32_t* d_dbg = nullptr;
+    uint32_t* h_dbg = nullptr;
+    size_t c_dbg = 0, ch_dbg = 0;
+
+    tm_batch scratch;   // reused by tm_match_batch / tm_trie_match
+
+    // ------------------------------------------------------------ hash
+    uint32_t nslots() const { return (uint32_t)slots.size(); }
+    uint32_t bmask() const { return nslots() / 2 - 1; }
+
+    uint32_t find_slot(uint32_t p, uint32_t w) const {
+        uint32_t b = edge_hash(p, w) & bmask();
+        for (uint32_t i = 0; i <= max_disp; ++i) {
+            for (uint32_t s = 0; s < 2; ++s) {
+                const Slot& e = slots[2 * b + s];
+                if (e.parent == p && e.word == w) return 2 * b + s;
+            }
+            if (slots[2 * b].parent == SLOT_EMPTY || slots[2 * b + 1].parent == SLOT_EMPTY) return NONE;
+            b = (b + 1) & bmask();
+        }
+        return NONE;
+    }
+
+    uint32_t place_slot(std::vector<Slot>& tab, uint32_t p, uint32_t w, uint32_t& disp, bool& was_empty) const {
+        const uint32_t mask = (uint32_t)tab.size() / 2 - 1;
+        uint32_t b = edge_hash(p, w) & mask;
+        for (uint32_t i = 0;; ++i) {
+            for (uint32_t s = 0; s < 2; ++s) {
+                Slot& e = tab[2 * b + s];
+                if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) {
+                    disp = i;
+                    was_empty = e.parent == SLOT_EMPTY;
+                    return 2 * b + s;
+                }
+            }
+            b = (b + 1) & mask;
+        }
+    }
+
+    void rehash(size_t want_slots) {
+        size_t ns = 1024;
+        while (ns < want_slots) ns <<= 1;
+        std::vector<Slot> tab(ns);
+        for (Slot& s : tab) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
+        uint32_t md = 0;
+        uint64_t used = 0;
+        for (const Slot& e : slots) {
+            if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) continue;
+            uint32_t disp;
+            bool was_empty;
+            uint32_t i = place_slot(tab, e.parent, e.word, disp, was_empty);
+            tab[i] = e;
+            n_inslot[e.child] = i;
+            md = std::max(md, disp);
+            ++used;
+        }
+        slots.swap(tab);
+        max_disp = md;
+        used_slots = used;
+        full_dirty = true;
+        dirty.clear();
+        dirty_mark.assign(slots.size(), 0);
+    }
+
+    void mark_dirty(uint32_t i) {
+        if (full_dirty) return;
+        if (!dirty_mark[i]) { dirty_mark[i] = 1; dirty.push_back(i); }
+    }
+
+    uint32_t insert_edge(uint32_t p, uint32_t w, uint32_t c) {
+        if ((used_slots + 1) * 2 > slots.size() || max_disp > 24)
+            rehash(std::max<size_t>((live_edges + 1) * 3, slots.size() * (max_disp > 24 ? 2 : 1)));
+        uint32_t disp;
+        bool was_empty;
+        uint32_t i = place_slot(slots, p, w, disp, was_empty);
+        if (was_empty) ++used_slots;
+        max_disp = std::max(max_disp, disp);
+        Slot& e = slots[i];
+        e.parent = p; e.word = w; e.child = c;
+        n_inslot[c] = i;
+        write_summary(c);
+        ++live_edges;
+        return i;
+    }
+
+    void delete_edge_of(uint32_t c) {
+        const uint32_t i = n_inslot[c];
+        Slot& e = slots[i];
+        memset(&e, 0, sizeof(e));
+        e.parent = SLOT_TOMB;
+        e.word = 0;
+        n_inslot[c] = NONE;
+        --live_edges;
+        mark_dirty(i);
+    }
+
+    // ------------------------------------------------------------ nodes
+    uint32_t new_node(uint32_t parent, uint32_t word) {
+        uint32_t id;
+        if (!free_nodes.empty()) { id = free_nodes.back(); free_nodes.pop_back(); }
+        else {
+            id = (uint32_t)n_parent.size();
+            n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
+            n_hash.push_back(NONE); n_bloom.push_back(0); n_inslot.push_back(NONE); n_flen.push_back(0);
+            n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
+        }
+        n_parent[id] = parent; n_word[id] = word; n_ec[id] = 0; n_plus[id] = NONE; n_hash[id] = NONE;
+        n_bloom[id] = 0; n_inslot[id] = NONE; n_live[id] = 1; n_topic[id] = 0;
+        ++live_nodes;
+        return id;
+    }
+
+    void kill_node(uint32_t id) {
+        n_live[id] = 0;
+        n_topic[id] = 0;
+        n_ec[id] = 0;
+        --live_nodes;
+        if (id != ROOT) free_nodes.push_back(id);
+    }
+
+    uint32_t summary_flags(uint32_t c) const {
+        return (n_plus[c] != NONE ? NF_PLUS : 0) | (n_hash[c] != NONE ? NF_HASH : 0);
+    }
+    uint32_t hterm_of(uint32_t c) const {
+        const uint32_t h = n_hash[c];
+        return (h != NONE && n_topic[h]) ? h : NONE;
+    }
+
+    // rewrite c's summary into its incoming slot (or the root record)
+    void write_summary(uint32_t c) {
+        if (c == ROOT) return;   // root record is rebuilt at every launch
+        const uint32_t i = n_inslot[c];
+        if (i == NONE) return;
+        Slot& e = slots[i];
+        e.term = n_topic[c] ? c : NONE;
+        e.hterm = hterm_of(c);
+        e.flags = summary_flags(c);
+        e.bloom = n_bloom[c];
+        e.spare = 0;
+        mark_dirty(i);
+    }
+
+    RootRec root_rec() const {
+        RootRec r;
+        r.live = n_live[ROOT];
+        r.hterm = hterm_of(ROOT);
+        r.flags = summary_flags(ROOT);
+        r.bloom = n_bloom[ROOT];
+        return r;
+    }
+
+    void set_topic(uint32_t c, const uint8_t* bytes, size_t len) {
+        n_topic[c] = 1;
+        ++n_filters;
+        n_foff[c] = fbytes.size();
+        n_flen[c] = (uint32_t)len;
+        fbytes.insert(fbytes.end(), bytes, bytes + len);
+        if (!full_f_dirty) {
+            if (dirty_f_mark.size() < n_parent.size()) dirty_f_mark.resize(n_parent.size(), 0);
+            if (!dirty_f_mark[c]) { dirty_f_mark[c] = 1; dirty_f.push_back(c); }
+        }
+        write_summary(c);
+        if (c != ROOT && n_word[c] == W_HASH) write_summary(n_parent[c]);
+    }
+
+    void clear_topic(uint32_t c) {
+        if (!n_topic[c]) return;
+        n_topic[c] = 0;
+        --n_filters;
+        write_summary(c);
+        if (c != ROOT && n_word[c] == W_HASH) write_summary(n_parent[c]);
+    }
+
+    // intern (insert=true) or look up the words of a filter / node id
+    bool filter_words(const uint8_t* t, size_t len, bool insert, std::vector<uint32_t>& ids) {
+        static thread_local std::vector<TWord> ws;
+        split_words(t, len, ws);
+        ids.clear();
+        for (const TWord& w : ws) {
+            uint32_t id;
+            if (w.n == 0) id = W_EMPTY;
+            else if (is_plus(w)) id = W_PLUS;
+            else if (is_hash(w)) id = W_HASH;
+            else id = insert ? dict.intern(w.p, w.n) : dict.find(w.p, w.n);
+            if (id == W_UNKNOWN) return false;
+            ids.push_back(id);
+        }
+        return true;
+    }
+
+    uint32_t walk(const std::vector<uint32_t>& ids) const {
+        if (!n_live[ROOT]) return NONE;
+        uint32_t n = ROOT;
+        for (uint32_t w : ids) {
+            const uint32_t s = find_slot(n, w);
+            if (s == NONE) return NONE;
+            n = slots[s].child;
+        }
+        return n;
+    }
+
+    // emqx_trie:insert/1 (src/emqx_trie.erl:81-93)
+    int trie_insert(const uint8_t* t, size_t len) {
+        std::vector<uint32_t> ids;
+        filter_words(t, len, true, ids);
+        const uint32_t found = walk(ids);
+        if (found != NONE) {
+            if (!n_topic[found]) { set_topic(found, t, len); ++version; }
+            return TM_OK;
+        }
+        // add_path/1 for every triple (:145-158)
+        uint32_t p = ROOT;
+        for (uint32_t w : ids) {
+            if (!n_live[p]) {               // only the root can be absent here
+                n_live[p] = 1; n_ec[p] = 0; ++live_nodes;
+            }
+            const uint32_t s = find_slot(p, w);
+            uint32_t c;
+            if (s == NONE) {
+                c = new_node(p, w);
+                ++n_ec[p];
+                if (w == W_PLUS) n_plus[p] = c;
+                else if (w == W_HASH) n_hash[p] = c;
+                else n_bloom[p] |= bloom_bit(w);
+                insert_edge(p, w, c);
+                write_summary(p);
+            } else {
+                c = slots[s].child;
+            }
+            p = c;
+        }
+        set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
+        ++version;
+        return TM_OK;
+    }
+
+    // emqx_trie:delete/1 (src/emqx_trie.erl:107-116), delete_path/1 (:190-204)
+    int trie_delete(const uint8_t* t, size_t len) {
+        std::vector<uint32_t> ids;
+        if (!filter_words(t, len, false, ids)) return TM_OK;
+        const uint32_t n = walk(ids);
+        if (n == NONE) return TM_OK;
+        if (n_ec[n] != 0) {
+            if (n_topic[n]) { clear_topic(n); ++version; }
+            return TM_OK;
+        }
+        clear_topic(n);
+        uint32_t child = n;
+        int rc = TM_OK;
+        bool child_dead = false;
+        for (size_t k = ids.size(); k-- > 0;) {
+            const uint32_t p = n_parent[child];
+            const uint32_t w = ids[k];
+            delete_edge_of(child);
+            if (!child_dead) { kill_node(child); child_dead = true; }
+            if (w == W_PLUS) n_plus[p] = NONE;
+            else if (w == W_HASH) n_hash[p] = NONE;
+            if (!n_live[p]) { rc = TM_EABORT; break; }
+            if (n_ec[p] == 1 && !n_topic[p]) {
+                n_ec[p] = 0;
+                if (p == ROOT) { kill_node(p); break; }
+                kill_node(p);
+                child = p;
+                continue;
+            }
+            --n_ec[p];
+            write_summary(p);
+            break;
+        }
+        ++version;
+        return rc;
+    }
+
+    // ------------------------------------------------------------ device sync
+    int ensure_delta_idle() {
+        if (delta_inflight) {
+            HIP_OK(hipEventSynchronize(ev_delta));
+            delta_inflight = false;
+        }
+        return TM_OK;
+    }
+
+    int sync_device() {
+        if (device < 0) return TM_ENODEV;
+        int rc = ensure_delta_idle();
+        if (rc) return rc;
+        // edge hash
+        if (d_nslots != slots.size()) {
+            dev_free(d_slots);
+            HIP_OK(hipMalloc((void**)&d_slots, slots.size() * sizeof(Slot)));
+            d_nslots = slots.size();
+            full_dirty = true;
+        }
+        bool async_used = false, pageable_used = false;
+        if (full_dirty || dirty.size() > slots.size() / 8) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_slots, slots.data(), slots.size() * sizeof(Slot), hipMemcpyHostToDevice, stream));
+            ++uploads_full;
+            full_dirty = false;
+            for (uint32_t i : dirty) dirty_mark[i] = 0;
+            dirty.clear();
+            if (dirty_mark.size() != slots.size()) dirty_mark.assign(slots.size(), 0);
+        } else if (!dirty.empty()) {
+            const size_t nd = dirty.size();
+            if ((rc = host_reserve(h_didx, ch_didx, nd))) return rc;
+            if ((rc = host_reserve(h_dval, ch_dval, nd))) return rc;
+            if ((rc = dev_reserve(d_didx, cd_didx, nd))) return rc;
+            if ((rc = dev_reserve(d_dval, cd_dval, nd))) return rc;
+            for (size_t k = 0; k < nd; ++k) {
+                h_didx[k] = dirty[k];
+                h_dval[k] = slots[dirty[k]];
+                dirty_mark[dirty[k]] = 0;
+            }
+            HIP_OK(hipMemcpyAsync(d_didx, h_didx, nd * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_dval, h_dval, nd * sizeof(Slot), hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_slots(d_slots, d_didx, d_dval, (uint32_t)nd, stream));
+            ++uploads_delta;
+            delta_slots += nd;
+            dirty.clear();
+            async_used = true;
+        }
+        // filter bytes (slow-path sort) : arena + per-node (off, len)
+        const size_t nn = n_parent.size();
+        if (c_foff < nn || c_flen < nn) {
+            if ((rc = dev_reserve(d_foff, c_foff, nn))) return rc;
+            if ((rc = dev_reserve(d_flen, c_flen, nn))) return rc;
+            full_f_dirty = true;
+        }
+        if (c_fbytes < fbytes.size() + 1) {
+            if ((rc = dev_reserve(d_fbytes, c_fbytes, fbytes.size() + 1))) return rc;
+            fbytes_uploaded = 0;
+        }
+        if (fbytes.size() > fbytes_uploaded) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_fbytes + fbytes_uploaded, fbytes.data() + fbytes_uploaded,
+                                  fbytes.size() - fbytes_uploaded, hipMemcpyHostToDevice, stream));
+            fbytes_uploaded = fbytes.size();
+        }
+        if (full_f_dirty) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_foff, n_foff.data(), nn * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_flen, n_flen.data(), nn * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+            full_f_dirty = false;
+            dirty_f.clear();
+            dirty_f_mark.assign(nn, 0);
+        } else if (!dirty_f.empty()) {
+            const size_t nd = dirty_f.size();
+            if ((rc = host_reserve(h_fidx, ch_fidx, nd))) return rc;
+            if ((rc = host_reserve(h_foffv, ch_foffv, nd))) return rc;
+            if ((rc = host_reserve(h_flenv, ch_flenv, nd))) return rc;
+            if ((rc = dev_reserve(d_fidx, cd_fidx, nd))) return rc;
+            if ((rc = dev_reserve(d_foffv, cd_foffv, nd))) return rc;
+            if ((rc = dev_reserve(d_flenv, cd_flenv, nd))) return rc;
+            for (size_t k = 0; k < nd; ++k) {
+                const uint32_t c = dirty_f[k];
+                h_fidx[k] = c; h_foffv[k] = n_foff[c]; h_flenv[k] = n_flen[c];
+                dirty_f_mark[c] = 0;
+            }
+            HIP_OK(hipMemcpyAsync(d_fidx, h_fidx, nd * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_foffv, h_foffv, nd * 8, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_flenv, h_flenv, nd * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_fmeta(d_foff, d_flen, d_fidx, d_foffv, d_flenv, (uint32_t)nd, stream));
+            dirty_f.clear();
+            async_used = true;
+        }
+        if (pageable_used) {
+            // host vectors may be mutated / reallocated right after we return
+            HIP_OK(hipStreamSynchronize(stream));
+        } else if (async_used) {
+            HIP_OK(hipEventRecord(ev_delta, stream));
+            delta_inflight = true;
+        }
+        return TM_OK;
+    }
+
+    int ensure_slow_scratch() {
+        int rc;
+        const size_t q = (size_t)s_waves * s_qcap, o = (size_t)s_waves * s_ocap;
+        if ((rc = dev_reserve(d_sqpar, c_sq, q))) return rc;
+        if ((rc = dev_reserve(d_sqpw, c_sq2, q))) return rc;
+        if ((rc = dev_reserve(d_sqmeta, c_sq3, q))) return rc;
+        if ((rc = dev_reserve(d_sqkey, c_sq4, q))) return rc;
+        if ((rc = dev_reserve(d_sofid, c_so, o))) return rc;
+        if ((rc = dev_reserve(d_sokey, c_so2, o))) return rc;
+        return TM_OK;
+    }
+
+    // ------------------------------------------------------------ batches
+    void tokenize_range(tm_batch* b, uint32_t lo, uint32_t hi, std::vector<uint32_t>& slow_out) const {
+        std::vector<TWord> ws;
+        for (uint32_t t = lo; t < hi; ++t) {
+            const uint8_t* p = b->bytes.data() + b->offs[t];
+            const size_t len = b->offs[t + 1] - b->offs[t];
+            split_words(p, len, ws);
+            uint32_t* out = b->h_words.data() + b->h_toff[t];
+            bool irregular = false;
+            for (size_t i = 0; i < ws.size(); ++i) {
+                const TWord& w = ws[i];
+                const uint32_t cls = word_class(w, irregular);
+                uint32_t id;
+                if (w.n == 0) id = W_EMPTY;
+                else if (is_plus(w)) id = W_PLUS;
+                else if (is_hash(w)) id = W_HASH;
+                else id = dict.find(w.p, w.n);
+                out[i] = (cls << WID_BITS) | id;
+            }
+            uint8_t fl = 0;
+            if (len > 0 && p[0] == '$') fl |= TF_DOLLAR;
+            if (irregular || ws.size() > FAST_MAX_DEPTH) fl |= TF_SLOW;
+            b->h_tflags[t] = fl;
+            if (fl & TF_SLOW) slow_out.push_back(t);
+        }
+    }
+
+    int tokenize(tm_batch* b) {
+        const uint32_t n = b->n;
+        b->h_toff.resize((size_t)n + 1);
+        b->h_tflags.resize(n);
+        // word counts = separators + 1
+        uint64_t acc = 0;
+        for (uint32_t t = 0; t < n; ++t) {
+            b->h_toff[t] = (uint32_t)acc;
+            const uint8_t* p = b->bytes.data() + b->offs[t];
+            const size_t len = b->offs[t + 1] - b->offs[t];
+            acc += 1 + (uint64_t)std::count(p, p + len, (uint8_t)'/');
+            if (acc > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        }
+        b->h_toff[n] = (uint32_t)acc;
+        b->nwords = acc;
+        b->h_words.resize(acc ? acc : 1);
+        b->h_slow.clear();
+        const unsigned nt = (n >= 65536) ? threads : 1;
+        if (nt <= 1) {
+            tokenize_range(b, 0, n, b->h_slow);
+        } else {
+            std::vector<std::vector<uint32_t>> slow(nt);
+            std::vector<std::thread> th;
+            for (unsigned i = 0; i < nt; ++i) {
+                const uint32_t lo = (uint32_t)((uint64_t)n * i / nt), hi = (uint32_t)((uint64_t)n * (i + 1) / nt);
+                th.emplace_back([this, b, lo, hi, &slow, i] { tokenize_range(b, lo, hi, slow[i]); });
+            }
+            for (auto& x : th) x.join();
+            for (auto& v : slow) b->h_slow.insert(b->h_slow.end(), v.begin(), v.end());
+        }
+        b->dict_size = dict.size();
+        return TM_OK;
+    }
+
+    int upload_batch(tm_batch* b) {
+        int rc;
+        const uint32_t n = b->n;
+        if ((rc = dev_reserve(b->d_words, b->c_words, b->h_words.size()))) return rc;
+        if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(b->h_slow.size(), 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(b->d_words, b->h_words.data(), b->h_words.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(b->d_toff, b->h_toff.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, stream));
+        if (n) HIP_OK(hipMemcpyAsync(b->d_tflags, b->h_tflags.data(), n, hipMemcpyHostToDevice, stream));
+        if (!b->h_slow.empty())
+            HIP_OK(hipMemcpyAsync(b->d_slow, b->h_slow.data(), b->h_slow.size() * 4, hipMemcpyHostToDevice, stream));
+        // outputs
+        const size_t nn = std::max<size_t>(n, 1);
+        if ((rc = dev_reserve(b->d_count, b->c_count, nn))) return rc;
+        if ((rc = dev_reserve(b->d_src, b->c_src, nn))) return rc;
+        if ((rc = dev_reserve(b->d_rowoff, b->c_rowoff, nn + 1))) return rc;
+        if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
+        if ((rc = dev_reserve(b->d_ovf, b->c_ovf, nn))) return rc;
+        if ((rc = dev_reserve(b->d_ctrl, b->c_ctrl, CTRL_WORDS))) return rc;
+        if ((rc = dev_reserve(b->d_stats, b->c_stats, ST_N))) return rc;
+        if ((rc = dev_reserve(b->d_total, b->c_total, 1))) return rc;
+        if ((rc = reserve_rows(b))) return rc;
+        if ((rc = host_reserve(b->h_ctrl, b->ch_ctrl, CTRL_WORDS))) return rc;
+        if ((rc = host_reserve(b->h_stats, b->ch_stats, ST_N))) return rc;
+        if (!b->ev0) {
+            HIP_OK(hipEventCreate(&b->ev0));
+            HIP_OK(hipEventCreate(&b->ev1));
+            HIP_OK(hipEventCreate(&b->ev2));
+        }
+        return TM_OK;
+    }
+
+    // fids[] = n * K fast row slots + the slow region; ids[] (CSR) has the same capacity
+    int reserve_rows(tm_batch* b) {
+        int rc;
+        const uint64_t fast = (uint64_t)b->n * row_cap;
+        if (b->slow_cap == 0) b->slow_cap = std::max<uint64_t>((uint64_t)b->n / 4, 1u << 16);
+        const uint64_t need = fast + b->slow_cap;
+        if (need >= 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        if ((rc = dev_reserve(b->d_fids, b->c_fids, need))) return rc;
+        if ((rc = dev_reserve(b->d_ids, b->c_ids, need))) return rc;
+        if ((rc = dev_reserve(b->d_rkeys, b->c_rkeys, std::max<uint64_t>(fast, 1)))) return rc;
+        return TM_OK;
+    }
+
+    int prepare(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
+        b->n = n;
+        b->offs.assign(offsets, offsets + (size_t)n + 1);
+        const uint64_t base = offsets[0];
+        for (auto& o : b->offs) o -= base;
+        b->bytes.assign(topics + base, topics + base + b->offs[n]);
+        b->launched = b->done = false;
+        int rc = tokenize(b);
+        if (rc) return rc;
+        if (device < 0) return TM_OK;
+        return upload_batch(b);
+    }
+
+    int launch(tm_batch* b) {
+        if (device < 0) return TM_ENODEV;
+        int rc;
+        if (b->dict_size != dict.size()) {   // new words since tokenisation
+            if ((rc = tokenize(b))) return rc;
+            if ((rc = upload_batch(b))) return rc;
+        }
+        if ((rc = sync_device())) return rc;
+        if ((rc = ensure_slow_scratch())) return rc;
+        if (checked) {
+            if ((rc = dev_reserve(d_dbg, c_dbg, 8))) return rc;
+            if ((rc = host_reserve(h_dbg, ch_dbg, 8))) return rc;
+            HIP_OK(hipMemsetAsync(d_dbg, 0, 8 * 4, stream));
+        }
+        HIP_OK(hipMemsetAsync(b->d_ctrl, 0, CTRL_WORDS * 4, stream));
+        HIP_OK(hipMemsetAsync(b->d_stats, 0, ST_N * 8, stream));
+        MatchArgs a{};
+        a.slots = d_slots;
+        a.bucket_mask = bmask();
+        a.max_probe = max_disp;
+        a.root = root_rec();
+        a.foff = d_foff; a.flen = d_flen; a.fbytes = d_fbytes;
+        a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
+        a.slow_list = b->d_slow; a.n_slow = (uint32_t)b->h_slow.size();
+        a.count = b->d_count; a.src = b->d_src; a.fids = b->d_fids; a.rkeys = b->d_rkeys;
+        a.row_cap = row_cap;
+        a.slow_base = (uint64_t)b->n * row_cap;
+        a.fids_cap = std::min<uint64_t>(b->c_fids, a.slow_base + b->slow_cap);
+        a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
+        a.stats = b->d_stats;
+        a.s_qparent = d_sqpar; a.s_qpw = d_sqpw; a.s_qmeta = d_sqmeta; a.s_qkey = d_sqkey;
+        a.s_ofid = d_sofid; a.s_okey = d_sokey;
+        a.s_qcap = s_qcap; a.s_ocap = s_ocap; a.s_waves = s_waves;
+        a.nwords = (uint32_t)b->h_words.size();
+        a.nslots = (uint32_t)slots.size();
+        a.nnodes = (uint32_t)n_parent.size();
+        a.nfbytes = fbytes.size();
+        a.dbg = checked ? d_dbg : nullptr;
+        HIP_OK(launch_match(a, stream, b->ev0, b->ev1, checked));
+        ScanArgs s{};
+        s.count = b->d_count; s.src = b->d_src; s.fids = b->d_fids; s.fids_cap = a.fids_cap;
+        s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
+        s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
+        s.dbg = checked ? d_dbg : nullptr;
+        HIP_OK(launch_scan(s, stream, b->d_total));
+        HIP_OK(launch_copy(s, stream, checked));
+        HIP_OK(hipEventRecord(b->ev2, stream));
+        HIP_OK(hipMemcpyAsync(b->h_ctrl, b->d_ctrl, CTRL_WORDS * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(b->h_stats, b->d_stats, ST_N * 8, hipMemcpyDeviceToHost, stream));
+        if (checked) HIP_OK(hipMemcpyAsync(h_dbg, d_dbg, 8 * 4, hipMemcpyDeviceToHost, stream));
+        b->launched = true;
+        b->done = false;
+        return TM_OK;
+    }
+
+    int wait(tm_batch* b) {
+        if (!b->launched) return TM_EINVAL;
+        for (int attempt = 0;; ++attempt) {
+            HIP_OK(hipStreamSynchronize(stream));
+            if (checked && h_dbg[0]) {
+                snprintf(last_error(), 512, "bounds check %u failed: index %u bound %u (count %u, extra %u)",
+                         h_dbg[0], h_dbg[1], h_dbg[2], h_dbg[3], h_dbg[4]);
+                return TM_EIO;
+            }
+            const uint32_t err = b->h_ctrl[CTRL_ERR];
+            if (!err) break;
+            if (attempt >= 6) return TM_EOVERFLOW;
+            if (err & ERR_STAGING) {
+                const uint64_t need = b->h_ctrl[CTRL_STAGING_TOP];
+                b->slow_cap = need + need / 4 + 1024;
+                int rc = reserve_rows(b);
+                if (rc) return rc;
+            }
+            if (err & ERR_SLOW_SCRATCH) {
+                s_qcap *= 4;
+                s_ocap *= 4;
+            }
+            int rc = launch(b);
+            if (rc) return rc;
+        }
+        float ms_match = 0, ms_total = 0;
+        (void)hipEventElapsedTime(&ms_match, b->ev0, b->ev1);
+        (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
+        b->st.topics = b->n;
+        b->st.visits = b->h_stats[ST_VISITS];
+        b->st.hash_hits = b->h_stats[ST_HASH];
+        b->st.words = b->h_stats[ST_WORDS];
+        b->st.matches = b->h_stats[ST_MATCHES];
+        b->st.slow_topics = b->h_stats[ST_SLOW];
+        b->st.overflow_tiles = b->h_ctrl[CTRL_NOVF];
+        b->st.ms_match = ms_match;
+        b->st.ms_total = ms_total;
+        b->total = b->st.matches;
+        b->done = true;
+        return TM_OK;
+    }
+
+    int result(tm_batch* b, tm_result* out) {
+        if (!b->done) return TM_EINVAL;
+        int rc;
+        if ((rc = host_reserve(b->h_rowoff, b->ch_rowoff, (size_t)b->n + 1))) return rc;
+        HIP_OK(hipMemcpyAsync(b->h_rowoff, b->d_rowoff, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        const uint64_t total = b->h_rowoff[b->n];
+        if (total > b->c_ids || total != b->total) {
+            snprintf(last_error(), 512, "inconsistent CSR: total %llu, capacity %zu, kernel count %llu",
+                     (unsigned long long)total, b->c_ids, (unsigned long long)b->total);
+            return TM_EIO;
+        }
+        if ((rc = host_reserve(b->h_ids, b->ch_ids, std::max<uint64_t>(total, 1)))) return rc;
+        if (total) HIP_OK(hipMemcpyAsync(b->h_ids, b->d_ids, total * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        out->n_topics = b->n;
+        out->n_matches = total;
+        out->row_offsets = b->h_rowoff;
+        out->filter_ids = b->h_ids;
+        return TM_OK;
+    }
+
+    int init(const tm_config* cfg) {
+        device = cfg ? cfg->device : -1;
+        const char* ck = getenv("TM_CHECKED");
+        checked = ck && ck[0] == '1';
+        if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::max(1, atoi(rcap));
+        threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
+        // root node id 0 (absent until the first add_path, like the reference)
+        n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
+        n_hash.push_back(NONE); n_bloom.push_back(0); n_inslot.push_back(NONE); n_flen.push_back(0);
+        n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
+        slots.clear();
+        slots.resize(1024);
+        for (Slot& s : slots) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
+        if (cfg && cfg->init_slots) rehash(cfg->init_slots);
+        dirty_mark.assign(slots.size(), 0);
+        if (device >= 0) {
+            int ndev = 0;
+            if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return TM_ENODEV;
+            HIP_OK(hipSetDevice(device));
+            HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&ev_delta, hipEventDisableTiming));
+        }
+        return TM_OK;
+    }
+
+    void destroy() {
+        if (device >= 0) {
+            (void)hipSetDevice(device);
+            if (stream) (void)hipStreamSynchronize(stream);
+            scratch.release();
+            dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
+            dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
+            dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
+            dev_free(d_sokey); dev_free(d_dbg);
+            if (h_dbg) (void)hipHostFree(h_dbg);
+            if (h_didx) (void)hipHostFree(h_didx);
+            if (h_dval) (void)hipHostFree(h_dval);
+            if (h_fidx) (void)hipHostFree(h_fidx);
+            if (h_foffv) (void)hipHostFree(h_foffv);
+            if (h_flenv) (void)hipHostFree(h_flenv);
+            if (ev_delta) (void)hipEventDestroy(ev_delta);
+            if (stream) (void)hipStreamDestroy(stream);
+        }
+    }
+
+    int set_device() {
+        if (device < 0) return TM_ENODEV;
+        HIP_OK(hipSetDevice(device));
+        return TM_OK;
+    }
+};
+
+// ====================================================== emqx_topic predicates
+
+namespace {
+
+// emqx_topic:match/2 on word lists (src/emqx_topic.erl:74-87)
+bool words_match(const std::vector<TWord>& n, const std::vector<TWord>& f) {
+    size_t i = 0, j = 0;
+    auto kind = [](const TWord& w) { return w.n == 0 ? 1 : is_plus(w) ? 2 : is_hash(w) ? 3 : 0; };
+    for (;;) {
+        if (i == n.size() && j == f.size()) return true;
+        if (i < n.size() && j < f.size()) {
+            const int kn = kind(n[i]), kf = kind(f[j]);
+            const bool eq = kn == kf && (kn != 0 || (n[i].n == f[j].n && memcmp(n[i].p, f[j].p, n[i].n) == 0));
+            if (eq || kf == 2) { ++i; ++j; continue; }
+        }
+        if (j + 1 == f.size() && kind(f[j]) == 3) return true;
+        return false;
+    }
+}
+
+// strict UTF-8 (Erlang's <<C/utf8, _/binary>>): returns bytes consumed or 0
+size_t utf8_char(const uint8_t* p, size_t n, uint32_t& cp) {
+    const uint8_t c = p[0];
+    if (c < 0x80) { cp = c; return 1; }
+    size_t len;
+    uint32_t min;
+    if ((c & 0xE0) == 0xC0) { len = 2; cp = c & 0x1F; min = 0x80; }
+    else if ((c & 0xF0) == 0xE0) { len = 3; cp = c & 0x0F; min = 0x800; }
+    else if ((c & 0xF8) == 0xF0) { len = 4; cp = c & 0x07; min = 0x10000; }
+    else return 0;
+    if (len > n) return 0;
+    for (size_t i = 1; i < len; ++i) {
+        if ((p[i] & 0xC0) != 0x80) return 0;
+        cp = (cp << 6) | (p[i] & 0x3F);
+    }
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return 0;
+    return len;
+}
+
+}  // namespace
+
+// ======================================================================= ABI
+
+extern "C" {
+
+int tm_create(const tm_config* cfg, tm_engine** out) {
+    if (!out) return TM_EINVAL;
+    if (cfg && cfg->flags) return TM_EINVAL;
+    tm_engine* e = new (std::nothrow) tm_engine();
+    if (!e) return TM_ENOMEM;
+    int rc = e->init(cfg);
+    if (rc) { e->destroy(); delete e; return rc; }
+    *out = e;
+    return TM_OK;
+}
+
+void tm_destroy(tm_engine* e) {
+    if (!e) return;
+    e->destroy();
+    delete e;
+}
+
+uint64_t tm_version(tm_engine* e) {
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    return e->version;
+}
+
+int tm_stats(tm_engine* e, tm_engine_stats* o) {
+    if (!e || !o) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    o->version = e->version;
+    o->nodes = e->live_nodes;
+    o->edges = e->live_edges;
+    o->filters = e->n_filters;
+    o->words = e->dict.size();
+    o->slots = e->slots.size();
+    o->device_bytes = e->d_nslots * sizeof(Slot) + e->c_foff * 8 + e->c_flen * 4 + e->c_fbytes;
+    o->uploads_full = e->uploads_full;
+    o->uploads_delta = e->uploads_delta;
+    o->delta_slots = e->delta_slots;
+    return TM_OK;
+}
+
+int tm_sync(tm_engine* e) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    if ((rc = e->sync_device())) return rc;
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->delta_inflight = false;
+    return TM_OK;
+}
+
+int tm_trie_insert(tm_engine* e, const uint8_t* t, size_t len) {
+    if (!e || (!t && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->trie_insert(t, len);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_trie_delete(tm_engine* e, const uint8_t* t, size_t len) {
+    if (!e || (!t && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->trie_delete(t, len);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_trie_lookup(tm_engine* e, const uint8_t* id, size_t len, int is_root, tm_trie_node* out) {
+    if (!e || !out) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    uint32_t n;
+    if (is_root) {
+        n = e->n_live[ROOT] ? ROOT : NONE;
+    } else {
+        std::vector<uint32_t> ids;
+        if (!e->filter_words(id, len, false, ids)) return 0;
+        n = e->walk(ids);
+    }
+    if (n == NONE) return 0;
+    out->edge_count = e->n_ec[n];
+    out->has_topic = e->n_topic[n];
+    out->filter_id = e->n_topic[n] ? n : TM_NONE;
+    return 1;
+}
+
+int tm_trie_empty(tm_engine* e) {
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    return e->live_edges == 0;
+}
+
+int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_result* out) {
+    if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    try {
+        if ((rc = e->prepare(&e->scratch, topics, offsets, n))) return rc;
+        if ((rc = e->launch(&e->scratch))) return rc;
+        if ((rc = e->wait(&e->scratch))) return rc;
+        return e->result(&e->scratch, out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len, uint32_t* ids, uint32_t cap, uint32_t* n_out) {
+    if (!e || !n_out || (!topic && len)) return TM_EINVAL;
+    const uint64_t offs[2] = {0, len};
+    tm_result r;
+    static const uint8_t zero = 0;
+    int rc = tm_match_batch(e, topic ? topic : &zero, offs, 1, &r);
+    if (rc) return rc;
+    const uint32_t m = r.row_offsets[1] - r.row_offsets[0];
+    for (uint32_t i = 0; i < m && i < cap; ++i) ids[i] = r.filter_ids[r.row_offsets[0] + i];
+    *n_out = m;
+    return TM_OK;
+}
+
+int tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_batch** out) {
+    if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    tm_batch* b = new (std::nothrow) tm_batch();
+    if (!b) return TM_ENOMEM;
+    try {
+        rc = e->prepare(b, topics, offsets, n);
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
+    if (rc) { b->release(); delete b; return rc; }
+    HIP_OK(hipStreamSynchronize(e->stream));
+    *out = b;
+    return TM_OK;
+}
+
+int tm_batch_launch(tm_engine* e, tm_batch* b) {
+    if (!e || !b) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    return e->launch(b);
+}
+
+int tm_batch_wait(tm_engine* e, tm_batch* b) {
+    if (!e || !b) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    return e->wait(b);
+}
+
+int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {
+    if (!e || !b || !out) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    return e->result(b, out);
+}
+
+int tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out) {
+    if (!e || !b || !out) return TM_EINVAL;
+    *out = b->st;
+    return TM_OK;
+}
+
+int tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row, const uint32_t** d_ids, uint64_t* n) {
+    if (!e || !b || !b->done) return TM_EINVAL;
+    if (d_row) *d_row = b->d_rowoff;
+    if (d_ids) *d_ids = b->d_ids;
+    if (n) *n = b->total;
+    return TM_OK;
+}
+
+void tm_batch_free(tm_engine* e, tm_batch* b) {
+    if (!b) return;
+    if (e) {
+        std::lock_guard<std::recursive_mutex> g(e->mu);
+        if (e->device >= 0) {
+            (void)hipSetDevice(e->device);
+            (void)hipStreamSynchronize(e->stream);
+        }
+        b->release();
+    } else {
+        b->release();
+    }
+    delete b;
+}
+
+const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
+    if (!e) return nullptr;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (id >= e->n_topic.size() || !e->n_topic[id] || !e->n_live[id]) return nullptr;
+    if (len) *len = e->n_flen[id];
+    static const uint8_t empty = 0;
+    return e->n_flen[id] ? e->fbytes.data() + e->n_foff[id] : &empty;
+}
+
+int tm_filter_id(tm_engine* e, const uint8_t* f, size_t len, uint32_t* id) {
+    if (!e || !id) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    std::vector<uint32_t> ids;
+    if (!e->filter_words(f, len, false, ids)) return TM_ENOENT;
+    const uint32_t n = e->walk(ids);
+    if (n == NONE || !e->n_topic[n]) return TM_ENOENT;
+    *id = n;
+    return TM_OK;
+}
+
+int tm_topic_match(const uint8_t* name, size_t nl, const uint8_t* flt, size_t fl) {
+    // match(<<$$, _/binary>>, <<$+, _/binary>>) -> false; ... <<$#, ...>> -> false
+    if (nl > 0 && name[0] == '$' && fl > 0 && (flt[0] == '+' || flt[0] == '#')) return 0;
+    std::vector<TWord> a, b;
+    split_words(name, nl, a);
+    split_words(flt, fl, b);
+    return words_match(a, b) ? 1 : 0;
+}
+
+int tm_topic_wildcard(const uint8_t* t, size_t len) {
+    std::vector<TWord> ws;
+    split_words(t, len, ws);
+    for (const TWord& w : ws)
+        if (is_plus(w) || is_hash(w)) return 1;
+    return 0;
+}
+
+int tm_topic_validate(int is_name, const uint8_t* t, size_t len, const char** reason) {
+    const char* dummy;
+    if (!reason) reason = &dummy;
+    *reason = nullptr;
+    if (len == 0) { *reason = "empty_topic"; return TM_EINVAL; }
+    if (len > TM_MAX_TOPIC_LEN) { *reason = "topic_too_long"; return TM_EINVAL; }
+    std::vector<TWord> ws;
+    split_words(t, len, ws);
+    // validate2/1 (src/emqx_topic.erl:109-120)
+    bool wild = false;
+    for (size_t i = 0; i < ws.size(); ++i) {
+        const TWord& w = ws[i];
+        if (is_hash(w)) {
+            if (i + 1 != ws.size()) { *reason = "topic_invalid_#"; return TM_EINVAL; }
+            wild = true;
+            continue;
+        }
+        if (w.n == 0) continue;
+        if (is_plus(w)) { wild = true; continue; }
+        // validate3/1 (:122-127): utf8 chars, none of '#', '+', 0
+        size_t k = 0;
+        while (k < w.n) {
+            uint32_t cp;
+            size_t c = utf8_char(w.p + k, w.n - k, cp);
+            if (!c) { *reason = "function_clause"; return TM_EINVAL; }
+            if (cp == '#' || cp == '+' || cp == 0) { *reason = "topic_invalid_char"; return TM_EINVAL; }
+            k += c;
+        }
+    }
+    if (is_name && wild) { *reason = "topic_name_error"; return TM_EINVAL; }
+    return TM_OK;
+}
+
+const char* tm_last_error(void) { return last_error(); }
+
+const char* tm_build_info(void) {
+    return "emqx_tm gfx950 frontier-tile kernel; slots=32B buckets=64B; path-code sort; " __DATE__;
+}
+
+}  // extern "C"

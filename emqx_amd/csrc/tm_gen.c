@@ -1,0 +1,248 @@
+/*
+ * tm_gen.c -- seeded synthetic subscription/publish workloads.
+ *
+ * Bench/test tooling, not on the match path.  Mirrored bit-for-bit by
+ * emqx_amd/gen.py (tests check the two agree), so small fixtures generated in
+ * Python reproduce on the GPU box from the seed alone.
+ *
+ * RNG: splitmix64.  Vocabulary word k of level l is "w<l>_<k>" except 5 % that
+ * are random words of length 1..16 over a 64-symbol alphabet (alnum + '!' '%',
+ * so all three byte classes relative to '#' and '+' occur).  Word choice is
+ * Zipf(s) over the V-word vocabulary of each level.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+typedef struct {
+    uint64_t seed;
+    uint64_t n_filters;
+    uint32_t vocab;
+    uint32_t max_depth;
+    double   zipf_s;
+    double   p_plus;        /* '+' at a non-final level */
+    double   p_hash;        /* '#' at the final level */
+    double   p_final_plus;  /* '+' at the final level */
+    double   exact_frac;    /* fraction of exact (wildcard-free) filters */
+    int32_t  require_wildcard;
+    double   p_dollar;      /* filter rooted at $SYS */
+    double   p_empty;       /* filter has one empty level */
+    double   p_topic_dollar;
+    double   p_topic_inst;  /* topic instantiates a random filter */
+    double   p_unseen;      /* literal topic word not in any vocabulary */
+} tm_gen_params;
+
+static inline uint64_t sm_next(uint64_t* s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline double sm_u01(uint64_t* s) { return (double)(sm_next(s) >> 11) * (1.0 / 9007199254740992.0); }
+static inline uint64_t sm_below(uint64_t* s, uint64_t n) { return sm_next(s) % n; }
+
+static const char ALPH[65] = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789!%";
+
+typedef struct { char* b; size_t n, cap; } sbuf;
+static void sb_put(sbuf* s, const char* p, size_t n) {
+    if (s->n + n > s->cap) { s->cap = (s->n + n) * 2 + 256; s->b = (char*)realloc(s->b, s->cap); }
+    memcpy(s->b + s->n, p, n); s->n += n;
+}
+
+/* vocabulary word (l, k) written into out (<= 24 bytes); returns length */
+static int vocab_word(uint64_t seed, uint32_t l, uint32_t k, char* out) {
+    uint64_t st = seed * 0x9E3779B97F4A7C15ull + (((uint64_t)l << 32) | k) + 1;
+    if (sm_u01(&st) < 0.05) {
+        int len = 1 + (int)sm_below(&st, 16);
+        for (int i = 0; i < len; i++) out[i] = ALPH[sm_below(&st, 64)];
+        return len;
+    }
+    return snprintf(out, 24, "w%u_%u", l, k);
+}
+
+typedef struct {
+    const tm_gen_params* p;
+    double* cdf;
+} zipf_t;
+
+static void zipf_init(zipf_t* z, const tm_gen_params* p) {
+    z->p = p;
+    z->cdf = (double*)malloc(sizeof(double) * p->vocab);
+    double acc = 0;
+    for (uint32_t k = 0; k < p->vocab; k++) { acc += pow((double)(k + 1), -p->zipf_s); z->cdf[k] = acc; }
+    for (uint32_t k = 0; k < p->vocab; k++) z->cdf[k] /= acc;
+}
+
+static uint32_t zipf_draw(const zipf_t* z, uint64_t* s) {
+    double u = sm_u01(s);
+    uint32_t lo = 0, hi = z->p->vocab - 1;
+    while (lo < hi) { uint32_t mid = (lo + hi) / 2; if (u < z->cdf[mid]) hi = mid; else lo = mid + 1; }
+    return lo;
+}
+
+static void put_vocab(sbuf* o, const tm_gen_params* p, const zipf_t* z, uint64_t* s, uint32_t l) {
+    char w[32];
+    int n = vocab_word(p->seed, l, zipf_draw(z, s), w);
+    sb_put(o, w, (size_t)n);
+}
+
+/* one filter into o (no trailing separator); returns 1 if it has a wildcard */
+static int gen_filter(sbuf* o, const tm_gen_params* p, const zipf_t* z, uint64_t* s, int exact) {
+    uint32_t depth = 1 + (uint32_t)sm_below(s, p->max_depth);
+    int dollar = sm_u01(s) < p->p_dollar;
+    int64_t empty_at = sm_u01(s) < p->p_empty ? (int64_t)sm_below(s, depth) : -1;
+    int wild = 0;
+    for (uint32_t l = 0; l < depth; l++) {
+        if (l) sb_put(o, "/", 1);
+        if (l == 0 && dollar) { sb_put(o, "$SYS", 4); continue; }
+        if ((int64_t)l == empty_at) continue;
+        if (exact) { put_vocab(o, p, z, s, l); continue; }
+        if (l + 1 < depth) {
+            if (sm_u01(s) < p->p_plus) { sb_put(o, "+", 1); wild = 1; }
+            else put_vocab(o, p, z, s, l);
+        } else {
+            double r = sm_u01(s);
+            if (r < p->p_hash) { sb_put(o, "#", 1); wild = 1; }
+            else if (r < p->p_hash + p->p_final_plus) { sb_put(o, "+", 1); wild = 1; }
+            else put_vocab(o, p, z, s, l);
+        }
+    }
+    return wild;
+}
+
+/* string set for dedup */
+typedef struct { uint64_t* h; uint64_t* off; uint32_t* len; size_t cap, n; } sset;
+static uint64_t fnv(const char* p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; i++) { h ^= (uint8_t)p[i]; h *= 1099511628211ull; }
+    return h | 1;
+}
+static void sset_init(sset* s, size_t cap) {
+    size_t c = 1024; while (c < cap * 2) c <<= 1;
+    s->cap = c; s->n = 0;
+    s->h = (uint64_t*)calloc(c, 8); s->off = (uint64_t*)calloc(c, 8); s->len = (uint32_t*)calloc(c, 4);
+}
+/* returns 1 if inserted (new) */
+static int sset_add(sset* s, const char* base, uint64_t off, uint32_t len) {
+    uint64_t h = fnv(base + off, len);
+    size_t i = h & (s->cap - 1);
+    while (s->h[i]) {
+        if (s->h[i] == h && s->len[i] == len && memcmp(base + s->off[i], base + off, len) == 0) return 0;
+        i = (i + 1) & (s->cap - 1);
+    }
+    s->h[i] = h; s->off[i] = off; s->len[i] = len; s->n++;
+    return 1;
+}
+
+typedef struct {
+    char* buf; uint64_t* offs; uint64_t n;
+} tm_strs;
+
+EXPORT void tm_gen_free(tm_strs* s) { if (s) { free(s->buf); free(s->offs); s->buf = NULL; s->offs = NULL; } }
+
+/* Generates p->n_filters distinct filters. */
+EXPORT int tm_gen_filters(const tm_gen_params* p, tm_strs* out) {
+    zipf_t z; zipf_init(&z, p);
+    uint64_t s = p->seed;
+    sbuf o = {0};
+    sset set; sset_init(&set, p->n_filters);
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (p->n_filters + 1));
+    uint64_t n = 0;
+    offs[0] = 0;
+    uint64_t guard = 0;
+    while (n < p->n_filters) {
+        if (++guard > p->n_filters * 1000 + 100000) { free(z.cdf); free(o.b); free(offs); return -1; }
+        int exact = sm_u01(&s) < p->exact_frac;
+        size_t start = o.n;
+        int wild = gen_filter(&o, p, &z, &s, exact);
+        if (!exact && p->require_wildcard && !wild) { o.n = start; continue; }
+        if (!sset_add(&set, o.b, start, (uint32_t)(o.n - start))) { o.n = start; continue; }
+        offs[++n] = o.n;
+    }
+    free(set.h); free(set.off); free(set.len); free(z.cdf);
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
+    return 0;
+}
+
+static void put_unseen(sbuf* o, uint64_t* s) {
+    char w[16];
+    int n = snprintf(w, sizeof(w), "u%08x", (unsigned)(sm_next(s) & 0xffffffffu));
+    sb_put(o, w, (size_t)n);
+}
+
+/* instantiate filter f into o; returns number of words written */
+static uint32_t instantiate(sbuf* o, const tm_gen_params* p, const zipf_t* z, uint64_t* s,
+                            const char* f, uint32_t fl) {
+    uint32_t nw = 0, l = 0, i = 0;
+    while (1) {
+        uint32_t j = i;
+        while (j < fl && f[j] != '/') j++;
+        const char* w = f + i; uint32_t wl = j - i;
+        if (wl == 1 && w[0] == '#') {
+            uint32_t extra = (uint32_t)sm_below(s, 4);
+            for (uint32_t e = 0; e < extra; e++, l++, nw++) {
+                if (nw) sb_put(o, "/", 1);
+                put_vocab(o, p, z, s, l);
+            }
+        } else {
+            if (nw) sb_put(o, "/", 1);
+            if (wl == 1 && w[0] == '+') {
+                if (sm_u01(s) < 0.9) put_vocab(o, p, z, s, l); else put_unseen(o, s);
+            } else sb_put(o, w, wl);
+            nw++; l++;
+        }
+        if (j >= fl) break;
+        i = j + 1;
+    }
+    return nw;
+}
+
+/* Generates n topics against the given filter set with topic seed `tseed`. */
+EXPORT int tm_gen_topics(const tm_gen_params* p, const tm_strs* filters, uint64_t tseed,
+                         uint64_t n, tm_strs* out) {
+    zipf_t z; zipf_init(&z, p);
+    uint64_t s = tseed;
+    sbuf o = {0};
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    offs[0] = 0;
+    for (uint64_t t = 0; t < n; t++) {
+        double r = sm_u01(&s);
+        size_t start = o.n;
+        if (filters->n && r < p->p_topic_dollar + p->p_topic_inst) {
+            int dollar = r < p->p_topic_dollar;
+            uint64_t fi = sm_below(&s, filters->n);
+            const char* f = filters->buf + filters->offs[fi];
+            uint32_t fl = (uint32_t)(filters->offs[fi + 1] - filters->offs[fi]);
+            uint32_t nw = instantiate(&o, p, &z, &s, f, fl);
+            (void)nw;
+            if (o.n == start) put_vocab(&o, p, &z, &s, 0);
+            if (dollar) {
+                /* replace the first word with "$SYS" */
+                size_t k = start;
+                while (k < o.n && o.b[k] != '/') k++;
+                size_t rest = o.n - k;
+                char* tmp = (char*)malloc(rest + 1);
+                memcpy(tmp, o.b + k, rest);
+                o.n = start;
+                sb_put(&o, "$SYS", 4);
+                sb_put(&o, tmp, rest);
+                free(tmp);
+            }
+        } else {
+            uint32_t depth = 1 + (uint32_t)sm_below(&s, p->max_depth);
+            for (uint32_t l = 0; l < depth; l++) {
+                if (l) sb_put(&o, "/", 1);
+                if (sm_u01(&s) < p->p_unseen) put_unseen(&o, &s);
+                else put_vocab(&o, p, &z, &s, l);
+            }
+        }
+        offs[t + 1] = o.n;
+    }
+    free(z.cdf);
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
+    return 0;
+}

@@ -1,0 +1,160 @@
+// tm_internal.hpp -- layout shared by the host engine (tm_engine.cpp) and the
+// gfx950 kernels (tm_kernels.hip).  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace etm {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t SLOT_EMPTY = 0xFFFFFFFFu;   // slot.parent of a never-used slot
+constexpr uint32_t SLOT_TOMB = 0xFFFFFFFEu;    // slot.parent of a deleted edge
+constexpr uint32_t ROOT = 0;                   // node id of the atom `root`
+
+// Interned word ids (low 29 bits of a topic word entry).  '' is a regular word
+// for the trie (a literal edge), it only gets a fixed id.
+constexpr uint32_t W_UNKNOWN = 0;   // topic word absent from every filter
+constexpr uint32_t W_EMPTY = 1;     // ''
+constexpr uint32_t W_PLUS = 2;      // '+'
+constexpr uint32_t W_HASH = 3;      // '#'
+constexpr uint32_t W_FIRST = 4;
+constexpr uint32_t WID_BITS = 29;
+constexpr uint32_t WID_MASK = (1u << WID_BITS) - 1;
+
+// Byte class of a topic word relative to '#' (0x23) and '+' (0x2B): decides
+// where the literal branch sorts among {'#', '+'} filters at that level.
+constexpr uint32_t C_BELOW = 0;     // first byte < '#'
+constexpr uint32_t C_BETWEEN = 1;   // '#' <= first byte < '+'  (incl. the word '#')
+constexpr uint32_t C_ABOVE = 2;     // first byte > '+'
+constexpr uint32_t C_EMPTY = 3;     // ''
+
+// Topic flags
+constexpr uint8_t TF_DOLLAR = 1;    // first byte is '$' (src/emqx_trie.erl:162-163)
+constexpr uint8_t TF_SLOW = 2;      // deep (> FAST_MAX_DEPTH) or irregular word
+
+// Fast path: 3-bit sort digits for levels 0..20 packed MSB-first in a u64.
+constexpr uint32_t FAST_MAX_DEPTH = 20;
+
+// Node summary flags (slot.flags / root.flags)
+constexpr uint32_t NF_PLUS = 1;     // node has a '+' child
+constexpr uint32_t NF_HASH = 2;     // node has a '#' child
+
+// One edge of the trie in the open-addressed hash, keyed (parent, word), and
+// carrying the CHILD's summary so that one 64-B bucket read per visited node
+// is all the walk needs.  32 B, two slots per 64-B bucket.
+struct alignas(32) Slot {
+    uint32_t parent;   // key hi; SLOT_EMPTY / SLOT_TOMB
+    uint32_t word;     // key lo
+    uint32_t child;    // child node id (== its filter id when it has a topic)
+    uint32_t term;     // child's own filter id or NONE        (read(trie_node, Child))
+    uint32_t hterm;    // filter id of child/'#' or NONE        ('match_#'(Child))
+    uint32_t flags;    // NF_*
+    uint32_t bloom;    // 32-bit bloom of child's literal child words
+    uint32_t spare;
+};
+static_assert(sizeof(Slot) == 32, "slot is 32 bytes");
+
+struct RootRec {
+    uint32_t hterm;
+    uint32_t flags;
+    uint32_t bloom;
+    uint32_t live;
+};
+
+__host__ __device__ inline uint32_t edge_hash(uint32_t parent, uint32_t word) {
+    uint64_t k = ((uint64_t)parent << 32) | word;
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
+
+__host__ __device__ inline uint32_t bloom_bit(uint32_t word) {
+    return 1u << ((word * 0x9E3779B1u) >> 27);
+}
+
+// Control words of one batch launch (device memory, zeroed per launch).
+enum Ctrl : uint32_t {
+    CTRL_STAGING_TOP = 0,   // slow-region entries reserved (may exceed capacity -> rerun)
+    CTRL_NOVF = 1,          // topics appended to the ovf list
+    CTRL_ERR = 2,           // error bits
+    CTRL_SLOW_DONE = 3,
+    CTRL_WORDS = 16
+};
+constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
+constexpr uint32_t ERR_SLOW_SCRATCH = 2; // slow-path scratch exceeded
+constexpr uint32_t ERR_OVF_LIST = 4;
+
+enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_N = 8 };
+
+struct MatchArgs {
+    // trie replica
+    const Slot* slots;
+    uint32_t bucket_mask;     // nbuckets - 1 (bucket = 2 slots)
+    uint32_t max_probe;       // max bucket displacement of any live key
+    RootRec root;
+    const uint64_t* foff;     // filter bytes offset per node id (slow-path byte sort)
+    const uint32_t* flen;
+    const uint8_t* fbytes;
+    // batch input
+    const uint32_t* words;    // (class << 29) | word id
+    const uint32_t* toff;     // n + 1 word offsets
+    const uint8_t* tflags;
+    uint32_t n;
+    const uint32_t* slow_list;  // host-flagged slow topics
+    uint32_t n_slow;
+    // outputs
+    uint32_t* count;          // per topic |M(t)|
+    unsigned long long* src;  // per topic offset of its sorted row in fids[]
+    uint32_t* fids;           // [n * row_cap] fast rows, then the slow-path region
+    unsigned long long* rkeys;// [n * row_cap] path-code sort keys of the fast rows
+    uint32_t row_cap;         // K: per-topic row slots on the fast path
+    uint64_t slow_base;       // = n * row_cap
+    uint64_t fids_cap;
+    uint32_t* ctrl;
+    uint32_t* ovf_list;       // topics redone by the slow path (row > K or stack overflow)
+    uint32_t ovf_cap;
+    unsigned long long* stats;
+    // slow-path scratch
+    uint32_t* s_qparent;
+    uint32_t* s_qpw;
+    uint32_t* s_qmeta;
+    unsigned long long* s_qkey;
+    uint32_t* s_ofid;
+    unsigned long long* s_okey;
+    uint32_t s_qcap;
+    uint32_t s_ocap;
+    uint32_t s_waves;
+    // sizes for the bounds-checked debug variant (TM_CHECKED=1)
+    uint32_t nwords;
+    uint32_t nslots;
+    uint32_t nnodes;
+    uint64_t nfbytes;
+    uint32_t* dbg;            // [0] first failing check id, [1] index, [2] bound, [3] count
+};
+
+struct ScanArgs {
+    const uint32_t* count;
+    const unsigned long long* src;
+    const uint32_t* fids;
+    uint64_t fids_cap;
+    uint32_t* row_off;        // n + 1
+    uint32_t* ids;
+    uint32_t* block_sums;     // scratch
+    uint32_t n;
+    uint32_t ids_cap;
+    uint32_t* ctrl;
+    uint32_t* dbg;
+};
+
+// kernel launchers (tm_kernels.hip)
+hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
+hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
+hipError_t launch_copy(const ScanArgs& a, hipStream_t s, bool checked);
+hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n,
+                                hipStream_t s);
+hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx,
+                                const uint64_t* off, const uint32_t* len, uint32_t n, hipStream_t s);
+uint32_t scan_block_count(uint32_t n);
+
+}  // namespace etm

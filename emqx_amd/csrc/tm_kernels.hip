@@ -1,0 +1,690 @@
+// tm_kernels.hip -- gfx950 (CDNA4) kernels of the topic-matching engine.
+//
+// The reference walk is emqx_trie:match/1 -> match_node/3 (src/emqx_trie.erl:
+// 96-99, 162-186): per visited node, emit its '#' child's topic, then follow the
+// literal word and the '+' edge; at the end of the words emit the node's own
+// topic and its '#' child's.  Here that recursion becomes a frontier expansion:
+//
+//   tm_match_tiles  one 64-lane wavefront owns a TILE of 64 topics.  Pending
+//                   edge probes of all 64 topics live in an LDS stack; every
+//                   iteration pops up to 64 of them (one per lane), each lane
+//                   reads ONE 64-B hash bucket that holds the child's whole
+//                   summary, and the lanes push their children / emit their
+//                   matches through ballot + mbcnt prefix sums.  Matches carry a
+//                   3-bit-per-level path code whose order equals Erlang binary
+//                   order of the filters (DESIGN.md "Sort order"), so rows are
+//                   sorted in LDS with no byte compares, then written to staging.
+//   tm_match_slow   one wavefront per topic, frontier in global scratch: deep
+//                   (>20 levels) or irregular topics (sorted by filter bytes) and
+//                   topics of tiles whose LDS frontier overflowed.
+//   scan / copy     exclusive scan of the per-topic counts -> CSR rows.
+//
+// No MFMA: this is a dependent irregular gather, HBM/L2-latency bound.
+#include "tm_internal.hpp"
+
+namespace etm {
+
+constexpr int TILE = 64;
+constexpr int QCAP = 512;   // LDS probe stack entries per wave
+constexpr int WCAP = 512;   // LDS word cache per tile
+
+constexpr uint32_t M_SKIPE = 1u << 20;   // don't emit the child's own topic (literal '#' dup)
+constexpr uint32_t M_DSTART = 1u << 21;  // $-rooted start probe: the node was already counted
+
+// digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
+//   L = literal branch, H = '#' terminal, P = '+' branch; E = 0, L_lo = 1.
+__device__ __forceinline__ uint32_t dig_L(uint32_t c) { return (0x4432u >> (4 * c)) & 0xF; }
+__device__ __forceinline__ uint32_t dig_H(uint32_t c) { return (0x2223u >> (4 * c)) & 0xF; }
+__device__ __forceinline__ uint32_t dig_P(uint32_t c) { return (0x3344u >> (4 * c)) & 0xF; }
+
+__device__ __forceinline__ int key_shift(uint32_t level) { return 61 - 3 * (int)level; }
+
+__device__ __forceinline__ uint64_t put_digit(uint64_t key, uint32_t level, uint32_t d) {
+    return level <= FAST_MAX_DEPTH ? (key | ((uint64_t)d << key_shift(level))) : key;
+}
+
+__device__ __forceinline__ uint32_t prefix_count(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Bounds-checked debug variant: an out-of-range index is recorded (first
+// failing check id, index, bound) and clamped to 0 instead of faulting.
+template <bool CK>
+__device__ __forceinline__ uint64_t ck(uint64_t i, uint64_t bound, uint32_t* dbg, uint32_t id) {
+    if (CK && i >= bound) {
+        if (dbg) {
+            if (atomicCAS(&dbg[0], 0u, id) == 0u) { dbg[1] = (uint32_t)i; dbg[2] = (uint32_t)bound; }
+            atomicAdd(&dbg[3], 1u);
+        }
+        return 0;
+    }
+    return i;
+}
+#define CK_(i, bound, id) ck<CK>((i), (bound), a.dbg, (id))
+
+// One 64-B bucket read: both slots, key compare.  Returns true with the child
+// summary in s when (parent, word) is present.  max_probe bounds the scan.
+template <bool CK>
+__device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint32_t word, Slot& s) {
+    const Slot* __restrict__ slots = a.slots;
+    const uint32_t mask = a.bucket_mask, max_probe = a.max_probe;
+    uint32_t b = edge_hash(parent, word) & mask;
+    for (uint32_t p = 0; p <= max_probe; ++p) {
+        const uint4* q = reinterpret_cast<const uint4*>(slots + CK_(2 * (size_t)b + 1, a.nslots, 1) - 1);
+        uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+        if (a0.x == parent && a0.y == word) {
+            s.parent = a0.x; s.word = a0.y; s.child = a0.z; s.term = a0.w;
+            s.hterm = a1.x; s.flags = a1.y; s.bloom = a1.z; s.spare = a1.w;
+            return true;
+        }
+        if (a2.x == parent && a2.y == word) {
+            s.parent = a2.x; s.word = a2.y; s.child = a2.z; s.term = a2.w;
+            s.hterm = a3.x; s.flags = a3.y; s.bloom = a3.z; s.spare = a3.w;
+            return true;
+        }
+        if (a0.x == SLOT_EMPTY || a2.x == SLOT_EMPTY) return false;
+        b = (b + 1) & mask;
+    }
+    return false;
+}
+
+// Expansion of one found child at level lc (= words consumed), mirroring
+// match_node/3: at the end of the words the node's own topic and its '#'
+// child's (src/emqx_trie.erl:168-169); otherwise the '#' child's topic, then the
+// literal and '+' probes (:171-177).
+struct Expand {
+    uint32_t ne, np;
+    uint32_t ef0, ef1;
+    uint64_t ek0, ek1;
+    uint32_t pw0, pw1;
+    uint32_t pf0, pf1;
+    uint64_t pk0, pk1;
+};
+
+// register-only appends (no runtime-indexed arrays -> no scratch)
+__device__ __forceinline__ void add_e(Expand& x, uint32_t fid, uint64_t key) {
+    if (x.ne == 0) { x.ef0 = fid; x.ek0 = key; } else { x.ef1 = fid; x.ek1 = key; }
+    x.ne++;
+}
+__device__ __forceinline__ void add_p(Expand& x, uint32_t w, uint64_t key, uint32_t fl) {
+    if (x.np == 0) { x.pw0 = w; x.pk0 = key; x.pf0 = fl; } else { x.pw1 = w; x.pk1 = key; x.pf1 = fl; }
+    x.np++;
+}
+
+__device__ __forceinline__ void expand(const Slot& s, uint32_t lc, uint32_t d, uint32_t flags,
+                                       uint64_t key, uint32_t w_here, uint32_t w_prev, Expand& x) {
+    x.ne = 0; x.np = 0;
+    if (lc == d) {
+        if (!(flags & M_SKIPE) && s.term != NONE) {
+            uint64_t k = key;
+            // '' word at level lc-1 followed by the end: "P/" sorts before "P/#".
+            if ((w_prev >> WID_BITS) == C_EMPTY && lc - 1 <= FAST_MAX_DEPTH) {
+                int sp = key_shift(lc - 1);
+                if (((k >> sp) & 7) == 4) k = (k & ~(7ull << sp)) | (1ull << sp);
+            }
+            add_e(x, s.term, k);
+        }
+        if (s.hterm != NONE) add_e(x, s.hterm, put_digit(key, lc, 2));
+        return;
+    }
+    uint32_t cls = w_here >> WID_BITS, id = w_here & WID_MASK;
+    if (s.hterm != NONE) add_e(x, s.hterm, put_digit(key, lc, dig_H(cls)));
+    if (id == W_HASH) {
+        if (s.flags & NF_HASH) add_p(x, W_HASH, put_digit(key, lc, dig_L(cls)), (lc + 1 == d) ? M_SKIPE : 0);
+    } else if (id != W_UNKNOWN && id != W_PLUS && (s.bloom & bloom_bit(id))) {
+        add_p(x, id, put_digit(key, lc, dig_L(cls)), 0);
+    }
+    if (s.flags & NF_PLUS) add_p(x, W_PLUS, put_digit(key, lc, dig_P(cls)), 0);
+}
+
+// Root expansion for a topic (match_node(root, Words), or the $ rule that
+// starts at node W and never tries root's '+'/'#', src/emqx_trie.erl:162-166).
+__device__ __forceinline__ void expand_root(const RootRec& r, bool dollar, uint32_t d, uint32_t w0,
+                                            Expand& x) {
+    x.ne = 0; x.np = 0;
+    uint32_t cls = w0 >> WID_BITS, id = w0 & WID_MASK;
+    if (!dollar && r.hterm != NONE) add_e(x, r.hterm, (uint64_t)dig_H(cls) << 61);
+    if (id == W_HASH) {
+        if (!dollar && (r.flags & NF_HASH)) add_p(x, W_HASH, (uint64_t)dig_L(cls) << 61, (d == 1) ? M_SKIPE : 0);
+    } else if (id != W_UNKNOWN && id != W_PLUS && (r.bloom & bloom_bit(id))) {
+        add_p(x, id, (uint64_t)dig_L(cls) << 61, dollar ? M_DSTART : 0);
+    }
+    if (!dollar && (r.flags & NF_PLUS)) add_p(x, W_PLUS, (uint64_t)dig_P(cls) << 61, 0);
+}
+
+struct alignas(16) TileLds {
+    unsigned long long q_key[QCAP];
+    uint32_t q_parent[QCAP];
+    uint32_t q_pw[QCAP];
+    uint32_t q_meta[QCAP];
+    uint32_t words[WCAP];
+    uint32_t toff[TILE];
+    uint32_t depth[TILE];
+    uint32_t cnt[TILE];
+};
+
+// Stores one match of tile-topic tl into its HBM row slot (row capacity K);
+// a row that outgrows K keeps counting and is redone by the slow path.
+template <bool CK>
+__device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t t, uint32_t slot, uint64_t key, uint32_t fid) {
+    if (slot < a.row_cap) {
+        const uint64_t i = (uint64_t)t * a.row_cap + slot;
+        a.rkeys[CK_(i, a.slow_base, 13)] = key;
+        a.fids[CK_(i, a.slow_base, 14)] = fid;
+    }
+}
+
+template <bool CK>
+__global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
+    __shared__ TileLds L;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    unsigned long long sV = 0, sH = 0, sW = 0, sM = 0;
+
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint32_t t0 = tile * TILE;
+        const uint32_t tend = min(t0 + TILE, a.n);
+        const uint32_t t = t0 + lane;
+        const bool valid = t < a.n;
+        const uint32_t wbeg = a.toff[CK_(t0, a.n + 1, 2)], wend = a.toff[CK_(tend, a.n + 1, 3)];
+        const bool in_lds = (wend - wbeg) <= (uint32_t)WCAP;
+        const uint32_t my_off = valid ? a.toff[CK_(t, a.n + 1, 4)] : wend;
+        const uint32_t my_end = valid ? a.toff[CK_(t + 1, a.n + 1, 5)] : wend;
+        const uint8_t fl = valid ? a.tflags[CK_(t, a.n, 6)] : (uint8_t)TF_SLOW;
+        if (in_lds)
+            for (uint32_t i = lane; i < wend - wbeg; i += 64) L.words[CK_(i, WCAP, 7)] = a.words[CK_(wbeg + i, a.nwords, 8)];
+        L.toff[lane] = in_lds ? my_off - wbeg : my_off;
+        L.depth[lane] = my_end - my_off;
+        L.cnt[lane] = 0;
+        __syncthreads();
+        const uint32_t* wsrc = in_lds ? L.words : a.words;
+        const uint32_t wlim = in_lds ? (uint32_t)WCAP : a.nwords;
+
+        uint32_t qn = 0;
+        bool ovf = false;
+        const bool active = !(fl & TF_SLOW);
+        uint32_t tV = 0, tH = 0, tW = 0;   // committed only if the tile does not overflow
+        const uint32_t d_me = my_end - my_off;
+
+        // ---- level 0: root expansion, one topic per lane
+        {
+            Expand x; x.ne = 0; x.np = 0;
+            if (active && d_me > 0) {
+                const bool dollar = fl & TF_DOLLAR;
+                tV += 1;
+                if (!dollar && (a.root.flags & NF_HASH)) tH += 1;
+                tW += d_me;
+                expand_root(a.root, dollar, d_me, wsrc[CK_(L.toff[lane], wlim, 9)], x);
+            }
+            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+            const uint32_t meta = lane | (1u << 6);
+            if (x.np >= 1) {
+                const uint32_t pos = qn + pre;
+                L.q_parent[pos] = ROOT; L.q_pw[pos] = x.pw0; L.q_meta[pos] = meta | x.pf0; L.q_key[pos] = x.pk0;
+            }
+            if (x.np >= 2) {
+                const uint32_t pos = qn + pre + 1;
+                L.q_parent[pos] = ROOT; L.q_pw[pos] = x.pw1; L.q_meta[pos] = meta | x.pf1; L.q_key[pos] = x.pk1;
+            }
+            qn += __popcll(b0) + __popcll(b1);
+            if (x.ne) {   // at most one emission at the root ('#')
+                L.cnt[lane] = 1;
+                emit_row<CK>(a, t, 0, x.ek0, x.ef0);
+            }
+        }
+
+        // ---- frontier loop: LIFO stack, up to 64 probes per iteration
+        while (qn > 0) {
+            const uint32_t k = min(qn, 64u);
+            const bool has = lane < k;
+            const uint32_t idx = qn - k + lane;
+            uint32_t parent = 0, pw = 0, meta = 0;
+            uint64_t key = 0;
+            if (has) { parent = L.q_parent[idx]; pw = L.q_pw[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; }
+            qn -= k;
+            Slot s;
+            const bool found = has && probe<CK>(a, parent, pw, s);
+            Expand x; x.ne = 0; x.np = 0;
+            const uint32_t tl = meta & 63;
+            if (found) {
+                const uint32_t lc = (meta >> 6) & 0xFFF;
+                const uint32_t d = L.depth[tl];
+                const uint32_t base = L.toff[tl];
+                if (!(meta & M_DSTART)) tV += 1;
+                if (s.flags & NF_HASH) tH += 1;
+                const uint32_t w_here = lc < d ? wsrc[CK_(base + lc, wlim, 10)] : 0u;
+                const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 11)];
+                expand(s, lc, d, meta, key, w_here, w_prev, x);
+            }
+            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+            const uint32_t ptot = __popcll(b0) + __popcll(b1);
+            if (qn + ptot > (uint32_t)QCAP) { ovf = true; break; }
+            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+            const uint32_t nmeta = tl | ((((meta >> 6) & 0xFFF) + 1) << 6);
+            if (x.np >= 1) {
+                const uint32_t pos = qn + pre;
+                L.q_parent[pos] = s.child; L.q_pw[pos] = x.pw0; L.q_meta[pos] = nmeta | x.pf0; L.q_key[pos] = x.pk0;
+            }
+            if (x.np >= 2) {
+                const uint32_t pos = qn + pre + 1;
+                L.q_parent[pos] = s.child; L.q_pw[pos] = x.pw1; L.q_meta[pos] = nmeta | x.pf1; L.q_key[pos] = x.pk1;
+            }
+            qn += ptot;
+            if (x.ne) {
+                const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
+                emit_row<CK>(a, t0 + tl, slot, x.ek0, x.ef0);
+                if (x.ne >= 2) emit_row<CK>(a, t0 + tl, slot + 1, x.ek1, x.ef1);
+            }
+        }
+        __syncthreads();
+
+        if (ovf) {
+            // probe stack overflow: every regular topic of the tile goes to the slow path
+            const uint64_t m = __ballot(valid && active);
+            uint32_t base = 0;
+            if (lane == 0 && m) base = atomicAdd(&a.ctrl[CTRL_NOVF], (uint32_t)__popcll(m));
+            base = __shfl(base, 0, 64);
+            if (valid && active) {
+                const uint32_t slot = base + prefix_count(m);
+                if (slot < a.ovf_cap) a.ovf_list[CK_(slot, a.ovf_cap, 12)] = t;
+            }
+            __syncthreads();
+            continue;
+        }
+        sV += tV; sH += tH; sW += tW;
+
+        // ---- rows longer than K go to the slow path
+        const uint32_t c_me = L.cnt[lane];
+        const bool row_ovf = valid && active && c_me > a.row_cap;
+        {
+            const uint64_t m = __ballot(row_ovf);
+            uint32_t base = 0;
+            if (lane == 0 && m) base = atomicAdd(&a.ctrl[CTRL_NOVF], (uint32_t)__popcll(m));
+            base = __shfl(base, 0, 64);
+            if (row_ovf) {
+                const uint32_t slot = base + prefix_count(m);
+                if (slot < a.ovf_cap) a.ovf_list[CK_(slot, a.ovf_cap, 15)] = t;
+            }
+        }
+        if (valid && active && !row_ovf) {
+            a.count[CK_(t, a.n, 16)] = c_me;
+            a.src[CK_(t, a.n, 17)] = (unsigned long long)t * a.row_cap;
+            sM += c_me;
+        }
+
+        // ---- sort each row in place by path code: lane i holds element i,
+        //      rank = #{j : key_j < key_i} via broadcast shuffles (keys unique per row)
+        for (uint32_t tt = 0; tt < tend - t0; ++tt) {
+            const uint32_t c = L.cnt[tt];
+            const uint32_t ftt = __shfl(fl, tt, 64);
+            if (c < 2 || c > a.row_cap || (ftt & TF_SLOW)) continue;
+            const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
+            uint64_t kk = ~0ull;
+            uint32_t ff = 0;
+            if (lane < c) { kk = a.rkeys[CK_(rb + lane, a.slow_base, 18)]; ff = a.fids[CK_(rb + lane, a.slow_base, 19)]; }
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < c; ++j) {
+                const uint64_t kj = __shfl(kk, j, 64);
+                rank += kj < kk ? 1u : 0u;
+            }
+            if (lane < c) a.fids[CK_(rb + rank, a.slow_base, 20)] = ff;
+        }
+        __syncthreads();
+    }
+
+    // wave-reduce the stats, one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) {
+        sV += __shfl_xor(sV, o, 64); sH += __shfl_xor(sH, o, 64);
+        sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&a.stats[ST_VISITS], sV); atomicAdd(&a.stats[ST_HASH], sH);
+        atomicAdd(&a.stats[ST_WORDS], sW); atomicAdd(&a.stats[ST_MATCHES], sM);
+    }
+}
+
+// ---------------------------------------------------------------- slow path
+
+// Erlang binary order on two filters (unsigned bytes, shorter prefix first).
+template <bool CK>
+__device__ __forceinline__ bool filter_less(const MatchArgs& a, uint32_t x, uint32_t y) {
+    if (x == NONE) return false;
+    if (y == NONE) return true;
+    x = CK_(x, a.nnodes, 20); y = CK_(y, a.nnodes, 21);
+    const uint8_t* px = a.fbytes + CK_(a.foff[x], a.nfbytes + 1, 22);
+    const uint8_t* py = a.fbytes + CK_(a.foff[y], a.nfbytes + 1, 23);
+    const uint32_t lx = a.flen[x], ly = a.flen[y];
+    const uint32_t m = min(lx, ly);
+    for (uint32_t i = 0; i < m; ++i) {
+        if (px[i] != py[i]) return px[i] < py[i];
+    }
+    return lx < ly;
+}
+
+// Bitonic sort of n (power of two) (key, fid) pairs held at kp/fp (LDS or global).
+template <bool CK>
+__device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp, uint32_t n, bool by_bytes) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    bool gt;
+                    if (by_bytes) gt = filter_less<CK>(a, fp[ixj], fp[i]);
+                    else gt = kp[i] > kp[ixj];
+                    if (gt == up) {
+                        unsigned long long tk = kp[i]; kp[i] = kp[ixj]; kp[ixj] = tk;
+                        uint32_t tf = fp[i]; fp[i] = fp[ixj]; fp[ixj] = tf;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+}
+
+constexpr uint32_t SORT_LDS = 2048;
+constexpr uint32_t SM_SKIPE = 1u << 30;
+constexpr uint32_t SM_DSTART = 1u << 31;
+
+template <bool CK>
+__global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
+    __shared__ unsigned long long sk[SORT_LDS];
+    __shared__ uint32_t sf[SORT_LDS];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t wave = blockIdx.x;
+    uint32_t* qpar = a.s_qparent + (size_t)wave * a.s_qcap;
+    uint32_t* qpw = a.s_qpw + (size_t)wave * a.s_qcap;
+    uint32_t* qmeta = a.s_qmeta + (size_t)wave * a.s_qcap;
+    unsigned long long* qkey = a.s_qkey + (size_t)wave * a.s_qcap;
+    uint32_t* ofid = a.s_ofid + (size_t)wave * a.s_ocap;
+    unsigned long long* okey = a.s_okey + (size_t)wave * a.s_ocap;
+    const uint32_t novf = min(a.ctrl[CTRL_NOVF], a.ovf_cap);
+    const uint32_t total_items = a.n_slow + novf;
+    unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sS = 0;
+
+    for (uint32_t item = wave; item < total_items; item += gridDim.x) {
+        uint32_t t;
+        if (item < a.n_slow) t = a.slow_list[CK_(item, a.n_slow, 24)];
+        else t = a.ovf_list[CK_(item - a.n_slow, a.ovf_cap, 25)];
+        t = CK_(t, a.n, 26);
+        const uint8_t fl = a.tflags[t];
+        const bool dollar = fl & TF_DOLLAR;
+        const bool by_bytes = fl & TF_SLOW;
+        const uint32_t wb = a.toff[t];
+        const uint32_t d = a.toff[t + 1] - wb;
+        const uint32_t* w = a.words + wb;
+        sS += 1;
+        uint32_t qn = 0, on = 0;
+        bool err = false;
+        if (d > 0) {
+            Expand x; x.ne = 0; x.np = 0;
+            if (lane == 0) {
+                sV += 1; sW += d;
+                if (!dollar && (a.root.flags & NF_HASH)) sH += 1;
+                expand_root(a.root, dollar, d, w[0], x);
+                if (x.np >= 1) {
+                    qpar[0] = ROOT; qpw[0] = x.pw0; qkey[0] = x.pk0;
+                    qmeta[0] = 1u | (x.pf0 & M_SKIPE ? SM_SKIPE : 0) | (x.pf0 & M_DSTART ? SM_DSTART : 0);
+                }
+                if (x.np >= 2) {
+                    qpar[1] = ROOT; qpw[1] = x.pw1; qkey[1] = x.pk1;
+                    qmeta[1] = 1u | (x.pf1 & M_SKIPE ? SM_SKIPE : 0) | (x.pf1 & M_DSTART ? SM_DSTART : 0);
+                }
+                if (x.ne >= 1) { ofid[0] = x.ef0; okey[0] = x.ek0; }
+                if (x.ne >= 2) { ofid[1] = x.ef1; okey[1] = x.ek1; }
+            }
+            qn = __shfl(x.np, 0, 64);
+            on = __shfl(x.ne, 0, 64);
+            __threadfence_block();
+            __syncthreads();
+        }
+        while (qn > 0 && !err) {
+            const uint32_t k = min(qn, 64u);
+            const bool has = lane < k;
+            const uint32_t idx = qn - k + lane;
+            uint32_t parent = 0, pw = 0, meta = 0;
+            unsigned long long key = 0;
+            if (has) {
+                const uint32_t ci = CK_(idx, a.s_qcap, 27);
+                parent = qpar[ci]; pw = qpw[ci]; meta = qmeta[ci]; key = qkey[ci];
+            }
+            __threadfence_block();
+            __syncthreads();
+            qn -= k;
+            Slot s;
+            const bool found = has && probe<CK>(a, parent, pw, s);
+            Expand x; x.ne = 0; x.np = 0;
+            const uint32_t lc = meta & 0x3FFFFFFFu;
+            if (found) {
+                if (!(meta & SM_DSTART)) sV += 1;
+                if (s.flags & NF_HASH) sH += 1;
+                const uint32_t fl2 = (meta & SM_SKIPE) ? M_SKIPE : 0;
+                expand(s, lc, d, fl2, key, lc < d ? w[CK_(lc, d, 28)] : 0u, w[CK_(lc - 1, d, 29)], x);
+            }
+            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+            const uint64_t e0 = __ballot(x.ne >= 1), e1 = __ballot(x.ne >= 2);
+            const uint32_t ptot = __popcll(b0) + __popcll(b1);
+            const uint32_t etot = __popcll(e0) + __popcll(e1);
+            if (qn + ptot > a.s_qcap || on + etot > a.s_ocap) { err = true; break; }
+            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+            if (x.np >= 1) {
+                const uint32_t pos = qn + pre;
+                qpar[pos] = s.child; qpw[pos] = x.pw0; qkey[pos] = x.pk0;
+                qmeta[pos] = (lc + 1) | (x.pf0 & M_SKIPE ? SM_SKIPE : 0);
+            }
+            if (x.np >= 2) {
+                const uint32_t pos = qn + pre + 1;
+                qpar[pos] = s.child; qpw[pos] = x.pw1; qkey[pos] = x.pk1;
+                qmeta[pos] = (lc + 1) | (x.pf1 & M_SKIPE ? SM_SKIPE : 0);
+            }
+            qn += ptot;
+            const uint32_t epre = prefix_count(e0) + prefix_count(e1);
+            if (x.ne >= 1) { ofid[on + epre] = x.ef0; okey[on + epre] = x.ek0; }
+            if (x.ne >= 2) { ofid[on + epre + 1] = x.ef1; okey[on + epre + 1] = x.ek1; }
+            on += etot;
+            __threadfence_block();
+            __syncthreads();
+        }
+        if (err) {
+            if (lane == 0) atomicOr(&a.ctrl[CTRL_ERR], ERR_SLOW_SCRATCH);
+            __syncthreads();
+            continue;
+        }
+        // sort the row (path code, or filter bytes for deep/irregular topics)
+        uint32_t np2 = 1;
+        while (np2 < on) np2 <<= 1;
+        if (on > 1) {
+            if (np2 <= SORT_LDS) {
+                for (uint32_t i = lane; i < np2; i += 64) {
+                    sk[i] = i < on ? okey[i] : ~0ull;
+                    sf[i] = i < on ? ofid[i] : NONE;
+                }
+                __syncthreads();
+                bitonic<CK>(a, sk, sf, np2, by_bytes);
+                for (uint32_t i = lane; i < on; i += 64) ofid[i] = sf[i];
+            } else if (np2 <= a.s_ocap) {
+                for (uint32_t i = on + lane; i < np2; i += 64) { okey[i] = ~0ull; ofid[i] = NONE; }
+                __threadfence_block();
+                __syncthreads();
+                bitonic<CK>(a, okey, ofid, np2, by_bytes);
+            } else {
+                if (lane == 0) atomicOr(&a.ctrl[CTRL_ERR], ERR_SLOW_SCRATCH);
+                continue;
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        uint32_t base = 0;
+        if (lane == 0 && on) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], on);
+        base = __shfl(base, 0, 64);
+        const uint64_t dst = a.slow_base + base;
+        if (dst + on <= a.fids_cap) {
+            for (uint32_t i = lane; i < on; i += 64) a.fids[CK_(dst + i, a.fids_cap, 30)] = ofid[i];
+        } else if (lane == 0) {
+            atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);
+        }
+        if (lane == 0) { a.count[t] = on; a.src[t] = dst; }
+        sM += (lane == 0) ? on : 0;
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sV += __shfl_xor(sV, o, 64); sH += __shfl_xor(sH, o, 64);
+        sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
+    }
+    if (lane == 0 && sS) {
+        atomicAdd(&a.stats[ST_VISITS], sV); atomicAdd(&a.stats[ST_HASH], sH);
+        atomicAdd(&a.stats[ST_WORDS], sW); atomicAdd(&a.stats[ST_MATCHES], sM);
+        atomicAdd(&a.stats[ST_SLOW], sS);
+    }
+}
+
+// ------------------------------------------------------------ CSR build
+
+constexpr uint32_t SCAN_BLOCK = 1024;
+constexpr uint32_t SCAN_PER_THREAD = 4;
+constexpr uint32_t SCAN_TILE = SCAN_BLOCK * SCAN_PER_THREAD;
+
+uint32_t scan_block_count(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+
+__device__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += u;
+    }
+    if (lane == 63) sh[wid] = incl;
+    __syncthreads();
+    if (wid == 0) {
+        const uint32_t nw = blockDim.x >> 6;
+        uint32_t s = lane < nw ? sh[lane] : 0;
+        uint32_t si = s;
+        for (int o = 1; o < 64; o <<= 1) {
+            uint32_t u = __shfl_up(si, o, 64);
+            if (lane >= (uint32_t)o) si += u;
+        }
+        if (lane < nw) sh[lane] = si - s;
+        if (lane == nw - 1) sh[32] = si;
+    }
+    __syncthreads();
+    total = sh[32];
+    const uint32_t r = sh[wid] + incl - v;
+    __syncthreads();
+    return r;
+}
+
+// Pass 1: per-block exclusive scan of count[] (slow/overflow rows included).
+__global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_local(ScanArgs a) {
+    __shared__ uint32_t sh[33];
+    const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER_THREAD;
+    uint32_t v[SCAN_PER_THREAD];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_PER_THREAD; ++i) {
+        v[i] = (base + i < a.n) ? a.count[base + i] : 0u;
+        s += v[i];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(s, sh, tot);
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_PER_THREAD; ++i) {
+        if (base + i < a.n) a.row_off[base + i] = ex;
+        ex += v[i];
+    }
+    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
+}
+
+// Pass 2: exclusive scan of the block sums (single block), total -> row_off[n].
+__global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t nblocks, uint32_t* d_total) {
+    __shared__ uint32_t sh[33];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += SCAN_BLOCK) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < nblocks ? a.block_sums[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(v, sh, tot);
+        if (i < nblocks) a.block_sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        a.row_off[a.n] = carry;
+        if (d_total) *d_total = carry;
+    }
+}
+
+// Pass 3: finish offsets, copy each row from staging into the CSR.
+template <bool CK>
+__global__ __launch_bounds__(256) void tm_copy_rows(ScanArgs a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
+    a.row_off[t] = off;
+    const uint32_t c = a.count[t];
+    if ((uint64_t)off + c > a.ids_cap) return;   // staging overflow already flagged
+    const uint64_t s = a.src[t];
+    if (CK && s + c > a.fids_cap) {
+        if (a.dbg && atomicCAS(&a.dbg[0], 0u, 40u) == 0u) { a.dbg[1] = t; a.dbg[2] = (uint32_t)s; a.dbg[4] = c; }
+        return;
+    }
+    for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.fids[s + i];
+}
+
+__global__ void tm_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) slots[idx[i]] = vals[i];
+}
+
+__global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx, const uint64_t* off,
+                                 const uint32_t* len, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { foff[idx[i]] = off[i]; flen[idx[i]] = len[i]; }
+}
+
+// ------------------------------------------------------------ launchers
+
+hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked) {
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    if (ev_a) (void)hipEventRecord(ev_a, s);
+    if (ntiles) {
+        const uint32_t grid = min(ntiles, 256u * 16u);
+        if (checked) hipLaunchKernelGGL(tm_match_tiles<true>, dim3(grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(tm_match_tiles<false>, dim3(grid), dim3(64), 0, s, a);
+    }
+    if (ev_b) (void)hipEventRecord(ev_b, s);
+    if (checked) hipLaunchKernelGGL(tm_match_slow<true>, dim3(a.s_waves), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(tm_match_slow<false>, dim3(a.s_waves), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total) {
+    const uint32_t nb = scan_block_count(a.n);
+    if (nb) hipLaunchKernelGGL(tm_scan_local, dim3(nb), dim3(SCAN_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(tm_scan_sums, dim3(1), dim3(SCAN_BLOCK), 0, s, a, nb, d_total);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(const ScanArgs& a, hipStream_t s, bool checked) {
+    if (a.n && checked) hipLaunchKernelGGL(tm_copy_rows<true>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    else if (a.n) hipLaunchKernelGGL(tm_copy_rows<false>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_scatter_slots, dim3((n + 255) / 256), dim3(256), 0, s, slots, idx, vals, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx, const uint64_t* off,
+                                const uint32_t* len, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_scatter_fmeta, dim3((n + 255) / 256), dim3(256), 0, s, foff, flen, idx, off, len, n);
+    return hipGetLastError();
+}
+
+}  // namespace etm

@@ -1,0 +1,171 @@
+/*
+ * emqx_tm.h -- C ABI of the MI355X topic-matching engine (libemqx_tm.so).
+ *
+ * Drop-in boundary for EMQ X's publish-time matching path.  The reference is
+ * pure Erlang and has no FFI of its own; each entry point below names the
+ * reference function it replaces (paths relative to the reference tree).  An
+ * erl_nif shim (emqx_amd/csrc/nif/emqx_tm_nif.c) binds these
+ * 1:1 to the Erlang module API.
+ *
+ * Conventions
+ *   - plain pointers + sizes; caller-owned inputs are borrowed for the call;
+ *   - return codes: 0 = ok, negative errno-style values (TM_E*) on error;
+ *     predicates return 0/1; no C++ exceptions cross this boundary;
+ *   - one engine = one trie replica on one HIP device.  Calls on one engine are
+ *     serialised by an internal mutex (readers and the single writer of the
+ *     reference's mnesia tables become ordered operations on one HIP stream, so
+ *     a match issued after tm_trie_insert returns always sees the filter:
+ *     read-your-writes, src/emqx_broker.erl:150-158).
+ */
+#ifndef EMQX_TM_H
+#define EMQX_TM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TM_OK          0
+#define TM_ENOENT     (-2)
+#define TM_EIO        (-5)
+#define TM_ENOMEM     (-12)
+#define TM_ENODEV     (-19)
+#define TM_EINVAL     (-22)
+#define TM_EOVERFLOW  (-75)
+#define TM_EABORT     (-125)   /* mnesia:abort({node_not_found, _}), src/emqx_trie.erl:203 */
+
+#if defined(__GNUC__)
+#define TM_API __attribute__((visibility("default")))
+#else
+#define TM_API
+#endif
+
+#define TM_NONE        0xFFFFFFFFu
+#define TM_MAX_TOPIC_LEN 4096  /* ?MAX_TOPIC_LEN, src/emqx_topic.erl:45 */
+
+typedef struct tm_engine tm_engine;
+typedef struct tm_batch  tm_batch;
+
+typedef struct {
+    int32_t  device;        /* HIP device ordinal; -1 = host-only engine (trie ops, no match) */
+    uint32_t init_slots;    /* initial edge-hash capacity in 32-B slots (0 = default) */
+    uint32_t host_threads;  /* threads for host tokenise+intern (0 = auto) */
+    uint32_t flags;         /* reserved, must be 0 */
+} tm_config;
+
+/* #trie_node{} view (include/emqx.hrl:98-103) */
+typedef struct {
+    uint32_t edge_count;
+    uint32_t has_topic;     /* topic =/= undefined */
+    uint32_t filter_id;     /* id of `topic` when has_topic, else TM_NONE */
+} tm_trie_node;
+
+/* CSR result: row i = sorted (Erlang binary order), deduplicated filter ids
+ * matching topic i.  Memory is engine-owned, valid until the next match call on
+ * the same engine (or tm_batch_free for batch results). */
+typedef struct {
+    uint32_t        n_topics;
+    uint64_t        n_matches;
+    const uint32_t* row_offsets;  /* n_topics + 1 entries */
+    const uint32_t* filter_ids;   /* n_matches entries */
+} tm_result;
+
+typedef struct {
+    uint64_t topics;        /* topics matched */
+    uint64_t visits;        /* V: match_node invocations (src/emqx_trie.erl:165-177) */
+    uint64_t hash_hits;     /* H: 'match_#' hits (src/emqx_trie.erl:181-186) */
+    uint64_t words;         /* sum of topic depths d */
+    uint64_t matches;       /* sum |M(t)| */
+    uint64_t slow_topics;   /* topics served by the generic (deep/irregular/overflow) kernel */
+    uint64_t overflow_tiles;
+    float    ms_match;      /* device time of the frontier kernel (last launch) */
+    float    ms_total;      /* device time of the whole batch pipeline (last launch) */
+} tm_batch_stats;
+
+typedef struct {
+    uint64_t version;       /* bumped on every trie mutation */
+    uint64_t nodes;         /* live trie nodes incl. root */
+    uint64_t edges;         /* live edges (ets:info(emqx_trie, size)) */
+    uint64_t filters;       /* nodes with topic =/= undefined */
+    uint64_t words;         /* interned words */
+    uint64_t slots;         /* edge-hash capacity (32-B slots) */
+    uint64_t device_bytes;  /* HBM held by the trie replica */
+    uint64_t uploads_full;  /* full trie uploads */
+    uint64_t uploads_delta; /* incremental delta uploads */
+    uint64_t delta_slots;   /* slots written by delta uploads */
+} tm_engine_stats;
+
+/* ---- engine ---------------------------------------------------------- */
+TM_API int  tm_create(const tm_config* cfg, tm_engine** out);
+TM_API void tm_destroy(tm_engine* e);
+TM_API uint64_t tm_version(tm_engine* e);
+TM_API int  tm_stats(tm_engine* e, tm_engine_stats* out);
+/* Applies pending trie deltas to the device replica (also done implicitly by
+ * every match call). */
+TM_API int  tm_sync(tm_engine* e);
+
+/* ---- emqx_trie (src/emqx_trie.erl) ----------------------------------- */
+/* emqx_trie:insert/1 (:81-93): idempotent; add_path/1 (:145-158) semantics. */
+TM_API int  tm_trie_insert(tm_engine* e, const uint8_t* topic, size_t len);
+/* emqx_trie:delete/1 (:107-116) + delete_path/1 (:190-204). */
+TM_API int  tm_trie_delete(tm_engine* e, const uint8_t* topic, size_t len);
+/* emqx_trie:lookup/1 (:102-104): returns 1 found, 0 not found.  is_root
+ * selects the atom `root` node id. */
+TM_API int  tm_trie_lookup(tm_engine* e, const uint8_t* node_id, size_t len, int is_root,
+                    tm_trie_node* out);
+/* emqx_trie:empty/0 (:119-121): 1 if the edge table is empty. */
+TM_API int  tm_trie_empty(tm_engine* e);
+/* emqx_trie:match/1 (:96-99) for one topic: writes up to cap ids (sorted by
+ * filter bytes), *n_out = full count.  Runs on the device. */
+TM_API int  tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len,
+                   uint32_t* ids, uint32_t cap, uint32_t* n_out);
+
+/* ---- batched publish matching: emqx_router:match_routes/1 hot path ---- */
+/* (src/emqx_router.erl:127-141 applied to a batch of publishes,
+ *  src/emqx_broker.erl:201-210).  topics = concatenated topic bytes,
+ *  offsets[n+1] byte offsets.  Result as tm_result above. */
+TM_API int  tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
+                    uint32_t n, tm_result* out);
+
+/* Split form for pipelining / device-resident benchmarking:
+ * prepare = host tokenise+intern+H2D (emqx_topic:words/1, src/emqx_topic.erl:158-164);
+ * launch  = enqueue the device pipeline (async);
+ * wait    = block until done; result = D2H of the CSR. */
+TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
+                      uint32_t n, tm_batch** out);
+TM_API int  tm_batch_launch(tm_engine* e, tm_batch* b);
+TM_API int  tm_batch_wait(tm_engine* e, tm_batch* b);
+TM_API int  tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out);
+TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
+/* Device pointers of the batch's CSR (valid after wait): row_offsets, ids. */
+TM_API int  tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row_offsets,
+                         const uint32_t** d_ids, uint64_t* n_matches);
+TM_API void tm_batch_free(tm_engine* e, tm_batch* b);
+
+/* ---- filters ---------------------------------------------------------- */
+/* Bytes of a filter id returned by a match (the #trie_node.topic binary). */
+TM_API const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len);
+/* Id of an inserted filter, TM_ENOENT if absent. */
+TM_API int  tm_filter_id(tm_engine* e, const uint8_t* filter, size_t len, uint32_t* id);
+
+/* ---- emqx_topic (src/emqx_topic.erl), host predicates ----------------- */
+/* emqx_topic:match/2 (:65-87) on binaries: 1 match, 0 no match. */
+TM_API int  tm_topic_match(const uint8_t* name, size_t name_len, const uint8_t* filter, size_t filter_len);
+/* emqx_topic:wildcard/1 (:52-62). */
+TM_API int  tm_topic_wildcard(const uint8_t* topic, size_t len);
+/* emqx_topic:validate/2 (:96-127): 0 ok, TM_EINVAL otherwise; *reason set to
+ * one of "empty_topic", "topic_too_long", "topic_invalid_#",
+ * "topic_invalid_char", "topic_name_error". */
+TM_API int  tm_topic_validate(int is_name, const uint8_t* topic, size_t len, const char** reason);
+
+/* ---- diagnostics ------------------------------------------------------ */
+/* Text of the last TM_EIO on this thread (HIP error string + call site). */
+TM_API const char* tm_last_error(void);
+TM_API const char* tm_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_TM_H */
