@@ -295,7 +295,7 @@ struct tm_engine {
     bool delta_inflight = false;
 
     // slow-path scratch
-    uint32_t s_waves = 128, s_qcap = 1u << 14, s_ocap = 1u << 15;
+    uint32_t s_waves = 512, s_qcap = 1u << 13, s_ocap = 1u << 14;
     uint32_t *d_sqpar = nullptr, *d_sqpw = nullptr, *d_sqmeta = nullptr, *d_sofid = nullptr;
     unsigned long long *d_sqkey = nullptr, *d_sokey = nullptr;
     size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
@@ -303,7 +303,7 @@ struct tm_engine {
     uint64_t version = 1;
     uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
-    uint32_t row_cap = 64;         // K: fast-path row slots per topic (TM_ROWCAP)
+    uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
     uint32_t* d_dbg = nullptr;
     uint32_t* h_dbg = nullptr;
     size_t c_dbg = 0, ch_dbg = 0;
@@ -789,7 +789,7 @@ struct tm_engine {
     int reserve_rows(tm_batch* b) {
         int rc;
         const uint64_t fast = (uint64_t)b->n * row_cap;
-        if (b->slow_cap == 0) b->slow_cap = std::max<uint64_t>((uint64_t)b->n / 4, 1u << 16);
+        if (b->slow_cap == 0) b->slow_cap = std::max<uint64_t>((uint64_t)b->n, 1u << 16);
         const uint64_t need = fast + b->slow_cap;
         if (need >= 0xFFFFFFF0ull) return TM_EOVERFLOW;
         if ((rc = dev_reserve(b->d_fids, b->c_fids, need))) return rc;
@@ -934,7 +934,7 @@ struct tm_engine {
         device = cfg ? cfg->device : -1;
         const char* ck = getenv("TM_CHECKED");
         checked = ck && ck[0] == '1';
-        if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::max(1, atoi(rcap));
+        if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         // root node id 0 (absent until the first add_path, like the reference)
         n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);

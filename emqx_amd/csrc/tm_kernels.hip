@@ -315,22 +315,32 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
             sM += c_me;
         }
 
-        // ---- sort each row in place by path code: lane i holds element i,
-        //      rank = #{j : key_j < key_i} via broadcast shuffles (keys unique per row)
+        // ---- sort each row in place by path code.  Lane i holds elements i and
+        //      i + 64 (row_cap <= ROWCAP_MAX = 128); rank = #{j : key_j < key_i}
+        //      via broadcast shuffles (keys are unique within a row).
         for (uint32_t tt = 0; tt < tend - t0; ++tt) {
             const uint32_t c = L.cnt[tt];
             const uint32_t ftt = __shfl(fl, tt, 64);
             if (c < 2 || c > a.row_cap || (ftt & TF_SLOW)) continue;
             const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
-            uint64_t kk = ~0ull;
-            uint32_t ff = 0;
-            if (lane < c) { kk = a.rkeys[CK_(rb + lane, a.slow_base, 18)]; ff = a.fids[CK_(rb + lane, a.slow_base, 19)]; }
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < c; ++j) {
-                const uint64_t kj = __shfl(kk, j, 64);
-                rank += kj < kk ? 1u : 0u;
+            uint64_t k0 = ~0ull, k1 = ~0ull;
+            uint32_t f0 = 0, f1 = 0;
+            if (lane < c) { k0 = a.rkeys[CK_(rb + lane, a.slow_base, 18)]; f0 = a.fids[CK_(rb + lane, a.slow_base, 19)]; }
+            if (lane + 64 < c) { k1 = a.rkeys[CK_(rb + lane + 64, a.slow_base, 18)]; f1 = a.fids[CK_(rb + lane + 64, a.slow_base, 19)]; }
+            uint32_t r0 = 0, r1 = 0;
+            const uint32_t c0 = min(c, 64u);
+            for (uint32_t j = 0; j < c0; ++j) {
+                const uint64_t kj = __shfl(k0, j, 64);
+                r0 += kj < k0 ? 1u : 0u;
+                r1 += kj < k1 ? 1u : 0u;
             }
-            if (lane < c) a.fids[CK_(rb + rank, a.slow_base, 20)] = ff;
+            for (uint32_t j = 64; j < c; ++j) {
+                const uint64_t kj = __shfl(k1, j - 64, 64);
+                r0 += kj < k0 ? 1u : 0u;
+                r1 += kj < k1 ? 1u : 0u;
+            }
+            if (lane < c) a.fids[CK_(rb + r0, a.slow_base, 20)] = f0;
+            if (lane + 64 < c) a.fids[CK_(rb + r1, a.slow_base, 20)] = f1;
         }
         __syncthreads();
     }
@@ -629,10 +639,9 @@ __global__ __launch_bounds__(256) void tm_copy_rows(ScanArgs a) {
     const uint32_t c = a.count[t];
     if ((uint64_t)off + c > a.ids_cap) return;   // staging overflow already flagged
     const uint64_t s = a.src[t];
-    if (CK && s + c > a.fids_cap) {
-        if (a.dbg && atomicCAS(&a.dbg[0], 0u, 40u) == 0u) { a.dbg[1] = t; a.dbg[2] = (uint32_t)s; a.dbg[4] = c; }
-        return;
-    }
+    // a row whose slow-path output did not fit (ERR_STAGING, the host reruns
+    // the batch with a larger region) is skipped, never read out of range
+    if (s + c > a.fids_cap) return;
     for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.fids[s + i];
 }
 
