@@ -1,0 +1,257 @@
+"""bench.py -- publishes matched/sec at 1M wildcard subscriptions (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload: 1,000,000 distinct wildcard filters
+(depth <= 7, V = 1024, Zipf 1.1, p+ = 0.15, p# = 0.25, seed 2) compiled into
+the HBM trie replica; a batch of 10,000,000 synthetic publishes per GPU
+(seed 1000 + rank), tokenised + interned on the host and resident in HBM before
+timing.  One step = the whole device pipeline over the batch: frontier-walk
+kernel, generic slow path, CSR scan and sorted-row finalize -- every topic's
+complete, byte-sorted match set lands in HBM.
+
+Multi-GPU: one process per GPU (torchrun), the trie replicated on every GPU,
+each rank matching its own 10M batch (replicated mode, no data-path
+collective) -> "scaling": "weak"; value = all ranks' publishes / max rank time.
+
+Extra fields: roofline (HBM, algorithmic bytes per launch counted by the kernel,
+over the match kernel's HIP-event time), cpu_baseline (the CPU restatement of
+emqx_router:match_routes/1 on this host, rank 0 / N = 1 only), p99 batch latency
+at B = 65,536 and the host-inclusive end-to-end rate (bytes in host RAM ->
+sorted CSR in host RAM).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+ALG_BYTES_PER_VISIT = 64       # one 64-B DRAM request per visited trie node
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline(filters, topics, sample_1t, sample_mt, threads):
+    """emqx_router:match_routes/1 restated in C (oracle/, prefix-string ETS layout),
+    timed on this host's cores over a bounded sample of the same workload."""
+    from oracle import pyoracle
+    orc = pyoracle.Oracle()
+    t0 = time.time()
+    for f in filters.tolist():
+        orc.add_route(f)
+    build_s = time.time() - t0
+    s1 = topics.slice(0, sample_1t)
+    t0 = time.time()
+    orc.match_routes_batch(s1.buf, s1.offs, nthreads=1)
+    dt1 = time.time() - t0
+    sm = topics.slice(0, sample_mt)
+    t0 = time.time()
+    st = orc.match_routes_batch(sm.buf, sm.offs, nthreads=threads)
+    dtm = time.time() - t0
+    orc.close()
+    return {
+        "value": sample_mt / dtm,
+        "unit": "publishes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"C2 trie (1M filters, ETS-layout C restatement, build {build_s:.1f}s); "
+                   f"{sample_mt} publishes on {threads} threads in {dtm:.2f}s; "
+                   f"{sample_1t} publishes on 1 thread in {dt1:.2f}s = {sample_1t / dt1:.0f}/s; "
+                   f"routes returned {st['routes']}; cpu {cpu_info()}"),
+        "value_1thread": sample_1t / dt1,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--topics", type=int, default=10_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--latency-batches", type=int, default=200)
+    ap.add_argument("--profile", action="store_true",
+                    help="only the timed steps (no latency / e2e / cpu legs): for rocprofv3 runs")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {ws}; using WORLD_SIZE")
+    pg = None
+    if ws > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist
+
+    from emqx_amd import gen
+    from emqx_amd.engine import Engine
+
+    p = gen.C2
+    t0 = time.time()
+    filters = gen.gen_filters(p)
+    topics = gen.gen_topics(p, filters, 1000 + rank, args.topics)
+    log(f"[rank {rank}] generated {len(filters)} filters, {len(topics)} topics in {time.time() - t0:.1f}s")
+
+    eng = Engine(device=local)
+    t0 = time.time()
+    fl = filters.tolist()
+    for f in fl:
+        eng.insert(f)
+    eng.sync()
+    est = eng.stats()
+    log(f"[rank {rank}] trie built+uploaded in {time.time() - t0:.1f}s: {est}")
+
+    t0 = time.time()
+    b = eng.prepare(topics)
+    log(f"[rank {rank}] batch tokenised + resident in HBM in {time.time() - t0:.1f}s")
+
+    for _ in range(args.warmup):
+        b.launch().wait()
+    st = b.stats()
+    if st["topics"] != len(topics):
+        raise RuntimeError(f"batch stats inconsistent: {st}")
+
+    def barrier():
+        if pg is not None:
+            pg.barrier()
+
+    barrier()
+    ms_match, ms_total = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.launch().wait()
+        s = b.stats()
+        ms_match.append(s["ms_match"])
+        ms_total.append(s["ms_total"])
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if pg is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    n = len(topics)
+    value = ws * n * args.steps / elapsed
+    ms_step = 1e3 * elapsed / args.steps
+
+    # roofline of the dominant kernel (tm_match_tiles): algorithmic bytes per launch
+    alg_bytes = (ALG_BYTES_PER_VISIT * (st["visits"] + st["hash_hits"]) + 4 * st["words"]
+                 + 4 * st["matches"] + 4 * n)
+    k_ms = float(np.mean(ms_match))
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("workload") == "C2" and pmc.get("topics") == n:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    out = {
+        "metric": "publishes matched/sec (node) at 1M wildcard subs; p99 batch match latency",
+        "value": value,
+        "unit": "publishes/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded generator, SURVEY.md §8d C2)",
+        "config": {"workload": "C2: 1M wildcard filters depth<=7, 10M-publish batch per GPU",
+                   "filters": len(filters), "publishes_per_gpu": n, "mode": "replicated",
+                   "parallelism": f"replicated trie x{ws}, batches split per GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "tm_match_tiles", "kernel_ms": k_ms,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "per_publish": {"V": st["visits"] / n, "H": st["hash_hits"] / n,
+                                     "d": st["words"] / n, "M": st["matches"] / n}},
+        "pipeline_ms": float(np.mean(ms_total)),
+        "matches_per_step": st["matches"],
+        "slow_path_topics": st["slow_topics"],
+    }
+
+    if args.profile:
+        args.no_cpu = True
+    if rank == 0 and not args.profile:
+        # p99 batch latency at B = 65,536 (device-resident batches, launch -> results in HBM)
+        try:
+            lb = eng.prepare(topics.slice(0, 65536))
+            for _ in range(5):
+                lb.launch().wait()
+            lat = []
+            for _ in range(args.latency_batches):
+                t = time.perf_counter()
+                lb.launch().wait()
+                lat.append(1e3 * (time.perf_counter() - t))
+            lb.free()
+            out["p99_batch_ms"] = float(np.percentile(lat, 99))
+            out["p50_batch_ms"] = float(np.percentile(lat, 50))
+            out["latency_batch"] = 65536
+        except Exception as e:  # report, don't hide
+            out["p99_batch_ms"] = None
+            out["latency_error"] = str(e)
+        # host-inclusive end to end: topic bytes in host RAM -> sorted CSR in host RAM
+        sub = topics.slice(0, min(n, 2_000_000))
+        eng.match_batch(sub)
+        t = time.perf_counter()
+        eng.match_batch(sub)
+        out["e2e_host_publishes_per_s"] = len(sub) / (time.perf_counter() - t)
+
+    b.free()
+
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        threads = min(os.cpu_count() or 1, 16)
+        out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), threads)
+        out["speedup_vs_cpu_allcore"] = value / out["cpu_baseline"]["value"]
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -203,12 +203,13 @@ struct tm_batch {
     uint8_t* d_tflags = nullptr;
     size_t c_words = 0, c_toff = 0, c_slow = 0, c_tflags = 0;
     // device outputs
-    uint32_t *d_count = nullptr, *d_fids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
-    unsigned long long *d_src = nullptr, *d_rkeys = nullptr;
+    uint32_t *d_count = nullptr, *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
+    unsigned long long *d_src = nullptr, *d_rows = nullptr;
     uint32_t *d_bsums = nullptr, *d_ctrl = nullptr, *d_ovf = nullptr, *d_total = nullptr;
     unsigned long long* d_stats = nullptr;
-    size_t c_count = 0, c_src = 0, c_fids = 0, c_rkeys = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
-    uint64_t slow_cap = 0;      // slow-path region of fids[] (after the n * K fast rows)
+    size_t c_count = 0, c_src = 0, c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
+    uint32_t* h_total = nullptr;
+    size_t ch_total = 0;
     size_t c_ctrl = 0, c_stats = 0, c_total = 0;
     // pinned host results
     uint32_t* h_rowoff = nullptr;
@@ -220,10 +221,13 @@ struct tm_batch {
     bool launched = false, done = false;
     uint64_t total = 0;
     tm_batch_stats st{};
+    ScanArgs scan_args{};
 
     void release() {
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
-        dev_free(d_count); dev_free(d_src); dev_free(d_fids); dev_free(d_rkeys); dev_free(d_rowoff); dev_free(d_ids);
+        dev_free(d_count); dev_free(d_src); dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
+        if (h_total) (void)hipHostFree(h_total);
+        h_total = nullptr;
         dev_free(d_bsums); dev_free(d_ctrl); dev_free(d_ovf); dev_free(d_total); dev_free(d_stats);
         if (h_rowoff) (void)hipHostFree(h_rowoff);
         if (h_ids) (void)hipHostFree(h_ids);
@@ -249,7 +253,7 @@ struct tm_engine {
     WordDict dict;
 
     // node table (host)
-    std::vector<uint32_t> n_parent, n_word, n_ec, n_plus, n_hash, n_bloom, n_inslot, n_flen;
+    std::vector<uint32_t> n_parent, n_word, n_ec, n_plus, n_hash, n_inslot, n_flen;
     std::vector<uint64_t> n_foff;
     std::vector<uint8_t> n_live, n_topic;
     std::vector<uint32_t> free_nodes;
@@ -312,40 +316,45 @@ struct tm_engine {
 
     // ------------------------------------------------------------ hash
     uint32_t nslots() const { return (uint32_t)slots.size(); }
-    uint32_t bmask() const { return nslots() / 2 - 1; }
+    uint32_t nbuckets() const { return nslots() / BUCKET; }
 
+    // (parent, word) lookup: the same probe sequence as the kernel's probe()
     uint32_t find_slot(uint32_t p, uint32_t w) const {
-        uint32_t b = edge_hash(p, w) & bmask();
+        const uint32_t nb = nbuckets();
+        uint32_t b = home_bucket(p, w, nb);
         for (uint32_t i = 0; i <= max_disp; ++i) {
-            for (uint32_t s = 0; s < 2; ++s) {
-                const Slot& e = slots[2 * b + s];
-                if (e.parent == p && e.word == w) return 2 * b + s;
+            for (uint32_t s = 0; s < BUCKET; ++s) {
+                const Slot& e = slots[b * BUCKET + s];
+                if (e.parent == p && e.word == w) return b * BUCKET + s;
             }
-            if (slots[2 * b].parent == SLOT_EMPTY || slots[2 * b + 1].parent == SLOT_EMPTY) return NONE;
-            b = (b + 1) & bmask();
+            if (slots[b * BUCKET + BUCKET - 1].parent == SLOT_EMPTY) return NONE;
+            b = (b + 1 == nb) ? 0 : b + 1;
         }
         return NONE;
     }
 
+    // first free slot (empty or tombstone) along the probe sequence; slots of a
+    // bucket are taken in order, so "last slot empty" <=> "bucket has a hole"
     uint32_t place_slot(std::vector<Slot>& tab, uint32_t p, uint32_t w, uint32_t& disp, bool& was_empty) const {
-        const uint32_t mask = (uint32_t)tab.size() / 2 - 1;
-        uint32_t b = edge_hash(p, w) & mask;
+        const uint32_t nb = (uint32_t)(tab.size() / BUCKET);
+        uint32_t b = home_bucket(p, w, nb);
         for (uint32_t i = 0;; ++i) {
-            for (uint32_t s = 0; s < 2; ++s) {
-                Slot& e = tab[2 * b + s];
+            for (uint32_t s = 0; s < BUCKET; ++s) {
+                Slot& e = tab[b * BUCKET + s];
                 if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) {
                     disp = i;
                     was_empty = e.parent == SLOT_EMPTY;
-                    return 2 * b + s;
+                    return b * BUCKET + s;
                 }
             }
-            b = (b + 1) & mask;
+            b = (b + 1 == nb) ? 0 : b + 1;
         }
     }
 
+    // rebuild at load <= 0.6 (any bucket count: home_bucket is multiply-shift)
     void rehash(size_t want_slots) {
-        size_t ns = 1024;
-        while (ns < want_slots) ns <<= 1;
+        size_t nb = std::max<size_t>((want_slots + BUCKET - 1) / BUCKET, 256);
+        const size_t ns = nb * BUCKET;
         std::vector<Slot> tab(ns);
         for (Slot& s : tab) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
         uint32_t md = 0;
@@ -356,7 +365,7 @@ struct tm_engine {
             bool was_empty;
             uint32_t i = place_slot(tab, e.parent, e.word, disp, was_empty);
             tab[i] = e;
-            n_inslot[e.child] = i;
+            n_inslot[e.child & ID_MASK] = i;
             md = std::max(md, disp);
             ++used;
         }
@@ -374,8 +383,8 @@ struct tm_engine {
     }
 
     uint32_t insert_edge(uint32_t p, uint32_t w, uint32_t c) {
-        if ((used_slots + 1) * 2 > slots.size() || max_disp > 24)
-            rehash(std::max<size_t>((live_edges + 1) * 3, slots.size() * (max_disp > 24 ? 2 : 1)));
+        if ((used_slots + 1) * 5 > slots.size() * 4 || max_disp > 16)
+            rehash(std::max<size_t>((size_t)((live_edges + 1) / 0.6), slots.size() * (max_disp > 16 ? 2 : 1)));
         uint32_t disp;
         bool was_empty;
         uint32_t i = place_slot(slots, p, w, disp, was_empty);
@@ -401,17 +410,19 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------ nodes
+    bool node_capacity_left() const { return !free_nodes.empty() || n_parent.size() < MAX_NODES; }
+
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
         if (!free_nodes.empty()) { id = free_nodes.back(); free_nodes.pop_back(); }
         else {
             id = (uint32_t)n_parent.size();
             n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
-            n_hash.push_back(NONE); n_bloom.push_back(0); n_inslot.push_back(NONE); n_flen.push_back(0);
+            n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
             n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
         }
         n_parent[id] = parent; n_word[id] = word; n_ec[id] = 0; n_plus[id] = NONE; n_hash[id] = NONE;
-        n_bloom[id] = 0; n_inslot[id] = NONE; n_live[id] = 1; n_topic[id] = 0;
+        n_inslot[id] = NONE; n_live[id] = 1; n_topic[id] = 0;
         ++live_nodes;
         return id;
     }
@@ -438,11 +449,9 @@ struct tm_engine {
         const uint32_t i = n_inslot[c];
         if (i == NONE) return;
         Slot& e = slots[i];
-        e.term = n_topic[c] ? c : NONE;
-        e.hterm = hterm_of(c);
-        e.flags = summary_flags(c);
-        e.bloom = n_bloom[c];
-        e.spare = 0;
+        e.child = c | (n_topic[c] ? B_TOPIC : 0u) | (n_plus[c] != NONE ? B_PLUS : 0u);
+        const uint32_t h = n_hash[c];
+        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && n_topic[h]) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
         mark_dirty(i);
     }
 
@@ -451,7 +460,7 @@ struct tm_engine {
         r.live = n_live[ROOT];
         r.hterm = hterm_of(ROOT);
         r.flags = summary_flags(ROOT);
-        r.bloom = n_bloom[ROOT];
+        r.pad = 0;
         return r;
     }
 
@@ -500,7 +509,7 @@ struct tm_engine {
         for (uint32_t w : ids) {
             const uint32_t s = find_slot(n, w);
             if (s == NONE) return NONE;
-            n = slots[s].child;
+            n = slots[s].child & ID_MASK;
         }
         return n;
     }
@@ -514,6 +523,8 @@ struct tm_engine {
             if (!n_topic[found]) { set_topic(found, t, len); ++version; }
             return TM_OK;
         }
+        // node ids are 30-bit (two flag bits ride in the slot's id words)
+        if (n_parent.size() + ids.size() >= MAX_NODES && free_nodes.size() < ids.size()) return TM_ENOMEM;
         // add_path/1 for every triple (:145-158)
         uint32_t p = ROOT;
         for (uint32_t w : ids) {
@@ -527,11 +538,10 @@ struct tm_engine {
                 ++n_ec[p];
                 if (w == W_PLUS) n_plus[p] = c;
                 else if (w == W_HASH) n_hash[p] = c;
-                else n_bloom[p] |= bloom_bit(w);
                 insert_edge(p, w, c);
                 write_summary(p);
             } else {
-                c = slots[s].child;
+                c = slots[s].child & ID_MASK;
             }
             p = c;
         }
@@ -785,16 +795,15 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // fids[] = n * K fast row slots + the slow region; ids[] (CSR) has the same capacity
+    // rows[] = n * K fast-row slots (u64 path code | id); sfids[] = slow-path rows;
+    // ids[] = the CSR, sized from the last batch's total (grown on demand)
     int reserve_rows(tm_batch* b) {
         int rc;
-        const uint64_t fast = (uint64_t)b->n * row_cap;
-        if (b->slow_cap == 0) b->slow_cap = std::max<uint64_t>((uint64_t)b->n, 1u << 16);
-        const uint64_t need = fast + b->slow_cap;
-        if (need >= 0xFFFFFFF0ull) return TM_EOVERFLOW;
-        if ((rc = dev_reserve(b->d_fids, b->c_fids, need))) return rc;
-        if ((rc = dev_reserve(b->d_ids, b->c_ids, need))) return rc;
-        if ((rc = dev_reserve(b->d_rkeys, b->c_rkeys, std::max<uint64_t>(fast, 1)))) return rc;
+        const uint64_t fast = std::max<uint64_t>((uint64_t)b->n * row_cap, 1);
+        if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
+        if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n, 1u << 16)))) return rc;
+        if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 16, 1u << 16)))) return rc;
+        if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         return TM_OK;
     }
 
@@ -829,16 +838,14 @@ struct tm_engine {
         HIP_OK(hipMemsetAsync(b->d_stats, 0, ST_N * 8, stream));
         MatchArgs a{};
         a.slots = d_slots;
-        a.bucket_mask = bmask();
+        a.nbuckets = nbuckets();
         a.max_probe = max_disp;
         a.root = root_rec();
         a.foff = d_foff; a.flen = d_flen; a.fbytes = d_fbytes;
         a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
         a.slow_list = b->d_slow; a.n_slow = (uint32_t)b->h_slow.size();
-        a.count = b->d_count; a.src = b->d_src; a.fids = b->d_fids; a.rkeys = b->d_rkeys;
-        a.row_cap = row_cap;
-        a.slow_base = (uint64_t)b->n * row_cap;
-        a.fids_cap = std::min<uint64_t>(b->c_fids, a.slow_base + b->slow_cap);
+        a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
+        a.sfids = b->d_sfids; a.sfids_cap = b->c_sfids;
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
         a.s_qparent = d_sqpar; a.s_qpw = d_sqpw; a.s_qmeta = d_sqmeta; a.s_qkey = d_sqkey;
@@ -851,15 +858,18 @@ struct tm_engine {
         a.dbg = checked ? d_dbg : nullptr;
         HIP_OK(launch_match(a, stream, b->ev0, b->ev1, checked));
         ScanArgs s{};
-        s.count = b->d_count; s.src = b->d_src; s.fids = b->d_fids; s.fids_cap = a.fids_cap;
+        s.count = b->d_count; s.src = b->d_src; s.rows = b->d_rows; s.row_cap = row_cap;
+        s.sfids = b->d_sfids; s.sfids_cap = b->c_sfids;
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? d_dbg : nullptr;
         HIP_OK(launch_scan(s, stream, b->d_total));
-        HIP_OK(launch_copy(s, stream, checked));
+        HIP_OK(launch_finalize(s, stream, checked));
+        b->scan_args = s;
         HIP_OK(hipEventRecord(b->ev2, stream));
         HIP_OK(hipMemcpyAsync(b->h_ctrl, b->d_ctrl, CTRL_WORDS * 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipMemcpyAsync(b->h_stats, b->d_stats, ST_N * 8, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, stream));
         if (checked) HIP_OK(hipMemcpyAsync(h_dbg, d_dbg, 8 * 4, hipMemcpyDeviceToHost, stream));
         b->launched = true;
         b->done = false;
@@ -880,8 +890,7 @@ struct tm_engine {
             if (attempt >= 6) return TM_EOVERFLOW;
             if (err & ERR_STAGING) {
                 const uint64_t need = b->h_ctrl[CTRL_STAGING_TOP];
-                b->slow_cap = need + need / 4 + 1024;
-                int rc = reserve_rows(b);
+                int rc = dev_reserve(b->d_sfids, b->c_sfids, need + need / 4 + 1024);
                 if (rc) return rc;
             }
             if (err & ERR_SLOW_SCRATCH) {
@@ -890,6 +899,18 @@ struct tm_engine {
             }
             int rc = launch(b);
             if (rc) return rc;
+        }
+        // CSR capacity: the finalize pass is rerun alone when ids[] was too small
+        if (b->h_total[0] > b->c_ids) {
+            int rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->h_total[0] + b->h_total[0] / 4);
+            if (rc) return rc;
+            b->scan_args.ids = b->d_ids;
+            b->scan_args.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
+            // scan + finalize again (finalize turns the block-local offsets into global ones)
+            HIP_OK(launch_scan(b->scan_args, stream, b->d_total));
+            HIP_OK(launch_finalize(b->scan_args, stream, checked));
+            HIP_OK(hipEventRecord(b->ev2, stream));
+            HIP_OK(hipStreamSynchronize(stream));
         }
         float ms_match = 0, ms_total = 0;
         (void)hipEventElapsedTime(&ms_match, b->ev0, b->ev1);
@@ -938,7 +959,7 @@ struct tm_engine {
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         // root node id 0 (absent until the first add_path, like the reference)
         n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
-        n_hash.push_back(NONE); n_bloom.push_back(0); n_inslot.push_back(NONE); n_flen.push_back(0);
+        n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
         n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
         slots.clear();
         slots.resize(1024);

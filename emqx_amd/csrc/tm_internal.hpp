@@ -32,33 +32,42 @@ constexpr uint32_t C_EMPTY = 3;     // ''
 constexpr uint8_t TF_DOLLAR = 1;    // first byte is '$' (src/emqx_trie.erl:162-163)
 constexpr uint8_t TF_SLOW = 2;      // deep (> FAST_MAX_DEPTH) or irregular word
 
-// Fast path: 3-bit sort digits for levels 0..20 packed MSB-first in a u64.
-constexpr uint32_t FAST_MAX_DEPTH = 20;
+// Fast path: 3-bit sort digits for levels 0..10 packed MSB-first in bits
+// 63..31 of a u64; the low 31 bits carry the filter id, so one u64 per match
+// sorts by path code (== Erlang binary order of the filter).
+constexpr uint32_t FAST_MAX_DEPTH = 10;
+constexpr uint64_t KEY_MASK = 0xFFFFFFFF80000000ull;
 
-// Node summary flags (slot.flags / root.flags)
+// Node summary flags (RootRec.flags)
 constexpr uint32_t NF_PLUS = 1;     // node has a '+' child
 constexpr uint32_t NF_HASH = 2;     // node has a '#' child
 
+// Node ids (== filter ids) are < 2^30 so that two flag bits ride in each id word.
+constexpr uint32_t ID_BITS = 30;
+constexpr uint32_t ID_MASK = (1u << ID_BITS) - 1;
+constexpr uint32_t MAX_NODES = ID_MASK;          // ids 0 .. 2^30-2; ID_MASK = "none"
+constexpr uint32_t B_TOPIC = 1u << 30;           // child word: child has topic (term = child)
+constexpr uint32_t B_PLUS = 1u << 31;            // child word: child has a '+' child
+constexpr uint32_t B_HTERM = 1u << 30;           // hash word: child/'#' has topic (hterm valid)
+constexpr uint32_t B_HASH = 1u << 31;            // hash word: child has a '#' child
+
 // One edge of the trie in the open-addressed hash, keyed (parent, word), and
-// carrying the CHILD's summary so that one 64-B bucket read per visited node
-// is all the walk needs.  32 B, two slots per 64-B bucket.
-struct alignas(32) Slot {
+// carrying the CHILD's summary, so one 64-B bucket read per visited node is all
+// the walk needs.  16 B; four slots per 64-B bucket.
+struct alignas(16) Slot {
     uint32_t parent;   // key hi; SLOT_EMPTY / SLOT_TOMB
     uint32_t word;     // key lo
-    uint32_t child;    // child node id (== its filter id when it has a topic)
-    uint32_t term;     // child's own filter id or NONE        (read(trie_node, Child))
-    uint32_t hterm;    // filter id of child/'#' or NONE        ('match_#'(Child))
-    uint32_t flags;    // NF_*
-    uint32_t bloom;    // 32-bit bloom of child's literal child words
-    uint32_t spare;
+    uint32_t child;    // child id | B_TOPIC | B_PLUS
+    uint32_t hash;     // id of child/'#' (or ID_MASK) | B_HTERM | B_HASH
 };
-static_assert(sizeof(Slot) == 32, "slot is 32 bytes");
+static_assert(sizeof(Slot) == 16, "slot is 16 bytes");
+constexpr uint32_t BUCKET = 4;   // slots per 64-B bucket
 
 struct RootRec {
-    uint32_t hterm;
-    uint32_t flags;
-    uint32_t bloom;
+    uint32_t hterm;    // filter id of root/'#' or NONE
+    uint32_t flags;    // NF_*
     uint32_t live;
+    uint32_t pad;
 };
 
 __host__ __device__ inline uint32_t edge_hash(uint32_t parent, uint32_t word) {
@@ -69,8 +78,9 @@ __host__ __device__ inline uint32_t edge_hash(uint32_t parent, uint32_t word) {
     return (uint32_t)k;
 }
 
-__host__ __device__ inline uint32_t bloom_bit(uint32_t word) {
-    return 1u << ((word * 0x9E3779B1u) >> 27);
+// home bucket for any bucket count (multiply-shift, no power-of-two rounding)
+__host__ __device__ inline uint32_t home_bucket(uint32_t parent, uint32_t word, uint32_t nbuckets) {
+    return (uint32_t)(((uint64_t)edge_hash(parent, word) * nbuckets) >> 32);
 }
 
 // Control words of one batch launch (device memory, zeroed per launch).
@@ -90,7 +100,7 @@ enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES =
 struct MatchArgs {
     // trie replica
     const Slot* slots;
-    uint32_t bucket_mask;     // nbuckets - 1 (bucket = 2 slots)
+    uint32_t nbuckets;        // buckets of BUCKET slots
     uint32_t max_probe;       // max bucket displacement of any live key
     RootRec root;
     const uint64_t* foff;     // filter bytes offset per node id (slow-path byte sort)
@@ -105,12 +115,11 @@ struct MatchArgs {
     uint32_t n_slow;
     // outputs
     uint32_t* count;          // per topic |M(t)|
-    unsigned long long* src;  // per topic offset of its sorted row in fids[]
-    uint32_t* fids;           // [n * row_cap] fast rows, then the slow-path region
-    unsigned long long* rkeys;// [n * row_cap] path-code sort keys of the fast rows
+    unsigned long long* src;  // per topic: ~0 = fast row, else offset of its sorted row in sfids[]
+    unsigned long long* rows; // [n * row_cap] fast rows: (path code | filter id), unsorted
     uint32_t row_cap;         // K: per-topic row slots on the fast path
-    uint64_t slow_base;       // = n * row_cap
-    uint64_t fids_cap;
+    uint32_t* sfids;          // slow-path region: sorted filter ids
+    uint64_t sfids_cap;
     uint32_t* ctrl;
     uint32_t* ovf_list;       // topics redone by the slow path (row > K or stack overflow)
     uint32_t ovf_cap;
@@ -136,8 +145,10 @@ struct MatchArgs {
 struct ScanArgs {
     const uint32_t* count;
     const unsigned long long* src;
-    const uint32_t* fids;
-    uint64_t fids_cap;
+    const unsigned long long* rows;
+    uint32_t row_cap;
+    const uint32_t* sfids;
+    uint64_t sfids_cap;
     uint32_t* row_off;        // n + 1
     uint32_t* ids;
     uint32_t* block_sums;     // scratch
@@ -150,7 +161,7 @@ struct ScanArgs {
 // kernel launchers (tm_kernels.hip)
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
-hipError_t launch_copy(const ScanArgs& a, hipStream_t s, bool checked);
+hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked);
 hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n,
                                 hipStream_t s);
 hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx,

@@ -8,18 +8,20 @@
 //   tm_match_tiles  one 64-lane wavefront owns a TILE of 64 topics.  Pending
 //                   edge probes of all 64 topics live in an LDS stack; every
 //                   iteration pops up to 64 of them (one per lane), each lane
-//                   reads ONE 64-B hash bucket that holds the child's whole
-//                   summary, and the lanes push their children / emit their
-//                   matches through ballot + mbcnt prefix sums.  Matches carry a
-//                   3-bit-per-level path code whose order equals Erlang binary
-//                   order of the filters (DESIGN.md "Sort order"), so rows are
-//                   sorted in LDS with no byte compares, then written to staging.
+//                   reads ONE 64-B hash bucket whose matching 16-B slot holds the
+//                   child's whole summary, and the lanes push their children
+//                   through ballot + mbcnt prefix sums.  Each match is one u64
+//                   (3-bit-per-level path code | filter id) stored into the
+//                   topic's HBM row; path-code order == Erlang binary order of
+//                   the filters (DESIGN.md "Sort order").
 //   tm_match_slow   one wavefront per topic, frontier in global scratch: deep
-//                   (>20 levels) or irregular topics (sorted by filter bytes) and
-//                   topics of tiles whose LDS frontier overflowed.
-//   scan / copy     exclusive scan of the per-topic counts -> CSR rows.
+//                   (> 10 levels) or irregular topics (sorted by filter bytes),
+//                   rows longer than K and tiles whose LDS stack overflowed.
+//   scan            exclusive scan of the per-topic counts -> CSR offsets.
+//   tm_finalize     one workgroup per tile: rows staged in LDS, rank-sorted per
+//                   topic, filter ids written straight into the CSR.
 //
-// No MFMA: this is a dependent irregular gather, HBM/L2-latency bound.
+// No MFMA: this is a dependent irregular gather, bound by the memory system.
 #include "tm_internal.hpp"
 
 namespace etm {
@@ -28,8 +30,12 @@ constexpr int TILE = 64;
 constexpr int QCAP = 512;   // LDS probe stack entries per wave
 constexpr int WCAP = 512;   // LDS word cache per tile
 
-constexpr uint32_t M_SKIPE = 1u << 20;   // don't emit the child's own topic (literal '#' dup)
-constexpr uint32_t M_DSTART = 1u << 21;  // $-rooted start probe: the node was already counted
+// queue/meta encoding (fast path): tl (6 bits) | lc << 6 (8 bits) | flags
+constexpr uint32_t M_LVL_SHIFT = 6;
+constexpr uint32_t M_LVL_MASK = 0xFF;
+constexpr uint32_t M_PLUS = 1u << 20;    // probe the '+' edge (else the literal word w[lc-1])
+constexpr uint32_t M_SKIPE = 1u << 21;   // don't emit the child's own topic (literal '#' dup)
+constexpr uint32_t M_DSTART = 1u << 22;  // $-rooted start probe: the node was already counted
 
 // digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
 //   L = literal branch, H = '#' terminal, P = '+' branch; E = 0, L_lo = 1.
@@ -47,8 +53,6 @@ __device__ __forceinline__ uint32_t prefix_count(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
 // Bounds-checked debug variant: an out-of-range index is recorded (first
 // failing check id, index, bound) and clamped to 0 instead of faulting.
 template <bool CK>
@@ -64,28 +68,37 @@ __device__ __forceinline__ uint64_t ck(uint64_t i, uint64_t bound, uint32_t* dbg
 }
 #define CK_(i, bound, id) ck<CK>((i), (bound), a.dbg, (id))
 
-// One 64-B bucket read: both slots, key compare.  Returns true with the child
-// summary in s when (parent, word) is present.  max_probe bounds the scan.
+// Child summary decoded from one slot.
+struct Node {
+    uint32_t child;   // node id
+    uint32_t term;    // own filter id or NONE
+    uint32_t hterm;   // filter id of child/'#' or NONE
+    uint32_t flags;   // NF_*
+};
+
+// One 64-B bucket read (four 16-B slots, key compare).  max_probe bounds the scan.
 template <bool CK>
-__device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint32_t word, Slot& s) {
-    const Slot* __restrict__ slots = a.slots;
-    const uint32_t mask = a.bucket_mask, max_probe = a.max_probe;
-    uint32_t b = edge_hash(parent, word) & mask;
-    for (uint32_t p = 0; p <= max_probe; ++p) {
-        const uint4* q = reinterpret_cast<const uint4*>(slots + CK_(2 * (size_t)b + 1, a.nslots, 1) - 1);
-        uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-        if (a0.x == parent && a0.y == word) {
-            s.parent = a0.x; s.word = a0.y; s.child = a0.z; s.term = a0.w;
-            s.hterm = a1.x; s.flags = a1.y; s.bloom = a1.z; s.spare = a1.w;
+__device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint32_t word, Node& n) {
+    uint32_t b = home_bucket(parent, word, a.nbuckets);
+    for (uint32_t p = 0; p <= a.max_probe; ++p) {
+        const uint4* q = reinterpret_cast<const uint4*>(a.slots) + CK_((uint64_t)b * BUCKET, a.nslots, 1);
+        const uint4 s0 = q[0], s1 = q[1], s2 = q[2], s3 = q[3];
+        uint4 hit;
+        bool f = true;
+        if (s0.x == parent && s0.y == word) hit = s0;
+        else if (s1.x == parent && s1.y == word) hit = s1;
+        else if (s2.x == parent && s2.y == word) hit = s2;
+        else if (s3.x == parent && s3.y == word) hit = s3;
+        else f = false;
+        if (f) {
+            n.child = hit.z & ID_MASK;
+            n.term = (hit.z & B_TOPIC) ? n.child : NONE;
+            n.hterm = (hit.w & B_HTERM) ? (hit.w & ID_MASK) : NONE;
+            n.flags = ((hit.z & B_PLUS) ? NF_PLUS : 0u) | ((hit.w & B_HASH) ? NF_HASH : 0u);
             return true;
         }
-        if (a2.x == parent && a2.y == word) {
-            s.parent = a2.x; s.word = a2.y; s.child = a2.z; s.term = a2.w;
-            s.hterm = a3.x; s.flags = a3.y; s.bloom = a3.z; s.spare = a3.w;
-            return true;
-        }
-        if (a0.x == SLOT_EMPTY || a2.x == SLOT_EMPTY) return false;
-        b = (b + 1) & mask;
+        if (s3.x == SLOT_EMPTY) return false;   // slots fill in order: a free tail ends the run
+        b = (b + 1 == a.nbuckets) ? 0 : b + 1;
     }
     return false;
 }
@@ -98,22 +111,20 @@ struct Expand {
     uint32_t ne, np;
     uint32_t ef0, ef1;
     uint64_t ek0, ek1;
-    uint32_t pw0, pw1;
-    uint32_t pf0, pf1;
+    uint32_t pf0, pf1;     // M_PLUS / M_SKIPE / M_DSTART
     uint64_t pk0, pk1;
 };
 
-// register-only appends (no runtime-indexed arrays -> no scratch)
 __device__ __forceinline__ void add_e(Expand& x, uint32_t fid, uint64_t key) {
     if (x.ne == 0) { x.ef0 = fid; x.ek0 = key; } else { x.ef1 = fid; x.ek1 = key; }
     x.ne++;
 }
-__device__ __forceinline__ void add_p(Expand& x, uint32_t w, uint64_t key, uint32_t fl) {
-    if (x.np == 0) { x.pw0 = w; x.pk0 = key; x.pf0 = fl; } else { x.pw1 = w; x.pk1 = key; x.pf1 = fl; }
+__device__ __forceinline__ void add_p(Expand& x, uint64_t key, uint32_t fl) {
+    if (x.np == 0) { x.pk0 = key; x.pf0 = fl; } else { x.pk1 = key; x.pf1 = fl; }
     x.np++;
 }
 
-__device__ __forceinline__ void expand(const Slot& s, uint32_t lc, uint32_t d, uint32_t flags,
+__device__ __forceinline__ void expand(const Node& s, uint32_t lc, uint32_t d, uint32_t flags,
                                        uint64_t key, uint32_t w_here, uint32_t w_prev, Expand& x) {
     x.ne = 0; x.np = 0;
     if (lc == d) {
@@ -121,7 +132,7 @@ __device__ __forceinline__ void expand(const Slot& s, uint32_t lc, uint32_t d, u
             uint64_t k = key;
             // '' word at level lc-1 followed by the end: "P/" sorts before "P/#".
             if ((w_prev >> WID_BITS) == C_EMPTY && lc - 1 <= FAST_MAX_DEPTH) {
-                int sp = key_shift(lc - 1);
+                const int sp = key_shift(lc - 1);
                 if (((k >> sp) & 7) == 4) k = (k & ~(7ull << sp)) | (1ull << sp);
             }
             add_e(x, s.term, k);
@@ -129,35 +140,33 @@ __device__ __forceinline__ void expand(const Slot& s, uint32_t lc, uint32_t d, u
         if (s.hterm != NONE) add_e(x, s.hterm, put_digit(key, lc, 2));
         return;
     }
-    uint32_t cls = w_here >> WID_BITS, id = w_here & WID_MASK;
+    const uint32_t cls = w_here >> WID_BITS, id = w_here & WID_MASK;
     if (s.hterm != NONE) add_e(x, s.hterm, put_digit(key, lc, dig_H(cls)));
     if (id == W_HASH) {
-        if (s.flags & NF_HASH) add_p(x, W_HASH, put_digit(key, lc, dig_L(cls)), (lc + 1 == d) ? M_SKIPE : 0);
-    } else if (id != W_UNKNOWN && id != W_PLUS && (s.bloom & bloom_bit(id))) {
-        add_p(x, id, put_digit(key, lc, dig_L(cls)), 0);
+        if (s.flags & NF_HASH) add_p(x, put_digit(key, lc, dig_L(cls)), (lc + 1 == d) ? M_SKIPE : 0u);
+    } else if (id != W_UNKNOWN && id != W_PLUS) {
+        add_p(x, put_digit(key, lc, dig_L(cls)), 0u);
     }
-    if (s.flags & NF_PLUS) add_p(x, W_PLUS, put_digit(key, lc, dig_P(cls)), 0);
+    if (s.flags & NF_PLUS) add_p(x, put_digit(key, lc, dig_P(cls)), M_PLUS);
 }
 
 // Root expansion for a topic (match_node(root, Words), or the $ rule that
 // starts at node W and never tries root's '+'/'#', src/emqx_trie.erl:162-166).
-__device__ __forceinline__ void expand_root(const RootRec& r, bool dollar, uint32_t d, uint32_t w0,
-                                            Expand& x) {
+__device__ __forceinline__ void expand_root(const RootRec& r, bool dollar, uint32_t d, uint32_t w0, Expand& x) {
     x.ne = 0; x.np = 0;
-    uint32_t cls = w0 >> WID_BITS, id = w0 & WID_MASK;
+    const uint32_t cls = w0 >> WID_BITS, id = w0 & WID_MASK;
     if (!dollar && r.hterm != NONE) add_e(x, r.hterm, (uint64_t)dig_H(cls) << 61);
     if (id == W_HASH) {
-        if (!dollar && (r.flags & NF_HASH)) add_p(x, W_HASH, (uint64_t)dig_L(cls) << 61, (d == 1) ? M_SKIPE : 0);
-    } else if (id != W_UNKNOWN && id != W_PLUS && (r.bloom & bloom_bit(id))) {
-        add_p(x, id, (uint64_t)dig_L(cls) << 61, dollar ? M_DSTART : 0);
+        if (!dollar && (r.flags & NF_HASH)) add_p(x, (uint64_t)dig_L(cls) << 61, (d == 1) ? M_SKIPE : 0u);
+    } else if (id != W_UNKNOWN && id != W_PLUS) {
+        add_p(x, (uint64_t)dig_L(cls) << 61, dollar ? M_DSTART : 0u);
     }
-    if (!dollar && (r.flags & NF_PLUS)) add_p(x, W_PLUS, (uint64_t)dig_P(cls) << 61, 0);
+    if (!dollar && (r.flags & NF_PLUS)) add_p(x, (uint64_t)dig_P(cls) << 61, M_PLUS);
 }
 
 struct alignas(16) TileLds {
     unsigned long long q_key[QCAP];
     uint32_t q_parent[QCAP];
-    uint32_t q_pw[QCAP];
     uint32_t q_meta[QCAP];
     uint32_t words[WCAP];
     uint32_t toff[TILE];
@@ -165,14 +174,24 @@ struct alignas(16) TileLds {
     uint32_t cnt[TILE];
 };
 
-// Stores one match of tile-topic tl into its HBM row slot (row capacity K);
-// a row that outgrows K keeps counting and is redone by the slow path.
 template <bool CK>
 __device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t t, uint32_t slot, uint64_t key, uint32_t fid) {
     if (slot < a.row_cap) {
         const uint64_t i = (uint64_t)t * a.row_cap + slot;
-        a.rkeys[CK_(i, a.slow_base, 13)] = key;
-        a.fids[CK_(i, a.slow_base, 14)] = fid;
+        a.rows[CK_(i, (uint64_t)a.n * a.row_cap, 13)] = (key & KEY_MASK) | fid;
+    }
+}
+
+template <bool CK>
+__device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint32_t t) {
+    const uint64_t m = __ballot(mine);
+    uint32_t base = 0;
+    if (threadIdx.x == 0 && m) base = atomicAdd(&a.ctrl[CTRL_NOVF], (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (mine) {
+        const uint32_t slot = base + prefix_count(m);
+        if (slot < a.ovf_cap) a.ovf_list[CK_(slot, a.ovf_cap, 12)] = t;
+        else atomicOr(&a.ctrl[CTRL_ERR], ERR_OVF_LIST);
     }
 }
 
@@ -220,15 +239,9 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
             }
             const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
             const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            const uint32_t meta = lane | (1u << 6);
-            if (x.np >= 1) {
-                const uint32_t pos = qn + pre;
-                L.q_parent[pos] = ROOT; L.q_pw[pos] = x.pw0; L.q_meta[pos] = meta | x.pf0; L.q_key[pos] = x.pk0;
-            }
-            if (x.np >= 2) {
-                const uint32_t pos = qn + pre + 1;
-                L.q_parent[pos] = ROOT; L.q_pw[pos] = x.pw1; L.q_meta[pos] = meta | x.pf1; L.q_key[pos] = x.pk1;
-            }
+            const uint32_t meta = lane | (1u << M_LVL_SHIFT);
+            if (x.np >= 1) { const uint32_t p = qn + pre; L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf0; L.q_key[p] = x.pk0; }
+            if (x.np >= 2) { const uint32_t p = qn + pre + 1; L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf1; L.q_key[p] = x.pk1; }
             qn += __popcll(b0) + __popcll(b1);
             if (x.ne) {   // at most one emission at the root ('#')
                 L.cnt[lane] = 1;
@@ -241,37 +254,33 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
             const uint32_t k = min(qn, 64u);
             const bool has = lane < k;
             const uint32_t idx = qn - k + lane;
-            uint32_t parent = 0, pw = 0, meta = 0;
+            uint32_t parent = 0, meta = 0;
             uint64_t key = 0;
-            if (has) { parent = L.q_parent[idx]; pw = L.q_pw[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; }
+            if (has) { parent = L.q_parent[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; }
             qn -= k;
-            Slot s;
+            const uint32_t tl = meta & 63;
+            const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
+            const uint32_t base = L.toff[tl];
+            const uint32_t d = L.depth[tl];
+            uint32_t pw = W_PLUS;
+            if (has && !(meta & M_PLUS)) pw = wsrc[CK_(base + lc - 1, wlim, 10)] & WID_MASK;
+            Node s;
             const bool found = has && probe<CK>(a, parent, pw, s);
             Expand x; x.ne = 0; x.np = 0;
-            const uint32_t tl = meta & 63;
             if (found) {
-                const uint32_t lc = (meta >> 6) & 0xFFF;
-                const uint32_t d = L.depth[tl];
-                const uint32_t base = L.toff[tl];
                 if (!(meta & M_DSTART)) tV += 1;
                 if (s.flags & NF_HASH) tH += 1;
-                const uint32_t w_here = lc < d ? wsrc[CK_(base + lc, wlim, 10)] : 0u;
-                const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 11)];
+                const uint32_t w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
+                const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
                 expand(s, lc, d, meta, key, w_here, w_prev, x);
             }
             const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
             const uint32_t ptot = __popcll(b0) + __popcll(b1);
             if (qn + ptot > (uint32_t)QCAP) { ovf = true; break; }
             const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            const uint32_t nmeta = tl | ((((meta >> 6) & 0xFFF) + 1) << 6);
-            if (x.np >= 1) {
-                const uint32_t pos = qn + pre;
-                L.q_parent[pos] = s.child; L.q_pw[pos] = x.pw0; L.q_meta[pos] = nmeta | x.pf0; L.q_key[pos] = x.pk0;
-            }
-            if (x.np >= 2) {
-                const uint32_t pos = qn + pre + 1;
-                L.q_parent[pos] = s.child; L.q_pw[pos] = x.pw1; L.q_meta[pos] = nmeta | x.pf1; L.q_key[pos] = x.pk1;
-            }
+            const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
+            if (x.np >= 1) { const uint32_t p = qn + pre; L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf0; L.q_key[p] = x.pk0; }
+            if (x.np >= 2) { const uint32_t p = qn + pre + 1; L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf1; L.q_key[p] = x.pk1; }
             qn += ptot;
             if (x.ne) {
                 const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
@@ -283,69 +292,22 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
 
         if (ovf) {
             // probe stack overflow: every regular topic of the tile goes to the slow path
-            const uint64_t m = __ballot(valid && active);
-            uint32_t base = 0;
-            if (lane == 0 && m) base = atomicAdd(&a.ctrl[CTRL_NOVF], (uint32_t)__popcll(m));
-            base = __shfl(base, 0, 64);
-            if (valid && active) {
-                const uint32_t slot = base + prefix_count(m);
-                if (slot < a.ovf_cap) a.ovf_list[CK_(slot, a.ovf_cap, 12)] = t;
-            }
+            send_to_slow<CK>(a, valid && active, t);
             __syncthreads();
             continue;
         }
         sV += tV; sH += tH; sW += tW;
-
-        // ---- rows longer than K go to the slow path
         const uint32_t c_me = L.cnt[lane];
-        const bool row_ovf = valid && active && c_me > a.row_cap;
-        {
-            const uint64_t m = __ballot(row_ovf);
-            uint32_t base = 0;
-            if (lane == 0 && m) base = atomicAdd(&a.ctrl[CTRL_NOVF], (uint32_t)__popcll(m));
-            base = __shfl(base, 0, 64);
-            if (row_ovf) {
-                const uint32_t slot = base + prefix_count(m);
-                if (slot < a.ovf_cap) a.ovf_list[CK_(slot, a.ovf_cap, 15)] = t;
-            }
-        }
+        const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
+        send_to_slow<CK>(a, row_ovf, t);
         if (valid && active && !row_ovf) {
             a.count[CK_(t, a.n, 16)] = c_me;
-            a.src[CK_(t, a.n, 17)] = (unsigned long long)t * a.row_cap;
+            a.src[CK_(t, a.n, 17)] = ~0ull;
             sM += c_me;
-        }
-
-        // ---- sort each row in place by path code.  Lane i holds elements i and
-        //      i + 64 (row_cap <= ROWCAP_MAX = 128); rank = #{j : key_j < key_i}
-        //      via broadcast shuffles (keys are unique within a row).
-        for (uint32_t tt = 0; tt < tend - t0; ++tt) {
-            const uint32_t c = L.cnt[tt];
-            const uint32_t ftt = __shfl(fl, tt, 64);
-            if (c < 2 || c > a.row_cap || (ftt & TF_SLOW)) continue;
-            const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
-            uint64_t k0 = ~0ull, k1 = ~0ull;
-            uint32_t f0 = 0, f1 = 0;
-            if (lane < c) { k0 = a.rkeys[CK_(rb + lane, a.slow_base, 18)]; f0 = a.fids[CK_(rb + lane, a.slow_base, 19)]; }
-            if (lane + 64 < c) { k1 = a.rkeys[CK_(rb + lane + 64, a.slow_base, 18)]; f1 = a.fids[CK_(rb + lane + 64, a.slow_base, 19)]; }
-            uint32_t r0 = 0, r1 = 0;
-            const uint32_t c0 = min(c, 64u);
-            for (uint32_t j = 0; j < c0; ++j) {
-                const uint64_t kj = __shfl(k0, j, 64);
-                r0 += kj < k0 ? 1u : 0u;
-                r1 += kj < k1 ? 1u : 0u;
-            }
-            for (uint32_t j = 64; j < c; ++j) {
-                const uint64_t kj = __shfl(k1, j - 64, 64);
-                r0 += kj < k0 ? 1u : 0u;
-                r1 += kj < k1 ? 1u : 0u;
-            }
-            if (lane < c) a.fids[CK_(rb + r0, a.slow_base, 20)] = f0;
-            if (lane + 64 < c) a.fids[CK_(rb + r1, a.slow_base, 20)] = f1;
         }
         __syncthreads();
     }
 
-    // wave-reduce the stats, one atomic per wave
     for (int o = 32; o > 0; o >>= 1) {
         sV += __shfl_xor(sV, o, 64); sH += __shfl_xor(sH, o, 64);
         sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
@@ -368,9 +330,8 @@ __device__ __forceinline__ bool filter_less(const MatchArgs& a, uint32_t x, uint
     const uint8_t* py = a.fbytes + CK_(a.foff[y], a.nfbytes + 1, 23);
     const uint32_t lx = a.flen[x], ly = a.flen[y];
     const uint32_t m = min(lx, ly);
-    for (uint32_t i = 0; i < m; ++i) {
+    for (uint32_t i = 0; i < m; ++i)
         if (px[i] != py[i]) return px[i] < py[i];
-    }
     return lx < ly;
 }
 
@@ -384,12 +345,10 @@ __device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp
                 const uint32_t ixj = i ^ j;
                 if (ixj > i) {
                     const bool up = (i & k) == 0;
-                    bool gt;
-                    if (by_bytes) gt = filter_less<CK>(a, fp[ixj], fp[i]);
-                    else gt = kp[i] > kp[ixj];
+                    const bool gt = by_bytes ? filter_less<CK>(a, fp[ixj], fp[i]) : (kp[i] > kp[ixj]);
                     if (gt == up) {
-                        unsigned long long tk = kp[i]; kp[i] = kp[ixj]; kp[ixj] = tk;
-                        uint32_t tf = fp[i]; fp[i] = fp[ixj]; fp[ixj] = tf;
+                        const unsigned long long tk = kp[i]; kp[i] = kp[ixj]; kp[ixj] = tk;
+                        const uint32_t tf = fp[i]; fp[i] = fp[ixj]; fp[ixj] = tf;
                     }
                 }
             }
@@ -400,8 +359,14 @@ __device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp
 }
 
 constexpr uint32_t SORT_LDS = 2048;
+constexpr uint32_t SM_PLUS = 1u << 29;
 constexpr uint32_t SM_SKIPE = 1u << 30;
 constexpr uint32_t SM_DSTART = 1u << 31;
+constexpr uint32_t SM_LVL = (1u << 29) - 1;
+
+__device__ __forceinline__ uint32_t slow_flags(uint32_t pf) {
+    return ((pf & M_PLUS) ? SM_PLUS : 0u) | ((pf & M_SKIPE) ? SM_SKIPE : 0u) | ((pf & M_DSTART) ? SM_DSTART : 0u);
+}
 
 template <bool CK>
 __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
@@ -410,7 +375,6 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
     const uint32_t lane = threadIdx.x;
     const uint32_t wave = blockIdx.x;
     uint32_t* qpar = a.s_qparent + (size_t)wave * a.s_qcap;
-    uint32_t* qpw = a.s_qpw + (size_t)wave * a.s_qcap;
     uint32_t* qmeta = a.s_qmeta + (size_t)wave * a.s_qcap;
     unsigned long long* qkey = a.s_qkey + (size_t)wave * a.s_qcap;
     uint32_t* ofid = a.s_ofid + (size_t)wave * a.s_ocap;
@@ -420,13 +384,12 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sS = 0;
 
     for (uint32_t item = wave; item < total_items; item += gridDim.x) {
-        uint32_t t;
-        if (item < a.n_slow) t = a.slow_list[CK_(item, a.n_slow, 24)];
-        else t = a.ovf_list[CK_(item - a.n_slow, a.ovf_cap, 25)];
+        uint32_t t = (item < a.n_slow) ? a.slow_list[CK_(item, a.n_slow, 24)]
+                                       : a.ovf_list[CK_(item - a.n_slow, a.ovf_cap, 25)];
         t = CK_(t, a.n, 26);
         const uint8_t fl = a.tflags[t];
         const bool dollar = fl & TF_DOLLAR;
-        const bool by_bytes = fl & TF_SLOW;
+        const bool by_bytes = fl & TF_SLOW;   // deep or irregular: path code does not apply
         const uint32_t wb = a.toff[t];
         const uint32_t d = a.toff[t + 1] - wb;
         const uint32_t* w = a.words + wb;
@@ -439,16 +402,9 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
                 sV += 1; sW += d;
                 if (!dollar && (a.root.flags & NF_HASH)) sH += 1;
                 expand_root(a.root, dollar, d, w[0], x);
-                if (x.np >= 1) {
-                    qpar[0] = ROOT; qpw[0] = x.pw0; qkey[0] = x.pk0;
-                    qmeta[0] = 1u | (x.pf0 & M_SKIPE ? SM_SKIPE : 0) | (x.pf0 & M_DSTART ? SM_DSTART : 0);
-                }
-                if (x.np >= 2) {
-                    qpar[1] = ROOT; qpw[1] = x.pw1; qkey[1] = x.pk1;
-                    qmeta[1] = 1u | (x.pf1 & M_SKIPE ? SM_SKIPE : 0) | (x.pf1 & M_DSTART ? SM_DSTART : 0);
-                }
+                if (x.np >= 1) { qpar[0] = ROOT; qkey[0] = x.pk0; qmeta[0] = 1u | slow_flags(x.pf0); }
+                if (x.np >= 2) { qpar[1] = ROOT; qkey[1] = x.pk1; qmeta[1] = 1u | slow_flags(x.pf1); }
                 if (x.ne >= 1) { ofid[0] = x.ef0; okey[0] = x.ek0; }
-                if (x.ne >= 2) { ofid[1] = x.ef1; okey[1] = x.ek1; }
             }
             qn = __shfl(x.np, 0, 64);
             on = __shfl(x.ne, 0, 64);
@@ -459,24 +415,26 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             const uint32_t k = min(qn, 64u);
             const bool has = lane < k;
             const uint32_t idx = qn - k + lane;
-            uint32_t parent = 0, pw = 0, meta = 0;
+            uint32_t parent = 0, meta = 0;
             unsigned long long key = 0;
             if (has) {
                 const uint32_t ci = CK_(idx, a.s_qcap, 27);
-                parent = qpar[ci]; pw = qpw[ci]; meta = qmeta[ci]; key = qkey[ci];
+                parent = qpar[ci]; meta = qmeta[ci]; key = qkey[ci];
             }
             __threadfence_block();
             __syncthreads();
             qn -= k;
-            Slot s;
+            const uint32_t lc = meta & SM_LVL;
+            uint32_t pw = W_PLUS;
+            if (has && !(meta & SM_PLUS)) pw = w[CK_(lc - 1, d, 28)] & WID_MASK;
+            Node s;
             const bool found = has && probe<CK>(a, parent, pw, s);
             Expand x; x.ne = 0; x.np = 0;
-            const uint32_t lc = meta & 0x3FFFFFFFu;
             if (found) {
                 if (!(meta & SM_DSTART)) sV += 1;
                 if (s.flags & NF_HASH) sH += 1;
-                const uint32_t fl2 = (meta & SM_SKIPE) ? M_SKIPE : 0;
-                expand(s, lc, d, fl2, key, lc < d ? w[CK_(lc, d, 28)] : 0u, w[CK_(lc - 1, d, 29)], x);
+                const uint32_t fl2 = (meta & SM_SKIPE) ? M_SKIPE : 0u;
+                expand(s, lc, d, fl2, key, lc < d ? w[CK_(lc, d, 29)] : 0u, w[CK_(lc - 1, d, 28)], x);
             }
             const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
             const uint64_t e0 = __ballot(x.ne >= 1), e1 = __ballot(x.ne >= 2);
@@ -484,16 +442,8 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             const uint32_t etot = __popcll(e0) + __popcll(e1);
             if (qn + ptot > a.s_qcap || on + etot > a.s_ocap) { err = true; break; }
             const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            if (x.np >= 1) {
-                const uint32_t pos = qn + pre;
-                qpar[pos] = s.child; qpw[pos] = x.pw0; qkey[pos] = x.pk0;
-                qmeta[pos] = (lc + 1) | (x.pf0 & M_SKIPE ? SM_SKIPE : 0);
-            }
-            if (x.np >= 2) {
-                const uint32_t pos = qn + pre + 1;
-                qpar[pos] = s.child; qpw[pos] = x.pw1; qkey[pos] = x.pk1;
-                qmeta[pos] = (lc + 1) | (x.pf1 & M_SKIPE ? SM_SKIPE : 0);
-            }
+            if (x.np >= 1) { const uint32_t p = qn + pre; qpar[p] = s.child; qkey[p] = x.pk0; qmeta[p] = (lc + 1) | slow_flags(x.pf0); }
+            if (x.np >= 2) { const uint32_t p = qn + pre + 1; qpar[p] = s.child; qkey[p] = x.pk1; qmeta[p] = (lc + 1) | slow_flags(x.pf1); }
             qn += ptot;
             const uint32_t epre = prefix_count(e0) + prefix_count(e1);
             if (x.ne >= 1) { ofid[on + epre] = x.ef0; okey[on + epre] = x.ek0; }
@@ -534,13 +484,12 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
         uint32_t base = 0;
         if (lane == 0 && on) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], on);
         base = __shfl(base, 0, 64);
-        const uint64_t dst = a.slow_base + base;
-        if (dst + on <= a.fids_cap) {
-            for (uint32_t i = lane; i < on; i += 64) a.fids[CK_(dst + i, a.fids_cap, 30)] = ofid[i];
+        if ((uint64_t)base + on <= a.sfids_cap) {
+            for (uint32_t i = lane; i < on; i += 64) a.sfids[CK_(base + i, a.sfids_cap, 30)] = ofid[i];
         } else if (lane == 0) {
             atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);
         }
-        if (lane == 0) { a.count[t] = on; a.src[t] = dst; }
+        if (lane == 0) { a.count[t] = on; a.src[t] = base; }
         sM += (lane == 0) ? on : 0;
         __syncthreads();
     }
@@ -567,17 +516,17 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t incl = v;
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t u = __shfl_up(incl, o, 64);
+        const uint32_t u = __shfl_up(incl, o, 64);
         if (lane >= (uint32_t)o) incl += u;
     }
     if (lane == 63) sh[wid] = incl;
     __syncthreads();
     if (wid == 0) {
         const uint32_t nw = blockDim.x >> 6;
-        uint32_t s = lane < nw ? sh[lane] : 0;
+        const uint32_t s = lane < nw ? sh[lane] : 0;
         uint32_t si = s;
         for (int o = 1; o < 64; o <<= 1) {
-            uint32_t u = __shfl_up(si, o, 64);
+            const uint32_t u = __shfl_up(si, o, 64);
             if (lane >= (uint32_t)o) si += u;
         }
         if (lane < nw) sh[lane] = si - s;
@@ -629,20 +578,89 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t 
     }
 }
 
-// Pass 3: finish offsets, copy each row from staging into the CSR.
+// Pass 3: one 256-thread workgroup per tile of 64 topics.  The tile's fast rows
+// are staged in LDS, each element's rank inside its row is counted against the
+// other keys of that row, and the filter id is written straight to
+// ids[row_off[t] + rank].  Slow-path rows are already sorted: copied.
+constexpr uint32_t FIN_THREADS = 256;
+constexpr uint32_t FIN_LDS = 4096;   // staged elements per tile
+
 template <bool CK>
-__global__ __launch_bounds__(256) void tm_copy_rows(ScanArgs a) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    const uint32_t off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
-    a.row_off[t] = off;
-    const uint32_t c = a.count[t];
-    if ((uint64_t)off + c > a.ids_cap) return;   // staging overflow already flagged
-    const uint64_t s = a.src[t];
-    // a row whose slow-path output did not fit (ERR_STAGING, the host reruns
-    // the batch with a larger region) is skipped, never read out of range
-    if (s + c > a.fids_cap) return;
-    for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.fids[s + i];
+__global__ __launch_bounds__(FIN_THREADS) void tm_finalize(ScanArgs a) {
+    __shared__ unsigned long long sv[FIN_LDS];
+    __shared__ uint8_t srow[FIN_LDS];     // tile-local topic of the element
+    __shared__ uint32_t loff[TILE + 1];
+    __shared__ uint32_t roff[TILE];
+    __shared__ uint32_t cnt[TILE];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint32_t t0 = tile * TILE;
+        const uint32_t nt = min((uint32_t)TILE, a.n - t0);
+        if (tid < 64) {
+            const uint32_t t = t0 + tid;
+            uint32_t c = 0, off = 0;
+            bool f = false;
+            if (tid < nt) {
+                c = a.count[t];
+                const uint64_t s = a.src[t];
+                f = s == ~0ull;
+                off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
+                a.row_off[t] = off;      // finish the CSR offsets (scan pass 1 was block-local)
+                // slow rows: copy the already sorted ids
+                if (!f && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap)
+                    for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.sfids[s + i];
+            }
+            roff[tid] = off;
+            const uint32_t cf = f ? c : 0u;
+            uint32_t incl = cf;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, 64);
+                if (tid >= (uint32_t)o) incl += u;
+            }
+            loff[tid] = incl - cf;
+            cnt[tid] = cf;
+            if (tid == 63) loff[64] = incl;
+        }
+        __syncthreads();
+        const uint32_t total = loff[64];
+        if (total <= FIN_LDS) {
+            // stage the rows (one wave per topic row, coalesced)
+            for (uint32_t tt = tid >> 6; tt < nt; tt += FIN_THREADS / 64) {
+                const uint32_t c = cnt[tt];
+                const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
+                for (uint32_t i = tid & 63; i < c; i += 64) {
+                    const uint32_t e = loff[tt] + i;
+                    sv[e] = a.rows[rb + i];
+                    srow[e] = (uint8_t)tt;
+                }
+            }
+            __syncthreads();
+            for (uint32_t e = tid; e < total; e += FIN_THREADS) {
+                const unsigned long long v = sv[e];
+                const uint32_t tt = srow[e];
+                const uint32_t b = loff[tt], en = b + cnt[tt];
+                uint32_t r = 0;
+                for (uint32_t j = b; j < en; ++j) r += sv[j] < v ? 1u : 0u;
+                const uint32_t dst = roff[tt] + r;
+                if (dst < a.ids_cap) a.ids[dst] = (uint32_t)(v & ~KEY_MASK);
+            }
+        } else {
+            // rare: a tile with more than FIN_LDS matches -> keys straight from HBM
+            for (uint32_t tt = tid >> 6; tt < nt; tt += FIN_THREADS / 64) {
+                const uint32_t c = cnt[tt];
+                const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
+                for (uint32_t i = tid & 63; i < c; i += 64) {
+                    const unsigned long long v = a.rows[rb + i];
+                    uint32_t r = 0;
+                    for (uint32_t j = 0; j < c; ++j) r += a.rows[rb + j] < v ? 1u : 0u;
+                    const uint32_t dst = roff[tt] + r;
+                    if (dst < a.ids_cap) a.ids[dst] = (uint32_t)(v & ~KEY_MASK);
+                }
+            }
+        }
+        __syncthreads();
+    }
 }
 
 __global__ void tm_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n) {
@@ -679,9 +697,12 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total) {
     return hipGetLastError();
 }
 
-hipError_t launch_copy(const ScanArgs& a, hipStream_t s, bool checked) {
-    if (a.n && checked) hipLaunchKernelGGL(tm_copy_rows<true>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
-    else if (a.n) hipLaunchKernelGGL(tm_copy_rows<false>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    if (!ntiles) return hipGetLastError();
+    const uint32_t grid = min(ntiles, 256u * 8u);
+    if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(FIN_THREADS), 0, s, a);
+    else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(FIN_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

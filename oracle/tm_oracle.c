@@ -641,8 +641,15 @@ static void* job_run(void* arg) {
                 continue;
             }
         }
-        if (j->sorted && j->nout - start > 1)
+        if (j->sorted && j->nout - start > 1) {
             qsort_r(j->out + start, j->nout - start, sizeof(int64_t), cmp_idx_r, &sc);
+            /* the contract is the deduplicated set: the reference walk lists a
+             * filter twice only for topic names containing '+'/'#' words */
+            uint64_t w = start + 1;
+            for (uint64_t r = start + 1; r < j->nout; r++)
+                if (j->out[r] != j->out[w - 1]) j->out[w++] = j->out[r];
+            j->nout = w;
+        }
         j->counts[t] = (uint32_t)(j->nout - start);
         j->st.matches += j->nout - start;
     }

@@ -1,0 +1,41 @@
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(TESTS, "golden")
+for p in (ROOT, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def native_built():
+    """Build (or refresh) the in-tree native artefacts once per session."""
+    from emqx_amd import build as B
+    B.build_all()
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    yield
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def lb(s: str) -> bytes:
+    """fixture strings are latin-1 views of raw bytes"""
+    return s.encode("latin-1")
+
+
+@pytest.fixture
+def golden():
+    return load_golden

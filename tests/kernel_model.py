@@ -12,7 +12,7 @@ against the same oracle.
 from __future__ import annotations
 
 C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY = 0, 1, 2, 3
-FAST_MAX_DEPTH = 20
+FAST_MAX_DEPTH = 10
 DIG_L = {C_BELOW: 2, C_BETWEEN: 3, C_ABOVE: 4, C_EMPTY: 4}
 DIG_H = {C_BELOW: 3, C_BETWEEN: 2, C_ABOVE: 2, C_EMPTY: 2}
 DIG_P = {C_BELOW: 4, C_BETWEEN: 4, C_ABOVE: 3, C_EMPTY: 3}

@@ -1,0 +1,70 @@
+"""The device algorithm (tests/kernel_model.py restates tm_match_tiles) against the
+oracle: path-code order == Erlang binary order, $/'#'/'' rules, overflow.  CPU."""
+
+from dataclasses import replace
+
+import pytest
+from conftest import lb, load_golden
+from hypothesis import given, settings
+from hypothesis import strategies as st
+from kernel_model import Model
+
+from emqx_amd import gen
+from oracle import oracle as O
+
+
+@pytest.mark.parametrize("fixture", ["synth_c1_small.json", "synth_c2_small.json", "synth_adversarial.json"])
+def test_model_on_golden(fixture):
+    g = load_golden(fixture)
+    F = [lb(f) for f in g["filters"]]
+    T = [lb(t) for t in g["topics"]]
+    rows, slow = Model(F).match(T)
+    for i, t in enumerate(T):
+        if rows[i] is None:        # deep / irregular topic: slow path (byte sort), not modelled
+            continue
+        assert rows[i] == [F[j] for j in g["expected"][i]], t
+
+
+def test_model_on_c2_sample():
+    p = replace(gen.C2, n_filters=20000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 4, 1500).tolist()
+    rows, _ = Model(F).match(T)
+    tr = O.Trie()
+    for f in F:
+        tr.insert(f)
+    for t, r in zip(T, rows):
+        if r is not None:
+            assert r == sorted(set(tr.match(t))), t
+
+
+word = st.sampled_from([b"a", b"b", b"", b"!", b"%", b"$", b"~", b"#", b"+", b"#q", b"aa", b"\xc3\xa9"])
+filt = st.lists(word, min_size=1, max_size=6).map(lambda ws: b"/".join(ws))
+tword = st.sampled_from([b"a", b"b", b"", b"!", b"%", b"$", b"~", b"#q", b"aa", b"\xc3\xa9", b"zz"])
+topic = st.lists(tword, min_size=1, max_size=7).map(lambda ws: b"/".join(ws))
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(filt, min_size=1, max_size=40, unique=True), st.lists(topic, min_size=1, max_size=20))
+def test_model_property_sorted_equals_brute_force(filters, topics):
+    rows, _ = Model(filters).match(topics)
+    for t, r in zip(topics, rows):
+        if r is not None:
+            assert r == O.brute(t, filters), (t, r)
+
+
+def test_model_overflow_tiles_still_exact():
+    # tiny LDS capacities force the overflow path on every tile
+    p = replace(gen.C1, n_filters=500)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 8, 200).tolist()
+    m = Model(F)
+    r, ovf = m.match_tile(T[:64], qcap=8)
+    assert ovf
+    rows, slow = m.match(T)
+    assert slow > 0
+    tr = O.Trie()
+    for f in F:
+        tr.insert(f)
+    for t, row in zip(T, rows):
+        assert row == sorted(set(tr.match(t)))
