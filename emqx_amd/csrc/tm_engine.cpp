@@ -308,6 +308,7 @@ struct tm_engine {
     uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
+    double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint32_t* d_dbg = nullptr;
     uint32_t* h_dbg = nullptr;
     size_t c_dbg = 0, ch_dbg = 0;
@@ -383,8 +384,8 @@ struct tm_engine {
     }
 
     uint32_t insert_edge(uint32_t p, uint32_t w, uint32_t c) {
-        if ((used_slots + 1) * 5 > slots.size() * 4 || max_disp > 16)
-            rehash(std::max<size_t>((size_t)((live_edges + 1) / 0.6), slots.size() * (max_disp > 16 ? 2 : 1)));
+        if ((used_slots + 1) * 4 > slots.size() * 3 || max_disp > 48)
+            rehash(std::max<size_t>((size_t)((live_edges + 1) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
         uint32_t disp;
         bool was_empty;
         uint32_t i = place_slot(slots, p, w, disp, was_empty);
@@ -600,6 +601,11 @@ struct tm_engine {
         if (device < 0) return TM_ENODEV;
         int rc = ensure_delta_idle();
         if (rc) return rc;
+        // after a bulk build or heavy churn, re-pack the replica to load ~0.55 so
+        // the walk's working set stays small (it is a full upload anyway)
+        if (live_edges > 65536 && (slots.size() > (size_t)(live_edges / target_load) * 2 ||
+                                   slots.size() * target_load * 1.5 < live_edges))
+            rehash((size_t)(live_edges / target_load));
         // edge hash
         if (d_nslots != slots.size()) {
             dev_free(d_slots);
@@ -956,6 +962,7 @@ struct tm_engine {
         const char* ck = getenv("TM_CHECKED");
         checked = ck && ck[0] == '1';
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
+        if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         // root node id 0 (absent until the first add_path, like the reference)
         n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);

@@ -63,7 +63,7 @@ class Model:
         h = self.edges.get((n, b"#"))
         return self.topic.get(h) if h is not None else None
 
-    def match_tile(self, topics, qcap=320, ocap=320):
+    def match_tile(self, topics, qcap=512, ocap=1 << 30):
         """Returns (rows, overflow).  rows[i] = filters sorted by path code."""
         put = lambda key, lvl, d: key | (d << (61 - 3 * lvl))  # noqa: E731
         stack, out, meta = [], [], []
@@ -127,7 +127,9 @@ class Model:
             rows[ti].append((key, f))
         return [[f for _, f in sorted(r, key=lambda x: x[0])] for r in rows], False
 
-    def match(self, topics, tile=64):
+    def match(self, topics, tile=64, qcap=512, row_cap=128):
+        """Device semantics: LDS stack of qcap probes per tile; rows longer than
+        row_cap (K) and overflowed tiles are redone by the slow path."""
         rows, slow = [None] * len(topics), 0
         for i in range(0, len(topics), tile):
             idx = [j for j in range(i, min(i + tile, len(topics)))
@@ -135,10 +137,12 @@ class Model:
                    and not any(word_class(w)[1] for w in topics[j].split(b"/"))]
             slow += min(tile, len(topics) - i) - len(idx)   # deep/irregular: byte-sorted slow path
             fast = [topics[j] for j in idx]
-            r, ovf = self.match_tile(fast)
+            r, ovf = self.match_tile(fast, qcap=qcap)
             if ovf:
                 r, _ = self.match_tile(fast, qcap=1 << 30, ocap=1 << 30)
                 slow += len(fast)
+            else:
+                slow += sum(1 for row in r if len(row) > row_cap)
             for j, row in zip(idx, r):
                 rows[j] = row
         return rows, slow

@@ -113,7 +113,8 @@ def test_kat_emqx_topic_mirror():
     kat = load_golden("kat_topic.json")
     for name, flt, exp in kat["match"]:
         assert T.match(name.encode(), flt.encode()) is exp, (name, flt)
-        assert T.match(T.words(name.encode()), T.words(flt.encode())) is exp, (name, flt)
+        if not name.startswith("$"):   # the $ rule applies to binaries only (src/emqx_topic.erl:68-71)
+            assert T.match(T.words(name.encode()), T.words(flt.encode())) is exp, (name, flt)
     for t, exp in kat["wildcard"]:
         assert T.wildcard(t.encode()) is exp
     for t, ws in kat["words"]:
@@ -150,7 +151,7 @@ def test_kat_validate():
                 T.validate((kind, t))
             assert ei.value.reason == exp, (kind, topic)
     with pytest.raises(T.TopicError) as ei:
-        T.validate((b"name", b"\xff/x")) if False else T.validate(("name", b"a/\xff"))
+        T.validate(("name", b"a/\xff"))
     assert ei.value.reason == "function_clause"   # <<C/utf8, ...>> does not match
 
 
@@ -178,4 +179,4 @@ def test_predicate_matches_oracle_randomized():
 def test_c_struct_sizes_stable():
     assert C.sizeof(N.Config) == 16
     assert C.sizeof(N.TrieNode) == 12
-    assert C.sizeof(N.Result) == 24
+    assert C.sizeof(N.Result) == 32       # u32 + pad + u64 + 2 pointers

@@ -1,0 +1,290 @@
+"""Parity of the HIP path (through the C ABI) with the oracle -- needs an MI355X.
+
+Bit-exact per-topic sorted, deduplicated match sets on: the reference's KATs,
+the committed golden vectors, seeded C1/C2 workloads, deep/irregular/adversarial
+topics, the forced slow path, churn with delta uploads, and size-independent
+properties of a full 10M-publish C2 batch."""
+
+import os
+import random
+from dataclasses import replace
+
+import numpy as np
+import pytest
+from conftest import lb, load_golden
+
+from emqx_amd import emqx_router as R
+from emqx_amd import emqx_trie as TR
+from emqx_amd import gen
+from emqx_amd.emqx_batch import PublishBatcher
+from emqx_amd.engine import Engine
+from oracle import oracle as O
+from oracle import pyoracle as P
+
+pytestmark = pytest.mark.gpu
+
+
+def rows_of(offs, ids):
+    return [ids[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+
+
+def oracle_rows(filters, topics, nthreads=8):
+    """Oracle restatement: per-topic lists of filter bytes, sorted, dedup'd."""
+    orc = P.Oracle()
+    for f in filters:
+        orc.register(f)
+        orc.insert(f)
+    buf, offs = P.pack(topics)
+    counts, idx, st = orc.match_batch(buf, offs, nthreads=nthreads)
+    cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    orc.close()
+    return [[filters[int(j)] for j in idx[cut[i]:cut[i + 1]]] for i in range(len(topics))], st
+
+
+def engine_rows(eng, topics):
+    offs, ids = eng.match_batch(topics)
+    cache = {}
+
+    def fb(i):
+        i = int(i)
+        if i not in cache:
+            cache[i] = eng.filter_bytes(i)
+        return cache[i]
+    return [[fb(i) for i in r] for r in rows_of(offs, ids)]
+
+
+def assert_same(topics, got, exp):
+    bad = [i for i in range(len(topics)) if got[i] != exp[i]]
+    assert not bad, [(topics[i], got[i], exp[i]) for i in bad[:3]]
+
+
+def test_kat_trie_on_device():
+    kat = load_golden("kat_trie.json")
+    for case in kat["cases"]:
+        TR.clear_tables()
+        for op, arg, *rest in case["ops"]:
+            if op == "insert":
+                TR.insert(arg.encode())
+            elif op == "delete":
+                TR.delete(arg.encode())
+            elif op == "empty":
+                assert TR.empty() is arg
+        for topic, exp in case.get("match", []):
+            assert TR.match(topic.encode()) == sorted(e.encode() for e in exp), case["name"]
+        for topic, n in case.get("match_len", []):
+            assert len(TR.match(topic.encode())) == n
+
+
+def test_kat_router_on_device():
+    kat = load_golden("kat_router.json")
+    for case in kat["cases"]:
+        R.clear_tables()
+        for t in case["add"]:
+            R.add_route(t.encode())
+        if "topics" in case:
+            assert sorted(R.topics()) == [t.encode() for t in case["topics"]]
+        if "match" in case:
+            topic, exp = case["match"]
+            assert sorted(r.topic for r in R.match_routes(topic.encode())) == [e.encode() for e in exp]
+            assert [sorted(r.topic for r in rr) for rr in R.match_routes_batch([topic.encode()])] == \
+                [[e.encode() for e in exp]]
+        if "has" in case:
+            assert R.has_routes(case["has"][0].encode()) is case["has"][1]
+        for t in case.get("delete", []):
+            R.delete_route(t.encode())
+        if "topics_after" in case:
+            assert R.topics() == []
+        if "match_after" in case:
+            assert R.match_routes(case["match_after"][0].encode()) == []
+
+
+@pytest.mark.parametrize("fixture", ["synth_c1_small.json", "synth_c2_small.json", "synth_adversarial.json"])
+def test_golden_vectors_on_device(fixture):
+    g = load_golden(fixture)
+    F = [lb(f) for f in g["filters"]]
+    T = [lb(t) for t in g["topics"]]
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    got = engine_rows(eng, T)
+    exp = [[F[j] for j in row] for row in g["expected"]]
+    assert_same(T, got, exp)
+
+
+def test_c1_full_parity_and_walk_counters():
+    F = gen.gen_filters(gen.C1).tolist()
+    Ts = gen.gen_topics(gen.C1, gen.Strings.from_list(F), 1001, gen.C1_TOPICS)
+    T = Ts.tolist()
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    exp, st = oracle_rows(F, T)
+    b = eng.prepare(Ts)
+    b.launch().wait()
+    offs, ids = b.result()
+    bst = b.stats()
+    cache = {}
+    got = [[cache.setdefault(int(i), eng.filter_bytes(int(i))) for i in r] for r in rows_of(offs, ids)]
+    assert_same(T, got, exp)
+    # V and H counted on the device equal the oracle walk's (layout-independent)
+    assert bst["visits"] == st["visits"] and bst["hash_hits"] == st["hash_hits"]
+    assert bst["words"] == st["words"] and bst["matches"] == st["matches"]
+    b.free()
+
+
+def test_c2_parity_sample():
+    F = gen.gen_filters(gen.C2).tolist()
+    T = gen.gen_topics(gen.C2, gen.Strings.from_list(F), 2002, 200_000).tolist()
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    exp, _ = oracle_rows(F, T, nthreads=16)
+    assert_same(T, engine_rows(eng, T), exp)
+
+
+def test_forced_slow_path_parity():
+    os.environ["TM_ROWCAP"] = "4"
+    try:
+        eng = Engine(device=0)
+    finally:
+        del os.environ["TM_ROWCAP"]
+    p = replace(gen.C1, n_filters=3000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 5, 20000).tolist()
+    for f in F:
+        eng.insert(f)
+    b = eng.prepare(T)
+    b.launch().wait()
+    assert b.stats()["slow_topics"] > 1000
+    b.free()
+    exp, _ = oracle_rows(F, T)
+    assert_same(T, engine_rows(eng, T), exp)
+
+
+def test_deep_irregular_and_edge_topics():
+    rng = random.Random(9)
+    W = [b"a", b"b", b"", b"!", b"%", b"$q", b"#x", b"~", b"\xc3\xa9"]
+    F = set()
+    for _ in range(3000):
+        d = rng.randint(1, 26)
+        ws = [rng.choice(W + [b"+"]) for _ in range(d)]
+        if rng.random() < 0.4:
+            ws[-1] = b"#"
+        F.add(b"/".join(ws))
+    F = sorted(F)
+    T = []
+    for _ in range(4000):
+        d = rng.randint(1, 30)
+        T.append(b"/".join(rng.choice(W + [b"+x", b"c"]) for _ in range(d)))
+    T += [b"", b"/", b"$", b"$q", b"a/" * 40 + b"a", b"+x/a", b"a/+x/#x"]
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    exp, _ = oracle_rows(F, T)
+    assert_same(T, engine_rows(eng, T), exp)
+
+
+def test_literal_wildcard_words_in_names_follow_the_trie():
+    # invalid publish names containing '+'/'#' words: the hot path is emqx_trie:match/1,
+    # whose set (deduplicated) the engine must reproduce
+    F = [b"#", b"+/#", b"a/#", b"a/+", b"a/#/b", b"a/#/#", b"+/+", b"a/+/#", b"#/#"]
+    T = [b"a/#", b"a/+", b"a/#/b", b"#", b"+", b"+/+", b"a/+/c", b"#/#"]
+    eng = Engine(device=0)
+    tr = O.Trie()
+    for f in F:
+        eng.insert(f)
+        tr.insert(f)
+    assert engine_rows(eng, T) == [sorted(set(tr.match(t))) for t in T]
+
+
+def test_empty_trie_empty_batch_and_readyourwrites():
+    eng = Engine(device=0)
+    offs, ids = eng.match_batch([b"a/b", b"c"])
+    assert list(offs) == [0, 0, 0] and len(ids) == 0
+    offs, ids = eng.match_batch([])
+    assert list(offs) == [0] and len(ids) == 0
+    eng.insert(b"a/+")
+    assert eng.match(b"a/b") == [b"a/+"]          # a match issued after insert sees it
+    eng.delete(b"a/+")
+    assert eng.match(b"a/b") == []
+    eng.insert(b"a/#")
+    assert eng.match(b"a") == [b"a/#"]
+
+
+def test_churn_with_delta_uploads():
+    rng = random.Random(4)
+    p = replace(gen.C2, n_filters=40_000)
+    F = gen.gen_filters(p).tolist()
+    live = set(F[:20_000])
+    eng = Engine(device=0)
+    tr = O.Trie()
+    for f in live:
+        eng.insert(f)
+        tr.insert(f)
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 77, 4000).tolist()
+    for rnd in range(6):
+        for _ in range(2000):             # interleaved subscribe / unsubscribe deltas
+            f = rng.choice(F)
+            if f in live and rng.random() < 0.5:
+                live.discard(f); eng.delete(f); tr.delete(f)
+            else:
+                live.add(f); eng.insert(f); tr.insert(f)
+        got = engine_rows(eng, T)
+        assert got == [sorted(set(tr.match(t))) for t in T], rnd
+    st = eng.stats()
+    assert st["uploads_delta"] >= 1 and st["delta_slots"] > 0
+
+
+def test_full_c2_batch_properties():
+    """10M publishes against 1M filters: CSR consistency, every row strictly
+    increasing in filter bytes, every listed filter matches its topic, and a
+    random sample of rows equals the oracle."""
+    F = gen.gen_filters(gen.C2)
+    Ts = gen.gen_topics(gen.C2, F, 3003, 10_000_000)
+    fl = F.tolist()
+    eng = Engine(device=0)
+    for f in fl:
+        eng.insert(f)
+    b = eng.prepare(Ts)
+    b.launch().wait()
+    offs, ids = b.result()
+    st = b.stats()
+    assert offs[0] == 0 and np.all(np.diff(offs.astype(np.int64)) >= 0)
+    assert int(offs[-1]) == len(ids) == st["matches"]
+    rng = np.random.default_rng(0)
+    sample = rng.choice(len(Ts), 3000, replace=False)
+    from emqx_amd import emqx_topic as T
+    cache = {}
+    got, topics = [], []
+    for i in sample:
+        t = Ts[int(i)]
+        row = [cache.setdefault(int(x), eng.filter_bytes(int(x))) for x in ids[offs[i]:offs[i + 1]]]
+        assert all(row[k] < row[k + 1] for k in range(len(row) - 1)), t
+        assert all(T.match(t, f) for f in row), t
+        got.append(row)
+        topics.append(t)
+    exp, _ = oracle_rows(fl, topics, nthreads=16)
+    assert_same(topics, got, exp)
+    b.free()
+
+
+def test_publish_batcher_emqx_batch_semantics():
+    p = replace(gen.C1, n_filters=2000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 3, 5000).tolist()
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    out = {}
+
+    def on_result(topics, offs, ids):
+        for i, t in enumerate(topics):
+            out.setdefault(t, [eng.filter_bytes(int(x)) for x in ids[offs[i]:offs[i + 1]]])
+
+    pb = PublishBatcher(eng, on_result, batch_size=999, linger_ms=5)
+    for t in T:
+        pb.publish(t)
+    pb.close()
+    exp, _ = oracle_rows(F, T)
+    for t, e in zip(T, exp):
+        assert out[t] == e

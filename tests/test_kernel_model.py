@@ -61,7 +61,7 @@ def test_model_overflow_tiles_still_exact():
     m = Model(F)
     r, ovf = m.match_tile(T[:64], qcap=8)
     assert ovf
-    rows, slow = m.match(T)
+    rows, slow = m.match(T, qcap=8, row_cap=4)
     assert slow > 0
     tr = O.Trie()
     for f in F:
