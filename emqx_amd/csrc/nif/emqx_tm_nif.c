@@ -1,0 +1,228 @@
+/*
+ * emqx_tm_nif.c -- erl_nif shim binding include/emqx_tm.h to the Erlang module
+ * `emqx_tm` (emqx_amd/erlang/emqx_tm.erl).  It is the reference-side binding of
+ * the C ABI: EMQ X's emqx_trie / emqx_router call these instead of walking the
+ * mnesia trie tables.
+ *
+ * Build (needs OTP headers, absent from this image):
+ *   gcc -O2 -fPIC -shared -I$(erl -noshell -eval 'io:format("~s",[code:root_dir()])' \
+ *       -s init stop)/usr/include -I../../../include emqx_tm_nif.c \
+ *       -L../.. -lemqx_tm -Wl,-rpath,'$ORIGIN' -o priv/emqx_tm_nif.so
+ *
+ * Scheduling: trie mutations and lookups are host-only and short, but they
+ * share the engine mutex with device batches, so every call that takes the
+ * engine runs on a dirty I/O scheduler.  The pairwise predicate is pure and
+ * runs on a normal scheduler.
+ *
+ * Errors: a non-binary topic raises badarg (the reference's function_clause
+ * class, src/emqx_trie.erl:82,97,108); engine errors return {error, Reason}.
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "emqx_tm.h"
+
+static ErlNifResourceType* ENGINE_RT;
+
+typedef struct {
+    tm_engine* e;
+} engine_res;
+
+static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_UNDEFINED, ATOM_ROOT,
+    ATOM_TRIE_NODE, ATOM_NODE_NOT_FOUND, ATOM_ENOMEM, ATOM_EIO, ATOM_EINVAL, ATOM_ENODEV,
+    ATOM_EOVERFLOW;
+
+static void engine_dtor(ErlNifEnv* env, void* obj) {
+    (void)env;
+    engine_res* r = (engine_res*)obj;
+    if (r->e) tm_destroy(r->e);
+    r->e = NULL;
+}
+
+static ERL_NIF_TERM err(ErlNifEnv* env, int rc) {
+    ERL_NIF_TERM why;
+    switch (rc) {
+        case TM_ENOMEM: why = ATOM_ENOMEM; break;
+        case TM_ENODEV: why = ATOM_ENODEV; break;
+        case TM_EINVAL: why = ATOM_EINVAL; break;
+        case TM_EOVERFLOW: why = ATOM_EOVERFLOW; break;
+        default: why = ATOM_EIO; break;
+    }
+    return enif_make_tuple2(env, ATOM_ERROR, why);
+}
+
+static int get_engine(ErlNifEnv* env, ERL_NIF_TERM t, engine_res** out) {
+    return enif_get_resource(env, t, ENGINE_RT, (void**)out) && (*out)->e;
+}
+
+static ERL_NIF_TERM make_bin(ErlNifEnv* env, const uint8_t* p, size_t n) {
+    ERL_NIF_TERM t;
+    unsigned char* d = enif_make_new_binary(env, n, &t);
+    if (n) memcpy(d, p, n);
+    return t;
+}
+
+/* new(Device) -> {ok, Engine} | {error, Reason} */
+static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    int dev;
+    (void)argc;
+    if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+    tm_config cfg = {dev, 0, 0, 0};
+    tm_engine* e = NULL;
+    int rc = tm_create(&cfg, &e);
+    if (rc) return err(env, rc);
+    engine_res* r = enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
+    r->e = e;
+    ERL_NIF_TERM t = enif_make_resource(env, r);
+    enif_release_resource(r);
+    return enif_make_tuple2(env, ATOM_OK, t);
+}
+
+/* insert(Engine, Topic) -> ok  (emqx_trie:insert/1, src/emqx_trie.erl:81-93) */
+static ERL_NIF_TERM nif_insert(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+    int rc = tm_trie_insert(r->e, b.data, b.size);
+    return rc ? err(env, rc) : ATOM_OK;
+}
+
+/* delete(Engine, Topic) -> ok | {error, {node_not_found, Topic}}  (:107-116, :203) */
+static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+    int rc = tm_trie_delete(r->e, b.data, b.size);
+    if (rc == TM_EABORT)
+        return enif_make_tuple2(env, ATOM_ERROR, enif_make_tuple2(env, ATOM_NODE_NOT_FOUND, argv[1]));
+    return rc ? err(env, rc) : ATOM_OK;
+}
+
+/* lookup(Engine, NodeId | root) -> [] | [{trie_node, NodeId, EdgeCount, Topic | undefined, undefined}] */
+static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    tm_trie_node n;
+    int is_root = 0, rc;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r)) return enif_make_badarg(env);
+    if (enif_is_identical(argv[1], ATOM_ROOT)) { is_root = 1; b.data = NULL; b.size = 0; }
+    else if (!enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+    rc = tm_trie_lookup(r->e, b.data, b.size, is_root, &n);
+    if (rc < 0) return err(env, rc);
+    if (rc == 0) return enif_make_list(env, 0);
+    ERL_NIF_TERM topic = ATOM_UNDEFINED;
+    if (n.has_topic) {
+        size_t len = 0;
+        const uint8_t* p = tm_filter_bytes(r->e, n.filter_id, &len);
+        if (p) topic = make_bin(env, p, len);
+    }
+    ERL_NIF_TERM rec = enif_make_tuple5(env, ATOM_TRIE_NODE, argv[1], enif_make_uint(env, n.edge_count), topic,
+                                        ATOM_UNDEFINED);
+    return enif_make_list1(env, rec);
+}
+
+/* empty(Engine) -> boolean()  (:119-121) */
+static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r)) return enif_make_badarg(env);
+    return tm_trie_empty(r->e) ? ATOM_TRUE : ATOM_FALSE;
+}
+
+static ERL_NIF_TERM rows_to_terms(ErlNifEnv* env, tm_engine* e, const tm_result* res, uint32_t row) {
+    const uint32_t b = res->row_offsets[row], n = res->row_offsets[row + 1] - b;
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (uint32_t i = n; i-- > 0;) {       /* build back to front: list in sorted order */
+        size_t len = 0;
+        const uint8_t* p = tm_filter_bytes(e, res->filter_ids[b + i], &len);
+        list = enif_make_list_cell(env, make_bin(env, p, len), list);
+    }
+    return list;
+}
+
+/* match(Engine, Topic) -> [Filter]  (emqx_trie:match/1, :96-99; sorted set) */
+static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+    const uint64_t offs[2] = {0, b.size};
+    tm_result res;
+    int rc = tm_match_batch(r->e, b.size ? b.data : (const uint8_t*)"", offs, 1, &res);
+    if (rc) return err(env, rc);
+    return rows_to_terms(env, r->e, &res, 0);
+}
+
+/* match_batch(Engine, [Topic]) -> [[Filter]]  (one device pipeline per call) */
+static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_get_list_length(env, argv[1], &n)) return enif_make_badarg(env);
+    uint64_t* offs = enif_alloc(sizeof(uint64_t) * (n + 1));
+    ErlNifBinary* bins = enif_alloc(sizeof(ErlNifBinary) * (n ? n : 1));
+    ERL_NIF_TERM head, tail = argv[1];
+    uint64_t total = 0;
+    offs[0] = 0;
+    for (unsigned i = 0; i < n; i++) {
+        if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_inspect_binary(env, head, &bins[i])) {
+            enif_free(offs); enif_free(bins);
+            return enif_make_badarg(env);
+        }
+        total += bins[i].size;
+        offs[i + 1] = total;
+    }
+    uint8_t* buf = enif_alloc(total ? total : 1);
+    for (unsigned i = 0; i < n; i++) memcpy(buf + offs[i], bins[i].data, bins[i].size);
+    tm_result res;
+    int rc = tm_match_batch(r->e, buf, offs, n, &res);
+    enif_free(buf); enif_free(bins); enif_free(offs);
+    if (rc) return err(env, rc);
+    ERL_NIF_TERM out = enif_make_list(env, 0);
+    for (unsigned i = n; i-- > 0;) out = enif_make_list_cell(env, rows_to_terms(env, r->e, &res, i), out);
+    return out;
+}
+
+/* topic_match(Name, Filter) -> boolean()  (emqx_topic:match/2, src/emqx_topic.erl:65-87) */
+static ERL_NIF_TERM nif_topic_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    ErlNifBinary a, f;
+    (void)argc;
+    if (!enif_inspect_binary(env, argv[0], &a) || !enif_inspect_binary(env, argv[1], &f)) return enif_make_badarg(env);
+    return tm_topic_match(a.data, a.size, f.data, f.size) ? ATOM_TRUE : ATOM_FALSE;
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+    (void)priv; (void)info;
+    ENGINE_RT = enif_open_resource_type(env, NULL, "tm_engine", engine_dtor, ERL_NIF_RT_CREATE, NULL);
+    if (!ENGINE_RT) return -1;
+    ATOM_OK = enif_make_atom(env, "ok");
+    ATOM_ERROR = enif_make_atom(env, "error");
+    ATOM_TRUE = enif_make_atom(env, "true");
+    ATOM_FALSE = enif_make_atom(env, "false");
+    ATOM_UNDEFINED = enif_make_atom(env, "undefined");
+    ATOM_ROOT = enif_make_atom(env, "root");
+    ATOM_TRIE_NODE = enif_make_atom(env, "trie_node");
+    ATOM_NODE_NOT_FOUND = enif_make_atom(env, "node_not_found");
+    ATOM_ENOMEM = enif_make_atom(env, "enomem");
+    ATOM_EIO = enif_make_atom(env, "eio");
+    ATOM_EINVAL = enif_make_atom(env, "einval");
+    ATOM_ENODEV = enif_make_atom(env, "enodev");
+    ATOM_EOVERFLOW = enif_make_atom(env, "eoverflow");
+    return 0;
+}
+
+static ErlNifFunc funcs[] = {
+    {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"insert", 2, nif_insert, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"delete", 2, nif_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"lookup", 2, nif_lookup, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"empty", 1, nif_empty, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_batch", 2, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"topic_match", 2, nif_topic_match, 0},
+};
+
+ERL_NIF_INIT(emqx_tm, funcs, load, NULL, NULL, NULL)

@@ -578,85 +578,92 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t 
     }
 }
 
-// Pass 3: one 256-thread workgroup per tile of 64 topics.  The tile's fast rows
-// are staged in LDS, each element's rank inside its row is counted against the
-// other keys of that row, and the filter id is written straight to
-// ids[row_off[t] + rank].  Slow-path rows are already sorted: copied.
-constexpr uint32_t FIN_THREADS = 256;
-constexpr uint32_t FIN_LDS = 4096;   // staged elements per tile
-
+// Pass 3: one wavefront per tile of 64 topics (lane = topic).  Fast rows are
+// sorted in registers: rows of size class W (W/2 < c <= W, W = 2..64) are
+// packed 64/W per wave-instruction, one element per lane, and put through a
+// W-wide bitonic network of __shfl_xor exchanges; filter ids go straight to
+// ids[row_off[t] + e].  Rows of 65..128 elements (rare) use a rank count with
+// two elements per lane.  Slow-path rows are already sorted: copied.
 template <bool CK>
-__global__ __launch_bounds__(FIN_THREADS) void tm_finalize(ScanArgs a) {
-    __shared__ unsigned long long sv[FIN_LDS];
-    __shared__ uint8_t srow[FIN_LDS];     // tile-local topic of the element
-    __shared__ uint32_t loff[TILE + 1];
-    __shared__ uint32_t roff[TILE];
-    __shared__ uint32_t cnt[TILE];
-    const uint32_t tid = threadIdx.x;
+__global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
+    __shared__ uint32_t list[TILE];
+    const uint32_t lane = threadIdx.x;
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint32_t t0 = tile * TILE;
-        const uint32_t nt = min((uint32_t)TILE, a.n - t0);
-        if (tid < 64) {
-            const uint32_t t = t0 + tid;
-            uint32_t c = 0, off = 0;
-            bool f = false;
-            if (tid < nt) {
-                c = a.count[t];
-                const uint64_t s = a.src[t];
-                f = s == ~0ull;
-                off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
-                a.row_off[t] = off;      // finish the CSR offsets (scan pass 1 was block-local)
-                // slow rows: copy the already sorted ids
-                if (!f && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap)
-                    for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.sfids[s + i];
-            }
-            roff[tid] = off;
-            const uint32_t cf = f ? c : 0u;
-            uint32_t incl = cf;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o, 64);
-                if (tid >= (uint32_t)o) incl += u;
-            }
-            loff[tid] = incl - cf;
-            cnt[tid] = cf;
-            if (tid == 63) loff[64] = incl;
+        const uint32_t t = t0 + lane;
+        const bool valid = t < a.n;
+        uint32_t c = 0, off = 0;
+        bool fast = false;
+        if (valid) {
+            c = a.count[t];
+            const uint64_t s = a.src[t];
+            fast = s == ~0ull;
+            off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
+            a.row_off[t] = off;      // finish the CSR offsets (scan pass 1 was block-local)
+            if (!fast && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap)
+                for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.sfids[s + i];
+            if (fast && c == 1 && off < a.ids_cap)
+                a.ids[off] = (uint32_t)(a.rows[(uint64_t)t * a.row_cap] & ~KEY_MASK);
         }
-        __syncthreads();
-        const uint32_t total = loff[64];
-        if (total <= FIN_LDS) {
-            // stage the rows (one wave per topic row, coalesced)
-            for (uint32_t tt = tid >> 6; tt < nt; tt += FIN_THREADS / 64) {
-                const uint32_t c = cnt[tt];
-                const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
-                for (uint32_t i = tid & 63; i < c; i += 64) {
-                    const uint32_t e = loff[tt] + i;
-                    sv[e] = a.rows[rb + i];
-                    srow[e] = (uint8_t)tt;
+        // size classes W = 2, 4, ..., 64
+#pragma unroll
+        for (uint32_t W = 2; W <= 64; W <<= 1) {
+            const bool mine = fast && c > W / 2 && c <= W;
+            const uint64_t m = __ballot(mine);
+            if (!m) continue;
+            const uint32_t nrows = __popcll(m);
+            if (mine) list[prefix_count(m)] = lane;
+            __syncthreads();
+            const uint32_t e = lane & (W - 1);
+            for (uint32_t g = 0; g < nrows; g += 64 / W) {
+                const uint32_t r = g + lane / W;
+                const bool rv = r < nrows;
+                const uint32_t owner = rv ? list[r] : 0u;
+                const uint32_t cr = __shfl(c, owner, 64);
+                const uint32_t offr = __shfl(off, owner, 64);
+                unsigned long long key = ~0ull;
+                if (rv && e < cr) key = a.rows[(uint64_t)(t0 + owner) * a.row_cap + e];
+                for (uint32_t kk = 2; kk <= W; kk <<= 1) {
+                    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                        const unsigned long long other = __shfl_xor(key, j, 64);
+                        const bool up = (e & kk) == 0;
+                        const bool lower = (e & j) == 0;
+                        const unsigned long long lo = key < other ? key : other;
+                        const unsigned long long hi = key < other ? other : key;
+                        key = (lower == up) ? lo : hi;
+                    }
                 }
+                if (rv && e < cr && (uint64_t)offr + e < a.ids_cap) a.ids[offr + e] = (uint32_t)(key & ~KEY_MASK);
             }
             __syncthreads();
-            for (uint32_t e = tid; e < total; e += FIN_THREADS) {
-                const unsigned long long v = sv[e];
-                const uint32_t tt = srow[e];
-                const uint32_t b = loff[tt], en = b + cnt[tt];
-                uint32_t r = 0;
-                for (uint32_t j = b; j < en; ++j) r += sv[j] < v ? 1u : 0u;
-                const uint32_t dst = roff[tt] + r;
-                if (dst < a.ids_cap) a.ids[dst] = (uint32_t)(v & ~KEY_MASK);
-            }
-        } else {
-            // rare: a tile with more than FIN_LDS matches -> keys straight from HBM
-            for (uint32_t tt = tid >> 6; tt < nt; tt += FIN_THREADS / 64) {
-                const uint32_t c = cnt[tt];
-                const uint64_t rb = (uint64_t)(t0 + tt) * a.row_cap;
-                for (uint32_t i = tid & 63; i < c; i += 64) {
-                    const unsigned long long v = a.rows[rb + i];
-                    uint32_t r = 0;
-                    for (uint32_t j = 0; j < c; ++j) r += a.rows[rb + j] < v ? 1u : 0u;
-                    const uint32_t dst = roff[tt] + r;
-                    if (dst < a.ids_cap) a.ids[dst] = (uint32_t)(v & ~KEY_MASK);
+        }
+        // 64 < c <= 128: rank count, two elements per lane, one row at a time
+        {
+            const bool mine = fast && c > 64;
+            uint64_t m = __ballot(mine);
+            while (m) {
+                const uint32_t owner = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t cr = __shfl(c, owner, 64);
+                const uint32_t offr = __shfl(off, owner, 64);
+                const uint64_t rb = (uint64_t)(t0 + owner) * a.row_cap;
+                unsigned long long k0 = ~0ull, k1 = ~0ull;
+                if (lane < cr) k0 = a.rows[rb + lane];
+                if (lane + 64 < cr) k1 = a.rows[rb + lane + 64];
+                uint32_t r0 = 0, r1 = 0;
+                for (uint32_t j = 0; j < 64; ++j) {
+                    const unsigned long long kj = __shfl(k0, j, 64);
+                    r0 += kj < k0 ? 1u : 0u;
+                    r1 += kj < k1 ? 1u : 0u;
                 }
+                for (uint32_t j = 64; j < cr; ++j) {
+                    const unsigned long long kj = __shfl(k1, j - 64, 64);
+                    r0 += kj < k0 ? 1u : 0u;
+                    r1 += kj < k1 ? 1u : 0u;
+                }
+                if (lane < cr && (uint64_t)offr + r0 < a.ids_cap) a.ids[offr + r0] = (uint32_t)(k0 & ~KEY_MASK);
+                if (lane + 64 < cr && (uint64_t)offr + r1 < a.ids_cap) a.ids[offr + r1] = (uint32_t)(k1 & ~KEY_MASK);
             }
         }
         __syncthreads();
@@ -700,9 +707,9 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total) {
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     if (!ntiles) return hipGetLastError();
-    const uint32_t grid = min(ntiles, 256u * 8u);
-    if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(FIN_THREADS), 0, s, a);
-    else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(FIN_THREADS), 0, s, a);
+    const uint32_t grid = min(ntiles, 256u * 16u);
+    if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
