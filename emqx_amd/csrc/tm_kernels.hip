@@ -77,24 +77,41 @@ struct Node {
 };
 
 // One 64-B bucket read (four 16-B slots, key compare).  max_probe bounds the scan.
-template <bool CK>
+// Tables under 4 GiB are read with raw buffer loads (a wave-uniform descriptor
+// built from kernel arguments): four dwordx4 that the compiler cannot narrow,
+// issued back to back.  Larger tables use plain global loads.
+__device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return uint4{v[0], v[1], v[2], v[3]};
+}
+
+template <bool CK, bool BIG>
 __device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint32_t word, Node& n) {
     uint32_t b = home_bucket(parent, word, a.nbuckets);
+    const bool small = !BIG;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<Slot*>(a.slots), 0, BIG ? 0u : a.nslots * 16u, 0x00020000);
     for (uint32_t p = 0; p <= a.max_probe; ++p) {
-        const uint4* q = reinterpret_cast<const uint4*>(a.slots) + CK_((uint64_t)b * BUCKET, a.nslots, 1);
-        const uint4 s0 = q[0], s1 = q[1], s2 = q[2], s3 = q[3];
-        uint4 hit;
-        bool f = true;
-        if (s0.x == parent && s0.y == word) hit = s0;
-        else if (s1.x == parent && s1.y == word) hit = s1;
-        else if (s2.x == parent && s2.y == word) hit = s2;
-        else if (s3.x == parent && s3.y == word) hit = s3;
-        else f = false;
-        if (f) {
-            n.child = hit.z & ID_MASK;
-            n.term = (hit.z & B_TOPIC) ? n.child : NONE;
-            n.hterm = (hit.w & B_HTERM) ? (hit.w & ID_MASK) : NONE;
-            n.flags = ((hit.z & B_PLUS) ? NF_PLUS : 0u) | ((hit.w & B_HASH) ? NF_HASH : 0u);
+        uint4 s0, s1, s2, s3;
+        const uint64_t si = CK_((uint64_t)b * BUCKET, a.nslots, 1);
+        if (small) {
+            const uint32_t off = (uint32_t)si * 16u;
+            s0 = ld_b128(rs, off); s1 = ld_b128(rs, off + 16); s2 = ld_b128(rs, off + 32); s3 = ld_b128(rs, off + 48);
+        } else {
+            const uint4* q = reinterpret_cast<const uint4*>(a.slots) + si;
+            s0 = q[0]; s1 = q[1]; s2 = q[2]; s3 = q[3];
+        }
+        const bool m0 = s0.x == parent && s0.y == word;
+        const bool m1 = s1.x == parent && s1.y == word;
+        const bool m2 = s2.x == parent && s2.y == word;
+        const bool m3 = s3.x == parent && s3.y == word;
+        const uint32_t hz = m0 ? s0.z : m1 ? s1.z : m2 ? s2.z : s3.z;
+        const uint32_t hw = m0 ? s0.w : m1 ? s1.w : m2 ? s2.w : s3.w;
+        if (m0 | m1 | m2 | m3) {
+            n.child = hz & ID_MASK;
+            n.term = (hz & B_TOPIC) ? n.child : NONE;
+            n.hterm = (hw & B_HTERM) ? (hw & ID_MASK) : NONE;
+            n.flags = ((hz & B_PLUS) ? NF_PLUS : 0u) | ((hw & B_HASH) ? NF_HASH : 0u);
             return true;
         }
         if (s3.x == SLOT_EMPTY) return false;   // slots fill in order: a free tail ends the run
@@ -168,6 +185,7 @@ struct alignas(16) TileLds {
     unsigned long long q_key[QCAP];
     uint32_t q_parent[QCAP];
     uint32_t q_meta[QCAP];
+    uint32_t q_pw[QCAP];       // word to probe: the literal w[lc-1] or W_PLUS / W_HASH
     uint32_t words[WCAP];
     uint32_t toff[TILE];
     uint32_t depth[TILE];
@@ -195,7 +213,125 @@ __device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint
     }
 }
 
-template <bool CK>
+// One tile.  IN_LDS: the tile's words are staged in LDS (the common case);
+// otherwise they are read from HBM.  Templated so word reads are plain ds_read
+// or global_load, never flat.
+template <bool CK, bool BIG, bool IN_LDS>
+__device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint32_t t0, uint32_t tend, uint32_t wbase,
+                                           uint8_t fl, bool valid, unsigned long long& sV, unsigned long long& sH,
+                                           unsigned long long& sW, unsigned long long& sM) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t = t0 + lane;
+    const uint32_t* wsrc = IN_LDS ? L.words : a.words;
+    const uint32_t wlim = IN_LDS ? (uint32_t)WCAP : a.nwords;
+    (void)wbase;
+
+    uint32_t qn = 0;
+    bool ovf = false;
+    const bool active = !(fl & TF_SLOW);
+    uint32_t tV = 0, tH = 0, tW = 0;   // committed only if the tile does not overflow
+    const uint32_t d_me = L.depth[lane];
+
+    // ---- level 0: root expansion, one topic per lane
+    {
+        Expand x; x.ne = 0; x.np = 0;
+        uint32_t w0 = 0;
+        if (active && d_me > 0) {
+            const bool dollar = fl & TF_DOLLAR;
+            tV += 1;
+            if (!dollar && (a.root.flags & NF_HASH)) tH += 1;
+            tW += d_me;
+            w0 = wsrc[CK_(L.toff[lane], wlim, 9)];
+            expand_root(a.root, dollar, d_me, w0, x);
+        }
+        const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+        const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+        const uint32_t meta = lane | (1u << M_LVL_SHIFT);
+        const uint32_t wid = w0 & WID_MASK;
+        if (x.np >= 1) {
+            const uint32_t p = qn + pre;
+            L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf0; L.q_key[p] = x.pk0;
+            L.q_pw[p] = (x.pf0 & M_PLUS) ? W_PLUS : wid;
+        }
+        if (x.np >= 2) {
+            const uint32_t p = qn + pre + 1;
+            L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf1; L.q_key[p] = x.pk1;
+            L.q_pw[p] = (x.pf1 & M_PLUS) ? W_PLUS : wid;
+        }
+        qn += __popcll(b0) + __popcll(b1);
+        if (x.ne) {   // at most one emission at the root ('#')
+            L.cnt[lane] = 1;
+            emit_row<CK>(a, t, 0, x.ek0, x.ef0);
+        }
+    }
+
+    // ---- frontier loop: LIFO stack, up to 64 probes per iteration
+    while (qn > 0) {
+        const uint32_t k = min(qn, 64u);
+        const bool has = lane < k;
+        const uint32_t idx = qn - k + lane;
+        uint32_t parent = 0, meta = 0, pw = 0;
+        uint64_t key = 0;
+        if (has) { parent = L.q_parent[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; pw = L.q_pw[idx]; }
+        qn -= k;
+        const uint32_t tl = meta & 63;
+        const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
+        Node s;
+        const bool found = has && probe<CK, BIG>(a, parent, pw, s);
+        Expand x; x.ne = 0; x.np = 0;
+        uint32_t w_here = 0;
+        if (found) {
+            if (!(meta & M_DSTART)) tV += 1;
+            if (s.flags & NF_HASH) tH += 1;
+            const uint32_t base = L.toff[tl];
+            const uint32_t d = L.depth[tl];
+            w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
+            const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
+            expand(s, lc, d, meta, key, w_here, w_prev, x);
+        }
+        const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+        const uint32_t ptot = __popcll(b0) + __popcll(b1);
+        if (qn + ptot > (uint32_t)QCAP) { ovf = true; break; }
+        const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+        const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
+        const uint32_t wid = w_here & WID_MASK;
+        if (x.np >= 1) {
+            const uint32_t p = qn + pre;
+            L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf0; L.q_key[p] = x.pk0;
+            L.q_pw[p] = (x.pf0 & M_PLUS) ? W_PLUS : wid;
+        }
+        if (x.np >= 2) {
+            const uint32_t p = qn + pre + 1;
+            L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf1; L.q_key[p] = x.pk1;
+            L.q_pw[p] = (x.pf1 & M_PLUS) ? W_PLUS : wid;
+        }
+        qn += ptot;
+        if (x.ne) {
+            const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
+            emit_row<CK>(a, t0 + tl, slot, x.ek0, x.ef0);
+            if (x.ne >= 2) emit_row<CK>(a, t0 + tl, slot + 1, x.ek1, x.ef1);
+        }
+    }
+    __syncthreads();
+
+    if (ovf) {
+        // probe stack overflow: every regular topic of the tile goes to the slow path
+        send_to_slow<CK>(a, valid && active, t);
+        return;
+    }
+    sV += tV; sH += tH; sW += tW;
+    const uint32_t c_me = L.cnt[lane];
+    const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
+    send_to_slow<CK>(a, row_ovf, t);
+    if (valid && active && !row_ovf) {
+        a.count[CK_(t, a.n, 16)] = c_me;
+        a.src[CK_(t, a.n, 17)] = ~0ull;
+        sM += c_me;
+    }
+    (void)tend;
+}
+
+template <bool CK, bool BIG>
 __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
     __shared__ TileLds L;
     const uint32_t lane = threadIdx.x;
@@ -218,93 +354,8 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
         L.depth[lane] = my_end - my_off;
         L.cnt[lane] = 0;
         __syncthreads();
-        const uint32_t* wsrc = in_lds ? L.words : a.words;
-        const uint32_t wlim = in_lds ? (uint32_t)WCAP : a.nwords;
-
-        uint32_t qn = 0;
-        bool ovf = false;
-        const bool active = !(fl & TF_SLOW);
-        uint32_t tV = 0, tH = 0, tW = 0;   // committed only if the tile does not overflow
-        const uint32_t d_me = my_end - my_off;
-
-        // ---- level 0: root expansion, one topic per lane
-        {
-            Expand x; x.ne = 0; x.np = 0;
-            if (active && d_me > 0) {
-                const bool dollar = fl & TF_DOLLAR;
-                tV += 1;
-                if (!dollar && (a.root.flags & NF_HASH)) tH += 1;
-                tW += d_me;
-                expand_root(a.root, dollar, d_me, wsrc[CK_(L.toff[lane], wlim, 9)], x);
-            }
-            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
-            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            const uint32_t meta = lane | (1u << M_LVL_SHIFT);
-            if (x.np >= 1) { const uint32_t p = qn + pre; L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf0; L.q_key[p] = x.pk0; }
-            if (x.np >= 2) { const uint32_t p = qn + pre + 1; L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf1; L.q_key[p] = x.pk1; }
-            qn += __popcll(b0) + __popcll(b1);
-            if (x.ne) {   // at most one emission at the root ('#')
-                L.cnt[lane] = 1;
-                emit_row<CK>(a, t, 0, x.ek0, x.ef0);
-            }
-        }
-
-        // ---- frontier loop: LIFO stack, up to 64 probes per iteration
-        while (qn > 0) {
-            const uint32_t k = min(qn, 64u);
-            const bool has = lane < k;
-            const uint32_t idx = qn - k + lane;
-            uint32_t parent = 0, meta = 0;
-            uint64_t key = 0;
-            if (has) { parent = L.q_parent[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; }
-            qn -= k;
-            const uint32_t tl = meta & 63;
-            const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
-            const uint32_t base = L.toff[tl];
-            const uint32_t d = L.depth[tl];
-            uint32_t pw = W_PLUS;
-            if (has && !(meta & M_PLUS)) pw = wsrc[CK_(base + lc - 1, wlim, 10)] & WID_MASK;
-            Node s;
-            const bool found = has && probe<CK>(a, parent, pw, s);
-            Expand x; x.ne = 0; x.np = 0;
-            if (found) {
-                if (!(meta & M_DSTART)) tV += 1;
-                if (s.flags & NF_HASH) tH += 1;
-                const uint32_t w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
-                const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
-                expand(s, lc, d, meta, key, w_here, w_prev, x);
-            }
-            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
-            const uint32_t ptot = __popcll(b0) + __popcll(b1);
-            if (qn + ptot > (uint32_t)QCAP) { ovf = true; break; }
-            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
-            if (x.np >= 1) { const uint32_t p = qn + pre; L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf0; L.q_key[p] = x.pk0; }
-            if (x.np >= 2) { const uint32_t p = qn + pre + 1; L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf1; L.q_key[p] = x.pk1; }
-            qn += ptot;
-            if (x.ne) {
-                const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
-                emit_row<CK>(a, t0 + tl, slot, x.ek0, x.ef0);
-                if (x.ne >= 2) emit_row<CK>(a, t0 + tl, slot + 1, x.ek1, x.ef1);
-            }
-        }
-        __syncthreads();
-
-        if (ovf) {
-            // probe stack overflow: every regular topic of the tile goes to the slow path
-            send_to_slow<CK>(a, valid && active, t);
-            __syncthreads();
-            continue;
-        }
-        sV += tV; sH += tH; sW += tW;
-        const uint32_t c_me = L.cnt[lane];
-        const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
-        send_to_slow<CK>(a, row_ovf, t);
-        if (valid && active && !row_ovf) {
-            a.count[CK_(t, a.n, 16)] = c_me;
-            a.src[CK_(t, a.n, 17)] = ~0ull;
-            sM += c_me;
-        }
+        if (in_lds) match_tile<CK, BIG, true>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
+        else match_tile<CK, BIG, false>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
         __syncthreads();
     }
 
@@ -368,7 +419,7 @@ __device__ __forceinline__ uint32_t slow_flags(uint32_t pf) {
     return ((pf & M_PLUS) ? SM_PLUS : 0u) | ((pf & M_SKIPE) ? SM_SKIPE : 0u) | ((pf & M_DSTART) ? SM_DSTART : 0u);
 }
 
-template <bool CK>
+template <bool CK, bool BIG>
 __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
     __shared__ unsigned long long sk[SORT_LDS];
     __shared__ uint32_t sf[SORT_LDS];
@@ -428,7 +479,7 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             uint32_t pw = W_PLUS;
             if (has && !(meta & SM_PLUS)) pw = w[CK_(lc - 1, d, 28)] & WID_MASK;
             Node s;
-            const bool found = has && probe<CK>(a, parent, pw, s);
+            const bool found = has && probe<CK, BIG>(a, parent, pw, s);
             Expand x; x.ne = 0; x.np = 0;
             if (found) {
                 if (!(meta & SM_DSTART)) sV += 1;
@@ -683,17 +734,23 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 
 // ------------------------------------------------------------ launchers
 
-hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked) {
+template <bool CK, bool BIG>
+static void launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     if (ev_a) (void)hipEventRecord(ev_a, s);
     if (ntiles) {
         const uint32_t grid = min(ntiles, 256u * 16u);
-        if (checked) hipLaunchKernelGGL(tm_match_tiles<true>, dim3(grid), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL(tm_match_tiles<false>, dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((tm_match_tiles<CK, BIG>), dim3(grid), dim3(64), 0, s, a);
     }
     if (ev_b) (void)hipEventRecord(ev_b, s);
-    if (checked) hipLaunchKernelGGL(tm_match_slow<true>, dim3(a.s_waves), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(tm_match_slow<false>, dim3(a.s_waves), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((tm_match_slow<CK, BIG>), dim3(a.s_waves), dim3(64), 0, s, a);
+}
+
+hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked) {
+    // the edge hash is read with 32-bit-offset buffer loads unless it exceeds 4 GiB
+    const bool big = (uint64_t)a.nslots * sizeof(Slot) > 0xFFFFFFFFull;
+    if (checked) { if (big) launch_match_t<true, true>(a, s, ev_a, ev_b); else launch_match_t<true, false>(a, s, ev_a, ev_b); }
+    else { if (big) launch_match_t<false, true>(a, s, ev_a, ev_b); else launch_match_t<false, false>(a, s, ev_a, ev_b); }
     return hipGetLastError();
 }
 
