@@ -801,14 +801,15 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // rows[] = n * K fast-row slots (u64 path code | id); sfids[] = slow-path rows;
-    // ids[] = the CSR, sized from the last batch's total (grown on demand)
+    // rows[] = K u64 emission slots per lane of every match wave (reused tile after
+    // tile, so it stays cache-resident); sfids[] = sorted rows staged per tile;
+    // ids[] = the CSR.  sfids/ids start at 32 per topic and grow on demand.
     int reserve_rows(tm_batch* b) {
         int rc;
-        const uint64_t fast = std::max<uint64_t>((uint64_t)b->n * row_cap, 1);
+        const uint64_t fast = std::max<uint64_t>((uint64_t)match_waves(b->n, device) * 64 * row_cap, 1);
         if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
-        if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n, 1u << 16)))) return rc;
-        if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 16, 1u << 16)))) return rc;
+        if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
+        if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         return TM_OK;
     }
@@ -851,6 +852,11 @@ struct tm_engine {
         a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
         a.slow_list = b->d_slow; a.n_slow = (uint32_t)b->h_slow.size();
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
+        a.grid = match_waves(b->n, device);
+        if ((uint64_t)a.grid * 64 * row_cap > b->c_rows) {
+            snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
+            return TM_EIO;
+        }
         a.sfids = b->d_sfids; a.sfids_cap = b->c_sfids;
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
@@ -864,7 +870,7 @@ struct tm_engine {
         a.dbg = checked ? d_dbg : nullptr;
         HIP_OK(launch_match(a, stream, b->ev0, b->ev1, checked));
         ScanArgs s{};
-        s.count = b->d_count; s.src = b->d_src; s.rows = b->d_rows; s.row_cap = row_cap;
+        s.count = b->d_count; s.src = b->d_src;
         s.sfids = b->d_sfids; s.sfids_cap = b->c_sfids;
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;

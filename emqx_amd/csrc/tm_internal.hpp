@@ -89,6 +89,7 @@ enum Ctrl : uint32_t {
     CTRL_NOVF = 1,          // topics appended to the ovf list
     CTRL_ERR = 2,           // error bits
     CTRL_SLOW_DONE = 3,
+    CTRL_TILE_NEXT = 4,     // dynamic tile tickets of tm_match_tiles
     CTRL_WORDS = 16
 };
 constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
@@ -115,10 +116,12 @@ struct MatchArgs {
     uint32_t n_slow;
     // outputs
     uint32_t* count;          // per topic |M(t)|
-    unsigned long long* src;  // per topic: ~0 = fast row, else offset of its sorted row in sfids[]
-    unsigned long long* rows; // [n * row_cap] fast rows: (path code | filter id), unsorted
+    unsigned long long* src;  // per topic: offset of its sorted row in sfids[]
+    unsigned long long* rows; // [match_waves(n) * 64 * row_cap] wave-private emission rows,
+                              // (path code | filter id), reused by every tile of the wave
     uint32_t row_cap;         // K: per-topic row slots on the fast path
-    uint32_t* sfids;          // slow-path region: sorted filter ids
+    uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
+    uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;
     uint32_t* ovf_list;       // topics redone by the slow path (row > K or stack overflow)
@@ -145,8 +148,6 @@ struct MatchArgs {
 struct ScanArgs {
     const uint32_t* count;
     const unsigned long long* src;
-    const unsigned long long* rows;
-    uint32_t row_cap;
     const uint32_t* sfids;
     uint64_t sfids_cap;
     uint32_t* row_off;        // n + 1
@@ -167,5 +168,8 @@ hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* va
 hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx,
                                 const uint64_t* off, const uint32_t* len, uint32_t n, hipStream_t s);
 uint32_t scan_block_count(uint32_t n);
+// workgroups (one wave each) of tm_match_tiles for n topics on this device:
+// min(tiles, resident capacity), so that every wave is resident from the start
+uint32_t match_waves(uint32_t n, int device);
 
 }  // namespace etm

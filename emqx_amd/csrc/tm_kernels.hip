@@ -12,16 +12,21 @@
 //                   child's whole summary, and the lanes push their children
 //                   through ballot + mbcnt prefix sums.  Each match is one u64
 //                   (3-bit-per-level path code | filter id) stored into the
-//                   topic's HBM row; path-code order == Erlang binary order of
-//                   the filters (DESIGN.md "Sort order").
+//                   topic's row of the wave's private emission buffer; path-code
+//                   order == Erlang binary order of the filters (DESIGN.md "Sort
+//                   order").  When the tile's frontier is empty the wave sorts
+//                   its 64 rows in registers (bitonic over __shfl_xor) and
+//                   stages the filter ids as ONE contiguous run per tile.
 //   tm_match_slow   one wavefront per topic, frontier in global scratch: deep
 //                   (> 10 levels) or irregular topics (sorted by filter bytes),
 //                   rows longer than K and tiles whose LDS stack overflowed.
 //   scan            exclusive scan of the per-topic counts -> CSR offsets.
-//   tm_finalize     one workgroup per tile: rows staged in LDS, rank-sorted per
-//                   topic, filter ids written straight into the CSR.
+//   tm_finalize     one wave per tile: a tile's staged run is copied into the
+//                   CSR with coalesced loads/stores (per-topic copy for tiles
+//                   holding slow-path topics).
 //
 // No MFMA: this is a dependent irregular gather, bound by the memory system.
+#include <cstddef>
 #include "tm_internal.hpp"
 
 namespace etm {
@@ -190,13 +195,136 @@ struct alignas(16) TileLds {
     uint32_t toff[TILE];
     uint32_t depth[TILE];
     uint32_t cnt[TILE];
+    uint32_t list[TILE];
 };
 
+// Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
 template <bool CK>
-__device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t t, uint32_t slot, uint64_t key, uint32_t fid) {
+__device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t tl, uint32_t slot, uint64_t key, uint32_t fid) {
     if (slot < a.row_cap) {
-        const uint64_t i = (uint64_t)t * a.row_cap + slot;
-        a.rows[CK_(i, (uint64_t)a.n * a.row_cap, 13)] = (key & KEY_MASK) | fid;
+        const uint64_t i = ((uint64_t)blockIdx.x * TILE + tl) * a.row_cap + slot;
+        a.rows[CK_(i, (uint64_t)gridDim.x * TILE * a.row_cap, 13)] = (key & KEY_MASK) | fid;
+    }
+}
+
+// The probe stack and the word cache are free once a tile's frontier is empty:
+// the epilogue reuses those 12 KB as a staging area of STAGE u64.
+constexpr uint32_t STAGE = (QCAP * 8 + QCAP * 12 + WCAP * 4) / 8;
+static_assert(offsetof(TileLds, words) + sizeof(uint32_t) * WCAP == STAGE * 8, "staging area must be contiguous");
+
+// Tile epilogue: sort the 64 rows of this wave and write their filter ids to
+// sfids[dst .. dst + c).  The rows are pulled into LDS a chunk of whole rows at
+// a time (at most STAGE elements), eight rows per batch of independent loads:
+// the rows were written moments ago but have usually left L2, so a dependent
+// load per sort group would pay full memory latency ~20 times per tile.  Rows
+// of size class W (W/2 < c <= W, W = 2..64) are then packed 64/W per
+// wave-instruction, one element per lane, and sorted by a W-wide bitonic
+// network of __shfl_xor exchanges.  65..128 elements: rank count, two per lane.
+template <bool CK>
+__device__ __forceinline__ void sort_classes(const MatchArgs& a, TileLds& L, bool keep, uint32_t c, uint32_t pos,
+                                             uint32_t dst) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long* stg = reinterpret_cast<const unsigned long long*>(L.q_key);
+    if (keep && c == 1) a.sfids[CK_(dst, a.sfids_cap, 40)] = (uint32_t)(stg[CK_(pos, STAGE, 41)] & ~KEY_MASK);
+#pragma unroll
+    for (uint32_t W = 2; W <= 64; W <<= 1) {
+        const bool mine = keep && c > W / 2 && c <= W;
+        const uint64_t m = __ballot(mine);
+        if (!m) continue;
+        const uint32_t nrows = __popcll(m);
+        if (mine) L.list[prefix_count(m)] = lane;
+        __syncthreads();
+        const uint32_t e = lane & (W - 1);
+        const uint32_t STEP = 64 / W;
+        for (uint32_t g = 0; g < nrows; g += STEP) {
+            const uint32_t r = g + lane / W;
+            const bool rv = r < nrows;
+            const uint32_t owner = rv ? L.list[r] : 0u;
+            const uint32_t cr = __shfl(c, owner, 64);
+            const uint32_t pr = __shfl(pos, owner, 64);
+            const uint32_t dr = __shfl(dst, owner, 64);
+            unsigned long long key = ~0ull;
+            if (rv && e < cr) key = stg[CK_(pr + e, STAGE, 42)];
+#pragma unroll
+            for (uint32_t kk = 2; kk <= W; kk <<= 1) {
+#pragma unroll
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    const unsigned long long other = __shfl_xor(key, j, 64);
+                    const bool up = (e & kk) == 0;
+                    const bool lower = (e & j) == 0;
+                    const unsigned long long lo = key < other ? key : other;
+                    const unsigned long long hi = key < other ? other : key;
+                    key = (lower == up) ? lo : hi;
+                }
+            }
+            if (rv && e < cr) a.sfids[CK_((uint64_t)dr + e, a.sfids_cap, 44)] = (uint32_t)(key & ~KEY_MASK);
+        }
+        __syncthreads();
+    }
+    {
+        const bool mine = keep && c > 64;
+        uint64_t m = __ballot(mine);
+        while (m) {
+            const uint32_t owner = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t cr = __shfl(c, owner, 64);
+            const uint32_t pr = __shfl(pos, owner, 64);
+            const uint32_t dr = __shfl(dst, owner, 64);
+            unsigned long long k0 = ~0ull, k1 = ~0ull;
+            if (lane < cr) k0 = stg[CK_(pr + lane, STAGE, 45)];
+            if (lane + 64 < cr) k1 = stg[CK_(pr + lane + 64, STAGE, 46)];
+            uint32_t r0 = 0, r1 = 0;
+            for (uint32_t j = 0; j < 64; ++j) {
+                const unsigned long long kj = __shfl(k0, j, 64);
+                r0 += kj < k0 ? 1u : 0u;
+                r1 += kj < k1 ? 1u : 0u;
+            }
+            for (uint32_t j = 64; j < cr; ++j) {
+                const unsigned long long kj = __shfl(k1, j - 64, 64);
+                r0 += kj < k0 ? 1u : 0u;
+                r1 += kj < k1 ? 1u : 0u;
+            }
+            if (lane < cr) a.sfids[CK_((uint64_t)dr + r0, a.sfids_cap, 47)] = (uint32_t)(k0 & ~KEY_MASK);
+            if (lane + 64 < cr) a.sfids[CK_((uint64_t)dr + r1, a.sfids_cap, 48)] = (uint32_t)(k1 & ~KEY_MASK);
+        }
+    }
+}
+
+// c <= row_cap <= 128 for every kept row, so a chunk always holds at least one row.
+template <bool CK>
+__device__ __forceinline__ void sort_rows(const MatchArgs& a, TileLds& L, bool keep, uint32_t c, uint32_t pos,
+                                          uint32_t dst) {
+    const uint32_t lane = threadIdx.x;
+    unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q_key);
+    const uint64_t rbase = (uint64_t)blockIdx.x * TILE * a.row_cap;
+    const uint64_t rlim = (uint64_t)gridDim.x * TILE * a.row_cap;
+    uint32_t rs = 0;
+    while (rs < (uint32_t)TILE) {
+        const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
+        const uint64_t beyond = __ballot(lane >= rs && pos + c - p0 > STAGE);
+        const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : (uint32_t)TILE;
+        for (uint32_t r0 = rs; r0 < re; r0 += 8) {
+            unsigned long long v0[8], v1[8];
+            uint32_t cr[8], pr[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t r = (r0 + u) & (TILE - 1);
+                cr[u] = r0 + u < re ? __builtin_amdgcn_readlane(c, r) : 0u;
+                pr[u] = __builtin_amdgcn_readlane(pos, r) - p0;
+                const uint64_t rb = rbase + (uint64_t)r * a.row_cap;
+                v0[u] = lane < cr[u] ? a.rows[CK_(rb + lane, rlim, 50)] : 0ull;
+                v1[u] = lane + 64 < cr[u] ? a.rows[CK_(rb + lane + 64, rlim, 51)] : 0ull;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                if (lane < cr[u]) stg[CK_(pr[u] + lane, STAGE, 52)] = v0[u];
+                if (lane + 64 < cr[u]) stg[CK_(pr[u] + lane + 64, STAGE, 53)] = v1[u];
+            }
+        }
+        __syncthreads();
+        sort_classes<CK>(a, L, keep && lane >= rs && lane < re, c, pos - p0, dst);
+        __syncthreads();
+        rs = re;
     }
 }
 
@@ -261,7 +389,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
         qn += __popcll(b0) + __popcll(b1);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
-            emit_row<CK>(a, t, 0, x.ek0, x.ef0);
+            emit_row<CK>(a, lane, 0, x.ek0, x.ef0);
         }
     }
 
@@ -308,8 +436,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
         qn += ptot;
         if (x.ne) {
             const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
-            emit_row<CK>(a, t0 + tl, slot, x.ek0, x.ef0);
-            if (x.ne >= 2) emit_row<CK>(a, t0 + tl, slot + 1, x.ek1, x.ef1);
+            emit_row<CK>(a, tl, slot, x.ek0, x.ef0);
+            if (x.ne >= 2) emit_row<CK>(a, tl, slot + 1, x.ek1, x.ef1);
         }
     }
     __syncthreads();
@@ -323,9 +451,27 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
     const uint32_t c_me = L.cnt[lane];
     const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
     send_to_slow<CK>(a, row_ovf, t);
-    if (valid && active && !row_ovf) {
+    const bool keep = valid && active && !row_ovf;
+    const uint32_t c = keep ? c_me : 0u;
+    // one contiguous staging run per tile: exclusive scan of the counts
+    uint32_t incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += u;
+    }
+    const uint32_t tot = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 0 && tot) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], tot);
+    base = __shfl(base, 0, 64);
+    const uint32_t dst = base + incl - c;
+    if ((uint64_t)base + tot <= a.sfids_cap) {
+        sort_rows<CK>(a, L, keep, c, incl - c, dst);
+    } else if (lane == 0) {
+        atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
+    }
+    if (keep) {
         a.count[CK_(t, a.n, 16)] = c_me;
-        a.src[CK_(t, a.n, 17)] = ~0ull;
+        a.src[CK_(t, a.n, 17)] = dst;
         sM += c_me;
     }
     (void)tend;
@@ -338,7 +484,12 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0;
 
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // first tile static, then tickets; the next ticket is taken at the start of
+    // a tile so its latency hides behind the tile's work
+    uint32_t tile = blockIdx.x;
+    while (tile < ntiles) {
+        uint32_t ticket = 0;
+        if (lane == 0) ticket = atomicAdd(&a.ctrl[CTRL_TILE_NEXT], 1u);
         const uint32_t t0 = tile * TILE;
         const uint32_t tend = min(t0 + TILE, a.n);
         const uint32_t t = t0 + lane;
@@ -357,6 +508,7 @@ __global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
         if (in_lds) match_tile<CK, BIG, true>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
         else match_tile<CK, BIG, false>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
         __syncthreads();
+        tile = __builtin_amdgcn_readfirstlane(ticket) + gridDim.x;
     }
 
     for (int o = 32; o > 0; o >>= 1) {
@@ -629,95 +781,51 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t 
     }
 }
 
-// Pass 3: one wavefront per tile of 64 topics (lane = topic).  Fast rows are
-// sorted in registers: rows of size class W (W/2 < c <= W, W = 2..64) are
-// packed 64/W per wave-instruction, one element per lane, and put through a
-// W-wide bitonic network of __shfl_xor exchanges; filter ids go straight to
-// ids[row_off[t] + e].  Rows of 65..128 elements (rare) use a rank count with
-// two elements per lane.  Slow-path rows are already sorted: copied.
+// Pass 3: one wavefront per tile of 64 topics.  Finishes the CSR offsets and
+// copies the tile's sorted rows from the staging region.  A tile whose rows were
+// staged as one run (no slow-path topic in it) is one contiguous copy, four
+// coalesced dword loads in flight per lane; otherwise each topic is copied on its own.
 template <bool CK>
 __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
-    __shared__ uint32_t list[TILE];
     const uint32_t lane = threadIdx.x;
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t t0 = tile * TILE;
-        const uint32_t t = t0 + lane;
+        const uint32_t t = tile * TILE + lane;
         const bool valid = t < a.n;
         uint32_t c = 0, off = 0;
-        bool fast = false;
+        uint64_t s = 0;
         if (valid) {
             c = a.count[t];
-            const uint64_t s = a.src[t];
-            fast = s == ~0ull;
+            s = a.src[t];
             off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
             a.row_off[t] = off;      // finish the CSR offsets (scan pass 1 was block-local)
-            if (!fast && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap)
-                for (uint32_t i = 0; i < c; ++i) a.ids[off + i] = a.sfids[s + i];
-            if (fast && c == 1 && off < a.ids_cap)
-                a.ids[off] = (uint32_t)(a.rows[(uint64_t)t * a.row_cap] & ~KEY_MASK);
         }
-        // size classes W = 2, 4, ..., 64
-#pragma unroll
-        for (uint32_t W = 2; W <= 64; W <<= 1) {
-            const bool mine = fast && c > W / 2 && c <= W;
-            const uint64_t m = __ballot(mine);
-            if (!m) continue;
-            const uint32_t nrows = __popcll(m);
-            if (mine) list[prefix_count(m)] = lane;
-            __syncthreads();
-            const uint32_t e = lane & (W - 1);
-            for (uint32_t g = 0; g < nrows; g += 64 / W) {
-                const uint32_t r = g + lane / W;
-                const bool rv = r < nrows;
-                const uint32_t owner = rv ? list[r] : 0u;
-                const uint32_t cr = __shfl(c, owner, 64);
-                const uint32_t offr = __shfl(off, owner, 64);
-                unsigned long long key = ~0ull;
-                if (rv && e < cr) key = a.rows[(uint64_t)(t0 + owner) * a.row_cap + e];
-                for (uint32_t kk = 2; kk <= W; kk <<= 1) {
-                    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                        const unsigned long long other = __shfl_xor(key, j, 64);
-                        const bool up = (e & kk) == 0;
-                        const bool lower = (e & j) == 0;
-                        const unsigned long long lo = key < other ? key : other;
-                        const unsigned long long hi = key < other ? other : key;
-                        key = (lower == up) ? lo : hi;
-                    }
-                }
-                if (rv && e < cr && (uint64_t)offr + e < a.ids_cap) a.ids[offr + e] = (uint32_t)(key & ~KEY_MASK);
+        const bool any = c > 0;
+        const uint64_t m = __ballot(any);
+        if (!m) continue;
+        const uint64_t delta = s - (uint64_t)off;
+        const uint32_t first = (uint32_t)__builtin_ctzll(m);
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(m);
+        const uint64_t d0 = __shfl(delta, first, 64);
+        if (__ballot(any && delta != d0) == 0) {
+            const uint32_t lo = __shfl(off, first, 64);
+            const uint32_t hi = __shfl(off + c, last, 64);
+            const uint64_t sb = (uint64_t)lo + d0;
+            if ((uint64_t)hi > a.ids_cap || sb + (hi - lo) > a.sfids_cap) continue;   // rerun path
+            for (uint32_t i = lo + lane; i < hi; i += 256) {
+                const uint32_t i1 = i + 64, i2 = i + 128, i3 = i + 192;
+                const uint32_t v0 = a.sfids[CK_(sb + (i - lo), a.sfids_cap, 30)];
+                const uint32_t v1 = i1 < hi ? a.sfids[CK_(sb + (i1 - lo), a.sfids_cap, 31)] : 0u;
+                const uint32_t v2 = i2 < hi ? a.sfids[CK_(sb + (i2 - lo), a.sfids_cap, 32)] : 0u;
+                const uint32_t v3 = i3 < hi ? a.sfids[CK_(sb + (i3 - lo), a.sfids_cap, 33)] : 0u;
+                a.ids[CK_(i, a.ids_cap, 34)] = v0;
+                if (i1 < hi) a.ids[CK_(i1, a.ids_cap, 35)] = v1;
+                if (i2 < hi) a.ids[CK_(i2, a.ids_cap, 36)] = v2;
+                if (i3 < hi) a.ids[CK_(i3, a.ids_cap, 37)] = v3;
             }
-            __syncthreads();
+        } else if (any && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap) {
+            for (uint32_t i = 0; i < c; ++i) a.ids[CK_((uint64_t)off + i, a.ids_cap, 38)] = a.sfids[CK_(s + i, a.sfids_cap, 39)];
         }
-        // 64 < c <= 128: rank count, two elements per lane, one row at a time
-        {
-            const bool mine = fast && c > 64;
-            uint64_t m = __ballot(mine);
-            while (m) {
-                const uint32_t owner = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                const uint32_t cr = __shfl(c, owner, 64);
-                const uint32_t offr = __shfl(off, owner, 64);
-                const uint64_t rb = (uint64_t)(t0 + owner) * a.row_cap;
-                unsigned long long k0 = ~0ull, k1 = ~0ull;
-                if (lane < cr) k0 = a.rows[rb + lane];
-                if (lane + 64 < cr) k1 = a.rows[rb + lane + 64];
-                uint32_t r0 = 0, r1 = 0;
-                for (uint32_t j = 0; j < 64; ++j) {
-                    const unsigned long long kj = __shfl(k0, j, 64);
-                    r0 += kj < k0 ? 1u : 0u;
-                    r1 += kj < k1 ? 1u : 0u;
-                }
-                for (uint32_t j = 64; j < cr; ++j) {
-                    const unsigned long long kj = __shfl(k1, j - 64, 64);
-                    r0 += kj < k0 ? 1u : 0u;
-                    r1 += kj < k1 ? 1u : 0u;
-                }
-                if (lane < cr && (uint64_t)offr + r0 < a.ids_cap) a.ids[offr + r0] = (uint32_t)(k0 & ~KEY_MASK);
-                if (lane + 64 < cr && (uint64_t)offr + r1 < a.ids_cap) a.ids[offr + r1] = (uint32_t)(k1 & ~KEY_MASK);
-            }
-        }
-        __syncthreads();
     }
 }
 
@@ -734,12 +842,31 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 
 // ------------------------------------------------------------ launchers
 
+uint32_t match_waves(uint32_t n, int device) {
+    static uint32_t cap[64] = {0};
+    const uint32_t ntiles = (n + TILE - 1) / TILE;
+    uint32_t c = (device >= 0 && device < 64) ? cap[device] : 0u;
+    if (!c) {
+        int per_cu = 0, cus = 0;
+        // all four instances have the same LDS footprint, which bounds residency
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tm_match_tiles<false, false>, 64, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            per_cu <= 0 || cus <= 0) {
+            (void)hipGetLastError();
+            per_cu = 12; cus = 256;
+        }
+        c = (uint32_t)per_cu * (uint32_t)cus;
+        if (device >= 0 && device < 64) cap[device] = c;
+    }
+    return ntiles < c ? ntiles : c;
+}
+
 template <bool CK, bool BIG>
 static void launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     if (ev_a) (void)hipEventRecord(ev_a, s);
     if (ntiles) {
-        const uint32_t grid = min(ntiles, 256u * 16u);
+        const uint32_t grid = a.grid;
         hipLaunchKernelGGL((tm_match_tiles<CK, BIG>), dim3(grid), dim3(64), 0, s, a);
     }
     if (ev_b) (void)hipEventRecord(ev_b, s);
@@ -764,7 +891,7 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total) {
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     if (!ntiles) return hipGetLastError();
-    const uint32_t grid = min(ntiles, 256u * 16u);
+    const uint32_t grid = min(ntiles, 256u * 32u);   // 8 waves per SIMD
     if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(64), 0, s, a);
     else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
