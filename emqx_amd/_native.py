@@ -24,6 +24,7 @@ TM_EOVERFLOW = -75
 TM_EABORT = -125
 TM_NONE = 0xFFFFFFFF
 TM_MAX_TOPIC_LEN = 4096
+TM_CFG_FROZEN_DICT = 1
 
 _ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
              TM_EINVAL: "EINVAL", TM_EOVERFLOW: "EOVERFLOW", TM_EABORT: "EABORT"}
@@ -89,6 +90,13 @@ SIGNATURES = {
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_free": (None, [P, P]),
+    "tm_trie_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
+    "tm_filter_shard": (C.c_int, [P, U8P, SZ, C.c_uint32]),
+    "tm_tokenize": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64)]),
+    "tm_batch_prepare_tokens": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint64, C.c_int, C.POINTER(P)]),
+    "tm_tokens_shard": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, P]),
+    "tm_batch_export": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint32]),
     "tm_filter_bytes": (C.POINTER(C.c_uint8), [P, C.c_uint32, C.POINTER(SZ)]),
     "tm_filter_id": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32)]),
     "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),

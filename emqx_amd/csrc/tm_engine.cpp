@@ -222,8 +222,17 @@ struct tm_batch {
     uint64_t total = 0;
     tm_batch_stats st{};
     ScanArgs scan_args{};
+    // token batches (tm_batch_prepare_tokens): no bytes to re-tokenise; with
+    // device-resident tokens the generic-path list is built on the device
+    bool tokens_only = false;
+    bool dev_slow = false;
+    uint32_t *d_nslow = nullptr, *h_bad = nullptr;
+    size_t c_nslow = 0, ch_bad = 0;
 
     void release() {
+        dev_free(d_nslow);
+        if (h_bad) (void)hipHostFree(h_bad);
+        h_bad = nullptr;
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
         dev_free(d_count); dev_free(d_src); dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
         if (h_total) (void)hipHostFree(h_total);
@@ -306,6 +315,7 @@ struct tm_engine {
 
     uint64_t version = 1;
     uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
+    bool frozen = false;           // TM_CFG_FROZEN_DICT: words only via tm_dict_load
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
@@ -497,11 +507,38 @@ struct tm_engine {
             if (w.n == 0) id = W_EMPTY;
             else if (is_plus(w)) id = W_PLUS;
             else if (is_hash(w)) id = W_HASH;
-            else id = insert ? dict.intern(w.p, w.n) : dict.find(w.p, w.n);
+            else id = (insert && !frozen) ? dict.intern(w.p, w.n) : dict.find(w.p, w.n);
             if (id == W_UNKNOWN) return false;
             ids.push_back(id);
         }
         return true;
+    }
+
+    // tm_dict_load: intern words in order ('', '+', '#' have fixed ids)
+    int dict_load(const uint8_t* buf, const uint64_t* offs, uint32_t n) {
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t* p = buf + offs[i];
+            const size_t len = offs[i + 1] - offs[i];
+            if (offs[i + 1] < offs[i] || memchr(p, '/', len)) return TM_EINVAL;
+            if (len == 0 || (len == 1 && (p[0] == '+' || p[0] == '#'))) continue;
+            dict.intern(p, len);
+        }
+        return TM_OK;
+    }
+
+    // tm_filter_shard: shard of the literal (w0, w1) prefix, or nshards
+    int filter_shard(const uint8_t* t, size_t len, uint32_t nshards) {
+        if (nshards == 0) return TM_EINVAL;
+        static thread_local std::vector<TWord> ws;
+        split_words(t, len, ws);
+        if (ws.size() < 2 || is_plus(ws[0]) || is_hash(ws[0]) || is_plus(ws[1]) || is_hash(ws[1]))
+            return (int)nshards;
+        uint32_t id[2];
+        for (int k = 0; k < 2; ++k) {
+            id[k] = ws[k].n == 0 ? W_EMPTY : dict.find(ws[k].p, ws[k].n);
+            if (id[k] == W_UNKNOWN) return TM_ENOENT;
+        }
+        return (int)prefix_shard(id[0], id[1], nshards);
     }
 
     uint32_t walk(const std::vector<uint32_t>& ids) const {
@@ -517,8 +554,8 @@ struct tm_engine {
 
     // emqx_trie:insert/1 (src/emqx_trie.erl:81-93)
     int trie_insert(const uint8_t* t, size_t len) {
-        std::vector<uint32_t> ids;
-        filter_words(t, len, true, ids);
+        static thread_local std::vector<uint32_t> ids;
+        if (!filter_words(t, len, true, ids)) return TM_ENOENT;   // frozen dictionary only
         const uint32_t found = walk(ids);
         if (found != NONE) {
             if (!n_topic[found]) { set_topic(found, t, len); ++version; }
@@ -708,13 +745,22 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------ batches
-    void tokenize_range(tm_batch* b, uint32_t lo, uint32_t hi, std::vector<uint32_t>& slow_out) const {
+    // topic t = bytes[offs[t] .. offs[t+1]); its words go to words[toff[t] ..]
+    struct TokView {
+        const uint8_t* bytes;
+        const uint64_t* offs;
+        uint32_t* words;
+        const uint32_t* toff;
+        uint8_t* tflags;
+    };
+
+    void tokenize_range(const TokView& v, uint32_t lo, uint32_t hi, std::vector<uint32_t>& slow_out) const {
         std::vector<TWord> ws;
         for (uint32_t t = lo; t < hi; ++t) {
-            const uint8_t* p = b->bytes.data() + b->offs[t];
-            const size_t len = b->offs[t + 1] - b->offs[t];
+            const uint8_t* p = v.bytes + v.offs[t];
+            const size_t len = v.offs[t + 1] - v.offs[t];
             split_words(p, len, ws);
-            uint32_t* out = b->h_words.data() + b->h_toff[t];
+            uint32_t* out = v.words + v.toff[t];
             bool irregular = false;
             for (size_t i = 0; i < ws.size(); ++i) {
                 const TWord& w = ws[i];
@@ -729,42 +775,69 @@ struct tm_engine {
             uint8_t fl = 0;
             if (len > 0 && p[0] == '$') fl |= TF_DOLLAR;
             if (irregular || ws.size() > FAST_MAX_DEPTH) fl |= TF_SLOW;
-            b->h_tflags[t] = fl;
+            v.tflags[t] = fl;
             if (fl & TF_SLOW) slow_out.push_back(t);
         }
+    }
+
+    // word offsets (separators + 1 per topic); TM_EOVERFLOW past u32 offsets
+    static int count_words(const uint8_t* bytes, const uint64_t* offs, uint32_t n, uint32_t* toff, uint64_t* total) {
+        uint64_t acc = 0;
+        for (uint32_t t = 0; t < n; ++t) {
+            toff[t] = (uint32_t)acc;
+            const uint8_t* p = bytes + offs[t];
+            const size_t len = offs[t + 1] - offs[t];
+            acc += 1 + (uint64_t)std::count(p, p + len, (uint8_t)'/');
+            if (acc > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        }
+        toff[n] = (uint32_t)acc;
+        *total = acc;
+        return TM_OK;
+    }
+
+    void tokenize_view(const TokView& v, uint32_t n, std::vector<uint32_t>& slow_all) const {
+        slow_all.clear();
+        const unsigned nt = (n >= 65536) ? threads : 1;
+        if (nt <= 1) {
+            tokenize_range(v, 0, n, slow_all);
+            return;
+        }
+        std::vector<std::vector<uint32_t>> slow(nt);
+        std::vector<std::thread> th;
+        for (unsigned i = 0; i < nt; ++i) {
+            const uint32_t lo = (uint32_t)((uint64_t)n * i / nt), hi = (uint32_t)((uint64_t)n * (i + 1) / nt);
+            th.emplace_back([this, &v, lo, hi, &slow, i] { tokenize_range(v, lo, hi, slow[i]); });
+        }
+        for (auto& x : th) x.join();
+        for (auto& s : slow) slow_all.insert(slow_all.end(), s.begin(), s.end());
     }
 
     int tokenize(tm_batch* b) {
         const uint32_t n = b->n;
         b->h_toff.resize((size_t)n + 1);
         b->h_tflags.resize(n);
-        // word counts = separators + 1
         uint64_t acc = 0;
-        for (uint32_t t = 0; t < n; ++t) {
-            b->h_toff[t] = (uint32_t)acc;
-            const uint8_t* p = b->bytes.data() + b->offs[t];
-            const size_t len = b->offs[t + 1] - b->offs[t];
-            acc += 1 + (uint64_t)std::count(p, p + len, (uint8_t)'/');
-            if (acc > 0xFFFFFFF0ull) return TM_EOVERFLOW;
-        }
-        b->h_toff[n] = (uint32_t)acc;
+        int rc = count_words(b->bytes.data(), b->offs.data(), n, b->h_toff.data(), &acc);
+        if (rc) return rc;
         b->nwords = acc;
         b->h_words.resize(acc ? acc : 1);
-        b->h_slow.clear();
-        const unsigned nt = (n >= 65536) ? threads : 1;
-        if (nt <= 1) {
-            tokenize_range(b, 0, n, b->h_slow);
-        } else {
-            std::vector<std::vector<uint32_t>> slow(nt);
-            std::vector<std::thread> th;
-            for (unsigned i = 0; i < nt; ++i) {
-                const uint32_t lo = (uint32_t)((uint64_t)n * i / nt), hi = (uint32_t)((uint64_t)n * (i + 1) / nt);
-                th.emplace_back([this, b, lo, hi, &slow, i] { tokenize_range(b, lo, hi, slow[i]); });
-            }
-            for (auto& x : th) x.join();
-            for (auto& v : slow) b->h_slow.insert(b->h_slow.end(), v.begin(), v.end());
-        }
+        TokView v{b->bytes.data(), b->offs.data(), b->h_words.data(), b->h_toff.data(), b->h_tflags.data()};
+        tokenize_view(v, n, b->h_slow);
         b->dict_size = dict.size();
+        return TM_OK;
+    }
+
+    // tm_tokenize into caller arrays
+    int tokenize_into(const uint8_t* bytes, const uint64_t* offs, uint32_t n, uint32_t* words, uint64_t cap,
+                      uint32_t* toff, uint8_t* tflags, uint64_t* nwords) {
+        uint64_t acc = 0;
+        int rc = count_words(bytes, offs, n, toff, &acc);
+        if (rc) return rc;
+        *nwords = acc;
+        if (acc > cap) return TM_EOVERFLOW;
+        std::vector<uint32_t> slow;
+        TokView v{bytes, offs, words, toff, tflags};
+        tokenize_view(v, n, slow);
         return TM_OK;
     }
 
@@ -780,7 +853,76 @@ struct tm_engine {
         if (n) HIP_OK(hipMemcpyAsync(b->d_tflags, b->h_tflags.data(), n, hipMemcpyHostToDevice, stream));
         if (!b->h_slow.empty())
             HIP_OK(hipMemcpyAsync(b->d_slow, b->h_slow.data(), b->h_slow.size() * 4, hipMemcpyHostToDevice, stream));
-        // outputs
+        b->dev_slow = false;
+        return reserve_outputs(b);
+    }
+
+    // tm_batch_prepare_tokens: a batch from tokenised arrays (host or device)
+    int prepare_tokens(tm_batch* b, const uint32_t* words, const uint32_t* toff, const uint8_t* tflags, uint32_t n,
+                       uint64_t nwords, bool on_device) {
+        if (nwords > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        b->n = n;
+        b->nwords = nwords;
+        b->tokens_only = true;
+        b->launched = b->done = false;
+        b->bytes.clear();
+        b->offs.clear();
+        int rc;
+        if (!on_device) {
+            if (toff[0] != 0 || toff[n] != nwords) return TM_EINVAL;
+            b->h_slow.clear();
+            for (uint32_t t = 0; t < n; ++t) {
+                const uint8_t f = tflags[t];
+                if (toff[t + 1] < toff[t] || (f & ~(TF_DOLLAR | TF_SLOW))) return TM_EINVAL;
+                if (toff[t + 1] - toff[t] > FAST_MAX_DEPTH && !(f & TF_SLOW)) return TM_EINVAL;
+                if (f & TF_SLOW) b->h_slow.push_back(t);
+            }
+            b->h_words.assign(words, words + nwords);
+            if (b->h_words.empty()) b->h_words.push_back(0);
+            b->h_toff.assign(toff, toff + (size_t)n + 1);
+            b->h_tflags.assign(tflags, tflags + n);
+            if (device < 0) return TM_OK;
+            return upload_batch(b);
+        }
+        if (device < 0) return TM_ENODEV;
+        b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
+        if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(nwords, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
+        if ((rc = host_reserve(b->h_bad, b->ch_bad, 2))) return rc;
+        if (nwords) HIP_OK(hipMemcpyAsync(b->d_words, words, nwords * 4, hipMemcpyDeviceToDevice, stream));
+        HIP_OK(hipMemcpyAsync(b->d_toff, toff, ((size_t)n + 1) * 4, hipMemcpyDeviceToDevice, stream));
+        if (n) HIP_OK(hipMemcpyAsync(b->d_tflags, tflags, n, hipMemcpyDeviceToDevice, stream));
+        HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, stream));
+        // toff[0] and toff[n] checked with the rest: a walk must never read past words[]
+        HIP_OK(launch_token_check(b->d_toff, b->d_tflags, n, nwords, b->d_slow, b->d_nslow, b->d_nslow + 1, stream));
+        HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        if (b->h_bad[1] || (n == 0 && nwords != 0)) return TM_EINVAL;
+        if (n == 0) {   // no thread checked toff[0] == nwords == 0
+            uint32_t t0 = 0;
+            HIP_OK(hipMemcpy(&t0, b->d_toff, 4, hipMemcpyDeviceToHost));
+            if (t0 != 0) return TM_EINVAL;
+        }
+        b->dev_slow = true;
+        return reserve_outputs(b);
+    }
+
+    // tm_batch_export
+    int export_batch(tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
+        if (!b->done) return TM_EINVAL;
+        const uint64_t top = (uint64_t)(n_parent.size() ? n_parent.size() - 1 : 0) * mul + add;
+        if (top > 0xFFFFFFFFull) return TM_EOVERFLOW;
+        HIP_OK(launch_export(b->d_rowoff, b->d_ids, b->n, b->total, d_counts, d_ids, mul, add, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        return TM_OK;
+    }
+
+    int reserve_outputs(tm_batch* b) {
+        int rc;
+        const uint32_t n = b->n;
         const size_t nn = std::max<size_t>(n, 1);
         if ((rc = dev_reserve(b->d_count, b->c_count, nn))) return rc;
         if ((rc = dev_reserve(b->d_src, b->c_src, nn))) return rc;
@@ -821,6 +963,7 @@ struct tm_engine {
         for (auto& o : b->offs) o -= base;
         b->bytes.assign(topics + base, topics + base + b->offs[n]);
         b->launched = b->done = false;
+        b->tokens_only = false;
         int rc = tokenize(b);
         if (rc) return rc;
         if (device < 0) return TM_OK;
@@ -830,7 +973,7 @@ struct tm_engine {
     int launch(tm_batch* b) {
         if (device < 0) return TM_ENODEV;
         int rc;
-        if (b->dict_size != dict.size()) {   // new words since tokenisation
+        if (!b->tokens_only && b->dict_size != dict.size()) {   // new words since tokenisation
             if ((rc = tokenize(b))) return rc;
             if ((rc = upload_batch(b))) return rc;
         }
@@ -850,7 +993,8 @@ struct tm_engine {
         a.root = root_rec();
         a.foff = d_foff; a.flen = d_flen; a.fbytes = d_fbytes;
         a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
-        a.slow_list = b->d_slow; a.n_slow = (uint32_t)b->h_slow.size();
+        a.slow_list = b->d_slow; a.n_slow = b->dev_slow ? 0u : (uint32_t)b->h_slow.size();
+        a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
         a.grid = match_waves(b->n, device);
         if ((uint64_t)a.grid * 64 * row_cap > b->c_rows) {
@@ -863,7 +1007,7 @@ struct tm_engine {
         a.s_qparent = d_sqpar; a.s_qpw = d_sqpw; a.s_qmeta = d_sqmeta; a.s_qkey = d_sqkey;
         a.s_ofid = d_sofid; a.s_okey = d_sokey;
         a.s_qcap = s_qcap; a.s_ocap = s_ocap; a.s_waves = s_waves;
-        a.nwords = (uint32_t)b->h_words.size();
+        a.nwords = (uint32_t)std::max<uint64_t>(b->nwords, 1);
         a.nslots = (uint32_t)slots.size();
         a.nnodes = (uint32_t)n_parent.size();
         a.nfbytes = fbytes.size();
@@ -965,6 +1109,7 @@ struct tm_engine {
 
     int init(const tm_config* cfg) {
         device = cfg ? cfg->device : -1;
+        frozen = cfg && (cfg->flags & TM_CFG_FROZEN_DICT);
         const char* ck = getenv("TM_CHECKED");
         checked = ck && ck[0] == '1';
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
@@ -1063,7 +1208,7 @@ extern "C" {
 
 int tm_create(const tm_config* cfg, tm_engine** out) {
     if (!out) return TM_EINVAL;
-    if (cfg && cfg->flags) return TM_EINVAL;
+    if (cfg && (cfg->flags & ~TM_CFG_FROZEN_DICT)) return TM_EINVAL;
     tm_engine* e = new (std::nothrow) tm_engine();
     if (!e) return TM_ENOMEM;
     int rc = e->init(cfg);
@@ -1250,6 +1395,107 @@ void tm_batch_free(tm_engine* e, tm_batch* b) {
         b->release();
     }
     delete b;
+}
+
+int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n, uint32_t shard,
+                        uint32_t nshards, uint64_t* n_inserted) {
+    if (!e || !offsets || (!filters && n)) return TM_EINVAL;
+    if (nshards > 1 && shard >= nshards) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    uint64_t done = 0;
+    int rc = TM_OK;
+    try {
+        for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
+            const uint8_t* f = filters + offsets[i];
+            const size_t len = offsets[i + 1] - offsets[i];
+            if (offsets[i + 1] < offsets[i]) { rc = TM_EINVAL; break; }
+            if (nshards > 1) {
+                const int s = e->filter_shard(f, len, nshards);
+                if (s < 0) { rc = s; break; }
+                if ((uint32_t)s != shard && (uint32_t)s != nshards) continue;
+            }
+            rc = e->trie_insert(f, len);
+            if (rc == TM_OK) ++done;
+        }
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
+    if (n_inserted) *n_inserted = done;
+    return rc;
+}
+
+int tm_dict_load(tm_engine* e, const uint8_t* words, const uint64_t* offsets, uint32_t n) {
+    if (!e || !offsets || (!words && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->dict_load(words, offsets, n);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_filter_shard(tm_engine* e, const uint8_t* filter, size_t len, uint32_t nshards) {
+    if (!e || (!filter && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    return e->filter_shard(filter, len, nshards);
+}
+
+int tm_tokenize(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* words,
+                uint64_t words_cap, uint32_t* toff, uint8_t* tflags, uint64_t* nwords_out) {
+    if (!e || !offsets || !toff || !nwords_out || (!topics && n) || (!tflags && n) || (!words && words_cap))
+        return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->tokenize_into(topics, offsets, n, words, words_cap, toff, tflags, nwords_out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t* toff, const uint8_t* tflags,
+                            uint32_t n, uint64_t nwords, int on_device, tm_batch** out) {
+    if (!e || !out || !toff || (!tflags && n) || (!words && nwords)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (on_device) {
+        int rc = e->set_device();
+        if (rc) return rc;
+    }
+    const bool fresh = *out == nullptr;   // a non-NULL *out is reused (its buffers only grow)
+    tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *out;
+    if (!b) return TM_ENOMEM;
+    int rc;
+    try {
+        rc = e->prepare_tokens(b, words, toff, tflags, n, nwords, on_device != 0);
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
+    if (rc) {
+        if (fresh) { b->release(); delete b; }
+        else b->launched = b->done = false;
+        return rc;
+    }
+    if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
+    *out = b;
+    return TM_OK;
+}
+
+int tm_tokens_shard(tm_engine* e, const uint32_t* d_words, const uint32_t* d_toff, uint32_t n, uint32_t nshards,
+                    uint32_t* d_shard) {
+    if (!e || !d_toff || nshards == 0 || (n && (!d_words || !d_shard))) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    HIP_OK(launch_tokens_shard(d_words, d_toff, n, nshards, d_shard, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return TM_OK;
+}
+
+int tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
+    if (!e || !b || (!d_counts && b->n) || (!d_ids && b->total)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    return e->export_batch(b, d_counts, d_ids, mul, add);
 }
 
 const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {

@@ -246,3 +246,117 @@ EXPORT int tm_gen_topics(const tm_gen_params* p, const tm_strs* filters, uint64_
     out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
     return 0;
 }
+
+/* ---- C4: IoT filters and publishes ------------------------
+ *
+ * Filter i of n_filters is a pure function of (seed, i), so any index range can
+ * be generated on its own, and the filters are distinct by construction:
+ *   i <  0.7 F : device/d<id>/sensor/s<s>/#     (id, s) = perm(i) over ids x sensors
+ *   i <  0.9 F : device/d<id>/+/m<m>            (id, m) = perm(i - 0.7F) over ids x metrics
+ *   otherwise  : +/d<id>/sensor/+/#             id = perm(i - 0.9F) over ids   (replicated)
+ * Publishes: device/d<id>/sensor/s<s>/m<m>, or device/d<id>/status/m<m> with
+ * probability p_status; id ~ Zipf(zipf_s) over the ids.
+ */
+typedef struct {
+    uint64_t seed;
+    uint64_t n_filters;
+    uint32_t n_ids;
+    uint32_t n_sensors;
+    uint32_t n_metrics;
+    uint32_t pad;
+    double   zipf_s;
+    double   p_status;
+} tm_iot_params;
+
+/* bijection of [0, space) (cycle-walking a bijective mixer of [0, 2^k)) */
+static uint64_t iot_perm(uint64_t j, uint64_t space, uint64_t seed) {
+    uint32_t k = 1;
+    while ((1ull << k) < space) k++;
+    const uint64_t mask = (1ull << k) - 1;
+    const uint64_t c = (seed * 2 + 1) & mask;
+    uint64_t x = j;
+    do {
+        x = (x * 0x9E3779B97F4A7C15ull + c) & mask;
+        x ^= x >> (k / 2 + 1);
+        x = (x * 0xBF58476D1CE4E5B9ull) & mask;
+        x ^= x >> (k / 2 + 1);
+    } while (x >= space);
+    return x;
+}
+
+EXPORT int tm_gen_iot_vocab(const tm_iot_params* p, tm_strs* out) {
+    sbuf o = {0};
+    uint64_t n = 3ull + p->n_ids + p->n_sensors + p->n_metrics;
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    uint64_t k = 0;
+    char w[32];
+    offs[0] = 0;
+    sb_put(&o, "device", 6); offs[++k] = o.n;
+    sb_put(&o, "sensor", 6); offs[++k] = o.n;
+    sb_put(&o, "status", 6); offs[++k] = o.n;
+    for (uint32_t i = 0; i < p->n_ids; i++) { int l = snprintf(w, sizeof(w), "d%u", i); sb_put(&o, w, (size_t)l); offs[++k] = o.n; }
+    for (uint32_t i = 0; i < p->n_sensors; i++) { int l = snprintf(w, sizeof(w), "s%u", i); sb_put(&o, w, (size_t)l); offs[++k] = o.n; }
+    for (uint32_t i = 0; i < p->n_metrics; i++) { int l = snprintf(w, sizeof(w), "m%u", i); sb_put(&o, w, (size_t)l); offs[++k] = o.n; }
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
+    return 0;
+}
+
+EXPORT int tm_gen_iot_filters(const tm_iot_params* p, uint64_t lo, uint64_t hi, tm_strs* out) {
+    const uint64_t F = p->n_filters;
+    const uint64_t fa = F * 7 / 10, fb = F * 9 / 10;
+    if (hi > F || lo > hi) return -1;
+    if (fa > (uint64_t)p->n_ids * p->n_sensors || fb - fa > (uint64_t)p->n_ids * p->n_metrics || F - fb > p->n_ids)
+        return -1;
+    sbuf o = {0};
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (hi - lo + 1));
+    offs[0] = 0;
+    char w[96];
+    for (uint64_t i = lo; i < hi; i++) {
+        int l;
+        if (i < fa) {
+            const uint64_t key = iot_perm(i, (uint64_t)p->n_ids * p->n_sensors, p->seed);
+            l = snprintf(w, sizeof(w), "device/d%u/sensor/s%u/#", (unsigned)(key / p->n_sensors), (unsigned)(key % p->n_sensors));
+        } else if (i < fb) {
+            const uint64_t key = iot_perm(i - fa, (uint64_t)p->n_ids * p->n_metrics, p->seed + 1);
+            l = snprintf(w, sizeof(w), "device/d%u/+/m%u", (unsigned)(key / p->n_metrics), (unsigned)(key % p->n_metrics));
+        } else {
+            const uint64_t id = iot_perm(i - fb, p->n_ids, p->seed + 2);
+            l = snprintf(w, sizeof(w), "+/d%u/sensor/+/#", (unsigned)id);
+        }
+        sb_put(&o, w, (size_t)l);
+        offs[i - lo + 1] = o.n;
+    }
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = hi - lo;
+    return 0;
+}
+
+EXPORT int tm_gen_iot_topics(const tm_iot_params* p, uint64_t tseed, uint64_t n, tm_strs* out) {
+    /* Zipf over the ids: CDF table, binary search per draw */
+    double* cdf = (double*)malloc(sizeof(double) * p->n_ids);
+    double acc = 0;
+    for (uint32_t k = 0; k < p->n_ids; k++) { acc += pow((double)(k + 1), -p->zipf_s); cdf[k] = acc; }
+    for (uint32_t k = 0; k < p->n_ids; k++) cdf[k] /= acc;
+    uint64_t s = tseed;
+    sbuf o = {0};
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    offs[0] = 0;
+    char w[96];
+    for (uint64_t t = 0; t < n; t++) {
+        const double u = sm_u01(&s);
+        uint32_t lo = 0, hi = p->n_ids - 1;
+        while (lo < hi) { uint32_t mid = (lo + hi) / 2; if (u < cdf[mid]) hi = mid; else lo = mid + 1; }
+        const uint32_t id = lo;
+        int l;
+        if (sm_u01(&s) < p->p_status)
+            l = snprintf(w, sizeof(w), "device/d%u/status/m%u", id, (unsigned)sm_below(&s, p->n_metrics));
+        else {
+            const unsigned sn = (unsigned)sm_below(&s, p->n_sensors);
+            l = snprintf(w, sizeof(w), "device/d%u/sensor/s%u/m%u", id, sn, (unsigned)sm_below(&s, p->n_metrics));
+        }
+        sb_put(&o, w, (size_t)l);
+        offs[t + 1] = o.n;
+    }
+    free(cdf);
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
+    return 0;
+}

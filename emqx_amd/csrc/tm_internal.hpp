@@ -114,6 +114,7 @@ struct MatchArgs {
     uint32_t n;
     const uint32_t* slow_list;  // host-flagged slow topics
     uint32_t n_slow;
+    const uint32_t* d_nslow;    // device-resident count of slow_list (token batches), or null
     // outputs
     uint32_t* count;          // per topic |M(t)|
     unsigned long long* src;  // per topic: offset of its sorted row in sfids[]
@@ -168,6 +169,18 @@ hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* va
 hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx,
                                 const uint64_t* off, const uint32_t* len, uint32_t n, hipStream_t s);
 uint32_t scan_block_count(uint32_t n);
+// token batches (filter-sharded mode)
+hipError_t launch_token_check(const uint32_t* toff, const uint8_t* tflags, uint32_t n, uint64_t nwords,
+                              uint32_t* slow_list, uint32_t* d_nslow, uint32_t* d_bad, hipStream_t s);
+hipError_t launch_tokens_shard(const uint32_t* words, const uint32_t* toff, uint32_t n, uint32_t nshards,
+                               uint32_t* shard, hipStream_t s);
+hipError_t launch_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
+                         uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add, hipStream_t s);
+
+// shard of a (w0, w1) literal prefix; host and device agree (tm_filter_shard)
+__host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uint32_t nshards) {
+    return edge_hash(id0, id1) % nshards;
+}
 // workgroups (one wave each) of tm_match_tiles for n topics on this device:
 // min(tiles, resident capacity), so that every wave is resident from the start
 uint32_t match_waves(uint32_t n, int device);

@@ -583,12 +583,13 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
     uint32_t* ofid = a.s_ofid + (size_t)wave * a.s_ocap;
     unsigned long long* okey = a.s_okey + (size_t)wave * a.s_ocap;
     const uint32_t novf = min(a.ctrl[CTRL_NOVF], a.ovf_cap);
-    const uint32_t total_items = a.n_slow + novf;
+    const uint32_t n_slow = a.d_nslow ? min(*a.d_nslow, a.n) : a.n_slow;
+    const uint32_t total_items = n_slow + novf;
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sS = 0;
 
     for (uint32_t item = wave; item < total_items; item += gridDim.x) {
-        uint32_t t = (item < a.n_slow) ? a.slow_list[CK_(item, a.n_slow, 24)]
-                                       : a.ovf_list[CK_(item - a.n_slow, a.ovf_cap, 25)];
+        uint32_t t = (item < n_slow) ? a.slow_list[CK_(item, n_slow, 24)]
+                                     : a.ovf_list[CK_(item - n_slow, a.ovf_cap, 25)];
         t = CK_(t, a.n, 26);
         const uint8_t fl = a.tflags[t];
         const bool dollar = fl & TF_DOLLAR;
@@ -829,6 +830,61 @@ __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
     }
 }
 
+// ------------------------------------------------ token batches (sharded mode)
+
+// Validates a device-resident token batch before any walk reads it (toff
+// monotone from 0 to nwords, deep topics flagged for the generic path) and
+// compacts the generic-path topics into slow_list / *d_nslow.  Any violation
+// sets *d_bad; the host refuses the batch.
+__global__ __launch_bounds__(256) void tm_token_check(const uint32_t* toff, const uint8_t* tflags, uint32_t n,
+                                                       uint64_t nwords, uint32_t* slow_list, uint32_t* d_nslow,
+                                                       uint32_t* d_bad) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    bool slow = false;
+    if (t < n) {
+        const uint32_t b = toff[t], e = toff[t + 1];
+        const uint8_t f = tflags[t];
+        const bool ok = b <= e && (uint64_t)e <= nwords && (t > 0 || b == 0) && (t + 1 < n || (uint64_t)e == nwords) &&
+                        (f & ~(TF_DOLLAR | TF_SLOW)) == 0 && (e - b <= FAST_MAX_DEPTH || (f & TF_SLOW));
+        if (!ok) atomicOr(d_bad, 1u);
+        slow = ok && (f & TF_SLOW);
+    }
+    const uint64_t m = __ballot(slow);
+    if (!m) return;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(d_nslow, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    if (slow) slow_list[base + prefix_count(m)] = t;
+}
+
+// Shard of each topic (tm_filter_shard's rule on the topic side): the shard of
+// its first two words when both are interned literals, else nshards (every
+// shard resolves it: only replicated filters can match).
+__global__ __launch_bounds__(256) void tm_tokens_shard(const uint32_t* words, const uint32_t* toff, uint32_t n,
+                                                        uint32_t nshards, uint32_t* shard) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t b = toff[t], d = toff[t + 1] - b;
+    uint32_t s = nshards;
+    if (d >= 2) {
+        const uint32_t i0 = words[b] & WID_MASK, i1 = words[b + 1] & WID_MASK;
+        const bool lit0 = i0 != W_UNKNOWN && i0 != W_PLUS && i0 != W_HASH;
+        const bool lit1 = i1 != W_UNKNOWN && i1 != W_PLUS && i1 != W_HASH;
+        if (lit0 && lit1) s = prefix_shard(i0, i1, nshards);
+    }
+    shard[t] = s;
+}
+
+// counts[t] = |row t|; gids[i] = ids[i] * mul + add (a shard's global ids).
+__global__ __launch_bounds__(256) void tm_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
+                                                  uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) gids[i] = ids[i] * mul + add;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) counts[i] = row_off[i + 1] - row_off[i];
+}
+
 __global__ void tm_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) slots[idx[i]] = vals[i];
@@ -894,6 +950,29 @@ hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
     const uint32_t grid = min(ntiles, 256u * 32u);   // 8 waves per SIMD
     if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(64), 0, s, a);
     else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_token_check(const uint32_t* toff, const uint8_t* tflags, uint32_t n, uint64_t nwords,
+                              uint32_t* slow_list, uint32_t* d_nslow, uint32_t* d_bad, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_token_check, dim3((n + 255) / 256), dim3(256), 0, s, toff, tflags, n, nwords,
+                              slow_list, d_nslow, d_bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_tokens_shard(const uint32_t* words, const uint32_t* toff, uint32_t n, uint32_t nshards,
+                               uint32_t* shard, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_tokens_shard, dim3((n + 255) / 256), dim3(256), 0, s, words, toff, n, nshards, shard);
+    return hipGetLastError();
+}
+
+hipError_t launch_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
+                         uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add, hipStream_t s) {
+    const uint64_t work = total > n ? total : n;
+    if (!work) return hipGetLastError();
+    const uint64_t blocks = (work + 255) / 256;
+    const uint32_t grid = (uint32_t)(blocks < 4096u ? blocks : 4096u);
+    hipLaunchKernelGGL(tm_export, dim3(grid), dim3(256), 0, s, row_off, ids, n, total, counts, gids, mul, add);
     return hipGetLastError();
 }
 

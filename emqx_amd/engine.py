@@ -22,11 +22,30 @@ def _pack(topics) -> Strings:
     return Strings.from_list(list(topics))
 
 
+class Tokens:
+    """Tokenised publishes (tm_tokenize layout): words u32 = class << 29 | word id,
+    toff u32[n+1], tflags u8[n]."""
+
+    def __init__(self, words: np.ndarray, toff: np.ndarray, tflags: np.ndarray):
+        self.words, self.toff, self.tflags = words, toff, tflags
+
+    def __len__(self):
+        return len(self.toff) - 1
+
+    @property
+    def nwords(self) -> int:
+        return int(self.toff[-1])
+
+
 class Batch:
     """A device-resident publish batch (tm_batch_prepare / launch / wait / result)."""
 
-    def __init__(self, eng: "Engine", topics):
+    def __init__(self, eng: "Engine", topics=None, handle=None, n=0):
         self.eng = eng
+        if handle is not None:          # built by Engine.prepare_tokens
+            self.h = handle
+            self.n = n
+            return
         s = _pack(topics)
         self.n = len(s)
         buf = s.buf if s.buf.size else np.zeros(1, np.uint8)
@@ -36,6 +55,10 @@ class Batch:
         N.check(eng.L.tm_batch_prepare(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
                                        C.byref(h)), "tm_batch_prepare")
         self.h = h
+
+    def export(self, d_counts: int, d_ids: int, mul: int = 1, add: int = 0):
+        """Per-topic counts and ids*mul+add into caller device buffers (tm_batch_export)."""
+        N.check(self.eng.L.tm_batch_export(self.eng.h, self.h, d_counts, d_ids, mul, add), "tm_batch_export")
 
     def launch(self):
         N.check(self.eng.L.tm_batch_launch(self.eng.h, self.h), "tm_batch_launch")
@@ -82,9 +105,9 @@ def _result_arrays(r: N.Result):
 
 
 class Engine:
-    def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0):
+    def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0, frozen_dict: bool = False):
         self.L = N.lib()
-        cfg = N.Config(device, init_slots, host_threads, 0)
+        cfg = N.Config(device, init_slots, host_threads, N.TM_CFG_FROZEN_DICT if frozen_dict else 0)
         h = C.c_void_p()
         N.check(self.L.tm_create(C.byref(cfg), C.byref(h)), "tm_create")
         self.h = h
@@ -147,6 +170,62 @@ class Engine:
 
     def prepare(self, topics) -> Batch:
         return Batch(self, topics)
+
+    # ---- bulk load / filter-sharded mode -----------------------------------
+    def insert_many(self, filters, shard: int = 0, nshards: int = 1) -> int:
+        """emqx_trie:insert/1 over a filter list; with nshards > 1 only this
+        shard's filters and the replicated ones.  Returns how many were inserted."""
+        s = _pack(filters)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        done = C.c_uint64()
+        N.check(self.L.tm_trie_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), shard, nshards,
+                                           C.byref(done)), "tm_trie_insert_many")
+        return int(done.value)
+
+    def dict_load(self, words):
+        s = _pack(words)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        N.check(self.L.tm_dict_load(self.h, buf.ctypes.data, offs.ctypes.data, len(s)), "tm_dict_load")
+
+    def filter_shard(self, f: bytes, nshards: int) -> int:
+        return N.check(self.L.tm_filter_shard(self.h, f, len(f), nshards), "tm_filter_shard")
+
+    def tokenize(self, topics) -> Tokens:
+        s = _pack(topics)
+        n = len(s)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        cap = int(n + np.count_nonzero(s.buf == ord("/"))) if n else 0
+        words = np.zeros(max(cap, 1), np.uint32)
+        toff = np.zeros(n + 1, np.uint32)
+        tflags = np.zeros(max(n, 1), np.uint8)
+        nw = C.c_uint64()
+        N.check(self.L.tm_tokenize(self.h, buf.ctypes.data, offs.ctypes.data, n, words.ctypes.data, cap,
+                                   toff.ctypes.data, tflags.ctypes.data, C.byref(nw)), "tm_tokenize")
+        return Tokens(words[:nw.value], toff, tflags[:n])
+
+    def prepare_tokens(self, words: int, toff: int, tflags: int, n: int, nwords: int, on_device: bool,
+                       batch: Batch = None) -> Batch:
+        """A batch from tokenised arrays given as raw pointers (device pointers when
+        on_device, e.g. torch tensors' data_ptr()); `batch` is re-prepared in place."""
+        h = C.c_void_p(batch.h.value if batch is not None else None)
+        N.check(self.L.tm_batch_prepare_tokens(self.h, words, toff, tflags, n, nwords, int(on_device), C.byref(h)),
+                "tm_batch_prepare_tokens")
+        if batch is not None:
+            batch.n = n
+            return batch
+        return Batch(self, handle=h, n=n)
+
+    def prepare_tokens_host(self, tok: Tokens, batch: Batch = None) -> Batch:
+        w = np.ascontiguousarray(tok.words if len(tok.words) else np.zeros(1, np.uint32))
+        t = np.ascontiguousarray(tok.toff)
+        f = np.ascontiguousarray(tok.tflags if len(tok.tflags) else np.zeros(1, np.uint8))
+        return self.prepare_tokens(w.ctypes.data, t.ctypes.data, f.ctypes.data, len(tok), tok.nwords, False, batch)
+
+    def tokens_shard(self, d_words: int, d_toff: int, n: int, nshards: int, d_shard: int):
+        N.check(self.L.tm_tokens_shard(self.h, d_words, d_toff, n, nshards, d_shard), "tm_tokens_shard")
 
     # ---- filters -----------------------------------------------------------
     def filter_bytes(self, fid: int) -> bytes:

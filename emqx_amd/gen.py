@@ -281,3 +281,63 @@ def py_gen_topics(p: Params, filters, tseed: int, n: int):
             t = b"/".join(ws)
         out.append(t)
     return out
+
+
+# ---------------------------------------------------------------- C4 (IoT)
+
+@dataclass
+class IotParams:
+    """Mirrors tm_iot_params (csrc/tm_gen.c): SURVEY.md §8d config C4."""
+    seed: int = 4
+    n_filters: int = 100_000_000
+    n_ids: int = 10_000_000
+    n_sensors: int = 16
+    n_metrics: int = 8
+    zipf_s: float = 1.05
+    p_status: float = 0.2
+
+
+C4 = IotParams()
+
+
+class _CIot(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_filters", C.c_uint64), ("n_ids", C.c_uint32), ("n_sensors", C.c_uint32),
+                ("n_metrics", C.c_uint32), ("pad", C.c_uint32), ("zipf_s", C.c_double), ("p_status", C.c_double)]
+
+
+def _ciot(p: IotParams) -> _CIot:
+    return _CIot(p.seed, p.n_filters, p.n_ids, p.n_sensors, p.n_metrics, 0, p.zipf_s, p.p_status)
+
+
+def _iot_lib():
+    L = _lib()
+    if not getattr(L, "_iot_bound", False):
+        L.tm_gen_iot_vocab.argtypes = [C.POINTER(_CIot), C.POINTER(_CStrs)]
+        L.tm_gen_iot_filters.argtypes = [C.POINTER(_CIot), C.c_uint64, C.c_uint64, C.POINTER(_CStrs)]
+        L.tm_gen_iot_topics.argtypes = [C.POINTER(_CIot), C.c_uint64, C.c_uint64, C.POINTER(_CStrs)]
+        L._iot_bound = True
+    return L
+
+
+def gen_iot_vocab(p: IotParams) -> Strings:
+    """The shared word dictionary of the sharded mode, in canonical order."""
+    cs = _CStrs()
+    cp = _ciot(p)
+    _iot_lib().tm_gen_iot_vocab(C.byref(cp), C.byref(cs))
+    return _take(cs)
+
+
+def gen_iot_filters(p: IotParams, lo: int = 0, hi: int = None) -> Strings:
+    hi = p.n_filters if hi is None else hi
+    cs = _CStrs()
+    cp = _ciot(p)
+    if _iot_lib().tm_gen_iot_filters(C.byref(cp), lo, hi, C.byref(cs)) != 0:
+        raise ValueError("IoT filter counts exceed the id/sensor/metric spaces")
+    return _take(cs)
+
+
+def gen_iot_topics(p: IotParams, tseed: int, n: int) -> Strings:
+    cs = _CStrs()
+    cp = _ciot(p)
+    _iot_lib().tm_gen_iot_topics(C.byref(cp), tseed, n, C.byref(cs))
+    return _take(cs)

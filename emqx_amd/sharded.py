@@ -1,0 +1,196 @@
+"""Filter-sharded mode (BASELINE config C4).
+
+Subscription sets too large to replicate are partitioned over the G GPUs of a
+node, one process (and one engine) per GPU:
+
+* A filter whose first two levels are literal words lives on the shard
+  hash(id(w0), id(w1)) mod G (`tm_filter_shard`); every other filter ('+'/'#'
+  in level 0 or 1, or a single level) is replicated on all shards.
+* A publish whose first two words are interned literals can only be matched by
+  filters of that same shard or by replicated ones -- literal levels must be
+  equal -- so the owner shard resolves it completely: no merge of partial match
+  lists, and rows stay bit-exact (sorted, deduplicated).  Any other publish is
+  resolved by the rank it arrived on.  This is the "partition by leading words,
+  replicate root-wildcard filters" variant of SURVEY.md §8e.
+* Word ids must mean the same on every shard: the engines run with a frozen
+  dictionary (`TM_CFG_FROZEN_DICT`) loaded identically everywhere
+  (`tm_dict_load`), so tokenised batches can be exchanged as u32 arrays.
+
+One step over a rank's device-resident tokenised batch:
+  1. owner per topic on the device (`tm_tokens_shard`);
+  2. topics grouped by owner; `all_to_all_single` of the per-destination sizes,
+     the per-topic (depth << 2 | flags) words and the word ids (RCCL over xGMI);
+  3. the owner's engine matches what it received (HIP frontier kernel);
+  4. `all_to_all_single` back of the per-topic counts and the global filter ids
+     (gid = local filter id * G + owner rank, `tm_batch_export`);
+  5. rows restored to the publish order.
+Steps 2 and 4 are the only collectives; there is none in replicated mode.
+
+Reference: the filter set is the mnesia-replicated trie (src/emqx_trie.erl:53-74)
+that every node matches in full (src/emqx_router.erl:127-141); sharding it is new.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+from .engine import Batch, Engine
+
+META_SHIFT = 2            # meta = depth << 2 | tflags (TF_DOLLAR = 1, TF_SLOW = 2)
+
+
+def excl_cumsum(x: torch.Tensor) -> torch.Tensor:
+    out = torch.zeros_like(x)
+    if x.numel() > 1:
+        out[1:] = torch.cumsum(x[:-1], 0)
+    return out
+
+
+def gather_segments(src: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+    """concat(src[starts[i] : starts[i] + lens[i]] for i) with int64 index math."""
+    total = int(lens.sum().item()) if lens.numel() else 0
+    if total == 0:
+        return src[:0]
+    seg = torch.repeat_interleave(torch.arange(lens.numel(), device=lens.device), lens)
+    within = torch.arange(total, device=lens.device) - torch.repeat_interleave(excl_cumsum(lens), lens)
+    return src[starts[seg] + within]
+
+
+class ShardedMatcher:
+    """One rank of the filter-sharded engine.
+
+    engine:      this rank's Engine(frozen_dict=True) (a GPU engine in production).
+    shard_fn / local_match: injection points for the multi-process CPU tests only
+                 (gloo, no GPU); the production path uses the engine's HIP kernels and
+                 refuses to run without a device.
+    """
+
+    def __init__(self, engine: Engine, rank: int, world: int, group=None, device: Optional[torch.device] = None,
+                 shard_fn: Optional[Callable] = None, local_match: Optional[Callable] = None):
+        self.eng = engine
+        self.rank, self.world, self.group = rank, world, group
+        self.dev = device if device is not None else (
+            torch.device("cuda", engine.device) if engine.device >= 0 else torch.device("cpu"))
+        self._shard_fn = shard_fn
+        self._local_match = local_match
+        if engine.device < 0 and (shard_fn is None or local_match is None):
+            raise RuntimeError("filter-sharded matching needs a HIP device (no CPU fallback)")
+        self._batch: Optional[Batch] = None
+        self.last = {}
+        # gloo moves host tensors only: stage device tensors through host memory
+        # (used when several ranks share one GPU in tests); RCCL takes them as is
+        self._stage = (world > 1 and self.dev.type == "cuda" and dist.get_backend(group) == "gloo")
+
+    # ---- loading -----------------------------------------------------------
+    def load(self, vocab, filters) -> int:
+        """Shared dictionary, then this shard's filters + the replicated ones."""
+        self.eng.dict_load(vocab)
+        return self.eng.insert_many(filters, self.rank, self.world)
+
+    # ---- device pieces -------------------------------------------------------
+    def _shards(self, words: torch.Tensor, toff: torch.Tensor, n: int) -> torch.Tensor:
+        if self._shard_fn is not None:
+            return self._shard_fn(words, toff, n)
+        out = torch.empty(n, dtype=torch.int32, device=self.dev)
+        if n:
+            torch.cuda.current_stream(self.dev).synchronize()
+            self.eng.tokens_shard(words.data_ptr(), toff.data_ptr(), n, self.world, out.data_ptr())
+        return out
+
+    def _match(self, words: torch.Tensor, toff: torch.Tensor, tflags: torch.Tensor):
+        if self._local_match is not None:
+            return self._local_match(words, toff, tflags)
+        m = toff.numel() - 1
+        torch.cuda.current_stream(self.dev).synchronize()
+        self._batch = self.eng.prepare_tokens(words.data_ptr() if words.numel() else toff.data_ptr(),
+                                              toff.data_ptr(), tflags.data_ptr() if m else toff.data_ptr(),
+                                              m, int(words.numel()), True, self._batch)
+        self._batch.launch().wait()
+        st = self._batch.stats()
+        self.last["ms_match"] = st["ms_match"]
+        self.last["ms_total"] = st["ms_total"]
+        total = int(st["matches"])
+        counts = torch.empty(m, dtype=torch.int32, device=self.dev)
+        gids = torch.empty(total, dtype=torch.int32, device=self.dev)
+        self._batch.export(counts.data_ptr(), gids.data_ptr(), self.world, self.rank)
+        return counts, gids
+
+    def _a2a(self, x: torch.Tensor, send: list, recv: list) -> torch.Tensor:
+        out = torch.empty(sum(recv), dtype=x.dtype, device=x.device)
+        if self.world == 1:
+            out.copy_(x)
+            return out
+        if self._stage:
+            h = torch.empty(sum(recv), dtype=x.dtype)
+            dist.all_to_all_single(h, x.contiguous().cpu(), recv, send, group=self.group)
+            return h.to(x.device)
+        dist.all_to_all_single(out, x.contiguous(), recv, send, group=self.group)
+        return out
+
+    # ---- one step ------------------------------------------------------------
+    def step(self, words: torch.Tensor, toff: torch.Tensor, tflags: torch.Tensor):
+        """words int32 (u32 bits), toff int32 [n+1], tflags uint8 [n], all on this
+        rank's device.  Returns (row_off int64 [n+1], gids int32) in publish order:
+        row t = the sorted, deduplicated global ids of the filters matching topic t."""
+        G, dev = self.world, self.dev
+        n = toff.numel() - 1
+        shard = self._shards(words, toff, n).to(torch.int64)
+        owner = torch.where(shard == G, torch.full_like(shard, self.rank), shard)
+        order = torch.argsort(owner, stable=True)
+        depth = (toff[1:] - toff[:-1]).to(torch.int64)
+        depth_o = depth[order]
+        send_t = torch.bincount(owner, minlength=G)
+        send_w = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, owner, depth)
+        meta_o = ((depth_o << META_SHIFT) | tflags[order].to(torch.int64)).to(torch.int32)
+        words_o = gather_segments(words, toff[:-1].to(torch.int64)[order], depth_o)
+
+        sizes = torch.stack([send_t, send_w], 1)
+        if G > 1:
+            hs = sizes.cpu() if self._stage else sizes
+            rsizes = torch.empty_like(hs)
+            dist.all_to_all_single(rsizes, hs, group=self.group)
+        else:
+            rsizes = sizes
+        st, sw = send_t.tolist(), send_w.tolist()
+        rt, rw = rsizes[:, 0].tolist(), rsizes[:, 1].tolist()
+        r_meta = self._a2a(meta_o, st, rt)
+        r_words = self._a2a(words_o, sw, rw)
+
+        r_depth = (r_meta >> META_SHIFT).to(torch.int64)
+        r_toff = torch.zeros(r_meta.numel() + 1, dtype=torch.int32, device=dev)
+        if r_meta.numel():
+            r_toff[1:] = torch.cumsum(r_depth, 0).to(torch.int32)
+        r_flags = (r_meta & 3).to(torch.uint8)
+        counts, gids = self._match(r_words, r_toff, r_flags)
+
+        # back to the origins: counts per received topic, ids per source
+        src = torch.repeat_interleave(torch.arange(G, device=dev), torch.tensor(rt, device=dev))
+        back_g = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, src, counts.to(torch.int64))
+        counts_o = self._a2a(counts, rt, st)
+        c_o = counts_o.to(torch.int64)
+        recv_g = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, owner[order], c_o)
+        gids_o = self._a2a(gids, back_g.tolist(), recv_g.tolist())
+
+        # publish order
+        counts_orig = torch.empty(n, dtype=torch.int64, device=dev)
+        counts_orig[order] = c_o
+        inv = torch.empty_like(order)
+        inv[order] = torch.arange(n, device=dev)
+        row_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        if n:
+            row_off[1:] = torch.cumsum(counts_orig, 0)
+        gids_final = gather_segments(gids_o, excl_cumsum(c_o)[inv], counts_orig)
+        self.last.update(sent_topics=st, recv_topics=rt, local_matches=int(gids.numel()))
+        return row_off, gids_final
+
+    # ---- filter bytes of a global id ------------------------------------------
+    def owns(self, gid: int) -> bool:
+        return gid % self.world == self.rank
+
+    def filter_bytes(self, gid: int) -> bytes:
+        if not self.owns(gid):
+            raise KeyError(f"gid {gid} belongs to rank {gid % self.world}")
+        return self.eng.filter_bytes(gid // self.world)

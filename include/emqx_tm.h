@@ -52,8 +52,15 @@ typedef struct {
     int32_t  device;        /* HIP device ordinal; -1 = host-only engine (trie ops, no match) */
     uint32_t init_slots;    /* initial edge-hash capacity in 32-B slots (0 = default) */
     uint32_t host_threads;  /* threads for host tokenise+intern (0 = auto) */
-    uint32_t flags;         /* reserved, must be 0 */
+    uint32_t flags;         /* TM_CFG_* bits; unknown bits are rejected */
 } tm_config;
+
+/* Filter-sharded mode: the word dictionary is shared by every shard engine and
+ * grows only through tm_dict_load (called identically on every shard), so the
+ * u32 word ids of a tokenised topic mean the same on every GPU and tokenised
+ * publish batches can be exchanged between devices.  tm_trie_insert of a filter
+ * with a word outside the dictionary fails with TM_ENOENT. */
+#define TM_CFG_FROZEN_DICT 1u
 
 /* #trie_node{} view (include/emqx.hrl:98-103) */
 typedef struct {
@@ -143,6 +150,48 @@ TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
 TM_API int  tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row_offsets,
                          const uint32_t** d_ids, uint64_t* n_matches);
 TM_API void tm_batch_free(tm_engine* e, tm_batch* b);
+
+/* ---- bulk load + filter-sharded mode ------------------ */
+/* emqx_trie:insert/1 over n filters (filters = concatenated bytes, offsets[n+1]).
+ * nshards <= 1: every filter.  Otherwise only the filters whose
+ * tm_filter_shard() is `shard` or nshards (replicated); *n_inserted (may be
+ * NULL) counts them.  Stops at the first error. */
+TM_API int  tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets,
+                                uint32_t n, uint32_t shard, uint32_t nshards, uint64_t* n_inserted);
+/* Interns n words in order (the shared dictionary of the sharded mode).  Words
+ * must not contain '/'; '', "+" and "#" have fixed ids and are skipped. */
+TM_API int  tm_dict_load(tm_engine* e, const uint8_t* words, const uint64_t* offsets, uint32_t n);
+/* Shard of a filter among nshards: filters of >= 2 levels whose first two
+ * levels are literal words live on shard hash(id(w0), id(w1)) mod nshards; all
+ * others return nshards (replicated on every shard).  A publish whose first two
+ * words are known literals can only be matched by filters of its own shard or
+ * replicated ones, so one shard resolves it completely. */
+TM_API int  tm_filter_shard(tm_engine* e, const uint8_t* filter, size_t len, uint32_t nshards);
+/* Host tokenisation (emqx_topic:words/1 + interning): words[] = (class << 29 |
+ * word id) per level, toff[n+1] word offsets, tflags[n] (bit 0: '$' topic, bit
+ * 1: generic path).  *nwords_out = total words; TM_EOVERFLOW if > words_cap. */
+TM_API int  tm_tokenize(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                        uint32_t* words, uint64_t words_cap, uint32_t* toff, uint8_t* tflags,
+                        uint64_t* nwords_out);
+/* A batch from tokenised arrays (tm_tokenize layout).  on_device = 1: the
+ * pointers are device memory of this engine's GPU (e.g. received from another
+ * shard); they are copied (and validated on the device: TM_EINVAL for offsets
+ * that are not monotone from 0 to nwords or unflagged deep topics), so the
+ * caller may reuse them once this returns.  A non-NULL *out is re-prepared in
+ * place (its buffers only grow); NULL allocates a new batch. */
+TM_API int  tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t* toff,
+                                    const uint8_t* tflags, uint32_t n, uint64_t nwords, int on_device,
+                                    tm_batch** out);
+/* Device kernel: shard[t] = the shard owning tokenised topic t (tm_filter_shard's
+ * rule applied to its first two words), or nshards when any shard resolves it
+ * (only replicated filters can match).  Device pointers; returns when done. */
+TM_API int  tm_tokens_shard(tm_engine* e, const uint32_t* d_words, const uint32_t* d_toff, uint32_t n,
+                            uint32_t nshards, uint32_t* d_shard);
+/* Writes the batch's per-topic match counts and its filter ids mapped to
+ * id * mul + add (global ids of a shard) into caller device buffers
+ * (counts[n], ids[n_matches]) on the engine stream; returns when done. */
+TM_API int  tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_ids,
+                            uint32_t mul, uint32_t add);
 
 /* ---- filters ---------------------------------------------------------- */
 /* Bytes of a filter id returned by a match (the #trie_node.topic binary). */
