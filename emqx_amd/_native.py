@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libemqx_tm.so")
+LIB_PATH = os.environ.get("EMQX_TM_LIB") or os.path.join(HERE, "libemqx_tm.so")   # override: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "emqx_tm.h")
 
 TM_OK = 0
@@ -48,6 +48,11 @@ class TrieNode(C.Structure):
 class Result(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_matches", C.c_uint64),
                 ("row_offsets", C.POINTER(C.c_uint32)), ("filter_ids", C.POINTER(C.c_uint32))]
+
+
+class Routes(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_routes", C.c_uint64), ("row_offsets", C.POINTER(C.c_uint32)),
+                ("filter_ids", C.POINTER(C.c_uint32)), ("dests", C.POINTER(C.c_uint32))]
 
 
 class BatchStats(C.Structure):
@@ -90,6 +95,10 @@ SIGNATURES = {
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_free": (None, [P, P]),
+    "tm_route_add": (C.c_int, [P, U8P, SZ, C.c_uint32]),
+    "tm_route_delete": (C.c_int, [P, U8P, SZ, C.c_uint32]),
+    "tm_batch_routes": (C.c_int, [P, P, C.POINTER(Routes)]),
+    "tm_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
     "tm_trie_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
     "tm_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
     "tm_filter_shard": (C.c_int, [P, U8P, SZ, C.c_uint32]),

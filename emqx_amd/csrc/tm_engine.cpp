@@ -228,8 +228,18 @@ struct tm_batch {
     bool dev_slow = false;
     uint32_t *d_nslow = nullptr, *h_bad = nullptr;
     size_t c_nslow = 0, ch_bad = 0;
+    // route resolution (tm_batch_routes)
+    uint32_t *d_rcount = nullptr, *d_rrow = nullptr, *d_rbsums = nullptr, *d_rfid = nullptr, *d_rdest = nullptr;
+    uint32_t *d_rtotal = nullptr, *h_rtotal = nullptr, *h_rrow = nullptr, *h_rfid = nullptr, *h_rdest = nullptr;
+    size_t c_rcount = 0, c_rrow = 0, c_rbsums = 0, c_rfid = 0, c_rdest = 0, c_rtotal = 0;
+    size_t ch_rtotal = 0, ch_rrow = 0, ch_rfid = 0, ch_rdest = 0;
 
     void release() {
+        dev_free(d_rcount); dev_free(d_rrow); dev_free(d_rbsums); dev_free(d_rfid); dev_free(d_rdest); dev_free(d_rtotal);
+        for (uint32_t** h : {&h_rtotal, &h_rrow, &h_rfid, &h_rdest}) {
+            if (*h) (void)hipHostFree(*h);
+            *h = nullptr;
+        }
         dev_free(d_nslow);
         if (h_bad) (void)hipHostFree(h_bad);
         h_bad = nullptr;
@@ -318,12 +328,23 @@ struct tm_engine {
     bool frozen = false;           // TM_CFG_FROZEN_DICT: words only via tm_dict_load
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
+    uint32_t qcap = 384;           // LDS probe stack per wave, 384 or 512 (TM_QCAP); C2 tiles peak at ~340
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint32_t* d_dbg = nullptr;
     uint32_t* h_dbg = nullptr;
     size_t c_dbg = 0, ch_dbg = 0;
 
     tm_batch scratch;   // reused by tm_match_batch / tm_trie_match
+
+    // routes (the emqx_route bag, aggregated per destination by the caller):
+    // node id -> [(dest, count)] in first-added order; total routes per node
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> n_dests;
+    std::vector<uint32_t> n_nroutes;
+    bool routes_dirty = true;
+    uint64_t route_entries = 0;
+    uint32_t *d_roff = nullptr, *d_rdest = nullptr;
+    size_t c_roff = 0, c_rdest = 0;
+    std::vector<uint32_t> h_roff, h_rdest;
 
     // ------------------------------------------------------------ hash
     uint32_t nslots() const { return (uint32_t)slots.size(); }
@@ -439,6 +460,12 @@ struct tm_engine {
     }
 
     void kill_node(uint32_t id) {
+        if (id < n_dests.size() && !n_dests[id].empty()) {
+            route_entries -= n_dests[id].size();
+            n_dests[id].clear();
+            n_nroutes[id] = 0;
+            routes_dirty = true;
+        }
         n_live[id] = 0;
         n_topic[id] = 0;
         n_ec[id] = 0;
@@ -631,6 +658,131 @@ struct tm_engine {
             HIP_OK(hipEventSynchronize(ev_delta));
             delta_inflight = false;
         }
+        return TM_OK;
+    }
+
+    uint32_t node_of(const uint8_t* t, size_t len) {
+        static thread_local std::vector<uint32_t> ids;
+        if (!filter_words(t, len, false, ids)) return NONE;
+        const uint32_t n = walk(ids);
+        return (n != NONE && n_topic[n]) ? n : NONE;
+    }
+
+    // emqx_router:do_add_route/2 (src/emqx_router.erl:113-124, 229-234)
+    int route_add(const uint8_t* t, size_t len, uint32_t dest) {
+        uint32_t n = node_of(t, len);
+        if (n == NONE || n >= n_nroutes.size() || n_nroutes[n] == 0) {
+            int rc = trie_insert(t, len);     // first route: emqx_trie:insert/1 (idempotent)
+            if (rc) return rc;
+            n = node_of(t, len);
+            if (n == NONE) return TM_EIO;
+        }
+        if (n_dests.size() < n_parent.size()) {
+            n_dests.resize(n_parent.size());
+            n_nroutes.resize(n_parent.size(), 0);
+        }
+        auto& v = n_dests[n];
+        bool found = false;
+        for (auto& e : v)
+            if (e.first == dest) { ++e.second; found = true; break; }
+        if (!found) {
+            v.emplace_back(dest, 1u);
+            ++route_entries;
+            routes_dirty = true;
+        }
+        ++n_nroutes[n];
+        ++version;
+        return TM_OK;
+    }
+
+    // do_delete_route/2 (:163-169) + delete_trie_route/1 (:239-247)
+    int route_delete(const uint8_t* t, size_t len, uint32_t dest) {
+        const uint32_t n = node_of(t, len);
+        if (n == NONE || n >= n_dests.size()) return TM_ENOENT;
+        auto& v = n_dests[n];
+        size_t k = 0;
+        while (k < v.size() && v[k].first != dest) ++k;
+        if (k == v.size()) return TM_ENOENT;
+        if (--v[k].second == 0) {
+            v.erase(v.begin() + (long)k);
+            --route_entries;
+            routes_dirty = true;
+        }
+        --n_nroutes[n];
+        ++version;
+        if (n_nroutes[n] == 0) return trie_delete(t, len);   // last route: emqx_trie:delete/1
+        return TM_OK;
+    }
+
+    // dests CSR by node id -> HBM (rebuilt whole when routes changed)
+    int sync_routes() {
+        if (!routes_dirty && c_roff >= n_parent.size() + 1) return TM_OK;
+        const size_t nn = n_parent.size();
+        h_roff.assign(nn + 1, 0);
+        h_rdest.clear();
+        h_rdest.reserve(route_entries);
+        for (size_t i = 0; i < nn; ++i) {
+            h_roff[i] = (uint32_t)h_rdest.size();
+            if (i < n_dests.size())
+                for (const auto& e : n_dests[i]) h_rdest.push_back(e.first);
+        }
+        h_roff[nn] = (uint32_t)h_rdest.size();
+        int rc;
+        if ((rc = dev_reserve(d_roff, c_roff, nn + 1))) return rc;
+        if ((rc = dev_reserve(d_rdest, c_rdest, std::max<size_t>(h_rdest.size(), 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(d_roff, h_roff.data(), (nn + 1) * 4, hipMemcpyHostToDevice, stream));
+        if (!h_rdest.empty())
+            HIP_OK(hipMemcpyAsync(d_rdest, h_rdest.data(), h_rdest.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        routes_dirty = false;
+        return TM_OK;
+    }
+
+    // tm_batch_routes: route CSR of a waited batch, resolved on the device
+    int batch_routes(tm_batch* b, tm_routes* out) {
+        if (!b->done) return TM_EINVAL;
+        int rc;
+        if ((rc = sync_routes())) return rc;
+        const uint32_t n = b->n;
+        const size_t nn = std::max<size_t>(n, 1);
+        if ((rc = dev_reserve(b->d_rcount, b->c_rcount, nn))) return rc;
+        if ((rc = dev_reserve(b->d_rrow, b->c_rrow, nn + 1))) return rc;
+        if ((rc = dev_reserve(b->d_rbsums, b->c_rbsums, (size_t)scan_block_count(n) + 1))) return rc;
+        if ((rc = dev_reserve(b->d_rtotal, b->c_rtotal, 1))) return rc;
+        if ((rc = host_reserve(b->h_rtotal, b->ch_rtotal, 1))) return rc;
+        RouteArgs r{};
+        r.row_off = b->d_rowoff; r.ids = b->d_ids; r.n = n;
+        r.roff = d_roff; r.rdest = d_rdest; r.nnodes = (uint32_t)n_parent.size();
+        r.rcount = b->d_rcount; r.r_rowoff = b->d_rrow; r.bsums = b->d_rbsums;
+        HIP_OK(launch_route_count(r, stream));
+        ScanArgs sa{};
+        sa.count = b->d_rcount; sa.row_off = b->d_rrow; sa.block_sums = b->d_rbsums; sa.n = n;
+        HIP_OK(launch_scan(sa, stream, b->d_rtotal));
+        HIP_OK(hipMemcpyAsync(b->h_rtotal, b->d_rtotal, 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        const uint64_t total = b->h_rtotal[0];
+        if ((rc = dev_reserve(b->d_rfid, b->c_rfid, std::max<uint64_t>(total, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_rdest, b->c_rdest, std::max<uint64_t>(total, 1)))) return rc;
+        r.out_fid = b->d_rfid; r.out_dest = b->d_rdest; r.cap = total;
+        HIP_OK(launch_route_fill(r, stream));
+        if ((rc = host_reserve(b->h_rrow, b->ch_rrow, nn + 1))) return rc;
+        if ((rc = host_reserve(b->h_rfid, b->ch_rfid, std::max<uint64_t>(total, 1)))) return rc;
+        if ((rc = host_reserve(b->h_rdest, b->ch_rdest, std::max<uint64_t>(total, 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(b->h_rrow, b->d_rrow, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, stream));
+        if (total) {
+            HIP_OK(hipMemcpyAsync(b->h_rfid, b->d_rfid, total * 4, hipMemcpyDeviceToHost, stream));
+            HIP_OK(hipMemcpyAsync(b->h_rdest, b->d_rdest, total * 4, hipMemcpyDeviceToHost, stream));
+        }
+        HIP_OK(hipStreamSynchronize(stream));
+        if (b->h_rrow[n] != total) {
+            snprintf(last_error(), 512, "inconsistent route CSR: %u vs %llu", b->h_rrow[n], (unsigned long long)total);
+            return TM_EIO;
+        }
+        out->n_topics = n;
+        out->n_routes = total;
+        out->row_offsets = b->h_rrow;
+        out->filter_ids = b->h_rfid;
+        out->dests = b->h_rdest;
         return TM_OK;
     }
 
@@ -948,7 +1100,7 @@ struct tm_engine {
     // ids[] = the CSR.  sfids/ids start at 32 per topic and grow on demand.
     int reserve_rows(tm_batch* b) {
         int rc;
-        const uint64_t fast = std::max<uint64_t>((uint64_t)match_waves(b->n, device) * 64 * row_cap, 1);
+        const uint64_t fast = std::max<uint64_t>((uint64_t)match_waves(b->n, device, qcap) * 64 * row_cap, 1);
         if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
         if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
@@ -996,7 +1148,8 @@ struct tm_engine {
         a.slow_list = b->d_slow; a.n_slow = b->dev_slow ? 0u : (uint32_t)b->h_slow.size();
         a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
-        a.grid = match_waves(b->n, device);
+        a.grid = match_waves(b->n, device, qcap);
+        a.qcap = qcap;
         if ((uint64_t)a.grid * 64 * row_cap > b->c_rows) {
             snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
             return TM_EIO;
@@ -1113,6 +1266,7 @@ struct tm_engine {
         const char* ck = getenv("TM_CHECKED");
         checked = ck && ck[0] == '1';
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
+        if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         // root node id 0 (absent until the first add_path, like the reference)
@@ -1142,7 +1296,7 @@ struct tm_engine {
             dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
             dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
-            dev_free(d_sokey); dev_free(d_dbg);
+            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);
@@ -1395,6 +1549,53 @@ void tm_batch_free(tm_engine* e, tm_batch* b) {
         b->release();
     }
     delete b;
+}
+
+int tm_route_add(tm_engine* e, const uint8_t* topic, size_t len, uint32_t dest) {
+    if (!e || (!topic && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->route_add(topic, len, dest);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_route_delete(tm_engine* e, const uint8_t* topic, size_t len, uint32_t dest) {
+    if (!e || (!topic && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->route_delete(topic, len, dest);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_batch_routes(tm_engine* e, tm_batch* b, tm_routes* out) {
+    if (!e || !b || !out) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    try {
+        return e->batch_routes(b, out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_routes* out) {
+    if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    try {
+        if ((rc = e->prepare(&e->scratch, topics, offsets, n))) return rc;
+        if ((rc = e->launch(&e->scratch))) return rc;
+        if ((rc = e->wait(&e->scratch))) return rc;
+        return e->batch_routes(&e->scratch, out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
 }
 
 int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n, uint32_t shard,

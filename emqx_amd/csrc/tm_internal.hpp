@@ -122,6 +122,7 @@ struct MatchArgs {
                               // (path code | filter id), reused by every tile of the wave
     uint32_t row_cap;         // K: per-topic row slots on the fast path
     uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
+    uint32_t qcap;            // LDS probe-stack entries per wave (384 or 512)
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;
@@ -160,7 +161,25 @@ struct ScanArgs {
     uint32_t* dbg;
 };
 
+// Route resolution over a batch's match CSR (tm_batch_routes).
+struct RouteArgs {
+    const uint32_t* row_off;  // match CSR (n + 1) and filter ids
+    const uint32_t* ids;
+    uint32_t n;
+    const uint32_t* roff;     // per node id: dests roff[f] .. roff[f+1] (nnodes + 1)
+    const uint32_t* rdest;
+    uint32_t nnodes;
+    uint32_t* rcount;         // per topic: number of routes
+    uint32_t* r_rowoff;       // n + 1: route CSR offsets (block-local until tm_route_fill)
+    uint32_t* bsums;          // scan block sums
+    uint32_t* out_fid;        // route i: filter id, dest
+    uint32_t* out_dest;
+    uint64_t cap;             // capacity of out_fid / out_dest
+};
+
 // kernel launchers (tm_kernels.hip)
+hipError_t launch_route_count(const RouteArgs& a, hipStream_t s);
+hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked);
@@ -183,6 +202,6 @@ __host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uin
 }
 // workgroups (one wave each) of tm_match_tiles for n topics on this device:
 // min(tiles, resident capacity), so that every wave is resident from the start
-uint32_t match_waves(uint32_t n, int device);
+uint32_t match_waves(uint32_t n, int device, uint32_t qcap);
 
 }  // namespace etm

@@ -32,15 +32,20 @@
 namespace etm {
 
 constexpr int TILE = 64;
-constexpr int QCAP = 512;   // LDS probe stack entries per wave
 constexpr int WCAP = 512;   // LDS word cache per tile
+#ifndef TM_WPE384
+#define TM_WPE384 4         // waves/SIMD the 384-entry-stack kernel is register-allocated for
+#endif
 
-// queue/meta encoding (fast path): tl (6 bits) | lc << 6 (8 bits) | flags
+// queue/meta encoding (fast path): tl (6 bits) | lc << 6 (4 bits, lc <= FAST_MAX_DEPTH) | flags.
+// It rides in the low 31 bits of the probe's path-code key, which are zero
+// until a filter id is put there at emission.
 constexpr uint32_t M_LVL_SHIFT = 6;
-constexpr uint32_t M_LVL_MASK = 0xFF;
-constexpr uint32_t M_PLUS = 1u << 20;    // probe the '+' edge (else the literal word w[lc-1])
-constexpr uint32_t M_SKIPE = 1u << 21;   // don't emit the child's own topic (literal '#' dup)
-constexpr uint32_t M_DSTART = 1u << 22;  // $-rooted start probe: the node was already counted
+constexpr uint32_t M_LVL_MASK = 0xF;
+constexpr uint32_t M_PLUS = 1u << 10;    // probe the '+' edge (else the literal word w[lc-1])
+constexpr uint32_t M_SKIPE = 1u << 11;   // don't emit the child's own topic (literal '#' dup)
+constexpr uint32_t M_DSTART = 1u << 12;  // $-rooted start probe: the node was already counted
+static_assert(FAST_MAX_DEPTH <= (int)M_LVL_MASK, "level field too narrow");
 
 // digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
 //   L = literal branch, H = '#' terminal, P = '+' branch; E = 0, L_lo = 1.
@@ -186,17 +191,26 @@ __device__ __forceinline__ void expand_root(const RootRec& r, bool dollar, uint3
     if (!dollar && (r.flags & NF_PLUS)) add_p(x, (uint64_t)dig_P(cls) << 61, M_PLUS);
 }
 
+// Per-wave LDS of the tile kernel.  The probe stack holds QC 16-B entries
+// {key lo | meta, key hi, parent, word to probe (the literal w[lc-1] or
+// W_PLUS / W_HASH)}: one ds_write_b128 per push, one ds_read_b128 per pop.
+template <int QC>
 struct alignas(16) TileLds {
-    unsigned long long q_key[QCAP];
-    uint32_t q_parent[QCAP];
-    uint32_t q_meta[QCAP];
-    uint32_t q_pw[QCAP];       // word to probe: the literal w[lc-1] or W_PLUS / W_HASH
+    static constexpr int QCAP = QC;
+    uint4 q[QC];
     uint32_t words[WCAP];
     uint32_t toff[TILE];
     uint32_t depth[TILE];
     uint32_t cnt[TILE];
     uint32_t list[TILE];
+    // the stack and the word cache are free once a tile's frontier is empty: the
+    // epilogue reuses them as a staging area of STAGE u64
+    static constexpr uint32_t STAGE = (QC * 16 + WCAP * 4) / 8;
 };
+
+__device__ __forceinline__ uint4 q_pack(uint64_t key, uint32_t meta, uint32_t parent, uint32_t pw) {
+    return uint4{(uint32_t)key | meta, (uint32_t)(key >> 32), parent, pw};
+}
 
 // Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
 template <bool CK>
@@ -207,10 +221,10 @@ __device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t tl, uint32
     }
 }
 
-// The probe stack and the word cache are free once a tile's frontier is empty:
-// the epilogue reuses those 12 KB as a staging area of STAGE u64.
-constexpr uint32_t STAGE = (QCAP * 8 + QCAP * 12 + WCAP * 4) / 8;
-static_assert(offsetof(TileLds, words) + sizeof(uint32_t) * WCAP == STAGE * 8, "staging area must be contiguous");
+static_assert(offsetof(TileLds<512>, words) + sizeof(uint32_t) * WCAP == TileLds<512>::STAGE * 8,
+              "staging area must be contiguous");
+static_assert(offsetof(TileLds<384>, words) + sizeof(uint32_t) * WCAP == TileLds<384>::STAGE * 8,
+              "staging area must be contiguous");
 
 // Tile epilogue: sort the 64 rows of this wave and write their filter ids to
 // sfids[dst .. dst + c).  The rows are pulled into LDS a chunk of whole rows at
@@ -220,11 +234,12 @@ static_assert(offsetof(TileLds, words) + sizeof(uint32_t) * WCAP == STAGE * 8, "
 // of size class W (W/2 < c <= W, W = 2..64) are then packed 64/W per
 // wave-instruction, one element per lane, and sorted by a W-wide bitonic
 // network of __shfl_xor exchanges.  65..128 elements: rank count, two per lane.
-template <bool CK>
-__device__ __forceinline__ void sort_classes(const MatchArgs& a, TileLds& L, bool keep, uint32_t c, uint32_t pos,
+template <bool CK, class LT>
+__device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t pos,
                                              uint32_t dst) {
+    constexpr uint32_t STAGE = LT::STAGE;
     const uint32_t lane = threadIdx.x;
-    const unsigned long long* stg = reinterpret_cast<const unsigned long long*>(L.q_key);
+    const unsigned long long* stg = reinterpret_cast<const unsigned long long*>(L.q);
     if (keep && c == 1) a.sfids[CK_(dst, a.sfids_cap, 40)] = (uint32_t)(stg[CK_(pos, STAGE, 41)] & ~KEY_MASK);
 #pragma unroll
     for (uint32_t W = 2; W <= 64; W <<= 1) {
@@ -291,11 +306,13 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, TileLds& L, boo
 }
 
 // c <= row_cap <= 128 for every kept row, so a chunk always holds at least one row.
-template <bool CK>
-__device__ __forceinline__ void sort_rows(const MatchArgs& a, TileLds& L, bool keep, uint32_t c, uint32_t pos,
+template <bool CK, class LT>
+__device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t pos,
                                           uint32_t dst) {
+    constexpr uint32_t STAGE = LT::STAGE;
+    constexpr uint32_t RB = 8;   // rows per batch of independent loads
     const uint32_t lane = threadIdx.x;
-    unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q_key);
+    unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
     const uint64_t rbase = (uint64_t)blockIdx.x * TILE * a.row_cap;
     const uint64_t rlim = (uint64_t)gridDim.x * TILE * a.row_cap;
     uint32_t rs = 0;
@@ -303,11 +320,11 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, TileLds& L, bool k
         const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
         const uint64_t beyond = __ballot(lane >= rs && pos + c - p0 > STAGE);
         const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : (uint32_t)TILE;
-        for (uint32_t r0 = rs; r0 < re; r0 += 8) {
-            unsigned long long v0[8], v1[8];
-            uint32_t cr[8], pr[8];
+        for (uint32_t r0 = rs; r0 < re; r0 += RB) {
+            unsigned long long v0[RB], v1[RB];
+            uint32_t cr[RB], pr[RB];
 #pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < RB; ++u) {
                 const uint32_t r = (r0 + u) & (TILE - 1);
                 cr[u] = r0 + u < re ? __builtin_amdgcn_readlane(c, r) : 0u;
                 pr[u] = __builtin_amdgcn_readlane(pos, r) - p0;
@@ -316,13 +333,13 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, TileLds& L, bool k
                 v1[u] = lane + 64 < cr[u] ? a.rows[CK_(rb + lane + 64, rlim, 51)] : 0ull;
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < RB; ++u) {
                 if (lane < cr[u]) stg[CK_(pr[u] + lane, STAGE, 52)] = v0[u];
                 if (lane + 64 < cr[u]) stg[CK_(pr[u] + lane + 64, STAGE, 53)] = v1[u];
             }
         }
         __syncthreads();
-        sort_classes<CK>(a, L, keep && lane >= rs && lane < re, c, pos - p0, dst);
+        sort_classes<CK, LT>(a, L, keep && lane >= rs && lane < re, c, pos - p0, dst);
         __syncthreads();
         rs = re;
     }
@@ -344,8 +361,8 @@ __device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint
 // One tile.  IN_LDS: the tile's words are staged in LDS (the common case);
 // otherwise they are read from HBM.  Templated so word reads are plain ds_read
 // or global_load, never flat.
-template <bool CK, bool BIG, bool IN_LDS>
-__device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint32_t t0, uint32_t tend, uint32_t wbase,
+template <bool CK, bool BIG, bool IN_LDS, class LT>
+__device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t0, uint32_t tend, uint32_t wbase,
                                            uint8_t fl, bool valid, unsigned long long& sV, unsigned long long& sH,
                                            unsigned long long& sW, unsigned long long& sM) {
     const uint32_t lane = threadIdx.x;
@@ -376,16 +393,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
         const uint32_t pre = prefix_count(b0) + prefix_count(b1);
         const uint32_t meta = lane | (1u << M_LVL_SHIFT);
         const uint32_t wid = w0 & WID_MASK;
-        if (x.np >= 1) {
-            const uint32_t p = qn + pre;
-            L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf0; L.q_key[p] = x.pk0;
-            L.q_pw[p] = (x.pf0 & M_PLUS) ? W_PLUS : wid;
-        }
-        if (x.np >= 2) {
-            const uint32_t p = qn + pre + 1;
-            L.q_parent[p] = ROOT; L.q_meta[p] = meta | x.pf1; L.q_key[p] = x.pk1;
-            L.q_pw[p] = (x.pf1 & M_PLUS) ? W_PLUS : wid;
-        }
+        if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, meta | x.pf0, ROOT, (x.pf0 & M_PLUS) ? W_PLUS : wid);
+        if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, meta | x.pf1, ROOT, (x.pf1 & M_PLUS) ? W_PLUS : wid);
         qn += __popcll(b0) + __popcll(b1);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
@@ -398,41 +407,38 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         const uint32_t idx = qn - k + lane;
-        uint32_t parent = 0, meta = 0, pw = 0;
-        uint64_t key = 0;
-        if (has) { parent = L.q_parent[idx]; meta = L.q_meta[idx]; key = L.q_key[idx]; pw = L.q_pw[idx]; }
+        uint4 e = uint4{0u, 0u, 0u, 0u};
+        if (has) e = L.q[idx];
         qn -= k;
+        const uint32_t meta = e.x & 0x7FFFFFFFu;
+        const uint64_t key = ((uint64_t)e.y << 32) | (e.x & 0x80000000u);
+        const uint32_t parent = e.z, pw = e.w;
         const uint32_t tl = meta & 63;
         const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
+        // the topic's words are read before the probe's bucket arrives
+        uint32_t d = 0, w_here = 0, w_prev = 0;
+        if (has) {
+            const uint32_t base = L.toff[tl];
+            d = L.depth[tl];
+            w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
+            w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
+        }
         Node s;
         const bool found = has && probe<CK, BIG>(a, parent, pw, s);
         Expand x; x.ne = 0; x.np = 0;
-        uint32_t w_here = 0;
         if (found) {
             if (!(meta & M_DSTART)) tV += 1;
             if (s.flags & NF_HASH) tH += 1;
-            const uint32_t base = L.toff[tl];
-            const uint32_t d = L.depth[tl];
-            w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
-            const uint32_t w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
             expand(s, lc, d, meta, key, w_here, w_prev, x);
         }
         const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
         const uint32_t ptot = __popcll(b0) + __popcll(b1);
-        if (qn + ptot > (uint32_t)QCAP) { ovf = true; break; }
+        if (qn + ptot > (uint32_t)LT::QCAP) { ovf = true; break; }
         const uint32_t pre = prefix_count(b0) + prefix_count(b1);
         const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
         const uint32_t wid = w_here & WID_MASK;
-        if (x.np >= 1) {
-            const uint32_t p = qn + pre;
-            L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf0; L.q_key[p] = x.pk0;
-            L.q_pw[p] = (x.pf0 & M_PLUS) ? W_PLUS : wid;
-        }
-        if (x.np >= 2) {
-            const uint32_t p = qn + pre + 1;
-            L.q_parent[p] = s.child; L.q_meta[p] = nmeta | x.pf1; L.q_key[p] = x.pk1;
-            L.q_pw[p] = (x.pf1 & M_PLUS) ? W_PLUS : wid;
-        }
+        if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, nmeta | x.pf0, s.child, (x.pf0 & M_PLUS) ? W_PLUS : wid);
+        if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, nmeta | x.pf1, s.child, (x.pf1 & M_PLUS) ? W_PLUS : wid);
         qn += ptot;
         if (x.ne) {
             const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
@@ -465,7 +471,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
     base = __shfl(base, 0, 64);
     const uint32_t dst = base + incl - c;
     if ((uint64_t)base + tot <= a.sfids_cap) {
-        sort_rows<CK>(a, L, keep, c, incl - c, dst);
+        sort_rows<CK, LT>(a, L, keep, c, incl - c, dst);
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
     }
@@ -477,9 +483,9 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, TileLds& L, uint3
     (void)tend;
 }
 
-template <bool CK, bool BIG>
-__global__ __launch_bounds__(64) void tm_match_tiles(MatchArgs a) {
-    __shared__ TileLds L;
+template <bool CK, bool BIG, int QC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_tiles(MatchArgs a) {
+    __shared__ TileLds<QC> L;
     const uint32_t lane = threadIdx.x;
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0;
@@ -830,6 +836,39 @@ __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
     }
 }
 
+// ------------------------------------------------ routes (emqx_broker:aggre/1)
+
+// Routes per topic = sum over its matched filters of their dest counts
+// (lookup_routes/1 for every To in [Topic | Matched], src/emqx_router.erl:132;
+// the topic itself is in the trie, so Matched already holds an exact route).
+__global__ __launch_bounds__(256) void tm_route_count(RouteArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n) return;
+    uint32_t c = 0;
+    for (uint32_t i = a.row_off[t], e = a.row_off[t + 1]; i < e; ++i) {
+        const uint32_t f = a.ids[i];
+        if (f < a.nnodes) c += a.roff[f + 1] - a.roff[f];
+    }
+    a.rcount[t] = c;
+}
+
+// Writes each topic's (filter, dest) pairs at its global route offset
+// (finishes the block-local scan of rcount, like tm_finalize does for ids).
+__global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n) return;
+    uint64_t o = (uint64_t)a.r_rowoff[t] + a.bsums[t / SCAN_TILE];
+    a.r_rowoff[t] = (uint32_t)o;
+    for (uint32_t i = a.row_off[t], e = a.row_off[t + 1]; i < e; ++i) {
+        const uint32_t f = a.ids[i];
+        if (f >= a.nnodes) continue;
+        for (uint32_t k = a.roff[f], ke = a.roff[f + 1]; k < ke && o < a.cap; ++k, ++o) {
+            a.out_fid[o] = f;
+            a.out_dest[o] = a.rdest[k];
+        }
+    }
+}
+
 // ------------------------------------------------ token batches (sharded mode)
 
 // Validates a device-resident token batch before any walk reads it (toff
@@ -898,21 +937,25 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 
 // ------------------------------------------------------------ launchers
 
-uint32_t match_waves(uint32_t n, int device) {
-    static uint32_t cap[64] = {0};
+uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
+    static uint32_t cap[64][2] = {};
+    const int qi = qcap <= 384 ? 0 : 1;
     const uint32_t ntiles = (n + TILE - 1) / TILE;
-    uint32_t c = (device >= 0 && device < 64) ? cap[device] : 0u;
+    uint32_t c = (device >= 0 && device < 64) ? cap[device][qi] : 0u;
     if (!c) {
         int per_cu = 0, cus = 0;
-        // all four instances have the same LDS footprint, which bounds residency
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tm_match_tiles<false, false>, 64, 0) != hipSuccess ||
+        // the four instances of one stack size share its LDS footprint, which bounds residency
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, qi == 0 ? tm_match_tiles<false, false, 384> : tm_match_tiles<false, false, 512>, 64, 0) !=
+                hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
             per_cu <= 0 || cus <= 0) {
             (void)hipGetLastError();
-            per_cu = 12; cus = 256;
+            per_cu = qi == 0 ? 16 : 14;
+            cus = 256;
         }
         c = (uint32_t)per_cu * (uint32_t)cus;
-        if (device >= 0 && device < 64) cap[device] = c;
+        if (device >= 0 && device < 64) cap[device][qi] = c;
     }
     return ntiles < c ? ntiles : c;
 }
@@ -923,7 +966,8 @@ static void launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, h
     if (ev_a) (void)hipEventRecord(ev_a, s);
     if (ntiles) {
         const uint32_t grid = a.grid;
-        hipLaunchKernelGGL((tm_match_tiles<CK, BIG>), dim3(grid), dim3(64), 0, s, a);
+        if (a.qcap <= 384) hipLaunchKernelGGL((tm_match_tiles<CK, BIG, 384>), dim3(grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((tm_match_tiles<CK, BIG, 512>), dim3(grid), dim3(64), 0, s, a);
     }
     if (ev_b) (void)hipEventRecord(ev_b, s);
     hipLaunchKernelGGL((tm_match_slow<CK, BIG>), dim3(a.s_waves), dim3(64), 0, s, a);
@@ -950,6 +994,16 @@ hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
     const uint32_t grid = min(ntiles, 256u * 32u);   // 8 waves per SIMD
     if (checked) hipLaunchKernelGGL(tm_finalize<true>, dim3(grid), dim3(64), 0, s, a);
     else hipLaunchKernelGGL(tm_finalize<false>, dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_count(const RouteArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_route_count, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_route_fill, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -23,6 +23,23 @@ NODE = "emqx@127.0.0.1"
 
 _engine = None
 _routes = {}   # topic -> [dest, ...] in insertion order (bag)
+_agg_ids = {}  # aggregated destination (emqx_broker:aggre/1) -> u32 id of the device route table
+_agg_of = []   # id -> aggregated destination
+
+
+def aggregate(dest):
+    """The aggre/1 destination of a route dest (src/emqx_broker.erl:250-261):
+    a node stays the node, a shared-subscription dest {Group, Node} becomes Group."""
+    return ("group", dest[0]) if isinstance(dest, tuple) else ("node", dest)
+
+
+def _agg_id(dest) -> int:
+    a = aggregate(dest)
+    i = _agg_ids.get(a)
+    if i is None:
+        i = _agg_ids[a] = len(_agg_of)
+        _agg_of.append(a)
+    return i
 
 
 def use(engine: Engine):
@@ -38,12 +55,13 @@ def engine() -> Engine:
 
 
 def clear_tables():
-    global _engine, _routes
+    global _engine, _routes, _agg_ids, _agg_of
     dev = _engine.device if _engine is not None else (0 if N.gpu_available() else -1)
     if _engine is not None:
         _engine.close()
     _engine = Engine(device=dev)
     _routes = {}
+    _agg_ids, _agg_of = {}, []
 
 
 def add_route(topic: bytes, dest=NODE):
@@ -57,10 +75,9 @@ def do_add_route(topic: bytes, dest=NODE):
         raise TypeError("function_clause")
     topic = bytes(topic)
     dests = _routes.setdefault(topic, [])
-    if dest in dests:
+    if dest in dests:                      # lists:member(Route, lookup_routes(Topic)) (:116)
         return "ok"
-    if not dests:
-        engine().insert(topic)
+    engine().route_add(topic, _agg_id(dest))   # first route of the topic inserts it into the trie
     dests.append(dest)
     return "ok"
 
@@ -78,7 +95,7 @@ def do_delete_route(topic: bytes, dest=NODE):
     dests.remove(dest)
     if not dests:
         del _routes[topic]
-        engine().delete(topic)
+    engine().route_delete(topic, _agg_id(dest))   # the last route deletes the trie entry
     return "ok"
 
 
@@ -123,6 +140,27 @@ def match_routes_batch(topic_list):
             out.extend(Route(f, d) for d in _routes.get(f, []))
         res.append(out)
     return res
+
+
+def aggre_batch(topic_list):
+    """emqx_broker:aggre(match_routes(T)) for a batch, resolved on the device:
+    per topic the list of (To, Node) / (To, Group) pairs -- filters in Erlang
+    binary order, each filter's destinations in first-added order, no pair
+    twice (the reference's usort removes duplicate group pairs)."""
+    eng = engine()
+    offs, fids, dests = eng.match_routes_batch(topic_list)
+    cache = {}
+    out = []
+    for i in range(len(topic_list)):
+        row = []
+        for k in range(int(offs[i]), int(offs[i + 1])):
+            fid = int(fids[k])
+            f = cache.get(fid)
+            if f is None:
+                f = cache[fid] = eng.filter_bytes(fid)
+            row.append((f, _agg_of[int(dests[k])][1]))
+        out.append(row)
+    return out
 
 
 def print_routes(topic: bytes):

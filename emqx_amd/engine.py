@@ -73,6 +73,12 @@ class Batch:
         N.check(self.eng.L.tm_batch_result(self.eng.h, self.h, C.byref(r)), "tm_batch_result")
         return _result_arrays(r)
 
+    def routes(self):
+        """Device route resolution (tm_batch_routes) -> (row_offsets, filter_ids, dests)."""
+        r = N.Routes()
+        N.check(self.eng.L.tm_batch_routes(self.eng.h, self.h, C.byref(r)), "tm_batch_routes")
+        return _routes_arrays(r)
+
     def stats(self) -> dict:
         st = N.BatchStats()
         N.check(self.eng.L.tm_batch_stats_get(self.eng.h, self.h, C.byref(st)), "tm_batch_stats_get")
@@ -102,6 +108,16 @@ def _result_arrays(r: N.Result):
     m = int(r.n_matches)
     ids = np.ctypeslib.as_array(r.filter_ids, shape=(max(m, 1),))[:m].copy() if m else np.zeros(0, np.uint32)
     return offs, ids
+
+
+def _routes_arrays(r: N.Routes):
+    n, m = r.n_topics, int(r.n_routes)
+    offs = np.ctypeslib.as_array(r.row_offsets, shape=(n + 1,)).copy()
+    if not m:
+        return offs, np.zeros(0, np.uint32), np.zeros(0, np.uint32)
+    fids = np.ctypeslib.as_array(r.filter_ids, shape=(m,)).copy()
+    dests = np.ctypeslib.as_array(r.dests, shape=(m,)).copy()
+    return offs, fids, dests
 
 
 class Engine:
@@ -170,6 +186,27 @@ class Engine:
 
     def prepare(self, topics) -> Batch:
         return Batch(self, topics)
+
+    # ---- routes (emqx_router + emqx_broker:aggre/1) -------------------------
+    def route_add(self, topic: bytes, dest: int):
+        N.check(self.L.tm_route_add(self.h, topic, len(topic), dest), "tm_route_add")
+
+    def route_delete(self, topic: bytes, dest: int) -> bool:
+        rc = self.L.tm_route_delete(self.h, topic, len(topic), dest)
+        if rc == N.TM_ENOENT:
+            return False
+        N.check(rc, "tm_route_delete")
+        return True
+
+    def match_routes_batch(self, topics):
+        """-> (row_offsets, filter_ids, dests): aggre(match_routes(T)) per topic."""
+        s = _pack(topics)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        r = N.Routes()
+        N.check(self.L.tm_match_routes_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
+                "tm_match_routes_batch")
+        return _routes_arrays(r)
 
     # ---- bulk load / filter-sharded mode -----------------------------------
     def insert_many(self, filters, shard: int = 0, nshards: int = 1) -> int:

@@ -151,6 +151,37 @@ TM_API int  tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_ro
                          const uint32_t** d_ids, uint64_t* n_matches);
 TM_API void tm_batch_free(tm_engine* e, tm_batch* b);
 
+/* ---- routes: emqx_router + emqx_broker:aggre/1 on the device ----------- */
+/* One route of `topic` to an aggregated destination id chosen by the caller
+ * (emqx_broker:aggre/1, src/emqx_broker.erl:250-261: a node() dest aggregates
+ * to the node, a shared-subscription dest {Group, Node} to the Group, so the
+ * routes {G, n1} and {G, n2} share one id).  emqx_router:do_add_route/2
+ * (src/emqx_router.erl:113-124, 229-234): the first route of a topic puts it
+ * into the trie (exact topics too, so one walk returns exact + wildcard
+ * matches); a repeated (topic, dest) only counts. */
+TM_API int  tm_route_add(tm_engine* e, const uint8_t* topic, size_t len, uint32_t dest);
+/* do_delete_route/2 (:163-169, 239-247): TM_ENOENT if (topic, dest) has no
+ * route; removing the last route of a topic deletes it from the trie. */
+TM_API int  tm_route_delete(tm_engine* e, const uint8_t* topic, size_t len, uint32_t dest);
+
+/* aggre(match_routes(T)) per topic: row i lists (filter id, dest) pairs,
+ * filters in Erlang binary order, each filter's dests in first-added order,
+ * no (filter, dest) twice.  Engine-owned memory, valid like tm_result. */
+typedef struct {
+    uint32_t        n_topics;
+    uint64_t        n_routes;
+    const uint32_t* row_offsets;  /* n_topics + 1 */
+    const uint32_t* filter_ids;   /* n_routes */
+    const uint32_t* dests;        /* n_routes */
+} tm_routes;
+
+/* Device route resolution of a waited batch (its match CSR stays in HBM). */
+TM_API int  tm_batch_routes(tm_engine* e, tm_batch* b, tm_routes* out);
+/* tm_match_batch + tm_batch_routes in one call (emqx_router:match_routes/1 +
+ * emqx_broker:aggre/1 over a batch of publishes). */
+TM_API int  tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                  tm_routes* out);
+
 /* ---- bulk load + filter-sharded mode ------------------ */
 /* emqx_trie:insert/1 over n filters (filters = concatenated bytes, offsets[n+1]).
  * nshards <= 1: every filter.  Otherwise only the filters whose
