@@ -215,7 +215,11 @@ __device__ __forceinline__ uint4 q_pack(uint64_t key, uint32_t meta, uint32_t pa
 // Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
 template <bool CK>
 __device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t tl, uint32_t slot, uint64_t key, uint32_t fid) {
+#ifdef TM_EXPERIMENT_NO_EMIT   // timing experiments only
+    if (slot < a.row_cap && fid == 0xFFFFFFF0u) {
+#else
     if (slot < a.row_cap) {
+#endif
         const uint64_t i = ((uint64_t)blockIdx.x * TILE + tl) * a.row_cap + slot;
         a.rows[CK_(i, (uint64_t)gridDim.x * TILE * a.row_cap, 13)] = (key & KEY_MASK) | fid;
     }
@@ -225,6 +229,33 @@ static_assert(offsetof(TileLds<512>, words) + sizeof(uint32_t) * WCAP == TileLds
               "staging area must be contiguous");
 static_assert(offsetof(TileLds<384>, words) + sizeof(uint32_t) * WCAP == TileLds<384>::STAGE * 8,
               "staging area must be contiguous");
+
+// Lane exchange with lane ^ j in VALU (no LDS crossbar): DPP quad_perm for 1
+// and 2, row_half_mirror + quad reverse for 4, row_ror:8 for 8, and gfx950's
+// v_permlane16/32_swap for 16 and 32.  j is a compile-time constant after the
+// bitonic loops unroll, so the switch folds (tools/shx_check.hip checks all six).
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v, uint32_t j) {
+    const uint32_t lane = threadIdx.x & 63;
+    switch (j) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    case 4: return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false), 0x1B, 0xF,
+                                                      0xF, false);
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+    case 16: {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? p[0] : p[1];
+    }
+    default: {
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? p[0] : p[1];
+    }
+    }
+}
+
+__device__ __forceinline__ unsigned long long xor_lane64(unsigned long long v, uint32_t j) {
+    return ((unsigned long long)xor_lane32((uint32_t)(v >> 32), j) << 32) | xor_lane32((uint32_t)v, j);
+}
 
 // Tile epilogue: sort the 64 rows of this wave and write their filter ids to
 // sfids[dst .. dst + c).  The rows are pulled into LDS a chunk of whole rows at
@@ -264,7 +295,7 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
             for (uint32_t kk = 2; kk <= W; kk <<= 1) {
 #pragma unroll
                 for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                    const unsigned long long other = __shfl_xor(key, j, 64);
+                    const unsigned long long other = xor_lane64(key, j);
                     const bool up = (e & kk) == 0;
                     const bool lower = (e & j) == 0;
                     const unsigned long long lo = key < other ? key : other;
@@ -306,39 +337,43 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
 }
 
 // c <= row_cap <= 128 for every kept row, so a chunk always holds at least one row.
+// The rows are copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: 16 B per
+// lane, no register destination), every row of a chunk in flight at once, so
+// the read-back costs one memory round trip per chunk rather than one per row
+// batch.  Staging positions are padded to even counts: each row starts on a 16-B
+// boundary, and the odd row's extra 8 B land in its pad slot, which the sort
+// never reads.
 template <bool CK, class LT>
-__device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t pos,
-                                          uint32_t dst) {
+__device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst) {
     constexpr uint32_t STAGE = LT::STAGE;
-    constexpr uint32_t RB = 8;   // rows per batch of independent loads
     const uint32_t lane = threadIdx.x;
     unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
+    const uint32_t cp = (c + 1u) & ~1u;
+    uint32_t incl = cp;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += u;
+    }
+    const uint32_t pos = incl - cp;
     const uint64_t rbase = (uint64_t)blockIdx.x * TILE * a.row_cap;
     const uint64_t rlim = (uint64_t)gridDim.x * TILE * a.row_cap;
     uint32_t rs = 0;
     while (rs < (uint32_t)TILE) {
         const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
-        const uint64_t beyond = __ballot(lane >= rs && pos + c - p0 > STAGE);
+        const uint64_t beyond = __ballot(lane >= rs && pos + cp - p0 > STAGE);
         const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : (uint32_t)TILE;
-        for (uint32_t r0 = rs; r0 < re; r0 += RB) {
-            unsigned long long v0[RB], v1[RB];
-            uint32_t cr[RB], pr[RB];
-#pragma unroll
-            for (uint32_t u = 0; u < RB; ++u) {
-                const uint32_t r = (r0 + u) & (TILE - 1);
-                cr[u] = r0 + u < re ? __builtin_amdgcn_readlane(c, r) : 0u;
-                pr[u] = __builtin_amdgcn_readlane(pos, r) - p0;
-                const uint64_t rb = rbase + (uint64_t)r * a.row_cap;
-                v0[u] = lane < cr[u] ? a.rows[CK_(rb + lane, rlim, 50)] : 0ull;
-                v1[u] = lane + 64 < cr[u] ? a.rows[CK_(rb + lane + 64, rlim, 51)] : 0ull;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < RB; ++u) {
-                if (lane < cr[u]) stg[CK_(pr[u] + lane, STAGE, 52)] = v0[u];
-                if (lane + 64 < cr[u]) stg[CK_(pr[u] + lane + 64, STAGE, 53)] = v1[u];
+        for (uint32_t r = rs; r < re; ++r) {
+            const uint32_t cr = __builtin_amdgcn_readlane(c, r);
+            if (cr == 0) continue;
+            const uint32_t pr = __builtin_amdgcn_readlane(pos, r) - p0;
+            const uint64_t rb = rbase + (uint64_t)r * a.row_cap;
+            if (lane < (cr + 1) / 2) {
+                const unsigned long long* src = a.rows + CK_(rb + 2 * lane, rlim, 50);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(stg + pr), 16, 0, 0);
             }
         }
-        __syncthreads();
+        __syncthreads();   // waits for the LDS-DMA (vmcnt) before any lane reads the staging area
         sort_classes<CK, LT>(a, L, keep && lane >= rs && lane < re, c, pos - p0, dst);
         __syncthreads();
         rs = re;
@@ -470,11 +505,13 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     if (lane == 0 && tot) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], tot);
     base = __shfl(base, 0, 64);
     const uint32_t dst = base + incl - c;
+#ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if ((uint64_t)base + tot <= a.sfids_cap) {
-        sort_rows<CK, LT>(a, L, keep, c, incl - c, dst);
+        sort_rows<CK, LT>(a, L, keep, c, dst);
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
     }
+#endif
     if (keep) {
         a.count[CK_(t, a.n, 16)] = c_me;
         a.src[CK_(t, a.n, 17)] = dst;
