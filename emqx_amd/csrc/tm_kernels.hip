@@ -26,7 +26,9 @@
 //                   holding slow-path topics).
 //
 // No MFMA: this is a dependent irregular gather, bound by the memory system.
+#include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include "tm_internal.hpp"
 
 namespace etm {
@@ -46,6 +48,8 @@ constexpr uint32_t M_PLUS = 1u << 10;    // probe the '+' edge (else the literal
 constexpr uint32_t M_SKIPE = 1u << 11;   // don't emit the child's own topic (literal '#' dup)
 constexpr uint32_t M_DSTART = 1u << 12;  // $-rooted start probe: the node was already counted
 static_assert(FAST_MAX_DEPTH <= (int)M_LVL_MASK, "level field too narrow");
+constexpr uint32_t M_DISP_SHIFT = 13;    // bucket displacement of a continued probe (<= max_probe <= 48)
+constexpr uint32_t M_DISP_MASK = 0x3F;
 
 // digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
 //   L = literal branch, H = '#' terminal, P = '+' branch; E = 0, L_lo = 1.
@@ -438,19 +442,39 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     }
 
     // ---- frontier loop: LIFO stack, up to 64 probes per iteration
+    //
+    // Quad-cooperative probing: probe p (0..63) of an iteration is read by the
+    // quad of lanes 4q..4q+3 in round r (p = 16r + q), each lane loading one
+    // 16-B slot of the 64-B bucket, so a load instruction touches 16 cache
+    // lines instead of 64 (one L1 tag lookup per probe instead of four: the
+    // lookups, not the bytes, saturate the L1 at full occupancy).  The popped
+    // entries stay in their LDS slots during the probe: the owner lane writes
+    // the bucket index into its entry, the quads read it from there, and the
+    // matching lane writes the slot's child summary back for the owner.  A key
+    // that spilled past its home bucket is pushed again as a continuation
+    // (displacement + 1) rather than holding the whole wave for a dependent read.
+    const uint32_t qd = lane >> 2, qs = lane & 3;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<Slot*>(a.slots), 0, BIG ? 0u : a.nslots * 16u, 0x00020000);
     while (qn > 0) {
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
-        const uint32_t idx = qn - k + lane;
+        qn -= k;
+        const uint32_t idx = qn + lane;
         uint4 e = uint4{0u, 0u, 0u, 0u};
         if (has) e = L.q[idx];
-        qn -= k;
         const uint32_t meta = e.x & 0x7FFFFFFFu;
         const uint64_t key = ((uint64_t)e.y << 32) | (e.x & 0x80000000u);
         const uint32_t parent = e.z, pw = e.w;
         const uint32_t tl = meta & 63;
         const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
-        // the topic's words are read before the probe's bucket arrives
+        const uint32_t disp = (meta >> M_DISP_SHIFT) & M_DISP_MASK;
+        if (has) {
+            uint32_t hb = home_bucket(parent, pw, a.nbuckets) + disp;
+            if (hb >= a.nbuckets) hb -= a.nbuckets;
+            L.q[idx].x = hb;
+        }
+        // the topic's words are read while the buckets are in flight
         uint32_t d = 0, w_here = 0, w_prev = 0;
         if (has) {
             const uint32_t base = L.toff[tl];
@@ -458,22 +482,67 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
             w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
         }
+        uint32_t rp[4], rw[4];
+        uint4 sl[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t p = 16 * r + qd;
+            const bool v = p < k;
+            const uint4 rec = L.q[qn + (v ? p : 0u)];
+            rp[r] = v ? rec.z : SLOT_EMPTY;
+            rw[r] = rec.w;
+            const uint64_t si = CK_((uint64_t)rec.x * BUCKET + qs, a.nslots, 1);
+            if (!BIG) {
+                sl[r] = ld_b128(rsrc, v ? (uint32_t)si * 16u : 0xFFFFFFF0u);   // out of range: reads 0
+            } else {
+                sl[r] = v ? reinterpret_cast<const uint4*>(a.slots)[si] : uint4{0u, 0u, 0u, 0u};
+            }
+        }
+        uint64_t mm[4], te[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const bool m = rp[r] != SLOT_EMPTY && sl[r].x == rp[r] && sl[r].y == rw[r];
+            mm[r] = __ballot(m);
+            te[r] = __ballot(qs == 3 && sl[r].x == SLOT_EMPTY);   // bucket has a free tail: the run ends here
+            if (m) {
+                L.q[qn + 16 * r + qd].x = sl[r].z;
+                L.q[qn + 16 * r + qd].y = sl[r].w;
+            }
+        }
+        const uint32_t myr = lane >> 4, myq = lane & 15;
+        const uint64_t mym = myr == 0 ? mm[0] : myr == 1 ? mm[1] : myr == 2 ? mm[2] : mm[3];
+        const uint64_t myt = myr == 0 ? te[0] : myr == 1 ? te[1] : myr == 2 ? te[2] : te[3];
+        const bool found = has && ((mym >> (4 * myq)) & 0xF) != 0;
+        const bool cont = has && !found && !((myt >> (4 * myq + 3)) & 1) && disp < a.max_probe;
         Node s;
-        const bool found = has && probe<CK, BIG>(a, parent, pw, s);
+        s.child = 0; s.term = NONE; s.hterm = NONE; s.flags = 0;
+        if (found) {
+            const uint4 res = L.q[idx];
+            const uint32_t hz = res.x, hw = res.y;
+            s.child = hz & ID_MASK;
+            s.term = (hz & B_TOPIC) ? s.child : NONE;
+            s.hterm = (hw & B_HTERM) ? (hw & ID_MASK) : NONE;
+            s.flags = ((hz & B_PLUS) ? NF_PLUS : 0u) | ((hw & B_HASH) ? NF_HASH : 0u);
+        }
         Expand x; x.ne = 0; x.np = 0;
         if (found) {
             if (!(meta & M_DSTART)) tV += 1;
             if (s.flags & NF_HASH) tH += 1;
             expand(s, lc, d, meta, key, w_here, w_prev, x);
         }
-        const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+        const uint32_t np = cont ? 1u : x.np;
+        const uint64_t b0 = __ballot(np >= 1), b1 = __ballot(np >= 2);
         const uint32_t ptot = __popcll(b0) + __popcll(b1);
         if (qn + ptot > (uint32_t)LT::QCAP) { ovf = true; break; }
         const uint32_t pre = prefix_count(b0) + prefix_count(b1);
         const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
         const uint32_t wid = w_here & WID_MASK;
-        if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, nmeta | x.pf0, s.child, (x.pf0 & M_PLUS) ? W_PLUS : wid);
-        if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, nmeta | x.pf1, s.child, (x.pf1 & M_PLUS) ? W_PLUS : wid);
+        if (cont) {
+            L.q[qn + pre] = q_pack(key, meta + (1u << M_DISP_SHIFT), parent, pw);
+        } else {
+            if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, nmeta | x.pf0, s.child, (x.pf0 & M_PLUS) ? W_PLUS : wid);
+            if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, nmeta | x.pf1, s.child, (x.pf1 & M_PLUS) ? W_PLUS : wid);
+        }
         qn += ptot;
         if (x.ne) {
             const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
@@ -991,6 +1060,8 @@ uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
             per_cu = qi == 0 ? 16 : 14;
             cus = 256;
         }
+        // TM_WAVES_PER_CU: fewer resident waves (occupancy sweeps in tools/; never more than fit)
+        if (const char* w = getenv("TM_WAVES_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(w)));
         c = (uint32_t)per_cu * (uint32_t)cus;
         if (device >= 0 && device < 64) cap[device][qi] = c;
     }
