@@ -184,6 +184,81 @@ def run_c4(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
+def run_c5(args, ws, rank, local, pg):
+    """Config C5: 10k hot topics take 90% of the publishes, each matched by ~K
+    filters derived from it (+ 100k background C2-style filters); one step =
+    10,000 subscribe/unsubscribe deltas applied to the trie and uploaded to the
+    device, then the deduplicated batch is matched (every distinct topic once;
+    rows longer than the fast path's K go to the generic kernel)."""
+    from emqx_amd import gen
+    from emqx_amd.engine import Engine
+    from emqx_amd.skew import Churn, workload
+
+    p = gen.SkewParams(k_per_hot=args.c5_k)
+    t0 = time.time()
+    allf, derived, hot, pubs = workload(p, 100_000, args.topics, seed=5 + rank)
+    log(f"[rank {rank}] C5 workload: {len(allf)} filters, {len(pubs)} publishes in {time.time() - t0:.1f}s")
+    eng = Engine(device=local)
+    eng.insert_many(allf)
+    eng.sync()
+    churn = Churn(hot, derived.tolist(), seed=11 + rank)
+    b = eng.prepare(pubs, dedup=True)
+    row_of, n_rows = b.row_map()
+    for _ in range(args.warmup):
+        b.launch().wait()
+    if pg is not None:
+        pg.barrier()
+    # the deltas are drawn before timing; applying them (trie ops + the device
+    # delta upload inside launch) is inside each step
+    deltas = [churn.step(args.c5_deltas) for _ in range(args.steps)]
+    ms_match, ms_churn = [], []
+    t0 = time.perf_counter()
+    for dels, adds in deltas:
+        tc = time.perf_counter()
+        Churn.apply(eng, dels, adds)
+        ms_churn.append(1e3 * (time.perf_counter() - tc))
+        b.launch().wait()
+        ms_match.append(b.stats()["ms_total"])
+    elapsed = time.perf_counter() - t0
+    if pg is not None:
+        import torch
+        pg.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = b.stats()
+    offs, _ = b.result()
+    rowlen = np.diff(offs.astype(np.int64))
+    delivered = int(rowlen[row_of].sum())
+    n = len(pubs)
+    out = {
+        "metric": "publishes matched/sec (node), hot-topic skew + churn (C5)",
+        "value": ws * n * args.steps / elapsed,
+        "unit": "publishes/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded skew generator, SURVEY.md §8d C5)",
+        "config": {"workload": f"C5: 10k hot topics x ~{args.c5_k} filters + 100k background, "
+                               f"{n} publishes per GPU (90% hot, Zipf 1.0), {args.c5_deltas} deltas per step",
+                   "filters": len(allf), "distinct_topics": int(n_rows), "mode": "replicated, dedup batches"},
+        "device_pipeline_ms": float(np.mean(ms_match)),
+        "churn_apply_ms": float(np.mean(ms_churn)),
+        "matches_delivered_per_step": delivered,
+        "generic_path_topics": int(st["slow_topics"]),
+        "uploads_delta": eng.stats()["uploads_delta"],
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,8 +270,11 @@ def main():
     ap.add_argument("--latency-batches", type=int, default=200)
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (no latency / e2e / cpu legs): for rocprofv3 runs")
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
-                    help="c2: 1M wildcard filters, replicated (the BASELINE metric); c4: IoT filters, sharded")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
+                    help="c2: 1M wildcard filters, replicated (the BASELINE metric); c4: IoT filters, sharded; "
+                         "c5: hot-topic skew + churn")
+    ap.add_argument("--c5-k", type=int, default=100, help="C5 filters per hot topic (10 / 100 / 1000)")
+    ap.add_argument("--c5-deltas", type=int, default=10_000, help="C5 subscribe/unsubscribe deltas per step")
     ap.add_argument("--c4-filters", type=int, default=0, help="C4 filter count (default 100M)")
     args = ap.parse_args()
 
@@ -212,6 +290,8 @@ def main():
         pg = dist
     if args.workload == "c4":
         return run_c4(args, ws, rank, local, pg)
+    if args.workload == "c5":
+        return run_c5(args, ws, rank, local, pg)
 
     from emqx_amd import gen
     from emqx_amd.engine import Engine

@@ -25,6 +25,7 @@ TM_EABORT = -125
 TM_NONE = 0xFFFFFFFF
 TM_MAX_TOPIC_LEN = 4096
 TM_CFG_FROZEN_DICT = 1
+TM_BATCH_DEDUP = 1
 
 _ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
              TM_EINVAL: "EINVAL", TM_EOVERFLOW: "EOVERFLOW", TM_EABORT: "EABORT"}
@@ -89,6 +90,8 @@ SIGNATURES = {
     "tm_trie_match": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_batch_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
+    "tm_batch_prepare_ex": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "tm_batch_row_map": (C.c_int, [P, P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint32)]),
     "tm_batch_launch": (C.c_int, [P, P]),
     "tm_batch_wait": (C.c_int, [P, P]),
     "tm_batch_result": (C.c_int, [P, P, C.POINTER(Result)]),
@@ -100,10 +103,12 @@ SIGNATURES = {
     "tm_batch_routes": (C.c_int, [P, P, C.POINTER(Routes)]),
     "tm_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
     "tm_trie_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_trie_delete_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
     "tm_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
     "tm_filter_shard": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_tokenize": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64)]),
     "tm_batch_prepare_tokens": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint64, C.c_int, C.POINTER(P)]),
+    "tm_gather_rows": (C.c_int, [P, P, P, P, C.c_uint32, P, P]),
     "tm_tokens_shard": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, P]),
     "tm_batch_export": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint32]),
     "tm_filter_bytes": (C.POINTER(C.c_uint8), [P, C.c_uint32, C.POINTER(SZ)]),
@@ -111,6 +116,7 @@ SIGNATURES = {
     "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),
     "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
     "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),
+    "tm_rules_match": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),
 }

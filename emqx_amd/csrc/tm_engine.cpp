@@ -197,6 +197,10 @@ struct tm_batch {
     std::vector<uint64_t> offs;
     // host tokens
     std::vector<uint32_t> h_words, h_toff, h_slow;
+    // TM_BATCH_DEDUP: rows are per distinct topic; row_of[i] = row of publish i
+    bool dedup = false;
+    uint32_t n_pub = 0;
+    std::vector<uint32_t> row_of;
     std::vector<uint8_t> h_tflags;
     // device inputs
     uint32_t *d_words = nullptr, *d_toff = nullptr, *d_slow = nullptr;
@@ -786,6 +790,70 @@ struct tm_engine {
         return TM_OK;
     }
 
+    // tm_rules_match: rules tokenised with their own dictionary, names against it
+    uint32_t *d_rl = nullptr;
+    size_t c_rl = 0;
+    int rules_match(const uint8_t* names, const uint64_t* noffs, uint32_t n, const uint8_t* rules,
+                    const uint64_t* roffs, uint32_t r, bool dollar_rule, uint32_t* bits) {
+        WordDict rd;
+        std::vector<TWord> ws;
+        std::vector<uint32_t> rw, ro(1, 0), nw, no(1, 0);
+        std::vector<uint8_t> rf(r), nf(n);
+        auto id_of = [](const TWord& w) -> uint32_t {
+            return w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : W_UNKNOWN;
+        };
+        for (uint32_t j = 0; j < r; ++j) {
+            const uint8_t* p = rules + roffs[j];
+            const size_t len = roffs[j + 1] - roffs[j];
+            split_words(p, len, ws);
+            for (const TWord& w : ws) {
+                uint32_t id = id_of(w);
+                if (id == W_UNKNOWN) id = rd.intern(w.p, w.n);
+                rw.push_back(id);
+            }
+            ro.push_back((uint32_t)rw.size());
+            rf[j] = (len > 0 && (p[0] == '+' || p[0] == '#')) ? 1 : 0;
+        }
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint8_t* p = names + noffs[t];
+            const size_t len = noffs[t + 1] - noffs[t];
+            split_words(p, len, ws);
+            for (const TWord& w : ws) {
+                uint32_t id = id_of(w);
+                if (id == W_UNKNOWN) id = rd.find(w.p, w.n);
+                nw.push_back(id);
+            }
+            if (nw.size() > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+            no.push_back((uint32_t)nw.size());
+            nf[t] = (len > 0 && p[0] == '$') ? 1 : 0;
+        }
+        const uint32_t wpr = (r + 31) / 32;
+        // one device block: [rw | ro | nw | no | bits] in u32, then rf | nf bytes
+        const size_t nbits = (size_t)n * wpr;
+        const size_t words = rw.size() + ro.size() + nw.size() + no.size() + nbits + (r + n + 3) / 4 + 4;
+        int rc;
+        if ((rc = dev_reserve(d_rl, c_rl, words))) return rc;
+        uint32_t* d = d_rl;
+        uint32_t *d_rw = d, *d_ro = d_rw + rw.size(), *d_nw = d_ro + ro.size(), *d_no = d_nw + nw.size();
+        uint32_t* d_bits = d_no + no.size();
+        uint8_t* d_rf = reinterpret_cast<uint8_t*>(d_bits + nbits);
+        uint8_t* d_nf = d_rf + r;
+        HIP_OK(hipMemcpyAsync(d_rw, rw.data(), rw.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_ro, ro.data(), ro.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_nw, nw.data(), nw.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_no, no.data(), no.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_rf, rf.data(), r, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_nf, nf.data(), n, hipMemcpyHostToDevice, stream));
+        RulesArgs a{};
+        a.nwords = d_nw; a.noff = d_no; a.nflag = d_nf; a.n = n;
+        a.rwords = d_rw; a.roff = d_ro; a.rflag = d_rf; a.r = r;
+        a.dollar_rule = dollar_rule ? 1u : 0u; a.wpr = wpr; a.bits = d_bits;
+        HIP_OK(launch_rules_match(a, stream));
+        HIP_OK(hipMemcpyAsync(bits, d_bits, nbits * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));   // the host vectors above are freed on return
+        return TM_OK;
+    }
+
     int sync_device() {
         if (device < 0) return TM_ENODEV;
         int rc = ensure_delta_idle();
@@ -1108,12 +1176,75 @@ struct tm_engine {
         return TM_OK;
     }
 
-    int prepare(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
-        b->n = n;
-        b->offs.assign(offsets, offsets + (size_t)n + 1);
-        const uint64_t base = offsets[0];
-        for (auto& o : b->offs) o -= base;
-        b->bytes.assign(topics + base, topics + base + b->offs[n]);
+    // distinct topics of a batch in first-occurrence order; row_of maps publishes to them
+    void dedup_topics(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
+        std::vector<uint64_t> h(n);
+        const unsigned nt = (n >= 65536) ? threads : 1;
+        auto hash_range = [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t t = lo; t < hi; ++t) h[t] = hash_bytes(topics + offsets[t], offsets[t + 1] - offsets[t]);
+        };
+        if (nt <= 1) hash_range(0, n);
+        else {
+            std::vector<std::thread> th;
+            for (unsigned i = 0; i < nt; ++i)
+                th.emplace_back(hash_range, (uint32_t)((uint64_t)n * i / nt), (uint32_t)((uint64_t)n * (i + 1) / nt));
+            for (auto& x : th) x.join();
+        }
+        size_t cap = 1024;
+        while (cap < (size_t)n * 2) cap <<= 1;
+        std::vector<uint32_t> tab(cap, 0);          // distinct index + 1
+        std::vector<uint32_t> first;                 // publish index of each distinct topic
+        b->row_of.resize(n);
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint8_t* p = topics + offsets[t];
+            const size_t len = offsets[t + 1] - offsets[t];
+            size_t i = h[t] & (cap - 1);
+            for (;;) {
+                const uint32_t u = tab[i];
+                if (u == 0) {
+                    first.push_back(t);
+                    tab[i] = (uint32_t)first.size();
+                    b->row_of[t] = (uint32_t)first.size() - 1;
+                    break;
+                }
+                const uint32_t f = first[u - 1];
+                const size_t fl = offsets[f + 1] - offsets[f];
+                if (h[f] == h[t] && fl == len && memcmp(topics + offsets[f], p, len) == 0) {
+                    b->row_of[t] = u - 1;
+                    break;
+                }
+                i = (i + 1) & (cap - 1);
+            }
+        }
+        const uint32_t nu = (uint32_t)first.size();
+        b->offs.assign((size_t)nu + 1, 0);
+        uint64_t tot = 0;
+        for (uint32_t u = 0; u < nu; ++u) tot += offsets[first[u] + 1] - offsets[first[u]];
+        b->bytes.resize(tot);
+        uint64_t o = 0;
+        for (uint32_t u = 0; u < nu; ++u) {
+            const uint32_t f = first[u];
+            const size_t len = offsets[f + 1] - offsets[f];
+            if (len) memcpy(b->bytes.data() + o, topics + offsets[f], len);
+            o += len;
+            b->offs[u + 1] = o;
+        }
+        b->n = nu;
+    }
+
+    int prepare(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags = 0) {
+        b->dedup = (flags & TM_BATCH_DEDUP) != 0;
+        b->n_pub = n;
+        b->row_of.clear();
+        if (b->dedup) {
+            dedup_topics(b, topics, offsets, n);
+        } else {
+            b->n = n;
+            b->offs.assign(offsets, offsets + (size_t)n + 1);
+            const uint64_t base = offsets[0];
+            for (auto& o : b->offs) o -= base;
+            b->bytes.assign(topics + base, topics + base + b->offs[n]);
+        }
         b->launched = b->done = false;
         b->tokens_only = false;
         int rc = tokenize(b);
@@ -1296,7 +1427,7 @@ struct tm_engine {
             dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
             dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
-            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest);
+            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);
@@ -1498,6 +1629,41 @@ int tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offset
     return TM_OK;
 }
 
+int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
+                        tm_batch** out) {
+    if (!e || !offsets || !out || (!topics && n) || (flags & ~TM_BATCH_DEDUP)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (e->device >= 0) {
+        int rc = e->set_device();
+        if (rc) return rc;
+    }
+    tm_batch* b = new (std::nothrow) tm_batch();
+    if (!b) return TM_ENOMEM;
+    int rc;
+    try {
+        rc = e->prepare(b, topics, offsets, n, flags);
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
+    if (rc) { b->release(); delete b; return rc; }
+    if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
+    *out = b;
+    return TM_OK;
+}
+
+int tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_t* n_rows) {
+    if (!e || !b || !row_of) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (!b->dedup && b->row_of.size() != b->n) {
+        b->row_of.resize(b->n);
+        for (uint32_t i = 0; i < b->n; ++i) b->row_of[i] = i;
+    }
+    static const uint32_t none = 0;
+    *row_of = b->row_of.empty() ? &none : b->row_of.data();
+    if (n_rows) *n_rows = b->n;
+    return TM_OK;
+}
+
 int tm_batch_launch(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
@@ -1598,6 +1764,20 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uint64_t* o
     }
 }
 
+int tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* name_offsets, uint32_t n,
+                   const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule, uint32_t* bits) {
+    if (!e || !name_offsets || !rule_offsets || (n && !names) || (r && !rules) || (n && r && !bits)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    if (!n || !r) return TM_OK;
+    try {
+        return e->rules_match(names, name_offsets, n, rules, rule_offsets, r, dollar_rule != 0, bits);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
 int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n, uint32_t shard,
                         uint32_t nshards, uint64_t* n_inserted) {
     if (!e || !offsets || (!filters && n)) return TM_EINVAL;
@@ -1622,6 +1802,25 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
         rc = TM_ENOMEM;
     }
     if (n_inserted) *n_inserted = done;
+    return rc;
+}
+
+int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
+                        uint64_t* n_deleted) {
+    if (!e || !offsets || (!filters && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    uint64_t done = 0;
+    int rc = TM_OK;
+    try {
+        for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
+            if (offsets[i + 1] < offsets[i]) { rc = TM_EINVAL; break; }
+            rc = e->trie_delete(filters + offsets[i], offsets[i + 1] - offsets[i]);
+            if (rc == TM_OK) ++done;
+        }
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
+    if (n_deleted) *n_deleted = done;
     return rc;
 }
 
@@ -1677,6 +1876,17 @@ int tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t*
     }
     if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
     *out = b;
+    return TM_OK;
+}
+
+int tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d_src_off, const int64_t* d_idx, uint32_t n,
+                   const int64_t* d_dst_off, uint32_t* d_dst) {
+    if (!e || (n && (!d_src_off || !d_idx || !d_dst_off))) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    HIP_OK(launch_gather_rows(d_src, d_src_off, d_idx, n, d_dst_off, d_dst, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
     return TM_OK;
 }
 

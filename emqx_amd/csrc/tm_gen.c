@@ -360,3 +360,132 @@ EXPORT int tm_gen_iot_topics(const tm_iot_params* p, uint64_t tseed, uint64_t n,
     out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
     return 0;
 }
+
+/* ---- C5: high-fanout skew ---------------------------------
+ *
+ * n_hot distinct hot topics of hot_depth levels ("h<l>_<k>", k < vocab), and
+ * per hot topic k_per_hot distinct filters derived from it: each level becomes
+ * '+' with probability 0.3, and with probability 0.3 the filter is cut at a
+ * random level by '#'; at least 3 literal levels are kept, so filters of
+ * different hot topics rarely coincide (global duplicates are skipped).
+ * derive_one() makes one more such filter for the churn deltas.
+ */
+typedef struct {
+    uint64_t seed;
+    uint32_t n_hot;
+    uint32_t hot_depth;
+    uint32_t vocab;
+    uint32_t k_per_hot;
+} tm_skew_params;
+
+static uint32_t derive(sbuf* o, const char* t, uint32_t tl, uint32_t depth, uint64_t* s) {
+    /* word boundaries of t */
+    uint32_t st[64], en[64], nw = 0, i = 0;
+    while (nw < 64) {
+        uint32_t j = i;
+        while (j < tl && t[j] != '/') j++;
+        st[nw] = i; en[nw] = j; nw++;
+        if (j >= tl) break;
+        i = j + 1;
+    }
+    (void)depth;
+    for (int attempt = 0; attempt < 64; attempt++) {
+        uint32_t cut = nw;
+        if (sm_u01(s) < 0.3) cut = (uint32_t)sm_below(s, nw);    /* '#' replaces levels >= cut */
+        uint64_t plus = 0;
+        uint32_t lit = 0;
+        for (uint32_t l = 0; l < cut; l++) {
+            if (sm_u01(s) < 0.3) plus |= 1ull << l; else lit++;
+        }
+        if (lit < 3) continue;
+        size_t start = o->n;
+        for (uint32_t l = 0; l < cut; l++) {
+            if (l) sb_put(o, "/", 1);
+            if (plus >> l & 1) sb_put(o, "+", 1); else sb_put(o, t + st[l], en[l] - st[l]);
+        }
+        if (cut < nw) { if (cut) sb_put(o, "/", 1); sb_put(o, "#", 1); }
+        return (uint32_t)(o->n - start);
+    }
+    return 0;
+}
+
+EXPORT int tm_gen_skew(const tm_skew_params* p, tm_strs* hot, tm_strs* filters) {
+    uint64_t s = p->seed;
+    sbuf ho = {0}, fo = {0};
+    uint64_t* hoffs = (uint64_t*)malloc(sizeof(uint64_t) * (p->n_hot + 1));
+    uint64_t nf_cap = (uint64_t)p->n_hot * p->k_per_hot;
+    uint64_t* foffs = (uint64_t*)malloc(sizeof(uint64_t) * (nf_cap + 1));
+    sset hs; sset_init(&hs, p->n_hot);
+    sset fs; sset_init(&fs, nf_cap + 1);
+    char w[32];
+    hoffs[0] = 0; foffs[0] = 0;
+    uint64_t nh = 0, nf = 0, guard = 0;
+    while (nh < p->n_hot) {
+        if (++guard > (uint64_t)p->n_hot * 100) break;
+        size_t start = ho.n;
+        for (uint32_t l = 0; l < p->hot_depth; l++) {
+            if (l) sb_put(&ho, "/", 1);
+            int n = snprintf(w, sizeof(w), "h%u_%u", l, (unsigned)sm_below(&s, p->vocab));
+            sb_put(&ho, w, (size_t)n);
+        }
+        if (!sset_add(&hs, ho.b, start, (uint32_t)(ho.n - start))) { ho.n = start; continue; }
+        hoffs[++nh] = ho.n;
+    }
+    for (uint64_t h = 0; h < nh; h++) {
+        uint32_t got = 0, tries = 0;
+        while (got < p->k_per_hot && tries++ < p->k_per_hot * 40) {
+            size_t start = fo.n;
+            /* derive() reads the hot topic while appending to fo: copy it first (ho is not fo) */
+            uint32_t len = derive(&fo, ho.b + hoffs[h], (uint32_t)(hoffs[h + 1] - hoffs[h]), p->hot_depth, &s);
+            if (!len || !sset_add(&fs, fo.b, start, len)) { fo.n = start; continue; }
+            foffs[++nf] = fo.n;
+            got++;
+        }
+    }
+    free(hs.h); free(hs.off); free(hs.len); free(fs.h); free(fs.off); free(fs.len);
+    hot->buf = ho.b ? ho.b : (char*)malloc(1); hot->offs = hoffs; hot->n = nh;
+    filters->buf = fo.b ? fo.b : (char*)malloc(1); filters->offs = foffs; filters->n = nf;
+    return nh == p->n_hot ? 0 : -1;
+}
+
+/* One more derived filter of hot topic t (churn deltas), seeded. */
+EXPORT int tm_gen_derive_one(const char* t, uint32_t tl, uint64_t seed, char* out, uint32_t cap) {
+    sbuf o = {0};
+    uint64_t s = seed;
+    uint32_t len = derive(&o, t, tl, 0, &s);
+    int r = -1;
+    if (len && len <= cap) { memcpy(out, o.b, len); r = (int)len; }
+    free(o.b);
+    return r;
+}
+
+/* n publishes: with probability p_a a Zipf(zipf_s)-chosen element of A (rank 0
+ * hottest), otherwise a uniformly chosen element of B. */
+EXPORT int tm_gen_pick(const tm_strs* A, const tm_strs* B, uint64_t seed, uint64_t n, double p_a, double zipf_s,
+                       tm_strs* out) {
+    double* cdf = (double*)malloc(sizeof(double) * (A->n ? A->n : 1));
+    double acc = 0;
+    for (uint64_t k = 0; k < A->n; k++) { acc += pow((double)(k + 1), -zipf_s); cdf[k] = acc; }
+    for (uint64_t k = 0; k < A->n; k++) cdf[k] /= acc;
+    uint64_t s = seed;
+    sbuf o = {0};
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    offs[0] = 0;
+    for (uint64_t t = 0; t < n; t++) {
+        const tm_strs* S;
+        uint64_t i;
+        if (A->n && (B->n == 0 || sm_u01(&s) < p_a)) {
+            const double u = sm_u01(&s);
+            uint64_t lo = 0, hi = A->n - 1;
+            while (lo < hi) { uint64_t mid = (lo + hi) / 2; if (u < cdf[mid]) hi = mid; else lo = mid + 1; }
+            S = A; i = lo;
+        } else {
+            S = B; i = sm_below(&s, B->n);
+        }
+        sb_put(&o, S->buf + S->offs[i], S->offs[i + 1] - S->offs[i]);
+        offs[t + 1] = o.n;
+    }
+    free(cdf);
+    out->buf = o.b ? o.b : (char*)malloc(1); out->offs = offs; out->n = n;
+    return 0;
+}

@@ -177,7 +177,25 @@ struct RouteArgs {
     uint64_t cap;             // capacity of out_fid / out_dest
 };
 
+// Batched emqx_topic:match/2 (tm_rules_match): names x rules -> bitmap.
+struct RulesArgs {
+    const uint32_t* nwords;   // name word ids (rule dictionary; unknown = W_UNKNOWN)
+    const uint32_t* noff;     // n + 1
+    const uint8_t* nflag;     // bit 0: name starts with '$'
+    uint32_t n;
+    const uint32_t* rwords;
+    const uint32_t* roff;     // r + 1
+    const uint8_t* rflag;     // bit 0: rule starts with '+' or '#'
+    uint32_t r;
+    uint32_t dollar_rule;
+    uint32_t wpr;             // u32 words per name row = ceil(r / 32)
+    uint32_t* bits;
+};
+
 // kernel launchers (tm_kernels.hip)
+hipError_t launch_rules_match(const RulesArgs& a, hipStream_t s);
+hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const int64_t* idx, uint32_t n,
+                              const int64_t* dst_off, uint32_t* dst, hipStream_t s);
 hipError_t launch_route_count(const RouteArgs& a, hipStream_t s);
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);

@@ -975,7 +975,54 @@ __global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
     }
 }
 
+// ------------------------------------------ batched predicate (emqx_topic:match/2)
+
+// One thread per name, all rules: the word-by-word clauses of
+// emqx_topic:match/2 (src/emqx_topic.erl:74-87) -- equal words or a '+' rule
+// word advance, a trailing '#' matches the rest (zero words included), both
+// exhausted matches -- plus the binary form's '$' rule (:68-71) when asked.
+// Rule words are read by every thread at once (broadcast, L1/L2-resident).
+__global__ __launch_bounds__(256) void tm_rules_match(RulesArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t nb = a.noff[t], nl = a.noff[t + 1] - nb;
+    const bool dollar = a.dollar_rule && (a.nflag[t] & 1);
+    for (uint32_t w0 = 0; w0 < a.r; w0 += 32) {
+        uint32_t acc = 0;
+        const uint32_t w1 = min(a.r, w0 + 32);
+        for (uint32_t j = w0; j < w1; ++j) {
+            const uint32_t rb = a.roff[j], rl = a.roff[j + 1] - rb;
+            bool m = false;
+            if (!(dollar && (a.rflag[j] & 1))) {
+                uint32_t i = 0, k = 0;
+                for (;;) {
+                    if (i == nl && k == rl) { m = true; break; }
+                    const uint32_t fw = k < rl ? a.rwords[rb + k] : 0u;
+                    if (k + 1 == rl && fw == W_HASH) { m = true; break; }
+                    if (i == nl || k == rl) break;
+                    if (fw == W_PLUS || fw == a.nwords[nb + i]) { ++i; ++k; continue; }
+                    break;
+                }
+            }
+            acc |= (uint32_t)m << (j - w0);
+        }
+        a.bits[(uint64_t)t * a.wpr + w0 / 32] = acc;
+    }
+}
+
 // ------------------------------------------------ token batches (sharded mode)
+
+// Row gather for the sharded exchange: 16 lanes per row (rows are short: the
+// words of a topic, or one topic's match list), lanes stride over long rows.
+__global__ __launch_bounds__(256) void tm_gather_rows(const uint32_t* src, const int64_t* src_off, const int64_t* idx,
+                                                       uint32_t n, const int64_t* dst_off, uint32_t* dst) {
+    const uint64_t g = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const uint32_t sub = threadIdx.x & 15;
+    if (g >= n) return;
+    const int64_t r = idx[g];
+    const int64_t b = src_off[r], e = src_off[r + 1], d = dst_off[g];
+    for (int64_t i = sub; i < e - b; i += 16) dst[d + i] = src[b + i];
+}
 
 // Validates a device-resident token batch before any walk reads it (toff
 // monotone from 0 to nwords, deep topics flagged for the generic path) and
@@ -1112,6 +1159,18 @@ hipError_t launch_route_count(const RouteArgs& a, hipStream_t s) {
 
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s) {
     if (a.n) hipLaunchKernelGGL(tm_route_fill, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rules_match(const RulesArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_rules_match, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const int64_t* idx, uint32_t n,
+                              const int64_t* dst_off, uint32_t* dst, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_gather_rows, dim3((uint32_t)(((uint64_t)n * 16 + 255) / 256)), dim3(256), 0, s, src,
+                              src_off, idx, n, dst_off, dst);
     return hipGetLastError();
 }
 

@@ -40,7 +40,7 @@ class Tokens:
 class Batch:
     """A device-resident publish batch (tm_batch_prepare / launch / wait / result)."""
 
-    def __init__(self, eng: "Engine", topics=None, handle=None, n=0):
+    def __init__(self, eng: "Engine", topics=None, handle=None, n=0, dedup=False):
         self.eng = eng
         if handle is not None:          # built by Engine.prepare_tokens
             self.h = handle
@@ -52,9 +52,16 @@ class Batch:
         self._buf = np.ascontiguousarray(buf)
         self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
         h = C.c_void_p()
-        N.check(eng.L.tm_batch_prepare(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
-                                       C.byref(h)), "tm_batch_prepare")
+        N.check(eng.L.tm_batch_prepare_ex(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
+                                          N.TM_BATCH_DEDUP if dedup else 0, C.byref(h)), "tm_batch_prepare_ex")
         self.h = h
+
+    def row_map(self):
+        """-> (row_of uint32[n publishes], n_rows): result row of every publish."""
+        p = C.POINTER(C.c_uint32)()
+        nr = C.c_uint32()
+        N.check(self.eng.L.tm_batch_row_map(self.eng.h, self.h, C.byref(p), C.byref(nr)), "tm_batch_row_map")
+        return (np.ctypeslib.as_array(p, shape=(self.n,)).copy() if self.n else np.zeros(0, np.uint32)), nr.value
 
     def export(self, d_counts: int, d_ids: int, mul: int = 1, add: int = 0):
         """Per-topic counts and ids*mul+add into caller device buffers (tm_batch_export)."""
@@ -184,8 +191,9 @@ class Engine:
                 "tm_match_batch")
         return _result_arrays(r)
 
-    def prepare(self, topics) -> Batch:
-        return Batch(self, topics)
+    def prepare(self, topics, dedup: bool = False) -> Batch:
+        """Device-resident batch; dedup=True matches identical topics once (TM_BATCH_DEDUP)."""
+        return Batch(self, topics, dedup=dedup)
 
     # ---- routes (emqx_router + emqx_broker:aggre/1) -------------------------
     def route_add(self, topic: bytes, dest: int):
@@ -208,6 +216,25 @@ class Engine:
                 "tm_match_routes_batch")
         return _routes_arrays(r)
 
+    # ---- batched emqx_topic:match/2 (ACL / rewrite / tracer rules) -----------
+    def rules_match(self, names, rules, dollar_rule: bool = True) -> np.ndarray:
+        """-> bool[n, r]: emqx_topic:match(names[i], rules[j]) computed on the device
+        (dollar_rule: the binary form's '$' rule; False = word-list form, as ACL)."""
+        sn, sr = _pack(names), _pack(rules)
+        n, r = len(sn), len(sr)
+        if not n or not r:
+            return np.zeros((n, r), bool)
+        nb = np.ascontiguousarray(sn.buf if sn.buf.size else np.zeros(1, np.uint8))
+        no = np.ascontiguousarray(sn.offs.astype(np.uint64))
+        rb = np.ascontiguousarray(sr.buf if sr.buf.size else np.zeros(1, np.uint8))
+        ro = np.ascontiguousarray(sr.offs.astype(np.uint64))
+        wpr = (r + 31) // 32
+        bits = np.zeros(n * wpr, np.uint32)
+        N.check(self.L.tm_rules_match(self.h, nb.ctypes.data, no.ctypes.data, n, rb.ctypes.data, ro.ctypes.data, r,
+                                      int(dollar_rule), bits.ctypes.data), "tm_rules_match")
+        b = np.unpackbits(bits.view(np.uint8).reshape(n, wpr * 4), axis=1, bitorder="little")
+        return b[:, :r].astype(bool)
+
     # ---- bulk load / filter-sharded mode -----------------------------------
     def insert_many(self, filters, shard: int = 0, nshards: int = 1) -> int:
         """emqx_trie:insert/1 over a filter list; with nshards > 1 only this
@@ -218,6 +245,16 @@ class Engine:
         done = C.c_uint64()
         N.check(self.L.tm_trie_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), shard, nshards,
                                            C.byref(done)), "tm_trie_insert_many")
+        return int(done.value)
+
+    def delete_many(self, filters) -> int:
+        """emqx_trie:delete/1 over a filter list (one C call)."""
+        s = _pack(filters)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        done = C.c_uint64()
+        N.check(self.L.tm_trie_delete_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
+                "tm_trie_delete_many")
         return int(done.value)
 
     def dict_load(self, words):
@@ -260,6 +297,9 @@ class Engine:
         t = np.ascontiguousarray(tok.toff)
         f = np.ascontiguousarray(tok.tflags if len(tok.tflags) else np.zeros(1, np.uint8))
         return self.prepare_tokens(w.ctypes.data, t.ctypes.data, f.ctypes.data, len(tok), tok.nwords, False, batch)
+
+    def gather_rows(self, d_src: int, d_src_off: int, d_idx: int, n: int, d_dst_off: int, d_dst: int):
+        N.check(self.L.tm_gather_rows(self.h, d_src, d_src_off, d_idx, n, d_dst_off, d_dst), "tm_gather_rows")
 
     def tokens_shard(self, d_words: int, d_toff: int, n: int, nshards: int, d_shard: int):
         N.check(self.L.tm_tokens_shard(self.h, d_words, d_toff, n, nshards, d_shard), "tm_tokens_shard")

@@ -341,3 +341,60 @@ def gen_iot_topics(p: IotParams, tseed: int, n: int) -> Strings:
     cp = _ciot(p)
     _iot_lib().tm_gen_iot_topics(C.byref(cp), tseed, n, C.byref(cs))
     return _take(cs)
+
+
+# ---------------------------------------------------------------- C5 (skew + churn)
+
+@dataclass
+class SkewParams:
+    """Mirrors tm_skew_params (csrc/tm_gen.c): SURVEY.md §8d config C5."""
+    seed: int = 5
+    n_hot: int = 10_000
+    hot_depth: int = 10
+    vocab: int = 64
+    k_per_hot: int = 100
+
+
+class _CSkew(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_hot", C.c_uint32), ("hot_depth", C.c_uint32), ("vocab", C.c_uint32),
+                ("k_per_hot", C.c_uint32)]
+
+
+def _skew_lib():
+    L = _lib()
+    if not getattr(L, "_skew_bound", False):
+        L.tm_gen_skew.argtypes = [C.POINTER(_CSkew), C.POINTER(_CStrs), C.POINTER(_CStrs)]
+        L.tm_gen_derive_one.argtypes = [C.c_char_p, C.c_uint32, C.c_uint64, C.c_char_p, C.c_uint32]
+        L.tm_gen_pick.argtypes = [C.POINTER(_CStrs), C.POINTER(_CStrs), C.c_uint64, C.c_uint64, C.c_double,
+                                  C.c_double, C.POINTER(_CStrs)]
+        L._skew_bound = True
+    return L
+
+
+def gen_skew(p: SkewParams):
+    """-> (hot topics, filters derived from them: ~k_per_hot per hot topic)."""
+    h, f = _CStrs(), _CStrs()
+    cp = _CSkew(p.seed, p.n_hot, p.hot_depth, p.vocab, p.k_per_hot)
+    if _skew_lib().tm_gen_skew(C.byref(cp), C.byref(h), C.byref(f)) != 0:
+        raise ValueError("could not draw n_hot distinct hot topics")
+    return _take(h), _take(f)
+
+
+def derive_one(topic: bytes, seed: int) -> bytes:
+    out = C.create_string_buffer(8192)
+    n = _skew_lib().tm_gen_derive_one(topic, len(topic), seed, out, 8192)
+    return out.raw[:n] if n > 0 else b""
+
+
+def _cstrs(S: Strings):
+    b = np.ascontiguousarray(S.buf if S.buf.size else np.zeros(1, np.uint8))
+    o = np.ascontiguousarray(S.offs)
+    return _CStrs(b.ctypes.data, o.ctypes.data_as(C.POINTER(C.c_uint64)), len(S)), (b, o)
+
+
+def gen_pick(A: Strings, B: Strings, seed: int, n: int, p_a: float, zipf_s: float) -> Strings:
+    ca, keep_a = _cstrs(A)
+    cb, keep_b = _cstrs(B)
+    out = _CStrs()
+    _skew_lib().tm_gen_pick(C.byref(ca), C.byref(cb), seed, n, p_a, zipf_s, C.byref(out))
+    return _take(out)

@@ -130,6 +130,22 @@ class ShardedMatcher:
         dist.all_to_all_single(out, x.contiguous(), recv, send, group=self.group)
         return out
 
+    def _gather(self, src: torch.Tensor, src_off: torch.Tensor, idx: torch.Tensor, lens: torch.Tensor):
+        """Rows src[src_off[idx[i]] .. src_off[idx[i]+1]) concatenated -> (dst, dst_off int64 [n+1])."""
+        n = idx.numel()
+        dst_off = torch.zeros(n + 1, dtype=torch.int64, device=src.device)
+        if n:
+            dst_off[1:] = torch.cumsum(lens, 0)
+        total = int(dst_off[-1].item())
+        if self._local_match is not None or src.device.type != "cuda":   # CPU tests
+            return gather_segments(src, src_off[idx], lens), dst_off
+        dst = torch.empty(total, dtype=src.dtype, device=src.device)
+        if n and total:
+            torch.cuda.current_stream(src.device).synchronize()
+            self.eng.gather_rows(src.data_ptr(), src_off.data_ptr(), idx.data_ptr(), n, dst_off.data_ptr(),
+                                 dst.data_ptr())
+        return dst, dst_off
+
     # ---- one step ------------------------------------------------------------
     def step(self, words: torch.Tensor, toff: torch.Tensor, tflags: torch.Tensor):
         """words int32 (u32 bits), toff int32 [n+1], tflags uint8 [n], all on this
@@ -137,23 +153,29 @@ class ShardedMatcher:
         row t = the sorted, deduplicated global ids of the filters matching topic t."""
         G, dev = self.world, self.dev
         n = toff.numel() - 1
+        if G == 1:   # one shard holds every filter: no exchange, no reorder
+            counts, gids = self._match(words, toff, tflags)
+            row_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            if n:
+                row_off[1:] = torch.cumsum(counts.to(torch.int64), 0)
+            self.last.update(sent_topics=[n], recv_topics=[n], local_matches=int(gids.numel()))
+            return row_off, gids
         shard = self._shards(words, toff, n).to(torch.int64)
         owner = torch.where(shard == G, torch.full_like(shard, self.rank), shard)
-        order = torch.argsort(owner, stable=True)
-        depth = (toff[1:] - toff[:-1]).to(torch.int64)
+        # counting sort by owner (G is small): publishes grouped per destination
+        order = torch.cat([torch.nonzero(owner == g).flatten() for g in range(G)])
+        toff64 = toff.to(torch.int64)
+        depth = toff64[1:] - toff64[:-1]
         depth_o = depth[order]
         send_t = torch.bincount(owner, minlength=G)
         send_w = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, owner, depth)
         meta_o = ((depth_o << META_SHIFT) | tflags[order].to(torch.int64)).to(torch.int32)
-        words_o = gather_segments(words, toff[:-1].to(torch.int64)[order], depth_o)
+        words_o, _ = self._gather(words, toff64, order, depth_o)
 
         sizes = torch.stack([send_t, send_w], 1)
-        if G > 1:
-            hs = sizes.cpu() if self._stage else sizes
-            rsizes = torch.empty_like(hs)
-            dist.all_to_all_single(rsizes, hs, group=self.group)
-        else:
-            rsizes = sizes
+        hs = sizes.cpu() if self._stage else sizes
+        rsizes = torch.empty_like(hs)
+        dist.all_to_all_single(rsizes, hs, group=self.group)
         st, sw = send_t.tolist(), send_w.tolist()
         rt, rw = rsizes[:, 0].tolist(), rsizes[:, 1].tolist()
         r_meta = self._a2a(meta_o, st, rt)
@@ -179,10 +201,10 @@ class ShardedMatcher:
         counts_orig[order] = c_o
         inv = torch.empty_like(order)
         inv[order] = torch.arange(n, device=dev)
-        row_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        off_o = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         if n:
-            row_off[1:] = torch.cumsum(counts_orig, 0)
-        gids_final = gather_segments(gids_o, excl_cumsum(c_o)[inv], counts_orig)
+            off_o[1:] = torch.cumsum(c_o, 0)
+        gids_final, row_off = self._gather(gids_o, off_o, inv, counts_orig)
         self.last.update(sent_topics=st, recv_topics=rt, local_matches=int(gids.numel()))
         return row_off, gids_final
 

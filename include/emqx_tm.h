@@ -142,6 +142,17 @@ TM_API int  tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* 
  * wait    = block until done; result = D2H of the CSR. */
 TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
                       uint32_t n, tm_batch** out);
+/* tm_batch_prepare with flags.  TM_BATCH_DEDUP: identical topics of the batch
+ * are matched once (hot-topic skew, BASELINE config C5); the result then has
+ * one row per DISTINCT topic (tm_result.n_topics = distinct count) and
+ * tm_batch_row_map gives the row of every publish. */
+#define TM_BATCH_DEDUP 1u
+TM_API int  tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                uint32_t flags, tm_batch** out);
+/* row_of[i] = result row of publish i (identity for batches without
+ * TM_BATCH_DEDUP); *n_rows = number of result rows.  Engine-owned memory,
+ * valid until the batch is re-prepared or freed. */
+TM_API int  tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_t* n_rows);
 TM_API int  tm_batch_launch(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_wait(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out);
@@ -189,6 +200,10 @@ TM_API int  tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uin
  * NULL) counts them.  Stops at the first error. */
 TM_API int  tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets,
                                 uint32_t n, uint32_t shard, uint32_t nshards, uint64_t* n_inserted);
+/* emqx_trie:delete/1 over n filters; *n_deleted (may be NULL) counts the calls
+ * made.  Stops at the first error. */
+TM_API int  tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
+                                uint64_t* n_deleted);
 /* Interns n words in order (the shared dictionary of the sharded mode).  Words
  * must not contain '/'; '', "+" and "#" have fixed ids and are skipped. */
 TM_API int  tm_dict_load(tm_engine* e, const uint8_t* words, const uint64_t* offsets, uint32_t n);
@@ -224,6 +239,12 @@ TM_API int  tm_tokens_shard(tm_engine* e, const uint32_t* d_words, const uint32_
 TM_API int  tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_ids,
                             uint32_t mul, uint32_t add);
 
+/* Device row gather (the exchange's reorder step): for i < n, copies the u32
+ * row src[src_off[idx[i]] .. src_off[idx[i] + 1]) to dst[dst_off[i] ..).  All
+ * pointers are device memory; offsets and indices are int64.  Returns when done. */
+TM_API int  tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d_src_off, const int64_t* d_idx,
+                           uint32_t n, const int64_t* d_dst_off, uint32_t* d_dst);
+
 /* ---- filters ---------------------------------------------------------- */
 /* Bytes of a filter id returned by a match (the #trie_node.topic binary). */
 TM_API const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len);
@@ -239,6 +260,18 @@ TM_API int  tm_topic_wildcard(const uint8_t* topic, size_t len);
  * one of "empty_topic", "topic_too_long", "topic_invalid_#",
  * "topic_invalid_char", "topic_name_error". */
 TM_API int  tm_topic_validate(int is_name, const uint8_t* topic, size_t len, const char** reason);
+
+/* Batched predicate on the device: emqx_topic:match(Name_i, Rule_j) for n
+ * names x r rule filters -- the pairwise callers that do not use the trie:
+ * ACL rules (src/emqx_access_rule.erl:124-139, word-list form: dollar_rule = 0),
+ * rewrite rules (src/emqx_mod_rewrite.erl:86-90) and topic tracers
+ * (src/emqx_tracer.erl:142-151), both binary form: dollar_rule = 1 (a name
+ * starting with '$' never matches a filter starting with '+' or '#',
+ * src/emqx_topic.erl:68-71).  bits (host memory, n * ceil(r/32) u32): bit j%32
+ * of word i*ceil(r/32) + j/32 = match(name i, rule j). */
+TM_API int  tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* name_offsets, uint32_t n,
+                           const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule,
+                           uint32_t* bits);
 
 /* ---- diagnostics ------------------------------------------------------ */
 /* Text of the last TM_EIO on this thread (HIP error string + call site). */

@@ -1,0 +1,48 @@
+"""C5 workload tooling and TM_BATCH_DEDUP on the host (no device)."""
+
+from emqx_amd import gen
+from emqx_amd.engine import Engine
+from emqx_amd.skew import Churn, workload
+from oracle import oracle as O
+
+
+def test_derived_filters_match_their_hot_topic():
+    p = gen.SkewParams(seed=2, n_hot=40, k_per_hot=30)
+    hot, derived = gen.gen_skew(p)
+    H = hot.tolist()
+    assert len(set(H)) == 40
+    per = {h: 0 for h in H}
+    for f in derived.tolist():
+        hits = [h for h in H if O.match(h, f)]
+        assert hits
+        for h in hits:
+            per[h] += 1
+    assert min(per.values()) >= 25
+
+
+def test_workload_skew_and_dedup_rows():
+    p = gen.SkewParams(seed=3, n_hot=100, k_per_hot=5)
+    allf, derived, hot, pubs = workload(p, 500, 20_000, seed=3, background_pool=3000)
+    T = pubs.tolist()
+    hot_set = set(hot.tolist())
+    frac = sum(t in hot_set for t in T) / len(T)
+    assert 0.85 < frac < 0.95
+    e = Engine(device=-1)
+    b = e.prepare(pubs, dedup=True)
+    row_of, n_rows = b.row_map()
+    assert n_rows == len(set(T))
+    first = {}
+    for i, r in enumerate(row_of.tolist()):
+        assert first.setdefault(r, T[i]) == T[i]
+    assert sorted(first) == list(range(n_rows))
+
+
+def test_churn_keeps_live_set_consistent():
+    p = gen.SkewParams(seed=4, n_hot=20, k_per_hot=10)
+    hot, derived = gen.gen_skew(p)
+    c = Churn(hot, derived.tolist(), seed=1)
+    n0 = len(c.live)
+    dels, adds = c.step(50)
+    assert len(dels) == 25 and len(adds) == 25
+    assert len(c.live) == n0 and len(c.live_set) == n0
+    assert not (set(dels) & c.live_set) and set(adds) <= c.live_set
