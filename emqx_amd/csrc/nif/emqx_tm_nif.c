@@ -30,7 +30,7 @@ typedef struct {
 
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_UNDEFINED, ATOM_ROOT,
     ATOM_TRIE_NODE, ATOM_NODE_NOT_FOUND, ATOM_ENOMEM, ATOM_EIO, ATOM_EINVAL, ATOM_ENODEV,
-    ATOM_EOVERFLOW;
+    ATOM_EOVERFLOW, ATOM_NOT_FOUND;
 
 static void engine_dtor(ErlNifEnv* env, void* obj) {
     (void)env;
@@ -156,33 +156,130 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     return rows_to_terms(env, r->e, &res, 0);
 }
 
-/* match_batch(Engine, [Topic]) -> [[Filter]]  (one device pipeline per call) */
-static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-    engine_res* r;
+/* Concatenates a list of binaries: buf/offs are enif_alloc'ed (caller frees). */
+static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, unsigned* n_out, uint8_t** buf_out, uint64_t** offs_out) {
     unsigned n;
-    (void)argc;
-    if (!get_engine(env, argv[0], &r) || !enif_get_list_length(env, argv[1], &n)) return enif_make_badarg(env);
+    if (!enif_get_list_length(env, list, &n)) return 0;
     uint64_t* offs = enif_alloc(sizeof(uint64_t) * (n + 1));
     ErlNifBinary* bins = enif_alloc(sizeof(ErlNifBinary) * (n ? n : 1));
-    ERL_NIF_TERM head, tail = argv[1];
+    ERL_NIF_TERM head, tail = list;
     uint64_t total = 0;
     offs[0] = 0;
     for (unsigned i = 0; i < n; i++) {
         if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_inspect_binary(env, head, &bins[i])) {
             enif_free(offs); enif_free(bins);
-            return enif_make_badarg(env);
+            return 0;
         }
         total += bins[i].size;
         offs[i + 1] = total;
     }
     uint8_t* buf = enif_alloc(total ? total : 1);
     for (unsigned i = 0; i < n; i++) memcpy(buf + offs[i], bins[i].data, bins[i].size);
+    enif_free(bins);
+    *n_out = n; *buf_out = buf; *offs_out = offs;
+    return 1;
+}
+
+/* match_batch(Engine, [Topic]) -> [[Filter]]  (one device pipeline per call) */
+static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    uint8_t* buf;
+    uint64_t* offs;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
     tm_result res;
     int rc = tm_match_batch(r->e, buf, offs, n, &res);
-    enif_free(buf); enif_free(bins); enif_free(offs);
+    enif_free(buf); enif_free(offs);
     if (rc) return err(env, rc);
     ERL_NIF_TERM out = enif_make_list(env, 0);
     for (unsigned i = n; i-- > 0;) out = enif_make_list_cell(env, rows_to_terms(env, r->e, &res, i), out);
+    return out;
+}
+
+/* route_add(Engine, Topic, DestId) -> ok  (emqx_router:do_add_route/2 after the
+ * mnesia transaction committed; DestId = the aggre/1 destination's id: the node,
+ * or the share group, src/emqx_broker.erl:250-261) */
+static ERL_NIF_TERM nif_route_add(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    unsigned dest;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b) || !enif_get_uint(env, argv[2], &dest))
+        return enif_make_badarg(env);
+    int rc = tm_route_add(r->e, b.data, b.size, dest);
+    return rc ? err(env, rc) : ATOM_OK;
+}
+
+/* route_delete(Engine, Topic, DestId) -> ok | {error, not_found}  (do_delete_route/2) */
+static ERL_NIF_TERM nif_route_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    unsigned dest;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b) || !enif_get_uint(env, argv[2], &dest))
+        return enif_make_badarg(env);
+    int rc = tm_route_delete(r->e, b.data, b.size, dest);
+    if (rc == TM_ENOENT) return enif_make_tuple2(env, ATOM_ERROR, ATOM_NOT_FOUND);
+    return rc ? err(env, rc) : ATOM_OK;
+}
+
+/* match_routes_batch(Engine, [Topic]) -> [[{Filter, DestId}]]
+ * (aggre(emqx_router:match_routes(T)) per publish, resolved on the device) */
+static ERL_NIF_TERM nif_match_routes_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    uint8_t* buf;
+    uint64_t* offs;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
+    tm_routes res;
+    int rc = tm_match_routes_batch(r->e, buf, offs, n, &res);
+    enif_free(buf); enif_free(offs);
+    if (rc) return err(env, rc);
+    ERL_NIF_TERM out = enif_make_list(env, 0);
+    for (unsigned i = n; i-- > 0;) {
+        ERL_NIF_TERM row = enif_make_list(env, 0);
+        for (uint32_t k = res.row_offsets[i + 1]; k-- > res.row_offsets[i];) {
+            size_t len = 0;
+            const uint8_t* p = tm_filter_bytes(r->e, res.filter_ids[k], &len);
+            row = enif_make_list_cell(env, enif_make_tuple2(env, make_bin(env, p, len), enif_make_uint(env, res.dests[k])),
+                                      row);
+        }
+        out = enif_make_list_cell(env, row, out);
+    }
+    return out;
+}
+
+/* rules_match(Engine, [Name], [Rule], DollarRule) -> [[RuleIndex]]
+ * emqx_topic:match/2 of every name against every rule on the device (ACL rules
+ * with DollarRule = false, rewrite / tracer filters with true); per name the
+ * 0-based indices of the matching rules in rule order, so an ACL caller takes
+ * the first whose `who` also matches (src/emqx_access_rule.erl:91-99). */
+static ERL_NIF_TERM nif_rules_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n, nr;
+    uint8_t *nb, *rb;
+    uint64_t *no, *ro;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r)) return enif_make_badarg(env);
+    int dollar = enif_is_identical(argv[3], ATOM_TRUE);
+    if (!dollar && !enif_is_identical(argv[3], ATOM_FALSE)) return enif_make_badarg(env);
+    if (!pack_binaries(env, argv[1], &n, &nb, &no)) return enif_make_badarg(env);
+    if (!pack_binaries(env, argv[2], &nr, &rb, &ro)) { enif_free(nb); enif_free(no); return enif_make_badarg(env); }
+    const unsigned wpr = (nr + 31) / 32;
+    uint32_t* bits = enif_alloc(sizeof(uint32_t) * ((size_t)n * wpr + 1));
+    int rc = tm_rules_match(r->e, nb, no, n, rb, ro, nr, dollar, bits);
+    enif_free(nb); enif_free(no); enif_free(rb); enif_free(ro);
+    if (rc) { enif_free(bits); return err(env, rc); }
+    ERL_NIF_TERM out = enif_make_list(env, 0);
+    for (unsigned i = n; i-- > 0;) {
+        ERL_NIF_TERM row = enif_make_list(env, 0);
+        for (unsigned j = nr; j-- > 0;)
+            if (bits[(size_t)i * wpr + j / 32] >> (j % 32) & 1u) row = enif_make_list_cell(env, enif_make_uint(env, j), row);
+        out = enif_make_list_cell(env, row, out);
+    }
+    enif_free(bits);
     return out;
 }
 
@@ -211,6 +308,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
     ATOM_EINVAL = enif_make_atom(env, "einval");
     ATOM_ENODEV = enif_make_atom(env, "enodev");
     ATOM_EOVERFLOW = enif_make_atom(env, "eoverflow");
+    ATOM_NOT_FOUND = enif_make_atom(env, "not_found");
     return 0;
 }
 
@@ -222,6 +320,10 @@ static ErlNifFunc funcs[] = {
     {"empty", 1, nif_empty, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_batch", 2, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"route_delete", 3, nif_route_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_routes_batch", 2, nif_match_routes_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"rules_match", 4, nif_rules_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"topic_match", 2, nif_topic_match, 0},
 };
 

@@ -94,8 +94,11 @@ struct Node {
 // Tables under 4 GiB are read with raw buffer loads (a wave-uniform descriptor
 // built from kernel arguments): four dwordx4 that the compiler cannot narrow,
 // issued back to back.  Larger tables use plain global loads.
+#ifndef TM_PROBE_CPOL
+#define TM_PROBE_CPOL 0     // cache-policy bits of the bucket loads (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+#endif
 __device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, TM_PROBE_CPOL);
     return uint4{v[0], v[1], v[2], v[3]};
 }
 

@@ -14,6 +14,10 @@
         , match/2
         , match_batch/2
         , topic_match/2
+        , route_add/3
+        , route_delete/3
+        , match_routes_batch/2
+        , rules_match/4
         ]).
 
 -on_load(init/0).
@@ -55,3 +59,22 @@ match_batch(_Engine, _Topics) -> erlang:nif_error(nif_not_loaded).
 %% emqx_topic:match/2 on binaries
 -spec(topic_match(binary(), binary()) -> boolean()).
 topic_match(_Name, _Filter) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_router:do_add_route/2 after the mnesia transaction committed.
+%% DestId: the caller's id of the route's aggre/1 destination (node(), or the
+%% share Group of a {Group, Node} dest), src/emqx_broker.erl:250-261.
+-spec(route_add(reference(), binary(), non_neg_integer()) -> ok | {error, term()}).
+route_add(_Engine, _Topic, _DestId) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_router:do_delete_route/2 after the commit.
+-spec(route_delete(reference(), binary(), non_neg_integer()) -> ok | {error, term()}).
+route_delete(_Engine, _Topic, _DestId) -> erlang:nif_error(nif_not_loaded).
+
+%% aggre(match_routes(Topic)) for a batch of publishes, resolved on the device.
+-spec(match_routes_batch(reference(), [binary()]) -> [[{binary(), non_neg_integer()}]]).
+match_routes_batch(_Engine, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_topic:match/2 of every name against every rule (ACL: DollarRule = false,
+%% rewrite / tracer filters: true); per name the indices of the matching rules.
+-spec(rules_match(reference(), [binary()], [binary()], boolean()) -> [[non_neg_integer()]]).
+rules_match(_Engine, _Names, _Rules, _DollarRule) -> erlang:nif_error(nif_not_loaded).
