@@ -259,6 +259,30 @@ def run_c5(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
+def e2e_rate(eng, sub, reps: int = 3) -> dict:
+    """tm_match_batch over `sub` from host bytes to the host CSR, best of `reps`
+    after one warm-up call (pinned result buffers sized)."""
+    import ctypes as C
+
+    from emqx_amd import _native as N
+    buf = np.ascontiguousarray(sub.buf)
+    offs = np.ascontiguousarray(sub.offs.astype(np.uint64))
+    r = N.Result()
+
+    def call():
+        N.check(eng.L.tm_match_batch(eng.h, buf.ctypes.data, offs.ctypes.data, len(sub), C.byref(r)), "tm_match_batch")
+
+    call()
+    best = float("inf")
+    for _ in range(reps):
+        t = time.perf_counter()
+        call()
+        best = min(best, time.perf_counter() - t)
+    return {"publishes_per_s": len(sub) / best, "topics": len(sub), "ms": 1e3 * best,
+            "bytes_in": int(offs[-1] - offs[0]), "matches_out": int(r.n_matches),
+            "path": "tm_match_batch: H2D bytes, device tokeniser, match, D2H CSR (best of %d)" % reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +292,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--latency-batches", type=int, default=200)
+    ap.add_argument("--e2e-topics", type=int, default=10_000_000,
+                    help="publishes of the host-inclusive end-to-end measurement")
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (no latency / e2e / cpu legs): for rocprofv3 runs")
     ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
@@ -313,9 +339,12 @@ def main():
 
     t0 = time.time()
     b = eng.prepare(topics)
-    log(f"[rank {rank}] batch tokenised + resident in HBM in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] batch bytes resident in HBM in {time.time() - t0:.1f}s")
 
-    for _ in range(args.warmup):
+    # the first launch tokenises the resident bytes on the device (tm_tok_*);
+    # the timed steps reuse the tokens (the dictionary does not change), so a
+    # step is the trie walk + CSR over a tokenised batch already in HBM
+    for _ in range(max(args.warmup, 1)):
         b.launch().wait()
     st = b.stats()
     if st["topics"] != len(topics):
@@ -409,12 +438,11 @@ def main():
         except Exception as e:  # report, don't hide
             out["p99_batch_ms"] = None
             out["latency_error"] = str(e)
-        # host-inclusive end to end: topic bytes in host RAM -> sorted CSR in host RAM
-        sub = topics.slice(0, min(n, 2_000_000))
-        eng.match_batch(sub)
-        t = time.perf_counter()
-        eng.match_batch(sub)
-        out["e2e_host_publishes_per_s"] = len(sub) / (time.perf_counter() - t)
+        # host-inclusive end to end, timed at the C ABI (tm_match_batch): topic
+        # bytes in host RAM -> H2D -> device tokenise -> match -> sorted CSR in
+        # the engine's pinned host buffers (what a NIF hands to the broker)
+        out["e2e"] = e2e_rate(eng, topics.slice(0, min(n, args.e2e_topics)))
+        out["e2e_host_publishes_per_s"] = out["e2e"]["publishes_per_s"]
 
     b.free()
 

@@ -25,6 +25,7 @@ TM_EABORT = -125
 TM_NONE = 0xFFFFFFFF
 TM_MAX_TOPIC_LEN = 4096
 TM_CFG_FROZEN_DICT = 1
+TM_CFG_HOST_TOKENIZE = 2
 TM_BATCH_DEDUP = 1
 
 _ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
@@ -107,6 +108,7 @@ SIGNATURES = {
     "tm_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
     "tm_filter_shard": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_tokenize": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64)]),
+    "tm_tokenize_device": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64)]),
     "tm_batch_prepare_tokens": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint64, C.c_int, C.POINTER(P)]),
     "tm_gather_rows": (C.c_int, [P, P, P, P, C.c_uint32, P, P]),
     "tm_tokens_shard": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, P]),

@@ -43,24 +43,24 @@ char* last_error() {
     return buf;
 }
 
+// word hash (tm_internal.hpp hw_*; the device tokeniser computes the same)
 inline uint64_t hash_bytes(const uint8_t* p, size_t n) {
-    uint64_t h = 0xcbf29ce484222325ull ^ (n * 0x9E3779B97F4A7C15ull);
+    uint64_t h = hw_init(n);
     size_t i = 0;
     for (; i + 8 <= n; i += 8) {
         uint64_t v;
         memcpy(&v, p + i, 8);
-        h = (h ^ (v * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
-        h ^= h >> 29;
+        h = hw_mix(h, v);
     }
     uint64_t t = 0;
     for (size_t k = 0; i < n; ++i, ++k) t |= (uint64_t)p[i] << (8 * k);
-    h = (h ^ (t * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
-    h ^= h >> 31;
-    return h | 1;  // 0 = empty slot
+    return hw_final(h, t);
 }
 
 // ------------------------------------------------------------- word interner
-// Open-addressed string -> id map; bytes live in an append-only arena.
+// Open-addressed string -> id map; bytes live in an append-only arena.  The
+// table is mirrored verbatim in HBM for the device tokeniser: dirty_ lists the
+// slots written since the last upload, gen_ counts rehashes (full upload).
 class WordDict {
   public:
     WordDict() { rehash(1024); }
@@ -69,7 +69,7 @@ class WordDict {
         const uint64_t h = hash_bytes(p, n);
         size_t i = h & mask_;
         for (;;) {
-            const Ent& e = tab_[i];
+            const DictEnt& e = tab_[i];
             if (e.h == 0) return W_UNKNOWN;
             if (e.h == h && e.len == n && memcmp(arena_.data() + e.off, p, n) == 0) return e.id;
             i = (i + 1) & mask_;
@@ -84,36 +84,39 @@ class WordDict {
         const uint64_t h = hash_bytes(p, n);
         size_t i = h & mask_;
         while (tab_[i].h) i = (i + 1) & mask_;
-        tab_[i] = Ent{h, arena_.size(), (uint32_t)n, id};
+        tab_[i] = DictEnt{h, arena_.size(), (uint32_t)n, id};
+        dirty_.push_back((uint32_t)i);
         arena_.insert(arena_.end(), p, p + n);
         ++count_;
         return id;
     }
 
     size_t size() const { return count_; }
+    const std::vector<DictEnt>& table() const { return tab_; }
+    const std::vector<uint8_t>& arena() const { return arena_; }
+    uint64_t gen() const { return gen_; }
+    std::vector<uint32_t>& dirty() { return dirty_; }
 
   private:
-    struct Ent {
-        uint64_t h;
-        uint64_t off;
-        uint32_t len;
-        uint32_t id;
-    };
     void rehash(size_t cap) {
-        std::vector<Ent> old;
+        std::vector<DictEnt> old;
         old.swap(tab_);
-        tab_.assign(cap, Ent{0, 0, 0, 0});
+        tab_.assign(cap, DictEnt{0, 0, 0, 0});
         mask_ = cap - 1;
-        for (const Ent& e : old)
+        for (const DictEnt& e : old)
             if (e.h) {
                 size_t i = e.h & mask_;
                 while (tab_[i].h) i = (i + 1) & mask_;
                 tab_[i] = e;
             }
+        dirty_.clear();
+        ++gen_;
     }
-    std::vector<Ent> tab_;
+    std::vector<DictEnt> tab_;
     std::vector<uint8_t> arena_;
+    std::vector<uint32_t> dirty_;
     size_t mask_ = 0, count_ = 0;
+    uint64_t gen_ = 0;
     uint32_t next_id_ = W_FIRST;
 };
 
@@ -230,6 +233,17 @@ struct tm_batch {
     // device-resident tokens the generic-path list is built on the device
     bool tokens_only = false;
     bool dev_slow = false;
+    // device tokenisation: the topic bytes are uploaded by prepare and tokenised
+    // on the engine stream by the first launch, after the dictionary deltas; a
+    // later launch re-tokenises only if the dictionary grew meanwhile (ids of
+    // existing words never change), like the host path's re-tokenise
+    bool dev_tok = false;
+    uint64_t tok_dict = ~0ull;   // dict.size() the device tokens were made with
+    uint8_t* d_bytes = nullptr;
+    uint64_t* d_boffs = nullptr;
+    uint32_t* d_wcount = nullptr;
+    size_t c_bytes = 0, c_boffs = 0, c_wcount = 0;
+    uint64_t tok_base = 0;
     uint32_t *d_nslow = nullptr, *h_bad = nullptr;
     size_t c_nslow = 0, ch_bad = 0;
     // route resolution (tm_batch_routes)
@@ -245,6 +259,7 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
+        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount);
         if (h_bad) (void)hipHostFree(h_bad);
         h_bad = nullptr;
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
@@ -274,6 +289,7 @@ struct tm_engine {
     hipStream_t stream = nullptr;
 
     WordDict dict;
+    tm_batch tokb;   // staging of tm_tokenize_device
 
     // node table (host)
     std::vector<uint32_t> n_parent, n_word, n_ec, n_plus, n_hash, n_inslot, n_flen;
@@ -320,6 +336,18 @@ struct tm_engine {
     size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0, cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
     hipEvent_t ev_delta = nullptr;
     bool delta_inflight = false;
+    // device word dictionary (device tokeniser): verbatim table + arena
+    DictEnt* d_dict = nullptr;
+    size_t d_dict_n = 0;            // table slots on the device
+    uint64_t d_dict_gen = ~0ull;    // dict.gen() of the device table
+    uint8_t* d_arena = nullptr;
+    size_t c_arena = 0, arena_uploaded = 0;
+    uint32_t* h_dxidx = nullptr;
+    DictEnt* h_dxval = nullptr;
+    uint32_t* d_dxidx = nullptr;
+    DictEnt* d_dxval = nullptr;
+    size_t ch_dxidx = 0, ch_dxval = 0, cd_dxidx = 0, cd_dxval = 0;
+    bool dev_tok = true;            // TM_CFG_HOST_TOKENIZE / TM_HOST_TOKENIZE=1: tokenise on the host
 
     // slow-path scratch
     uint32_t s_waves = 512, s_qcap = 1u << 13, s_ocap = 1u << 14;
@@ -942,12 +970,60 @@ struct tm_engine {
             dirty_f.clear();
             async_used = true;
         }
+        if (dev_tok && (rc = sync_dict(pageable_used, async_used))) return rc;
         if (pageable_used) {
             // host vectors may be mutated / reallocated right after we return
             HIP_OK(hipStreamSynchronize(stream));
         } else if (async_used) {
             HIP_OK(hipEventRecord(ev_delta, stream));
             delta_inflight = true;
+        }
+        return TM_OK;
+    }
+
+    // word dictionary -> HBM: the whole table after a rehash, else the slots
+    // written since the last upload; the arena's new tail
+    int sync_dict(bool& pageable_used, bool& async_used) {
+        int rc;
+        const std::vector<DictEnt>& tab = dict.table();
+        const std::vector<uint8_t>& ar = dict.arena();
+        std::vector<uint32_t>& dx = dict.dirty();
+        if (d_dict_n != tab.size()) {
+            dev_free(d_dict);
+            HIP_OK(hipMalloc((void**)&d_dict, tab.size() * sizeof(DictEnt)));
+            d_dict_n = tab.size();
+            d_dict_gen = ~0ull;
+        }
+        if (d_dict_gen != dict.gen() || dx.size() > tab.size() / 8) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_dict, tab.data(), tab.size() * sizeof(DictEnt), hipMemcpyHostToDevice, stream));
+            d_dict_gen = dict.gen();
+            dx.clear();
+        } else if (!dx.empty()) {
+            const size_t nd = dx.size();
+            if ((rc = host_reserve(h_dxidx, ch_dxidx, nd))) return rc;
+            if ((rc = host_reserve(h_dxval, ch_dxval, nd))) return rc;
+            if ((rc = dev_reserve(d_dxidx, cd_dxidx, nd))) return rc;
+            if ((rc = dev_reserve(d_dxval, cd_dxval, nd))) return rc;
+            for (size_t k = 0; k < nd; ++k) {
+                h_dxidx[k] = dx[k];
+                h_dxval[k] = tab[dx[k]];
+            }
+            HIP_OK(hipMemcpyAsync(d_dxidx, h_dxidx, nd * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_dxval, h_dxval, nd * sizeof(DictEnt), hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_dict(d_dict, d_dxidx, d_dxval, (uint32_t)nd, stream));
+            dx.clear();
+            async_used = true;
+        }
+        if (c_arena < ar.size() + 1) {
+            if ((rc = dev_reserve(d_arena, c_arena, ar.size() + 1))) return rc;
+            arena_uploaded = 0;
+        }
+        if (ar.size() > arena_uploaded) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_arena + arena_uploaded, ar.data() + arena_uploaded, ar.size() - arena_uploaded,
+                                  hipMemcpyHostToDevice, stream));
+            arena_uploaded = ar.size();
         }
         return TM_OK;
     }
@@ -1077,6 +1153,40 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
+    // tm_tokenize_device: the device tokeniser into caller device arrays
+    int tokenize_device(const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* d_words, uint64_t cap,
+                        uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords) {
+        if (device < 0) return TM_ENODEV;
+        int rc;
+        tm_batch* b = &tokb;
+        const uint64_t base = offsets[0], nbytes = offsets[n] - base;
+        if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        if ((rc = sync_device())) return rc;
+        if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;
+        if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
+        if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
+        if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
+        if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, stream));
+        if (!n) HIP_OK(hipMemsetAsync(d_toff, 0, 4, stream));
+        TokArgs t{};
+        t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
+        t.dict = d_dict; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+        t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
+        t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
+        ScanArgs ts{};
+        ts.block_sums = b->d_bsums;
+        HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
+        HIP_OK(hipMemcpyAsync(b->h_total, b->d_nslow + 1, 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        *nwords = n ? b->h_total[0] : 0;
+        return *nwords > cap ? TM_EOVERFLOW : TM_OK;
+    }
+
     // tm_batch_prepare_tokens: a batch from tokenised arrays (host or device)
     int prepare_tokens(tm_batch* b, const uint32_t* words, const uint32_t* toff, const uint8_t* tflags, uint32_t n,
                        uint64_t nwords, bool on_device) {
@@ -1084,6 +1194,7 @@ struct tm_engine {
         b->n = n;
         b->nwords = nwords;
         b->tokens_only = true;
+        b->dev_tok = false;
         b->launched = b->done = false;
         b->bytes.clear();
         b->offs.clear();
@@ -1236,6 +1347,19 @@ struct tm_engine {
         b->dedup = (flags & TM_BATCH_DEDUP) != 0;
         b->n_pub = n;
         b->row_of.clear();
+        b->dev_tok = false;
+        if (device >= 0 && dev_tok) {
+            b->launched = b->done = false;
+            b->tokens_only = false;
+            if (b->dedup) {
+                dedup_topics(b, topics, offsets, n);
+                return upload_bytes(b, b->bytes.data(), b->offs.data(), b->n);
+            }
+            b->n = n;
+            b->bytes.clear();
+            b->offs.clear();
+            return upload_bytes(b, topics, offsets, n);
+        }
         if (b->dedup) {
             dedup_topics(b, topics, offsets, n);
         } else {
@@ -1253,10 +1377,36 @@ struct tm_engine {
         return upload_batch(b);
     }
 
+    // device tokenisation: the caller's bytes and offsets go to HBM now (the
+    // caller's buffers are only borrowed for the call); words are produced at launch
+    int upload_bytes(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
+        int rc;
+        const uint64_t base = offsets[0], nbytes = offsets[n] - base;
+        if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;   // u32 word offsets
+        b->tok_base = base;
+        b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
+        if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;   // +16: no tail reads past
+        if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(b->nwords, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
+        if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
+        b->dev_tok = true;
+        b->tok_dict = ~0ull;
+        b->dev_slow = true;
+        return reserve_outputs(b);
+    }
+
     int launch(tm_batch* b) {
         if (device < 0) return TM_ENODEV;
         int rc;
-        if (!b->tokens_only && b->dict_size != dict.size()) {   // new words since tokenisation
+        if (!b->tokens_only && !b->dev_tok && b->dict_size != dict.size()) {   // new words since tokenisation
             if ((rc = tokenize(b))) return rc;
             if ((rc = upload_batch(b))) return rc;
         }
@@ -1269,6 +1419,19 @@ struct tm_engine {
         }
         HIP_OK(hipMemsetAsync(b->d_ctrl, 0, CTRL_WORDS * 4, stream));
         HIP_OK(hipMemsetAsync(b->d_stats, 0, ST_N * 8, stream));
+        if (b->dev_tok && b->tok_dict != dict.size()) {
+            b->tok_dict = dict.size();
+            HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, stream));
+            TokArgs t{};
+            t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = b->tok_base; t.n = b->n;
+            t.dict = d_dict; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+            t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
+            t.words_cap = b->c_words;
+            t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
+            ScanArgs ts{};
+            ts.block_sums = b->d_bsums;
+            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
+        }
         MatchArgs a{};
         a.slots = d_slots;
         a.nbuckets = nbuckets();
@@ -1400,6 +1563,8 @@ struct tm_engine {
         if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
+        dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
+        if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');
         // root node id 0 (absent until the first add_path, like the reference)
         n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
         n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
@@ -1424,7 +1589,11 @@ struct tm_engine {
             (void)hipSetDevice(device);
             if (stream) (void)hipStreamSynchronize(stream);
             scratch.release();
+            tokb.release();
             dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
+            dev_free(d_dict); dev_free(d_arena); dev_free(d_dxidx); dev_free(d_dxval);
+            if (h_dxidx) (void)hipHostFree(h_dxidx);
+            if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
             dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
             dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl);
@@ -1493,7 +1662,7 @@ extern "C" {
 
 int tm_create(const tm_config* cfg, tm_engine** out) {
     if (!out) return TM_EINVAL;
-    if (cfg && (cfg->flags & ~TM_CFG_FROZEN_DICT)) return TM_EINVAL;
+    if (cfg && (cfg->flags & ~(TM_CFG_FROZEN_DICT | TM_CFG_HOST_TOKENIZE))) return TM_EINVAL;
     tm_engine* e = new (std::nothrow) tm_engine();
     if (!e) return TM_ENOMEM;
     int rc = e->init(cfg);
@@ -1847,6 +2016,19 @@ int tm_tokenize(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, ui
     std::lock_guard<std::recursive_mutex> g(e->mu);
     try {
         return e->tokenize_into(topics, offsets, n, words, words_cap, toff, tflags, nwords_out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_tokenize_device(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* d_words,
+                       uint64_t words_cap, uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords_out) {
+    if (!e || !offsets || !d_toff || !nwords_out || (n && (!topics || !d_words || !d_tflags))) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    try {
+        return e->tokenize_device(topics, offsets, n, d_words, words_cap, d_toff, d_tflags, nwords_out);
     } catch (...) {
         return TM_ENOMEM;
     }

@@ -214,6 +214,53 @@ hipError_t launch_tokens_shard(const uint32_t* words, const uint32_t* toff, uint
 hipError_t launch_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
                          uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add, hipStream_t s);
 
+// ------------------------------------------------------------ word dictionary
+// One entry of the word interner's open-addressed table (emqx_topic:words/1
+// tokens -> ids).  The host table is uploaded verbatim so the device tokeniser
+// probes exactly the host's slots; word bytes live in an append-only arena.
+struct DictEnt {
+    uint64_t h;      // hash_word(bytes) | 1; 0 = empty
+    uint64_t off;    // arena offset
+    uint32_t len;
+    uint32_t id;
+};
+static_assert(sizeof(DictEnt) == 24, "dictionary entry is 24 bytes");
+
+constexpr uint64_t HW_K0 = 0xcbf29ce484222325ull, HW_K1 = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t HW_M1 = 0xBF58476D1CE4E5B9ull, HW_M2 = 0x94D049BB133111EBull;
+__host__ __device__ inline uint64_t hw_init(uint64_t n) { return HW_K0 ^ (n * HW_K1); }
+__host__ __device__ inline uint64_t hw_mix(uint64_t h, uint64_t v) {
+    h = (h ^ (v * HW_M1)) * HW_M2;
+    return h ^ (h >> 29);
+}
+__host__ __device__ inline uint64_t hw_final(uint64_t h, uint64_t tail) {
+    h = (h ^ (tail * HW_M1)) * HW_M2;
+    return (h ^ (h >> 31)) | 1;   // 0 = empty slot
+}
+
+// Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
+// the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp
+// tokenize_range), against the uploaded dictionary.
+struct TokArgs {
+    const uint8_t* bytes;
+    const uint64_t* offs;     // n + 1 absolute offsets (caller's), minus base
+    uint64_t base;
+    uint32_t n;
+    const DictEnt* dict;
+    uint64_t dict_mask;       // table size - 1 (power of two)
+    const uint8_t* arena;
+    uint32_t* wcount;         // pass 1: words per topic
+    uint8_t* tflags;
+    uint32_t* toff;           // pass 2: word offsets (block-local scan of wcount, made global here)
+    const uint32_t* bsums;    // scan block offsets (tm_scan_sums)
+    uint32_t* words;
+    uint64_t words_cap;       // entries of words[]; nothing at or past it is written
+    uint32_t* slow_list;
+    uint32_t* d_nslow;
+};
+hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
+hipError_t launch_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n, hipStream_t s);
+
 // shard of a (w0, w1) literal prefix; host and device agree (tm_filter_shard)
 __host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uint32_t nshards) {
     return edge_hash(id0, id1) % nshards;

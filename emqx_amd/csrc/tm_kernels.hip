@@ -1091,6 +1091,121 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
     if (i < n) { foff[idx[i]] = off[i]; flen[idx[i]] = len[i]; }
 }
 
+// ------------------------------------------------------------ device tokeniser
+// emqx_topic:words/1 (src/emqx_topic.erl:150-164: binary:split on "/", '' / '+'
+// / '#' as their atoms) plus the engine's interning, on the device: the same
+// word entries (class << 29 | id), flags and generic-path list as the host
+// tokeniser (tm_engine.cpp tokenize_range).  One thread per topic; a batch is
+// a few hundred MB of bytes at most, so these kernels are a small fraction of
+// the PCIe copy that brings the bytes in.
+
+__device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint64_t n, bool& irregular) {
+    if (n == 0) return C_EMPTY;
+    if (c0 == '+') {
+        if (n > 1) irregular = true;
+        return C_ABOVE;
+    }
+    if (c0 < '#') return C_BELOW;
+    if (c0 < '+') return C_BETWEEN;
+    return C_ABOVE;
+}
+
+// pass 1: words per topic (1 + separators) and the topic flags
+__global__ __launch_bounds__(256) void tm_tok_count(TokArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n) return;
+    const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
+    const uint8_t* p = a.bytes;
+    uint32_t words = 1;
+    bool irregular = false;
+    uint64_t ws = b;
+    for (uint64_t i = b; i < e; ++i) {
+        if (p[i] == '/') {
+            if (i - ws > 1 && p[ws] == '+') irregular = true;
+            ++words;
+            ws = i + 1;
+        }
+    }
+    if (e - ws > 1 && p[ws] == '+') irregular = true;
+    uint8_t fl = 0;
+    if (e > b && p[b] == '$') fl |= TF_DOLLAR;
+    if (irregular || words > FAST_MAX_DEPTH) fl |= TF_SLOW;
+    a.wcount[t] = words;
+    a.tflags[t] = fl;
+}
+
+__device__ __forceinline__ uint64_t load_le(const uint8_t* p, uint32_t n) {
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < n; ++k) v |= (uint64_t)p[k] << (8 * k);
+    return v;
+}
+
+// id of word p[0..n) in the uploaded interner table (W_UNKNOWN if absent)
+__device__ uint32_t dict_find(const TokArgs& a, const uint8_t* p, uint32_t n) {
+    uint64_t h = hw_init(n);
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) h = hw_mix(h, load_le(p + i, 8));
+    h = hw_final(h, load_le(p + i, n - i));
+    uint64_t s = h & a.dict_mask;
+    for (uint64_t probe = 0; probe <= a.dict_mask; ++probe) {
+        const DictEnt* e = a.dict + s;
+        const uint64_t eh = e->h;
+        if (eh == 0) return W_UNKNOWN;
+        if (eh == h && e->len == n) {
+            const uint8_t* q = a.arena + e->off;
+            uint32_t k = 0;
+            while (k < n && q[k] == p[k]) ++k;
+            if (k == n) return e->id;
+        }
+        s = (s + 1) & a.dict_mask;
+    }
+    return W_UNKNOWN;
+}
+
+// pass 2 (after the scan of wcount into toff): word entries + generic-path list
+__global__ __launch_bounds__(256) void tm_tok_fill(TokArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    bool slow = false;
+    if (t < a.n) {
+        const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
+        const uint8_t* p = a.bytes;
+        uint64_t o = a.toff[t] + a.bsums[t / SCAN_TILE];   // tm_scan_local is block-local
+        a.toff[t] = (uint32_t)o;
+        uint64_t ws = b;
+        for (uint64_t i = b;; ++i) {
+            if (i == e || p[i] == '/') {
+                const uint32_t n = (uint32_t)(i - ws);
+                const uint8_t c0 = n ? p[ws] : 0;
+                bool irr = false;
+                const uint32_t cls = tok_class(c0, n, irr);
+                uint32_t id;
+                if (n == 0) id = W_EMPTY;
+                else if (n == 1 && c0 == '+') id = W_PLUS;
+                else if (n == 1 && c0 == '#') id = W_HASH;
+                else id = dict_find(a, p + ws, n);
+                if (o < a.words_cap) a.words[o] = (cls << WID_BITS) | id;
+                ++o;
+                if (i == e) break;
+                ws = i + 1;
+            }
+        }
+        slow = (a.tflags[t] & TF_SLOW) != 0;
+    }
+    const uint64_t m = __ballot(slow);
+    if (!m) return;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(a.d_nslow, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    if (slow) a.slow_list[base + prefix_count(m)] = t;
+}
+
+__global__ void tm_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) tab[idx[i]] = vals[i];
+}
+
 // ------------------------------------------------------------ launchers
 
 uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
@@ -1208,6 +1323,26 @@ hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* va
 hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx, const uint64_t* off,
                                 const uint32_t* len, uint32_t n, hipStream_t s) {
     if (n) hipLaunchKernelGGL(tm_scatter_fmeta, dim3((n + 255) / 256), dim3(256), 0, s, foff, flen, idx, off, len, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
+    if (!a.n) return hipGetLastError();
+    const uint32_t g = (a.n + 255) / 256;
+    hipLaunchKernelGGL(tm_tok_count, dim3(g), dim3(256), 0, s, a);
+    scan.count = a.wcount;
+    scan.row_off = a.toff;
+    scan.n = a.n;
+    const hipError_t e = launch_scan(scan, s, d_nwords);
+    if (e != hipSuccess) return e;
+    TokArgs f = a;
+    f.bsums = scan.block_sums;
+    hipLaunchKernelGGL(tm_tok_fill, dim3(g), dim3(256), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_scatter_dict, dim3((n + 255) / 256), dim3(256), 0, s, tab, idx, vals, n);
     return hipGetLastError();
 }
 

@@ -128,9 +128,11 @@ def _routes_arrays(r: N.Routes):
 
 
 class Engine:
-    def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0, frozen_dict: bool = False):
+    def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0, frozen_dict: bool = False,
+                 host_tokenize: bool = False):
         self.L = N.lib()
-        cfg = N.Config(device, init_slots, host_threads, N.TM_CFG_FROZEN_DICT if frozen_dict else 0)
+        flags = (N.TM_CFG_FROZEN_DICT if frozen_dict else 0) | (N.TM_CFG_HOST_TOKENIZE if host_tokenize else 0)
+        cfg = N.Config(device, init_slots, host_threads, flags)
         h = C.c_void_p()
         N.check(self.L.tm_create(C.byref(cfg), C.byref(h)), "tm_create")
         self.h = h
@@ -279,6 +281,26 @@ class Engine:
         N.check(self.L.tm_tokenize(self.h, buf.ctypes.data, offs.ctypes.data, n, words.ctypes.data, cap,
                                    toff.ctypes.data, tflags.ctypes.data, C.byref(nw)), "tm_tokenize")
         return Tokens(words[:nw.value], toff, tflags[:n])
+
+    def tokenize_device(self, topics, words_cap: int = None):
+        """tm_tokenize_device -> (words, toff, tflags) as torch tensors on this
+        engine's GPU (the device tokeniser tm_match_batch uses)."""
+        import torch
+        s = _pack(topics)
+        n = len(s)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        if words_cap is None:
+            words_cap = int(n + np.count_nonzero(s.buf == ord("/"))) if n else 0
+        dev = torch.device("cuda", self.device)
+        words = torch.zeros(max(words_cap, 1), dtype=torch.int32, device=dev)
+        toff = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+        tflags = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        nw = C.c_uint64()
+        N.check(self.L.tm_tokenize_device(self.h, buf.ctypes.data, offs.ctypes.data, n, words.data_ptr(), words_cap,
+                                          toff.data_ptr(), tflags.data_ptr(), C.byref(nw)), "tm_tokenize_device")
+        return words[:nw.value], toff, tflags[:n]
 
     def prepare_tokens(self, words: int, toff: int, tflags: int, n: int, nwords: int, on_device: bool,
                        batch: Batch = None) -> Batch:

@@ -61,6 +61,11 @@ typedef struct {
  * publish batches can be exchanged between devices.  tm_trie_insert of a filter
  * with a word outside the dictionary fails with TM_ENOENT. */
 #define TM_CFG_FROZEN_DICT 1u
+/* Tokenise + intern publish batches on the host (emqx_topic:words/1 on the
+ * CPU, then the word ids are copied to HBM) instead of the default device
+ * tokeniser, which copies the topic bytes and tokenises them in HBM against
+ * the device mirror of the word dictionary.  Results are identical. */
+#define TM_CFG_HOST_TOKENIZE 2u
 
 /* #trie_node{} view (include/emqx.hrl:98-103) */
 typedef struct {
@@ -137,8 +142,13 @@ TM_API int  tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* 
                     uint32_t n, tm_result* out);
 
 /* Split form for pipelining / device-resident benchmarking:
- * prepare = host tokenise+intern+H2D (emqx_topic:words/1, src/emqx_topic.erl:158-164);
- * launch  = enqueue the device pipeline (async);
+ * prepare = H2D of the topic bytes and offsets (default), or host tokenise +
+ *           intern + H2D of the word ids with TM_CFG_HOST_TOKENIZE
+ *           (emqx_topic:words/1, src/emqx_topic.erl:158-164);
+ * launch  = enqueue the device pipeline (async): with device tokenisation the
+ *           first launch tokenises the bytes in HBM against the dictionary
+ *           mirror, after the pending deltas; later launches reuse the tokens
+ *           unless the dictionary grew in between;
  * wait    = block until done; result = D2H of the CSR. */
 TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
                       uint32_t n, tm_batch** out);
@@ -219,6 +229,16 @@ TM_API int  tm_filter_shard(tm_engine* e, const uint8_t* filter, size_t len, uin
 TM_API int  tm_tokenize(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                         uint32_t* words, uint64_t words_cap, uint32_t* toff, uint8_t* tflags,
                         uint64_t* nwords_out);
+/* tm_tokenize on the device (the tokeniser tm_match_batch uses by default):
+ * the host topic bytes are copied to HBM and tokenised against the device
+ * mirror of the word dictionary into caller DEVICE buffers words[words_cap],
+ * toff[n+1], tflags[n] -- the same values tm_tokenize writes.  *nwords_out =
+ * total words; TM_EOVERFLOW (nothing past words_cap written) if > words_cap.
+ * Returns when done.  Replaces emqx_topic:words/1 (src/emqx_topic.erl:150-164)
+ * for a whole batch. */
+TM_API int  tm_tokenize_device(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                               uint32_t* d_words, uint64_t words_cap, uint32_t* d_toff, uint8_t* d_tflags,
+                               uint64_t* nwords_out);
 /* A batch from tokenised arrays (tm_tokenize layout).  on_device = 1: the
  * pointers are device memory of this engine's GPU (e.g. received from another
  * shard); they are copied (and validated on the device: TM_EINVAL for offsets
