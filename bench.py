@@ -278,7 +278,23 @@ def e2e_rate(eng, sub, reps: int = 3) -> dict:
         t = time.perf_counter()
         call()
         best = min(best, time.perf_counter() - t)
+    # stage breakdown through the split API (same work, separate calls)
+    h = C.c_void_p()
+    stages = {"prepare_h2d": [], "launch_wait": [], "result_d2h": []}
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        N.check(eng.L.tm_batch_prepare(eng.h, buf.ctypes.data, offs.ctypes.data, len(sub), C.byref(h)), "prepare")
+        t1 = time.perf_counter()
+        N.check(eng.L.tm_batch_launch(eng.h, h), "launch")
+        N.check(eng.L.tm_batch_wait(eng.h, h), "wait")
+        t2 = time.perf_counter()
+        N.check(eng.L.tm_batch_result(eng.h, h, C.byref(r)), "result")
+        t3 = time.perf_counter()
+        for k, v in zip(stages, (t1 - t0, t2 - t1, t3 - t2)):
+            stages[k].append(1e3 * v)
+    eng.L.tm_batch_free(eng.h, h)
     return {"publishes_per_s": len(sub) / best, "topics": len(sub), "ms": 1e3 * best,
+            "stages_ms": {k: min(v[1:]) for k, v in stages.items()},
             "bytes_in": int(offs[-1] - offs[0]), "matches_out": int(r.n_matches),
             "path": "tm_match_batch: H2D bytes, device tokeniser, match, D2H CSR (best of %d)" % reps}
 

@@ -1781,21 +1781,7 @@ int tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len, uint32_t* ids,
 }
 
 int tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_batch** out) {
-    if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
-    std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
-    if (rc) return rc;
-    tm_batch* b = new (std::nothrow) tm_batch();
-    if (!b) return TM_ENOMEM;
-    try {
-        rc = e->prepare(b, topics, offsets, n);
-    } catch (...) {
-        rc = TM_ENOMEM;
-    }
-    if (rc) { b->release(); delete b; return rc; }
-    HIP_OK(hipStreamSynchronize(e->stream));
-    *out = b;
-    return TM_OK;
+    return tm_batch_prepare_ex(e, topics, offsets, n, 0, out);
 }
 
 int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
@@ -1806,7 +1792,8 @@ int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* off
         int rc = e->set_device();
         if (rc) return rc;
     }
-    tm_batch* b = new (std::nothrow) tm_batch();
+    const bool fresh = *out == nullptr;   // non-NULL: re-prepared in place (buffers only grow)
+    tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *out;
     if (!b) return TM_ENOMEM;
     int rc;
     try {
@@ -1814,7 +1801,11 @@ int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* off
     } catch (...) {
         rc = TM_ENOMEM;
     }
-    if (rc) { b->release(); delete b; return rc; }
+    if (rc) {
+        if (fresh) { b->release(); delete b; }
+        else { b->launched = b->done = false; }
+        return rc;
+    }
     if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
     *out = b;
     return TM_OK;

@@ -149,7 +149,10 @@ TM_API int  tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* 
  *           first launch tokenises the bytes in HBM against the dictionary
  *           mirror, after the pending deltas; later launches reuse the tokens
  *           unless the dictionary grew in between;
- * wait    = block until done; result = D2H of the CSR. */
+ * wait    = block until done; result = D2H of the CSR.
+ * *out must be NULL (a new batch) or a batch of this engine, which is then
+ * re-prepared in place: its device and pinned buffers are reused and only
+ * grow, so a caller cycling a few batches allocates nothing in steady state. */
 TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
                       uint32_t n, tm_batch** out);
 /* tm_batch_prepare with flags.  TM_BATCH_DEDUP: identical topics of the batch
