@@ -259,6 +259,85 @@ def run_c5(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
+def run_dispatch(args, ws, rank, local, pg):
+    """Publish -> match -> fan-out on the device: the C2
+    trie and publishes, every filter with local subscribers (75% one, 24% 2-8,
+    64 hot filters with 4096 each; ids from a pool of 1M subscribers).  One step
+    = the match pipeline (tm_batch_launch/wait) + tm_batch_dispatch kept in HBM
+    (per-match delivery scan + the load-balanced subscriber copy)."""
+    from emqx_amd import gen
+    from emqx_amd.engine import Engine
+
+    p = gen.C2
+    filters = gen.gen_filters(p)
+    topics = gen.gen_topics(p, filters, 1000 + rank, args.topics)
+    eng = Engine(device=local)
+    fl = filters.tolist()
+    eng.insert_many(fl)
+    rng = np.random.default_rng(77)
+    u = rng.random(len(fl))
+    nsub = np.where(u < 0.75, 1, rng.integers(2, 9, len(fl)))
+    nsub[rng.choice(len(fl), 64, replace=False)] = 4096
+    t0 = time.time()
+    pool = rng.integers(0, 1_000_000, int(nsub.sum()), dtype=np.uint32)
+    k = 0
+    for f, c in zip(fl, nsub.tolist()):
+        for s in pool[k:k + c].tolist():
+            eng.subscribe(f, s)
+        k += c
+    log(f"[rank {rank}] {k} subscriptions in {time.time() - t0:.1f}s")
+    eng.sync()
+    b = eng.prepare(topics)
+    for _ in range(max(args.warmup, 1)):
+        b.launch().wait()
+        b.dispatch_device()
+    if pg is not None:
+        pg.barrier()
+    ms_match, ms_fill, ms_disp = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.launch().wait()
+        td = time.perf_counter()
+        total, fill_ms, *_ = b.dispatch_device()
+        ms_disp.append(1e3 * (time.perf_counter() - td))
+        ms_fill.append(fill_ms)
+        ms_match.append(b.stats()["ms_total"])
+    elapsed = time.perf_counter() - t0
+    if pg is not None:
+        import torch
+        pg.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = b.stats()
+    n, m = len(topics), int(st["matches"])
+    f_ms = float(np.mean(ms_fill))
+    alg = 8 * total + 20 * m          # read + write a subscriber id; ids[j], moff[j], soff[f] per entry
+    achieved = alg / (f_ms * 1e-3) / 1e9
+    out = {
+        "metric": "publishes matched + fanned out/sec (node), C2 trie with local subscribers",
+        "value": ws * n * args.steps / elapsed,
+        "unit": "publishes/s",
+        "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (seeded C2 generator + seeded subscriber counts)",
+        "config": {"workload": f"dispatch: C2 1M filters, {k} subscriptions, {n} publishes per GPU",
+                   "filters": len(fl), "subscriptions": k, "mode": "replicated"},
+        "deliveries_per_step": int(total),
+        "deliveries_per_s": ws * total * args.steps / elapsed,
+        "match_pipeline_ms": float(np.mean(ms_match)),
+        "dispatch_ms": float(np.mean(ms_disp)),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tm_fan_fill",
+                     "kernel_ms": f_ms, "alg_bytes_per_launch": alg},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def e2e_rate(eng, sub, reps: int = 3) -> dict:
     """tm_match_batch over `sub` from host bytes to the host CSR, best of `reps`
     after one warm-up call (pinned result buffers sized)."""
@@ -312,7 +391,7 @@ def main():
                     help="publishes of the host-inclusive end-to-end measurement")
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (no latency / e2e / cpu legs): for rocprofv3 runs")
-    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "dispatch"], default="c2",
                     help="c2: 1M wildcard filters, replicated (the BASELINE metric); c4: IoT filters, sharded; "
                          "c5: hot-topic skew + churn")
     ap.add_argument("--c5-k", type=int, default=100, help="C5 filters per hot topic (10 / 100 / 1000)")
@@ -334,6 +413,8 @@ def main():
         return run_c4(args, ws, rank, local, pg)
     if args.workload == "c5":
         return run_c5(args, ws, rank, local, pg)
+    if args.workload == "dispatch":
+        return run_dispatch(args, ws, rank, local, pg)
 
     from emqx_amd import gen
     from emqx_amd.engine import Engine

@@ -57,6 +57,17 @@ class Routes(C.Structure):
                 ("filter_ids", C.POINTER(C.c_uint32)), ("dests", C.POINTER(C.c_uint32))]
 
 
+class Deliveries(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("n_matches", C.c_uint64), ("n_deliveries", C.c_uint64),
+                ("row_offsets", C.POINTER(C.c_uint64)), ("match_offsets", C.POINTER(C.c_uint64)),
+                ("subscribers", C.POINTER(C.c_uint32)), ("fill_ms", C.c_float)]
+
+
+TM_DISPATCH_COUNT_ONLY = 1
+TM_DISPATCH_MATCH_OFFSETS = 2
+TM_DISPATCH_DEVICE = 4
+
+
 class BatchStats(C.Structure):
     _fields_ = [("topics", C.c_uint64), ("visits", C.c_uint64), ("hash_hits", C.c_uint64),
                 ("words", C.c_uint64), ("matches", C.c_uint64), ("slow_topics", C.c_uint64),
@@ -102,6 +113,10 @@ SIGNATURES = {
     "tm_route_add": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_route_delete": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_batch_routes": (C.c_int, [P, P, C.POINTER(Routes)]),
+    "tm_subscribe": (C.c_int, [P, U8P, SZ, C.c_uint32, C.c_uint32]),
+    "tm_unsubscribe": (C.c_int, [P, U8P, SZ, C.c_uint32, C.c_uint32]),
+    "tm_subscriber_down": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_batch_dispatch": (C.c_int, [P, P, C.c_uint32, C.POINTER(Deliveries)]),
     "tm_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
     "tm_trie_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
     "tm_trie_delete_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/emqx_tm.h"
@@ -251,8 +252,25 @@ struct tm_batch {
     uint32_t *d_rtotal = nullptr, *h_rtotal = nullptr, *h_rrow = nullptr, *h_rfid = nullptr, *h_rdest = nullptr;
     size_t c_rcount = 0, c_rrow = 0, c_rbsums = 0, c_rfid = 0, c_rdest = 0, c_rtotal = 0;
     size_t ch_rtotal = 0, ch_rrow = 0, ch_rfid = 0, ch_rdest = 0;
+    // subscriber fan-out (tm_batch_dispatch)
+    uint64_t *d_moff = nullptr, *d_fbsums = nullptr, *d_ftotal = nullptr, *d_drow = nullptr;
+    uint64_t *h_ftotal = nullptr, *h_drow = nullptr, *h_moff = nullptr;
+    uint32_t *d_fout = nullptr, *h_fout = nullptr;
+    size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0;
+    size_t ch_ftotal = 0, ch_drow = 0, ch_moff = 0, ch_fout = 0;
+    hipEvent_t fev0 = nullptr, fev1 = nullptr;
 
     void release() {
+        dev_free(d_moff); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
+        for (uint64_t** h : {&h_ftotal, &h_drow, &h_moff}) {
+            if (*h) (void)hipHostFree(*h);
+            *h = nullptr;
+        }
+        if (h_fout) (void)hipHostFree(h_fout);
+        h_fout = nullptr;
+        if (fev0) (void)hipEventDestroy(fev0);
+        if (fev1) (void)hipEventDestroy(fev1);
+        fev0 = fev1 = nullptr;
         dev_free(d_rcount); dev_free(d_rrow); dev_free(d_rbsums); dev_free(d_rfid); dev_free(d_rdest); dev_free(d_rtotal);
         for (uint32_t** h : {&h_rtotal, &h_rrow, &h_rfid, &h_rdest}) {
             if (*h) (void)hipHostFree(*h);
@@ -815,6 +833,189 @@ struct tm_engine {
         out->row_offsets = b->h_rrow;
         out->filter_ids = b->h_rfid;
         out->dests = b->h_rdest;
+        return TM_OK;
+    }
+
+    // ---- subscribers: the emqx_subscriber / emqx_subscription bags of the
+    // local node (src/emqx_broker.erl:145-158, 179-191, 332-347), non-shared.
+    // topic -> subscriber ids in subscription order (an ETS bag key keeps
+    // insertion order); subscriber -> its topics.  The reference splits topics
+    // with > 1024 subscribers into {shard, Topic, I} keys
+    // (src/emqx_broker_helper.erl:82-87); that is a storage split of the same
+    // set, so here every topic keeps one run.
+    std::unordered_map<std::string, std::vector<uint32_t>> subs_of;
+    std::unordered_map<uint32_t, std::vector<std::string>> topics_of;
+    bool subs_dirty = true;
+    uint64_t sub_entries = 0, subs_version = 0;
+    uint64_t* d_soff = nullptr;
+    uint32_t* d_subs = nullptr;
+    size_t c_soff = 0, c_subs = 0;
+    uint32_t subs_nn = 0;
+    std::vector<uint64_t> h_soff;
+    std::vector<uint32_t> h_subs;
+
+    // do_subscribe/4, non-shared clause (:150-158): insert into the bag; the
+    // topic's first subscriber adds the node's route (handle_call({subscribe,
+    // Topic}) -> emqx_router:do_add_route/1, :438-440).
+    int subscribe(const uint8_t* t, size_t len, uint32_t sub, uint32_t node_dest) {
+        std::string k((const char*)t, len);
+        auto it = topics_of.find(sub);
+        if (it != topics_of.end() && std::find(it->second.begin(), it->second.end(), k) != it->second.end())
+            return TM_OK;   // subscribed already: only subopts would change (:127-139)
+        auto sit = subs_of.find(k);
+        if (sit == subs_of.end()) {
+            int rc = route_add(t, len, node_dest);
+            if (rc) return rc;
+            sit = subs_of.emplace(k, std::vector<uint32_t>()).first;
+        }
+        sit->second.push_back(sub);
+        topics_of[sub].push_back(std::move(k));
+        ++sub_entries;
+        subs_dirty = true;
+        return TM_OK;
+    }
+
+    // do_unsubscribe/4 (:179-191) + handle_cast({unsubscribed, Topic}) (:463-469):
+    // the last subscriber of a topic deletes the node's route.
+    int unsubscribe(const uint8_t* t, size_t len, uint32_t sub, uint32_t node_dest) {
+        std::string k((const char*)t, len);
+        auto it = topics_of.find(sub);
+        if (it == topics_of.end()) return TM_ENOENT;
+        auto& ts = it->second;
+        auto ti = std::find(ts.begin(), ts.end(), k);
+        if (ti == ts.end()) return TM_ENOENT;   // unsubscribe/1's `[] -> ok` (:170-177)
+        ts.erase(ti);
+        if (ts.empty()) topics_of.erase(it);
+        auto sit = subs_of.find(k);
+        if (sit == subs_of.end()) return TM_EIO;
+        auto& v = sit->second;
+        auto vi = std::find(v.begin(), v.end(), sub);
+        if (vi == v.end()) return TM_EIO;
+        v.erase(vi);
+        --sub_entries;
+        subs_dirty = true;
+        if (v.empty()) {
+            subs_of.erase(sit);
+            int rc = route_delete(t, len, node_dest);
+            if (rc && rc != TM_ENOENT) return rc;
+        }
+        return TM_OK;
+    }
+
+    // subscriber_down/1 (:332-347): drop every subscription of the subscriber.
+    int subscriber_down(uint32_t sub, uint32_t node_dest, uint64_t* n_removed) {
+        uint64_t n = 0;
+        auto it = topics_of.find(sub);
+        if (it != topics_of.end()) {
+            const std::vector<std::string> ts = it->second;
+            for (const auto& k : ts) {
+                int rc = unsubscribe((const uint8_t*)k.data(), k.size(), sub, node_dest);
+                if (rc) return rc;
+                ++n;
+            }
+        }
+        if (n_removed) *n_removed = n;
+        return TM_OK;
+    }
+
+    // subscriber runs by node id -> HBM (rebuilt whole after subscription or
+    // trie changes: a topic's node id is looked up at build time)
+    int sync_subs() {
+        const size_t nn = n_parent.size();
+        if (!subs_dirty && subs_version == version && subs_nn == nn && d_soff) return TM_OK;
+        h_soff.assign(nn + 1, 0);
+        std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> runs;
+        runs.reserve(subs_of.size());
+        for (const auto& kv : subs_of) {
+            const uint32_t n = node_of((const uint8_t*)kv.first.data(), kv.first.size());
+            if (n == NONE || n >= nn) continue;   // not in the trie: no route, no dispatch
+            runs.emplace_back(n, &kv.second);
+            h_soff[n + 1] += kv.second.size();
+        }
+        for (size_t i = 0; i < nn; ++i) h_soff[i + 1] += h_soff[i];
+        h_subs.resize(h_soff[nn]);
+        for (const auto& r : runs) std::copy(r.second->begin(), r.second->end(), h_subs.begin() + (long)h_soff[r.first]);
+        int rc;
+        if ((rc = dev_reserve(d_soff, c_soff, nn + 1))) return rc;
+        if ((rc = dev_reserve(d_subs, c_subs, std::max<size_t>(h_subs.size(), 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(d_soff, h_soff.data(), (nn + 1) * 8, hipMemcpyHostToDevice, stream));
+        if (!h_subs.empty())
+            HIP_OK(hipMemcpyAsync(d_subs, h_subs.data(), h_subs.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        subs_dirty = false;
+        subs_version = version;
+        subs_nn = (uint32_t)nn;
+        return TM_OK;
+    }
+
+    // tm_batch_dispatch: deliveries of a waited batch, resolved on the device
+    int batch_dispatch(tm_batch* b, uint32_t flags, tm_deliveries* out) {
+        if (!b->done) return TM_EINVAL;
+        int rc;
+        if ((rc = sync_subs())) return rc;
+        const uint32_t n = b->n;
+        const uint64_t nm = b->total;
+        const uint32_t nb = (uint32_t)((nm + 1 + 1023) / 1024);
+        if ((rc = dev_reserve(b->d_moff, b->c_moff, nm + 1))) return rc;
+        if ((rc = dev_reserve(b->d_fbsums, b->c_fbsums, nb))) return rc;
+        if ((rc = dev_reserve(b->d_ftotal, b->c_ftotal, 1))) return rc;
+        if ((rc = dev_reserve(b->d_drow, b->c_drow, (size_t)n + 1))) return rc;
+        if ((rc = host_reserve(b->h_ftotal, b->ch_ftotal, 1))) return rc;
+        if (!b->fev0) {
+            HIP_OK(hipEventCreate(&b->fev0));
+            HIP_OK(hipEventCreate(&b->fev1));
+        }
+        FanArgs fa{};
+        fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
+        fa.soff = d_soff; fa.subs = d_subs; fa.nnodes = subs_nn;
+        fa.moff = b->d_moff; fa.bsums = b->d_fbsums; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
+        HIP_OK(launch_fan_scan(fa, stream));
+        HIP_OK(hipMemcpyAsync(b->h_ftotal, b->d_ftotal, 8, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        const uint64_t total = b->h_ftotal[0];
+        const bool counts_only = flags & TM_DISPATCH_COUNT_ONLY;
+        float fill_ms = 0.f;
+        if (!counts_only) {
+            if ((rc = dev_reserve(b->d_fout, b->c_fout, std::max<uint64_t>(total, 1)))) return rc;
+            fa.out = b->d_fout; fa.total = total;
+            HIP_OK(hipEventRecord(b->fev0, stream));
+            HIP_OK(launch_fan_fill(fa, stream));
+            HIP_OK(hipEventRecord(b->fev1, stream));
+        }
+        out->n_topics = n;
+        out->n_matches = nm;
+        out->n_deliveries = total;
+        if (flags & TM_DISPATCH_DEVICE) {
+            HIP_OK(hipStreamSynchronize(stream));
+            if (!counts_only) HIP_OK(hipEventElapsedTime(&fill_ms, b->fev0, b->fev1));
+            out->row_offsets = b->d_drow;
+            out->match_offsets = b->d_moff;
+            out->subscribers = counts_only ? nullptr : b->d_fout;
+            out->fill_ms = fill_ms;
+            return TM_OK;
+        }
+        if ((rc = host_reserve(b->h_drow, b->ch_drow, (size_t)n + 1))) return rc;
+        HIP_OK(hipMemcpyAsync(b->h_drow, b->d_drow, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, stream));
+        const bool want_moff = flags & TM_DISPATCH_MATCH_OFFSETS;
+        if (want_moff) {
+            if ((rc = host_reserve(b->h_moff, b->ch_moff, nm + 1))) return rc;
+            HIP_OK(hipMemcpyAsync(b->h_moff, b->d_moff, (nm + 1) * 8, hipMemcpyDeviceToHost, stream));
+        }
+        if (!counts_only) {
+            if ((rc = host_reserve(b->h_fout, b->ch_fout, std::max<uint64_t>(total, 1)))) return rc;
+            if (total) HIP_OK(hipMemcpyAsync(b->h_fout, b->d_fout, total * 4, hipMemcpyDeviceToHost, stream));
+        }
+        HIP_OK(hipStreamSynchronize(stream));
+        if (!counts_only) HIP_OK(hipEventElapsedTime(&fill_ms, b->fev0, b->fev1));
+        if (b->h_drow[n] != total) {
+            snprintf(last_error(), 512, "inconsistent delivery CSR: %llu vs %llu", (unsigned long long)b->h_drow[n],
+                     (unsigned long long)total);
+            return TM_EIO;
+        }
+        out->row_offsets = b->h_drow;
+        out->match_offsets = want_moff ? b->h_moff : nullptr;
+        out->subscribers = counts_only ? nullptr : b->h_fout;
+        out->fill_ms = fill_ms;
         return TM_OK;
     }
 
@@ -1596,7 +1797,7 @@ struct tm_engine {
             if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
             dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
-            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl);
+            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);
@@ -1892,6 +2093,48 @@ int tm_route_delete(tm_engine* e, const uint8_t* topic, size_t len, uint32_t des
     std::lock_guard<std::recursive_mutex> g(e->mu);
     try {
         return e->route_delete(topic, len, dest);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_subscribe(tm_engine* e, const uint8_t* topic, size_t len, uint32_t subscriber, uint32_t node_dest) {
+    if (!e || (!topic && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->subscribe(topic, len, subscriber, node_dest);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_unsubscribe(tm_engine* e, const uint8_t* topic, size_t len, uint32_t subscriber, uint32_t node_dest) {
+    if (!e || (!topic && len)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->unsubscribe(topic, len, subscriber, node_dest);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_subscriber_down(tm_engine* e, uint32_t subscriber, uint32_t node_dest, uint64_t* n_removed) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    try {
+        return e->subscriber_down(subscriber, node_dest, n_removed);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
+int tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deliveries* out) {
+    if (!e || !b || !out) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    try {
+        return e->batch_dispatch(b, flags, out);
     } catch (...) {
         return TM_ENOMEM;
     }

@@ -177,6 +177,24 @@ struct RouteArgs {
     uint64_t cap;             // capacity of out_fid / out_dest
 };
 
+// Subscriber fan-out over a batch's match CSR (tm_batch_dispatch):
+// emqx_broker:dispatch/2 (src/emqx_broker.erl:284-309) for every matched filter.
+struct FanArgs {
+    const uint32_t* row_off;  // match CSR (n + 1) and filter ids
+    const uint32_t* ids;
+    uint32_t n;
+    uint64_t n_matches;
+    const uint64_t* soff;     // per node id: subscribers soff[f] .. soff[f+1] (nnodes + 1)
+    const uint32_t* subs;
+    uint32_t nnodes;
+    uint64_t* moff;           // n_matches + 1: deliveries of match entry j
+    uint64_t* bsums;          // scan block sums (FAN_SCAN_TILE entries per block)
+    uint64_t* d_total;
+    uint64_t* drow;           // n + 1: deliveries of publish i
+    uint32_t* out;            // subscriber of delivery p
+    uint64_t total;
+};
+
 // Batched emqx_topic:match/2 (tm_rules_match): names x rules -> bitmap.
 struct RulesArgs {
     const uint32_t* nwords;   // name word ids (rule dictionary; unknown = W_UNKNOWN)
@@ -198,6 +216,10 @@ hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const
                               const int64_t* dst_off, uint32_t* dst, hipStream_t s);
 hipError_t launch_route_count(const RouteArgs& a, hipStream_t s);
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
+// fan-out: per-match delivery counts + u64 scan (moff, d_total), publish row
+// offsets (drow), then the load-balanced subscriber copy (out[total])
+hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s);
+hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s);
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked);

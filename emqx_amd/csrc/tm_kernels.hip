@@ -978,6 +978,116 @@ __global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
     }
 }
 
+// ------------------------------------------ fan-out (emqx_broker:dispatch/2)
+//
+// dispatch(To, Delivery) folds over subscribers(To) for every local route of the
+// publish (src/emqx_broker.erl:243-244, 284-309).  The match CSR already lists
+// the publish's filters in order, so the deliveries of a batch are the
+// concatenation, over match entries j, of the subscriber run of filter ids[j]:
+//   scan  moff[j] = sum of the run lengths before entry j (u64: a hot filter can
+//         carry millions of subscribers), drow[i] = moff[row_off[i]];
+//   fill  one thread per DELIVERY, not per publish or filter: a workgroup owns
+//         4096 consecutive outputs, finds the entries covering them by binary
+//         search of moff, and copies subscriber ids with coalesced loads and
+//         stores -- balanced whatever the fan-out skew (1 vs 10^6 subscribers).
+
+constexpr uint32_t FAN_BLOCK = 256;
+constexpr uint32_t FAN_PER = 4;
+constexpr uint32_t FAN_SCAN_TILE = FAN_BLOCK * FAN_PER;
+constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * 16;
+
+__device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
+    if (j >= a.n_matches) return 0;
+    const uint32_t f = a.ids[j];
+    return f < a.nnodes ? a.soff[f + 1] - a.soff[f] : 0;
+}
+
+// Exclusive scan of one u64 per thread over a 256-thread block (4 waves).
+__device__ inline uint64_t fan_block_scan(uint64_t v, uint64_t* lds, uint64_t& total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    uint64_t base = 0;
+    for (uint32_t k = 0; k < w; ++k) base += lds[k];
+    total = lds[0] + lds[1] + lds[2] + lds[3];
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
+    __shared__ uint64_t lds[4];
+    const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + threadIdx.x * FAN_PER;
+    uint64_t c[FAN_PER], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_PER; ++k) { c[k] = fan_count(a, j0 + k); s += c[k]; }
+    uint64_t tot;
+    uint64_t e = fan_block_scan(s, lds, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_PER; ++k)
+        if (j0 + k <= a.n_matches) { a.moff[j0 + k] = e; e += c[k]; }
+    if (threadIdx.x == 0) a.bsums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_t nb) {
+    __shared__ uint64_t lds[4];
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += FAN_BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? a.bsums[i] : 0;
+        uint64_t tot;
+        const uint64_t e = fan_block_scan(v, lds, tot);
+        if (i < nb) a.bsums[i] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *a.d_total = carry;
+}
+
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_add(FanArgs a) {
+    const uint64_t j = (uint64_t)blockIdx.x * FAN_BLOCK + threadIdx.x;
+    if (j <= a.n_matches) a.moff[j] += a.bsums[j / FAN_SCAN_TILE];
+}
+
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_rows(FanArgs a) {
+    const uint32_t i = blockIdx.x * FAN_BLOCK + threadIdx.x;
+    if (i <= a.n) a.drow[i] = a.moff[a.row_off[i]];
+}
+
+// first j in [lo, hi) with moff[j] > p (hi if none)
+__device__ inline uint64_t fan_upper(const uint64_t* moff, uint64_t lo, uint64_t hi, uint64_t p) {
+    while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        if (moff[m] > p) hi = m;
+        else lo = m + 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
+    __shared__ uint64_t jr[2];
+    const uint64_t start = (uint64_t)blockIdx.x * FAN_FILL_TILE;
+    const uint64_t end = min(start + FAN_FILL_TILE, a.total);
+    if (threadIdx.x < 2) {
+        const uint64_t p = threadIdx.x == 0 ? start : end - 1;
+        jr[threadIdx.x] = fan_upper(a.moff, 0, a.n_matches + 1, p) - 1;
+    }
+    __syncthreads();
+    const uint64_t jhi = jr[1];
+    uint64_t j = jr[0];
+    // moff[j] <= p < moff[j + 1] for the entry of delivery p; p only grows per
+    // thread, so each search starts at the previous entry
+    for (uint64_t p = start + threadIdx.x; p < end; p += FAN_BLOCK) {
+        j = fan_upper(a.moff, j, jhi + 1, p) - 1;
+        const uint32_t f = a.ids[j];
+        a.out[p] = a.subs[a.soff[f] + (p - a.moff[j])];
+    }
+}
+
 // ------------------------------------------ batched predicate (emqx_topic:match/2)
 
 // One thread per name, all rules: the word-by-word clauses of
@@ -1277,6 +1387,23 @@ hipError_t launch_route_count(const RouteArgs& a, hipStream_t s) {
 
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s) {
     if (a.n) hipLaunchKernelGGL(tm_route_fill, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s) {
+    const uint64_t ne = a.n_matches + 1;
+    const uint32_t nb = (uint32_t)((ne + FAN_SCAN_TILE - 1) / FAN_SCAN_TILE);
+    hipLaunchKernelGGL(tm_fan_scan_local, dim3(nb), dim3(FAN_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(tm_fan_scan_sums, dim3(1), dim3(FAN_BLOCK), 0, s, a, nb);
+    hipLaunchKernelGGL(tm_fan_scan_add, dim3((uint32_t)((ne + FAN_BLOCK - 1) / FAN_BLOCK)), dim3(FAN_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(tm_fan_rows, dim3((a.n + 1 + FAN_BLOCK - 1) / FAN_BLOCK), dim3(FAN_BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s) {
+    if (a.total)
+        hipLaunchKernelGGL(tm_fan_fill, dim3((uint32_t)((a.total + FAN_FILL_TILE - 1) / FAN_FILL_TILE)),
+                           dim3(FAN_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 

@@ -86,6 +86,32 @@ class Batch:
         N.check(self.eng.L.tm_batch_routes(self.eng.h, self.h, C.byref(r)), "tm_batch_routes")
         return _routes_arrays(r)
 
+    def dispatch(self, match_offsets: bool = False, counts_only: bool = False):
+        """Device fan-out (tm_batch_dispatch): emqx_broker:dispatch/2 for every
+        matched filter of every publish -> (row_offsets u64[n+1], match_offsets
+        u64[m+1] or None, subscribers u32[deliveries] or None)."""
+        d = self._dispatch((N.TM_DISPATCH_MATCH_OFFSETS if match_offsets else 0)
+                           | (N.TM_DISPATCH_COUNT_ONLY if counts_only else 0))
+        n, m, t = d.n_topics, int(d.n_matches), int(d.n_deliveries)
+        offs = np.ctypeslib.as_array(d.row_offsets, shape=(n + 1,)).copy()
+        moff = np.ctypeslib.as_array(d.match_offsets, shape=(m + 1,)).copy() if match_offsets else None
+        if counts_only:
+            subs = None
+        else:
+            subs = np.ctypeslib.as_array(d.subscribers, shape=(t,)).copy() if t else np.zeros(0, np.uint32)
+        return offs, moff, subs
+
+    def dispatch_device(self):
+        """Device-resident fan-out: -> (n_deliveries, fill kernel ms, device ptrs row/moff/subs)."""
+        d = self._dispatch(N.TM_DISPATCH_DEVICE)
+        ptr = lambda p: C.cast(p, C.c_void_p).value  # noqa: E731
+        return int(d.n_deliveries), float(d.fill_ms), ptr(d.row_offsets), ptr(d.match_offsets), ptr(d.subscribers)
+
+    def _dispatch(self, flags: int) -> "N.Deliveries":
+        d = N.Deliveries()
+        N.check(self.eng.L.tm_batch_dispatch(self.eng.h, self.h, flags, C.byref(d)), "tm_batch_dispatch")
+        return d
+
     def stats(self) -> dict:
         st = N.BatchStats()
         N.check(self.eng.L.tm_batch_stats_get(self.eng.h, self.h, C.byref(st)), "tm_batch_stats_get")
@@ -207,6 +233,22 @@ class Engine:
             return False
         N.check(rc, "tm_route_delete")
         return True
+
+    # ---- subscribers (emqx_broker subscribe/unsubscribe/subscriber_down) ------
+    def subscribe(self, topic: bytes, sub: int, node_dest: int = 0):
+        N.check(self.L.tm_subscribe(self.h, topic, len(topic), sub, node_dest), "tm_subscribe")
+
+    def unsubscribe(self, topic: bytes, sub: int, node_dest: int = 0) -> bool:
+        rc = self.L.tm_unsubscribe(self.h, topic, len(topic), sub, node_dest)
+        if rc == N.TM_ENOENT:
+            return False
+        N.check(rc, "tm_unsubscribe")
+        return True
+
+    def subscriber_down(self, sub: int, node_dest: int = 0) -> int:
+        n = C.c_uint64()
+        N.check(self.L.tm_subscriber_down(self.h, sub, node_dest, C.byref(n)), "tm_subscriber_down")
+        return n.value
 
     def match_routes_batch(self, topics):
         """-> (row_offsets, filter_ids, dests): aggre(match_routes(T)) per topic."""

@@ -206,6 +206,51 @@ TM_API int  tm_batch_routes(tm_engine* e, tm_batch* b, tm_routes* out);
 TM_API int  tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                   tm_routes* out);
 
+/* ---- subscribers + fan-out: emqx_broker dispatch on the device --------- */
+/* The local node's subscriber bag (?SUBSCRIBER / ?SUBSCRIPTION,
+ * src/emqx_broker.erl:145-196), non-shared subscriptions; subscriber ids are
+ * the caller's (one per subscriber pid).  node_dest = the aggregated dest id
+ * the caller uses for node() in tm_route_add.
+ * tm_subscribe: do_subscribe/4 (:150-158); idempotent per (topic, subscriber)
+ * (:127-139); the topic's first subscriber adds route (topic, node_dest)
+ * (handle_call({subscribe, Topic}), :438-440 -> emqx_router:do_add_route/1).
+ * Topics with > 1024 subscribers are sharded into {shard, Topic, I} keys by the
+ * reference (src/emqx_broker_helper.erl:82-87): a storage split of the same
+ * set, so a topic keeps one run here, in subscription order. */
+TM_API int  tm_subscribe(tm_engine* e, const uint8_t* topic, size_t len, uint32_t subscriber, uint32_t node_dest);
+/* do_unsubscribe/4 (:179-191): TM_ENOENT if not subscribed (unsubscribe/1's
+ * `[] -> ok`, :170-177); the last subscriber of a topic deletes its route
+ * (handle_cast({unsubscribed, Topic}), :463-469). */
+TM_API int  tm_unsubscribe(tm_engine* e, const uint8_t* topic, size_t len, uint32_t subscriber, uint32_t node_dest);
+/* subscriber_down/1 (:332-347): drops every subscription of the subscriber;
+ * *n_removed (may be NULL) = how many. */
+TM_API int  tm_subscriber_down(tm_engine* e, uint32_t subscriber, uint32_t node_dest, uint64_t* n_removed);
+
+/* Deliveries of a waited batch: dispatch(To, Delivery) (:284-309) for every
+ * filter To matched by publish i (its local route, do_route/2 :243-244):
+ * deliveries of row i = subscribers[row_offsets[i] .. row_offsets[i+1]), the
+ * runs of its matched filters in match (Erlang binary) order, each run in
+ * subscription order; row_offsets[i+1] - row_offsets[i] = DispN (0 =
+ * {error, no_subscribers}).  match_offsets[j] (TM_DISPATCH_MATCH_OFFSETS) =
+ * first delivery of match entry j, i.e. of filter ids[j] of tm_batch_result.
+ * TM_DISPATCH_COUNT_ONLY: counts only, subscribers = NULL.
+ * TM_DISPATCH_DEVICE: no copy back; the pointers are device memory of the
+ * batch, valid until its next dispatch or re-prepare.  Otherwise engine-owned
+ * pinned memory valid likewise.  fill_ms = device time of the copy kernel. */
+typedef struct {
+    uint32_t        n_topics;
+    uint64_t        n_matches;
+    uint64_t        n_deliveries;
+    const uint64_t* row_offsets;    /* n_topics + 1 */
+    const uint64_t* match_offsets;  /* n_matches + 1, or NULL */
+    const uint32_t* subscribers;    /* n_deliveries, or NULL */
+    float           fill_ms;
+} tm_deliveries;
+#define TM_DISPATCH_COUNT_ONLY    1u
+#define TM_DISPATCH_MATCH_OFFSETS 2u
+#define TM_DISPATCH_DEVICE        4u
+TM_API int  tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deliveries* out);
+
 /* ---- bulk load + filter-sharded mode ------------------ */
 /* emqx_trie:insert/1 over n filters (filters = concatenated bytes, offsets[n+1]).
  * nshards <= 1: every filter.  Otherwise only the filters whose

@@ -236,3 +236,86 @@ def match_routes(trie: Trie, routes: dict, topic: bytes):
     for to in [topic] + matched:
         out.extend((to, d) for d in routes.get(to, []))
     return out
+
+
+class Broker:
+    """emqx_broker's local subscriber bag and dispatch, non-shared subscriptions.
+
+    subscribe    do_subscribe/4 non-shared clause   src/emqx_broker.erl:145-158
+                 (first subscriber -> do_add_route  :438-440, emqx_router:108-124)
+    unsubscribe  do_unsubscribe/4                   :179-191
+                 (last subscriber -> do_delete_route :463-469)
+    subscriber_down/1                               :332-347
+    publish      route/2 -> do_route/2 -> dispatch/2 (local node) :233-309
+                 over emqx_router:match_routes/1
+
+    publish() returns the deliveries [(To, SubPid)] of one message: its matched
+    filters in Erlang binary order (the reference folds the route list in
+    DFS/ETS order -- a set, its order is not part of the contract), each
+    filter's subscribers in subscription order (ETS bag insertion order).
+    len() == 0 is the reference's {error, no_subscribers}.
+    """
+
+    NODE = "node@local"
+
+    def __init__(self):
+        self.trie = Trie()
+        self.routes = {}        # emqx_route bag: topic -> [dest]
+        self.subscriber = {}    # ?SUBSCRIBER bag: topic -> [pid]
+        self.subscription = {}  # ?SUBSCRIPTION bag: pid -> [topic]
+
+    def _add_route(self, topic):
+        dests = self.routes.setdefault(topic, [])
+        if self.NODE in dests:
+            return
+        if not dests and wildcard(topic):
+            self.trie.insert(topic)           # insert_trie_route/1 (src/emqx_router.erl:229-234)
+        dests.append(self.NODE)
+
+    def _delete_route(self, topic):
+        dests = self.routes.get(topic, [])
+        if self.NODE not in dests:
+            return
+        dests.remove(self.NODE)
+        if not dests:
+            del self.routes[topic]
+            if wildcard(topic):
+                self.trie.delete(topic)       # delete_trie_route/1 (:239-247)
+
+    def subscribe(self, topic: bytes, pid):
+        ts = self.subscription.setdefault(pid, [])
+        if topic in ts:
+            return
+        ts.append(topic)
+        subs = self.subscriber.setdefault(topic, [])
+        first = not subs
+        subs.append(pid)
+        if first:
+            self._add_route(topic)
+
+    def unsubscribe(self, topic: bytes, pid) -> bool:
+        ts = self.subscription.get(pid, [])
+        if topic not in ts:
+            return False                      # `[] -> ok` (:170-177)
+        ts.remove(topic)
+        if not ts:
+            del self.subscription[pid]
+        subs = self.subscriber[topic]
+        subs.remove(pid)
+        if not subs:
+            del self.subscriber[topic]
+            self._delete_route(topic)
+        return True
+
+    def subscriber_down(self, pid) -> int:
+        ts = list(self.subscription.get(pid, []))
+        for t in ts:
+            self.unsubscribe(t, pid)
+        return len(ts)
+
+    def subscribers(self, topic: bytes):
+        return list(self.subscriber.get(topic, []))
+
+    def publish(self, topic: bytes):
+        tos = sorted({to for to, d in match_routes(self.trie, self.routes, topic) if d == self.NODE})
+        return [(to, pid) for to in tos for pid in self.subscriber.get(to, [])]

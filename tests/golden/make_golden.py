@@ -160,6 +160,36 @@ KAT_TRIE = {
     "triples": [["a/b/c", [["root", "a", "a"], ["a", "b", "a/b"], ["a/b", "c", "a/b/c"]]]],
 }
 
+KAT_BROKER = {
+    "source": "test/emqx_broker_SUITE.erl, test/emqx_client_SUITE.erl",
+    "note": "ops: sub/unsub/down change the subscriber bag; pub lists the deliveries "
+            "[filter, subscriber] of one publish (filters in binary order); "
+            "subscribers/topics are the table reads the tests assert",
+    "cases": [
+        {"name": "t_subscribers", "line": "emqx_broker_SUITE.erl:92-95",
+         "ops": [["sub", "topic", "self"], ["subscribers", "topic", ["self"]], ["unsub", "topic", "self"],
+                 ["subscribers", "topic", []]]},
+        {"name": "t_sub_pub", "line": "emqx_broker_SUITE.erl:106-118",
+         "ops": [["sub", "topic", "self"], ["pub", "topic", [["topic", "self"]]]]},
+        {"name": "t_nosub_pub", "line": "emqx_broker_SUITE.erl:120-123",
+         "ops": [["pub", "topic", []]]},
+        {"name": "t_shard", "line": "emqx_broker_SUITE.erl:177-192",
+         "ops": [["sub", "topic", "clientid"], ["pub", "topic", [["topic", "clientid"]]]]},
+        {"name": "t_topics", "line": "emqx_broker_SUITE.erl:76-90",
+         "ops": [["sub", "topic", "clientId"], ["sub", "topic/1", "clientId"], ["sub", "topic/2", "clientId"],
+                 ["topics", ["topic", "topic/1", "topic/2"]],
+                 ["unsub", "topic", "clientId"], ["unsub", "topic/1", "clientId"], ["unsub", "topic/2", "clientId"],
+                 ["topics", []]]},
+        {"name": "t_overlapping_subscriptions", "line": "emqx_client_SUITE.erl:166-186",
+         "note": "this broker publishes one message per matching subscription (Num == 2)",
+         "ops": [["sub", "TopicA/#", "C"], ["sub", "TopicA/+", "C"],
+                 ["pub", "TopicA/C", [["TopicA/#", "C"], ["TopicA/+", "C"]]]]},
+        {"name": "t_dollar_topics", "line": "emqx_client_SUITE.erl:234-247",
+         "ops": [["sub", "+/+", "C"], ["pub", "$TopicA/B", []]]},
+    ],
+}
+
+
 KAT_ROUTER = {
     "source": "test/emqx_router_SUITE.erl",
     "cases": [
@@ -222,6 +252,7 @@ def main():
     dump("kat_topic.json", KAT_TOPIC)
     dump("kat_trie.json", KAT_TRIE)
     dump("kat_router.json", KAT_ROUTER)
+    dump("kat_broker.json", KAT_BROKER)
     synth("synth_c1_small.json", replace(gen.C1, n_filters=800), 600, 11)
     synth("synth_c2_small.json", replace(gen.C2, n_filters=1500, vocab=48), 600, 22)
     synth("synth_adversarial.json", replace(gen.C1, n_filters=150, vocab=6, p_empty=0.2, p_dollar=0.1), 300, 33,

@@ -1,0 +1,115 @@
+"""Device fan-out (tm_batch_dispatch): emqx_broker's publish -> route ->
+dispatch over a whole batch, checked against the oracle's Broker restatement
+(oracle/oracle.py, pinned by tests/golden/kat_broker.json) on the same inputs."""
+
+import random
+from dataclasses import replace
+
+import numpy as np
+import pytest
+from conftest import load_golden
+from test_broker import run_kat_ops
+
+from emqx_amd import emqx_broker as B
+from emqx_amd import emqx_router as R
+from emqx_amd import gen
+from emqx_amd.engine import Engine
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_kat_broker_on_device():
+    kat = load_golden("kat_broker.json")
+    for case in kat["cases"]:
+        B.clear_tables()
+        run_kat_ops(case["ops"], B.subscribe, B.unsubscribe, B.subscriber_down,
+                    lambda t: B.publish_batch([t])[0], B.subscribers, B.topics)
+
+
+def test_dispatch_random_churn_vs_oracle():
+    rng = random.Random(5)
+    p = replace(gen.C1, n_filters=2500)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 17, 5000).tolist()
+    B.clear_tables()
+    orc = O.Broker()
+    for rnd in range(3):
+        for _ in range(6000):
+            f, pid = rng.choice(F), rng.randrange(300)
+            r = rng.random()
+            if r < 0.3:
+                B.unsubscribe(f, pid)
+                orc.unsubscribe(f, pid)
+            elif r < 0.31:
+                assert B.subscriber_down(pid) == orc.subscriber_down(pid)
+            else:
+                B.subscribe(f, pid)
+                orc.subscribe(f, pid)
+        got = B.publish_batch(T)
+        for t, row in zip(T, got):
+            assert row == orc.publish(t), (rnd, t)
+        assert sorted(B.topics()) == sorted(orc.routes)
+
+
+def test_dispatch_skewed_fanout_and_modes():
+    """One '#' filter with 150k subscribers next to thousands of 1-subscriber
+    filters: the fill kernel's workgroups straddle both kinds of runs."""
+    p = replace(gen.C1, n_filters=4000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 23, 3000).tolist()
+    eng = Engine(device=0)
+    subs = {}
+    for i, f in enumerate(F):
+        eng.subscribe(f, 1_000_000 + i)
+        subs[f] = [1_000_000 + i]
+    hot = list(range(150_000))
+    for s in hot:
+        eng.subscribe(b"#", s)
+    subs[b"#"] = subs.get(b"#", []) + hot
+    b = eng.prepare(T)
+    b.launch()
+    b.wait()
+    roff, ids = b.result()
+    offs, moff, out = b.dispatch(match_offsets=True)
+    c_offs, _, none = b.dispatch(counts_only=True)
+    assert none is None and np.array_equal(c_offs, offs)
+    total, fill_ms, d_row, d_moff, d_subs = b.dispatch_device()
+    assert total == int(offs[-1]) and fill_ms > 0 and d_subs
+    names = [eng.filter_bytes(int(i)) for i in ids]
+    for i, t in enumerate(T):
+        exp = []
+        for j in range(int(roff[i]), int(roff[i + 1])):
+            assert int(moff[j]) == offs[i] + len(exp)
+            exp.extend(subs.get(names[j], []))
+        got = out[offs[i]:offs[i + 1]]
+        assert len(got) == len(exp) and np.array_equal(got, np.asarray(exp, np.uint32)), t
+        # every publish matches '#' unless it is a '$' topic
+        assert (len(got) >= len(hot)) == (not t.startswith(b"$"))
+    b.free()
+
+
+def test_dispatch_dedup_rows_and_unsubscribe_all():
+    eng = Engine(device=0)
+    for s in range(5):
+        eng.subscribe(b"a/+", s)
+        eng.subscribe(b"a/b", 10 + s)
+    T = [b"a/b", b"a/c", b"a/b", b"x", b"a/b"]
+    b = eng.prepare(T, dedup=True)
+    b.launch()
+    b.wait()
+    rows, _ = b.row_map()
+    offs, _, out = b.dispatch()
+    per = {T[i]: out[offs[rows[i]]:offs[rows[i] + 1]].tolist() for i in range(len(T))}
+    assert per[b"a/b"] == [0, 1, 2, 3, 4, 10, 11, 12, 13, 14]
+    assert per[b"a/c"] == [0, 1, 2, 3, 4] and per[b"x"] == []
+    for s in range(5):
+        assert eng.subscriber_down(s) == 1
+        assert eng.unsubscribe(b"a/b", 10 + s)
+    assert not eng.unsubscribe(b"a/b", 10)
+    assert eng.empty()
+    b2 = eng.prepare(T)
+    b2.launch()
+    b2.wait()
+    offs, _, out = b2.dispatch()
+    assert int(offs[-1]) == 0
