@@ -27,6 +27,8 @@ TM_MAX_TOPIC_LEN = 4096
 TM_CFG_FROZEN_DICT = 1
 TM_CFG_HOST_TOKENIZE = 2
 TM_BATCH_DEDUP = 1
+TM_ROUTE_DELETE = 0
+TM_ROUTE_WRITE = 1
 
 _ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
              TM_EINVAL: "EINVAL", TM_EOVERFLOW: "EOVERFLOW", TM_EABORT: "EABORT"}
@@ -112,6 +114,7 @@ SIGNATURES = {
     "tm_batch_free": (None, [P, P]),
     "tm_route_add": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_route_delete": (C.c_int, [P, U8P, SZ, C.c_uint32]),
+    "tm_route_apply": (C.c_int, [P, P, P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
     "tm_batch_routes": (C.c_int, [P, P, C.POINTER(Routes)]),
     "tm_subscribe": (C.c_int, [P, U8P, SZ, C.c_uint32, C.c_uint32]),
     "tm_unsubscribe": (C.c_int, [P, U8P, SZ, C.c_uint32, C.c_uint32]),

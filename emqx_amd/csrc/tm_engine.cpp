@@ -253,15 +253,16 @@ struct tm_batch {
     size_t c_rcount = 0, c_rrow = 0, c_rbsums = 0, c_rfid = 0, c_rdest = 0, c_rtotal = 0;
     size_t ch_rtotal = 0, ch_rrow = 0, ch_rfid = 0, ch_rdest = 0;
     // subscriber fan-out (tm_batch_dispatch)
-    uint64_t *d_moff = nullptr, *d_fbsums = nullptr, *d_ftotal = nullptr, *d_drow = nullptr;
+    uint64_t *d_moff = nullptr, *d_fbsums = nullptr, *d_ftotal = nullptr, *d_drow = nullptr, *d_ftile = nullptr;
     uint64_t *h_ftotal = nullptr, *h_drow = nullptr, *h_moff = nullptr;
     uint32_t *d_fout = nullptr, *h_fout = nullptr;
-    size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0;
+    size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0, c_ftile = 0;
     size_t ch_ftotal = 0, ch_drow = 0, ch_moff = 0, ch_fout = 0;
     hipEvent_t fev0 = nullptr, fev1 = nullptr;
 
     void release() {
         dev_free(d_moff); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
+        dev_free(d_ftile);
         for (uint64_t** h : {&h_ftotal, &h_drow, &h_moff}) {
             if (*h) (void)hipHostFree(*h);
             *h = nullptr;
@@ -955,7 +956,7 @@ struct tm_engine {
         if ((rc = sync_subs())) return rc;
         const uint32_t n = b->n;
         const uint64_t nm = b->total;
-        const uint32_t nb = (uint32_t)((nm + 1 + 1023) / 1024);
+        const uint32_t nb = (uint32_t)((nm + 1 + fan_scan_tile() - 1) / fan_scan_tile());
         if ((rc = dev_reserve(b->d_moff, b->c_moff, nm + 1))) return rc;
         if ((rc = dev_reserve(b->d_fbsums, b->c_fbsums, nb))) return rc;
         if ((rc = dev_reserve(b->d_ftotal, b->c_ftotal, 1))) return rc;
@@ -977,7 +978,8 @@ struct tm_engine {
         float fill_ms = 0.f;
         if (!counts_only) {
             if ((rc = dev_reserve(b->d_fout, b->c_fout, std::max<uint64_t>(total, 1)))) return rc;
-            fa.out = b->d_fout; fa.total = total;
+            if ((rc = dev_reserve(b->d_ftile, b->c_ftile, (size_t)(total / fan_fill_tile()) + 2))) return rc;
+            fa.out = b->d_fout; fa.total = total; fa.tile_j = b->d_ftile;
             HIP_OK(hipEventRecord(b->fev0, stream));
             HIP_OK(launch_fan_fill(fa, stream));
             HIP_OK(hipEventRecord(b->fev1, stream));
@@ -2096,6 +2098,35 @@ int tm_route_delete(tm_engine* e, const uint8_t* topic, size_t len, uint32_t des
     } catch (...) {
         return TM_ENOMEM;
     }
+}
+
+int tm_route_apply(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, const uint32_t* dests,
+                   const uint8_t* ops, uint32_t n, uint64_t* n_changed) {
+    if (n_changed) *n_changed = 0;
+    if (!e || (n && (!offsets || !dests || !ops))) return TM_EINVAL;
+    if (n && offsets[n] && !topics) return TM_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i] || ops[i] > TM_ROUTE_WRITE) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    uint64_t changed = 0;
+    try {
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t* t = topics + offsets[i];
+            const size_t len = (size_t)(offsets[i + 1] - offsets[i]);
+            int rc = ops[i] == TM_ROUTE_WRITE ? e->route_add(t, len, dests[i]) : e->route_delete(t, len, dests[i]);
+            if (rc == TM_ENOENT && ops[i] == TM_ROUTE_DELETE) continue;   // delete_object of no record: no-op
+            if (rc) {
+                if (n_changed) *n_changed = changed;
+                return rc;
+            }
+            ++changed;
+        }
+    } catch (...) {
+        if (n_changed) *n_changed = changed;
+        return TM_ENOMEM;
+    }
+    if (n_changed) *n_changed = changed;
+    return TM_OK;
 }
 
 int tm_subscribe(tm_engine* e, const uint8_t* topic, size_t len, uint32_t subscriber, uint32_t node_dest) {

@@ -193,6 +193,7 @@ struct FanArgs {
     uint64_t* drow;           // n + 1: deliveries of publish i
     uint32_t* out;            // subscriber of delivery p
     uint64_t total;
+    uint64_t* tile_j;         // total / fan_fill_tile() + 2: match entry of each fill tile's first delivery
 };
 
 // Batched emqx_topic:match/2 (tm_rules_match): names x rules -> bitmap.
@@ -220,6 +221,8 @@ hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
 // offsets (drow), then the load-balanced subscriber copy (out[total])
 hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s);
 hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s);
+uint32_t fan_scan_tile();   // match entries per scan block
+uint32_t fan_fill_tile();   // deliveries per fill block
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked);

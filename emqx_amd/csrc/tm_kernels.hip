@@ -992,9 +992,11 @@ __global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
 //         stores -- balanced whatever the fan-out skew (1 vs 10^6 subscribers).
 
 constexpr uint32_t FAN_BLOCK = 256;
-constexpr uint32_t FAN_PER = 4;
+constexpr uint32_t FAN_PER = 16;                           // entries per scan thread
 constexpr uint32_t FAN_SCAN_TILE = FAN_BLOCK * FAN_PER;
-constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * 16;
+constexpr uint32_t FAN_FILL_PER = 16;                      // deliveries per fill thread
+constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * FAN_FILL_PER;
+constexpr uint32_t FAN_LDS_ENTRIES = 3072;                 // match entries a fill tile can stage
 
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
     if (j >= a.n_matches) return 0;
@@ -1020,18 +1022,25 @@ __device__ inline uint64_t fan_block_scan(uint64_t v, uint64_t* lds, uint64_t& t
     return base + x - v;
 }
 
+// A block scans FAN_SCAN_TILE entries as FAN_PER striped chunks of FAN_BLOCK
+// (coalesced ids loads and moff stores); all chunks' run lengths are gathered
+// before the first scan so the soff loads overlap.
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
     __shared__ uint64_t lds[4];
-    const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + threadIdx.x * FAN_PER;
-    uint64_t c[FAN_PER], s = 0;
+    const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + threadIdx.x;
+    uint64_t c[FAN_PER];
 #pragma unroll
-    for (uint32_t k = 0; k < FAN_PER; ++k) { c[k] = fan_count(a, j0 + k); s += c[k]; }
-    uint64_t tot;
-    uint64_t e = fan_block_scan(s, lds, tot);
+    for (uint32_t k = 0; k < FAN_PER; ++k) c[k] = fan_count(a, j0 + (uint64_t)k * FAN_BLOCK);
+    uint64_t carry = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < FAN_PER; ++k)
-        if (j0 + k <= a.n_matches) { a.moff[j0 + k] = e; e += c[k]; }
-    if (threadIdx.x == 0) a.bsums[blockIdx.x] = tot;
+    for (uint32_t k = 0; k < FAN_PER; ++k) {
+        uint64_t tot;
+        const uint64_t e = fan_block_scan(c[k], lds, tot);
+        const uint64_t j = j0 + (uint64_t)k * FAN_BLOCK;
+        if (j <= a.n_matches) a.moff[j] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) a.bsums[blockIdx.x] = carry;
 }
 
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_t nb) {
@@ -1068,23 +1077,85 @@ __device__ inline uint64_t fan_upper(const uint64_t* moff, uint64_t lo, uint64_t
     return lo;
 }
 
+// tile_j[k] = match entry of delivery k * FAN_FILL_TILE (k < ntiles), and
+// tile_j[ntiles] = entry of the last delivery: one search per tile, all tiles
+// at once, instead of a dependent search chain at the head of every fill block.
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_tiles(FanArgs a, uint64_t ntiles) {
+    const uint64_t k = (uint64_t)blockIdx.x * FAN_BLOCK + threadIdx.x;
+    if (k > ntiles) return;
+    const uint64_t p = k < ntiles ? k * FAN_FILL_TILE : a.total - 1;
+    a.tile_j[k] = fan_upper(a.moff, 0, a.n_matches + 1, p) - 1;
+}
+
+// One workgroup per 4096 consecutive deliveries.  The entries covering the
+// tile (jlo..jhi) are staged in LDS: each non-empty run marks its first
+// delivery in the tile with its entry index and keeps soff[f] - moff[j]; an
+// inclusive max-scan over the marks gives every delivery its entry, and the
+// copy is then one LDS read + one subscriber load + one coalesced store per
+// delivery.  A tile covering more than FAN_LDS_ENTRIES entries (long stretches
+// of filters without local subscribers) searches moff per delivery instead.
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
-    __shared__ uint64_t jr[2];
+    __shared__ int64_t base[FAN_LDS_ENTRIES];
+    __shared__ __attribute__((aligned(16))) uint16_t own[FAN_FILL_TILE];
+    __shared__ uint32_t wmax[FAN_BLOCK / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint64_t start = (uint64_t)blockIdx.x * FAN_FILL_TILE;
     const uint64_t end = min(start + FAN_FILL_TILE, a.total);
-    if (threadIdx.x < 2) {
-        const uint64_t p = threadIdx.x == 0 ? start : end - 1;
-        jr[threadIdx.x] = fan_upper(a.moff, 0, a.n_matches + 1, p) - 1;
+    const uint32_t len = (uint32_t)(end - start);
+    const uint64_t jlo = a.tile_j[blockIdx.x];
+    const uint64_t jhi = a.tile_j[blockIdx.x + 1];
+    const uint64_t ne = jhi - jlo + 1;
+    if (ne > FAN_LDS_ENTRIES) {
+        // moff[j] <= p < moff[j + 1] for the entry of delivery p; p only grows
+        // per thread, so each search starts at the previous entry
+        uint64_t j = jlo;
+        for (uint64_t p = start + t; p < end; p += FAN_BLOCK) {
+            j = fan_upper(a.moff, j, jhi + 1, p) - 1;
+            a.out[p] = a.subs[a.soff[a.ids[j]] + (p - a.moff[j])];
+        }
+        return;
+    }
+    uint4* own4 = reinterpret_cast<uint4*>(own);
+    for (uint32_t i = t; i < FAN_FILL_TILE / 8; i += FAN_BLOCK) own4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (uint32_t e = t; e < (uint32_t)ne; e += FAN_BLOCK) {
+        const uint64_t j = jlo + e;
+        const uint64_t m0 = a.moff[j], m1 = a.moff[j + 1];
+        if (m1 > m0 && m1 > start && m0 < end) {
+            base[e] = (int64_t)a.soff[a.ids[j]] - (int64_t)m0;
+            own[m0 > start ? (uint32_t)(m0 - start) : 0u] = (uint16_t)(e + 1);
+        }
     }
     __syncthreads();
-    const uint64_t jhi = jr[1];
-    uint64_t j = jr[0];
-    // moff[j] <= p < moff[j + 1] for the entry of delivery p; p only grows per
-    // thread, so each search starts at the previous entry
-    for (uint64_t p = start + threadIdx.x; p < end; p += FAN_BLOCK) {
-        j = fan_upper(a.moff, j, jhi + 1, p) - 1;
-        const uint32_t f = a.ids[j];
-        a.out[p] = a.subs[a.soff[f] + (p - a.moff[j])];
+    // inclusive max-scan of own[] (entry starts only grow along the tile)
+    uint4 q0 = own4[2 * t], q1 = own4[2 * t + 1];
+    uint32_t v[FAN_FILL_PER];
+    const uint32_t wd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) { v[2 * k] = wd[k] & 0xFFFFu; v[2 * k + 1] = wd[k] >> 16; }
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < FAN_FILL_PER; ++k) { run = max(run, v[k]); v[k] = run; }
+    uint32_t x = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x = max(x, y);
+    }
+    if (lane == 63) wmax[w] = x;
+    uint32_t pre = __shfl_up(x, 1, 64);
+    if (lane == 0) pre = 0;
+    __syncthreads();
+    for (uint32_t k = 0; k < w; ++k) pre = max(pre, wmax[k]);
+    uint32_t o[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) o[k] = max(v[2 * k], pre) | (max(v[2 * k + 1], pre) << 16);
+    own4[2 * t] = make_uint4(o[0], o[1], o[2], o[3]);
+    own4[2 * t + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    __syncthreads();
+    for (uint32_t i = t; i < len; i += FAN_BLOCK) {
+        const uint32_t e = (uint32_t)own[i] - 1u;
+        a.out[start + i] = a.subs[(uint64_t)(base[e] + (int64_t)(start + i))];
     }
 }
 
@@ -1401,11 +1472,17 @@ hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s) {
-    if (a.total)
-        hipLaunchKernelGGL(tm_fan_fill, dim3((uint32_t)((a.total + FAN_FILL_TILE - 1) / FAN_FILL_TILE)),
-                           dim3(FAN_BLOCK), 0, s, a);
+    if (a.total) {
+        const uint64_t nt = (a.total + FAN_FILL_TILE - 1) / FAN_FILL_TILE;
+        hipLaunchKernelGGL(tm_fan_tiles, dim3((uint32_t)((nt + 1 + FAN_BLOCK - 1) / FAN_BLOCK)), dim3(FAN_BLOCK), 0, s,
+                           a, nt);
+        hipLaunchKernelGGL(tm_fan_fill, dim3((uint32_t)nt), dim3(FAN_BLOCK), 0, s, a);
+    }
     return hipGetLastError();
 }
+
+uint32_t fan_scan_tile() { return FAN_SCAN_TILE; }
+uint32_t fan_fill_tile() { return FAN_FILL_TILE; }
 
 hipError_t launch_rules_match(const RulesArgs& a, hipStream_t s) {
     if (a.n) hipLaunchKernelGGL(tm_rules_match, dim3((a.n + 255) / 256), dim3(256), 0, s, a);

@@ -234,6 +234,20 @@ class Engine:
         N.check(rc, "tm_route_delete")
         return True
 
+    def route_apply(self, events) -> int:
+        """tm_route_apply: [(op, topic, dest)] in order, op 1 = write (add), 0 =
+        delete_object (absent = no-op).  Returns how many changed the table."""
+        n = len(events)
+        s = _pack([t for _, t, _ in events])
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        dests = np.ascontiguousarray(np.array([d for _, _, d in events] or [0], np.uint32))
+        ops = np.ascontiguousarray(np.array([o for o, _, _ in events] or [0], np.uint8))
+        done = C.c_uint64()
+        N.check(self.L.tm_route_apply(self.h, buf.ctypes.data, offs.ctypes.data, dests.ctypes.data,
+                                      ops.ctypes.data, n, C.byref(done)), "tm_route_apply")
+        return int(done.value)
+
     # ---- subscribers (emqx_broker subscribe/unsubscribe/subscriber_down) ------
     def subscribe(self, topic: bytes, sub: int, node_dest: int = 0):
         N.check(self.L.tm_subscribe(self.h, topic, len(topic), sub, node_dest), "tm_subscribe")

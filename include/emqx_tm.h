@@ -188,6 +188,23 @@ TM_API int  tm_route_add(tm_engine* e, const uint8_t* topic, size_t len, uint32_
  * route; removing the last route of a topic deletes it from the trie. */
 TM_API int  tm_route_delete(tm_engine* e, const uint8_t* topic, size_t len, uint32_t dest);
 
+/* Cluster route delta feed: n route-table events applied
+ * in order under one engine lock.  The emqx_route bag and the trie tables are
+ * mnesia ram_copies replicated to every node (src/emqx_router.erl:77-86,
+ * src/emqx_trie.erl:53-74), so a node sees remote route writes as table
+ * events ({write, #route{}} / {delete_object, #route{}}); the feed also carries
+ * the deletes of cleanup_routes(Node) on nodedown
+ * (src/emqx_router_helper.erl:135-141, 173-177) and the
+ * {Group, node()} routes of shared subscriptions (src/emqx_shared_sub.erl:
+ * 297-313).  ops[i] = TM_ROUTE_WRITE -> tm_route_add(topic i, dests[i]);
+ * TM_ROUTE_DELETE -> tm_route_delete, where a missing (topic, dest) is a no-op
+ * (mnesia:delete_object of an absent record).  *n_changed (may be NULL) counts
+ * the events that changed the table.  Stops at the first other error. */
+#define TM_ROUTE_DELETE 0u
+#define TM_ROUTE_WRITE  1u
+TM_API int  tm_route_apply(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, const uint32_t* dests,
+                           const uint8_t* ops, uint32_t n, uint64_t* n_changed);
+
 /* aggre(match_routes(T)) per topic: row i lists (filter id, dest) pairs,
  * filters in Erlang binary order, each filter's dests in first-added order,
  * no (filter, dest) twice.  Engine-owned memory, valid like tm_result. */

@@ -319,3 +319,58 @@ class Broker:
     def publish(self, topic: bytes):
         tos = sorted({to for to, d in match_routes(self.trie, self.routes, topic) if d == self.NODE})
         return [(to, pid) for to in tos for pid in self.subscriber.get(to, [])]
+
+
+class RouteTable:
+    """The replicated emqx_route bag as a node sees it through the cluster delta
+    feed -- test infrastructure only.
+
+    write         mnesia:write of #route{} into a bag: an identical record is
+                  stored once (do_add_route/2's lists:member check,
+                  src/emqx_router.erl:113-124); the first route of a wildcard
+                  topic inserts it into the trie (insert_trie_route/1 :229-234)
+    delete_object removes the record if present (do_delete_route/2 :163-169);
+                  the last route of a wildcard topic deletes it from the trie
+                  (delete_trie_route/1 :239-247)
+    cleanup_routes(Node)  src/emqx_router_helper.erl:173-177: every route whose
+                  dest is Node or {_, Node}
+    aggre(topic)  emqx_broker:aggre(match_routes(T)) (src/emqx_broker.erl:250-261)
+                  as a set of (To, Node | Group) pairs
+    """
+
+    def __init__(self):
+        self.trie = Trie()
+        self.routes = {}   # topic -> [dest] (bag, insertion order)
+
+    def write(self, topic: bytes, dest):
+        ds = self.routes.setdefault(topic, [])
+        if dest in ds:
+            return False
+        if not ds and wildcard(topic):
+            self.trie.insert(topic)
+        ds.append(dest)
+        return True
+
+    def delete_object(self, topic: bytes, dest):
+        ds = self.routes.get(topic)
+        if not ds or dest not in ds:
+            return False
+        ds.remove(dest)
+        if not ds:
+            del self.routes[topic]
+            if wildcard(topic):
+                self.trie.delete(topic)
+        return True
+
+    def cleanup_routes(self, node):
+        gone = [(t, d) for t, ds in self.routes.items() for d in ds
+                if d == node or (isinstance(d, tuple) and d[1] == node)]
+        for t, d in gone:
+            self.delete_object(t, d)
+        return gone
+
+    def aggre(self, topic: bytes):
+        out = set()
+        for to, d in match_routes(self.trie, self.routes, topic):
+            out.add((to, d[0] if isinstance(d, tuple) else d))
+        return out

@@ -113,3 +113,44 @@ def test_dispatch_dedup_rows_and_unsubscribe_all():
     b2.wait()
     offs, _, out = b2.dispatch()
     assert int(offs[-1]) == 0
+
+
+def test_dispatch_sparse_subscribers_take_the_search_path():
+    """Most matched filters have no local subscriber: fill tiles then cover far
+    more match entries than they can stage in LDS (the per-delivery search
+    path).  A '#' subscriber set then makes every tile dense (the staged path)."""
+    p = replace(gen.C1, n_filters=4000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 29, 40000).tolist()
+    eng = Engine(device=0)
+    eng.insert_many(F)
+    subs = {}
+    rng = np.random.default_rng(8)
+    for i, f in enumerate(F):
+        if rng.random() < 0.01:
+            subs[f] = [7 * i + q for q in range(int(rng.integers(1, 4)))]
+            for s in subs[f]:
+                eng.subscribe(f, s)
+
+    def check():
+        b = eng.prepare(T)
+        b.launch()
+        b.wait()
+        roff, ids = b.result()
+        offs, moff, out = b.dispatch(match_offsets=True)
+        names = [eng.filter_bytes(int(i)) for i in ids]
+        for i in range(len(T)):
+            exp = []
+            for j in range(int(roff[i]), int(roff[i + 1])):
+                assert int(moff[j]) == offs[i] + len(exp)
+                exp.extend(subs.get(names[j], []))
+            assert np.array_equal(out[offs[i]:offs[i + 1]], np.asarray(exp, np.uint32)), T[i]
+        b.free()
+        return int(offs[-1]), len(ids)
+    nd, nm = check()
+    assert nm > 4 * 3072 and nd < nm // 4           # sparse: tiles span > FAN_LDS_ENTRIES entries
+    subs[b"#"] = [5_000_000 + s for s in range(64)]
+    for s in subs[b"#"]:
+        eng.subscribe(b"#", s)
+    nd, nm = check()
+    assert nd > nm                                   # dense: staged path
