@@ -30,7 +30,7 @@ typedef struct {
 
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_UNDEFINED, ATOM_ROOT,
     ATOM_TRIE_NODE, ATOM_NODE_NOT_FOUND, ATOM_ENOMEM, ATOM_EIO, ATOM_EINVAL, ATOM_ENODEV,
-    ATOM_EOVERFLOW, ATOM_NOT_FOUND;
+    ATOM_EOVERFLOW, ATOM_NOT_FOUND, ATOM_WRITE, ATOM_DELETE_OBJECT;
 
 static void engine_dtor(ErlNifEnv* env, void* obj) {
     (void)env;
@@ -224,6 +224,45 @@ static ERL_NIF_TERM nif_route_delete(ErlNifEnv* env, int argc, const ERL_NIF_TER
     return rc ? err(env, rc) : ATOM_OK;
 }
 
+/* route_apply(Engine, [{write | delete_object, Topic, DestId}]) -> {ok, NChanged}
+ * The cluster route delta feed: emqx_route table events (mnesia replication,
+ * cleanup_routes/1 on nodedown, shared-subscription group routes) applied in
+ * order in one call; an absent delete_object is a no-op. */
+static ERL_NIF_TERM nif_route_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_get_list_length(env, argv[1], &n)) return enif_make_badarg(env);
+    uint64_t* offs = enif_alloc(sizeof(uint64_t) * (n + 1));
+    uint32_t* dests = enif_alloc(sizeof(uint32_t) * (n ? n : 1));
+    uint8_t* ops = enif_alloc(n ? n : 1);
+    ErlNifBinary* bins = enif_alloc(sizeof(ErlNifBinary) * (n ? n : 1));
+    ERL_NIF_TERM l = argv[1], h;
+    size_t total = 0;
+    offs[0] = 0;
+    for (unsigned i = 0; i < n; ++i) {
+        const ERL_NIF_TERM* el;
+        int arity;
+        unsigned d;
+        if (!enif_get_list_cell(env, l, &h, &l) || !enif_get_tuple(env, h, &arity, &el) || arity != 3 ||
+            !enif_inspect_binary(env, el[1], &bins[i]) || !enif_get_uint(env, el[2], &d) ||
+            (enif_compare(el[0], ATOM_WRITE) != 0 && enif_compare(el[0], ATOM_DELETE_OBJECT) != 0)) {
+            enif_free(offs); enif_free(dests); enif_free(ops); enif_free(bins);
+            return enif_make_badarg(env);
+        }
+        ops[i] = enif_compare(el[0], ATOM_WRITE) == 0 ? TM_ROUTE_WRITE : TM_ROUTE_DELETE;
+        dests[i] = d;
+        total += bins[i].size;
+        offs[i + 1] = total;
+    }
+    uint8_t* buf = enif_alloc(total ? total : 1);
+    for (unsigned i = 0; i < n; ++i) memcpy(buf + offs[i], bins[i].data, bins[i].size);
+    uint64_t changed = 0;
+    int rc = tm_route_apply(r->e, buf, offs, dests, ops, n, &changed);
+    enif_free(buf); enif_free(offs); enif_free(dests); enif_free(ops); enif_free(bins);
+    return rc ? err(env, rc) : enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, changed));
+}
+
 /* match_routes_batch(Engine, [Topic]) -> [[{Filter, DestId}]]
  * (aggre(emqx_router:match_routes(T)) per publish, resolved on the device) */
 static ERL_NIF_TERM nif_match_routes_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -309,6 +348,8 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
     ATOM_ENODEV = enif_make_atom(env, "enodev");
     ATOM_EOVERFLOW = enif_make_atom(env, "eoverflow");
     ATOM_NOT_FOUND = enif_make_atom(env, "not_found");
+    ATOM_WRITE = enif_make_atom(env, "write");
+    ATOM_DELETE_OBJECT = enif_make_atom(env, "delete_object");
     return 0;
 }
 
@@ -322,6 +363,7 @@ static ErlNifFunc funcs[] = {
     {"match_batch", 2, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_delete", 3, nif_route_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"route_apply", 2, nif_route_apply, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_routes_batch", 2, nif_match_routes_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"rules_match", 4, nif_rules_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"topic_match", 2, nif_topic_match, 0},

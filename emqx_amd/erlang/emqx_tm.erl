@@ -16,6 +16,7 @@
         , topic_match/2
         , route_add/3
         , route_delete/3
+        , route_apply/2
         , match_routes_batch/2
         , rules_match/4
         ]).
@@ -69,6 +70,13 @@ route_add(_Engine, _Topic, _DestId) -> erlang:nif_error(nif_not_loaded).
 %% emqx_router:do_delete_route/2 after the commit.
 -spec(route_delete(reference(), binary(), non_neg_integer()) -> ok | {error, term()}).
 route_delete(_Engine, _Topic, _DestId) -> erlang:nif_error(nif_not_loaded).
+
+%% Cluster route delta feed: emqx_route table events in order, one call
+%% (mnesia replication of remote routes, cleanup_routes/1 on nodedown,
+%% shared-subscription {Group, node()} routes).  Absent delete_object = no-op.
+-spec(route_apply(reference(), [{write | delete_object, binary(), non_neg_integer()}])
+      -> {ok, non_neg_integer()} | {error, term()}).
+route_apply(_Engine, _Events) -> erlang:nif_error(nif_not_loaded).
 
 %% aggre(match_routes(Topic)) for a batch of publishes, resolved on the device.
 -spec(match_routes_batch(reference(), [binary()]) -> [[{binary(), non_neg_integer()}]]).
