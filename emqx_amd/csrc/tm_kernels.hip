@@ -994,9 +994,12 @@ __global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
 constexpr uint32_t FAN_BLOCK = 256;
 constexpr uint32_t FAN_PER = 16;                           // entries per scan thread
 constexpr uint32_t FAN_SCAN_TILE = FAN_BLOCK * FAN_PER;
-constexpr uint32_t FAN_FILL_PER = 16;                      // deliveries per fill thread
+#ifndef TM_FAN_FILL_PER
+#define TM_FAN_FILL_PER 8
+#endif
+constexpr uint32_t FAN_FILL_PER = TM_FAN_FILL_PER;         // deliveries per fill thread (8 or 16)
 constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * FAN_FILL_PER;
-constexpr uint32_t FAN_LDS_ENTRIES = 3072;                 // match entries a fill tile can stage
+constexpr uint32_t FAN_LDS_ENTRIES = FAN_FILL_TILE * 3 / 4;  // match entries a fill tile can stage
 
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
     if (j >= a.n_matches) return 0;
@@ -1128,11 +1131,15 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     }
     __syncthreads();
     // inclusive max-scan of own[] (entry starts only grow along the tile)
-    uint4 q0 = own4[2 * t], q1 = own4[2 * t + 1];
+    constexpr uint32_t NQ = FAN_FILL_PER / 8;                // uint4 words of marks per thread
     uint32_t v[FAN_FILL_PER];
-    const uint32_t wd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) { v[2 * k] = wd[k] & 0xFFFFu; v[2 * k + 1] = wd[k] >> 16; }
+    for (uint32_t q = 0; q < NQ; ++q) {
+        const uint4 u = own4[NQ * t + q];
+        const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) { v[8 * q + 2 * k] = wd[k] & 0xFFFFu; v[8 * q + 2 * k + 1] = wd[k] >> 16; }
+    }
     uint32_t run = 0;
 #pragma unroll
     for (uint32_t k = 0; k < FAN_FILL_PER; ++k) { run = max(run, v[k]); v[k] = run; }
@@ -1147,11 +1154,14 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     if (lane == 0) pre = 0;
     __syncthreads();
     for (uint32_t k = 0; k < w; ++k) pre = max(pre, wmax[k]);
-    uint32_t o[8];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) o[k] = max(v[2 * k], pre) | (max(v[2 * k + 1], pre) << 16);
-    own4[2 * t] = make_uint4(o[0], o[1], o[2], o[3]);
-    own4[2 * t + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    for (uint32_t q = 0; q < NQ; ++q) {
+        uint32_t o[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            o[k] = max(v[8 * q + 2 * k], pre) | (max(v[8 * q + 2 * k + 1], pre) << 16);
+        own4[NQ * t + q] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
     __syncthreads();
     for (uint32_t i = t; i < len; i += FAN_BLOCK) {
         const uint32_t e = (uint32_t)own[i] - 1u;
