@@ -314,6 +314,16 @@ def run_dispatch(args, ws, rank, local, pg):
     f_ms = float(np.mean(ms_fill))
     alg = 8 * total + 20 * m          # read + write a subscriber id; ids[j], moff[j], soff[f] per entry
     achieved = alg / (f_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_dispatch.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("workload") == "dispatch" and pmc.get("topics") == n:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
     out = {
         "metric": "publishes matched + fanned out/sec (node), C2 trie with local subscribers",
         "value": ws * n * args.steps / elapsed,
@@ -329,7 +339,7 @@ def run_dispatch(args, ws, rank, local, pg):
         "match_pipeline_ms": float(np.mean(ms_match)),
         "dispatch_ms": float(np.mean(ms_disp)),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tm_fan_fill",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "tm_fan_fill",
                      "kernel_ms": f_ms, "alg_bytes_per_launch": alg},
     }
     if rank == 0:
