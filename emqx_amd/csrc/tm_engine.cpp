@@ -984,6 +984,8 @@ struct tm_engine {
             HIP_OK(launch_fan_fill(fa, stream));
             HIP_OK(hipEventRecord(b->fev1, stream));
         }
+        const bool want_moff = flags & TM_DISPATCH_MATCH_OFFSETS;
+        if (want_moff) HIP_OK(launch_fan_globalize(fa, stream));   // moff is block-relative until now
         out->n_topics = n;
         out->n_matches = nm;
         out->n_deliveries = total;
@@ -991,14 +993,13 @@ struct tm_engine {
             HIP_OK(hipStreamSynchronize(stream));
             if (!counts_only) HIP_OK(hipEventElapsedTime(&fill_ms, b->fev0, b->fev1));
             out->row_offsets = b->d_drow;
-            out->match_offsets = b->d_moff;
+            out->match_offsets = want_moff ? b->d_moff : nullptr;
             out->subscribers = counts_only ? nullptr : b->d_fout;
             out->fill_ms = fill_ms;
             return TM_OK;
         }
         if ((rc = host_reserve(b->h_drow, b->ch_drow, (size_t)n + 1))) return rc;
         HIP_OK(hipMemcpyAsync(b->h_drow, b->d_drow, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, stream));
-        const bool want_moff = flags & TM_DISPATCH_MATCH_OFFSETS;
         if (want_moff) {
             if ((rc = host_reserve(b->h_moff, b->ch_moff, nm + 1))) return rc;
             HIP_OK(hipMemcpyAsync(b->h_moff, b->d_moff, (nm + 1) * 8, hipMemcpyDeviceToHost, stream));

@@ -187,7 +187,7 @@ struct FanArgs {
     const uint64_t* soff;     // per node id: subscribers soff[f] .. soff[f+1] (nnodes + 1)
     const uint32_t* subs;
     uint32_t nnodes;
-    uint64_t* moff;           // n_matches + 1: deliveries of match entry j
+    uint64_t* moff;           // n_matches + 1: first delivery of match entry j (block-relative until globalized)
     uint64_t* bsums;          // scan block sums (FAN_SCAN_TILE entries per block)
     uint64_t* d_total;
     uint64_t* drow;           // n + 1: deliveries of publish i
@@ -221,6 +221,7 @@ hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
 // offsets (drow), then the load-balanced subscriber copy (out[total])
 hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s);
 hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s);
+hipError_t launch_fan_globalize(const FanArgs& a, hipStream_t s);   // block-relative moff -> global
 uint32_t fan_scan_tile();   // match entries per scan block
 uint32_t fan_fill_tile();   // deliveries per fill block
 hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);

@@ -1001,6 +1001,10 @@ constexpr uint32_t FAN_FILL_PER = TM_FAN_FILL_PER;         // deliveries per fil
 constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * FAN_FILL_PER;
 constexpr uint32_t FAN_LDS_ENTRIES = FAN_FILL_TILE * 3 / 4;  // match entries a fill tile can stage
 
+__device__ inline uint64_t fan_moff(const FanArgs& a, uint64_t j) {
+    return a.moff[j] + a.bsums[j / FAN_SCAN_TILE];
+}
+
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
     if (j >= a.n_matches) return 0;
     const uint32_t f = a.ids[j];
@@ -1060,6 +1064,11 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_
     if (threadIdx.x == 0) *a.d_total = carry;
 }
 
+// After scan_local + scan_sums, moff[j] is relative to its scan block and
+// bsums[b] is the block's exclusive offset: rows, tiles and fill read the sum
+// (bsums is small and cache-resident).  tm_fan_scan_add makes moff global in
+// place -- only when the caller asks for the match offsets, and only after the
+// fill, which no longer needs it.
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_add(FanArgs a) {
     const uint64_t j = (uint64_t)blockIdx.x * FAN_BLOCK + threadIdx.x;
     if (j <= a.n_matches) a.moff[j] += a.bsums[j / FAN_SCAN_TILE];
@@ -1067,14 +1076,14 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_add(FanArgs a) {
 
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_rows(FanArgs a) {
     const uint32_t i = blockIdx.x * FAN_BLOCK + threadIdx.x;
-    if (i <= a.n) a.drow[i] = a.moff[a.row_off[i]];
+    if (i <= a.n) a.drow[i] = fan_moff(a, a.row_off[i]);
 }
 
 // first j in [lo, hi) with moff[j] > p (hi if none)
-__device__ inline uint64_t fan_upper(const uint64_t* moff, uint64_t lo, uint64_t hi, uint64_t p) {
+__device__ inline uint64_t fan_upper(const FanArgs& a, uint64_t lo, uint64_t hi, uint64_t p) {
     while (lo < hi) {
         const uint64_t m = (lo + hi) >> 1;
-        if (moff[m] > p) hi = m;
+        if (fan_moff(a, m) > p) hi = m;
         else lo = m + 1;
     }
     return lo;
@@ -1087,7 +1096,7 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_tiles(FanArgs a, uint64_t nt
     const uint64_t k = (uint64_t)blockIdx.x * FAN_BLOCK + threadIdx.x;
     if (k > ntiles) return;
     const uint64_t p = k < ntiles ? k * FAN_FILL_TILE : a.total - 1;
-    a.tile_j[k] = fan_upper(a.moff, 0, a.n_matches + 1, p) - 1;
+    a.tile_j[k] = fan_upper(a, 0, a.n_matches + 1, p) - 1;
 }
 
 // One workgroup per 4096 consecutive deliveries.  The entries covering the
@@ -1113,8 +1122,8 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
         // per thread, so each search starts at the previous entry
         uint64_t j = jlo;
         for (uint64_t p = start + t; p < end; p += FAN_BLOCK) {
-            j = fan_upper(a.moff, j, jhi + 1, p) - 1;
-            a.out[p] = a.subs[a.soff[a.ids[j]] + (p - a.moff[j])];
+            j = fan_upper(a, j, jhi + 1, p) - 1;
+            a.out[p] = a.subs[a.soff[a.ids[j]] + (p - fan_moff(a, j))];
         }
         return;
     }
@@ -1123,7 +1132,7 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     __syncthreads();
     for (uint32_t e = t; e < (uint32_t)ne; e += FAN_BLOCK) {
         const uint64_t j = jlo + e;
-        const uint64_t m0 = a.moff[j], m1 = a.moff[j + 1];
+        const uint64_t m0 = fan_moff(a, j), m1 = fan_moff(a, j + 1);
         if (m1 > m0 && m1 > start && m0 < end) {
             base[e] = (int64_t)a.soff[a.ids[j]] - (int64_t)m0;
             own[m0 > start ? (uint32_t)(m0 - start) : 0u] = (uint16_t)(e + 1);
@@ -1476,8 +1485,13 @@ hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s) {
     const uint32_t nb = (uint32_t)((ne + FAN_SCAN_TILE - 1) / FAN_SCAN_TILE);
     hipLaunchKernelGGL(tm_fan_scan_local, dim3(nb), dim3(FAN_BLOCK), 0, s, a);
     hipLaunchKernelGGL(tm_fan_scan_sums, dim3(1), dim3(FAN_BLOCK), 0, s, a, nb);
-    hipLaunchKernelGGL(tm_fan_scan_add, dim3((uint32_t)((ne + FAN_BLOCK - 1) / FAN_BLOCK)), dim3(FAN_BLOCK), 0, s, a);
     hipLaunchKernelGGL(tm_fan_rows, dim3((a.n + 1 + FAN_BLOCK - 1) / FAN_BLOCK), dim3(FAN_BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fan_globalize(const FanArgs& a, hipStream_t s) {
+    const uint64_t ne = a.n_matches + 1;
+    hipLaunchKernelGGL(tm_fan_scan_add, dim3((uint32_t)((ne + FAN_BLOCK - 1) / FAN_BLOCK)), dim3(FAN_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 

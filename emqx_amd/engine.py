@@ -101,9 +101,10 @@ class Batch:
             subs = np.ctypeslib.as_array(d.subscribers, shape=(t,)).copy() if t else np.zeros(0, np.uint32)
         return offs, moff, subs
 
-    def dispatch_device(self):
-        """Device-resident fan-out: -> (n_deliveries, fill kernel ms, device ptrs row/moff/subs)."""
-        d = self._dispatch(N.TM_DISPATCH_DEVICE)
+    def dispatch_device(self, match_offsets: bool = False):
+        """Device-resident fan-out: -> (n_deliveries, fill kernel ms, device ptrs row/moff/subs);
+        the moff pointer is None unless match_offsets."""
+        d = self._dispatch(N.TM_DISPATCH_DEVICE | (N.TM_DISPATCH_MATCH_OFFSETS if match_offsets else 0))
         ptr = lambda p: C.cast(p, C.c_void_p).value  # noqa: E731
         return int(d.n_deliveries), float(d.fill_ms), ptr(d.row_offsets), ptr(d.match_offsets), ptr(d.subscribers)
 

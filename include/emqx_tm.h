@@ -252,7 +252,9 @@ TM_API int  tm_subscriber_down(tm_engine* e, uint32_t subscriber, uint32_t node_
  * first delivery of match entry j, i.e. of filter ids[j] of tm_batch_result.
  * TM_DISPATCH_COUNT_ONLY: counts only, subscribers = NULL.
  * TM_DISPATCH_DEVICE: no copy back; the pointers are device memory of the
- * batch, valid until its next dispatch or re-prepare.  Otherwise engine-owned
+ * batch, valid until its next dispatch or re-prepare (match_offsets only with
+ * TM_DISPATCH_MATCH_OFFSETS too: without it the engine skips making them
+ * global).  Otherwise engine-owned
  * pinned memory valid likewise.  fill_ms = device time of the copy kernel. */
 typedef struct {
     uint32_t        n_topics;

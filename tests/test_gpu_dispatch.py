@@ -75,7 +75,11 @@ def test_dispatch_skewed_fanout_and_modes():
     c_offs, _, none = b.dispatch(counts_only=True)
     assert none is None and np.array_equal(c_offs, offs)
     total, fill_ms, d_row, d_moff, d_subs = b.dispatch_device()
-    assert total == int(offs[-1]) and fill_ms > 0 and d_subs
+    assert total == int(offs[-1]) and fill_ms > 0 and d_subs and d_moff is None
+    total, _, _, d_moff, _ = b.dispatch_device(match_offsets=True)
+    assert total == int(offs[-1]) and d_moff
+    offs2, moff2, out2 = b.dispatch(match_offsets=True)        # re-dispatch: offsets made global once
+    assert np.array_equal(moff2, moff) and np.array_equal(offs2, offs) and np.array_equal(out2, out)
     names = [eng.filter_bytes(int(i)) for i in ids]
     for i, t in enumerate(T):
         exp = []
