@@ -850,7 +850,9 @@ struct tm_engine {
     uint64_t sub_entries = 0, subs_version = 0;
     uint64_t* d_soff = nullptr;
     uint32_t* d_subs = nullptr;
-    size_t c_soff = 0, c_subs = 0;
+    uint8_t* d_scnt = nullptr;    // per node: min(soff[f + 1] - soff[f], 255) (the scan's 1-B gather)
+    size_t c_soff = 0, c_subs = 0, c_scnt = 0;
+    std::vector<uint8_t> h_scnt;
     uint32_t subs_nn = 0;
     std::vector<uint64_t> h_soff;
     std::vector<uint32_t> h_subs;
@@ -936,10 +938,14 @@ struct tm_engine {
         for (size_t i = 0; i < nn; ++i) h_soff[i + 1] += h_soff[i];
         h_subs.resize(h_soff[nn]);
         for (const auto& r : runs) std::copy(r.second->begin(), r.second->end(), h_subs.begin() + (long)h_soff[r.first]);
+        h_scnt.resize(std::max<size_t>(nn, 1));
+        for (size_t i = 0; i < nn; ++i) h_scnt[i] = (uint8_t)std::min<uint64_t>(h_soff[i + 1] - h_soff[i], 255);
         int rc;
         if ((rc = dev_reserve(d_soff, c_soff, nn + 1))) return rc;
+        if ((rc = dev_reserve(d_scnt, c_scnt, std::max<size_t>(nn, 1)))) return rc;
         if ((rc = dev_reserve(d_subs, c_subs, std::max<size_t>(h_subs.size(), 1)))) return rc;
         HIP_OK(hipMemcpyAsync(d_soff, h_soff.data(), (nn + 1) * 8, hipMemcpyHostToDevice, stream));
+        if (nn) HIP_OK(hipMemcpyAsync(d_scnt, h_scnt.data(), nn, hipMemcpyHostToDevice, stream));
         if (!h_subs.empty())
             HIP_OK(hipMemcpyAsync(d_subs, h_subs.data(), h_subs.size() * 4, hipMemcpyHostToDevice, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -968,7 +974,7 @@ struct tm_engine {
         }
         FanArgs fa{};
         fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
-        fa.soff = d_soff; fa.subs = d_subs; fa.nnodes = subs_nn;
+        fa.soff = d_soff; fa.scnt = d_scnt; fa.subs = d_subs; fa.nnodes = subs_nn;
         fa.moff = b->d_moff; fa.bsums = b->d_fbsums; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
         HIP_OK(launch_fan_scan(fa, stream));
         HIP_OK(hipMemcpyAsync(b->h_ftotal, b->d_ftotal, 8, hipMemcpyDeviceToHost, stream));
@@ -1800,7 +1806,7 @@ struct tm_engine {
             if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
             dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
-            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs);
+            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);

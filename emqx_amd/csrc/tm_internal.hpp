@@ -185,6 +185,7 @@ struct FanArgs {
     uint32_t n;
     uint64_t n_matches;
     const uint64_t* soff;     // per node id: subscribers soff[f] .. soff[f+1] (nnodes + 1)
+    const uint8_t* scnt;      // per node id: min(soff[f + 1] - soff[f], 255); 255 = read soff
     const uint32_t* subs;
     uint32_t nnodes;
     uint64_t* moff;           // n_matches + 1: first delivery of match entry j (block-relative until globalized)

@@ -1008,7 +1008,9 @@ __device__ inline uint64_t fan_moff(const FanArgs& a, uint64_t j) {
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
     if (j >= a.n_matches) return 0;
     const uint32_t f = a.ids[j];
-    return f < a.nnodes ? a.soff[f + 1] - a.soff[f] : 0;
+    if (f >= a.nnodes) return 0;
+    const uint32_t c = a.scnt[f];   // 1 B per node: the gather's footprint stays L2-sized
+    return c < 255 ? c : a.soff[f + 1] - a.soff[f];
 }
 
 // Exclusive scan of one u64 per thread over a 256-thread block (4 waves).
