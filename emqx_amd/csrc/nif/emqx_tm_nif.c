@@ -263,6 +263,80 @@ static ERL_NIF_TERM nif_route_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     return rc ? err(env, rc) : enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, changed));
 }
 
+/* subscribe(Engine, Topic, SubId, NodeDestId) -> ok
+ * emqx_broker:do_subscribe/4, non-shared (src/emqx_broker.erl:150-158): the
+ * topic's first local subscriber also adds the (Topic, node()) route. */
+static ERL_NIF_TERM nif_subscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    unsigned sub, dest;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b) || !enif_get_uint(env, argv[2], &sub) ||
+        !enif_get_uint(env, argv[3], &dest))
+        return enif_make_badarg(env);
+    int rc = tm_subscribe(r->e, b.data, b.size, sub, dest);
+    return rc ? err(env, rc) : ATOM_OK;
+}
+
+/* unsubscribe(Engine, Topic, SubId, NodeDestId) -> ok  (do_unsubscribe/4, :179-191;
+ * not subscribed -> ok, as unsubscribe/1's `[] -> ok`) */
+static ERL_NIF_TERM nif_unsubscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    ErlNifBinary b;
+    unsigned sub, dest;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b) || !enif_get_uint(env, argv[2], &sub) ||
+        !enif_get_uint(env, argv[3], &dest))
+        return enif_make_badarg(env);
+    int rc = tm_unsubscribe(r->e, b.data, b.size, sub, dest);
+    return (rc && rc != TM_ENOENT) ? err(env, rc) : ATOM_OK;
+}
+
+/* subscriber_down(Engine, SubId, NodeDestId) -> {ok, NRemoved}  (subscriber_down/1, :332-347) */
+static ERL_NIF_TERM nif_subscriber_down(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned sub, dest;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !enif_get_uint(env, argv[1], &sub) || !enif_get_uint(env, argv[2], &dest))
+        return enif_make_badarg(env);
+    uint64_t n = 0;
+    int rc = tm_subscriber_down(r->e, sub, dest, &n);
+    return rc ? err(env, rc) : enif_make_tuple2(env, ATOM_OK, enif_make_uint64(env, n));
+}
+
+/* dispatch_batch(Engine, [Topic]) -> [[SubId]]
+ * Per publish, the local deliveries dispatch/2 makes (src/emqx_broker.erl:284-309):
+ * the subscribers of every matched filter, filters in Erlang binary order, each
+ * filter's subscribers in subscription order; [] = {error, no_subscribers}. */
+static ERL_NIF_TERM nif_dispatch_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    engine_res* r;
+    unsigned n;
+    uint8_t* buf;
+    uint64_t* offs;
+    (void)argc;
+    if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
+    tm_batch* b = NULL;
+    tm_deliveries d;
+    int rc = tm_batch_prepare(r->e, buf, offs, n, &b);
+    if (!rc) rc = tm_batch_launch(r->e, b);
+    if (!rc) rc = tm_batch_wait(r->e, b);
+    if (!rc) rc = tm_batch_dispatch(r->e, b, 0, &d);
+    enif_free(buf); enif_free(offs);
+    if (rc) {
+        if (b) tm_batch_free(r->e, b);
+        return err(env, rc);
+    }
+    ERL_NIF_TERM out = enif_make_list(env, 0);
+    for (unsigned i = n; i-- > 0;) {
+        ERL_NIF_TERM row = enif_make_list(env, 0);
+        for (uint64_t k = d.row_offsets[i + 1]; k-- > d.row_offsets[i];)
+            row = enif_make_list_cell(env, enif_make_uint(env, d.subscribers[k]), row);
+        out = enif_make_list_cell(env, row, out);
+    }
+    tm_batch_free(r->e, b);
+    return out;
+}
+
 /* match_routes_batch(Engine, [Topic]) -> [[{Filter, DestId}]]
  * (aggre(emqx_router:match_routes(T)) per publish, resolved on the device) */
 static ERL_NIF_TERM nif_match_routes_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -364,6 +438,10 @@ static ErlNifFunc funcs[] = {
     {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_delete", 3, nif_route_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_apply", 2, nif_route_apply, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"subscribe", 4, nif_subscribe, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"unsubscribe", 4, nif_unsubscribe, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"subscriber_down", 3, nif_subscriber_down, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"dispatch_batch", 2, nif_dispatch_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"match_routes_batch", 2, nif_match_routes_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"rules_match", 4, nif_rules_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"topic_match", 2, nif_topic_match, 0},

@@ -17,6 +17,10 @@
         , route_add/3
         , route_delete/3
         , route_apply/2
+        , subscribe/4
+        , unsubscribe/4
+        , subscriber_down/3
+        , dispatch_batch/2
         , match_routes_batch/2
         , rules_match/4
         ]).
@@ -77,6 +81,23 @@ route_delete(_Engine, _Topic, _DestId) -> erlang:nif_error(nif_not_loaded).
 -spec(route_apply(reference(), [{write | delete_object, binary(), non_neg_integer()}])
       -> {ok, non_neg_integer()} | {error, term()}).
 route_apply(_Engine, _Events) -> erlang:nif_error(nif_not_loaded).
+
+%% Local subscriber bag (emqx_broker do_subscribe/4, do_unsubscribe/4,
+%% subscriber_down/1, non-shared): SubId = the caller's id of the subscriber
+%% pid, NodeDestId = its id of node() in route_add/3.
+-spec(subscribe(reference(), binary(), non_neg_integer(), non_neg_integer()) -> ok | {error, term()}).
+subscribe(_Engine, _Topic, _SubId, _NodeDestId) -> erlang:nif_error(nif_not_loaded).
+
+-spec(unsubscribe(reference(), binary(), non_neg_integer(), non_neg_integer()) -> ok | {error, term()}).
+unsubscribe(_Engine, _Topic, _SubId, _NodeDestId) -> erlang:nif_error(nif_not_loaded).
+
+-spec(subscriber_down(reference(), non_neg_integer(), non_neg_integer()) -> {ok, non_neg_integer()} | {error, term()}).
+subscriber_down(_Engine, _SubId, _NodeDestId) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_broker:dispatch/2 fan-out for a batch of publishes: per publish the
+%% SubIds to deliver to ([] = {error, no_subscribers}).
+-spec(dispatch_batch(reference(), [binary()]) -> [[non_neg_integer()]]).
+dispatch_batch(_Engine, _Topics) -> erlang:nif_error(nif_not_loaded).
 
 %% aggre(match_routes(Topic)) for a batch of publishes, resolved on the device.
 -spec(match_routes_batch(reference(), [binary()]) -> [[{binary(), non_neg_integer()}]]).
