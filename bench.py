@@ -458,6 +458,10 @@ def main():
         raise RuntimeError(f"batch stats inconsistent: {st}")
 
     def barrier():
+        # wait() has drained the engine's stream (hipEventSynchronize), the only
+        # stream this process uses.  torch.cuda is not initialised here at N=1:
+        # initialising it after the engine's HIP runtime reports "No HIP GPUs
+        # are available" (gpurun_out v16, round 1), so no torch synchronize.
         if pg is not None:
             pg.barrier()
 
