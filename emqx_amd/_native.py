@@ -103,6 +103,8 @@ SIGNATURES = {
     "tm_trie_empty": (C.c_int, [P]),
     "tm_trie_match": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_match_coalesced": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "tm_coalesce_config": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "tm_batch_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
     "tm_batch_prepare_ex": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
     "tm_batch_row_map": (C.c_int, [P, P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint32)]),
@@ -139,6 +141,7 @@ SIGNATURES = {
     "tm_rules_match": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),
+    "tm_device_count": (C.c_int, []),
 }
 
 _lib = None
@@ -169,9 +172,10 @@ def check(rc, what=""):
 
 
 def gpu_available() -> bool:
-    """True when a HIP device is visible (checked without initialising HIP twice)."""
+    """True when a HIP device is visible, asked through the engine's own HIP
+    runtime (torch.cuda.is_available() turns False once the engine has
+    initialised HIP first in the process, so it is not asked)."""
     try:
-        import torch
-        return torch.cuda.is_available() and torch.cuda.device_count() > 0
-    except Exception:
+        return lib().tm_device_count() > 0
+    except (ImportError, OSError):
         return False

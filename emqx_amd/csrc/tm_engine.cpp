@@ -13,6 +13,8 @@
 // the reference's tests (test/emqx_trie_SUITE.erl:49-142).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -301,8 +303,27 @@ struct tm_batch {
 
 // ==================================================================== engine
 
+// One tm_match_coalesced caller waiting for its row.
+struct CoalesceReq {
+    const uint8_t* topic;
+    size_t len;
+    uint32_t* ids;
+    uint32_t cap;
+    uint32_t n_out;
+    int rc;
+    bool done;
+};
+
 struct tm_engine {
     std::recursive_mutex mu;
+    // tm_match_coalesced: pending single-topic callers; the first caller to find
+    // no leader becomes it, lingers, and runs one batch for everyone queued
+    std::mutex cmu;
+    std::condition_variable ccv;
+    std::vector<CoalesceReq*> cpending;
+    bool cleader = false;
+    uint32_t c_max = 65536, c_linger_us = 50;
+    uint64_t c_batches = 0, c_requests = 0;
     int device = -1;
     unsigned threads = 1;
     hipStream_t stream = nullptr;
@@ -1994,6 +2015,81 @@ int tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offset
     return tm_batch_prepare_ex(e, topics, offsets, n, 0, out);
 }
 
+// The leader's device round trip for a set of queued callers: one
+// tm_match_batch under the engine lock (its result buffers stay valid while the
+// rows are copied out); if the batch fails, each caller is matched alone so a
+// bad topic fails only its own request.
+static void coalesce_run(tm_engine* e, std::vector<CoalesceReq*>& batch) {
+    std::vector<uint8_t> buf;
+    std::vector<uint64_t> offs(batch.size() + 1, 0);
+    for (size_t i = 0; i < batch.size(); ++i) {
+        buf.insert(buf.end(), batch[i]->topic, batch[i]->topic + batch[i]->len);
+        offs[i + 1] = buf.size();
+    }
+    static const uint8_t zero = 0;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    tm_result r;
+    int rc = tm_match_batch(e, buf.empty() ? &zero : buf.data(), offs.data(), (uint32_t)batch.size(), &r);
+    if (rc == TM_OK) {
+        for (size_t i = 0; i < batch.size(); ++i) {
+            CoalesceReq* q = batch[i];
+            const uint32_t lo = r.row_offsets[i], m = r.row_offsets[i + 1] - lo;
+            for (uint32_t k = 0; k < m && k < q->cap; ++k) q->ids[k] = r.filter_ids[lo + k];
+            q->n_out = m;
+            q->rc = TM_OK;
+        }
+        return;
+    }
+    for (CoalesceReq* q : batch) q->rc = tm_trie_match(e, q->topic, q->len, q->ids, q->cap, &q->n_out);
+}
+
+int tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len, uint32_t* ids, uint32_t cap, uint32_t* n_out) {
+    if (!e || !n_out || (!topic && len) || (cap && !ids)) return TM_EINVAL;
+    if (len > TM_MAX_TOPIC_LEN) return TM_EINVAL;
+    CoalesceReq req{topic, len, ids, cap, 0, TM_OK, false};
+    std::unique_lock<std::mutex> lk(e->cmu);
+    e->cpending.push_back(&req);
+    e->ccv.notify_all();   // a lingering leader re-checks the batch size
+    while (!req.done) {
+        if (e->cleader) {
+            e->ccv.wait(lk);
+            continue;
+        }
+        e->cleader = true;
+        const size_t max_b = std::max<uint32_t>(e->c_max, 1);
+        e->ccv.wait_for(lk, std::chrono::microseconds(e->c_linger_us),
+                        [&] { return e->cpending.size() >= max_b; });
+        std::vector<CoalesceReq*> batch;
+        const size_t take = std::min(e->cpending.size(), max_b);
+        batch.assign(e->cpending.begin(), e->cpending.begin() + (long)take);
+        e->cpending.erase(e->cpending.begin(), e->cpending.begin() + (long)take);
+        lk.unlock();
+        try {
+            coalesce_run(e, batch);
+        } catch (...) {
+            for (CoalesceReq* q : batch) q->rc = TM_ENOMEM;
+        }
+        lk.lock();
+        for (CoalesceReq* q : batch) q->done = true;
+        ++e->c_batches;
+        e->c_requests += batch.size();
+        e->cleader = false;
+        e->ccv.notify_all();
+    }
+    *n_out = req.n_out;
+    return req.rc;
+}
+
+int tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us, uint64_t* batches, uint64_t* requests) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::mutex> lk(e->cmu);
+    if (max_batch) e->c_max = max_batch;
+    if (linger_us != TM_NONE) e->c_linger_us = linger_us;
+    if (batches) *batches = e->c_batches;
+    if (requests) *requests = e->c_requests;
+    return TM_OK;
+}
+
 int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
                         tm_batch** out) {
     if (!e || !offsets || !out || (!topics && n) || (flags & ~TM_BATCH_DEDUP)) return TM_EINVAL;
@@ -2434,6 +2530,11 @@ int tm_topic_validate(int is_name, const uint8_t* t, size_t len, const char** re
 }
 
 const char* tm_last_error(void) { return last_error(); }
+
+int tm_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 
 const char* tm_build_info(void) {
     return "emqx_tm gfx950 frontier-tile kernel; slots=32B buckets=64B; path-code sort; " __DATE__;

@@ -209,6 +209,24 @@ class Engine:
     def match(self, topic: bytes):
         return [self.filter_bytes(i) for i in self.match_ids(topic)]
 
+    def match_coalesced(self, topic: bytes):
+        """emqx_trie:match/1 ids through tm_match_coalesced: concurrent callers
+        (threads; ctypes drops the GIL) share device batches."""
+        cap = 1024
+        while True:
+            ids = (C.c_uint32 * cap)()
+            n = C.c_uint32()
+            N.check(self.L.tm_match_coalesced(self.h, topic, len(topic), ids, cap, C.byref(n)), "tm_match_coalesced")
+            if n.value <= cap:
+                return list(ids[:n.value])
+            cap = n.value
+
+    def coalesce_config(self, max_batch: int = 0, linger_us: int = N.TM_NONE):
+        """-> (batches, requests) served by tm_match_coalesced so far."""
+        b, r = C.c_uint64(), C.c_uint64()
+        N.check(self.L.tm_coalesce_config(self.h, max_batch, linger_us, C.byref(b), C.byref(r)), "tm_coalesce_config")
+        return int(b.value), int(r.value)
+
     # ---- batches -----------------------------------------------------------
     def match_batch(self, topics):
         """-> (row_offsets uint32[n+1], filter_ids uint32[total]); rows sorted by filter bytes."""

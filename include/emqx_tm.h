@@ -134,6 +134,22 @@ TM_API int  tm_trie_empty(tm_engine* e);
 TM_API int  tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len,
                    uint32_t* ids, uint32_t cap, uint32_t* n_out);
 
+/* emqx_trie:match/1 for one topic, called concurrently by many threads (the
+ * NIF's dirty schedulers, one call per publishing process): callers that
+ * arrive while a device batch is being formed are coalesced into one
+ * tm_match_batch -- the first caller without a running leader lingers up to
+ * linger_us (or until max_batch callers queue), then matches all of them in one
+ * device round trip; later callers form the next batch.  emqx_batch's size +
+ * linger policy (src/emqx_batch.erl:49-90) applied across callers.  Results and
+ * errors as tm_trie_match, per caller (len > TM_MAX_TOPIC_LEN -> TM_EINVAL). */
+TM_API int  tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len,
+                               uint32_t* ids, uint32_t cap, uint32_t* n_out);
+/* Sets max_batch (0 = keep; default 65536) and linger_us (TM_NONE = keep;
+ * default 50); *batches / *requests (may be NULL) = coalesced batches run and
+ * requests served so far. */
+TM_API int  tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us,
+                               uint64_t* batches, uint64_t* requests);
+
 /* ---- batched publish matching: emqx_router:match_routes/1 hot path ---- */
 /* (src/emqx_router.erl:127-141 applied to a batch of publishes,
  *  src/emqx_broker.erl:201-210).  topics = concatenated topic bytes,
@@ -364,6 +380,8 @@ TM_API int  tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* n
 /* Text of the last TM_EIO on this thread (HIP error string + call site). */
 TM_API const char* tm_last_error(void);
 TM_API const char* tm_build_info(void);
+/* Number of visible HIP devices (0 when there is no driver or device). */
+TM_API int  tm_device_count(void);
 
 #ifdef __cplusplus
 }
