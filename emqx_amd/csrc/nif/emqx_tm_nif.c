@@ -143,17 +143,33 @@ static ERL_NIF_TERM rows_to_terms(ErlNifEnv* env, tm_engine* e, const tm_result*
     return list;
 }
 
-/* match(Engine, Topic) -> [Filter]  (emqx_trie:match/1, :96-99; sorted set) */
+/* match(Engine, Topic) -> [Filter]  (emqx_trie:match/1, :96-99; sorted set).
+ * One call per publishing process: concurrent calls are coalesced into shared
+ * device batches by tm_match_coalesced. */
 static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     engine_res* r;
     ErlNifBinary b;
     (void)argc;
     if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
-    const uint64_t offs[2] = {0, b.size};
-    tm_result res;
-    int rc = tm_match_batch(r->e, b.size ? b.data : (const uint8_t*)"", offs, 1, &res);
-    if (rc) return err(env, rc);
-    return rows_to_terms(env, r->e, &res, 0);
+    uint32_t local[256];
+    uint32_t* ids = local;
+    uint32_t cap = 256, n = 0;
+    int rc = tm_match_coalesced(r->e, b.size ? b.data : (const uint8_t*)"", b.size, ids, cap, &n);
+    if (!rc && n > cap) {                     /* a longer row: ask again with room for it */
+        cap = n;
+        ids = enif_alloc(sizeof(uint32_t) * cap);
+        rc = tm_match_coalesced(r->e, b.size ? b.data : (const uint8_t*)"", b.size, ids, cap, &n);
+        if (!rc && n > cap) n = cap;          /* the trie grew in between: the first cap ids */
+    }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    if (!rc)
+        for (uint32_t i = n; i-- > 0;) {
+            size_t len = 0;
+            const uint8_t* p = tm_filter_bytes(r->e, ids[i], &len);
+            list = enif_make_list_cell(env, make_bin(env, p, len), list);
+        }
+    if (ids != local) enif_free(ids);
+    return rc ? err(env, rc) : list;
 }
 
 /* Concatenates a list of binaries: buf/offs are enif_alloc'ed (caller frees). */
