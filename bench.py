@@ -259,6 +259,51 @@ def run_c5(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
+def run_coalesce(args, ws, rank, local, pg):
+    """Per-publish emqx_trie:match/1 calls from many concurrent callers
+    (tm_match_coalesced, what the NIF's match/2 does): C2 trie, 64 threads each
+    matching its own slice of the publishes one topic per call.  Reports calls/s
+    and the mean coalesced batch size; Python threads (ctypes drops the GIL in
+    the call) stand in for the BEAM's dirty schedulers."""
+    import threading
+
+    from emqx_amd import gen
+    from emqx_amd.engine import Engine
+
+    p = gen.C2
+    filters = gen.gen_filters(p)
+    n = min(args.topics, 400_000)
+    topics = gen.gen_topics(p, filters, 1000 + rank, n).tolist()
+    eng = Engine(device=local)
+    eng.insert_many(filters.tolist())
+    eng.sync()
+    eng.coalesce_config(linger_us=args.coalesce_linger_us)
+    for t in topics[:1000]:
+        eng.match_coalesced(t)
+    b0, r0 = eng.coalesce_config()
+    nth = 64
+
+    def worker(k):
+        for i in range(k, n, nth):
+            eng.match_coalesced(topics[i])
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(nth)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    elapsed = time.perf_counter() - t0
+    b1, r1 = eng.coalesce_config()
+    out = {"metric": "emqx_trie:match/1 calls/sec through tm_match_coalesced (64 concurrent callers)",
+           "value": n / elapsed, "unit": "calls/s", "n_gpus": ws, "steps": 1, "warmup": 1,
+           "ms_per_step": 1e3 * elapsed, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u32", "data": "synthetic (seeded C2 generator)",
+           "config": {"workload": f"coalesce: C2 1M filters, {n} single-topic calls, {nth} threads"},
+           "batches": b1 - b0, "mean_batch": (r1 - r0) / max(b1 - b0, 1), "linger_us": args.coalesce_linger_us}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def run_dispatch(args, ws, rank, local, pg):
     """Publish -> match -> fan-out on the device: the C2
     trie and publishes, every filter with local subscribers (75% one, 24% 2-8,
@@ -401,9 +446,10 @@ def main():
                     help="publishes of the host-inclusive end-to-end measurement")
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (no latency / e2e / cpu legs): for rocprofv3 runs")
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "dispatch"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "dispatch", "coalesce"], default="c2",
                     help="c2: 1M wildcard filters, replicated (the BASELINE metric); c4: IoT filters, sharded; "
                          "c5: hot-topic skew + churn")
+    ap.add_argument("--coalesce-linger-us", type=int, default=0, help="coalesce leg: leader linger")
     ap.add_argument("--c5-k", type=int, default=100, help="C5 filters per hot topic (10 / 100 / 1000)")
     ap.add_argument("--c5-deltas", type=int, default=10_000, help="C5 subscribe/unsubscribe deltas per step")
     ap.add_argument("--c4-filters", type=int, default=0, help="C4 filter count (default 100M)")
@@ -425,6 +471,8 @@ def main():
         return run_c5(args, ws, rank, local, pg)
     if args.workload == "dispatch":
         return run_dispatch(args, ws, rank, local, pg)
+    if args.workload == "coalesce":
+        return run_coalesce(args, ws, rank, local, pg)
 
     from emqx_amd import gen
     from emqx_amd.engine import Engine

@@ -322,7 +322,7 @@ struct tm_engine {
     std::condition_variable ccv;
     std::vector<CoalesceReq*> cpending;
     bool cleader = false;
-    uint32_t c_max = 65536, c_linger_us = 50;
+    uint32_t c_max = 65536, c_linger_us = 0;
     uint64_t c_batches = 0, c_requests = 0;
     int device = -1;
     unsigned threads = 1;

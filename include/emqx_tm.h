@@ -145,7 +145,7 @@ TM_API int  tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len,
 TM_API int  tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len,
                                uint32_t* ids, uint32_t cap, uint32_t* n_out);
 /* Sets max_batch (0 = keep; default 65536) and linger_us (TM_NONE = keep;
- * default 50); *batches / *requests (may be NULL) = coalesced batches run and
+ * default 0: the batch is whoever queued while the previous one ran); *batches / *requests (may be NULL) = coalesced batches run and
  * requests served so far. */
 TM_API int  tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us,
                                uint64_t* batches, uint64_t* requests);
