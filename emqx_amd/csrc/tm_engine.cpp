@@ -1766,18 +1766,23 @@ struct tm_engine {
     int result(tm_batch* b, tm_result* out) {
         if (!b->done) return TM_EINVAL;
         int rc;
-        if ((rc = host_reserve(b->h_rowoff, b->ch_rowoff, (size_t)b->n + 1))) return rc;
-        HIP_OK(hipMemcpyAsync(b->h_rowoff, b->d_rowoff, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipStreamSynchronize(stream));
-        const uint64_t total = b->h_rowoff[b->n];
-        if (total > b->c_ids || total != b->total) {
-            snprintf(last_error(), 512, "inconsistent CSR: total %llu, capacity %zu, kernel count %llu",
-                     (unsigned long long)total, b->c_ids, (unsigned long long)b->total);
+        // the match count is known since wait(): both copies go out behind one sync
+        const uint64_t total = b->total;
+        if (total > b->c_ids) {
+            snprintf(last_error(), 512, "inconsistent CSR: kernel count %llu, capacity %zu",
+                     (unsigned long long)total, b->c_ids);
             return TM_EIO;
         }
+        if ((rc = host_reserve(b->h_rowoff, b->ch_rowoff, (size_t)b->n + 1))) return rc;
         if ((rc = host_reserve(b->h_ids, b->ch_ids, std::max<uint64_t>(total, 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(b->h_rowoff, b->d_rowoff, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, stream));
         if (total) HIP_OK(hipMemcpyAsync(b->h_ids, b->d_ids, total * 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
+        if (b->h_rowoff[b->n] != total) {
+            snprintf(last_error(), 512, "inconsistent CSR: row offsets end at %u, kernel count %llu",
+                     b->h_rowoff[b->n], (unsigned long long)total);
+            return TM_EIO;
+        }
         out->n_topics = b->n;
         out->n_matches = total;
         out->row_offsets = b->h_rowoff;
