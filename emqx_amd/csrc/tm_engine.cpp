@@ -324,6 +324,7 @@ struct tm_engine {
     bool cleader = false;
     uint32_t c_max = 65536, c_linger_us = 0;
     uint64_t c_batches = 0, c_requests = 0;
+    bool upload_nosync = false;   // set by tm_match_batch (prepare -> launch -> wait in one call)
     int device = -1;
     unsigned threads = 1;
     hipStream_t stream = nullptr;
@@ -1626,7 +1627,9 @@ struct tm_engine {
         if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
         if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
         HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipStreamSynchronize(stream));
+        // the caller's buffers are only borrowed for the call; tm_match_batch
+        // waits for the whole pipeline before returning, so it skips this sync
+        if (!upload_nosync) HIP_OK(hipStreamSynchronize(stream));
         b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
         b->dev_tok = true;
         b->tok_dict = ~0ull;
@@ -1994,11 +1997,15 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
     int rc = e->set_device();
     if (rc) return rc;
     try {
-        if ((rc = e->prepare(&e->scratch, topics, offsets, n))) return rc;
+        e->upload_nosync = true;
+        rc = e->prepare(&e->scratch, topics, offsets, n);
+        e->upload_nosync = false;
+        if (rc) return rc;
         if ((rc = e->launch(&e->scratch))) return rc;
         if ((rc = e->wait(&e->scratch))) return rc;
         return e->result(&e->scratch, out);
     } catch (...) {
+        e->upload_nosync = false;
         return TM_ENOMEM;
     }
 }
