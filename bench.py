@@ -62,10 +62,42 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(filters, topics, sample_1t, sample_mt, threads):
+def host_cpu_share() -> dict:
+    """CPUs this process may really use: the affinity mask capped by the cgroup
+    CPU quota (cpu.max).  On the GPU box os.cpu_count() / nproc report the whole
+    machine (256 threads of two EPYC 9575F) while the lease's cgroup grants 16
+    CPUs of bandwidth, so more threads than the quota only time-slice."""
+    info = {"nproc": os.cpu_count() or 1, "affinity": len(os.sched_getaffinity(0)), "cgroup_quota": None}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            info["cgroup_quota"] = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    share = info["affinity"]
+    if info["cgroup_quota"]:
+        share = min(share, max(1, int(info["cgroup_quota"] + 0.5)))
+    info["threads"] = share
+    info["model"] = cpu_info()
+    mhz = None
+    for p in ("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq",):
+        try:
+            with open(p) as f:
+                mhz = int(f.read().strip()) / 1000.0
+        except (OSError, ValueError):
+            pass
+    info["max_mhz"] = mhz
+    return info
+
+
+def cpu_baseline(filters, topics, sample_1t, sample_mt, host, label="C2 trie (1M filters"):
     """emqx_router:match_routes/1 restated in C (oracle/, prefix-string ETS layout),
-    timed on this host's cores over a bounded sample of the same workload."""
+    timed on this host's cores over a bounded sample of the same workload:
+    1 thread, and host['threads'] threads (the lease's CPU share) each taking a
+    contiguous slice."""
     from oracle import pyoracle
+    threads = host["threads"]
     orc = pyoracle.Oracle()
     t0 = time.time()
     for f in filters.tolist():
@@ -85,12 +117,46 @@ def cpu_baseline(filters, topics, sample_1t, sample_mt, threads):
         "unit": "publishes/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"C2 trie (1M filters, ETS-layout C restatement, build {build_s:.1f}s); "
+        "sample": (f"{label}, ETS-layout C restatement, build {build_s:.1f}s); "
                    f"{sample_mt} publishes on {threads} threads in {dtm:.2f}s; "
                    f"{sample_1t} publishes on 1 thread in {dt1:.2f}s = {sample_1t / dt1:.0f}/s; "
-                   f"routes returned {st['routes']}; cpu {cpu_info()}"),
+                   f"routes returned {st['routes']}; cpu {host['model']} (max {host['max_mhz']} MHz), "
+                   f"nproc {host['nproc']}, affinity {host['affinity']}, cgroup quota {host['cgroup_quota']} CPUs"),
         "value_1thread": sample_1t / dt1,
+        "host": host,
     }
+
+
+def c1_leg(host, device=0):
+    """BASELINE config 1: 10k mixed '+'/'#' filters (10 %
+    exact), 100k publishes.  The CPU restatement of match_routes/1 on the
+    lease's cores and the device pipeline on the same workload."""
+    from emqx_amd import gen
+    from emqx_amd.engine import Engine
+    p = gen.C1
+    filters = gen.gen_filters(p)
+    topics = gen.gen_topics(p, filters, 1001, 100_000)
+    out = {"workload": "C1: 10k filters (10% exact), 100k publishes",
+           "cpu_baseline": cpu_baseline(filters, topics, len(topics), len(topics), host,
+                                        label="C1 trie (10k filters")}
+    eng = Engine(device=device)
+    for f in filters.tolist():
+        eng.route_add(f, 0)
+    eng.sync()
+    b = eng.prepare(topics)
+    for _ in range(3):
+        b.launch().wait()
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.launch().wait()
+    dt = (time.perf_counter() - t0) / reps
+    out["gpu_publishes_per_s"] = len(topics) / dt
+    out["gpu_ms_per_batch"] = 1e3 * dt
+    out["speedup_vs_cpu_allcore"] = out["gpu_publishes_per_s"] / out["cpu_baseline"]["value"]
+    b.free()
+    eng.close()
+    return out
 
 
 def run_c4(args, ws, rank, local, pg):
@@ -184,7 +250,7 @@ def run_c4(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
-def run_c5(args, ws, rank, local, pg):
+def run_c5(args, ws, rank, local, sync):
     """Config C5: 10k hot topics take 90% of the publishes, each matched by ~K
     filters derived from it (+ 100k background C2-style filters); one step =
     10,000 subscribe/unsubscribe deltas applied to the trie and uploaded to the
@@ -206,8 +272,8 @@ def run_c5(args, ws, rank, local, pg):
     row_of, n_rows = b.row_map()
     for _ in range(args.warmup):
         b.launch().wait()
-    if pg is not None:
-        pg.barrier()
+    if sync is not None:
+        sync.barrier()
     # the deltas are drawn before timing; applying them (trie ops + the device
     # delta upload inside launch) is inside each step
     deltas = [churn.step(args.c5_deltas) for _ in range(args.steps)]
@@ -220,12 +286,9 @@ def run_c5(args, ws, rank, local, pg):
         b.launch().wait()
         ms_match.append(b.stats()["ms_total"])
     elapsed = time.perf_counter() - t0
-    if pg is not None:
-        import torch
-        pg.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    if sync is not None:
+        sync.barrier()
+        elapsed = sync.allmax(elapsed)
     st = b.stats()
     offs, _ = b.result()
     rowlen = np.diff(offs.astype(np.int64))
@@ -255,11 +318,11 @@ def run_c5(args, ws, rank, local, pg):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    if sync is not None:
+        sync.close()
 
 
-def run_coalesce(args, ws, rank, local, pg):
+def run_coalesce(args, ws, rank, local, sync):
     """Per-publish emqx_trie:match/1 calls from many concurrent callers
     (tm_match_coalesced, what the NIF's match/2 does): C2 trie, 64 threads each
     matching its own slice of the publishes one topic per call.  Reports calls/s
@@ -304,7 +367,7 @@ def run_coalesce(args, ws, rank, local, pg):
         print(json.dumps(out), flush=True)
 
 
-def run_dispatch(args, ws, rank, local, pg):
+def run_dispatch(args, ws, rank, local, sync):
     """Publish -> match -> fan-out on the device: the C2
     trie and publishes, every filter with local subscribers (75% one, 24% 2-8,
     64 hot filters with 4096 each; ids from a pool of 1M subscribers).  One step
@@ -336,8 +399,8 @@ def run_dispatch(args, ws, rank, local, pg):
     for _ in range(max(args.warmup, 1)):
         b.launch().wait()
         b.dispatch_device()
-    if pg is not None:
-        pg.barrier()
+    if sync is not None:
+        sync.barrier()
     ms_match, ms_fill, ms_disp = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -348,12 +411,9 @@ def run_dispatch(args, ws, rank, local, pg):
         ms_fill.append(fill_ms)
         ms_match.append(b.stats()["ms_total"])
     elapsed = time.perf_counter() - t0
-    if pg is not None:
-        import torch
-        pg.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    if sync is not None:
+        sync.barrier()
+        elapsed = sync.allmax(elapsed)
     st = b.stats()
     n, m = len(topics), int(st["matches"])
     f_ms = float(np.mean(ms_fill))
@@ -389,8 +449,74 @@ def run_dispatch(args, ws, rank, local, pg):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    if sync is not None:
+        sync.close()
+
+
+def run_group(args):
+    """Config C3 in ONE process (tm_group_*): the C2 trie replicated on devices
+    0..N-1, one batch of N x the per-GPU publishes split into N contiguous
+    slices matched concurrently (no collective).  Weak scaling like the
+    torchrun form: every device gets --topics publishes."""
+    from emqx_amd import gen
+    from emqx_amd.engine import Group
+
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    ng = len(devs)
+    p = gen.C2
+    t0 = time.time()
+    filters = gen.gen_filters(p)
+    one = gen.gen_topics(p, filters, 1000, args.topics)
+    # device k's slice is the publishes rank k would generate (seed 1000 + k)
+    parts = [one] + [gen.gen_topics(p, filters, 1000 + k, args.topics) for k in range(1, ng)]
+    topics = gen.Strings.concat(parts)
+    del parts, one
+    log(f"[group] {len(filters)} filters, {len(topics)} topics in {time.time() - t0:.1f}s")
+    grp = Group(devs)
+    t0 = time.time()
+    grp.insert_many(filters)
+    grp.sync()
+    log(f"[group] {ng} replicas built+uploaded in {time.time() - t0:.1f}s")
+    b = grp.prepare(topics)
+    for _ in range(max(args.warmup, 1)):
+        b.launch().wait()
+    ms_match = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.launch().wait()
+        ms_match.append(b.stats()["ms_match"])
+    elapsed = time.perf_counter() - t0
+    st = b.stats()
+    n = len(topics)
+    alg_bytes = (ALG_BYTES_PER_VISIT * (st["visits"] + st["hash_hits"]) + 4 * st["words"]
+                 + 4 * st["matches"] + 4 * n) / ng      # per device
+    k_ms = float(np.mean(ms_match))                      # slowest slice per step
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    out = {
+        "metric": "publishes matched/sec (node) at 1M wildcard subs; p99 batch match latency",
+        "value": n * args.steps / elapsed,
+        "unit": "publishes/s",
+        "n_gpus": ng,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded generator, SURVEY.md §8d C2/C3)",
+        "config": {"workload": f"C3: 1M wildcard filters replicated on {ng} devices, {args.topics} publishes per "
+                               f"device, one process (tm_group)", "devices": devs,
+                   "filters": len(filters), "publishes_per_gpu": args.topics, "mode": "replicated, in-process",
+                   "parallelism": f"replicated trie x{ng}, batch split in {ng} slices"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tm_match_tiles",
+                     "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes},
+        "matches_per_step": st["matches"],
+    }
+    b.free()
+    grp.close()
+    print(json.dumps(out), flush=True)
 
 
 def e2e_rate(eng, sub, reps: int = 3) -> dict:
@@ -453,13 +579,21 @@ def main():
     ap.add_argument("--c5-k", type=int, default=100, help="C5 filters per hot topic (10 / 100 / 1000)")
     ap.add_argument("--c5-deltas", type=int, default=10_000, help="C5 subscribe/unsubscribe deltas per step")
     ap.add_argument("--c4-filters", type=int, default=0, help="C4 filter count (default 100M)")
+    ap.add_argument("--devices", type=str, default="",
+                    help="comma list of HIP devices: replicas of the in-process group (--gpus N without torchrun), "
+                         "or the device of each local rank; default 0..N-1 (e.g. 0,0 rehearses 2 on one GPU)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
-    if ws != args.gpus:
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else None
+    if devs and ws > 1:
+        local = devs[local]
+    if ws > 1 and ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {ws}; using WORLD_SIZE")
     pg = None
-    if ws > 1:
+    if ws > 1 and args.workload == "c4":
+        # the filter-sharded exchange is RCCL: torch (and its HIP runtime) is
+        # initialised before the engine library loads, so both share one runtime
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -467,12 +601,20 @@ def main():
         pg = dist
     if args.workload == "c4":
         return run_c4(args, ws, rank, local, pg)
+    sync = None
+    if ws > 1:
+        # replicated mode has no data-path collective: a host file barrier and
+        # max-reduce line the ranks up (emqx_amd/hostsync.py), no torch
+        from emqx_amd.hostsync import FileGroup
+        sync = FileGroup(rank, ws)
     if args.workload == "c5":
-        return run_c5(args, ws, rank, local, pg)
+        return run_c5(args, ws, rank, local, sync)
     if args.workload == "dispatch":
-        return run_dispatch(args, ws, rank, local, pg)
+        return run_dispatch(args, ws, rank, local, sync)
     if args.workload == "coalesce":
-        return run_coalesce(args, ws, rank, local, pg)
+        return run_coalesce(args, ws, rank, local, sync)
+    if ws == 1 and args.gpus > 1:
+        return run_group(args)
 
     from emqx_amd import gen
     from emqx_amd.engine import Engine
@@ -485,9 +627,7 @@ def main():
 
     eng = Engine(device=local)
     t0 = time.time()
-    fl = filters.tolist()
-    for f in fl:
-        eng.insert(f)
+    eng.insert_many(filters)
     eng.sync()
     est = eng.stats()
     log(f"[rank {rank}] trie built+uploaded in {time.time() - t0:.1f}s: {est}")
@@ -505,15 +645,9 @@ def main():
     if st["topics"] != len(topics):
         raise RuntimeError(f"batch stats inconsistent: {st}")
 
-    def barrier():
-        # wait() has drained the engine's stream (hipEventSynchronize), the only
-        # stream this process uses.  torch.cuda is not initialised here at N=1:
-        # initialising it after the engine's HIP runtime reports "No HIP GPUs
-        # are available" (gpurun_out v16, round 1), so no torch synchronize.
-        if pg is not None:
-            pg.barrier()
-
-    barrier()
+    # wait() drains the engine's stream, the only stream this process uses
+    if sync is not None:
+        sync.barrier()
     ms_match, ms_total = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -522,13 +656,10 @@ def main():
         ms_match.append(s["ms_match"])
         ms_total.append(s["ms_total"])
     t1 = time.perf_counter()
-    barrier()
     elapsed = t1 - t0
-    if pg is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        pg.all_reduce(tt, op=pg.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    if sync is not None:
+        sync.barrier()
+        elapsed = sync.allmax(elapsed)
 
     n = len(topics)
     value = ws * n * args.steps / elapsed
@@ -615,14 +746,15 @@ def main():
     b.free()
 
     if rank == 0 and ws == 1 and not args.no_cpu:
-        threads = min(os.cpu_count() or 1, 16)
-        out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), threads)
+        host = host_cpu_share()
+        out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), host)
         out["speedup_vs_cpu_allcore"] = value / out["cpu_baseline"]["value"]
+        out["c1"] = c1_leg(host, device=local)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    if sync is not None:
+        sync.close()
 
 
 if __name__ == "__main__":

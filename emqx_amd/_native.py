@@ -139,6 +139,22 @@ SIGNATURES = {
     "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
     "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),
     "tm_rules_match": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P]),
+    "tm_group_create": (C.c_int, [P, C.c_uint32, C.POINTER(Config), C.POINTER(P)]),
+    "tm_group_destroy": (None, [P]),
+    "tm_group_size": (C.c_uint32, [P]),
+    "tm_group_engine": (P, [P, C.c_uint32]),
+    "tm_group_trie_insert": (C.c_int, [P, U8P, SZ]),
+    "tm_group_trie_delete": (C.c_int, [P, U8P, SZ]),
+    "tm_group_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_group_route_apply": (C.c_int, [P, P, P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_group_sync": (C.c_int, [P]),
+    "tm_group_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
+    "tm_group_launch": (C.c_int, [P, P]),
+    "tm_group_wait": (C.c_int, [P, P]),
+    "tm_group_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_group_batch_stats": (C.c_int, [P, P, C.POINTER(BatchStats)]),
+    "tm_group_batch_free": (None, [P, P]),
+    "tm_group_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),
     "tm_device_count": (C.c_int, []),

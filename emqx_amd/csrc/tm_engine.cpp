@@ -403,6 +403,7 @@ struct tm_engine {
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
     uint32_t qcap = 384;           // LDS probe stack per wave, 384 or 512 (TM_QCAP); C2 tiles peak at ~340
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
+    uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
     uint32_t* d_dbg = nullptr;
     uint32_t* h_dbg = nullptr;
     size_t c_dbg = 0, ch_dbg = 0;
@@ -1575,7 +1576,16 @@ struct tm_engine {
         b->n = nu;
     }
 
+    // publish names are at most ?MAX_TOPIC_LEN bytes (src/emqx_topic.erl:45,
+    // validate/2 :99-100); offsets must not decrease
+    static int check_topics(const uint64_t* offsets, uint32_t n) {
+        for (uint32_t t = 0; t < n; ++t)
+            if (offsets[t + 1] < offsets[t] || offsets[t + 1] - offsets[t] > TM_MAX_TOPIC_LEN) return TM_EINVAL;
+        return TM_OK;
+    }
+
     int prepare(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags = 0) {
+        if (int rc = check_topics(offsets, n)) return rc;
         b->dedup = (flags & TM_BATCH_DEDUP) != 0;
         b->n_pub = n;
         b->row_of.clear();
@@ -1682,7 +1692,7 @@ struct tm_engine {
             snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
             return TM_EIO;
         }
-        a.sfids = b->d_sfids; a.sfids_cap = b->c_sfids;
+        a.sfids = b->d_sfids; a.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
         a.s_qparent = d_sqpar; a.s_qpw = d_sqpw; a.s_qmeta = d_sqmeta; a.s_qkey = d_sqkey;
@@ -1696,7 +1706,7 @@ struct tm_engine {
         HIP_OK(launch_match(a, stream, b->ev0, b->ev1, checked));
         ScanArgs s{};
         s.count = b->d_count; s.src = b->d_src;
-        s.sfids = b->d_sfids; s.sfids_cap = b->c_sfids;
+        s.sfids = b->d_sfids; s.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? d_dbg : nullptr;
@@ -1723,11 +1733,18 @@ struct tm_engine {
                 return TM_EIO;
             }
             const uint32_t err = b->h_ctrl[CTRL_ERR];
+            const uint64_t need = (uint64_t)b->h_ctrl[CTRL_STAGING64] | ((uint64_t)b->h_ctrl[CTRL_STAGING64 + 1] << 32);
+            const uint64_t nmatch = b->h_stats[ST_MATCHES];
+            // a CSR with u32 offsets cannot hold more (tm_result): refuse, never wrap
+            if ((err & ERR_CSR_RANGE) || need > result_limit || nmatch > result_limit) {
+                snprintf(last_error(), 512, "batch result too large: %llu staged / %llu matched > limit %llu",
+                         (unsigned long long)need, (unsigned long long)nmatch, (unsigned long long)result_limit);
+                return TM_EOVERFLOW;
+            }
             if (!err) break;
             if (attempt >= 6) return TM_EOVERFLOW;
             if (err & ERR_STAGING) {
-                const uint64_t need = b->h_ctrl[CTRL_STAGING_TOP];
-                int rc = dev_reserve(b->d_sfids, b->c_sfids, need + need / 4 + 1024);
+                int rc = dev_reserve(b->d_sfids, b->c_sfids, std::min<uint64_t>(need + need / 4 + 1024, MAX_RESULT));
                 if (rc) return rc;
             }
             if (err & ERR_SLOW_SCRATCH) {
@@ -1801,6 +1818,8 @@ struct tm_engine {
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
         if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
+        if (const char* rl = getenv("TM_RESULT_LIMIT"))
+            result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
         if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');
@@ -1996,6 +2015,17 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
     std::lock_guard<std::recursive_mutex> g(e->mu);
     int rc = e->set_device();
     if (rc) return rc;
+    // prepare's H2D of the caller's buffers is not waited for (the pipeline is,
+    // below); on any early exit the stream is drained before returning, so
+    // the borrowed buffers are never read after the caller frees them
+    struct Drain {
+        tm_engine* e;
+        bool armed = true;
+        ~Drain() {
+            e->upload_nosync = false;
+            if (armed) (void)hipStreamSynchronize(e->stream);
+        }
+    } drain{e};
     try {
         e->upload_nosync = true;
         rc = e->prepare(&e->scratch, topics, offsets, n);
@@ -2003,9 +2033,10 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
         if (rc) return rc;
         if ((rc = e->launch(&e->scratch))) return rc;
         if ((rc = e->wait(&e->scratch))) return rc;
-        return e->result(&e->scratch, out);
+        rc = e->result(&e->scratch, out);
+        drain.armed = rc != TM_OK;   // result() synchronised the stream
+        return rc;
     } catch (...) {
-        e->upload_nosync = false;
         return TM_ENOMEM;
     }
 }

@@ -85,16 +85,24 @@ __host__ __device__ inline uint32_t home_bucket(uint32_t parent, uint32_t word, 
 
 // Control words of one batch launch (device memory, zeroed per launch).
 enum Ctrl : uint32_t {
-    CTRL_STAGING_TOP = 0,   // slow-region entries reserved (may exceed capacity -> rerun)
     CTRL_NOVF = 1,          // topics appended to the ovf list
     CTRL_ERR = 2,           // error bits
     CTRL_SLOW_DONE = 3,
     CTRL_TILE_NEXT = 4,     // dynamic tile tickets of tm_match_tiles
+    CTRL_STAGING64 = 6,     // words 6-7: u64 staging entries reserved (may exceed capacity -> rerun)
     CTRL_WORDS = 16
 };
 constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
 constexpr uint32_t ERR_SLOW_SCRATCH = 2; // slow-path scratch exceeded
 constexpr uint32_t ERR_OVF_LIST = 4;
+constexpr uint32_t ERR_CSR_RANGE = 8;    // the batch's match count does not fit u32 CSR offsets
+// Staging and CSR offsets are u32 (tm_result.row_offsets): a batch with more
+// matches than this fails with TM_EOVERFLOW instead of wrapping.
+constexpr uint64_t MAX_RESULT = 0xFFFFFFF0ull;
+
+__device__ __forceinline__ unsigned long long* ctrl_staging(uint32_t* ctrl) {
+    return reinterpret_cast<unsigned long long*>(ctrl + CTRL_STAGING64);
+}
 
 enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_N = 8 };
 

@@ -573,12 +573,16 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         if (lane >= (uint32_t)o) incl += u;
     }
     const uint32_t tot = __shfl(incl, 63, 64);
-    uint32_t base = 0;
-    if (lane == 0 && tot) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], tot);
-    base = __shfl(base, 0, 64);
+    // u64 ticket: a batch may reserve more than 2^32 entries; the host then
+    // fails it with TM_EOVERFLOW (sfids_cap < 2^32, so dst below never wraps)
+    unsigned long long base64 = 0;
+    if (lane == 0 && tot) base64 = atomicAdd(ctrl_staging(a.ctrl), (unsigned long long)tot);
+    base64 = __shfl(base64, 0, 64);
+    const bool fits = base64 + tot <= a.sfids_cap;
+    const uint32_t base = (uint32_t)base64;
     const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
-    if ((uint64_t)base + tot <= a.sfids_cap) {
+    if (fits) {
         sort_rows<CK, LT>(a, L, keep, c, dst);
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
@@ -800,10 +804,10 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             __threadfence_block();
             __syncthreads();
         }
-        uint32_t base = 0;
-        if (lane == 0 && on) base = atomicAdd(&a.ctrl[CTRL_STAGING_TOP], on);
+        unsigned long long base = 0;
+        if (lane == 0 && on) base = atomicAdd(ctrl_staging(a.ctrl), (unsigned long long)on);
         base = __shfl(base, 0, 64);
-        if ((uint64_t)base + on <= a.sfids_cap) {
+        if (base + on <= a.sfids_cap) {
             for (uint32_t i = lane; i < on; i += 64) a.sfids[CK_(base + i, a.sfids_cap, 30)] = ofid[i];
         } else if (lane == 0) {
             atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);
@@ -882,18 +886,19 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_local(ScanArgs a) {
 // Pass 2: exclusive scan of the block sums (single block), total -> row_off[n].
 __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t nblocks, uint32_t* d_total) {
     __shared__ uint32_t sh[33];
-    uint32_t carry = 0;
+    uint64_t carry = 0;   // u64: a total past u32 is flagged, never wrapped silently
     for (uint32_t b0 = 0; b0 < nblocks; b0 += SCAN_BLOCK) {
         const uint32_t i = b0 + threadIdx.x;
         const uint32_t v = i < nblocks ? a.block_sums[i] : 0u;
         uint32_t tot;
         const uint32_t ex = block_excl_scan(v, sh, tot);
-        if (i < nblocks) a.block_sums[i] = carry + ex;
+        if (i < nblocks) a.block_sums[i] = (uint32_t)(carry + ex);
         carry += tot;
     }
     if (threadIdx.x == 0) {
-        a.row_off[a.n] = carry;
-        if (d_total) *d_total = carry;
+        a.row_off[a.n] = (uint32_t)carry;
+        if (d_total) *d_total = (uint32_t)carry;
+        if (carry > MAX_RESULT && a.ctrl) atomicOr(&a.ctrl[CTRL_ERR], ERR_CSR_RANGE);
     }
 }
 

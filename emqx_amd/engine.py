@@ -154,6 +154,128 @@ def _routes_arrays(r: N.Routes):
     return offs, fids, dests
 
 
+class GroupBatch:
+    """A publish batch split over a Group's replicas (tm_group_prepare ...)."""
+
+    def __init__(self, grp: "Group", topics):
+        self.grp = grp
+        s = _pack(topics)
+        self.n = len(s)
+        self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        h = C.c_void_p()
+        N.check(grp.L.tm_group_prepare(grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n, C.byref(h)),
+                "tm_group_prepare")
+        self.h = h
+
+    def launch(self):
+        N.check(self.grp.L.tm_group_launch(self.grp.h, self.h), "tm_group_launch")
+        return self
+
+    def wait(self):
+        N.check(self.grp.L.tm_group_wait(self.grp.h, self.h), "tm_group_wait")
+        return self
+
+    def result(self):
+        r = N.Result()
+        N.check(self.grp.L.tm_group_result(self.grp.h, self.h, C.byref(r)), "tm_group_result")
+        return _result_arrays(r)
+
+    def stats(self) -> dict:
+        st = N.BatchStats()
+        N.check(self.grp.L.tm_group_batch_stats(self.grp.h, self.h, C.byref(st)), "tm_group_batch_stats")
+        return st.asdict()
+
+    def free(self):
+        if self.h:
+            self.grp.L.tm_group_batch_free(self.grp.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Group:
+    """Replicated multi-device matching in one process (tm_group_*, config C3):
+    one trie replica per listed device, mutations applied to all, batches split
+    into one contiguous slice per replica."""
+
+    def __init__(self, devices, host_threads: int = 0):
+        self.L = N.lib()
+        devs = (C.c_int32 * len(devices))(*devices)
+        cfg = N.Config(0, 0, host_threads, 0)
+        h = C.c_void_p()
+        N.check(self.L.tm_group_create(devs, len(devices), C.byref(cfg), C.byref(h)), "tm_group_create")
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tm_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self.L.tm_group_size(self.h))
+
+    def insert(self, f: bytes):
+        N.check(self.L.tm_group_trie_insert(self.h, f, len(f)), "tm_group_trie_insert")
+
+    def delete(self, f: bytes):
+        N.check(self.L.tm_group_trie_delete(self.h, f, len(f)), "tm_group_trie_delete")
+
+    def insert_many(self, filters) -> int:
+        s = _pack(filters)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        done = C.c_uint64()
+        N.check(self.L.tm_group_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
+                "tm_group_insert_many")
+        return int(done.value)
+
+    def route_apply(self, events) -> int:
+        s = _pack([t for _, t, _ in events])
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        dests = np.ascontiguousarray(np.array([d for _, _, d in events] or [0], np.uint32))
+        ops = np.ascontiguousarray(np.array([o for o, _, _ in events] or [0], np.uint8))
+        done = C.c_uint64()
+        N.check(self.L.tm_group_route_apply(self.h, buf.ctypes.data, offs.ctypes.data, dests.ctypes.data,
+                                            ops.ctypes.data, len(events), C.byref(done)), "tm_group_route_apply")
+        return int(done.value)
+
+    def sync(self):
+        N.check(self.L.tm_group_sync(self.h), "tm_group_sync")
+
+    def prepare(self, topics) -> GroupBatch:
+        return GroupBatch(self, topics)
+
+    def match_batch(self, topics):
+        s = _pack(topics)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        r = N.Result()
+        N.check(self.L.tm_group_match_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
+                "tm_group_match_batch")
+        return _result_arrays(r)
+
+    def filter_bytes(self, fid: int, replica: int = 0) -> bytes:
+        e = self.L.tm_group_engine(self.h, replica)
+        n = C.c_size_t()
+        p = self.L.tm_filter_bytes(e, fid, C.byref(n))
+        if not p:
+            raise KeyError(fid)
+        return C.string_at(p, n.value)
+
+
 class Engine:
     def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0, frozen_dict: bool = False,
                  host_tokenize: bool = False):

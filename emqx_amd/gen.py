@@ -111,6 +111,16 @@ class Strings:
         a, b = int(self.offs[lo]), int(self.offs[hi])
         return Strings(self.buf[a:b].copy(), (self.offs[lo:hi + 1] - self.offs[lo]).astype(np.uint64))
 
+    @classmethod
+    def concat(cls, parts) -> "Strings":
+        """parts[0] ++ parts[1] ++ ... as one packed list."""
+        bufs, offs, base = [], [np.zeros(1, np.uint64)], 0
+        for s in parts:
+            bufs.append(s.buf[int(s.offs[0]):int(s.offs[-1])])
+            offs.append((s.offs[1:] - s.offs[0] + base).astype(np.uint64))
+            base += int(s.offs[-1] - s.offs[0])
+        return cls(np.concatenate(bufs) if bufs else np.zeros(0, np.uint8), np.concatenate(offs))
+
 
 def _take(cs: _CStrs) -> Strings:
     n = cs.n

@@ -376,6 +376,43 @@ TM_API int  tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* n
                            const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule,
                            uint32_t* bits);
 
+/* ---- replicated multi-device group (BASELINE config C3) --------------- */
+/* One process drives one trie replica per listed device (a device may be
+ * listed twice: two replicas on one GPU).  Every mutation is applied to every
+ * replica in the same order, so node / filter ids are identical everywhere
+ * (the reference replicates emqx_trie to every node the same way,
+ * src/emqx_trie.erl:53-74); a publish batch is split into contiguous slices,
+ * one per replica, matched concurrently with no collective, and the slices'
+ * CSRs concatenate into the batch's CSR. */
+typedef struct tm_group tm_group;
+typedef struct tm_group_batch tm_group_batch;
+TM_API int  tm_group_create(const int32_t* devices, uint32_t n_devices, const tm_config* cfg, tm_group** out);
+TM_API void tm_group_destroy(tm_group* g);
+TM_API uint32_t tm_group_size(tm_group* g);
+/* Replica i (read-only use: stats, filter bytes; mutate only through tm_group_*). */
+TM_API tm_engine* tm_group_engine(tm_group* g, uint32_t i);
+TM_API int  tm_group_trie_insert(tm_group* g, const uint8_t* topic, size_t len);
+TM_API int  tm_group_trie_delete(tm_group* g, const uint8_t* topic, size_t len);
+TM_API int  tm_group_insert_many(tm_group* g, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
+                                 uint64_t* n_inserted);
+TM_API int  tm_group_route_apply(tm_group* g, const uint8_t* topics, const uint64_t* offsets, const uint32_t* dests,
+                                 const uint8_t* ops, uint32_t n, uint64_t* n_changed);
+TM_API int  tm_group_sync(tm_group* g);
+/* Split form: prepare slices (H2D on every device), launch all (async), wait
+ * all, merged CSR (group-owned pinned memory, valid until the batch is
+ * re-prepared or freed).  A non-NULL *out is re-prepared in place. */
+TM_API int  tm_group_prepare(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                             tm_group_batch** out);
+TM_API int  tm_group_launch(tm_group* g, tm_group_batch* b);
+TM_API int  tm_group_wait(tm_group* g, tm_group_batch* b);
+TM_API int  tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out);
+/* Counters summed over the slices; ms_match / ms_total = the slowest slice. */
+TM_API int  tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out);
+TM_API void tm_group_batch_free(tm_group* g, tm_group_batch* b);
+/* prepare + launch + wait + result in one call. */
+TM_API int  tm_group_match_batch(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                 tm_result* out);
+
 /* ---- diagnostics ------------------------------------------------------ */
 /* Text of the last TM_EIO on this thread (HIP error string + call site). */
 TM_API const char* tm_last_error(void);

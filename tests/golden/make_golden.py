@@ -204,6 +204,31 @@ KAT_ROUTER = {
     ],
 }
 
+KAT_BATCH = {
+    "source": "test/emqx_batch_SUITE.erl",
+    "note": "steps run in order against init(opts); 'commits' = the lists commit_fun received, in order",
+    "cases": [
+        {"name": "t_batch_full_commit", "line": "26-37", "opts": {"batch_size": 3, "linger_ms": 2000},
+         "steps": [{"push": "a"}, {"push": "b"}, {"push": "c"},
+                   {"size": 3, "items": ["a", "b", "c"]},
+                   {"push": "a"},          # 4th push onto 3 queued items: commit at batch_size + 1
+                   {"size": 0, "items": []}],
+         "commits": [["a", "b", "c", "a"]]},
+        {"name": "t_batch_linger_commit", "line": "39-56", "opts": {"batch_size": 3, "linger_ms": 500},
+         "steps": [{"push": "a"}, {"push": "b"}, {"push": "c"},
+                   {"size": 3, "items": ["a", "b", "c"]},
+                   {"await_linger_within_ms": 1000},   # batch_linger_expired arrives
+                   {"commit": True},
+                   {"size": 0, "items": []}],
+         "commits": [["a", "b", "c"]]},
+        # src/emqx_batch.erl:64-66 (no suite case): batch_size = 0 never commits on push
+        {"name": "src_unlimited", "line": "src/emqx_batch.erl:64-66", "opts": {"batch_size": 0, "linger_ms": 60000},
+         "steps": [{"push": "a"}, {"push": "b"}, {"push": "c"}, {"push": "d"},
+                   {"size": 4, "items": ["a", "b", "c", "d"]}],
+         "commits": []},
+    ],
+}
+
 # Hand-written adversarial filters/topics: byte classes around '#' (0x23) and
 # '+' (0x2B), empty levels, '$' rules, literal '#'/'+' topic words, deep topics,
 # irregular '+x' words, shared-prefix filters.
@@ -253,6 +278,7 @@ def main():
     dump("kat_trie.json", KAT_TRIE)
     dump("kat_router.json", KAT_ROUTER)
     dump("kat_broker.json", KAT_BROKER)
+    dump("kat_batch.json", KAT_BATCH)
     synth("synth_c1_small.json", replace(gen.C1, n_filters=800), 600, 11)
     synth("synth_c2_small.json", replace(gen.C2, n_filters=1500, vocab=48), 600, 22)
     synth("synth_adversarial.json", replace(gen.C1, n_filters=150, vocab=6, p_empty=0.2, p_dollar=0.1), 300, 33,

@@ -180,3 +180,14 @@ def test_c_struct_sizes_stable():
     assert C.sizeof(N.Config) == 16
     assert C.sizeof(N.TrieNode) == 12
     assert C.sizeof(N.Result) == 32       # u32 + pad + u64 + 2 pointers
+
+
+def test_group_without_device_is_refused():
+    from emqx_amd.engine import Group
+    with pytest.raises(N.TmError) as ei:
+        Group([-1])
+    assert ei.value.rc == N.TM_EINVAL
+    if N.lib().tm_device_count() == 0:
+        with pytest.raises(N.TmError) as ei:
+            Group([0, 0])
+        assert ei.value.rc == N.TM_ENODEV

@@ -1,0 +1,73 @@
+"""Error contract of the batch path -- needs an MI355X.
+
+* a batch whose match count does not fit the u32 CSR fails with TM_EOVERFLOW
+  (never a wrapped, silently wrong CSR); the limit is lowered through the
+  test-only TM_RESULT_LIMIT knob so the case runs at a small size;
+* a topic longer than ?MAX_TOPIC_LEN (src/emqx_topic.erl:45) is TM_EINVAL."""
+
+import os
+
+import pytest
+from test_gpu_parity import assert_same, engine_rows, oracle_rows
+
+from emqx_amd import _native as N
+from emqx_amd.engine import Engine
+
+pytestmark = pytest.mark.gpu
+
+
+def limited_engine(limit):
+    os.environ["TM_RESULT_LIMIT"] = str(limit)
+    try:
+        return Engine(device=0)
+    finally:
+        del os.environ["TM_RESULT_LIMIT"]
+
+
+def test_result_past_the_limit_is_eoverflow_not_wrapped():
+    eng = limited_engine(1000)
+    F = [b"#", b"+/#", b"a/#", b"a/+"]
+    for f in F:
+        eng.insert(f)
+    big = [b"a/%d" % i for i in range(300)]           # 4 matches each: 1200 > 1000
+    with pytest.raises(N.TmError) as ei:
+        eng.match_batch(big)
+    assert ei.value.rc == N.TM_EOVERFLOW
+    # the engine stays usable, and a batch under the limit is exact
+    small = big[:250]                                   # 1000 matches == limit
+    exp, _ = oracle_rows(F, small)
+    assert_same(small, engine_rows(eng, small), exp)
+    # the split API fails the same way at wait()
+    b = eng.prepare(big)
+    with pytest.raises(N.TmError) as ei:
+        b.launch().wait()
+    assert ei.value.rc == N.TM_EOVERFLOW
+    b.free()
+
+
+def test_slow_path_rows_count_against_the_limit():
+    eng = limited_engine(50)
+    deep = b"/".join([b"a"] * 20)                       # > 10 levels: generic kernel
+    for k in range(1, 21):
+        eng.insert(b"/".join([b"a"] * k) + b"/#")
+    with pytest.raises(N.TmError) as ei:
+        eng.match_batch([deep] * 3)                      # 3 x 20 = 60 > 50
+    assert ei.value.rc == N.TM_EOVERFLOW
+    offs, ids = eng.match_batch([deep, deep])            # 40
+    assert int(offs[-1]) == 40
+
+
+def test_topic_longer_than_max_topic_len_is_einval():
+    eng = Engine(device=0)
+    eng.insert(b"+/#")
+    ok = b"a/" + b"x" * (N.TM_MAX_TOPIC_LEN - 2)
+    assert len(ok) == N.TM_MAX_TOPIC_LEN
+    assert eng.match(ok) == [b"+/#"]
+    for topics in ([ok + b"y"], [b"a/b", ok + b"y", b"c/d"]):
+        with pytest.raises(N.TmError) as ei:
+            eng.match_batch(topics)
+        assert ei.value.rc == N.TM_EINVAL
+        with pytest.raises(N.TmError) as ei:
+            eng.prepare(topics)
+        assert ei.value.rc == N.TM_EINVAL
+    assert eng.match(b"a/b") == [b"+/#"]               # still usable
