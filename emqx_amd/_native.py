@@ -87,6 +87,18 @@ class EngineStats(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
+class AsyncStats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("requests", C.c_uint64), ("recoveries", C.c_uint64),
+                ("max_batch", C.c_uint64), ("depth", C.c_uint32), ("queued", C.c_uint32),
+                ("us_launch", C.c_double), ("us_wait", C.c_double), ("us_deliver", C.c_double)]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+# void (*tm_match_cb)(void* ctx, int rc, const uint32_t* ids, uint32_t n)
+MATCH_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(C.c_uint32), C.c_uint32)
+
 # exported symbol -> (restype, argtypes); must cover every declaration in include/emqx_tm.h
 P = C.c_void_p
 SZ = C.c_size_t
@@ -105,6 +117,8 @@ SIGNATURES = {
     "tm_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_match_coalesced": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_coalesce_config": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "tm_match_async": (C.c_int, [P, U8P, SZ, MATCH_CB, P]),
+    "tm_async_stats_get": (C.c_int, [P, C.POINTER(AsyncStats)]),
     "tm_batch_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
     "tm_batch_prepare_ex": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
     "tm_batch_row_map": (C.c_int, [P, P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint32)]),
@@ -135,6 +149,7 @@ SIGNATURES = {
     "tm_batch_export": (C.c_int, [P, P, P, P, C.c_uint32, C.c_uint32]),
     "tm_filter_bytes": (C.POINTER(C.c_uint8), [P, C.c_uint32, C.POINTER(SZ)]),
     "tm_filter_id": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32)]),
+    "tm_filter_copy": (C.c_int, [P, C.c_uint32, P, SZ, C.POINTER(SZ)]),
     "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),
     "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
     "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),

@@ -38,8 +38,8 @@ def build_tm(force=False):
     if force or _stale(out, deps):
         tmp = out + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-fvisibility=hidden", "-Wall", "-o", tmp] + [os.path.join(CSRC, f) for f in TM_SOURCES]
-             + ["-lpthread"])
+              "-fvisibility=hidden", "-Wall", "-Wl,-soname,libemqx_tm.so", "-o", tmp]
+             + [os.path.join(CSRC, f) for f in TM_SOURCES] + ["-lpthread"])
         os.replace(tmp, out)
     return out
 
@@ -52,8 +52,19 @@ def build_gen(force=False):
     return out
 
 
+def build_load(force=False):
+    """libemqx_load.so: the per-publish load generator (bench / tests only)."""
+    out = os.path.join(HERE, "libemqx_load.so")
+    src = os.path.join(CSRC, "tm_load.cpp")
+    deps = [src, os.path.join(HERE, "libemqx_tm.so"), os.path.join(ROOT, "include", "emqx_tm.h")]
+    if force or _stale(out, deps):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall", "-o", out, src,
+              "-L" + HERE, "-lemqx_tm", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+    return out
+
+
 def build_all(force=False):
-    return [build_tm(force), build_gen(force)]
+    return [build_tm(force), build_gen(force), build_load(force)]
 
 
 if __name__ == "__main__":

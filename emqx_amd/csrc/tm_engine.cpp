@@ -11,6 +11,10 @@
 // :145-158, delete/1 :107-116, delete_path/1 :190-204, lookup/1, empty/0); the
 // node record's edge_count is kept so that emqx_trie:lookup/1 answers match
 // the reference's tests (test/emqx_trie_SUITE.erl:49-142).
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -18,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -87,7 +92,9 @@ class WordDict {
         const uint64_t h = hash_bytes(p, n);
         size_t i = h & mask_;
         while (tab_[i].h) i = (i + 1) & mask_;
-        tab_[i] = DictEnt{h, arena_.size(), (uint32_t)n, id};
+        tab_[i] = DictEnt{h, le_bytes(p, (uint32_t)std::min<size_t>(n, 8)),
+                          n > 8 ? le_bytes(p + 8, (uint32_t)std::min<size_t>(n - 8, 8)) : 0, (uint32_t)n, id,
+                          arena_.size(), 0};
         dirty_.push_back((uint32_t)i);
         arena_.insert(arena_.end(), p, p + n);
         ++count_;
@@ -104,7 +111,7 @@ class WordDict {
     void rehash(size_t cap) {
         std::vector<DictEnt> old;
         old.swap(tab_);
-        tab_.assign(cap, DictEnt{0, 0, 0, 0});
+        tab_.assign(cap, DictEnt{0, 0, 0, 0, 0, 0, 0});
         mask_ = cap - 1;
         for (const DictEnt& e : old)
             if (e.h) {
@@ -185,6 +192,19 @@ int host_reserve(T*& p, size_t& cap, size_t n) {
     return TM_OK;
 }
 
+// pinned host memory the device writes directly (tm_export_host): coherent,
+// so a kernel's stores are visible to the host once its completion is
+int host_reserve_coherent(uint8_t*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap && p) return TM_OK;
+    const size_t nc = std::max<size_t>(bytes + bytes / 4, 4096);
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_OK(hipHostMalloc((void**)&p, nc, hipHostMallocCoherent | hipHostMallocMapped));
+    cap = nc;
+    return TM_OK;
+}
+
 unsigned default_threads() {
     unsigned h = std::thread::hardware_concurrency();
     return std::max(1u, std::min(h ? h : 1u, 16u));
@@ -213,22 +233,36 @@ struct tm_batch {
     uint8_t* d_tflags = nullptr;
     size_t c_words = 0, c_toff = 0, c_slow = 0, c_tflags = 0;
     // device outputs
-    uint32_t *d_count = nullptr, *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
-    unsigned long long *d_src = nullptr, *d_rows = nullptr;
-    uint32_t *d_bsums = nullptr, *d_ctrl = nullptr, *d_ovf = nullptr, *d_total = nullptr;
-    unsigned long long* d_stats = nullptr;
-    size_t c_count = 0, c_src = 0, c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
+    uint32_t *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
+    unsigned long long* d_rows = nullptr;
+    uint32_t *d_bsums = nullptr, *d_ovf = nullptr, *d_total = nullptr;
+    size_t c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
     uint32_t* h_total = nullptr;
     size_t ch_total = 0;
-    size_t c_ctrl = 0, c_stats = 0, c_total = 0;
+    size_t c_total = 0;
+    // Per-topic outputs in ONE block, [ctrl CTRL_WORDS u32 | stats ST_N u64 |
+    // src cap u64 | count cap u32], mirrored in pinned memory: the async path
+    // reads a whole batch's control words and row descriptors back in one copy.
+    uint8_t *d_hdr = nullptr, *h_hdr = nullptr;
+    size_t hdr_cap = 0;   // topics the block holds
+    uint32_t *d_count = nullptr, *d_ctrl = nullptr, *h_ctrl = nullptr, *h_count = nullptr;
+    unsigned long long *d_src = nullptr, *d_stats = nullptr, *h_src = nullptr, *h_stats = nullptr;
+    static constexpr size_t HDR_FIXED = CTRL_WORDS * 4 + ST_N * 8;
+    static size_t hdr_bytes(size_t n) { return HDR_FIXED + n * 12; }
     // pinned host results
     uint32_t* h_rowoff = nullptr;
     uint32_t* h_ids = nullptr;
-    uint32_t* h_ctrl = nullptr;
-    unsigned long long* h_stats = nullptr;
-    size_t ch_rowoff = 0, ch_ids = 0, ch_ctrl = 0, ch_stats = 0;
+    size_t ch_rowoff = 0, ch_ids = 0;
+    // the stream the batch runs on: async slots own one, other batches use the engine's
+    hipStream_t own = nullptr;
+    // generic-path scratch, per batch (batches on different streams run concurrently)
+    uint32_t s_waves = 0, s_qcap = 1u << 13, s_ocap = 1u << 14;
+    uint32_t *d_sqpar = nullptr, *d_sqpw = nullptr, *d_sqmeta = nullptr, *d_sofid = nullptr;
+    unsigned long long *d_sqkey = nullptr, *d_sokey = nullptr;
+    size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool launched = false, done = false;
+    bool csr = true;   // the last launch built the CSR (false: async, rows left in staging)
     uint64_t total = 0;
     tm_batch_stats st{};
     ScanArgs scan_args{};
@@ -244,6 +278,13 @@ struct tm_batch {
     uint64_t tok_dict = ~0ull;   // dict.size() the device tokens were made with
     uint8_t* d_bytes = nullptr;
     uint64_t* d_boffs = nullptr;
+    // the tokeniser's inputs: d_bytes / d_boffs, or both inside d_in when the
+    // batch came as one packed [offs | bytes] block (async slots: one H2D)
+    uint8_t* d_in = nullptr;
+    size_t c_in = 0;
+    const uint8_t* in_bytes = nullptr;
+    const uint64_t* in_offs = nullptr;
+    uint64_t seen_upload = 0;   // own-stream batches: the last trie upload this batch's stream waited for
     uint32_t* d_wcount = nullptr;
     size_t c_bytes = 0, c_boffs = 0, c_wcount = 0;
     uint64_t tok_base = 0;
@@ -280,20 +321,27 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount);
+        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in);
+        in_bytes = nullptr;
+        in_offs = nullptr;
         if (h_bad) (void)hipHostFree(h_bad);
         h_bad = nullptr;
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
-        dev_free(d_count); dev_free(d_src); dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
+        dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
         if (h_total) (void)hipHostFree(h_total);
         h_total = nullptr;
-        dev_free(d_bsums); dev_free(d_ctrl); dev_free(d_ovf); dev_free(d_total); dev_free(d_stats);
+        dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total);
+        dev_free(d_hdr);
+        if (h_hdr) (void)hipHostFree(h_hdr);
+        h_hdr = nullptr;
+        hdr_cap = 0;
+        d_count = d_ctrl = h_ctrl = h_count = nullptr;
+        d_src = d_stats = h_src = h_stats = nullptr;
+        dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid); dev_free(d_sokey);
+        c_sq = c_so = c_sq2 = c_sq3 = c_so2 = c_sq4 = 0;
         if (h_rowoff) (void)hipHostFree(h_rowoff);
         if (h_ids) (void)hipHostFree(h_ids);
-        if (h_ctrl) (void)hipHostFree(h_ctrl);
-        if (h_stats) (void)hipHostFree(h_stats);
-        h_rowoff = h_ids = h_ctrl = nullptr;
-        h_stats = nullptr;
+        h_rowoff = h_ids = nullptr;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev2) (void)hipEventDestroy(ev2);
@@ -303,27 +351,67 @@ struct tm_batch {
 
 // ==================================================================== engine
 
-// One tm_match_coalesced caller waiting for its row.
-struct CoalesceReq {
-    const uint8_t* topic;
-    size_t len;
-    uint32_t* ids;
-    uint32_t cap;
-    uint32_t n_out;
-    int rc;
-    bool done;
+// ------------------------------------------------------------ async matching
+// One tm_match_async call.
+struct AsyncCall {
+    tm_match_cb cb;
+    void* ctx;
+};
+
+// One device batch of the async pipeline: a tm_batch on a stream of its own,
+// its inputs in pinned memory, and the read-back of its rows.
+struct AsyncSlot {
+    tm_batch b;
+    std::vector<uint8_t> bytes;          // the calls' topics, concatenated
+    std::vector<uint64_t> offs;
+    std::vector<AsyncCall> calls;
+    uint8_t* h_in = nullptr;             // pinned [offs (n+1) u64 | bytes] (H2D source)
+    size_t c_in = 0;
+    // written by tm_export_host: [ctrl | stats | src n u64 | count n u32] and the rows
+    uint8_t* h_out = nullptr;
+    size_t c_out = 0;
+    uint32_t* h_rows = nullptr;
+    size_t c_rows = 0;
+    hipEvent_t ev_done = nullptr;
+    int rc = TM_OK;                      // launch failure (delivered to every call)
+    bool claimed = false;                // a completer is delivering it
 };
 
 struct tm_engine {
     std::recursive_mutex mu;
-    // tm_match_coalesced: pending single-topic callers; the first caller to find
-    // no leader becomes it, lingers, and runs one batch for everyone queued
-    std::mutex cmu;
-    std::condition_variable ccv;
-    std::vector<CoalesceReq*> cpending;
-    bool cleader = false;
-    uint32_t c_max = 65536, c_linger_us = 0;
-    uint64_t c_batches = 0, c_requests = 0;
+    // async pipeline (tm_match_async / tm_match_coalesced): calls queue on amu;
+    // the launcher thread turns the queue into a device batch on a free slot
+    // (under mu, like every other engine operation), the completer thread
+    // waits for slots in launch order and delivers the rows
+    std::mutex amu;
+    std::condition_variable a_work, a_done;
+    // submissions go to one of QSHARDS queues picked by the calling thread, so
+    // concurrent submitters (the NIF's scheduler threads) rarely share a lock;
+    // the launcher drains them into a batch
+    struct alignas(64) QShard {
+        std::mutex mu;
+        std::vector<uint8_t> bytes;
+        std::vector<uint32_t> lens;
+        std::vector<AsyncCall> calls;
+        size_t head = 0;                 // calls before head were taken
+        size_t head_bytes = 0;
+    };
+    static constexpr uint32_t QSHARDS = 16;
+    QShard qs[QSHARDS];
+    std::atomic<uint64_t> q_count{0};    // calls queued in all shards
+    std::atomic<bool> a_live{false};     // pipeline threads running and accepting calls
+    std::vector<AsyncSlot*> a_slots, a_free;
+    std::deque<AsyncSlot*> a_inflight;
+    std::thread a_launcher;
+    std::vector<std::thread> a_completers;
+    bool a_started = false, a_stop = false, a_launcher_done = false;
+    // a batch launches when a slot is free and either nothing is in flight or
+    // at least a_busy_min calls queued: under load, calls accumulate while the
+    // device works instead of trickling out as tiny batches
+    uint32_t a_max = 16384, a_linger_us = 0, a_depth = 3, a_busy_min = 128, a_ncompleters = 2;
+    uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0;
+    // where the pipeline's time goes (host microseconds, summed over batches)
+    double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
     bool upload_nosync = false;   // set by tm_match_batch (prepare -> launch -> wait in one call)
     int device = -1;
     unsigned threads = 1;
@@ -376,6 +464,11 @@ struct tm_engine {
     uint32_t* d_flenv = nullptr;
     size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0, cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
     hipEvent_t ev_delta = nullptr;
+    hipEvent_t ev_sync = nullptr;        // end of the delta uploads, waited for by own-stream batches
+    // batches on streams of their own (async slots) read the replica
+    // concurrently with the engine stream: uploads wait for their walks first
+    std::vector<tm_batch*> readers;
+    uint64_t upload_seq = 0;             // async trie uploads recorded on ev_sync
     bool delta_inflight = false;
     // device word dictionary (device tokeniser): verbatim table + arena
     DictEnt* d_dict = nullptr;
@@ -390,11 +483,6 @@ struct tm_engine {
     size_t ch_dxidx = 0, ch_dxval = 0, cd_dxidx = 0, cd_dxval = 0;
     bool dev_tok = true;            // TM_CFG_HOST_TOKENIZE / TM_HOST_TOKENIZE=1: tokenise on the host
 
-    // slow-path scratch
-    uint32_t s_waves = 512, s_qcap = 1u << 13, s_ocap = 1u << 14;
-    uint32_t *d_sqpar = nullptr, *d_sqpw = nullptr, *d_sqmeta = nullptr, *d_sofid = nullptr;
-    unsigned long long *d_sqkey = nullptr, *d_sokey = nullptr;
-    size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
 
     uint64_t version = 1;
     uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
@@ -1115,15 +1203,32 @@ struct tm_engine {
         return TM_OK;
     }
 
+    bool needs_repack() const {
+        return live_edges > 65536 && (slots.size() > (size_t)(live_edges / target_load) * 2 ||
+                                      slots.size() * target_load * 1.5 < live_edges);
+    }
+
+    // anything for sync_device to upload?
+    bool upload_pending() {
+        if (full_dirty || !dirty.empty() || d_nslots != slots.size() || needs_repack()) return true;
+        if (full_f_dirty || !dirty_f.empty() || fbytes.size() > fbytes_uploaded) return true;
+        if (c_foff < n_parent.size() || c_flen < n_parent.size() || c_fbytes < fbytes.size() + 1) return true;
+        if (dev_tok && (d_dict_n != dict.table().size() || d_dict_gen != dict.gen() || !dict.dirty().empty() ||
+                        dict.arena().size() > arena_uploaded || c_arena < dict.arena().size() + 1))
+            return true;
+        return false;
+    }
+
     int sync_device() {
         if (device < 0) return TM_ENODEV;
         int rc = ensure_delta_idle();
         if (rc) return rc;
+        if (!readers.empty() && upload_pending())
+            for (tm_batch* r : readers)   // batches on other streams finish before the tables change
+                if (r->launched) HIP_OK(hipStreamSynchronize(r->own));
         // after a bulk build or heavy churn, re-pack the replica to load ~0.55 so
         // the walk's working set stays small (it is a full upload anyway)
-        if (live_edges > 65536 && (slots.size() > (size_t)(live_edges / target_load) * 2 ||
-                                   slots.size() * target_load * 1.5 < live_edges))
-            rehash((size_t)(live_edges / target_load));
+        if (needs_repack()) rehash((size_t)(live_edges / target_load));
         // edge hash
         if (d_nslots != slots.size()) {
             dev_free(d_slots);
@@ -1210,6 +1315,10 @@ struct tm_engine {
         } else if (async_used) {
             HIP_OK(hipEventRecord(ev_delta, stream));
             delta_inflight = true;
+            if (!readers.empty()) {   // own-stream batches launched from now on wait for this upload
+                HIP_OK(hipEventRecord(ev_sync, stream));
+                ++upload_seq;
+            }
         }
         return TM_OK;
     }
@@ -1261,15 +1370,18 @@ struct tm_engine {
         return TM_OK;
     }
 
-    int ensure_slow_scratch() {
+    // generic-path scratch of a batch: one frontier + match area per slow wave;
+    // 64 waves for small batches, up to 512 for large ones
+    int ensure_slow_scratch(tm_batch* b) {
         int rc;
-        const size_t q = (size_t)s_waves * s_qcap, o = (size_t)s_waves * s_ocap;
-        if ((rc = dev_reserve(d_sqpar, c_sq, q))) return rc;
-        if ((rc = dev_reserve(d_sqpw, c_sq2, q))) return rc;
-        if ((rc = dev_reserve(d_sqmeta, c_sq3, q))) return rc;
-        if ((rc = dev_reserve(d_sqkey, c_sq4, q))) return rc;
-        if ((rc = dev_reserve(d_sofid, c_so, o))) return rc;
-        if ((rc = dev_reserve(d_sokey, c_so2, o))) return rc;
+        if (!b->s_waves) b->s_waves = std::min<uint32_t>(512, std::max<uint32_t>(64, b->n / 2048));
+        const size_t q = (size_t)b->s_waves * b->s_qcap, o = (size_t)b->s_waves * b->s_ocap;
+        if ((rc = dev_reserve(b->d_sqpar, b->c_sq, q))) return rc;
+        if ((rc = dev_reserve(b->d_sqpw, b->c_sq2, q))) return rc;
+        if ((rc = dev_reserve(b->d_sqmeta, b->c_sq3, q))) return rc;
+        if ((rc = dev_reserve(b->d_sqkey, b->c_sq4, q))) return rc;
+        if ((rc = dev_reserve(b->d_sofid, b->c_so, o))) return rc;
+        if ((rc = dev_reserve(b->d_sokey, b->c_so2, o))) return rc;
         return TM_OK;
     }
 
@@ -1377,11 +1489,12 @@ struct tm_engine {
         if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(b->h_slow.size(), 1)))) return rc;
-        HIP_OK(hipMemcpyAsync(b->d_words, b->h_words.data(), b->h_words.size() * 4, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(b->d_toff, b->h_toff.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, stream));
-        if (n) HIP_OK(hipMemcpyAsync(b->d_tflags, b->h_tflags.data(), n, hipMemcpyHostToDevice, stream));
+        const hipStream_t S = st(b);
+        HIP_OK(hipMemcpyAsync(b->d_words, b->h_words.data(), b->h_words.size() * 4, hipMemcpyHostToDevice, S));
+        HIP_OK(hipMemcpyAsync(b->d_toff, b->h_toff.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, S));
+        if (n) HIP_OK(hipMemcpyAsync(b->d_tflags, b->h_tflags.data(), n, hipMemcpyHostToDevice, S));
         if (!b->h_slow.empty())
-            HIP_OK(hipMemcpyAsync(b->d_slow, b->h_slow.data(), b->h_slow.size() * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(b->d_slow, b->h_slow.data(), b->h_slow.size() * 4, hipMemcpyHostToDevice, S));
         b->dev_slow = false;
         return reserve_outputs(b);
     }
@@ -1397,14 +1510,13 @@ struct tm_engine {
         if ((rc = sync_device())) return rc;
         if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;
         if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
-        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
         if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
         if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
         HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, stream));
         if (!n) HIP_OK(hipMemsetAsync(d_toff, 0, 4, stream));
         TokArgs t{};
         t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
@@ -1484,21 +1596,40 @@ struct tm_engine {
         return TM_OK;
     }
 
+    // the [ctrl | stats | src | count] block and its pinned mirror, for cap topics
+    static int reserve_hdr(tm_batch* b, size_t cap) {
+        if (b->d_hdr && b->hdr_cap >= cap) return TM_OK;
+        cap = std::max<size_t>(cap + cap / 4, 1024);
+        uint8_t *d = nullptr, *h = nullptr;
+        HIP_OK(hipMalloc((void**)&d, tm_batch::hdr_bytes(cap)));
+        if (hipHostMalloc((void**)&h, tm_batch::hdr_bytes(cap), hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(d);
+            snprintf(last_error(), 512, "hipHostMalloc of %zu bytes failed", tm_batch::hdr_bytes(cap));
+            return TM_ENOMEM;
+        }
+        dev_free(b->d_hdr);
+        if (b->h_hdr) (void)hipHostFree(b->h_hdr);
+        b->d_hdr = d;
+        b->h_hdr = h;
+        b->hdr_cap = cap;
+        const size_t o_stats = CTRL_WORDS * 4, o_src = tm_batch::HDR_FIXED, o_count = o_src + cap * 8;
+        b->d_ctrl = (uint32_t*)d; b->h_ctrl = (uint32_t*)h;
+        b->d_stats = (unsigned long long*)(d + o_stats); b->h_stats = (unsigned long long*)(h + o_stats);
+        b->d_src = (unsigned long long*)(d + o_src); b->h_src = (unsigned long long*)(h + o_src);
+        b->d_count = (uint32_t*)(d + o_count); b->h_count = (uint32_t*)(h + o_count);
+        return TM_OK;
+    }
+
     int reserve_outputs(tm_batch* b) {
         int rc;
         const uint32_t n = b->n;
         const size_t nn = std::max<size_t>(n, 1);
-        if ((rc = dev_reserve(b->d_count, b->c_count, nn))) return rc;
-        if ((rc = dev_reserve(b->d_src, b->c_src, nn))) return rc;
+        if ((rc = reserve_hdr(b, nn))) return rc;
         if ((rc = dev_reserve(b->d_rowoff, b->c_rowoff, nn + 1))) return rc;
         if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
         if ((rc = dev_reserve(b->d_ovf, b->c_ovf, nn))) return rc;
-        if ((rc = dev_reserve(b->d_ctrl, b->c_ctrl, CTRL_WORDS))) return rc;
-        if ((rc = dev_reserve(b->d_stats, b->c_stats, ST_N))) return rc;
         if ((rc = dev_reserve(b->d_total, b->c_total, 1))) return rc;
         if ((rc = reserve_rows(b))) return rc;
-        if ((rc = host_reserve(b->h_ctrl, b->ch_ctrl, CTRL_WORDS))) return rc;
-        if ((rc = host_reserve(b->h_stats, b->ch_stats, ST_N))) return rc;
         if (!b->ev0) {
             HIP_OK(hipEventCreate(&b->ev0));
             HIP_OK(hipEventCreate(&b->ev1));
@@ -1512,7 +1643,8 @@ struct tm_engine {
     // ids[] = the CSR.  sfids/ids start at 32 per topic and grow on demand.
     int reserve_rows(tm_batch* b) {
         int rc;
-        const uint64_t fast = std::max<uint64_t>((uint64_t)match_waves(b->n, device, qcap) * 64 * row_cap, 1);
+        const uint64_t fast =
+            std::max<uint64_t>((uint64_t)match_waves(b->n, device, qcap) * tile_topics(b->n) * row_cap, 1);
         if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
         if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
@@ -1619,27 +1751,44 @@ struct tm_engine {
         return upload_batch(b);
     }
 
+    hipStream_t st(const tm_batch* b) const { return b->own ? b->own : stream; }
+
     // device tokenisation: the caller's bytes and offsets go to HBM now (the
     // caller's buffers are only borrowed for the call); words are produced at launch
     int upload_bytes(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
         int rc;
+        const hipStream_t S = st(b);
         const uint64_t base = offsets[0], nbytes = offsets[n] - base;
         if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;   // u32 word offsets
         b->tok_base = base;
-        b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
         if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;   // +16: no tail reads past
         if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
-        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = reserve_tokens(b, n, nbytes))) return rc;
+        if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, S));
+        HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, S));
+        // the caller's buffers are only borrowed for the call; tm_match_batch
+        // (and the async slots, whose inputs are their own pinned buffers)
+        // wait for the whole pipeline later, so they skip this sync
+        if (!upload_nosync && !b->own) HIP_OK(hipStreamSynchronize(S));
+        b->in_bytes = b->d_bytes;
+        b->in_offs = b->d_boffs;
+        return tokens_pending(b);
+    }
+
+    // the device tokeniser's buffers for n topics of nbytes; words at launch
+    int reserve_tokens(tm_batch* b, uint32_t n, uint64_t nbytes) {
+        int rc;
+        b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
         if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(b->nwords, 1)))) return rc;
         if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
-        if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
-        // the caller's buffers are only borrowed for the call; tm_match_batch
-        // waits for the whole pipeline before returning, so it skips this sync
-        if (!upload_nosync) HIP_OK(hipStreamSynchronize(stream));
+        return TM_OK;
+    }
+
+    int tokens_pending(tm_batch* b) {
         b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
         b->dev_tok = true;
         b->tok_dict = ~0ull;
@@ -1647,34 +1796,67 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
-    int launch(tm_batch* b) {
+    // An async slot's batch: blk = pinned [offs (n+1) u64 from 0 | bytes],
+    // one H2D on the slot's stream (topic lengths were checked at submit).
+    int upload_packed(tm_batch* b, const uint8_t* blk, uint32_t n, uint64_t nbytes) {
+        int rc;
+        const size_t head = ((size_t)n + 1) * 8;
+        if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        b->dedup = false;
+        b->n_pub = n;
+        b->row_of.clear();
+        b->launched = b->done = false;
+        b->tokens_only = false;
+        b->n = n;
+        b->bytes.clear();
+        b->offs.clear();
+        b->tok_base = 0;
+        if ((rc = reserve_tokens(b, n, nbytes))) return rc;
+        if ((rc = dev_reserve(b->d_in, b->c_in, head + nbytes + 16))) return rc;   // +16: no tail reads past
+        HIP_OK(hipMemcpyAsync(b->d_in, blk, head + nbytes, hipMemcpyHostToDevice, b->own));
+        b->in_offs = reinterpret_cast<const uint64_t*>(b->d_in);
+        b->in_bytes = b->d_in + head;
+        return tokens_pending(b);
+    }
+
+    // Enqueues the pipeline on the batch's stream.  csr = false (async slots):
+    // stop after the walk -- rows stay in the staging area, described by the
+    // per-topic (src, count) of the header block, and the caller enqueues its
+    // own read-back; ev2 then marks the end of the walk.
+    int launch(tm_batch* b, bool csr = true) {
         if (device < 0) return TM_ENODEV;
         int rc;
+        const hipStream_t S = st(b);
         if (!b->tokens_only && !b->dev_tok && b->dict_size != dict.size()) {   // new words since tokenisation
             if ((rc = tokenize(b))) return rc;
             if ((rc = upload_batch(b))) return rc;
         }
         if ((rc = sync_device())) return rc;
-        if ((rc = ensure_slow_scratch())) return rc;
+        if (b->own && b->seen_upload != upload_seq) {   // trie deltas still in flight on the engine stream land first
+            HIP_OK(hipStreamWaitEvent(S, ev_sync, 0));
+            b->seen_upload = upload_seq;
+        }
+        if ((rc = ensure_slow_scratch(b))) return rc;
         if (checked) {
             if ((rc = dev_reserve(d_dbg, c_dbg, 8))) return rc;
             if ((rc = host_reserve(h_dbg, ch_dbg, 8))) return rc;
-            HIP_OK(hipMemsetAsync(d_dbg, 0, 8 * 4, stream));
+            HIP_OK(hipMemsetAsync(d_dbg, 0, 8 * 4, S));
         }
-        HIP_OK(hipMemsetAsync(b->d_ctrl, 0, CTRL_WORDS * 4, stream));
-        HIP_OK(hipMemsetAsync(b->d_stats, 0, ST_N * 8, stream));
-        if (b->dev_tok && b->tok_dict != dict.size()) {
+        const bool tokenize_now = b->dev_tok && b->tok_dict != dict.size();
+        if (!tokenize_now) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
+        if (tokenize_now) {
             b->tok_dict = dict.size();
-            HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, stream));
             TokArgs t{};
-            t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = b->tok_base; t.n = b->n;
+            t.zero = reinterpret_cast<uint32_t*>(b->d_hdr);   // the tokeniser's first kernel clears ctrl + stats
+            t.zero_words = tm_batch::HDR_FIXED / 4;
+            t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
             t.dict = d_dict; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
             t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
             ScanArgs ts{};
             ts.block_sums = b->d_bsums;
-            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
+            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
         }
         MatchArgs a{};
         a.slots = d_slots;
@@ -1687,85 +1869,73 @@ struct tm_engine {
         a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
         a.grid = match_waves(b->n, device, qcap);
+        a.tile_topics = tile_topics(b->n);
         a.qcap = qcap;
-        if ((uint64_t)a.grid * 64 * row_cap > b->c_rows) {
+        if ((uint64_t)a.grid * a.tile_topics * row_cap > b->c_rows) {
             snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
             return TM_EIO;
         }
         a.sfids = b->d_sfids; a.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
-        a.s_qparent = d_sqpar; a.s_qpw = d_sqpw; a.s_qmeta = d_sqmeta; a.s_qkey = d_sqkey;
-        a.s_ofid = d_sofid; a.s_okey = d_sokey;
-        a.s_qcap = s_qcap; a.s_ocap = s_ocap; a.s_waves = s_waves;
+        a.s_qparent = b->d_sqpar; a.s_qpw = b->d_sqpw; a.s_qmeta = b->d_sqmeta; a.s_qkey = b->d_sqkey;
+        a.s_ofid = b->d_sofid; a.s_okey = b->d_sokey;
+        a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;
         a.nwords = (uint32_t)std::max<uint64_t>(b->nwords, 1);
         a.nslots = (uint32_t)slots.size();
         a.nnodes = (uint32_t)n_parent.size();
         a.nfbytes = fbytes.size();
         a.dbg = checked ? d_dbg : nullptr;
-        HIP_OK(launch_match(a, stream, b->ev0, b->ev1, checked));
+        HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        b->launched = true;
+        b->done = false;
+        b->csr = csr;
+        if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
         ScanArgs s{};
         s.count = b->d_count; s.src = b->d_src;
         s.sfids = b->d_sfids; s.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? d_dbg : nullptr;
-        HIP_OK(launch_scan(s, stream, b->d_total));
-        HIP_OK(launch_finalize(s, stream, checked));
+        HIP_OK(launch_scan(s, S, b->d_total));
+        HIP_OK(launch_finalize(s, S, checked));
         b->scan_args = s;
-        HIP_OK(hipEventRecord(b->ev2, stream));
-        HIP_OK(hipMemcpyAsync(b->h_ctrl, b->d_ctrl, CTRL_WORDS * 4, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipMemcpyAsync(b->h_stats, b->d_stats, ST_N * 8, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, stream));
-        if (checked) HIP_OK(hipMemcpyAsync(h_dbg, d_dbg, 8 * 4, hipMemcpyDeviceToHost, stream));
-        b->launched = true;
-        b->done = false;
+        HIP_OK(hipEventRecord(b->ev2, S));
+        HIP_OK(hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S));   // ctrl + stats
+        HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S));
+        if (checked) HIP_OK(hipMemcpyAsync(h_dbg, d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
         return TM_OK;
     }
 
-    int wait(tm_batch* b) {
-        if (!b->launched) return TM_EINVAL;
-        for (int attempt = 0;; ++attempt) {
-            HIP_OK(hipStreamSynchronize(stream));
-            if (checked && h_dbg[0]) {
-                snprintf(last_error(), 512, "bounds check %u failed: index %u bound %u (count %u, extra %u)",
-                         h_dbg[0], h_dbg[1], h_dbg[2], h_dbg[3], h_dbg[4]);
-                return TM_EIO;
-            }
-            const uint32_t err = b->h_ctrl[CTRL_ERR];
-            const uint64_t need = (uint64_t)b->h_ctrl[CTRL_STAGING64] | ((uint64_t)b->h_ctrl[CTRL_STAGING64 + 1] << 32);
-            const uint64_t nmatch = b->h_stats[ST_MATCHES];
-            // a CSR with u32 offsets cannot hold more (tm_result): refuse, never wrap
-            if ((err & ERR_CSR_RANGE) || need > result_limit || nmatch > result_limit) {
-                snprintf(last_error(), 512, "batch result too large: %llu staged / %llu matched > limit %llu",
-                         (unsigned long long)need, (unsigned long long)nmatch, (unsigned long long)result_limit);
-                return TM_EOVERFLOW;
-            }
-            if (!err) break;
-            if (attempt >= 6) return TM_EOVERFLOW;
-            if (err & ERR_STAGING) {
-                int rc = dev_reserve(b->d_sfids, b->c_sfids, std::min<uint64_t>(need + need / 4 + 1024, MAX_RESULT));
-                if (rc) return rc;
-            }
-            if (err & ERR_SLOW_SCRATCH) {
-                s_qcap *= 4;
-                s_ocap *= 4;
-            }
-            int rc = launch(b);
+    // control words of a finished launch: TM_EOVERFLOW past the u32 CSR, the
+    // retry reasons in *err (0 = clean)
+    int check_ctrl(const uint32_t* ctrl, const unsigned long long* stats, uint32_t* err, uint64_t* need) {
+        *err = ctrl[CTRL_ERR];
+        *need = (uint64_t)ctrl[CTRL_STAGING64] | ((uint64_t)ctrl[CTRL_STAGING64 + 1] << 32);
+        const uint64_t nmatch = stats[ST_MATCHES];
+        // a CSR with u32 offsets cannot hold more (tm_result): refuse, never wrap
+        if ((*err & ERR_CSR_RANGE) || *need > result_limit || nmatch > result_limit) {
+            snprintf(last_error(), 512, "batch result too large: %llu staged / %llu matched > limit %llu",
+                     (unsigned long long)*need, (unsigned long long)nmatch, (unsigned long long)result_limit);
+            return TM_EOVERFLOW;
+        }
+        return TM_OK;
+    }
+
+    // capacity misses of the last launch: grow what overflowed (the caller relaunches)
+    int grow_for(tm_batch* b, uint32_t err, uint64_t need) {
+        if (err & ERR_STAGING) {
+            int rc = dev_reserve(b->d_sfids, b->c_sfids, std::min<uint64_t>(need + need / 4 + 1024, MAX_RESULT));
             if (rc) return rc;
         }
-        // CSR capacity: the finalize pass is rerun alone when ids[] was too small
-        if (b->h_total[0] > b->c_ids) {
-            int rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->h_total[0] + b->h_total[0] / 4);
-            if (rc) return rc;
-            b->scan_args.ids = b->d_ids;
-            b->scan_args.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
-            // scan + finalize again (finalize turns the block-local offsets into global ones)
-            HIP_OK(launch_scan(b->scan_args, stream, b->d_total));
-            HIP_OK(launch_finalize(b->scan_args, stream, checked));
-            HIP_OK(hipEventRecord(b->ev2, stream));
-            HIP_OK(hipStreamSynchronize(stream));
+        if (err & ERR_SLOW_SCRATCH) {
+            b->s_qcap *= 4;
+            b->s_ocap *= 4;
         }
+        return TM_OK;
+    }
+
+    void fill_stats(tm_batch* b) {
         float ms_match = 0, ms_total = 0;
         (void)hipEventElapsedTime(&ms_match, b->ev0, b->ev1);
         (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
@@ -1779,6 +1949,44 @@ struct tm_engine {
         b->st.ms_match = ms_match;
         b->st.ms_total = ms_total;
         b->total = b->st.matches;
+    }
+
+    int wait(tm_batch* b) {
+        if (!b->launched) return TM_EINVAL;
+        const hipStream_t S = st(b);
+        if (!b->csr) {   // an async launch stopped after the walk: redo it the CSR way
+            int rc = launch(b, true);
+            if (rc) return rc;
+        }
+        for (int attempt = 0;; ++attempt) {
+            HIP_OK(hipStreamSynchronize(S));
+            if (checked && h_dbg[0]) {
+                snprintf(last_error(), 512, "bounds check %u failed: index %u bound %u (count %u, extra %u)",
+                         h_dbg[0], h_dbg[1], h_dbg[2], h_dbg[3], h_dbg[4]);
+                return TM_EIO;
+            }
+            uint32_t err;
+            uint64_t need;
+            int rc = check_ctrl(b->h_ctrl, b->h_stats, &err, &need);
+            if (rc) return rc;
+            if (!err) break;
+            if (attempt >= 6) return TM_EOVERFLOW;
+            if ((rc = grow_for(b, err, need))) return rc;
+            if ((rc = launch(b))) return rc;
+        }
+        // CSR capacity: the finalize pass is rerun alone when ids[] was too small
+        if (b->h_total[0] > b->c_ids) {
+            int rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->h_total[0] + b->h_total[0] / 4);
+            if (rc) return rc;
+            b->scan_args.ids = b->d_ids;
+            b->scan_args.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
+            // scan + finalize again (finalize turns the block-local offsets into global ones)
+            HIP_OK(launch_scan(b->scan_args, S, b->d_total));
+            HIP_OK(launch_finalize(b->scan_args, S, checked));
+            HIP_OK(hipEventRecord(b->ev2, S));
+            HIP_OK(hipStreamSynchronize(S));
+        }
+        fill_stats(b);
         b->done = true;
         return TM_OK;
     }
@@ -1786,6 +1994,7 @@ struct tm_engine {
     int result(tm_batch* b, tm_result* out) {
         if (!b->done) return TM_EINVAL;
         int rc;
+        const hipStream_t S = st(b);
         // the match count is known since wait(): both copies go out behind one sync
         const uint64_t total = b->total;
         if (total > b->c_ids) {
@@ -1795,9 +2004,9 @@ struct tm_engine {
         }
         if ((rc = host_reserve(b->h_rowoff, b->ch_rowoff, (size_t)b->n + 1))) return rc;
         if ((rc = host_reserve(b->h_ids, b->ch_ids, std::max<uint64_t>(total, 1)))) return rc;
-        HIP_OK(hipMemcpyAsync(b->h_rowoff, b->d_rowoff, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, stream));
-        if (total) HIP_OK(hipMemcpyAsync(b->h_ids, b->d_ids, total * 4, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipStreamSynchronize(stream));
+        HIP_OK(hipMemcpyAsync(b->h_rowoff, b->d_rowoff, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, S));
+        if (total) HIP_OK(hipMemcpyAsync(b->h_ids, b->d_ids, total * 4, hipMemcpyDeviceToHost, S));
+        HIP_OK(hipStreamSynchronize(S));
         if (b->h_rowoff[b->n] != total) {
             snprintf(last_error(), 512, "inconsistent CSR: row offsets end at %u, kernel count %llu",
                      b->h_rowoff[b->n], (unsigned long long)total);
@@ -1808,6 +2017,304 @@ struct tm_engine {
         out->row_offsets = b->h_rowoff;
         out->filter_ids = b->h_ids;
         return TM_OK;
+    }
+
+
+    // ------------------------------------------------------------ async pipeline
+    // Slots are created on first use (under amu; takes mu).
+    int async_start() {
+        if (a_started) return TM_OK;
+        if (device < 0) return TM_ENODEV;
+        if (const char* d = getenv("TM_ASYNC_DEPTH")) a_depth = (uint32_t)std::min(16, std::max(1, atoi(d)));
+        if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) a_busy_min = (uint32_t)std::max(1, atoi(d));
+        if (const char* d = getenv("TM_ASYNC_COMPLETERS")) a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
+        {
+            std::lock_guard<std::recursive_mutex> g(mu);
+            HIP_OK(hipSetDevice(device));
+            for (uint32_t i = 0; i < a_depth; ++i) {
+                AsyncSlot* sl = new AsyncSlot();
+                a_slots.push_back(sl);
+                HIP_OK(hipStreamCreateWithFlags(&sl->b.own, hipStreamNonBlocking));
+                HIP_OK(hipEventCreateWithFlags(&sl->ev_done, hipEventDisableTiming));
+                a_free.push_back(sl);
+                readers.push_back(&sl->b);
+            }
+        }
+        a_stop = false;
+        a_launcher_done = false;
+        a_launcher = std::thread([this] { launcher_loop(); });
+        for (uint32_t i = 0; i < a_ncompleters; ++i) a_completers.emplace_back([this] { completer_loop(); });
+        a_started = true;
+        a_live.store(true, std::memory_order_release);
+        return TM_OK;
+    }
+
+    void async_stop() {
+        {
+            std::lock_guard<std::mutex> lk(amu);
+            if (!a_started && a_slots.empty()) return;
+            a_stop = true;
+            a_live.store(false, std::memory_order_release);
+        }
+        a_work.notify_all();
+        a_done.notify_all();
+        if (a_launcher.joinable()) a_launcher.join();
+        for (auto& t : a_completers)
+            if (t.joinable()) t.join();
+        a_completers.clear();
+        std::lock_guard<std::recursive_mutex> g(mu);
+        (void)hipSetDevice(device);
+        for (AsyncSlot* sl : a_slots) {
+            if (sl->b.own) (void)hipStreamSynchronize(sl->b.own);
+            sl->b.release();
+            if (sl->b.own) (void)hipStreamDestroy(sl->b.own);
+            if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
+            if (sl->h_in) (void)hipHostFree(sl->h_in);
+            if (sl->h_rows) (void)hipHostFree(sl->h_rows);
+            if (sl->h_out) (void)hipHostFree(sl->h_out);
+            delete sl;
+        }
+        a_slots.clear();
+        a_free.clear();
+        readers.clear();
+        a_started = false;
+    }
+
+    int match_async(const uint8_t* t, size_t len, tm_match_cb cb, void* ctx) {
+        if (!a_live.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> lk(amu);
+            if (a_stop) return TM_ENODEV;
+            if (!a_started) {
+                int rc = async_start();
+                if (rc) return rc;
+            }
+        }
+        static std::atomic<uint32_t> next_shard{0};
+        static thread_local uint32_t my_shard = next_shard.fetch_add(1) % QSHARDS;
+        QShard& sh = qs[my_shard];
+        {
+            std::lock_guard<std::mutex> g(sh.mu);
+            if (len) sh.bytes.insert(sh.bytes.end(), t, t + len);
+            sh.lens.push_back((uint32_t)len);
+            sh.calls.push_back(AsyncCall{cb, ctx});
+        }
+        const uint64_t q = q_count.fetch_add(1, std::memory_order_acq_rel) + 1;
+        if (q == 1 || q == a_busy_min || q == a_max) {   // the launcher may be waiting for this
+            std::lock_guard<std::mutex> lk(amu);
+            a_work.notify_one();
+        }
+        return TM_OK;
+    }
+
+    // moves exactly `take` queued calls (at least that many are queued) into the slot
+    void drain_queue(AsyncSlot* sl, size_t take) {
+        sl->calls.clear();
+        sl->bytes.clear();
+        sl->offs.assign(1, 0);
+        static thread_local uint32_t start = 0;
+        for (uint32_t k = 0; k < QSHARDS && sl->calls.size() < take; ++k) {
+            QShard& sh = qs[(start + k) % QSHARDS];
+            std::lock_guard<std::mutex> g(sh.mu);
+            size_t h = sh.head, hb = sh.head_bytes;
+            while (h < sh.calls.size() && sl->calls.size() < take) {
+                const uint32_t len = sh.lens[h];
+                sl->calls.push_back(sh.calls[h]);
+                sl->bytes.insert(sl->bytes.end(), sh.bytes.begin() + (long)hb, sh.bytes.begin() + (long)(hb + len));
+                sl->offs.push_back(sl->bytes.size());
+                hb += len;
+                ++h;
+            }
+            if (h == sh.calls.size()) {   // shard emptied: reset, keep the capacity
+                sh.calls.clear();
+                sh.lens.clear();
+                sh.bytes.clear();
+                sh.head = sh.head_bytes = 0;
+            } else {
+                sh.head = h;
+                sh.head_bytes = hb;
+            }
+        }
+        start = (start + 1) % QSHARDS;   // no shard is always last
+        q_count.fetch_sub(sl->calls.size(), std::memory_order_acq_rel);
+    }
+
+    // Forms batches from the queue: everything queued while the pipeline was
+    // busy (up to a_max), optionally after a linger, on the next free slot.
+    void launcher_loop() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(amu);
+        for (;;) {
+            a_work.wait(lk, [&] {
+                const uint64_t q = q_count.load(std::memory_order_acquire);
+                if (a_stop) return q == 0 || !a_free.empty();
+                const bool idle = a_free.size() == a_slots.size();
+                return q && !a_free.empty() && (idle || q >= a_busy_min);
+            });
+            if (q_count.load(std::memory_order_acquire) == 0) break;   // stopping, queue drained
+            if (a_linger_us && !a_stop && q_count.load() < a_max)
+                a_work.wait_for(lk, std::chrono::microseconds(a_linger_us),
+                                [&] { return a_stop || q_count.load() >= a_max; });
+            AsyncSlot* sl = a_free.back();
+            a_free.pop_back();
+            const size_t take = std::min<uint64_t>(q_count.load(std::memory_order_acquire), std::max<uint32_t>(a_max, 1));
+            lk.unlock();
+            drain_queue(sl, take);
+            const auto t0 = std::chrono::steady_clock::now();
+            try {
+                sl->rc = slot_launch(sl);
+            } catch (...) {
+                sl->rc = TM_ENOMEM;
+            }
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            lk.lock();
+            a_max_seen = std::max<uint64_t>(a_max_seen, sl->calls.size());
+            a_us_launch += us;
+            a_inflight.push_back(sl);
+            a_done.notify_all();
+        }
+        a_launcher_done = true;
+        a_done.notify_all();
+    }
+
+    // H2D of the slot's topics (one copy), device tokeniser, walk, and one
+    // kernel writing the per-topic (src, count) and the staged rows into the
+    // slot's pinned buffers -- all on the slot's stream; ev_done marks the end.
+    int slot_launch(AsyncSlot* sl) {
+        const uint32_t n = (uint32_t)sl->calls.size();
+        const size_t nb = sl->bytes.size(), head = ((size_t)n + 1) * 8;
+        int rc;
+        if ((rc = host_reserve(sl->h_in, sl->c_in, head + nb))) return rc;
+        memcpy(sl->h_in, sl->offs.data(), head);
+        if (nb) memcpy(sl->h_in + head, sl->bytes.data(), nb);
+        std::lock_guard<std::recursive_mutex> g(mu);
+        HIP_OK(hipSetDevice(device));
+        tm_batch* b = &sl->b;
+        const hipStream_t S = b->own;
+        rc = dev_tok ? upload_packed(b, sl->h_in, n, nb)
+                     : prepare(b, sl->h_in + head, reinterpret_cast<const uint64_t*>(sl->h_in), n);
+        if (rc) return rc;
+        if ((rc = launch(b, false))) return rc;
+        const size_t hdr_bytes = tm_batch::HDR_FIXED + (size_t)n * 8;
+        if ((rc = host_reserve_coherent(sl->h_out, sl->c_out, hdr_bytes + (size_t)n * 4 + 8))) return rc;
+        uint8_t* rows8 = reinterpret_cast<uint8_t*>(sl->h_rows);
+        if ((rc = host_reserve_coherent(rows8, sl->c_rows, std::max<size_t>(b->c_sfids, 1) * 4))) return rc;
+        sl->h_rows = reinterpret_cast<uint32_t*>(rows8);
+        void *d_out = nullptr, *d_rows = nullptr;
+        HIP_OK(hipHostGetDevicePointer(&d_out, sl->h_out, 0));
+        HIP_OK(hipHostGetDevicePointer(&d_rows, sl->h_rows, 0));
+        ExportArgs x{};
+        x.hdr = reinterpret_cast<const uint32_t*>(b->d_hdr);
+        x.hdr_words = hdr_bytes / 4;
+        x.h_hdr = reinterpret_cast<uint32_t*>(d_out);
+        x.count = b->d_count;
+        x.h_count = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_out) + hdr_bytes);
+        x.n = n;
+        x.rows = b->d_sfids;
+        x.h_rows = reinterpret_cast<uint32_t*>(d_rows);
+        x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
+        HIP_OK(launch_export_host(x, S));
+        HIP_OK(hipEventRecord(sl->ev_done, S));
+        return TM_OK;
+    }
+
+    // Each completer claims the oldest in-flight slot nobody delivers yet,
+    // waits for it and runs its callbacks; several completers deliver
+    // consecutive batches concurrently.
+    void completer_loop() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(amu);
+        for (;;) {
+            AsyncSlot* sl = nullptr;
+            a_done.wait(lk, [&] {
+                for (AsyncSlot* x : a_inflight)
+                    if (!x->claimed) {
+                        sl = x;
+                        return true;
+                    }
+                return a_launcher_done;
+            });
+            if (!sl) break;
+            sl->claimed = true;
+            lk.unlock();
+            bool recovered = false;
+            double us_wait = 0, us_deliver = 0;
+            try {
+                recovered = slot_deliver(sl, us_wait, us_deliver);
+            } catch (...) {
+            }
+            lk.lock();
+            a_inflight.erase(std::find(a_inflight.begin(), a_inflight.end(), sl));
+            a_us_wait += us_wait;
+            a_us_deliver += us_deliver;
+            ++a_batches;
+            a_recoveries += recovered ? 1 : 0;
+            a_requests += sl->calls.size();
+            sl->calls.clear();
+            sl->claimed = false;
+            a_free.push_back(sl);
+            a_work.notify_all();
+            a_done.notify_all();
+        }
+    }
+
+    // Returns true when the batch had to be re-run through the CSR path.
+    bool slot_deliver(AsyncSlot* sl, double& us_wait, double& us_deliver) {
+        tm_batch* b = &sl->b;
+        const uint32_t n = (uint32_t)sl->calls.size();
+        auto fail_all = [&](int rc) {
+            for (const AsyncCall& c : sl->calls) c.cb(c.ctx, rc, nullptr, 0);
+        };
+        if (sl->rc) {
+            (void)hipStreamSynchronize(b->own);   // whatever was enqueued before the failure
+            fail_all(sl->rc);
+            return false;
+        }
+        const auto tw = std::chrono::steady_clock::now();
+        if (hipEventSynchronize(sl->ev_done) != hipSuccess) {
+            fail_all(TM_EIO);
+            return false;
+        }
+        const auto td = std::chrono::steady_clock::now();
+        us_wait = std::chrono::duration<double, std::micro>(td - tw).count();
+        const size_t hdr_bytes = tm_batch::HDR_FIXED + (size_t)n * 8;
+        const uint32_t* ctrl = reinterpret_cast<const uint32_t*>(sl->h_out);
+        const unsigned long long* stats = reinterpret_cast<const unsigned long long*>(sl->h_out + CTRL_WORDS * 4);
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(sl->h_out + tm_batch::HDR_FIXED);
+        const uint32_t* count = reinterpret_cast<const uint32_t*>(sl->h_out + hdr_bytes);
+        uint32_t err = 0;
+        uint64_t need = 0;
+        int rc = check_ctrl(ctrl, stats, &err, &need);
+        if (rc) {
+            fail_all(rc);
+            return false;
+        }
+        if (!err && need > sl->c_rows / 4) err = ERR_STAGING;   // (cannot happen: rows hold the staging area)
+        if (err) {
+            // capacity miss (staging, generic-path scratch): the CSR path grows
+            // and re-runs, then the rows come from the CSR
+            tm_result r{};
+            {
+                std::lock_guard<std::recursive_mutex> g(mu);
+                (void)hipSetDevice(device);
+                rc = grow_for(b, err, need);
+                if (!rc) rc = wait(b);
+                if (!rc) rc = result(b, &r);
+            }
+            if (rc) {
+                fail_all(rc);
+                return true;
+            }
+            for (uint32_t i = 0; i < n; ++i)
+                sl->calls[i].cb(sl->calls[i].ctx, TM_OK, r.filter_ids + r.row_offsets[i],
+                                r.row_offsets[i + 1] - r.row_offsets[i]);
+            return true;
+        }
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t c = count[i];
+            sl->calls[i].cb(sl->calls[i].ctx, TM_OK, c ? sl->h_rows + src[i] : sl->h_rows, c);
+        }
+        us_deliver = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - td).count();
+        return false;
     }
 
     int init(const tm_config* cfg) {
@@ -1838,11 +2345,13 @@ struct tm_engine {
             HIP_OK(hipSetDevice(device));
             HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
             HIP_OK(hipEventCreateWithFlags(&ev_delta, hipEventDisableTiming));
+            HIP_OK(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
         }
         return TM_OK;
     }
 
     void destroy() {
+        async_stop();
         if (device >= 0) {
             (void)hipSetDevice(device);
             if (stream) (void)hipStreamSynchronize(stream);
@@ -1853,8 +2362,7 @@ struct tm_engine {
             if (h_dxidx) (void)hipHostFree(h_dxidx);
             if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
-            dev_free(d_sqpar); dev_free(d_sqpw); dev_free(d_sqmeta); dev_free(d_sqkey); dev_free(d_sofid);
-            dev_free(d_sokey); dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt);
+            dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);
@@ -1862,6 +2370,7 @@ struct tm_engine {
             if (h_foffv) (void)hipHostFree(h_foffv);
             if (h_flenv) (void)hipHostFree(h_flenv);
             if (ev_delta) (void)hipEventDestroy(ev_delta);
+            if (ev_sync) (void)hipEventDestroy(ev_sync);
             if (stream) (void)hipStreamDestroy(stream);
         }
     }
@@ -2058,78 +2567,76 @@ int tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t* offset
     return tm_batch_prepare_ex(e, topics, offsets, n, 0, out);
 }
 
-// The leader's device round trip for a set of queued callers: one
-// tm_match_batch under the engine lock (its result buffers stay valid while the
-// rows are copied out); if the batch fails, each caller is matched alone so a
-// bad topic fails only its own request.
-static void coalesce_run(tm_engine* e, std::vector<CoalesceReq*>& batch) {
-    std::vector<uint8_t> buf;
-    std::vector<uint64_t> offs(batch.size() + 1, 0);
-    for (size_t i = 0; i < batch.size(); ++i) {
-        buf.insert(buf.end(), batch[i]->topic, batch[i]->topic + batch[i]->len);
-        offs[i + 1] = buf.size();
+// tm_match_coalesced = tm_match_async + a wait: the callback copies the row
+// and releases the caller (brief spin, then a futex sleep).
+namespace {
+struct SyncWait {
+    std::atomic<int> state{0};   // 0 pending, 1 done, 2 caller asleep
+    uint32_t* ids;
+    uint32_t cap;
+    uint32_t n = 0;
+    int rc = TM_OK;
+};
+
+void sync_cb(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
+    SyncWait* w = static_cast<SyncWait*>(ctx);
+    w->rc = rc;
+    w->n = n;
+    if (rc == TM_OK && n && w->cap) memcpy(w->ids, ids, (size_t)std::min(n, w->cap) * 4);
+    if (w->state.exchange(1, std::memory_order_acq_rel) == 2)
+        syscall(SYS_futex, reinterpret_cast<int*>(&w->state), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+}  // namespace
+
+int tm_match_async(tm_engine* e, const uint8_t* topic, size_t len, tm_match_cb cb, void* ctx) {
+    if (!e || !cb || (!topic && len)) return TM_EINVAL;
+    if (len > TM_MAX_TOPIC_LEN) return TM_EINVAL;
+    try {
+        return e->match_async(topic, len, cb, ctx);
+    } catch (...) {
+        return TM_ENOMEM;
     }
-    static const uint8_t zero = 0;
-    std::lock_guard<std::recursive_mutex> g(e->mu);
-    tm_result r;
-    int rc = tm_match_batch(e, buf.empty() ? &zero : buf.data(), offs.data(), (uint32_t)batch.size(), &r);
-    if (rc == TM_OK) {
-        for (size_t i = 0; i < batch.size(); ++i) {
-            CoalesceReq* q = batch[i];
-            const uint32_t lo = r.row_offsets[i], m = r.row_offsets[i + 1] - lo;
-            for (uint32_t k = 0; k < m && k < q->cap; ++k) q->ids[k] = r.filter_ids[lo + k];
-            q->n_out = m;
-            q->rc = TM_OK;
-        }
-        return;
-    }
-    for (CoalesceReq* q : batch) q->rc = tm_trie_match(e, q->topic, q->len, q->ids, q->cap, &q->n_out);
 }
 
 int tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len, uint32_t* ids, uint32_t cap, uint32_t* n_out) {
     if (!e || !n_out || (!topic && len) || (cap && !ids)) return TM_EINVAL;
     if (len > TM_MAX_TOPIC_LEN) return TM_EINVAL;
-    CoalesceReq req{topic, len, ids, cap, 0, TM_OK, false};
-    std::unique_lock<std::mutex> lk(e->cmu);
-    e->cpending.push_back(&req);
-    e->ccv.notify_all();   // a lingering leader re-checks the batch size
-    while (!req.done) {
-        if (e->cleader) {
-            e->ccv.wait(lk);
-            continue;
-        }
-        e->cleader = true;
-        const size_t max_b = std::max<uint32_t>(e->c_max, 1);
-        e->ccv.wait_for(lk, std::chrono::microseconds(e->c_linger_us),
-                        [&] { return e->cpending.size() >= max_b; });
-        std::vector<CoalesceReq*> batch;
-        const size_t take = std::min(e->cpending.size(), max_b);
-        batch.assign(e->cpending.begin(), e->cpending.begin() + (long)take);
-        e->cpending.erase(e->cpending.begin(), e->cpending.begin() + (long)take);
-        lk.unlock();
-        try {
-            coalesce_run(e, batch);
-        } catch (...) {
-            for (CoalesceReq* q : batch) q->rc = TM_ENOMEM;
-        }
-        lk.lock();
-        for (CoalesceReq* q : batch) q->done = true;
-        ++e->c_batches;
-        e->c_requests += batch.size();
-        e->cleader = false;
-        e->ccv.notify_all();
-    }
-    *n_out = req.n_out;
-    return req.rc;
+    SyncWait w;
+    w.ids = ids;
+    w.cap = cap;
+    int rc = tm_match_async(e, topic, len, sync_cb, &w);
+    if (rc) return rc;
+    for (int i = 0; i < 4000 && w.state.load(std::memory_order_acquire) != 1; ++i) __builtin_ia32_pause();
+    int expect = 0;
+    if (w.state.compare_exchange_strong(expect, 2, std::memory_order_acq_rel))
+        while (w.state.load(std::memory_order_acquire) == 2)
+            syscall(SYS_futex, reinterpret_cast<int*>(&w.state), FUTEX_WAIT_PRIVATE, 2, nullptr, nullptr, 0);
+    *n_out = w.n;
+    return w.rc;
 }
 
 int tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us, uint64_t* batches, uint64_t* requests) {
     if (!e) return TM_EINVAL;
-    std::lock_guard<std::mutex> lk(e->cmu);
-    if (max_batch) e->c_max = max_batch;
-    if (linger_us != TM_NONE) e->c_linger_us = linger_us;
-    if (batches) *batches = e->c_batches;
-    if (requests) *requests = e->c_requests;
+    std::lock_guard<std::mutex> lk(e->amu);
+    if (max_batch) e->a_max = max_batch;
+    if (linger_us != TM_NONE) e->a_linger_us = linger_us;
+    if (batches) *batches = e->a_batches;
+    if (requests) *requests = e->a_requests;
+    return TM_OK;
+}
+
+int tm_async_stats_get(tm_engine* e, tm_async_stats* out) {
+    if (!e || !out) return TM_EINVAL;
+    std::lock_guard<std::mutex> lk(e->amu);
+    out->batches = e->a_batches;
+    out->requests = e->a_requests;
+    out->recoveries = e->a_recoveries;
+    out->max_batch = e->a_max_seen;
+    out->depth = e->a_depth;
+    out->queued = (uint32_t)e->q_count.load();
+    out->us_launch = e->a_us_launch;
+    out->us_wait = e->a_us_wait;
+    out->us_deliver = e->a_us_deliver;
     return TM_OK;
 }
 
@@ -2509,6 +3016,15 @@ const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
     if (len) *len = e->n_flen[id];
     static const uint8_t empty = 0;
     return e->n_flen[id] ? e->fbytes.data() + e->n_foff[id] : &empty;
+}
+
+int tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len) {
+    if (!e || !len || (cap && !buf)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (id >= e->n_topic.size() || !e->n_topic[id] || !e->n_live[id]) return TM_ENOENT;
+    *len = e->n_flen[id];
+    if (*len <= cap && *len) memcpy(buf, e->fbytes.data() + e->n_foff[id], *len);
+    return TM_OK;
 }
 
 int tm_filter_id(tm_engine* e, const uint8_t* f, size_t len, uint32_t* id) {

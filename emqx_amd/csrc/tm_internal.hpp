@@ -126,9 +126,10 @@ struct MatchArgs {
     // outputs
     uint32_t* count;          // per topic |M(t)|
     unsigned long long* src;  // per topic: offset of its sorted row in sfids[]
-    unsigned long long* rows; // [match_waves(n) * 64 * row_cap] wave-private emission rows,
+    unsigned long long* rows; // [match_waves(n) * tile_topics * row_cap] wave-private emission rows,
                               // (path code | filter id), reused by every tile of the wave
     uint32_t row_cap;         // K: per-topic row slots on the fast path
+    uint32_t tile_topics;     // topics per tm_match_tiles tile (tile_topics(n): 64 .. 1)
     uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
     uint32_t qcap;            // LDS probe-stack entries per wave (384 or 512)
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
@@ -255,11 +256,20 @@ hipError_t launch_export(const uint32_t* row_off, const uint32_t* ids, uint32_t 
 // probes exactly the host's slots; word bytes live in an append-only arena.
 struct DictEnt {
     uint64_t h;      // hash_word(bytes) | 1; 0 = empty
-    uint64_t off;    // arena offset
+    uint64_t head;   // bytes 0..7 and 8..15, little-endian, zero-padded: words of up
+    uint64_t head2;  // to 16 bytes compare without touching the arena
     uint32_t len;
     uint32_t id;
+    uint64_t off;    // arena offset (longer words: bytes 16.. are compared there)
+    uint64_t pad;
 };
-static_assert(sizeof(DictEnt) == 24, "dictionary entry is 24 bytes");
+static_assert(sizeof(DictEnt) == 48, "dictionary entry is 48 bytes (three 16-B loads)");
+
+__host__ __device__ inline uint64_t le_bytes(const uint8_t* p, uint32_t n) {   // n <= 8
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < n; ++k) v |= (uint64_t)p[k] << (8 * k);
+    return v;
+}
 
 constexpr uint64_t HW_K0 = 0xcbf29ce484222325ull, HW_K1 = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t HW_M1 = 0xBF58476D1CE4E5B9ull, HW_M2 = 0x94D049BB133111EBull;
@@ -276,6 +286,12 @@ __host__ __device__ inline uint64_t hw_final(uint64_t h, uint64_t tail) {
 // Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
 // the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp
 // tokenize_range), against the uploaded dictionary.
+// One wavefront per tile of 64 topics: a tile's bytes are contiguous, so
+// pass 1 counts the tile's words ('/' + 1 per topic) with coalesced loads,
+// a scan over tiles gives each tile its first word, and pass 2 stages the
+// tile's bytes in LDS, splits every topic there, looks its words up in the
+// dictionary with the lookups spread over the lanes, and writes the tile's
+// words with coalesced stores.
 struct TokArgs {
     const uint8_t* bytes;
     const uint64_t* offs;     // n + 1 absolute offsets (caller's), minus base
@@ -284,16 +300,32 @@ struct TokArgs {
     const DictEnt* dict;
     uint64_t dict_mask;       // table size - 1 (power of two)
     const uint8_t* arena;
-    uint32_t* wcount;         // pass 1: words per topic
+    uint32_t* wcount;         // pass 1: words per TILE (ntiles + 1 entries)
     uint8_t* tflags;
-    uint32_t* toff;           // pass 2: word offsets (block-local scan of wcount, made global here)
-    const uint32_t* bsums;    // scan block offsets (tm_scan_sums)
+    uint32_t* toff;           // n + 1 word offsets
+    const uint32_t* bsums;    // scan block offsets of the tile scan (tm_scan_sums)
     uint32_t* words;
     uint64_t words_cap;       // entries of words[]; nothing at or past it is written
     uint32_t* slow_list;
-    uint32_t* d_nslow;
+    uint32_t* d_nslow;        // [0] generic-path topics, [1] total words; zeroed by pass 1
+    uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
+    uint32_t zero_words;
 };
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
+
+// tm_export_host: an async batch's per-topic results and rows -> pinned host memory
+struct ExportArgs {
+    const uint32_t* hdr;      // batch header block (ctrl | stats | src ...), as u32
+    uint64_t hdr_words;       // u32 words of it to copy: ctrl + stats + src[n]
+    uint32_t* h_hdr;          // device-visible pointers of the pinned destinations
+    const uint32_t* count;
+    uint32_t* h_count;
+    uint64_t n;
+    const uint32_t* rows;     // staging area
+    uint32_t* h_rows;
+    uint64_t rows_cap;        // entries h_rows holds
+};
+hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
 hipError_t launch_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n, hipStream_t s);
 
 // shard of a (w0, w1) literal prefix; host and device agree (tm_filter_shard)
@@ -303,5 +335,6 @@ __host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uin
 // workgroups (one wave each) of tm_match_tiles for n topics on this device:
 // min(tiles, resident capacity), so that every wave is resident from the start
 uint32_t match_waves(uint32_t n, int device, uint32_t qcap);
+uint32_t tile_topics(uint32_t n);
 
 }  // namespace etm

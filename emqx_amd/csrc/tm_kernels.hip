@@ -227,8 +227,8 @@ __device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t tl, uint32
 #else
     if (slot < a.row_cap) {
 #endif
-        const uint64_t i = ((uint64_t)blockIdx.x * TILE + tl) * a.row_cap + slot;
-        a.rows[CK_(i, (uint64_t)gridDim.x * TILE * a.row_cap, 13)] = (key & KEY_MASK) | fid;
+        const uint64_t i = ((uint64_t)blockIdx.x * a.tile_topics + tl) * a.row_cap + slot;
+        a.rows[CK_(i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13)] = (key & KEY_MASK) | fid;
     }
 }
 
@@ -362,13 +362,13 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
         if (lane >= (uint32_t)o) incl += u;
     }
     const uint32_t pos = incl - cp;
-    const uint64_t rbase = (uint64_t)blockIdx.x * TILE * a.row_cap;
-    const uint64_t rlim = (uint64_t)gridDim.x * TILE * a.row_cap;
+    const uint64_t rbase = (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
+    const uint64_t rlim = (uint64_t)gridDim.x * a.tile_topics * a.row_cap;
     uint32_t rs = 0;
-    while (rs < (uint32_t)TILE) {
+    while (rs < a.tile_topics) {
         const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
         const uint64_t beyond = __ballot(lane >= rs && pos + cp - p0 > STAGE);
-        const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : (uint32_t)TILE;
+        const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : a.tile_topics;
         for (uint32_t r = rs; r < re; ++r) {
             const uint32_t cr = __builtin_amdgcn_readlane(c, r);
             if (cr == 0) continue;
@@ -600,7 +600,8 @@ template <bool CK, bool BIG, int QC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_tiles(MatchArgs a) {
     __shared__ TileLds<QC> L;
     const uint32_t lane = threadIdx.x;
-    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    const uint32_t tt = a.tile_topics;   // topics per tile: 64, or fewer for small batches
+    const uint32_t ntiles = (a.n + tt - 1) / tt;
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0;
 
     // first tile static, then tickets; the next ticket is taken at the start of
@@ -609,10 +610,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
     while (tile < ntiles) {
         uint32_t ticket = 0;
         if (lane == 0) ticket = atomicAdd(&a.ctrl[CTRL_TILE_NEXT], 1u);
-        const uint32_t t0 = tile * TILE;
-        const uint32_t tend = min(t0 + TILE, a.n);
+        const uint32_t t0 = tile * tt;
+        const uint32_t tend = min(t0 + tt, a.n);
         const uint32_t t = t0 + lane;
-        const bool valid = t < a.n;
+        const bool valid = lane < tt && t < a.n;
         const uint32_t wbeg = a.toff[CK_(t0, a.n + 1, 2)], wend = a.toff[CK_(tend, a.n + 1, 3)];
         const bool in_lds = (wend - wbeg) <= (uint32_t)WCAP;
         const uint32_t my_off = valid ? a.toff[CK_(t, a.n + 1, 4)] : wend;
@@ -863,7 +864,9 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
 }
 
 // Pass 1: per-block exclusive scan of count[] (slow/overflow rows included).
-__global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_local(ScanArgs a) {
+// A single-block scan (n <= SCAN_TILE: small batches) is final here: block
+// offset 0, total -> row_off[n] and *d_total, and pass 2 is not launched.
+__global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_local(ScanArgs a, uint32_t* d_total) {
     __shared__ uint32_t sh[33];
     const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER_THREAD;
     uint32_t v[SCAN_PER_THREAD];
@@ -880,7 +883,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_local(ScanArgs a) {
         if (base + i < a.n) a.row_off[base + i] = ex;
         ex += v[i];
     }
-    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
+    if (threadIdx.x == 0) {
+        if (gridDim.x == 1) {
+            a.block_sums[0] = 0;
+            a.row_off[a.n] = tot;
+            if (d_total) *d_total = tot;
+        } else {
+            a.block_sums[blockIdx.x] = tot;
+        }
+    }
 }
 
 // Pass 2: exclusive scan of the block sums (single block), total -> row_off[n].
@@ -1302,11 +1313,31 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 // emqx_topic:words/1 (src/emqx_topic.erl:150-164: binary:split on "/", '' / '+'
 // / '#' as their atoms) plus the engine's interning, on the device: the same
 // word entries (class << 29 | id), flags and generic-path list as the host
-// tokeniser (tm_engine.cpp tokenize_range).  One thread per topic; a batch is
-// a few hundred MB of bytes at most, so these kernels are a small fraction of
-// the PCIe copy that brings the bytes in.
+// tokeniser (tm_engine.cpp tokenize_range).  One wavefront per tile of 64
+// topics, whose bytes are contiguous in the batch:
+//   tm_tok_count  words per tile = '/' bytes in the tile's range + topics,
+//                 counted from coalesced dword loads (bit tricks, no per-byte
+//                 loop); also clears the launch's control words;
+//   (scan of the tile counts)
+//   tm_tok_fill   the tile's bytes are staged in LDS by coalesced loads; each
+//                 lane splits its own topic there (word starts / lengths into
+//                 an LDS list, flags, in-tile word offsets by a wave scan);
+//                 then the lanes take the tile's WORDS round-robin -- class,
+//                 reserved atoms, dictionary probe with the first 8 bytes
+//                 compared inline -- and the tile's words leave LDS as one
+//                 coalesced run.  Tiles too long for the LDS budget take a
+//                 lane-per-topic path that reads the bytes from HBM.
 
-__device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint64_t n, bool& irregular) {
+constexpr uint32_t TOK_BYTES = 4096;   // LDS bytes per tile (4-aligned window)
+constexpr uint32_t TOK_WORDS = 512;    // LDS words per tile
+
+// bytes with value v in the 4 bytes of x (SWAR): each matching byte -> 0x80
+__device__ __forceinline__ uint32_t byte_eq(uint32_t x, uint32_t v) {
+    const uint32_t y = x ^ (v * 0x01010101u);
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+
+__device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint32_t n, bool& irregular) {
     if (n == 0) return C_EMPTY;
     if (c0 == '+') {
         if (n > 1) irregular = true;
@@ -1317,95 +1348,359 @@ __device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint64_t n, bool& irre
     return C_ABOVE;
 }
 
-// pass 1: words per topic (1 + separators) and the topic flags
-__global__ __launch_bounds__(256) void tm_tok_count(TokArgs a) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.n) return;
-    const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
-    const uint8_t* p = a.bytes;
-    uint32_t words = 1;
-    bool irregular = false;
-    uint64_t ws = b;
-    for (uint64_t i = b; i < e; ++i) {
-        if (p[i] == '/') {
-            if (i - ws > 1 && p[ws] == '+') irregular = true;
-            ++words;
-            ws = i + 1;
-        }
-    }
-    if (e - ws > 1 && p[ws] == '+') irregular = true;
-    uint8_t fl = 0;
-    if (e > b && p[b] == '$') fl |= TF_DOLLAR;
-    if (irregular || words > FAST_MAX_DEPTH) fl |= TF_SLOW;
-    a.wcount[t] = words;
-    a.tflags[t] = fl;
-}
-
-__device__ __forceinline__ uint64_t load_le(const uint8_t* p, uint32_t n) {
-    uint64_t v = 0;
-    for (uint32_t k = 0; k < n; ++k) v |= (uint64_t)p[k] << (8 * k);
-    return v;
-}
-
-// id of word p[0..n) in the uploaded interner table (W_UNKNOWN if absent)
-__device__ uint32_t dict_find(const TokArgs& a, const uint8_t* p, uint32_t n) {
+// id of word p[0..n) in the uploaded interner table (W_UNKNOWN if absent);
+// P is an LDS or global byte pointer
+template <class P>
+__device__ __forceinline__ uint32_t dict_find(const TokArgs& a, P p, uint32_t n) {
     uint64_t h = hw_init(n);
     uint32_t i = 0;
-    for (; i + 8 <= n; i += 8) h = hw_mix(h, load_le(p + i, 8));
-    h = hw_final(h, load_le(p + i, n - i));
+    for (; i + 8 <= n; i += 8) {
+        uint64_t v = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v |= (uint64_t)p[i + k] << (8 * k);
+        h = hw_mix(h, v);
+    }
+    uint64_t tail = 0;
+    for (uint32_t k = 0; i + k < n; ++k) tail |= (uint64_t)p[i + k] << (8 * k);
+    h = hw_final(h, tail);
+    uint64_t head = 0, head2 = 0;
+    for (uint32_t k = 0; k < 8 && k < n; ++k) head |= (uint64_t)p[k] << (8 * k);
+    for (uint32_t k = 8; k < 16 && k < n; ++k) head2 |= (uint64_t)p[k] << (8 * (k - 8));
     uint64_t s = h & a.dict_mask;
     for (uint64_t probe = 0; probe <= a.dict_mask; ++probe) {
-        const DictEnt* e = a.dict + s;
-        const uint64_t eh = e->h;
-        if (eh == 0) return W_UNKNOWN;
-        if (eh == h && e->len == n) {
-            const uint8_t* q = a.arena + e->off;
-            uint32_t k = 0;
+        const DictEnt e = a.dict[s];
+        if (e.h == 0) return W_UNKNOWN;
+        if (e.h == h && e.len == n && e.head == head && e.head2 == head2) {
+            const uint8_t* q = a.arena + e.off;
+            uint32_t k = 16;
             while (k < n && q[k] == p[k]) ++k;
-            if (k == n) return e->id;
+            if (k >= n) return e.id;
         }
         s = (s + 1) & a.dict_mask;
     }
     return W_UNKNOWN;
 }
 
-// pass 2 (after the scan of wcount into toff): word entries + generic-path list
-__global__ __launch_bounds__(256) void tm_tok_fill(TokArgs a) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63;
-    bool slow = false;
-    if (t < a.n) {
-        const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
-        const uint8_t* p = a.bytes;
-        uint64_t o = a.toff[t] + a.bsums[t / SCAN_TILE];   // tm_scan_local is block-local
-        a.toff[t] = (uint32_t)o;
-        uint64_t ws = b;
-        for (uint64_t i = b;; ++i) {
-            if (i == e || p[i] == '/') {
-                const uint32_t n = (uint32_t)(i - ws);
-                const uint8_t c0 = n ? p[ws] : 0;
-                bool irr = false;
-                const uint32_t cls = tok_class(c0, n, irr);
-                uint32_t id;
-                if (n == 0) id = W_EMPTY;
-                else if (n == 1 && c0 == '+') id = W_PLUS;
-                else if (n == 1 && c0 == '#') id = W_HASH;
-                else id = dict_find(a, p + ws, n);
-                if (o < a.words_cap) a.words[o] = (cls << WID_BITS) | id;
-                ++o;
-                if (i == e) break;
-                ws = i + 1;
-            }
-        }
-        slow = (a.tflags[t] & TF_SLOW) != 0;
-    }
+// entry of the word p[0..n): class << 29 | id
+template <class P>
+__device__ __forceinline__ uint32_t word_entry(const TokArgs& a, P p, uint32_t n, bool& irregular) {
+    const uint8_t c0 = n ? p[0] : 0;
+    const uint32_t cls = tok_class(c0, n, irregular);
+    uint32_t id;
+    if (n == 0) id = W_EMPTY;
+    else if (n == 1 && c0 == '+') id = W_PLUS;
+    else if (n == 1 && c0 == '#') id = W_HASH;
+    else id = dict_find(a, p, n);
+    return (cls << WID_BITS) | id;
+}
+
+__device__ __forceinline__ void tok_append_slow(const TokArgs& a, bool slow, uint32_t t) {
     const uint64_t m = __ballot(slow);
     if (!m) return;
-    const uint32_t first = (uint32_t)__builtin_ctzll(m);
     uint32_t base = 0;
-    if (lane == first) base = atomicAdd(a.d_nslow, (uint32_t)__popcll(m));
-    base = __shfl(base, first, 64);
+    if ((threadIdx.x & 63) == 0) base = atomicAdd(a.d_nslow, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
     if (slow) a.slow_list[base + prefix_count(m)] = t;
+}
+
+// pass 1: words per tile
+__global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x == 0) {   // the launch's control words (kernels after this one use them)
+        if (lane < 2) a.d_nslow[lane] = 0;
+        for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
+    }
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint32_t t0 = tile * TILE, tend = min(t0 + TILE, a.n);
+        const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
+        const uint64_t a0 = b0 & ~3ull;
+        uint32_t slashes = 0;
+        for (uint64_t p = a0 + 4ull * lane; p < b1; p += 256) {
+            uint32_t x = *reinterpret_cast<const uint32_t*>(a.bytes + p);
+            uint32_t m = byte_eq(x, '/');
+            // drop bytes outside [b0, b1)
+            if (p < b0) m &= ~0u << (8 * (uint32_t)(b0 - p));
+            if (p + 4 > b1) m &= (1u << (8 * (uint32_t)(b1 - p))) - 1u;
+            slashes += __popc(m);
+        }
+        for (int o = 32; o > 0; o >>= 1) slashes += __shfl_xor(slashes, o, 64);
+        if (lane == 0) a.wcount[tile] = slashes + (tend - t0);
+    }
+}
+
+struct alignas(16) TokLds {
+    uint8_t bytes[TOK_BYTES + 16];   // + 16: 8-byte reads past a word stay in the array
+    uint32_t wpos[TOK_WORDS];        // start (in bytes[]) | len << 16
+    uint32_t out[TOK_WORDS];
+};
+
+// 8 bytes at byte offset s of a 4-aligned LDS array (any alignment of s)
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t* base, uint32_t s) {
+    const uint32_t a = s & ~3u, sh = (s & 3u) * 8u;
+    const uint32_t d0 = *reinterpret_cast<const uint32_t*>(base + a);
+    const uint32_t d1 = *reinterpret_cast<const uint32_t*>(base + a + 4);
+    const uint32_t d2 = *reinterpret_cast<const uint32_t*>(base + a + 8);
+    const uint64_t lo = ((uint64_t)d1 << 32) | d0;
+    return sh ? (lo >> sh) | ((uint64_t)d2 << (64u - sh)) : lo;
+}
+
+__device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // first k (< 8) bytes of v
+    return k >= 8 ? v : (v & ((1ull << (8u * k)) - 1ull));
+}
+
+#ifndef TM_TOK_WPL
+#define TM_TOK_WPL 4
+#endif
+constexpr uint32_t TOK_WPL = TM_TOK_WPL;   // words per lane per lookup round (register budget: occupancy)
+
+// Dictionary ids of the tile's words w = lane + 64 k: TOK_WPL words per lane
+// at a time, their hashes and heads from LDS first, then one probe round per
+// collision-chain step with every pending probe of the lane in flight.
+__device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
+        uint64_t h[TOK_WPL], head[TOK_WPL], head2[TOK_WPL];
+        uint32_t slot[TOK_WPL], ent[TOK_WPL];
+        bool pend[TOK_WPL];
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_WPL; ++k) {
+            const uint32_t w = base + lane + 64 * k;
+            pend[k] = false;
+            ent[k] = 0;
+            h[k] = head[k] = head2[k] = 0;
+            slot[k] = 0;
+            if (w >= tw) continue;
+            const uint32_t wp = L.wpos[w];
+            const uint32_t s0 = wp & 0xFFFF, n = wp >> 16;
+            const uint8_t c0 = n ? L.bytes[s0] : 0;
+            bool irr = false;
+            const uint32_t cls = tok_class(c0, n, irr);
+            ent[k] = cls << WID_BITS;
+            if (n == 0) { ent[k] |= W_EMPTY; continue; }
+            if (n == 1 && c0 == '+') { ent[k] |= W_PLUS; continue; }
+            if (n == 1 && c0 == '#') { ent[k] |= W_HASH; continue; }
+            const uint64_t c0w = lds_u64(L.bytes, s0), c1w = lds_u64(L.bytes, s0 + 8);
+            uint64_t hh = hw_init(n);
+            if (n >= 8) hh = hw_mix(hh, c0w);
+            if (n >= 16) hh = hw_mix(hh, c1w);
+            uint32_t i = 16;
+            for (; i + 8 <= n; i += 8) hh = hw_mix(hh, lds_u64(L.bytes, s0 + i));
+            const uint32_t done = n < 8 ? 0 : n < 16 ? 8 : i;
+            const uint64_t tw8 = done == 0 ? c0w : done == 8 ? c1w : lds_u64(L.bytes, s0 + done);
+            hh = hw_final(hh, done < n ? low_bytes(tw8, n - done) : 0ull);
+            h[k] = hh;
+            head[k] = low_bytes(c0w, n < 8 ? n : 8);
+            head2[k] = n > 8 ? low_bytes(c1w, n - 8 < 8 ? n - 8 : 8) : 0ull;
+            slot[k] = (uint32_t)(hh & a.dict_mask);
+            pend[k] = true;
+        }
+        for (uint64_t round = 0; round <= a.dict_mask; ++round) {
+            bool any = false;
+            uint4 e0[TOK_WPL], e1[TOK_WPL];   // {h, head}, {head2, len, id}
+#pragma unroll
+            for (uint32_t k = 0; k < TOK_WPL; ++k)
+                if (pend[k]) {
+                    const uint4* ep = reinterpret_cast<const uint4*>(a.dict + slot[k]);
+                    e0[k] = ep[0];
+                    e1[k] = ep[1];
+                }
+#pragma unroll
+            for (uint32_t k = 0; k < TOK_WPL; ++k) {
+                if (!pend[k]) continue;
+                const uint64_t eh = ((uint64_t)e0[k].y << 32) | e0[k].x;
+                const uint64_t ehead = ((uint64_t)e0[k].w << 32) | e0[k].z;
+                const uint64_t ehead2 = ((uint64_t)e1[k].y << 32) | e1[k].x;
+                if (eh == 0) {                 // not in the dictionary: W_UNKNOWN (0)
+                    pend[k] = false;
+                    continue;
+                }
+                const uint32_t wp = L.wpos[base + lane + 64 * k];
+                const uint32_t n = wp >> 16;
+                if (eh == h[k] && e1[k].z == n && ehead == head[k] && ehead2 == head2[k]) {
+                    bool eq = true;
+                    if (n > 16) {   // rare: bytes 16.. from the arena
+                        const uint8_t* q = a.arena + a.dict[slot[k]].off;
+                        for (uint32_t i = 16; i < n && eq; ++i) eq = q[i] == L.bytes[(wp & 0xFFFF) + i];
+                    }
+                    if (eq) {
+                        ent[k] |= e1[k].w;
+                        pend[k] = false;
+                        continue;
+                    }
+                }
+                slot[k] = (uint32_t)((slot[k] + 1) & a.dict_mask);
+                any = true;
+            }
+            if (!__any(any)) break;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_WPL; ++k)
+            if (base + lane + 64 * k < tw) L.out[base + lane + 64 * k] = ent[k];
+    }
+}
+
+// lane-per-topic path of a tile too long for the LDS budget: bytes from HBM
+__device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t t, uint64_t o, bool& slow) {
+    const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
+    const uint8_t* p = a.bytes;
+    bool irregular = false;
+    uint32_t nw = 0;
+    uint64_t ws = b;
+    for (uint64_t i = b;; ++i) {
+        if (i == e || p[i] == '/') {
+            const uint32_t w = word_entry(a, p + ws, (uint32_t)(i - ws), irregular);
+            if (o < a.words_cap) a.words[o] = w;
+            ++o;
+            ++nw;
+            if (i == e) break;
+            ws = i + 1;
+        }
+    }
+    uint8_t fl = 0;
+    if (e > b && p[b] == '$') fl |= TF_DOLLAR;
+    if (irregular || nw > FAST_MAX_DEPTH) fl |= TF_SLOW;
+    a.tflags[t] = fl;
+    slow = (fl & TF_SLOW) != 0;
+}
+
+// pass 2 (after the scan of the tile counts): word entries, offsets, flags
+#ifndef TM_TOK_WPE
+#define TM_TOK_WPE 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
+    __shared__ TokLds L;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint32_t t0 = tile * TILE, tend = min(t0 + TILE, a.n), cnt = tend - t0;
+        const uint32_t t = t0 + lane;
+        const bool valid = lane < cnt;
+        // everything that does not depend on the tile's bytes is loaded first
+        const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
+        const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
+        const uint64_t my_b = valid ? a.offs[t] - a.base : 0, my_e = valid ? a.offs[t + 1] - a.base : 0;
+        const uint64_t a0 = b0 & ~3ull;
+        bool slow = false;
+        if (b1 - a0 <= TOK_BYTES) {
+            // stage the tile's bytes (4-aligned window starting at a0): every
+            // load of the lane in flight before the first LDS store
+            constexpr uint32_t PER_LANE = TOK_BYTES / 256;
+            uint32_t v[PER_LANE];
+#pragma unroll
+            for (uint32_t k = 0; k < PER_LANE; ++k) {
+                const uint64_t p = a0 + 4ull * (lane + 64 * k);
+                v[k] = p < b1 ? *reinterpret_cast<const uint32_t*>(a.bytes + p) : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < PER_LANE; ++k) {
+                const uint64_t p = a0 + 4ull * (lane + 64 * k);
+                if (p < b1) *reinterpret_cast<uint32_t*>(L.bytes + (p - a0)) = v[k];
+            }
+            __syncthreads();
+            // split my topic in LDS: '/' found four bytes at a time (SWAR)
+            uint32_t tb = 0, te = 0, nw = 0;
+            if (valid) {
+                tb = (uint32_t)(my_b - a0);
+                te = (uint32_t)(my_e - a0);
+                nw = 1;
+                for (uint32_t q = tb & ~3u; q < te; q += 4) {
+                    uint32_t m = byte_eq(*reinterpret_cast<const uint32_t*>(L.bytes + q), '/');
+                    if (q < tb) m &= ~0u << (8u * (tb - q));
+                    if (q + 4 > te) m &= (1u << (8u * (te - q))) - 1u;
+                    nw += __popc(m);
+                }
+            }
+            uint32_t incl = nw;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += u;
+            }
+            const uint32_t tw = __shfl(incl, 63, 64);
+            const uint32_t woff = incl - nw;
+            if (tw <= TOK_WORDS) {
+                if (valid) {
+                    bool irregular = false;
+                    uint32_t k = woff, ws = tb;
+                    for (uint32_t q = tb & ~3u; q < te; q += 4) {
+                        uint32_t m = byte_eq(*reinterpret_cast<const uint32_t*>(L.bytes + q), '/');
+                        if (q < tb) m &= ~0u << (8u * (tb - q));
+                        if (q + 4 > te) m &= (1u << (8u * (te - q))) - 1u;
+                        while (m) {
+                            const uint32_t pos = q + (__builtin_ctz(m) >> 3);
+                            m &= m - 1;
+                            L.wpos[k++] = ws | ((pos - ws) << 16);
+                            if (pos - ws > 1 && L.bytes[ws] == '+') irregular = true;
+                            ws = pos + 1;
+                        }
+                    }
+                    L.wpos[k] = ws | ((te - ws) << 16);
+                    if (te - ws > 1 && L.bytes[ws] == '+') irregular = true;
+                    uint8_t fl = 0;
+                    if (te > tb && L.bytes[tb] == '$') fl |= TF_DOLLAR;
+                    if (irregular || nw > FAST_MAX_DEPTH) fl |= TF_SLOW;
+                    a.tflags[t] = fl;
+                    a.toff[t] = (uint32_t)(tile_base + woff);
+                    slow = (fl & TF_SLOW) != 0;
+                }
+                __syncthreads();
+                tok_lookup(a, L, tw);            // the tile's words, round-robin over lanes
+                __syncthreads();
+                for (uint32_t w = lane; w < tw; w += 64)
+                    if (tile_base + w < a.words_cap) a.words[tile_base + w] = L.out[w];
+                if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
+                tok_append_slow(a, slow, t);
+                __syncthreads();
+                continue;
+            }
+        }
+        // long tile: one lane per topic, bytes from HBM; in-tile offsets by a
+        // wave scan of the per-topic word counts ('/' + 1)
+#ifdef TOK_NO_FALLBACK
+        continue;
+#endif
+        uint32_t nw = 0;
+        if (valid) {
+            const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
+            nw = 1;
+            for (uint64_t i = b; i < e; ++i) nw += a.bytes[i] == '/';
+        }
+        uint32_t incl = nw;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += u;
+        }
+        const uint64_t o = tile_base + incl - nw;
+        if (valid) {
+            a.toff[t] = (uint32_t)o;
+            tok_fill_topic_global(a, t, o, slow);
+        }
+        if (tend == a.n && lane == 63) a.toff[a.n] = (uint32_t)(tile_base + incl);
+        tok_append_slow(a, slow, t);
+        __syncthreads();
+    }
+}
+
+// Read-back of an async batch in ONE kernel, written straight into pinned host
+// memory: the header block's first hdr_words (ctrl + stats + src), the counts,
+// and exactly the staging entries the walk reserved (ctrl's u64 ticket; the
+// host checks it against rows_cap) -- instead of three DMA copies, one of them
+// sized by a guess.
+__global__ __launch_bounds__(256) void tm_export_host(ExportArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (uint64_t i = i0; i < a.hdr_words; i += stride) a.h_hdr[i] = a.hdr[i];
+    for (uint64_t i = i0; i < a.n; i += stride) a.h_count[i] = a.count[i];
+    const uint64_t top = *reinterpret_cast<const unsigned long long*>(a.hdr + CTRL_STAGING64);
+    const uint64_t rows = top < a.rows_cap ? top : a.rows_cap;
+    for (uint64_t i = i0; i < rows; i += stride) a.h_rows[i] = a.rows[i];
+}
+
+hipError_t launch_export_host(const ExportArgs& a, hipStream_t s) {
+    const uint64_t work = a.hdr_words + a.n + a.rows_cap;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((work / 4 + 255) / 256, 1), 512);
+    hipLaunchKernelGGL(tm_export_host, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 __global__ void tm_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n) {
@@ -1415,10 +1710,21 @@ __global__ void tm_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt
 
 // ------------------------------------------------------------ launchers
 
+// Topics per tile: 64 (one per lane) for large batches; small batches use
+// fewer per wave so that they spread over >= ~2048 waves -- a tile's latency
+// is its probe count / 64 iterations, so one topic per wave walks in about
+// depth dependent rounds instead of the 64 topics' combined frontier.
+uint32_t tile_topics(uint32_t n) {
+    uint32_t tt = 64;
+    while (tt > 1 && (n + tt - 1) / tt < 2048) tt >>= 1;
+    return tt;
+}
+
 uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
     static uint32_t cap[64][2] = {};
     const int qi = qcap <= 384 ? 0 : 1;
-    const uint32_t ntiles = (n + TILE - 1) / TILE;
+    const uint32_t tt = tile_topics(n);
+    const uint32_t ntiles = (n + tt - 1) / tt;
     uint32_t c = (device >= 0 && device < 64) ? cap[device][qi] : 0u;
     if (!c) {
         int per_cu = 0, cus = 0;
@@ -1442,7 +1748,7 @@ uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
 
 template <bool CK, bool BIG>
 static void launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
-    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
     if (ev_a) (void)hipEventRecord(ev_a, s);
     if (ntiles) {
         const uint32_t grid = a.grid;
@@ -1463,7 +1769,11 @@ hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipE
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total) {
     const uint32_t nb = scan_block_count(a.n);
-    if (nb) hipLaunchKernelGGL(tm_scan_local, dim3(nb), dim3(SCAN_BLOCK), 0, s, a);
+    if (nb <= 1) {
+        hipLaunchKernelGGL(tm_scan_local, dim3(1), dim3(SCAN_BLOCK), 0, s, a, d_total);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(tm_scan_local, dim3(nb), dim3(SCAN_BLOCK), 0, s, a, (uint32_t*)nullptr);
     hipLaunchKernelGGL(tm_scan_sums, dim3(1), dim3(SCAN_BLOCK), 0, s, a, nb, d_total);
     return hipGetLastError();
 }
@@ -1562,17 +1872,18 @@ hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* 
 }
 
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
+    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    const uint32_t grid = ntiles ? min(ntiles, 256u * 32u) : 1u;
+    hipLaunchKernelGGL(tm_tok_count, dim3(grid), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
     if (!a.n) return hipGetLastError();
-    const uint32_t g = (a.n + 255) / 256;
-    hipLaunchKernelGGL(tm_tok_count, dim3(g), dim3(256), 0, s, a);
     scan.count = a.wcount;
-    scan.row_off = a.toff;
-    scan.n = a.n;
+    scan.row_off = a.wcount;   // in place: tile counts -> block-local tile offsets
+    scan.n = ntiles;
     const hipError_t e = launch_scan(scan, s, d_nwords);
     if (e != hipSuccess) return e;
     TokArgs f = a;
     f.bsums = scan.block_sums;
-    hipLaunchKernelGGL(tm_tok_fill, dim3(g), dim3(256), 0, s, f);
+    hipLaunchKernelGGL(tm_tok_fill, dim3(grid), dim3(64), 0, s, f);
     return hipGetLastError();
 }
 

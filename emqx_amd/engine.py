@@ -343,6 +343,32 @@ class Engine:
                 return list(ids[:n.value])
             cap = n.value
 
+    def match_async(self, topic: bytes, done):
+        """tm_match_async: done(rc, ids list) runs on the engine's completion
+        thread.  The ctypes callback object is kept alive until it has run."""
+        keep = getattr(self, "_async_keep", None)
+        if keep is None:
+            keep = self._async_keep = {}
+
+        def cb(ctx, rc, ids, n, _key=[None]):
+            try:
+                done(rc, [ids[i] for i in range(n)] if rc == 0 else None)
+            finally:
+                keep.pop(_key[0], None)
+        c = N.MATCH_CB(cb)
+        key = id(c)
+        cb.__defaults__[0][0] = key
+        keep[key] = c
+        rc = self.L.tm_match_async(self.h, topic, len(topic), c, None)
+        if rc:
+            keep.pop(key, None)
+        N.check(rc, "tm_match_async")
+
+    def async_stats(self) -> dict:
+        st = N.AsyncStats()
+        N.check(self.L.tm_async_stats_get(self.h, C.byref(st)), "tm_async_stats_get")
+        return st.asdict()
+
     def coalesce_config(self, max_batch: int = 0, linger_us: int = N.TM_NONE):
         """-> (batches, requests) served by tm_match_coalesced so far."""
         b, r = C.c_uint64(), C.c_uint64()
@@ -530,6 +556,16 @@ class Engine:
         if not p:
             raise KeyError(fid)
         return C.string_at(p, n.value)
+
+    def filter_copy(self, fid: int) -> bytes:
+        """tm_filter_copy: the filter's bytes copied under the engine lock."""
+        n = C.c_size_t()
+        buf = C.create_string_buffer(N.TM_MAX_TOPIC_LEN + 1)
+        rc = self.L.tm_filter_copy(self.h, fid, buf, len(buf), C.byref(n))
+        if rc == N.TM_ENOENT:
+            raise KeyError(fid)
+        N.check(rc, "tm_filter_copy")
+        return buf.raw[:n.value]
 
     def filter_id(self, f: bytes) -> int:
         out = C.c_uint32()

@@ -144,11 +144,41 @@ TM_API int  tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len,
  * errors as tm_trie_match, per caller (len > TM_MAX_TOPIC_LEN -> TM_EINVAL). */
 TM_API int  tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len,
                                uint32_t* ids, uint32_t cap, uint32_t* n_out);
-/* Sets max_batch (0 = keep; default 65536) and linger_us (TM_NONE = keep;
- * default 0: the batch is whoever queued while the previous one ran); *batches / *requests (may be NULL) = coalesced batches run and
- * requests served so far. */
+/* Sets max_batch (0 = keep; default 16384) and linger_us (TM_NONE = keep;
+ * default 0: a batch is whatever queued while the pipeline was busy) of the
+ * async pipeline below, which tm_match_coalesced rides on; *batches /
+ * *requests (may be NULL) = device batches run and requests served so far. */
 TM_API int  tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us,
                                uint64_t* batches, uint64_t* requests);
+
+/* Asynchronous emqx_trie:match/1 for one topic -- the form the NIF uses:
+ * the caller (an Erlang process) returns at once and receives its row later
+ * (enif_send), so every publishing process can have a match in flight, as
+ * every publisher runs match_routes/1 concurrently in the reference
+ * (src/emqx_broker.erl:201-210).  Calls are queued; an engine thread forms
+ * device batches from the queue (emqx_batch's size + linger policy,
+ * src/emqx_batch.erl:49-90) and keeps up to `depth` of them in flight, each on
+ * a HIP stream of its own: H2D of the topics, device tokeniser, trie walk,
+ * read-back of the rows.  cb(ctx, rc, ids, n) runs once per call on the
+ * engine's completion thread: rc 0 and the topic's sorted filter ids
+ * (engine memory, valid during the callback only), or a TM_E* code with no
+ * ids.  A match submitted after tm_trie_insert returned sees the filter.
+ * Returns TM_EINVAL (no callback) for len > TM_MAX_TOPIC_LEN; callbacks must
+ * not destroy the engine. */
+typedef void (*tm_match_cb)(void* ctx, int rc, const uint32_t* ids, uint32_t n);
+TM_API int  tm_match_async(tm_engine* e, const uint8_t* topic, size_t len, tm_match_cb cb, void* ctx);
+typedef struct {
+    uint64_t batches;       /* device batches completed */
+    uint64_t requests;      /* calls completed */
+    uint64_t recoveries;    /* batches re-run through the CSR path (capacity misses) */
+    uint64_t max_batch;     /* largest batch formed */
+    uint32_t depth;         /* batches in flight at most (TM_ASYNC_DEPTH, default 3) */
+    uint32_t queued;        /* calls waiting for a batch now */
+    double   us_launch;     /* host time forming + enqueueing batches (launcher thread) */
+    double   us_wait;       /* completer time blocked on device batches */
+    double   us_deliver;    /* completer time running callbacks */
+} tm_async_stats;
+TM_API int  tm_async_stats_get(tm_engine* e, tm_async_stats* out);
 
 /* ---- batched publish matching: emqx_router:match_routes/1 hot path ---- */
 /* (src/emqx_router.erl:127-141 applied to a batch of publishes,
@@ -349,8 +379,14 @@ TM_API int  tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d
                            uint32_t n, const int64_t* d_dst_off, uint32_t* d_dst);
 
 /* ---- filters ---------------------------------------------------------- */
-/* Bytes of a filter id returned by a match (the #trie_node.topic binary). */
+/* Bytes of a filter id returned by a match (the #trie_node.topic binary).
+ * The pointer is into engine memory that a later insert may move: callers
+ * racing with writers use tm_filter_copy. */
 TM_API const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len);
+/* Copies the bytes of filter `id` into buf[cap] under the engine lock; *len =
+ * its length (copied only if <= cap).  TM_ENOENT if the id is not a live
+ * filter (deleted since the match that returned it). */
+TM_API int  tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len);
 /* Id of an inserted filter, TM_ENOENT if absent. */
 TM_API int  tm_filter_id(tm_engine* e, const uint8_t* filter, size_t len, uint32_t* id);
 

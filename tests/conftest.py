@@ -5,6 +5,17 @@ import sys
 
 import pytest
 
+# One HIP runtime per process: torch bundles its own libamdhip64 /
+# libhsa-runtime64 (ROCm 7.0), the engine links /opt/rocm's (7.2).  Loading
+# torch after the engine maps a second HSA runtime and torch's GPU init fails
+# ("No HIP GPUs are available"); importing torch first makes the
+# engine bind to torch's already-loaded runtime.  GPU tests that exchange
+# tensors with the engine rely on this, whatever subset of tests runs.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TESTS = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(TESTS, "golden")

@@ -1,6 +1,6 @@
-"""tm_match_coalesced on a host-only engine: the leader/follower hand-off
-completes for many concurrent callers and every caller gets its own error
-(no device -> TM_ENODEV, too long -> TM_EINVAL), none hangs."""
+"""The per-publish ABI on a host-only engine: every call returns at once with
+its own error (no device -> TM_ENODEV, longer than ?MAX_TOPIC_LEN -> TM_EINVAL),
+none hangs, and no device batch is formed."""
 
 import threading
 
@@ -35,5 +35,26 @@ def test_concurrent_callers_all_return_their_error():
     assert all(not t.is_alive() for t in ths)
     assert len(rcs) == 600
     assert all(rc == (N.TM_EINVAL if bad else N.TM_ENODEV) for bad, rc in rcs)
-    batches, requests = eng.coalesce_config()
-    assert requests == sum(1 for bad, _ in rcs if not bad) and 0 < batches <= requests
+    assert eng.coalesce_config() == (0, 0)
+
+
+def test_async_refused_without_device():
+    eng = Engine(device=-1)
+    with pytest.raises(N.TmError) as ei:
+        eng.match_async(b"a/b", lambda rc, ids: None)
+    assert ei.value.rc == N.TM_ENODEV
+    with pytest.raises(N.TmError) as ei:
+        eng.match_async(b"x" * (N.TM_MAX_TOPIC_LEN + 1), lambda rc, ids: None)
+    assert ei.value.rc == N.TM_EINVAL
+    st = eng.async_stats()
+    assert st["batches"] == 0 and st["requests"] == 0
+
+
+def test_filter_copy_host_engine():
+    eng = Engine(device=-1)
+    eng.insert(b"a/+/#")
+    fid = eng.filter_id(b"a/+/#")
+    assert eng.filter_copy(fid) == b"a/+/#"
+    eng.delete(b"a/+/#")
+    with pytest.raises(KeyError):
+        eng.filter_copy(fid)
