@@ -278,17 +278,32 @@ def run_c5(args, ws, rank, local, sync):
         b.launch().wait()
     if sync is not None:
         sync.barrier()
-    # the deltas are drawn before timing; applying them (trie ops + the device
-    # delta upload inside launch) is inside each step
-    deltas = [churn.step(args.c5_deltas) for _ in range(args.steps)]
+    # The deltas are drawn before timing, as packed binaries (what the NIF's
+    # route_apply hands over).  Step i applies deltas i (emqx_trie:delete/1 and
+    # insert/1 on the host mirror) and matches batch i against the result.
+    # Pipelined: the host applies deltas i + 1 while the device walks batch i
+    # -- the host mirror and the HBM replica are separate, and launch i + 1
+    # uploads deltas i + 1 (read-your-writes) -- so the step costs
+    # max(apply, device) rather than their sum.
+    deltas = []
+    for _ in range(args.steps):
+        dels, adds = churn.step(args.c5_deltas)
+        deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
     ms_match, ms_churn = [], []
     t0 = time.perf_counter()
-    for dels, adds in deltas:
-        tc = time.perf_counter()
-        Churn.apply(eng, dels, adds)
-        ms_churn.append(1e3 * (time.perf_counter() - tc))
-        b.launch().wait()
+    tc = time.perf_counter()
+    Churn.apply(eng, *deltas[0])
+    ms_churn.append(1e3 * (time.perf_counter() - tc))
+    b.launch()
+    for i in range(args.steps):
+        if i + 1 < args.steps:
+            tc = time.perf_counter()
+            Churn.apply(eng, *deltas[i + 1])
+            ms_churn.append(1e3 * (time.perf_counter() - tc))
+        b.wait()
         ms_match.append(b.stats()["ms_total"])
+        if i + 1 < args.steps:
+            b.launch()
     elapsed = time.perf_counter() - t0
     if sync is not None:
         sync.barrier()
@@ -316,6 +331,7 @@ def run_c5(args, ws, rank, local, sync):
                    "filters": len(allf), "distinct_topics": int(n_rows), "mode": "replicated, dedup batches"},
         "device_pipeline_ms": float(np.mean(ms_match)),
         "churn_apply_ms": float(np.mean(ms_churn)),
+        "churn_overlapped_with_device": True,
         "matches_delivered_per_step": delivered,
         "generic_path_topics": int(st["slow_topics"]),
         "uploads_delta": eng.stats()["uploads_delta"],

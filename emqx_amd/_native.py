@@ -170,6 +170,7 @@ SIGNATURES = {
     "tm_group_batch_stats": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_group_batch_free": (None, [P, P]),
     "tm_group_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_debug_check": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),
     "tm_device_count": (C.c_int, []),

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <set>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -52,17 +53,36 @@ char* last_error() {
 }
 
 // word hash (tm_internal.hpp hw_*; the device tokeniser computes the same)
+inline uint64_t hash_word(const uint8_t* p, size_t n) {
+    uint32_t h = HW_SEED;
+    size_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint32_t v;
+        memcpy(&v, p + i, 4);
+        h = hw_step(h, v);
+    }
+    if (i < n) {
+        uint32_t t = 0;
+        for (size_t k = 0; i + k < n; ++k) t |= (uint32_t)p[i + k] << (8 * k);
+        h = hw_step(h, t);
+    }
+    return hw_final(h, (uint32_t)n);
+}
+
+// 64-bit hash of a whole topic (TM_BATCH_DEDUP)
 inline uint64_t hash_bytes(const uint8_t* p, size_t n) {
-    uint64_t h = hw_init(n);
+    uint64_t h = 0xcbf29ce484222325ull ^ (n * 0x9E3779B97F4A7C15ull);
     size_t i = 0;
     for (; i + 8 <= n; i += 8) {
         uint64_t v;
         memcpy(&v, p + i, 8);
-        h = hw_mix(h, v);
+        h = (h ^ (v * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+        h ^= h >> 29;
     }
     uint64_t t = 0;
     for (size_t k = 0; i < n; ++i, ++k) t |= (uint64_t)p[i] << (8 * k);
-    return hw_final(h, t);
+    h = (h ^ (t * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+    return h ^ (h >> 31);
 }
 
 // ------------------------------------------------------------- word interner
@@ -74,7 +94,7 @@ class WordDict {
     WordDict() { rehash(1024); }
 
     uint32_t find(const uint8_t* p, size_t n) const {
-        const uint64_t h = hash_bytes(p, n);
+        const uint64_t h = hash_word(p, n);
         size_t i = h & mask_;
         for (;;) {
             const DictEnt& e = tab_[i];
@@ -89,7 +109,7 @@ class WordDict {
         if (id != W_UNKNOWN) return id;
         if ((count_ + 1) * 2 > tab_.size()) rehash(tab_.size() * 2);
         id = next_id_++;
-        const uint64_t h = hash_bytes(p, n);
+        const uint64_t h = hash_word(p, n);
         size_t i = h & mask_;
         while (tab_[i].h) i = (i + 1) & mask_;
         tab_[i] = DictEnt{h, le_bytes(p, (uint32_t)std::min<size_t>(n, 8)),
@@ -263,6 +283,7 @@ struct tm_batch {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool launched = false, done = false;
     bool csr = true;   // the last launch built the CSR (false: async, rows left in staging)
+    uint64_t seq = 0;  // launch sequence number while its results may be read (0: none)
     uint64_t total = 0;
     tm_batch_stats st{};
     ScanArgs scan_args{};
@@ -425,6 +446,16 @@ struct tm_engine {
     std::vector<uint64_t> n_foff;
     std::vector<uint8_t> n_live, n_topic;
     std::vector<uint32_t> free_nodes;
+    // A freed node id (== filter id) is not reused while a batch launched
+    // before the free may still hand it out: results are read (ids mapped to
+    // filter bytes) after the walk, possibly after later deletes, and a
+    // recycled id would name another filter.  Batches hold their launch
+    // sequence number from launch until re-launch or free; an id freed at
+    // sequence L returns to free_nodes once every live batch is newer than L.
+    std::deque<std::pair<uint64_t, uint32_t>> pending_free;
+    std::multiset<uint64_t> live_launches;
+    uint64_t launch_seq = 0;
+    std::vector<uint8_t> n_hasbytes;   // n_foff / n_flen name this id's filter (until the id is reused)
     uint64_t live_nodes = 0, live_edges = 0, n_filters = 0;
     std::vector<uint8_t> fbytes;
 
@@ -535,9 +566,9 @@ struct tm_engine {
         for (uint32_t i = 0;; ++i) {
             for (uint32_t s = 0; s < BUCKET; ++s) {
                 Slot& e = tab[b * BUCKET + s];
-                if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) {
+                if (e.parent == SLOT_EMPTY) {
                     disp = i;
-                    was_empty = e.parent == SLOT_EMPTY;
+                    was_empty = true;
                     return b * BUCKET + s;
                 }
             }
@@ -592,28 +623,117 @@ struct tm_engine {
         return i;
     }
 
-    void delete_edge_of(uint32_t c) {
-        const uint32_t i = n_inslot[c];
-        Slot& e = slots[i];
+    // Removes the edge into c without tombstones.  The table keeps two
+    // invariants the lookups (host find_slot, the kernels' probes) rely on:
+    // a bucket's slots fill in order, and every key stored in bucket c with
+    // home bucket h has all of [h, c) full -- so a bucket with a free last slot
+    // ends every probe run through it.  The hole is closed by compacting its
+    // bucket and pulling back the nearest later key whose run crosses it
+    // (backward-shift deletion at bucket granularity); churn then leaves probe
+    // runs as short as a fresh build's instead of lengthening them with
+    // tombstones until a full rebuild.
+    void move_slot(uint32_t to, uint32_t from) {
+        slots[to] = slots[from];
+        n_inslot[slots[to].child & ID_MASK] = to;
+        Slot& e = slots[from];
         memset(&e, 0, sizeof(e));
-        e.parent = SLOT_TOMB;
-        e.word = 0;
+        e.parent = SLOT_EMPTY;
+        mark_dirty(to);
+        mark_dirty(from);
+    }
+
+    // compacts bucket b after slot i was emptied; returns the bucket's
+    // (now last) free slot
+    uint32_t compact_bucket(uint32_t b, uint32_t i) {
+        uint32_t last = b * BUCKET + BUCKET - 1;
+        while (last > i && slots[last].parent == SLOT_EMPTY) --last;
+        if (last > i) {
+            move_slot(i, last);
+            return last;
+        }
+        return i;
+    }
+
+    void delete_edge_of(uint32_t c) {
+        uint32_t i = n_inslot[c];
         n_inslot[c] = NONE;
         --live_edges;
-        mark_dirty(i);
+        --used_slots;
+        const uint32_t nb = nbuckets();
+        uint32_t hb = i / BUCKET;
+        const bool was_full = slots[hb * BUCKET + BUCKET - 1].parent != SLOT_EMPTY;
+        {
+            Slot& e = slots[i];
+            memset(&e, 0, sizeof(e));
+            e.parent = SLOT_EMPTY;
+            mark_dirty(i);
+        }
+        uint32_t hole = compact_bucket(hb, i);
+        if (!was_full) return;   // no run crossed hb
+        uint32_t cb = hb;
+        // a key crossing the hole lives at most max_disp buckets past it
+        for (uint32_t dist = 1; dist <= max_disp + 1; ++dist) {
+            cb = (cb + 1 == nb) ? 0 : cb + 1;
+            bool moved = false;
+            for (uint32_t k = 0; k < BUCKET; ++k) {
+                const uint32_t j = cb * BUCKET + k;
+                const Slot& e = slots[j];
+                if (e.parent == SLOT_EMPTY) break;
+                const uint32_t h = home_bucket(e.parent, e.word, nb);
+                // the run of e goes h .. cb; it crosses hb iff hb lies in [h, cb)
+                const uint32_t dist_e = (cb + nb - h) % nb, dist_hole = (cb + nb - hb) % nb;
+                if (dist_e >= dist_hole) {
+                    const bool cb_full = slots[cb * BUCKET + BUCKET - 1].parent != SLOT_EMPTY;
+                    move_slot(hole, j);
+                    hole = compact_bucket(cb, j);
+                    hb = cb;
+                    dist = 0;   // the hole moved: measure from here
+                    moved = true;
+                    if (!cb_full) return;   // cb had room: nothing beyond it crossed it
+                    break;
+                }
+            }
+            if (!moved && slots[cb * BUCKET + BUCKET - 1].parent == SLOT_EMPTY) return;   // runs end here
+        }
     }
 
     // ------------------------------------------------------------ nodes
     bool node_capacity_left() const { return !free_nodes.empty() || n_parent.size() < MAX_NODES; }
 
+    void release_pending_ids() {
+        const uint64_t watermark = live_launches.empty() ? ~0ull : *live_launches.begin();
+        while (!pending_free.empty() && pending_free.front().first < watermark) {
+            free_nodes.push_back(pending_free.front().second);
+            pending_free.pop_front();
+        }
+    }
+
+    // batch b's ids stay valid from this launch until its next launch or free
+    void note_launch(tm_batch* b) {
+        forget_launch(b);
+        b->seq = ++launch_seq;
+        live_launches.insert(b->seq);
+    }
+    void forget_launch(tm_batch* b) {
+        if (!b->seq) return;
+        auto it = live_launches.find(b->seq);
+        if (it != live_launches.end()) live_launches.erase(it);
+        b->seq = 0;
+    }
+
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
-        if (!free_nodes.empty()) { id = free_nodes.back(); free_nodes.pop_back(); }
+        if (free_nodes.empty()) release_pending_ids();
+        if (!free_nodes.empty()) {
+            id = free_nodes.back();
+            free_nodes.pop_back();
+            n_hasbytes[id] = 0;
+        }
         else {
             id = (uint32_t)n_parent.size();
             n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
             n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
-            n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
+            n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0); n_hasbytes.push_back(0);
         }
         n_parent[id] = parent; n_word[id] = word; n_ec[id] = 0; n_plus[id] = NONE; n_hash[id] = NONE;
         n_inslot[id] = NONE; n_live[id] = 1; n_topic[id] = 0;
@@ -632,7 +752,7 @@ struct tm_engine {
         n_topic[id] = 0;
         n_ec[id] = 0;
         --live_nodes;
-        if (id != ROOT) free_nodes.push_back(id);
+        if (id != ROOT) pending_free.emplace_back(launch_seq, id);
     }
 
     uint32_t summary_flags(uint32_t c) const {
@@ -666,6 +786,7 @@ struct tm_engine {
 
     void set_topic(uint32_t c, const uint8_t* bytes, size_t len) {
         n_topic[c] = 1;
+        n_hasbytes[c] = 1;
         ++n_filters;
         n_foff[c] = fbytes.size();
         n_flen[c] = (uint32_t)len;
@@ -701,6 +822,52 @@ struct tm_engine {
             ids.push_back(id);
         }
         return true;
+    }
+
+    // Bulk mutations (tm_trie_insert_many / delete_many, the churn path) walk
+    // a chunk of filters level by level first, every probe of a level
+    // prefetched before any is read, so the chunk's cache misses on the
+    // (hundreds-of-MB) edge hash overlap instead of costing one memory round
+    // trip per level per filter; the sequential insert / delete pass that
+    // follows finds the lines in cache.  Read-only: results are discarded.
+    static constexpr uint32_t WARM = 32;
+    void warm_paths(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi) {
+        static thread_local std::vector<uint32_t> ids[WARM];
+        uint32_t node[WARM], depth[WARM];
+        const uint32_t m = std::min<uint32_t>(hi - lo, WARM);
+        if (!n_live[ROOT]) return;
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint8_t* f = buf + offs[lo + i];
+            filter_words_prefix(f, offs[lo + i + 1] - offs[lo + i], ids[i]);
+            node[i] = ROOT;
+            depth[i] = 0;
+        }
+        const uint32_t nb = nbuckets();
+        for (bool any = true; any;) {
+            any = false;
+            for (uint32_t i = 0; i < m; ++i)
+                if (node[i] != NONE && depth[i] < ids[i].size())
+                    __builtin_prefetch(&slots[(size_t)home_bucket(node[i], ids[i][depth[i]], nb) * BUCKET]);
+            for (uint32_t i = 0; i < m; ++i) {
+                if (node[i] == NONE || depth[i] >= ids[i].size()) continue;
+                const uint32_t sl = find_slot(node[i], ids[i][depth[i]]);
+                node[i] = sl == NONE ? NONE : (slots[sl].child & ID_MASK);
+                ++depth[i];
+                any = true;
+            }
+        }
+    }
+
+    // word ids of a filter up to its first word absent from the dictionary
+    void filter_words_prefix(const uint8_t* t, size_t len, std::vector<uint32_t>& ids) {
+        static thread_local std::vector<TWord> ws;
+        split_words(t, len, ws);
+        ids.clear();
+        for (const TWord& w : ws) {
+            const uint32_t id = w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find(w.p, w.n);
+            if (id == W_UNKNOWN) return;
+            ids.push_back(id);
+        }
     }
 
     // tm_dict_load: intern words in order ('', '+', '#' have fixed ids)
@@ -745,33 +912,37 @@ struct tm_engine {
     int trie_insert(const uint8_t* t, size_t len) {
         static thread_local std::vector<uint32_t> ids;
         if (!filter_words(t, len, true, ids)) return TM_ENOENT;   // frozen dictionary only
-        const uint32_t found = walk(ids);
-        if (found != NONE) {
-            if (!n_topic[found]) { set_topic(found, t, len); ++version; }
-            return TM_OK;
-        }
-        // node ids are 30-bit (two flag bits ride in the slot's id words)
-        if (n_parent.size() + ids.size() >= MAX_NODES && free_nodes.size() < ids.size()) return TM_ENOMEM;
-        // add_path/1 for every triple (:145-158)
+        // add_path/1 for every triple (:145-158), in one walk: existing edges
+        // are followed, the missing suffix is created
         uint32_t p = ROOT;
-        for (uint32_t w : ids) {
-            if (!n_live[p]) {               // only the root can be absent here
-                n_live[p] = 1; n_ec[p] = 0; ++live_nodes;
-            }
-            const uint32_t s = find_slot(p, w);
+        bool created = false;
+        for (size_t k = 0; k < ids.size(); ++k) {
+            const uint32_t w = ids[k];
+            const uint32_t s = n_live[p] ? find_slot(p, w) : NONE;
             uint32_t c;
-            if (s == NONE) {
+            if (s != NONE) {
+                c = slots[s].child & ID_MASK;
+            } else {
+                if (!created) {
+                    // node ids are 30-bit (two flag bits ride in the slot's id words)
+                    const size_t need = ids.size() - k;
+                    if (n_parent.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
+                        return TM_ENOMEM;
+                    created = true;
+                }
+                if (!n_live[p]) {               // only the root can be absent here
+                    n_live[p] = 1; n_ec[p] = 0; ++live_nodes;
+                }
                 c = new_node(p, w);
                 ++n_ec[p];
                 if (w == W_PLUS) n_plus[p] = c;
                 else if (w == W_HASH) n_hash[p] = c;
                 insert_edge(p, w, c);
                 write_summary(p);
-            } else {
-                c = slots[s].child & ID_MASK;
             }
             p = c;
         }
+        if (!created && n_topic[p]) return TM_OK;   // inserted already: idempotent
         set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
         ++version;
         return TM_OK;
@@ -1718,6 +1889,7 @@ struct tm_engine {
 
     int prepare(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags = 0) {
         if (int rc = check_topics(offsets, n)) return rc;
+        forget_launch(b);   // its previous results are gone
         b->dedup = (flags & TM_BATCH_DEDUP) != 0;
         b->n_pub = n;
         b->row_of.clear();
@@ -1887,6 +2059,7 @@ struct tm_engine {
         a.nfbytes = fbytes.size();
         a.dbg = checked ? d_dbg : nullptr;
         HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        note_launch(b);
         b->launched = true;
         b->done = false;
         b->csr = csr;
@@ -2066,6 +2239,7 @@ struct tm_engine {
         (void)hipSetDevice(device);
         for (AsyncSlot* sl : a_slots) {
             if (sl->b.own) (void)hipStreamSynchronize(sl->b.own);
+            forget_launch(&sl->b);
             sl->b.release();
             if (sl->b.own) (void)hipStreamDestroy(sl->b.own);
             if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
@@ -2333,7 +2507,7 @@ struct tm_engine {
         // root node id 0 (absent until the first add_path, like the reference)
         n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
         n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
-        n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0);
+        n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0); n_hasbytes.push_back(0);
         slots.clear();
         slots.resize(1024);
         for (Slot& s : slots) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
@@ -2726,6 +2900,7 @@ void tm_batch_free(tm_engine* e, tm_batch* b) {
             (void)hipSetDevice(e->device);
             (void)hipStreamSynchronize(e->stream);
         }
+        e->forget_launch(b);
         b->release();
     } else {
         b->release();
@@ -2872,11 +3047,13 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     std::lock_guard<std::recursive_mutex> g(e->mu);
     uint64_t done = 0;
     int rc = TM_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
             const uint8_t* f = filters + offsets[i];
             const size_t len = offsets[i + 1] - offsets[i];
-            if (offsets[i + 1] < offsets[i]) { rc = TM_EINVAL; break; }
+            if (i % tm_engine::WARM == 0 && nshards <= 1) e->warm_paths(filters, offsets, i, n);
             if (nshards > 1) {
                 const int s = e->filter_shard(f, len, nshards);
                 if (s < 0) { rc = s; break; }
@@ -2901,6 +3078,7 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     try {
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
             if (offsets[i + 1] < offsets[i]) { rc = TM_EINVAL; break; }
+            if (i % tm_engine::WARM == 0) e->warm_paths(filters, offsets, i, n);
             rc = e->trie_delete(filters + offsets[i], offsets[i + 1] - offsets[i]);
             if (rc == TM_OK) ++done;
         }
@@ -3012,7 +3190,7 @@ int tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_i
 const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
     if (!e) return nullptr;
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    if (id >= e->n_topic.size() || !e->n_topic[id] || !e->n_live[id]) return nullptr;
+    if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) return nullptr;   // matched ids keep their bytes
     if (len) *len = e->n_flen[id];
     static const uint8_t empty = 0;
     return e->n_flen[id] ? e->fbytes.data() + e->n_foff[id] : &empty;
@@ -3021,7 +3199,7 @@ const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
 int tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len) {
     if (!e || !len || (cap && !buf)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    if (id >= e->n_topic.size() || !e->n_topic[id] || !e->n_live[id]) return TM_ENOENT;
+    if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) return TM_ENOENT;
     *len = e->n_flen[id];
     if (*len <= cap && *len) memcpy(buf, e->fbytes.data() + e->n_foff[id], *len);
     return TM_OK;
@@ -3085,6 +3263,48 @@ int tm_topic_validate(int is_name, const uint8_t* t, size_t len, const char** re
         }
     }
     if (is_name && wild) { *reason = "topic_name_error"; return TM_EINVAL; }
+    return TM_OK;
+}
+
+int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    const uint32_t nb = e->nbuckets();
+    uint64_t live = 0, md = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        bool hole = false;
+        for (uint32_t k = 0; k < BUCKET; ++k) {
+            const Slot& sl = e->slots[b * BUCKET + k];
+            if (sl.parent == SLOT_EMPTY) { hole = true; continue; }
+            if (hole || sl.parent == SLOT_TOMB) {
+                snprintf(last_error(), 512, "bucket %u not filled in order", b);
+                return TM_EIO;
+            }
+            ++live;
+            const uint32_t h = home_bucket(sl.parent, sl.word, nb);
+            const uint32_t d = (b + nb - h) % nb;
+            md = std::max<uint64_t>(md, d);
+            if (d > e->max_disp) {
+                snprintf(last_error(), 512, "slot %u displaced %u > max_disp %u", b * BUCKET + k, d, e->max_disp);
+                return TM_EIO;
+            }
+            for (uint32_t x = h; x != b; x = (x + 1 == nb) ? 0 : x + 1)
+                if (e->slots[x * BUCKET + BUCKET - 1].parent == SLOT_EMPTY) {
+                    snprintf(last_error(), 512, "run of slot %u (home %u) broken at bucket %u", b * BUCKET + k, h, x);
+                    return TM_EIO;
+                }
+            if (e->find_slot(sl.parent, sl.word) != b * BUCKET + k || e->n_inslot[sl.child & ID_MASK] != b * BUCKET + k) {
+                snprintf(last_error(), 512, "slot %u not found by its key", b * BUCKET + k);
+                return TM_EIO;
+            }
+        }
+    }
+    if (live != e->live_edges) {
+        snprintf(last_error(), 512, "live slots %llu != live edges %llu", (unsigned long long)live,
+                 (unsigned long long)e->live_edges);
+        return TM_EIO;
+    }
+    if (max_disp_out) *max_disp_out = md;
     return TM_OK;
 }
 

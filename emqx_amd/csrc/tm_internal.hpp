@@ -271,17 +271,31 @@ __host__ __device__ inline uint64_t le_bytes(const uint8_t* p, uint32_t n) {   /
     return v;
 }
 
-constexpr uint64_t HW_K0 = 0xcbf29ce484222325ull, HW_K1 = 0x9E3779B97F4A7C15ull;
-constexpr uint64_t HW_M1 = 0xBF58476D1CE4E5B9ull, HW_M2 = 0x94D049BB133111EBull;
-__host__ __device__ inline uint64_t hw_init(uint64_t n) { return HW_K0 ^ (n * HW_K1); }
-__host__ __device__ inline uint64_t hw_mix(uint64_t h, uint64_t v) {
-    h = (h ^ (v * HW_M1)) * HW_M2;
-    return h ^ (h >> 29);
+// Word hash of the dictionary (host interner and device tokeniser agree):
+// murmur3-style 32-bit steps over the word's little-endian dwords (the tail
+// zero-padded), the length mixed in at the end.  32-bit multiplies only: the
+// device tokeniser hashes ~50M words per 10M publishes.  |1: 0 marks an empty
+// table slot.  (Equality is decided by length + the inline 16 bytes + arena,
+// never by the hash.)
+__host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__host__ __device__ inline uint32_t hw_step(uint32_t h, uint32_t d) {
+    d *= 0xCC9E2D51u;
+    d = rotl32(d, 15);
+    d *= 0x1B873593u;
+    h ^= d;
+    h = rotl32(h, 13);
+    return h * 5u + 0xE6546B64u;
 }
-__host__ __device__ inline uint64_t hw_final(uint64_t h, uint64_t tail) {
-    h = (h ^ (tail * HW_M1)) * HW_M2;
-    return (h ^ (h >> 31)) | 1;   // 0 = empty slot
+__host__ __device__ inline uint32_t hw_final(uint32_t h, uint32_t n) {
+    h ^= n;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h | 1u;
 }
+constexpr uint32_t HW_SEED = 0x9E3779B9u;
 
 // Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
 // the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp

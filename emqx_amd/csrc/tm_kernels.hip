@@ -1352,17 +1352,13 @@ __device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint32_t n, bool& irre
 // P is an LDS or global byte pointer
 template <class P>
 __device__ __forceinline__ uint32_t dict_find(const TokArgs& a, P p, uint32_t n) {
-    uint64_t h = hw_init(n);
-    uint32_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        uint64_t v = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) v |= (uint64_t)p[i + k] << (8 * k);
-        h = hw_mix(h, v);
+    uint32_t h32 = HW_SEED;
+    for (uint32_t i = 0; i < n; i += 4) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 4 && i + k < n; ++k) v |= (uint32_t)p[i + k] << (8 * k);
+        h32 = hw_step(h32, v);
     }
-    uint64_t tail = 0;
-    for (uint32_t k = 0; i + k < n; ++k) tail |= (uint64_t)p[i + k] << (8 * k);
-    h = hw_final(h, tail);
+    const uint64_t h = hw_final(h32, n);
     uint64_t head = 0, head2 = 0;
     for (uint32_t k = 0; k < 8 && k < n; ++k) head |= (uint64_t)p[k] << (8 * k);
     for (uint32_t k = 8; k < 16 && k < n; ++k) head2 |= (uint64_t)p[k] << (8 * (k - 8));
@@ -1480,19 +1476,22 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
             if (n == 0) { ent[k] |= W_EMPTY; continue; }
             if (n == 1 && c0 == '+') { ent[k] |= W_PLUS; continue; }
             if (n == 1 && c0 == '#') { ent[k] |= W_HASH; continue; }
-            const uint64_t c0w = lds_u64(L.bytes, s0), c1w = lds_u64(L.bytes, s0 + 8);
-            uint64_t hh = hw_init(n);
-            if (n >= 8) hh = hw_mix(hh, c0w);
-            if (n >= 16) hh = hw_mix(hh, c1w);
-            uint32_t i = 16;
-            for (; i + 8 <= n; i += 8) hh = hw_mix(hh, lds_u64(L.bytes, s0 + i));
-            const uint32_t done = n < 8 ? 0 : n < 16 ? 8 : i;
-            const uint64_t tw8 = done == 0 ? c0w : done == 8 ? c1w : lds_u64(L.bytes, s0 + done);
-            hh = hw_final(hh, done < n ? low_bytes(tw8, n - done) : 0ull);
-            h[k] = hh;
-            head[k] = low_bytes(c0w, n < 8 ? n : 8);
-            head2[k] = n > 8 ? low_bytes(c1w, n - 8 < 8 ? n - 8 : 8) : 0ull;
-            slot[k] = (uint32_t)(hh & a.dict_mask);
+            // bytes 0..15 zero-padded past n: the inline compare keys and the first four hash dwords
+            const uint64_t c0w = low_bytes(lds_u64(L.bytes, s0), n < 8 ? n : 8);
+            const uint64_t c1w = n > 8 ? low_bytes(lds_u64(L.bytes, s0 + 8), n - 8 < 8 ? n - 8 : 8) : 0ull;
+            uint32_t h32 = hw_step(HW_SEED, (uint32_t)c0w);
+            if (n > 4) h32 = hw_step(h32, (uint32_t)(c0w >> 32));
+            if (n > 8) h32 = hw_step(h32, (uint32_t)c1w);
+            if (n > 12) h32 = hw_step(h32, (uint32_t)(c1w >> 32));
+            for (uint32_t i = 16; i < n; i += 8) {   // rare: words longer than 16 bytes
+                const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
+                h32 = hw_step(h32, (uint32_t)c);
+                if (n - i > 4) h32 = hw_step(h32, (uint32_t)(c >> 32));
+            }
+            h[k] = hw_final(h32, n);
+            head[k] = c0w;
+            head2[k] = c1w;
+            slot[k] = (uint32_t)(h[k] & a.dict_mask);
             pend[k] = true;
         }
         for (uint64_t round = 0; round <= a.dict_mask; ++round) {

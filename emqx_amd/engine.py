@@ -587,3 +587,9 @@ class Engine:
 
     def sync(self):
         N.check(self.L.tm_sync(self.h), "tm_sync")
+
+    def debug_check(self) -> int:
+        """tm_debug_check: edge-hash invariants; -> largest displacement."""
+        md = C.c_uint64()
+        N.check(self.L.tm_debug_check(self.h, C.byref(md)), "tm_debug_check")
+        return int(md.value)

@@ -62,8 +62,9 @@ class Churn:
 
     @staticmethod
     def apply(engine, dels, adds):
-        """Unsubscribes then subscribes, two bulk C calls (emqx_trie:delete/1, insert/1)."""
-        if dels:
+        """Unsubscribes then subscribes, two bulk C calls (emqx_trie:delete/1,
+        insert/1); dels / adds are lists of binaries or packed gen.Strings."""
+        if len(dels):
             engine.delete_many(dels)
-        if adds:
+        if len(adds):
             engine.insert_many(adds)

@@ -380,12 +380,15 @@ TM_API int  tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d
 
 /* ---- filters ---------------------------------------------------------- */
 /* Bytes of a filter id returned by a match (the #trie_node.topic binary).
- * The pointer is into engine memory that a later insert may move: callers
- * racing with writers use tm_filter_copy. */
+ * A matched id keeps naming its filter while the result that holds it is
+ * valid, even if the filter is deleted meanwhile: ids freed by deletes are
+ * reused only after every batch launched before the delete has been
+ * re-launched or freed.  The pointer is into engine memory that a later
+ * insert may move: callers racing with writers use tm_filter_copy. */
 TM_API const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len);
 /* Copies the bytes of filter `id` into buf[cap] under the engine lock; *len =
- * its length (copied only if <= cap).  TM_ENOENT if the id is not a live
- * filter (deleted since the match that returned it). */
+ * its length (copied only if <= cap).  TM_ENOENT if the id never named a
+ * filter or was reused for a node without one. */
 TM_API int  tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len);
 /* Id of an inserted filter, TM_ENOENT if absent. */
 TM_API int  tm_filter_id(tm_engine* e, const uint8_t* filter, size_t len, uint32_t* id);
@@ -450,6 +453,11 @@ TM_API int  tm_group_match_batch(tm_group* g, const uint8_t* topics, const uint6
                                  tm_result* out);
 
 /* ---- diagnostics ------------------------------------------------------ */
+/* Consistency check of the host edge hash (tests): slots of a bucket filled
+ * in order, every key's probe run unbroken and within max_disp, every key
+ * found by the lookup the kernels mirror.  TM_EIO + tm_last_error() on the
+ * first violation; *max_disp_out (may be NULL) = the largest displacement. */
+TM_API int  tm_debug_check(tm_engine* e, uint64_t* max_disp_out);
 /* Text of the last TM_EIO on this thread (HIP error string + call site). */
 TM_API const char* tm_last_error(void);
 TM_API const char* tm_build_info(void);

@@ -50,11 +50,18 @@ def test_async_refused_without_device():
     assert st["batches"] == 0 and st["requests"] == 0
 
 
-def test_filter_copy_host_engine():
+def test_filter_copy_and_id_reuse_host_engine():
+    """A deleted filter's id keeps its bytes until the id is reused; with no
+    batch holding results (host-only engine), the next new node reuses it."""
     eng = Engine(device=-1)
     eng.insert(b"a/+/#")
     fid = eng.filter_id(b"a/+/#")
-    assert eng.filter_copy(fid) == b"a/+/#"
+    assert eng.filter_copy(fid) == eng.filter_bytes(fid) == b"a/+/#"
     eng.delete(b"a/+/#")
+    assert eng.filter_copy(fid) == b"a/+/#"        # still names the filter a result may hold
     with pytest.raises(KeyError):
-        eng.filter_copy(fid)
+        eng.filter_id(b"a/+/#")
+    eng.insert(b"x/y/z")                            # reuses the freed ids
+    assert eng.filter_copy(eng.filter_id(b"x/y/z")) == b"x/y/z"
+    with pytest.raises(KeyError):
+        eng.filter_copy(10_000)

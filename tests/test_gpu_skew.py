@@ -52,3 +52,45 @@ def test_skew_dedup_churn_parity():
             exp = [F[int(j)] for j in idx[cut[r]:cut[r + 1]]]
             assert got == exp, (rnd, Td[r][:60])
     assert eng.stats()["uploads_delta"] >= 1
+
+
+def test_churn_applied_while_the_device_walks():
+    """The C5 bench's pipeline: deltas i + 1 are applied on the host while
+    batch i runs.  Batch i must equal the oracle on snapshot i (deltas <= i),
+    and its ids must still name their filters after deltas i + 1 deleted some
+    of them (freed ids are not reused while a result may hold them)."""
+    p = gen.SkewParams(seed=9, n_hot=120, k_per_hot=60)
+    allf, derived, hot, pubs = workload(p, 2000, 20_000, seed=9, background_pool=4000)
+    background = allf.tolist()[len(derived):]
+    eng = Engine(device=0)
+    eng.insert_many(allf)
+    churn = Churn(hot, derived.tolist(), seed=4)
+    b = eng.prepare(pubs, dedup=True)
+    row_of, n_rows = b.row_map()
+    T = pubs.tolist()
+    distinct = {}
+    for i, r in enumerate(row_of.tolist()):
+        distinct.setdefault(r, T[i])
+    Td = [distinct[r] for r in range(n_rows)]
+    snapshot = sorted(churn.live_set) + background
+    b.launch().wait()          # sizes the staging area: no capacity re-run inside the pipelined rounds
+    b.launch()
+    for rnd in range(3):
+        dels, adds = churn.step(800)                      # deltas of the NEXT step
+        Churn.apply(eng, gen.Strings.from_list(dels), gen.Strings.from_list(adds))
+        b.wait()
+        offs, ids = b.result()
+        got = [[eng.filter_bytes(int(x)) for x in ids[offs[r]:offs[r + 1]]] for r in range(n_rows)]
+        orc = P.Oracle()
+        for f in snapshot:
+            orc.register(f)
+            orc.insert(f)
+        buf, o = P.pack(Td)
+        counts, idx, _ = orc.match_batch(buf, o, nthreads=8)
+        cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+        for r in range(n_rows):
+            assert got[r] == [snapshot[int(j)] for j in idx[cut[r]:cut[r + 1]]], (rnd, Td[r][:60])
+        snapshot = sorted(churn.live_set) + background
+        b.launch()                                         # sees the deltas applied above
+    b.wait()
+    b.free()
