@@ -150,6 +150,7 @@ SIGNATURES = {
     "tm_filter_bytes": (C.POINTER(C.c_uint8), [P, C.c_uint32, C.POINTER(SZ)]),
     "tm_filter_id": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32)]),
     "tm_filter_copy": (C.c_int, [P, C.c_uint32, P, SZ, C.POINTER(SZ)]),
+    "tm_filters_copy": (C.c_int, [P, P, C.c_uint32, P, SZ, P, P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),
     "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
     "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),

@@ -63,8 +63,23 @@ def build_load(force=False):
     return out
 
 
+def build_nif_mock(force=False):
+    """libemqx_nif_mock.so: the erl_nif shim linked against the test stand-in
+    for the Erlang runtime (tests/nif_mock), so tests can drive the NIF."""
+    out = os.path.join(HERE, "libemqx_nif_mock.so")
+    mock = os.path.join(ROOT, "tests", "nif_mock")
+    srcs = [os.path.join(CSRC, "nif", "emqx_tm_nif.c"), os.path.join(mock, "mock_erts.c")]
+    deps = srcs + [os.path.join(mock, "erl_nif.h"), os.path.join(HERE, "libemqx_tm.so"),
+                   os.path.join(ROOT, "include", "emqx_tm.h")]
+    if force or _stale(out, deps):
+        _run(["gcc", "-O1", "-g", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror",
+              "-I" + mock, "-I" + os.path.join(ROOT, "include"), "-o", out] + srcs +
+             ["-L" + HERE, "-lemqx_tm", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+    return out
+
+
 def build_all(force=False):
-    return [build_tm(force), build_gen(force), build_load(force)]
+    return [build_tm(force), build_gen(force), build_load(force), build_nif_mock(force)]
 
 
 if __name__ == "__main__":

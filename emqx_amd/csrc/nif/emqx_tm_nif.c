@@ -11,13 +11,22 @@
  *
  * Scheduling: trie mutations and lookups are host-only and short, but they
  * share the engine mutex with device batches, so every call that takes the
- * engine runs on a dirty I/O scheduler.  The pairwise predicate is pure and
- * runs on a normal scheduler.
+ * engine runs on a dirty I/O scheduler.  match_async/3 only queues the topic
+ * (tm_match_async) and runs on a normal scheduler; the engine's completion
+ * thread builds the reply in a process-independent environment and sends it.
+ * The pairwise predicate is pure and runs on a normal scheduler.
+ *
+ * Results never alias engine scratch: batch calls run on a tm_batch of their
+ * own (freed before the NIF returns), and filter ids become binaries through
+ * tm_filters_copy, which copies under the engine lock and skips ids whose
+ * filter is gone -- so concurrent callers and writers cannot free or rewrite
+ * what a reply is being built from.
  *
  * Errors: a non-binary topic raises badarg (the reference's function_clause
  * class, src/emqx_trie.erl:82,97,108); engine errors return {error, Reason}.
  */
 #include <erl_nif.h>
+#include <pthread.h>
 #include <string.h>
 
 #include "emqx_tm.h"
@@ -30,12 +39,27 @@ typedef struct {
 
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_UNDEFINED, ATOM_ROOT,
     ATOM_TRIE_NODE, ATOM_NODE_NOT_FOUND, ATOM_ENOMEM, ATOM_EIO, ATOM_EINVAL, ATOM_ENODEV,
-    ATOM_EOVERFLOW, ATOM_NOT_FOUND, ATOM_WRITE, ATOM_DELETE_OBJECT;
+    ATOM_EOVERFLOW, ATOM_NOT_FOUND, ATOM_WRITE, ATOM_DELETE_OBJECT, ATOM_EMQX_TM_MATCH;
+
+/* set while a match callback runs on the engine's completion thread */
+static __thread int in_engine_callback;
+
+static void* destroy_engine(void* e) {
+    tm_destroy((tm_engine*)e);
+    return NULL;
+}
 
 static void engine_dtor(ErlNifEnv* env, void* obj) {
     (void)env;
     engine_res* r = (engine_res*)obj;
-    if (r->e) tm_destroy(r->e);
+    if (r->e && in_engine_callback) {
+        /* the last reference went away in a match callback: tm_destroy joins
+         * the completion thread, so it runs on a thread of its own */
+        pthread_t t;
+        if (pthread_create(&t, NULL, destroy_engine, r->e) == 0) pthread_detach(t);
+    } else if (r->e) {
+        tm_destroy(r->e);
+    }
     r->e = NULL;
 }
 
@@ -115,9 +139,10 @@ static ERL_NIF_TERM nif_lookup(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     if (rc == 0) return enif_make_list(env, 0);
     ERL_NIF_TERM topic = ATOM_UNDEFINED;
     if (n.has_topic) {
+        uint8_t tmp[TM_MAX_TOPIC_LEN];
         size_t len = 0;
-        const uint8_t* p = tm_filter_bytes(r->e, n.filter_id, &len);
-        if (p) topic = make_bin(env, p, len);
+        if (tm_filter_copy(r->e, n.filter_id, tmp, sizeof tmp, &len) == TM_OK && len <= sizeof tmp)
+            topic = make_bin(env, tmp, len);
     }
     ERL_NIF_TERM rec = enif_make_tuple5(env, ATOM_TRIE_NODE, argv[1], enif_make_uint(env, n.edge_count), topic,
                                         ATOM_UNDEFINED);
@@ -132,44 +157,105 @@ static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     return tm_trie_empty(r->e) ? ATOM_TRUE : ATOM_FALSE;
 }
 
-static ERL_NIF_TERM rows_to_terms(ErlNifEnv* env, tm_engine* e, const tm_result* res, uint32_t row) {
-    const uint32_t b = res->row_offsets[row], n = res->row_offsets[row + 1] - b;
+/* Filter ids -> their bytes, packed under one engine lock (tm_filters_copy):
+ * filter k = buf[offs[k], offs[k+1]) for ids[keep[k]]; ids whose filter was
+ * deleted and its id reused are skipped.  enif_alloc'ed; packed_free. */
+typedef struct {
+    uint8_t* buf;
+    uint64_t* offs;
+    uint32_t* keep;
+    uint32_t n;
+} packed;
+
+static void packed_free(packed* p) {
+    enif_free(p->buf); enif_free(p->offs); enif_free(p->keep);
+    p->buf = NULL; p->offs = NULL; p->keep = NULL;
+}
+
+static int pack_filters(tm_engine* e, const uint32_t* ids, uint64_t n, packed* p) {
+    if (n > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+    size_t cap = 32 * (size_t)n + 64;
+    uint64_t need = 0;
+    p->offs = enif_alloc(sizeof(uint64_t) * (n + 1));
+    p->keep = enif_alloc(sizeof(uint32_t) * (n ? n : 1));
+    p->buf = NULL;
+    for (;;) {
+        p->buf = enif_alloc(cap);
+        if (!p->offs || !p->keep || !p->buf) { packed_free(p); return TM_ENOMEM; }
+        int rc = tm_filters_copy(e, ids, (uint32_t)n, p->buf, cap, p->offs, p->keep, &p->n, &need);
+        if (rc) { packed_free(p); return rc; }
+        if (need <= cap) return TM_OK;
+        enif_free(p->buf);
+        cap = (size_t)need;
+    }
+}
+
+/* The list of the packed filters k with lo <= keep[k] < hi, for *k counting
+ * down from the end (rows are built back to front: lists come out in order). */
+static ERL_NIF_TERM packed_row(ErlNifEnv* env, const packed* p, uint32_t* k, uint64_t lo) {
     ERL_NIF_TERM list = enif_make_list(env, 0);
-    for (uint32_t i = n; i-- > 0;) {       /* build back to front: list in sorted order */
-        size_t len = 0;
-        const uint8_t* p = tm_filter_bytes(e, res->filter_ids[b + i], &len);
-        list = enif_make_list_cell(env, make_bin(env, p, len), list);
+    while (*k > 0 && p->keep[*k - 1] >= lo) {
+        --*k;
+        list = enif_make_list_cell(env, make_bin(env, p->buf + p->offs[*k], p->offs[*k + 1] - p->offs[*k]), list);
     }
     return list;
 }
 
-/* match(Engine, Topic) -> [Filter]  (emqx_trie:match/1, :96-99; sorted set).
- * One call per publishing process: concurrent calls are coalesced into shared
- * device batches by tm_match_coalesced. */
-static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+static ERL_NIF_TERM ids_to_filters(ErlNifEnv* env, tm_engine* e, const uint32_t* ids, uint32_t n) {
+    packed p;
+    int rc = pack_filters(e, ids, n, &p);
+    if (rc) return err(env, rc);
+    uint32_t k = p.n;
+    ERL_NIF_TERM list = packed_row(env, &p, &k, 0);
+    packed_free(&p);
+    return list;
+}
+
+typedef struct {
+    ErlNifPid pid;
+    ErlNifEnv* env;       /* process-independent: the reply is built here */
+    ERL_NIF_TERM ref;     /* the caller's reference, copied into env */
+    engine_res* res;      /* kept until the reply is sent */
+} match_call;
+
+static void match_done(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
+    match_call* c = (match_call*)ctx;
+    in_engine_callback = 1;
+    ERL_NIF_TERM reply = rc ? err(c->env, rc) : ids_to_filters(c->env, c->res->e, ids, n);
+    enif_send(NULL, &c->pid, c->env, enif_make_tuple3(c->env, ATOM_EMQX_TM_MATCH, c->ref, reply));
+    enif_free_env(c->env);
+    enif_release_resource(c->res);
+    enif_free(c);
+    in_engine_callback = 0;
+}
+
+/* match_async(Engine, Topic, Ref) -> ok | {error, Reason}
+ * emqx_trie:match/1 (:96-99) for one publish, answered by the message
+ * {emqx_tm_match, Ref, [Filter] | {error, Reason}} (sorted set of filters).
+ * Every publishing process can have its match in flight: the engine forms
+ * device batches from everything queued (tm_match_async). */
+static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     engine_res* r;
     ErlNifBinary b;
     (void)argc;
-    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
-    uint32_t local[256];
-    uint32_t* ids = local;
-    uint32_t cap = 256, n = 0;
-    int rc = tm_match_coalesced(r->e, b.size ? b.data : (const uint8_t*)"", b.size, ids, cap, &n);
-    if (!rc && n > cap) {                     /* a longer row: ask again with room for it */
-        cap = n;
-        ids = enif_alloc(sizeof(uint32_t) * cap);
-        rc = tm_match_coalesced(r->e, b.size ? b.data : (const uint8_t*)"", b.size, ids, cap, &n);
-        if (!rc && n > cap) n = cap;          /* the trie grew in between: the first cap ids */
+    if (!get_engine(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &b) || !enif_is_ref(env, argv[2]))
+        return enif_make_badarg(env);
+    match_call* c = enif_alloc(sizeof(match_call));
+    if (!c) return err(env, TM_ENOMEM);
+    c->env = enif_alloc_env();
+    if (!c->env) { enif_free(c); return err(env, TM_ENOMEM); }
+    enif_self(env, &c->pid);
+    c->ref = enif_make_copy(c->env, argv[2]);
+    c->res = r;
+    enif_keep_resource(r);
+    int rc = tm_match_async(r->e, b.size ? b.data : (const uint8_t*)"", b.size, match_done, c);
+    if (rc) {   /* not queued: no callback will run */
+        enif_release_resource(r);
+        enif_free_env(c->env);
+        enif_free(c);
+        return err(env, rc);
     }
-    ERL_NIF_TERM list = enif_make_list(env, 0);
-    if (!rc)
-        for (uint32_t i = n; i-- > 0;) {
-            size_t len = 0;
-            const uint8_t* p = tm_filter_bytes(r->e, ids[i], &len);
-            list = enif_make_list_cell(env, make_bin(env, p, len), list);
-        }
-    if (ids != local) enif_free(ids);
-    return rc ? err(env, rc) : list;
+    return ATOM_OK;
 }
 
 /* Concatenates a list of binaries: buf/offs are enif_alloc'ed (caller frees). */
@@ -196,6 +282,18 @@ static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, unsigned* n_out, uin
     return 1;
 }
 
+/* Runs the device pipeline for the packed topics on a batch of this call's
+ * own (its pinned result buffers belong to no other caller). */
+static int run_batch(tm_engine* e, uint8_t* buf, uint64_t* offs, unsigned n, tm_batch** out) {
+    tm_batch* b = NULL;
+    int rc = tm_batch_prepare(e, buf, offs, n, &b);
+    if (!rc) rc = tm_batch_launch(e, b);
+    if (!rc) rc = tm_batch_wait(e, b);
+    if (rc && b) { tm_batch_free(e, b); b = NULL; }
+    *out = b;
+    return rc;
+}
+
 /* match_batch(Engine, [Topic]) -> [[Filter]]  (one device pipeline per call) */
 static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
     engine_res* r;
@@ -204,12 +302,22 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     uint64_t* offs;
     (void)argc;
     if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
+    tm_batch* b;
     tm_result res;
-    int rc = tm_match_batch(r->e, buf, offs, n, &res);
+    packed p;
+    int rc = run_batch(r->e, buf, offs, n, &b);
     enif_free(buf); enif_free(offs);
-    if (rc) return err(env, rc);
+    if (!rc) rc = tm_batch_result(r->e, b, &res);
+    if (!rc) rc = pack_filters(r->e, res.filter_ids, res.n_matches, &p);
+    if (rc) {
+        if (b) tm_batch_free(r->e, b);
+        return err(env, rc);
+    }
     ERL_NIF_TERM out = enif_make_list(env, 0);
-    for (unsigned i = n; i-- > 0;) out = enif_make_list_cell(env, rows_to_terms(env, r->e, &res, i), out);
+    uint32_t k = p.n;
+    for (unsigned i = n; i-- > 0;) out = enif_make_list_cell(env, packed_row(env, &p, &k, res.row_offsets[i]), out);
+    packed_free(&p);
+    tm_batch_free(r->e, b);
     return out;
 }
 
@@ -331,13 +439,11 @@ static ERL_NIF_TERM nif_dispatch_batch(ErlNifEnv* env, int argc, const ERL_NIF_T
     uint64_t* offs;
     (void)argc;
     if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
-    tm_batch* b = NULL;
+    tm_batch* b;
     tm_deliveries d;
-    int rc = tm_batch_prepare(r->e, buf, offs, n, &b);
-    if (!rc) rc = tm_batch_launch(r->e, b);
-    if (!rc) rc = tm_batch_wait(r->e, b);
-    if (!rc) rc = tm_batch_dispatch(r->e, b, 0, &d);
+    int rc = run_batch(r->e, buf, offs, n, &b);
     enif_free(buf); enif_free(offs);
+    if (!rc) rc = tm_batch_dispatch(r->e, b, 0, &d);
     if (rc) {
         if (b) tm_batch_free(r->e, b);
         return err(env, rc);
@@ -362,21 +468,30 @@ static ERL_NIF_TERM nif_match_routes_batch(ErlNifEnv* env, int argc, const ERL_N
     uint64_t* offs;
     (void)argc;
     if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
+    tm_batch* b;
     tm_routes res;
-    int rc = tm_match_routes_batch(r->e, buf, offs, n, &res);
+    packed p;
+    int rc = run_batch(r->e, buf, offs, n, &b);
     enif_free(buf); enif_free(offs);
-    if (rc) return err(env, rc);
+    if (!rc) rc = tm_batch_routes(r->e, b, &res);
+    if (!rc) rc = pack_filters(r->e, res.filter_ids, res.n_routes, &p);
+    if (rc) {
+        if (b) tm_batch_free(r->e, b);
+        return err(env, rc);
+    }
     ERL_NIF_TERM out = enif_make_list(env, 0);
+    uint32_t k = p.n;
     for (unsigned i = n; i-- > 0;) {
         ERL_NIF_TERM row = enif_make_list(env, 0);
-        for (uint32_t k = res.row_offsets[i + 1]; k-- > res.row_offsets[i];) {
-            size_t len = 0;
-            const uint8_t* p = tm_filter_bytes(r->e, res.filter_ids[k], &len);
-            row = enif_make_list_cell(env, enif_make_tuple2(env, make_bin(env, p, len), enif_make_uint(env, res.dests[k])),
-                                      row);
+        while (k > 0 && p.keep[k - 1] >= res.row_offsets[i]) {
+            --k;
+            ERL_NIF_TERM f = make_bin(env, p.buf + p.offs[k], p.offs[k + 1] - p.offs[k]);
+            row = enif_make_list_cell(env, enif_make_tuple2(env, f, enif_make_uint(env, res.dests[p.keep[k]])), row);
         }
         out = enif_make_list_cell(env, row, out);
     }
+    packed_free(&p);
+    tm_batch_free(r->e, b);
     return out;
 }
 
@@ -440,6 +555,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
     ATOM_NOT_FOUND = enif_make_atom(env, "not_found");
     ATOM_WRITE = enif_make_atom(env, "write");
     ATOM_DELETE_OBJECT = enif_make_atom(env, "delete_object");
+    ATOM_EMQX_TM_MATCH = enif_make_atom(env, "emqx_tm_match");
     return 0;
 }
 
@@ -449,7 +565,7 @@ static ErlNifFunc funcs[] = {
     {"delete", 2, nif_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"lookup", 2, nif_lookup, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"empty", 1, nif_empty, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"match", 2, nif_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_async", 3, nif_match_async, 0},
     {"match_batch", 2, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_add", 3, nif_route_add, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"route_delete", 3, nif_route_delete, ERL_NIF_DIRTY_JOB_IO_BOUND},

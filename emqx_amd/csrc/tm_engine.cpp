@@ -3205,6 +3205,31 @@ int tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* 
     return TM_OK;
 }
 
+int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, size_t cap, uint64_t* offs,
+                    uint32_t* keep, uint32_t* n_out, uint64_t* need) {
+    if (!e || !offs || !n_out || !need || (n && !ids) || (cap && !buf)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (ids[i] < e->n_hasbytes.size() && e->n_hasbytes[ids[i]]) total += e->n_flen[ids[i]];
+    *need = total;
+    if (total > cap) return TM_OK;   // nothing copied: the caller grows buf and asks again
+    uint32_t k = 0;
+    uint64_t at = 0;
+    offs[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t id = ids[i];
+        if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) continue;
+        const uint32_t len = e->n_flen[id];
+        if (len) memcpy(buf + at, e->fbytes.data() + e->n_foff[id], len);
+        at += len;
+        if (keep) keep[k] = i;
+        offs[++k] = at;
+    }
+    *n_out = k;
+    return TM_OK;
+}
+
 int tm_filter_id(tm_engine* e, const uint8_t* f, size_t len, uint32_t* id) {
     if (!e || !id) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);

@@ -567,6 +567,25 @@ class Engine:
         N.check(rc, "tm_filter_copy")
         return buf.raw[:n.value]
 
+    def filters_copy(self, ids) -> list:
+        """tm_filters_copy: [(index in ids, filter bytes)] for the ids that
+        still name a filter, copied under one acquisition of the engine lock."""
+        a = np.ascontiguousarray(ids, dtype=np.uint32)
+        n = len(a)
+        offs = np.zeros(n + 1, np.uint64)
+        keep = np.zeros(max(n, 1), np.uint32)
+        k, need = C.c_uint32(), C.c_uint64()
+        cap = 64 * max(n, 1)
+        while True:
+            buf = np.zeros(max(cap, 1), np.uint8)
+            N.check(self.L.tm_filters_copy(self.h, a.ctypes.data, n, buf.ctypes.data, cap, offs.ctypes.data,
+                                           keep.ctypes.data, C.byref(k), C.byref(need)), "tm_filters_copy")
+            if need.value <= cap:
+                break
+            cap = need.value
+        raw = buf.tobytes()
+        return [(int(keep[j]), raw[int(offs[j]):int(offs[j + 1])]) for j in range(k.value)]
+
     def filter_id(self, f: bytes) -> int:
         out = C.c_uint32()
         rc = self.L.tm_filter_id(self.h, f, len(f), C.byref(out))

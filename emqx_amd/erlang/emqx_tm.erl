@@ -12,6 +12,7 @@
         , lookup/2
         , empty/1
         , match/2
+        , match_async/3
         , match_batch/2
         , topic_match/2
         , route_add/3
@@ -53,9 +54,21 @@ lookup(_Engine, _NodeId) -> erlang:nif_error(nif_not_loaded).
 -spec(empty(reference()) -> boolean()).
 empty(_Engine) -> erlang:nif_error(nif_not_loaded).
 
-%% emqx_trie:match/1 (sorted, deduplicated)
--spec(match(reference(), binary()) -> [binary()]).
-match(_Engine, _Topic) -> erlang:nif_error(nif_not_loaded).
+%% emqx_trie:match/1 (sorted, deduplicated).  The calling process queues its
+%% topic and waits for its own reply: every publishing process can have a
+%% match in flight, and the engine batches whatever is queued onto the device.
+-spec(match(reference(), binary()) -> [binary()] | {error, term()}).
+match(Engine, Topic) ->
+    Ref = make_ref(),
+    case match_async(Engine, Topic, Ref) of
+        ok -> receive {emqx_tm_match, Ref, Result} -> Result end;
+        {error, _} = Error -> Error
+    end.
+
+%% Queue one match; the reply {emqx_tm_match, Ref, [Filter] | {error, Reason}}
+%% arrives as a message (runs on a normal scheduler: it only enqueues).
+-spec(match_async(reference(), binary(), reference()) -> ok | {error, term()}).
+match_async(_Engine, _Topic, _Ref) -> erlang:nif_error(nif_not_loaded).
 
 %% match/1 over a batch of publishes, one device pipeline
 -spec(match_batch(reference(), [binary()]) -> [[binary()]]).

@@ -134,14 +134,13 @@ TM_API int  tm_trie_empty(tm_engine* e);
 TM_API int  tm_trie_match(tm_engine* e, const uint8_t* topic, size_t len,
                    uint32_t* ids, uint32_t cap, uint32_t* n_out);
 
-/* emqx_trie:match/1 for one topic, called concurrently by many threads (the
- * NIF's dirty schedulers, one call per publishing process): callers that
- * arrive while a device batch is being formed are coalesced into one
- * tm_match_batch -- the first caller without a running leader lingers up to
- * linger_us (or until max_batch callers queue), then matches all of them in one
- * device round trip; later callers form the next batch.  emqx_batch's size +
- * linger policy (src/emqx_batch.erl:49-90) applied across callers.  Results and
- * errors as tm_trie_match, per caller (len > TM_MAX_TOPIC_LEN -> TM_EINVAL). */
+/* emqx_trie:match/1 for one topic, blocking, for callers on many threads:
+ * tm_match_async below plus a futex wait for the caller's own row, so
+ * concurrent callers share device batches formed by the engine's launcher
+ * (see tm_match_async / tm_coalesce_config for the batching policy and
+ * INTEGRATION.md for how it relates to emqx_batch, src/emqx_batch.erl:56-82).
+ * Results and errors as tm_trie_match, per caller (len > TM_MAX_TOPIC_LEN ->
+ * TM_EINVAL). */
 TM_API int  tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len,
                                uint32_t* ids, uint32_t cap, uint32_t* n_out);
 /* Sets max_batch (0 = keep; default 16384) and linger_us (TM_NONE = keep;
@@ -390,6 +389,15 @@ TM_API const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len);
  * its length (copied only if <= cap).  TM_ENOENT if the id never named a
  * filter or was reused for a node without one. */
 TM_API int  tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len);
+/* Bulk tm_filter_copy under one acquisition of the engine lock (a result row
+ * turned into filter binaries).  *need = the bytes of every id still naming a
+ * filter; if *need > cap nothing is copied (grow buf and call again).
+ * Otherwise the live filters are packed into buf in id order: filter k is
+ * buf[offs[k], offs[k+1]), *n_out = count (offs holds n+1 entries); ids no
+ * longer naming a filter are skipped, and keep[k] (may be NULL) = the index
+ * in ids of filter k. */
+TM_API int  tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, size_t cap,
+                            uint64_t* offs, uint32_t* keep, uint32_t* n_out, uint64_t* need);
 /* Id of an inserted filter, TM_ENOENT if absent. */
 TM_API int  tm_filter_id(tm_engine* e, const uint8_t* filter, size_t len, uint32_t* id);
 

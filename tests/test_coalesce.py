@@ -65,3 +65,15 @@ def test_filter_copy_and_id_reuse_host_engine():
     assert eng.filter_copy(eng.filter_id(b"x/y/z")) == b"x/y/z"
     with pytest.raises(KeyError):
         eng.filter_copy(10_000)
+
+
+def test_filters_copy_packs_live_filters_and_skips_dead_ids():
+    eng = Engine(device=-1)
+    fs = [b"a/+/#", b"sensor/1/temp", b"#", b"x/" + b"y" * 300]
+    for f in fs:
+        eng.insert(f)
+    ids = [eng.filter_id(f) for f in fs]
+    assert eng.filters_copy(ids) == list(enumerate(fs))   # grows past the first guess (300-B filter)
+    got = eng.filters_copy([ids[2], 99_999, ids[0]])      # never a filter: skipped, not <<>>
+    assert got == [(0, b"#"), (2, b"a/+/#")]
+    assert eng.filters_copy([]) == []
