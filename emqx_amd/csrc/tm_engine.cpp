@@ -87,11 +87,16 @@ inline uint64_t hash_bytes(const uint8_t* p, size_t n) {
 
 // ------------------------------------------------------------- word interner
 // Open-addressed string -> id map; bytes live in an append-only arena.  The
-// table is mirrored verbatim in HBM for the device tokeniser: dirty_ lists the
-// slots written since the last upload, gen_ counts rehashes (full upload).
+// device tokeniser gets its own mirror: a 2-choice cuckoo table of probe keys
+// (tm_internal.hpp DictKey) at load <= 1/4 plus the per-id tails; ck_dirty_
+// lists the cuckoo slots written since the last upload, ck_gen_ counts
+// rebuilds (full upload); tails and arena only grow.
 class WordDict {
   public:
-    WordDict() { rehash(1024); }
+    WordDict() {
+        rehash(1024);
+        ck_rebuild(1024);
+    }
 
     uint32_t find(const uint8_t* p, size_t n) const {
         const uint64_t h = hash_word(p, n);
@@ -115,19 +120,56 @@ class WordDict {
         tab_[i] = DictEnt{h, le_bytes(p, (uint32_t)std::min<size_t>(n, 8)),
                           n > 8 ? le_bytes(p + 8, (uint32_t)std::min<size_t>(n - 8, 8)) : 0, (uint32_t)n, id,
                           arena_.size(), 0};
-        dirty_.push_back((uint32_t)i);
         arena_.insert(arena_.end(), p, p + n);
         ++count_;
+        if (tails_.size() <= id) tails_.resize((size_t)id + 1, DictTail{0, 0});
+        tails_[id] = DictTail{tab_[i].head2, tab_[i].off};
+        if (count_ * 4 > ck_.size()) ck_rebuild(ck_.size() * 2);
+        else if (!ck_put(DictKey{tab_[i].head, (uint32_t)n, id}, (uint32_t)h)) ck_rebuild(ck_.size() * 2);
         return id;
     }
 
     size_t size() const { return count_; }
-    const std::vector<DictEnt>& table() const { return tab_; }
     const std::vector<uint8_t>& arena() const { return arena_; }
-    uint64_t gen() const { return gen_; }
-    std::vector<uint32_t>& dirty() { return dirty_; }
+    const std::vector<DictKey>& keys() const { return ck_; }
+    const std::vector<DictTail>& tails() const { return tails_; }
+    uint64_t gen() const { return ck_gen_; }
+    std::vector<uint32_t>& dirty() { return ck_dirty_; }
 
   private:
+    // cuckoo insert with a random walk of evictions; false: the table must grow
+    bool ck_put(DictKey k, uint32_t h) {
+        const uint32_t m = (uint32_t)ck_.size() - 1;
+        uint32_t from = ~0u;
+        for (int kick = 0; kick < 512; ++kick) {
+            const uint32_t a = h & m, b = ck_alt(h) & m;
+            const uint32_t i = ck_[a].id == 0 ? a : ck_[b].id == 0 ? b : (a != from ? a : b);
+            std::swap(k, ck_[i]);
+            std::swap(h, ck_h_[i]);
+            ck_dirty_.push_back(i);
+            if (k.id == 0) return true;
+            from = i;
+        }
+        return false;   // k is homeless: the rebuild reinserts every word from tab_
+    }
+
+    void ck_rebuild(size_t cap) {
+        for (;;) {
+            ck_.assign(cap, DictKey{0, 0, 0});
+            ck_h_.assign(cap, 0);
+            bool ok = true;
+            for (const DictEnt& e : tab_)
+                if (e.h && !ck_put(DictKey{e.head, e.len, e.id}, (uint32_t)e.h)) {
+                    ok = false;
+                    break;
+                }
+            if (ok) break;
+            cap *= 2;
+        }
+        ck_dirty_.clear();
+        ++ck_gen_;
+    }
+
     void rehash(size_t cap) {
         std::vector<DictEnt> old;
         old.swap(tab_);
@@ -139,15 +181,16 @@ class WordDict {
                 while (tab_[i].h) i = (i + 1) & mask_;
                 tab_[i] = e;
             }
-        dirty_.clear();
-        ++gen_;
     }
     std::vector<DictEnt> tab_;
     std::vector<uint8_t> arena_;
-    std::vector<uint32_t> dirty_;
     size_t mask_ = 0, count_ = 0;
-    uint64_t gen_ = 0;
     uint32_t next_id_ = W_FIRST;
+    std::vector<DictKey> ck_;
+    std::vector<uint32_t> ck_h_;
+    std::vector<uint32_t> ck_dirty_;
+    std::vector<DictTail> tails_;
+    uint64_t ck_gen_ = 0;
 };
 
 struct TWord {
@@ -281,6 +324,8 @@ struct tm_batch {
     unsigned long long *d_sqkey = nullptr, *d_sokey = nullptr;
     size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipEvent_t evt = nullptr;   // before the device tokeniser (fresh launches)
+    bool tok_timed = false;     // the last launch tokenised: evt..ev0 is its time
     bool launched = false, done = false;
     bool csr = true;   // the last launch built the CSR (false: async, rows left in staging)
     uint64_t seq = 0;  // launch sequence number while its results may be read (0: none)
@@ -366,7 +411,8 @@ struct tm_batch {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev2) (void)hipEventDestroy(ev2);
-        ev0 = ev1 = ev2 = nullptr;
+        if (evt) (void)hipEventDestroy(evt);
+        ev0 = ev1 = ev2 = evt = nullptr;
     }
 };
 
@@ -501,16 +547,18 @@ struct tm_engine {
     std::vector<tm_batch*> readers;
     uint64_t upload_seq = 0;             // async trie uploads recorded on ev_sync
     bool delta_inflight = false;
-    // device word dictionary (device tokeniser): verbatim table + arena
-    DictEnt* d_dict = nullptr;
-    size_t d_dict_n = 0;            // table slots on the device
+    // device word dictionary (device tokeniser): cuckoo key table, tails, arena
+    DictKey* d_dkey = nullptr;
+    size_t d_dict_n = 0;            // cuckoo slots on the device
     uint64_t d_dict_gen = ~0ull;    // dict.gen() of the device table
+    DictTail* d_tail = nullptr;
+    size_t c_tail = 0, tails_uploaded = 0;
     uint8_t* d_arena = nullptr;
     size_t c_arena = 0, arena_uploaded = 0;
     uint32_t* h_dxidx = nullptr;
-    DictEnt* h_dxval = nullptr;
+    DictKey* h_dxval = nullptr;
     uint32_t* d_dxidx = nullptr;
-    DictEnt* d_dxval = nullptr;
+    DictKey* d_dxval = nullptr;
     size_t ch_dxidx = 0, ch_dxval = 0, cd_dxidx = 0, cd_dxval = 0;
     bool dev_tok = true;            // TM_CFG_HOST_TOKENIZE / TM_HOST_TOKENIZE=1: tokenise on the host
 
@@ -1384,8 +1432,9 @@ struct tm_engine {
         if (full_dirty || !dirty.empty() || d_nslots != slots.size() || needs_repack()) return true;
         if (full_f_dirty || !dirty_f.empty() || fbytes.size() > fbytes_uploaded) return true;
         if (c_foff < n_parent.size() || c_flen < n_parent.size() || c_fbytes < fbytes.size() + 1) return true;
-        if (dev_tok && (d_dict_n != dict.table().size() || d_dict_gen != dict.gen() || !dict.dirty().empty() ||
-                        dict.arena().size() > arena_uploaded || c_arena < dict.arena().size() + 1))
+        if (dev_tok && (d_dict_n != dict.keys().size() || d_dict_gen != dict.gen() || !dict.dirty().empty() ||
+                        dict.tails().size() > tails_uploaded || dict.arena().size() > arena_uploaded ||
+                        c_arena < dict.arena().size() + 1))
             return true;
         return false;
     }
@@ -1494,25 +1543,28 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // word dictionary -> HBM: the whole table after a rehash, else the slots
-    // written since the last upload; the arena's new tail
+    // word dictionary -> HBM: the whole cuckoo table after a rebuild, else the
+    // slots written since the last upload; the tails' and the arena's new ends
     int sync_dict(bool& pageable_used, bool& async_used) {
         int rc;
-        const std::vector<DictEnt>& tab = dict.table();
+        const std::vector<DictKey>& tab = dict.keys();
+        const std::vector<DictTail>& tl = dict.tails();
         const std::vector<uint8_t>& ar = dict.arena();
         std::vector<uint32_t>& dx = dict.dirty();
         if (d_dict_n != tab.size()) {
-            dev_free(d_dict);
-            HIP_OK(hipMalloc((void**)&d_dict, tab.size() * sizeof(DictEnt)));
+            dev_free(d_dkey);
+            HIP_OK(hipMalloc((void**)&d_dkey, tab.size() * sizeof(DictKey)));
             d_dict_n = tab.size();
             d_dict_gen = ~0ull;
         }
         if (d_dict_gen != dict.gen() || dx.size() > tab.size() / 8) {
             pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_dict, tab.data(), tab.size() * sizeof(DictEnt), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_dkey, tab.data(), tab.size() * sizeof(DictKey), hipMemcpyHostToDevice, stream));
             d_dict_gen = dict.gen();
             dx.clear();
         } else if (!dx.empty()) {
+            std::sort(dx.begin(), dx.end());
+            dx.erase(std::unique(dx.begin(), dx.end()), dx.end());   // a slot may move twice: scatter it once
             const size_t nd = dx.size();
             if ((rc = host_reserve(h_dxidx, ch_dxidx, nd))) return rc;
             if ((rc = host_reserve(h_dxval, ch_dxval, nd))) return rc;
@@ -1523,10 +1575,20 @@ struct tm_engine {
                 h_dxval[k] = tab[dx[k]];
             }
             HIP_OK(hipMemcpyAsync(d_dxidx, h_dxidx, nd * 4, hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_dxval, h_dxval, nd * sizeof(DictEnt), hipMemcpyHostToDevice, stream));
-            HIP_OK(launch_scatter_dict(d_dict, d_dxidx, d_dxval, (uint32_t)nd, stream));
+            HIP_OK(hipMemcpyAsync(d_dxval, h_dxval, nd * sizeof(DictKey), hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_keys(d_dkey, d_dxidx, d_dxval, (uint32_t)nd, stream));
             dx.clear();
             async_used = true;
+        }
+        if (c_tail < tl.size() + 1) {
+            if ((rc = dev_reserve(d_tail, c_tail, tl.size() + tl.size() / 2 + 64))) return rc;
+            tails_uploaded = 0;
+        }
+        if (tl.size() > tails_uploaded) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(d_tail + tails_uploaded, tl.data() + tails_uploaded,
+                                  (tl.size() - tails_uploaded) * sizeof(DictTail), hipMemcpyHostToDevice, stream));
+            tails_uploaded = tl.size();
         }
         if (c_arena < ar.size() + 1) {
             if ((rc = dev_reserve(d_arena, c_arena, ar.size() + 1))) return rc;
@@ -1691,9 +1753,10 @@ struct tm_engine {
         if (!n) HIP_OK(hipMemsetAsync(d_toff, 0, 4, stream));
         TokArgs t{};
         t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
-        t.dict = d_dict; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+        t.keys = d_dkey; t.tails = d_tail; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
         t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
         t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
+        t.tile_topics = tok_tile_topics(n, nbytes);
         ScanArgs ts{};
         ts.block_sums = b->d_bsums;
         HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
@@ -1805,6 +1868,7 @@ struct tm_engine {
             HIP_OK(hipEventCreate(&b->ev0));
             HIP_OK(hipEventCreate(&b->ev1));
             HIP_OK(hipEventCreate(&b->ev2));
+            HIP_OK(hipEventCreate(&b->evt));
         }
         return TM_OK;
     }
@@ -1968,11 +2032,15 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
-    // An async slot's batch: blk = pinned [offs (n+1) u64 from 0 | bytes],
+    // offsets block of a packed batch, padded so the bytes start 16-B aligned
+    // (the tokeniser stages tiles with 16-B loads from 16-B aligned windows)
+    static size_t packed_head(uint32_t n) { return (((size_t)n + 1) * 8 + 15) & ~(size_t)15; }
+
+    // An async slot's batch: blk = pinned [offs (n+1) u64 from 0 | pad | bytes],
     // one H2D on the slot's stream (topic lengths were checked at submit).
     int upload_packed(tm_batch* b, const uint8_t* blk, uint32_t n, uint64_t nbytes) {
         int rc;
-        const size_t head = ((size_t)n + 1) * 8;
+        const size_t head = packed_head(n);
         if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
         b->dedup = false;
         b->n_pub = n;
@@ -2016,16 +2084,19 @@ struct tm_engine {
         }
         const bool tokenize_now = b->dev_tok && b->tok_dict != dict.size();
         if (!tokenize_now) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
+        b->tok_timed = tokenize_now && csr;
+        if (b->tok_timed) HIP_OK(hipEventRecord(b->evt, S));
         if (tokenize_now) {
             b->tok_dict = dict.size();
             TokArgs t{};
             t.zero = reinterpret_cast<uint32_t*>(b->d_hdr);   // the tokeniser's first kernel clears ctrl + stats
             t.zero_words = tm_batch::HDR_FIXED / 4;
             t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
-            t.dict = d_dict; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+            t.keys = d_dkey; t.tails = d_tail; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
             t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
+            t.tile_topics = tok_tile_topics(b->n, b->nwords - b->n);   // nwords = bytes + topics (reserve_tokens)
             ScanArgs ts{};
             ts.block_sums = b->d_bsums;
             HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
@@ -2109,9 +2180,11 @@ struct tm_engine {
     }
 
     void fill_stats(tm_batch* b) {
-        float ms_match = 0, ms_total = 0;
+        float ms_match = 0, ms_total = 0, ms_tok = 0;
         (void)hipEventElapsedTime(&ms_match, b->ev0, b->ev1);
         (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
+        if (b->tok_timed) (void)hipEventElapsedTime(&ms_tok, b->evt, b->ev0);
+        b->st.ms_tokenize = ms_tok;
         b->st.topics = b->n;
         b->st.visits = b->h_stats[ST_VISITS];
         b->st.hash_hits = b->h_stats[ST_HASH];
@@ -2355,10 +2428,10 @@ struct tm_engine {
     // slot's pinned buffers -- all on the slot's stream; ev_done marks the end.
     int slot_launch(AsyncSlot* sl) {
         const uint32_t n = (uint32_t)sl->calls.size();
-        const size_t nb = sl->bytes.size(), head = ((size_t)n + 1) * 8;
+        const size_t nb = sl->bytes.size(), head = packed_head(n);
         int rc;
         if ((rc = host_reserve(sl->h_in, sl->c_in, head + nb))) return rc;
-        memcpy(sl->h_in, sl->offs.data(), head);
+        memcpy(sl->h_in, sl->offs.data(), ((size_t)n + 1) * 8);
         if (nb) memcpy(sl->h_in + head, sl->bytes.data(), nb);
         std::lock_guard<std::recursive_mutex> g(mu);
         HIP_OK(hipSetDevice(device));
@@ -2532,7 +2605,7 @@ struct tm_engine {
             scratch.release();
             tokb.release();
             dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
-            dev_free(d_dict); dev_free(d_arena); dev_free(d_dxidx); dev_free(d_dxval);
+            dev_free(d_dkey); dev_free(d_tail); dev_free(d_arena); dev_free(d_dxidx); dev_free(d_dxval);
             if (h_dxidx) (void)hipHostFree(h_dxidx);
             if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
@@ -2889,6 +2962,14 @@ int tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row, const
     if (d_row) *d_row = b->d_rowoff;
     if (d_ids) *d_ids = b->d_ids;
     if (n) *n = b->total;
+    return TM_OK;
+}
+
+int tm_batch_retokenize(tm_engine* e, tm_batch* b) {
+    if (!e || !b) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (!b->dev_tok) return TM_EINVAL;
+    b->tok_dict = ~0ull;
     return TM_OK;
 }
 

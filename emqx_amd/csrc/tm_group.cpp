@@ -227,6 +227,7 @@ int tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out) {
         s.matches += p.matches; s.slow_topics += p.slow_topics; s.overflow_tiles += p.overflow_tiles;
         s.ms_match = std::max(s.ms_match, p.ms_match);
         s.ms_total = std::max(s.ms_total, p.ms_total);
+        s.ms_tokenize = std::max(s.ms_tokenize, p.ms_tokenize);
     }
     *out = s;
     return TM_OK;

@@ -265,6 +265,23 @@ struct DictEnt {
 };
 static_assert(sizeof(DictEnt) == 48, "dictionary entry is 48 bytes (three 16-B loads)");
 
+// The device tokeniser's dictionary: a 2-choice cuckoo table of probe keys
+// (a word lives in slot h1 & mask or ck_alt(h1) & mask, h1 = hash_word), so a
+// lookup is two independent 16-B loads and no probe chain; head + len are the
+// whole word up to 8 bytes, longer words also compare their DictTail (by id).
+// Mirrored from the host interner (tm_engine.cpp WordDict).
+struct DictKey {
+    uint64_t head;   // bytes 0..7, little-endian, zero-padded
+    uint32_t len;
+    uint32_t id;     // 0 = empty slot (ids start at W_FIRST)
+};
+struct DictTail {
+    uint64_t head2;  // bytes 8..15, zero-padded
+    uint64_t off;    // arena offset of the word (bytes 16.. are compared there)
+};
+static_assert(sizeof(DictTail) == 16, "dictionary tail is one 16-B load");
+static_assert(sizeof(DictKey) == 16, "dictionary key is one 16-B load");
+
 __host__ __device__ inline uint64_t le_bytes(const uint8_t* p, uint32_t n) {   // n <= 8
     uint64_t v = 0;
     for (uint32_t k = 0; k < n; ++k) v |= (uint64_t)p[k] << (8 * k);
@@ -296,6 +313,11 @@ __host__ __device__ inline uint32_t hw_final(uint32_t h, uint32_t n) {
     return h | 1u;
 }
 constexpr uint32_t HW_SEED = 0x9E3779B9u;
+// the second cuckoo slot of a word with hash h1
+__host__ __device__ inline uint32_t ck_alt(uint32_t h) {
+    h *= 0x9E3779B1u;
+    return h ^ (h >> 15) ^ 0x5BD1E995u;
+}
 
 // Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
 // the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp
@@ -311,10 +333,11 @@ struct TokArgs {
     const uint64_t* offs;     // n + 1 absolute offsets (caller's), minus base
     uint64_t base;
     uint32_t n;
-    const DictEnt* dict;
-    uint64_t dict_mask;       // table size - 1 (power of two)
+    const DictKey* keys;      // cuckoo table of probe keys (DictKey)
+    const DictTail* tails;    // by word id
+    uint64_t dict_mask;       // cuckoo table size - 1 (power of two)
     const uint8_t* arena;
-    uint32_t* wcount;         // pass 1: words per TILE (ntiles + 1 entries)
+    uint32_t* wcount;         // pass 1: words per tile (ntiles + 1 entries), scanned in place
     uint8_t* tflags;
     uint32_t* toff;           // n + 1 word offsets
     const uint32_t* bsums;    // scan block offsets of the tile scan (tm_scan_sums)
@@ -324,8 +347,11 @@ struct TokArgs {
     uint32_t* d_nslow;        // [0] generic-path topics, [1] total words; zeroed by pass 1
     uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
     uint32_t zero_words;
+    uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
 };
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
+// topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
+uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 
 // tm_export_host: an async batch's per-topic results and rows -> pinned host memory
 struct ExportArgs {
@@ -340,7 +366,8 @@ struct ExportArgs {
     uint64_t rows_cap;        // entries h_rows holds
 };
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
-hipError_t launch_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n, hipStream_t s);
+// dirty cuckoo slots -> the device table
+hipError_t launch_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKey* vals, uint32_t n, hipStream_t s);
 
 // shard of a (w0, w1) literal prefix; host and device agree (tm_filter_shard)
 __host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uint32_t nshards) {

@@ -1328,8 +1328,9 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 //                 coalesced run.  Tiles too long for the LDS budget take a
 //                 lane-per-topic path that reads the bytes from HBM.
 
-constexpr uint32_t TOK_BYTES = 4096;   // LDS bytes per tile (4-aligned window)
-constexpr uint32_t TOK_WORDS = 512;    // LDS words per tile
+constexpr uint32_t TOK_LANE_BYTES = 48;                 // bytes of the window each lane splits
+constexpr uint32_t TOK_BYTES = 64 * TOK_LANE_BYTES;     // LDS bytes per tile (16-B aligned window)
+constexpr uint32_t TOK_WORDS = 512;                     // words per tile on the LDS path
 
 // bytes with value v in the 4 bytes of x (SWAR): each matching byte -> 0x80
 __device__ __forceinline__ uint32_t byte_eq(uint32_t x, uint32_t v) {
@@ -1348,8 +1349,24 @@ __device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint32_t n, bool& irre
     return C_ABOVE;
 }
 
-// id of word p[0..n) in the uploaded interner table (W_UNKNOWN if absent);
-// P is an LDS or global byte pointer
+// does the cuckoo key e (DictKey as uint4) hold the word of (head, n) whose
+// bytes 8.. are p[8..n)?  (words over 8 bytes: the tail by id, then the arena)
+template <class P>
+__device__ __forceinline__ bool ck_match(const TokArgs& a, const uint4& e, uint64_t head, uint32_t n, P p) {
+    if (e.z != n || e.x != (uint32_t)head || e.y != (uint32_t)(head >> 32)) return false;
+    if (n <= 8) return true;
+    const DictTail t = a.tails[e.w];
+    uint64_t h2 = 0;
+    for (uint32_t k = 8; k < 16 && k < n; ++k) h2 |= (uint64_t)p[k] << (8 * (k - 8));
+    if (t.head2 != h2) return false;
+    const uint8_t* q = a.arena + t.off;
+    for (uint32_t k = 16; k < n; ++k)
+        if (q[k] != p[k]) return false;
+    return true;
+}
+
+// id of word p[0..n) in the device dictionary (W_UNKNOWN if absent); P is an
+// LDS or global byte pointer
 template <class P>
 __device__ __forceinline__ uint32_t dict_find(const TokArgs& a, P p, uint32_t n) {
     uint32_t h32 = HW_SEED;
@@ -1358,22 +1375,14 @@ __device__ __forceinline__ uint32_t dict_find(const TokArgs& a, P p, uint32_t n)
         for (uint32_t k = 0; k < 4 && i + k < n; ++k) v |= (uint32_t)p[i + k] << (8 * k);
         h32 = hw_step(h32, v);
     }
-    const uint64_t h = hw_final(h32, n);
-    uint64_t head = 0, head2 = 0;
+    const uint32_t h = hw_final(h32, n), m = (uint32_t)a.dict_mask;
+    uint64_t head = 0;
     for (uint32_t k = 0; k < 8 && k < n; ++k) head |= (uint64_t)p[k] << (8 * k);
-    for (uint32_t k = 8; k < 16 && k < n; ++k) head2 |= (uint64_t)p[k] << (8 * (k - 8));
-    uint64_t s = h & a.dict_mask;
-    for (uint64_t probe = 0; probe <= a.dict_mask; ++probe) {
-        const DictEnt e = a.dict[s];
-        if (e.h == 0) return W_UNKNOWN;
-        if (e.h == h && e.len == n && e.head == head && e.head2 == head2) {
-            const uint8_t* q = a.arena + e.off;
-            uint32_t k = 16;
-            while (k < n && q[k] == p[k]) ++k;
-            if (k >= n) return e.id;
-        }
-        s = (s + 1) & a.dict_mask;
-    }
+    const uint4 e1 = *reinterpret_cast<const uint4*>(a.keys + (h & m));
+    if (e1.w == 0) return W_UNKNOWN;   // slots never empty again once filled: absent
+    if (ck_match(a, e1, head, n, p)) return e1.w;
+    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (ck_alt(h) & m));
+    if (ck_match(a, e2, head, n, p)) return e2.w;
     return W_UNKNOWN;
 }
 
@@ -1399,36 +1408,65 @@ __device__ __forceinline__ void tok_append_slow(const TokArgs& a, bool slow, uin
     if (slow) a.slow_list[base + prefix_count(m)] = t;
 }
 
-// pass 1: words per tile
+// '/' bytes of the 16 bytes x at tile-relative offset q that lie in [lo, hi)
+__device__ __forceinline__ uint32_t slashes16(const uint4& x, int64_t q, int64_t lo, int64_t hi) {
+    const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t m = byte_eq(d[j], '/');
+        const int64_t s = q + 4 * j;
+        if (s < lo) m = (lo - s >= 4) ? 0u : m & (~0u << (8 * (uint32_t)(lo - s)));
+        if (s + 4 > hi) m = (s >= hi) ? 0u : m & ((1u << (8 * (uint32_t)(hi - s))) - 1u);
+        c += __popc(m);
+    }
+    return c;
+}
+
+// pass 1: words per tile = '/' bytes + topics, from 16-B loads of the tile's
+// 16-B aligned window (two tiles per iteration: twice the loads in flight);
+// also clears the launch's control words
 __global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
     const uint32_t lane = threadIdx.x;
     if (blockIdx.x == 0) {   // the launch's control words (kernels after this one use them)
         if (lane < 2) a.d_nslow[lane] = 0;
         for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
     }
-    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t t0 = tile * TILE, tend = min(t0 + TILE, a.n);
-        const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
-        const uint64_t a0 = b0 & ~3ull;
-        uint32_t slashes = 0;
-        for (uint64_t p = a0 + 4ull * lane; p < b1; p += 256) {
-            uint32_t x = *reinterpret_cast<const uint32_t*>(a.bytes + p);
-            uint32_t m = byte_eq(x, '/');
-            // drop bytes outside [b0, b1)
-            if (p < b0) m &= ~0u << (8 * (uint32_t)(b0 - p));
-            if (p + 4 > b1) m &= (1u << (8 * (uint32_t)(b1 - p))) - 1u;
-            slashes += __popc(m);
+    const uint32_t tt = a.tile_topics;
+    const uint32_t ntiles = (a.n + tt - 1) / tt;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += 2 * gridDim.x) {
+        const uint32_t tile2 = tile + gridDim.x;
+        const bool two = tile2 < ntiles;
+        const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n);
+        const uint32_t u0 = two ? tile2 * tt : t0, uend = two ? min(u0 + tt, a.n) : tend;
+        const int64_t b0 = (int64_t)(a.offs[t0] - a.base), b1 = (int64_t)(a.offs[tend] - a.base);
+        const int64_t c0 = (int64_t)(a.offs[u0] - a.base), c1 = (int64_t)(a.offs[uend] - a.base);
+        const int64_t a0 = b0 & ~15ll, d0 = c0 & ~15ll;
+        uint32_t s1 = 0, s2 = 0;
+        int64_t p = a0 + 16 * lane, r = d0 + 16 * lane;
+        for (; p < b1 || (two && r < c1); p += 1024, r += 1024) {
+            uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+            if (p < b1) x = *reinterpret_cast<const uint4*>(a.bytes + p);
+            if (two && r < c1) y = *reinterpret_cast<const uint4*>(a.bytes + r);
+            if (p < b1) s1 += slashes16(x, p, b0, b1);
+            if (two && r < c1) s2 += slashes16(y, r, c0, c1);
         }
-        for (int o = 32; o > 0; o >>= 1) slashes += __shfl_xor(slashes, o, 64);
-        if (lane == 0) a.wcount[tile] = slashes + (tend - t0);
+        for (int o = 32; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+        }
+        if (lane == 0) a.wcount[tile] = s1 + (tend - t0);
+        if (lane == 0 && two) a.wcount[tile2] = s2 + (uend - u0);
     }
 }
 
 struct alignas(16) TokLds {
-    uint8_t bytes[TOK_BYTES + 16];   // + 16: 8-byte reads past a word stay in the array
-    uint32_t wpos[TOK_WORDS];        // start (in bytes[]) | len << 16
-    uint32_t out[TOK_WORDS];
+    uint8_t bytes[TOK_BYTES + 32];      // the tile's window; + 32: 8-byte reads past a word stay inside
+    uint64_t tsb[TOK_BYTES / 64 + 1];   // topic-start bitmap of the window (+1: a lane's bits may straddle)
+    uint16_t wst[TOK_WORDS];            // word start | 0x8000 when it is its topic's first word
+    uint8_t wtop[TOK_WORDS];            // tile-local topic of each word
+    uint32_t ttoff[TILE + 1];           // tile-local first word of each topic; [cnt] = words
+    uint32_t tirr[TILE];                // a word of the topic starts with '+' but is not '+'
 };
 
 // 8 bytes at byte offset s of a 4-aligned LDS array (any alignment of s)
@@ -1445,97 +1483,87 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // fir
     return k >= 8 ? v : (v & ((1ull << (8u * k)) - 1ull));
 }
 
+// byte_eq's 0x80 flags of one dword -> 4 bits (byte j -> bit j)
+__device__ __forceinline__ uint32_t gather4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
+
 #ifndef TM_TOK_WPL
-#define TM_TOK_WPL 4
+#define TM_TOK_WPL 2
 #endif
 constexpr uint32_t TOK_WPL = TM_TOK_WPL;   // words per lane per lookup round (register budget: occupancy)
 
-// Dictionary ids of the tile's words w = lane + 64 k: TOK_WPL words per lane
-// at a time, their hashes and heads from LDS first, then one probe round per
-// collision-chain step with every pending probe of the lane in flight.
-__device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw) {
+// The tile's words w = lane + 64 k, TOK_WPL per lane at a time: start from
+// wst, length from the next word's start (the last word of a topic ends at
+// the next topic's start, others one byte ('/') before the next word), class
+// and reserved atoms, then the dictionary: hash and head from LDS, every
+// word's primary cuckoo slot loaded at once; the alternate slot only when the
+// primary holds another word (cuckoo slots never empty again once filled, so
+// an empty primary slot means the word is absent).  Lookups are bound by L2
+// requests, not instructions: one per word is the point.
+// Entries (class << 29 | id) go straight to words[].
+__device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw, uint32_t wend,
+                                           uint64_t tile_base) {
     const uint32_t lane = threadIdx.x;
+    const uint32_t mask = (uint32_t)a.dict_mask;
     for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
-        uint64_t h[TOK_WPL], head[TOK_WPL], head2[TOK_WPL];
-        uint32_t slot[TOK_WPL], ent[TOK_WPL];
-        bool pend[TOK_WPL];
+        uint64_t head[TOK_WPL];
+        uint32_t ent[TOK_WPL], len[TOK_WPL], st[TOK_WPL], hh[TOK_WPL], pend = 0;
+        uint4 e[TOK_WPL];
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
             const uint32_t w = base + lane + 64 * k;
-            pend[k] = false;
             ent[k] = 0;
-            h[k] = head[k] = head2[k] = 0;
-            slot[k] = 0;
+            head[k] = 0;
+            len[k] = 0;
+            st[k] = 0;
+            hh[k] = 0;
             if (w >= tw) continue;
-            const uint32_t wp = L.wpos[w];
-            const uint32_t s0 = wp & 0xFFFF, n = wp >> 16;
+            const uint32_t s0 = L.wst[w] & 0x7FFFu;
+            const uint32_t nx = w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u);
+            const uint32_t n = (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u);
             const uint8_t c0 = n ? L.bytes[s0] : 0;
             bool irr = false;
-            const uint32_t cls = tok_class(c0, n, irr);
-            ent[k] = cls << WID_BITS;
+            ent[k] = tok_class(c0, n, irr) << WID_BITS;
+            if (irr) L.tirr[L.wtop[w]] = 1;
             if (n == 0) { ent[k] |= W_EMPTY; continue; }
             if (n == 1 && c0 == '+') { ent[k] |= W_PLUS; continue; }
             if (n == 1 && c0 == '#') { ent[k] |= W_HASH; continue; }
-            // bytes 0..15 zero-padded past n: the inline compare keys and the first four hash dwords
             const uint64_t c0w = low_bytes(lds_u64(L.bytes, s0), n < 8 ? n : 8);
-            const uint64_t c1w = n > 8 ? low_bytes(lds_u64(L.bytes, s0 + 8), n - 8 < 8 ? n - 8 : 8) : 0ull;
             uint32_t h32 = hw_step(HW_SEED, (uint32_t)c0w);
             if (n > 4) h32 = hw_step(h32, (uint32_t)(c0w >> 32));
-            if (n > 8) h32 = hw_step(h32, (uint32_t)c1w);
-            if (n > 12) h32 = hw_step(h32, (uint32_t)(c1w >> 32));
-            for (uint32_t i = 16; i < n; i += 8) {   // rare: words longer than 16 bytes
+            for (uint32_t i = 8; i < n; i += 8) {   // words over 8 bytes
                 const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
                 h32 = hw_step(h32, (uint32_t)c);
                 if (n - i > 4) h32 = hw_step(h32, (uint32_t)(c >> 32));
             }
-            h[k] = hw_final(h32, n);
+            const uint32_t h = hw_final(h32, n);
+            e[k] = *reinterpret_cast<const uint4*>(a.keys + (h & mask));
+            hh[k] = h;
             head[k] = c0w;
-            head2[k] = c1w;
-            slot[k] = (uint32_t)(h[k] & a.dict_mask);
-            pend[k] = true;
+            len[k] = n;
+            st[k] = s0;
+            pend |= 1u << k;
         }
-        for (uint64_t round = 0; round <= a.dict_mask; ++round) {
-            bool any = false;
-            uint4 e0[TOK_WPL], e1[TOK_WPL];   // {h, head}, {head2, len, id}
+        // primary slots: a match or an empty slot settles the word
 #pragma unroll
-            for (uint32_t k = 0; k < TOK_WPL; ++k)
-                if (pend[k]) {
-                    const uint4* ep = reinterpret_cast<const uint4*>(a.dict + slot[k]);
-                    e0[k] = ep[0];
-                    e1[k] = ep[1];
-                }
-#pragma unroll
-            for (uint32_t k = 0; k < TOK_WPL; ++k) {
-                if (!pend[k]) continue;
-                const uint64_t eh = ((uint64_t)e0[k].y << 32) | e0[k].x;
-                const uint64_t ehead = ((uint64_t)e0[k].w << 32) | e0[k].z;
-                const uint64_t ehead2 = ((uint64_t)e1[k].y << 32) | e1[k].x;
-                if (eh == 0) {                 // not in the dictionary: W_UNKNOWN (0)
-                    pend[k] = false;
-                    continue;
-                }
-                const uint32_t wp = L.wpos[base + lane + 64 * k];
-                const uint32_t n = wp >> 16;
-                if (eh == h[k] && e1[k].z == n && ehead == head[k] && ehead2 == head2[k]) {
-                    bool eq = true;
-                    if (n > 16) {   // rare: bytes 16.. from the arena
-                        const uint8_t* q = a.arena + a.dict[slot[k]].off;
-                        for (uint32_t i = 16; i < n && eq; ++i) eq = q[i] == L.bytes[(wp & 0xFFFF) + i];
-                    }
-                    if (eq) {
-                        ent[k] |= e1[k].w;
-                        pend[k] = false;
-                        continue;
-                    }
-                }
-                slot[k] = (uint32_t)((slot[k] + 1) & a.dict_mask);
-                any = true;
+        for (uint32_t k = 0; k < TOK_WPL; ++k) {
+            if (!(pend >> k & 1u)) continue;
+            if (e[k].w == 0) {
+                pend &= ~(1u << k);
+            } else if (ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) {
+                ent[k] |= e[k].w;
+                pend &= ~(1u << k);
             }
-            if (!__any(any)) break;
         }
+        // alternate slots of the rest, all in flight
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k)
-            if (base + lane + 64 * k < tw) L.out[base + lane + 64 * k] = ent[k];
+            if (pend >> k & 1u) e[k] = *reinterpret_cast<const uint4*>(a.keys + (ck_alt(hh[k]) & mask));
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_WPL; ++k) {
+            if ((pend >> k & 1u) && ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) ent[k] |= e[k].w;
+            const uint32_t w = base + lane + 64 * k;
+            if (w < tw && tile_base + w < a.words_cap) a.words[tile_base + w] = ent[k];
+        }
     }
 }
 
@@ -1565,118 +1593,135 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
 
 // pass 2 (after the scan of the tile counts): word entries, offsets, flags
 #ifndef TM_TOK_WPE
-#define TM_TOK_WPE 4
+#define TM_TOK_WPE 5
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
     __shared__ TokLds L;
     const uint32_t lane = threadIdx.x;
-    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    const uint32_t tt = a.tile_topics;
+    const uint32_t ntiles = (a.n + tt - 1) / tt;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t t0 = tile * TILE, tend = min(t0 + TILE, a.n), cnt = tend - t0;
+        const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n), cnt = tend - t0;
         const uint32_t t = t0 + lane;
         const bool valid = lane < cnt;
-        // everything that does not depend on the tile's bytes is loaded first
-        const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
         const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
         const uint64_t my_b = valid ? a.offs[t] - a.base : 0, my_e = valid ? a.offs[t + 1] - a.base : 0;
-        const uint64_t a0 = b0 & ~3ull;
+        const uint64_t a0 = b0 & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
+        const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
         bool slow = false;
-        if (b1 - a0 <= TOK_BYTES) {
-            // stage the tile's bytes (4-aligned window starting at a0): every
-            // load of the lane in flight before the first LDS store
-            constexpr uint32_t PER_LANE = TOK_BYTES / 256;
-            uint32_t v[PER_LANE];
+        // the LDS path: the window fits and no topic is empty (an empty topic
+        // starts where the next one does: one bit cannot mark both)
+        bool lds = b1 - a0 <= TOK_BYTES && !__any(valid && my_b == my_e);
+        uint32_t tw = 0, wend = 0, incl = 0, mine = 0;
+        uint64_t S = 0, TS = 0;
+        const uint32_t lb = lane * TOK_LANE_BYTES;   // my 48 bytes of the window
+        if (lds) {
+            wend = (uint32_t)(b1 - a0);
+            const uint32_t r0 = (uint32_t)(b0 - a0);
+            uint4 v[TOK_LANE_BYTES / 16];
 #pragma unroll
-            for (uint32_t k = 0; k < PER_LANE; ++k) {
-                const uint64_t p = a0 + 4ull * (lane + 64 * k);
-                v[k] = p < b1 ? *reinterpret_cast<const uint32_t*>(a.bytes + p) : 0u;
-            }
+            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
+                v[k] = lb + 16 * k < wend ? *reinterpret_cast<const uint4*>(a.bytes + a0 + lb + 16 * k)
+                                          : make_uint4(0, 0, 0, 0);
 #pragma unroll
-            for (uint32_t k = 0; k < PER_LANE; ++k) {
-                const uint64_t p = a0 + 4ull * (lane + 64 * k);
-                if (p < b1) *reinterpret_cast<uint32_t*>(L.bytes + (p - a0)) = v[k];
-            }
+            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
+                *reinterpret_cast<uint4*>(L.bytes + lb + 16 * k) = v[k];
+            for (uint32_t i = lane; i < TOK_BYTES / 64 + 1; i += 64) L.tsb[i] = 0;
+            if (lane < TILE) L.tirr[lane] = 0;
             __syncthreads();
-            // split my topic in LDS: '/' found four bytes at a time (SWAR)
-            uint32_t tb = 0, te = 0, nw = 0;
             if (valid) {
-                tb = (uint32_t)(my_b - a0);
-                te = (uint32_t)(my_e - a0);
-                nw = 1;
-                for (uint32_t q = tb & ~3u; q < te; q += 4) {
-                    uint32_t m = byte_eq(*reinterpret_cast<const uint32_t*>(L.bytes + q), '/');
-                    if (q < tb) m &= ~0u << (8u * (tb - q));
-                    if (q + 4 > te) m &= (1u << (8u * (te - q))) - 1u;
-                    nw += __popc(m);
-                }
+                const uint32_t p = (uint32_t)(my_b - a0);
+                atomicOr(reinterpret_cast<unsigned long long*>(&L.tsb[p >> 6]), 1ull << (p & 63));
             }
-            uint32_t incl = nw;
+            // '/' bytes of my 48 (inside [r0, wend)) and topic starts, as bit masks
+#pragma unroll
+            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k) {
+                S |= (uint64_t)gather4(byte_eq(v[k].x, '/')) << (16 * k);
+                S |= (uint64_t)gather4(byte_eq(v[k].y, '/')) << (16 * k + 4);
+                S |= (uint64_t)gather4(byte_eq(v[k].z, '/')) << (16 * k + 8);
+                S |= (uint64_t)gather4(byte_eq(v[k].w, '/')) << (16 * k + 12);
+            }
+            const uint32_t lo = r0 > lb ? min(r0 - lb, TOK_LANE_BYTES) : 0u;
+            const uint32_t hi = wend > lb ? min(wend - lb, TOK_LANE_BYTES) : 0u;
+            S &= ((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull);
+            __syncthreads();
+            const uint32_t q = lb >> 6, sh = lb & 63;
+            TS = L.tsb[q] >> sh;
+            if (sh) TS |= L.tsb[q + 1] << (64 - sh);
+            TS &= (1ull << TOK_LANE_BYTES) - 1ull;
+            // word starts = topic starts + '/' bytes; one scan numbers them
+            mine = (uint32_t)(__popcll(S) + __popcll(TS)) | ((uint32_t)__popcll(TS) << 16);
+            incl = mine;
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t u = __shfl_up(incl, o, 64);
                 if (lane >= (uint32_t)o) incl += u;
             }
-            const uint32_t tw = __shfl(incl, 63, 64);
-            const uint32_t woff = incl - nw;
-            if (tw <= TOK_WORDS) {
-                if (valid) {
-                    bool irregular = false;
-                    uint32_t k = woff, ws = tb;
-                    for (uint32_t q = tb & ~3u; q < te; q += 4) {
-                        uint32_t m = byte_eq(*reinterpret_cast<const uint32_t*>(L.bytes + q), '/');
-                        if (q < tb) m &= ~0u << (8u * (tb - q));
-                        if (q + 4 > te) m &= (1u << (8u * (te - q))) - 1u;
-                        while (m) {
-                            const uint32_t pos = q + (__builtin_ctz(m) >> 3);
-                            m &= m - 1;
-                            L.wpos[k++] = ws | ((pos - ws) << 16);
-                            if (pos - ws > 1 && L.bytes[ws] == '+') irregular = true;
-                            ws = pos + 1;
-                        }
-                    }
-                    L.wpos[k] = ws | ((te - ws) << 16);
-                    if (te - ws > 1 && L.bytes[ws] == '+') irregular = true;
-                    uint8_t fl = 0;
-                    if (te > tb && L.bytes[tb] == '$') fl |= TF_DOLLAR;
-                    if (irregular || nw > FAST_MAX_DEPTH) fl |= TF_SLOW;
-                    a.tflags[t] = fl;
-                    a.toff[t] = (uint32_t)(tile_base + woff);
-                    slow = (fl & TF_SLOW) != 0;
-                }
+            tw = __shfl(incl, 63, 64) & 0xFFFFu;
+            if (tw > TOK_WORDS) {
+                lds = false;
                 __syncthreads();
-                tok_lookup(a, L, tw);            // the tile's words, round-robin over lanes
-                __syncthreads();
-                for (uint32_t w = lane; w < tw; w += 64)
-                    if (tile_base + w < a.words_cap) a.words[tile_base + w] = L.out[w];
-                if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
-                tok_append_slow(a, slow, t);
-                __syncthreads();
-                continue;
             }
         }
-        // long tile: one lane per topic, bytes from HBM; in-tile offsets by a
-        // wave scan of the per-topic word counts ('/' + 1)
-#ifdef TOK_NO_FALLBACK
-        continue;
+        uint32_t nw = 0, tincl = 0;
+        if (!lds) {
+            // long tile: one lane per topic, bytes from HBM; in-tile offsets by
+            // a wave scan of the per-topic word counts ('/' + 1)
+            if (valid) {
+                nw = 1;
+                for (uint64_t i = my_b; i < my_e; ++i) nw += a.bytes[i] == '/';
+            }
+            tincl = nw;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(tincl, o, 64);
+                if (lane >= (uint32_t)o) tincl += u;
+            }
+            tw = __shfl(tincl, 63, 64);
+        }
+        if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
+        if (lds) {
+            uint32_t wi = (incl - mine) & 0xFFFFu;            // my first word
+            int32_t tc = (int32_t)((incl - mine) >> 16) - 1;   // the topic my first byte is in
+            uint64_t m = S | TS;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t pos = lb + b;
+                if (TS >> b & 1ull) {
+                    ++tc;
+                    L.ttoff[tc] = wi;
+                    L.wst[wi] = (uint16_t)(pos | 0x8000u);
+                    L.wtop[wi++] = (uint8_t)tc;
+                }
+                if (S >> b & 1ull) {
+                    L.wst[wi] = (uint16_t)(pos + 1);
+                    L.wtop[wi++] = (uint8_t)tc;
+                }
+            }
+            if (lane == 0) L.ttoff[cnt] = tw;
+            __syncthreads();
+#ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
+            tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
 #endif
-        uint32_t nw = 0;
-        if (valid) {
-            const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
-            nw = 1;
-            for (uint64_t i = b; i < e; ++i) nw += a.bytes[i] == '/';
+            __syncthreads();
+            if (valid) {
+                const uint32_t w0 = L.ttoff[lane], tn = L.ttoff[lane + 1] - w0;
+                uint8_t fl = 0;
+                if (L.bytes[my_b - a0] == '$') fl |= TF_DOLLAR;
+                if (L.tirr[lane] || tn > FAST_MAX_DEPTH) fl |= TF_SLOW;
+                a.tflags[t] = fl;
+                a.toff[t] = (uint32_t)(tile_base + w0);
+                slow = (fl & TF_SLOW) != 0;
+            }
+            tok_append_slow(a, slow, t);
+            __syncthreads();
+        } else {
+            const uint64_t o = tile_base + tincl - nw;
+            if (valid) {
+                a.toff[t] = (uint32_t)o;
+                tok_fill_topic_global(a, t, o, slow);
+            }
+            tok_append_slow(a, slow, t);
         }
-        uint32_t incl = nw;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(incl, o, 64);
-            if (lane >= (uint32_t)o) incl += u;
-        }
-        const uint64_t o = tile_base + incl - nw;
-        if (valid) {
-            a.toff[t] = (uint32_t)o;
-            tok_fill_topic_global(a, t, o, slow);
-        }
-        if (tend == a.n && lane == 63) a.toff[a.n] = (uint32_t)(tile_base + incl);
-        tok_append_slow(a, slow, t);
-        __syncthreads();
     }
 }
 
@@ -1702,9 +1747,9 @@ hipError_t launch_export_host(const ExportArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-__global__ void tm_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n) {
+__global__ void tm_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKey* vals, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) tab[idx[i]] = vals[i];
+    if (i < n) keys[idx[i]] = vals[i];
 }
 
 // ------------------------------------------------------------ launchers
@@ -1870,10 +1915,29 @@ hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* 
     return hipGetLastError();
 }
 
+uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes) {
+    // the most topics (64 at most) whose average bytes fill ~3/4 of the LDS window
+    uint32_t tt = TILE;
+    while (tt > 1 && (uint64_t)tt * nbytes > (uint64_t)(TOK_BYTES * 3 / 4) * (n ? n : 1)) tt >>= 1;
+    return tt;
+}
+
+// blocks of `kernel` (block threads, no dynamic LDS) the device holds at once:
+// a grid of that size runs in one round (no tail of late blocks)
+template <class K>
+static uint32_t resident_blocks(K kernel, int block) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || cus <= 0 || per <= 0)
+        return 256u * 32u;
+    return (uint32_t)(cus * per);
+}
+
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
-    const uint32_t ntiles = (a.n + TILE - 1) / TILE;
-    const uint32_t grid = ntiles ? min(ntiles, 256u * 32u) : 1u;
-    hipLaunchKernelGGL(tm_tok_count, dim3(grid), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
+    static const uint32_t cap_count = resident_blocks(tm_tok_count, 64);
+    static const uint32_t cap_fill = resident_blocks(tm_tok_fill, 64);
+    const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
+    hipLaunchKernelGGL(tm_tok_count, dim3(ntiles ? min(ntiles, cap_count) : 1u), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
     if (!a.n) return hipGetLastError();
     scan.count = a.wcount;
     scan.row_off = a.wcount;   // in place: tile counts -> block-local tile offsets
@@ -1882,12 +1946,12 @@ hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, 
     if (e != hipSuccess) return e;
     TokArgs f = a;
     f.bsums = scan.block_sums;
-    hipLaunchKernelGGL(tm_tok_fill, dim3(grid), dim3(64), 0, s, f);
+    hipLaunchKernelGGL(tm_tok_fill, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
     return hipGetLastError();
 }
 
-hipError_t launch_scatter_dict(DictEnt* tab, const uint32_t* idx, const DictEnt* vals, uint32_t n, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(tm_scatter_dict, dim3((n + 255) / 256), dim3(256), 0, s, tab, idx, vals, n);
+hipError_t launch_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKey* vals, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_scatter_keys, dim3((n + 255) / 256), dim3(256), 0, s, keys, idx, vals, n);
     return hipGetLastError();
 }
 

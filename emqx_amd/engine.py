@@ -75,6 +75,11 @@ class Batch:
         N.check(self.eng.L.tm_batch_wait(self.eng.h, self.h), "tm_batch_wait")
         return self
 
+    def retokenize(self):
+        """tm_batch_retokenize: the next launch tokenises the resident bytes again."""
+        N.check(self.eng.L.tm_batch_retokenize(self.eng.h, self.h), "tm_batch_retokenize")
+        return self
+
     def result(self):
         r = N.Result()
         N.check(self.eng.L.tm_batch_result(self.eng.h, self.h, C.byref(r)), "tm_batch_result")

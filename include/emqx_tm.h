@@ -94,6 +94,7 @@ typedef struct {
     uint64_t overflow_tiles;
     float    ms_match;      /* device time of the frontier kernel (last launch) */
     float    ms_total;      /* device time of the whole batch pipeline (last launch) */
+    float    ms_tokenize;   /* device tokeniser time of the last launch (0: tokens reused) */
 } tm_batch_stats;
 
 typedef struct {
@@ -219,6 +220,10 @@ TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
 TM_API int  tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row_offsets,
                          const uint32_t** d_ids, uint64_t* n_matches);
 TM_API void tm_batch_free(tm_engine* e, tm_batch* b);
+/* Drops the tokens of a device-tokenised batch: its next launch tokenises the
+ * resident bytes again -- a never-seen batch's full device pipeline without a
+ * new H2D (bench: pipeline_fresh_ms).  TM_EINVAL for host-tokenised batches. */
+TM_API int  tm_batch_retokenize(tm_engine* e, tm_batch* b);
 
 /* ---- routes: emqx_router + emqx_broker:aggre/1 on the device ----------- */
 /* One route of `topic` to an aggregated destination id chosen by the caller
