@@ -1408,25 +1408,26 @@ __device__ __forceinline__ void tok_append_slow(const TokArgs& a, bool slow, uin
     if (slow) a.slow_list[base + prefix_count(m)] = t;
 }
 
-// '/' bytes of the 16 bytes x at tile-relative offset q that lie in [lo, hi)
-__device__ __forceinline__ uint32_t slashes16(const uint4& x, int64_t q, int64_t lo, int64_t hi) {
-    const uint32_t d[4] = {x.x, x.y, x.z, x.w};
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t m = byte_eq(d[j], '/');
-        const int64_t s = q + 4 * j;
-        if (s < lo) m = (lo - s >= 4) ? 0u : m & (~0u << (8 * (uint32_t)(lo - s)));
-        if (s + 4 > hi) m = (s >= hi) ? 0u : m & ((1u << (8 * (uint32_t)(hi - s))) - 1u);
-        c += __popc(m);
-    }
-    return c;
+// byte_eq's 0x80 flags of one dword -> 4 bits (byte j -> bit j)
+__device__ __forceinline__ uint32_t gather4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
+
+// '/' bytes of 16 bytes, byte j -> bit j
+__device__ __forceinline__ uint32_t slash_mask16(const uint4& x) {
+    return gather4(byte_eq(x.x, '/')) | (gather4(byte_eq(x.y, '/')) << 4) | (gather4(byte_eq(x.z, '/')) << 8) |
+           (gather4(byte_eq(x.w, '/')) << 12);
 }
 
-// pass 1: words per tile = '/' bytes + topics, from 16-B loads of the tile's
-// 16-B aligned window (two tiles per iteration: twice the loads in flight);
-// also clears the launch's control words
+constexpr uint32_t TOK_RUN = 63;   // tiles per count run (their 64 boundaries: one per lane)
+
+// pass 1: words per tile = '/' bytes + topics.  Each wave takes a contiguous
+// run of tiles (a slice of the grid's share, TOK_RUN at a time): their
+// boundaries in one vector load, then the run's bytes streamed with four
+// 16-B loads per lane in flight; each lane walks a cursor over the boundaries
+// and adds its chunks' '/' counts to the tiles' LDS counters.  Block 0 also
+// clears the launch's control words.
 __global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
+    __shared__ uint64_t bnd[TOK_RUN + 1];
+    __shared__ uint32_t cnt[TOK_RUN];
     const uint32_t lane = threadIdx.x;
     if (blockIdx.x == 0) {   // the launch's control words (kernels after this one use them)
         if (lane < 2) a.d_nslow[lane] = 0;
@@ -1434,29 +1435,49 @@ __global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
     }
     const uint32_t tt = a.tile_topics;
     const uint32_t ntiles = (a.n + tt - 1) / tt;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += 2 * gridDim.x) {
-        const uint32_t tile2 = tile + gridDim.x;
-        const bool two = tile2 < ntiles;
-        const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n);
-        const uint32_t u0 = two ? tile2 * tt : t0, uend = two ? min(u0 + tt, a.n) : tend;
-        const int64_t b0 = (int64_t)(a.offs[t0] - a.base), b1 = (int64_t)(a.offs[tend] - a.base);
-        const int64_t c0 = (int64_t)(a.offs[u0] - a.base), c1 = (int64_t)(a.offs[uend] - a.base);
-        const int64_t a0 = b0 & ~15ll, d0 = c0 & ~15ll;
-        uint32_t s1 = 0, s2 = 0;
-        int64_t p = a0 + 16 * lane, r = d0 + 16 * lane;
-        for (; p < b1 || (two && r < c1); p += 1024, r += 1024) {
-            uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
-            if (p < b1) x = *reinterpret_cast<const uint4*>(a.bytes + p);
-            if (two && r < c1) y = *reinterpret_cast<const uint4*>(a.bytes + r);
-            if (p < b1) s1 += slashes16(x, p, b0, b1);
-            if (two && r < c1) s2 += slashes16(y, r, c0, c1);
+    const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    const uint32_t first = blockIdx.x * per, last = min(first + per, ntiles);
+    for (uint32_t run = first; run < last; run += TOK_RUN) {
+        const uint32_t K = min(TOK_RUN, last - run);
+        if (lane <= K) bnd[lane] = a.offs[min((run + lane) * tt, a.n)] - a.base;
+        if (lane < K) cnt[lane] = 0;
+        __syncthreads();
+        const uint64_t B0 = bnd[0], BK = bnd[K], a0 = B0 & ~15ull;
+        uint32_t j = 0;   // my cursor: the tile of my current chunk
+        for (uint64_t p0 = a0 + 16u * lane; p0 < BK; p0 += 4096) {
+            uint4 x[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint64_t p = p0 + 1024u * u;
+                x[u] = p < BK ? *reinterpret_cast<const uint4*>(a.bytes + p) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint64_t p = p0 + 1024u * u;
+                if (p >= BK) break;
+                uint32_t m = slash_mask16(x[u]);
+                if (p < B0) m &= ~0u << (uint32_t)(B0 - p);
+                if (p + 16 > BK) m &= (1u << (uint32_t)(BK - p)) - 1u;
+                while (j + 1 < K && bnd[j + 1] <= p) ++j;
+                while (m) {   // bits up to the next boundary belong to tile j
+                    const uint64_t lim = j + 1 < K ? bnd[j + 1] - p : 16u;
+                    if (lim >= 16) {
+                        atomicAdd(&cnt[j], (uint32_t)__popc(m));
+                        break;
+                    }
+                    const uint32_t below = m & ((1u << (uint32_t)lim) - 1u);
+                    if (below) atomicAdd(&cnt[j], (uint32_t)__popc(below));
+                    m &= ~((1u << (uint32_t)lim) - 1u);
+                    ++j;
+                }
+            }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
+        __syncthreads();
+        if (lane < K) {
+            const uint32_t t0 = (run + lane) * tt;
+            a.wcount[run + lane] = cnt[lane] + (min(t0 + tt, a.n) - t0);
         }
-        if (lane == 0) a.wcount[tile] = s1 + (tend - t0);
-        if (lane == 0 && two) a.wcount[tile2] = s2 + (uend - u0);
+        __syncthreads();
     }
 }
 
@@ -1483,8 +1504,6 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // fir
     return k >= 8 ? v : (v & ((1ull << (8u * k)) - 1ull));
 }
 
-// byte_eq's 0x80 flags of one dword -> 4 bits (byte j -> bit j)
-__device__ __forceinline__ uint32_t gather4(uint32_t m) { return (((m >> 7) * 0x204081u) >> 21) & 0xFu; }
 
 #ifndef TM_TOK_WPL
 #define TM_TOK_WPL 2
