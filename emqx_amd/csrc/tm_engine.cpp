@@ -53,8 +53,8 @@ char* last_error() {
 }
 
 // word hash (tm_internal.hpp hw_*; the device tokeniser computes the same)
-inline uint64_t hash_word(const uint8_t* p, size_t n) {
-    uint32_t h = HW_SEED;
+inline uint64_t hash_word(const uint8_t* p, size_t n, uint32_t seed = HW_SEED) {
+    uint32_t h = seed;
     size_t i = 0;
     for (; i + 4 <= n; i += 4) {
         uint32_t v;
@@ -124,8 +124,9 @@ class WordDict {
         ++count_;
         if (tails_.size() <= id) tails_.resize((size_t)id + 1, DictTail{0, 0});
         tails_[id] = DictTail{tab_[i].head2, tab_[i].off};
+        const uint64_t hh = (uint32_t)h | (hash_word(p, n, HW_SEED2) << 32);
         if (count_ * 4 > ck_.size()) ck_rebuild(ck_.size() * 2);
-        else if (!ck_put(DictKey{tab_[i].head, (uint32_t)n, id}, (uint32_t)h)) ck_rebuild(ck_.size() * 2);
+        else if (!ck_put(DictKey{tab_[i].head, (uint32_t)n, id}, hh)) ck_rebuild(ck_.size() * 2);
         return id;
     }
 
@@ -137,12 +138,13 @@ class WordDict {
     std::vector<uint32_t>& dirty() { return ck_dirty_; }
 
   private:
-    // cuckoo insert with a random walk of evictions; false: the table must grow
-    bool ck_put(DictKey k, uint32_t h) {
+    // cuckoo insert with a random walk of evictions; h = h1 | h2 << 32; false:
+    // the table must grow
+    bool ck_put(DictKey k, uint64_t h) {
         const uint32_t m = (uint32_t)ck_.size() - 1;
         uint32_t from = ~0u;
         for (int kick = 0; kick < 512; ++kick) {
-            const uint32_t a = h & m, b = ck_alt(h) & m;
+            const uint32_t a = (uint32_t)h & m, b = (uint32_t)(h >> 32) & m;
             const uint32_t i = ck_[a].id == 0 ? a : ck_[b].id == 0 ? b : (a != from ? a : b);
             std::swap(k, ck_[i]);
             std::swap(h, ck_h_[i]);
@@ -155,11 +157,14 @@ class WordDict {
 
     void ck_rebuild(size_t cap) {
         for (;;) {
+            // independent hashes place any set at load 1/4; never grow without bound
+            if (cap > 64 * std::max<size_t>(count_, 1024)) throw std::bad_alloc();
             ck_.assign(cap, DictKey{0, 0, 0});
             ck_h_.assign(cap, 0);
             bool ok = true;
             for (const DictEnt& e : tab_)
-                if (e.h && !ck_put(DictKey{e.head, e.len, e.id}, (uint32_t)e.h)) {
+                if (e.h && !ck_put(DictKey{e.head, e.len, e.id},
+                                   (uint32_t)e.h | (hash_word(arena_.data() + e.off, e.len, HW_SEED2) << 32))) {
                     ok = false;
                     break;
                 }
@@ -187,7 +192,7 @@ class WordDict {
     size_t mask_ = 0, count_ = 0;
     uint32_t next_id_ = W_FIRST;
     std::vector<DictKey> ck_;
-    std::vector<uint32_t> ck_h_;
+    std::vector<uint64_t> ck_h_;   // h1 | h2 << 32 of each slot's key (relocation)
     std::vector<uint32_t> ck_dirty_;
     std::vector<DictTail> tails_;
     uint64_t ck_gen_ = 0;
@@ -299,6 +304,7 @@ struct tm_batch {
     uint32_t *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
     unsigned long long* d_rows = nullptr;
     uint32_t *d_bsums = nullptr, *d_ovf = nullptr, *d_total = nullptr;
+    uint32_t* d_xticket = nullptr;   // tail tickets of the tile walk (TICKET_GROUPS lines)
     size_t c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
     uint32_t* h_total = nullptr;
     size_t ch_total = 0;
@@ -396,7 +402,7 @@ struct tm_batch {
         dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
         if (h_total) (void)hipHostFree(h_total);
         h_total = nullptr;
-        dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total);
+        dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total); dev_free(d_xticket);
         dev_free(d_hdr);
         if (h_hdr) (void)hipHostFree(h_hdr);
         h_hdr = nullptr;
@@ -569,6 +575,7 @@ struct tm_engine {
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
     uint32_t qcap = 384;           // LDS probe stack per wave, 384 or 512 (TM_QCAP); C2 tiles peak at ~340
+    double static_frac = 0.5;       // share of tiles scheduled round-robin before tickets (TM_STATIC_FRAC)
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
     uint32_t* d_dbg = nullptr;
@@ -2114,6 +2121,14 @@ struct tm_engine {
         a.grid = match_waves(b->n, device, qcap);
         a.tile_topics = tile_topics(b->n);
         a.qcap = qcap;
+        {   // the first static_frac of the tiles round-robin, the tail by per-XCD tickets
+            const uint64_t ntiles = ((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics;
+            a.static_rounds = std::max<uint32_t>(1, (uint32_t)(static_frac * (double)ntiles / std::max(a.grid, 1u)));
+            if (!b->d_xticket) HIP_OK(hipMalloc((void**)&b->d_xticket, TICKET_GROUPS * TICKET_STRIDE * 4));
+            if ((uint64_t)a.static_rounds * a.grid < ntiles)   // the tail is scheduled by tickets
+                HIP_OK(hipMemsetAsync(b->d_xticket, 0, TICKET_GROUPS * TICKET_STRIDE * 4, S));
+            a.xtickets = b->d_xticket;
+        }
         if ((uint64_t)a.grid * a.tile_topics * row_cap > b->c_rows) {
             snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
             return TM_EIO;
@@ -2191,6 +2206,7 @@ struct tm_engine {
         b->st.words = b->h_stats[ST_WORDS];
         b->st.matches = b->h_stats[ST_MATCHES];
         b->st.slow_topics = b->h_stats[ST_SLOW];
+        b->st.probes = b->h_stats[ST_PROBES];
         b->st.overflow_tiles = b->h_ctrl[CTRL_NOVF];
         b->st.ms_match = ms_match;
         b->st.ms_total = ms_total;
@@ -2571,6 +2587,7 @@ struct tm_engine {
         checked = ck && ck[0] == '1';
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
         if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
+        if (const char* sf = getenv("TM_STATIC_FRAC")) static_frac = std::min(1.0, std::max(0.0, atof(sf)));
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         if (const char* rl = getenv("TM_RESULT_LIMIT"))
             result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));

@@ -228,6 +228,7 @@ int tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out) {
         s.ms_match = std::max(s.ms_match, p.ms_match);
         s.ms_total = std::max(s.ms_total, p.ms_total);
         s.ms_tokenize = std::max(s.ms_tokenize, p.ms_tokenize);
+        s.probes += p.probes;
     }
     *out = s;
     return TM_OK;

@@ -88,10 +88,14 @@ enum Ctrl : uint32_t {
     CTRL_NOVF = 1,          // topics appended to the ovf list
     CTRL_ERR = 2,           // error bits
     CTRL_SLOW_DONE = 3,
-    CTRL_TILE_NEXT = 4,     // dynamic tile tickets of tm_match_tiles
+    CTRL_TILE_NEXT = 4,     // (unused: tail tickets live in MatchArgs.xtickets)
     CTRL_STAGING64 = 6,     // words 6-7: u64 staging entries reserved (may exceed capacity -> rerun)
     CTRL_WORDS = 16
 };
+// Tail tickets of the tile walk: one counter per XCD (blockIdx % 8 on the
+// round-robin dispatch), each on its own 128-B line, so the 8 groups never
+// contend for one address; group g hands out tail tiles g, g + 8, g + 16, ...
+constexpr uint32_t TICKET_GROUPS = 8, TICKET_STRIDE = 32;
 constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
 constexpr uint32_t ERR_SLOW_SCRATCH = 2; // slow-path scratch exceeded
 constexpr uint32_t ERR_OVF_LIST = 4;
@@ -104,7 +108,7 @@ __device__ __forceinline__ unsigned long long* ctrl_staging(uint32_t* ctrl) {
     return reinterpret_cast<unsigned long long*>(ctrl + CTRL_STAGING64);
 }
 
-enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_N = 8 };
+enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_PROBES = 5, ST_N = 8 };
 
 struct MatchArgs {
     // trie replica
@@ -132,6 +136,8 @@ struct MatchArgs {
     uint32_t tile_topics;     // topics per tm_match_tiles tile (tile_topics(n): 64 .. 1)
     uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
     uint32_t qcap;            // LDS probe-stack entries per wave (384 or 512)
+    uint32_t static_rounds;   // round-robin tiles per wave before tickets (>= 1)
+    uint32_t* xtickets;       // TICKET_GROUPS counters, TICKET_STRIDE u32 apart (zeroed per launch)
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;
@@ -266,7 +272,8 @@ struct DictEnt {
 static_assert(sizeof(DictEnt) == 48, "dictionary entry is 48 bytes (three 16-B loads)");
 
 // The device tokeniser's dictionary: a 2-choice cuckoo table of probe keys
-// (a word lives in slot h1 & mask or ck_alt(h1) & mask, h1 = hash_word), so a
+// (a word lives in slot h1 & mask or h2 & mask: hash_word with seeds HW_SEED
+// and HW_SEED2), so a
 // lookup is two independent 16-B loads and no probe chain; head + len are the
 // whole word up to 8 bytes, longer words also compare their DictTail (by id).
 // Mirrored from the host interner (tm_engine.cpp WordDict).
@@ -313,11 +320,10 @@ __host__ __device__ inline uint32_t hw_final(uint32_t h, uint32_t n) {
     return h | 1u;
 }
 constexpr uint32_t HW_SEED = 0x9E3779B9u;
-// the second cuckoo slot of a word with hash h1
-__host__ __device__ inline uint32_t ck_alt(uint32_t h) {
-    h *= 0x9E3779B1u;
-    return h ^ (h >> 15) ^ 0x5BD1E995u;
-}
+// the second cuckoo slot comes from an independent hash of the word (another
+// seed): a function of h1 alone would put every word of a full-h1 collision
+// triple on the same two slots, which no table size separates
+constexpr uint32_t HW_SEED2 = 0x7F4A7C15u;
 
 // Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
 // the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp

@@ -406,7 +406,7 @@ __device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint
 template <bool CK, bool BIG, bool IN_LDS, class LT>
 __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t0, uint32_t tend, uint32_t wbase,
                                            uint8_t fl, bool valid, unsigned long long& sV, unsigned long long& sH,
-                                           unsigned long long& sW, unsigned long long& sM) {
+                                           unsigned long long& sW, unsigned long long& sM, unsigned long long& sP) {
     const uint32_t lane = threadIdx.x;
     const uint32_t t = t0 + lane;
     const uint32_t* wsrc = IN_LDS ? L.words : a.words;
@@ -416,7 +416,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     uint32_t qn = 0;
     bool ovf = false;
     const bool active = !(fl & TF_SLOW);
-    uint32_t tV = 0, tH = 0, tW = 0;   // committed only if the tile does not overflow
+    uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
     const uint32_t d_me = L.depth[lane];
 
     // ---- level 0: root expansion, one topic per lane
@@ -459,10 +459,14 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const uint32_t qd = lane >> 2, qs = lane & 3;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<Slot*>(a.slots), 0, BIG ? 0u : a.nslots * 16u, 0x00020000);
+#ifdef TM_EXPERIMENT_PHASES   // (timing experiments only: cycles per phase into the H / W stats)
+    const uint64_t ph0 = __builtin_amdgcn_s_memtime();
+#endif
     while (qn > 0) {
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         qn -= k;
+        tP += lane == 0 ? k : 0u;   // bucket reads (hits, misses, continuations)
         const uint32_t idx = qn + lane;
         uint4 e = uint4{0u, 0u, 0u, 0u};
         if (has) e = L.q[idx];
@@ -554,13 +558,17 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         }
     }
     __syncthreads();
+#ifdef TM_EXPERIMENT_PHASES
+    tW = 0;
+    tH = lane == 0 ? (uint32_t)(__builtin_amdgcn_s_memtime() - ph0) : 0u;   // frontier loop
+#endif
 
     if (ovf) {
         // probe stack overflow: every regular topic of the tile goes to the slow path
         send_to_slow<CK>(a, valid && active, t);
         return;
     }
-    sV += tV; sH += tH; sW += tW;
+    sV += tV; sH += tH; sW += tW; sP += tP;
     const uint32_t c_me = L.cnt[lane];
     const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
     send_to_slow<CK>(a, row_ovf, t);
@@ -576,9 +584,18 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     // u64 ticket: a batch may reserve more than 2^32 entries; the host then
     // fails it with TM_EOVERFLOW (sfids_cap < 2^32, so dst below never wraps)
     unsigned long long base64 = 0;
+#ifdef TM_EXPERIMENT_XSTAGE   // (timing experiments only: per-group staging regions, results not exported)
+    const uint64_t rcap = a.sfids_cap / TICKET_GROUPS, g = blockIdx.x % TICKET_GROUPS;
+    if (lane == 0 && tot)
+        base64 = g * rcap + atomicAdd(reinterpret_cast<unsigned long long*>(&a.xtickets[g * TICKET_STRIDE + 2]),
+                                      (unsigned long long)tot);
+    base64 = __shfl(base64, 0, 64);
+    const bool fits = base64 + tot <= (g + 1) * rcap;
+#else
     if (lane == 0 && tot) base64 = atomicAdd(ctrl_staging(a.ctrl), (unsigned long long)tot);
     base64 = __shfl(base64, 0, 64);
     const bool fits = base64 + tot <= a.sfids_cap;
+#endif
     const uint32_t base = (uint32_t)base64;
     const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
@@ -602,14 +619,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;   // topics per tile: 64, or fewer for small batches
     const uint32_t ntiles = (a.n + tt - 1) / tt;
-    unsigned long long sV = 0, sH = 0, sW = 0, sM = 0;
+    unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sP = 0;
 
-    // first tile static, then tickets; the next ticket is taken at the start of
-    // a tile so its latency hides behind the tile's work
-    uint32_t tile = blockIdx.x;
+    // static round-robin tiles, then tickets for the tail; a ticket is taken at
+    // the start of a tile so its latency hides behind the tile's work
+    uint32_t tile = blockIdx.x, round = 0;
+#ifdef TM_EXPERIMENT_PHASES
+    uint64_t pro = 0;
+#endif
     while (tile < ntiles) {
+#ifdef TM_EXPERIMENT_PHASES
+        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+        // the next tile: round-robin for the first static_rounds, then from a
+        // ticket (a contended counter's latency would stall every in-order vmcnt
+        // wait of the tile, so only the tail balances by tickets, per XCD)
         uint32_t ticket = 0;
-        if (lane == 0) ticket = atomicAdd(&a.ctrl[CTRL_TILE_NEXT], 1u);
+        if (round + 1 >= a.static_rounds && lane == 0)
+            ticket = atomicAdd(&a.xtickets[(blockIdx.x % TICKET_GROUPS) * TICKET_STRIDE], 1u);
         const uint32_t t0 = tile * tt;
         const uint32_t tend = min(t0 + tt, a.n);
         const uint32_t t = t0 + lane;
@@ -625,19 +652,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
         L.depth[lane] = my_end - my_off;
         L.cnt[lane] = 0;
         __syncthreads();
-        if (in_lds) match_tile<CK, BIG, true>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
-        else match_tile<CK, BIG, false>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM);
+#ifdef TM_EXPERIMENT_PHASES
+        pro += __builtin_amdgcn_s_memtime() - pt0;   // prologue: ticket, offsets, words to LDS
+#endif
+        if (in_lds) match_tile<CK, BIG, true>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM, sP);
+        else match_tile<CK, BIG, false>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM, sP);
         __syncthreads();
-        tile = __builtin_amdgcn_readfirstlane(ticket) + gridDim.x;
+        ++round;
+        tile = round < a.static_rounds
+                   ? blockIdx.x + round * gridDim.x
+                   : a.static_rounds * gridDim.x + __builtin_amdgcn_readfirstlane(ticket) * TICKET_GROUPS +
+                         blockIdx.x % TICKET_GROUPS;
     }
 
+#ifdef TM_EXPERIMENT_PHASES
+    sW = lane == 0 ? pro : 0;
+#endif
     for (int o = 32; o > 0; o >>= 1) {
         sV += __shfl_xor(sV, o, 64); sH += __shfl_xor(sH, o, 64);
         sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
+        sP += __shfl_xor(sP, o, 64);
     }
     if (lane == 0) {
         atomicAdd(&a.stats[ST_VISITS], sV); atomicAdd(&a.stats[ST_HASH], sH);
         atomicAdd(&a.stats[ST_WORDS], sW); atomicAdd(&a.stats[ST_MATCHES], sM);
+        atomicAdd(&a.stats[ST_PROBES], sP);
     }
 }
 
@@ -1381,7 +1420,13 @@ __device__ __forceinline__ uint32_t dict_find(const TokArgs& a, P p, uint32_t n)
     const uint4 e1 = *reinterpret_cast<const uint4*>(a.keys + (h & m));
     if (e1.w == 0) return W_UNKNOWN;   // slots never empty again once filled: absent
     if (ck_match(a, e1, head, n, p)) return e1.w;
-    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (ck_alt(h) & m));
+    uint32_t g32 = HW_SEED2;
+    for (uint32_t i = 0; i < n; i += 4) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 4 && i + k < n; ++k) v |= (uint32_t)p[i + k] << (8 * k);
+        g32 = hw_step(g32, v);
+    }
+    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (hw_final(g32, n) & m));
     if (ck_match(a, e2, head, n, p)) return e2.w;
     return W_UNKNOWN;
 }
@@ -1525,7 +1570,7 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
     const uint32_t mask = (uint32_t)a.dict_mask;
     for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
         uint64_t head[TOK_WPL];
-        uint32_t ent[TOK_WPL], len[TOK_WPL], st[TOK_WPL], hh[TOK_WPL], pend = 0;
+        uint32_t ent[TOK_WPL], len[TOK_WPL], st[TOK_WPL], pend = 0;
         uint4 e[TOK_WPL];
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
@@ -1534,7 +1579,6 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
             head[k] = 0;
             len[k] = 0;
             st[k] = 0;
-            hh[k] = 0;
             if (w >= tw) continue;
             const uint32_t s0 = L.wst[w] & 0x7FFFu;
             const uint32_t nx = w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u);
@@ -1556,7 +1600,6 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
             }
             const uint32_t h = hw_final(h32, n);
             e[k] = *reinterpret_cast<const uint4*>(a.keys + (h & mask));
-            hh[k] = h;
             head[k] = c0w;
             len[k] = n;
             st[k] = s0;
@@ -1573,10 +1616,19 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
                 pend &= ~(1u << k);
             }
         }
-        // alternate slots of the rest, all in flight
+        // alternate slots of the rest (second hash, from LDS), all in flight
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k)
-            if (pend >> k & 1u) e[k] = *reinterpret_cast<const uint4*>(a.keys + (ck_alt(hh[k]) & mask));
+            if (pend >> k & 1u) {
+                const uint32_t n = len[k], s0 = st[k];
+                uint32_t g32 = HW_SEED2;
+                for (uint32_t i = 0; i < n; i += 8) {
+                    const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
+                    g32 = hw_step(g32, (uint32_t)c);
+                    if (n - i > 4) g32 = hw_step(g32, (uint32_t)(c >> 32));
+                }
+                e[k] = *reinterpret_cast<const uint4*>(a.keys + (hw_final(g32, n) & mask));
+            }
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
             if ((pend >> k & 1u) && ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) ent[k] |= e[k].w;

@@ -95,6 +95,7 @@ typedef struct {
     float    ms_match;      /* device time of the frontier kernel (last launch) */
     float    ms_total;      /* device time of the whole batch pipeline (last launch) */
     float    ms_tokenize;   /* device tokeniser time of the last launch (0: tokens reused) */
+    uint64_t probes;        /* 64-B edge-hash bucket reads of the tile walk (hits + misses) */
 } tm_batch_stats;
 
 typedef struct {
