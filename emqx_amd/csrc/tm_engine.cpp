@@ -304,7 +304,6 @@ struct tm_batch {
     uint32_t *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
     unsigned long long* d_rows = nullptr;
     uint32_t *d_bsums = nullptr, *d_ovf = nullptr, *d_total = nullptr;
-    uint32_t* d_xticket = nullptr;   // tail tickets of the tile walk (TICKET_GROUPS lines)
     size_t c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
     uint32_t* h_total = nullptr;
     size_t ch_total = 0;
@@ -316,7 +315,7 @@ struct tm_batch {
     size_t hdr_cap = 0;   // topics the block holds
     uint32_t *d_count = nullptr, *d_ctrl = nullptr, *h_ctrl = nullptr, *h_count = nullptr;
     unsigned long long *d_src = nullptr, *d_stats = nullptr, *h_src = nullptr, *h_stats = nullptr;
-    static constexpr size_t HDR_FIXED = CTRL_WORDS * 4 + ST_N * 8;
+    static constexpr size_t HDR_FIXED = ((size_t)XG_WORD + TICKET_GROUPS * TICKET_STRIDE) * 4;
     static size_t hdr_bytes(size_t n) { return HDR_FIXED + n * 12; }
     // pinned host results
     uint32_t* h_rowoff = nullptr;
@@ -402,7 +401,7 @@ struct tm_batch {
         dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
         if (h_total) (void)hipHostFree(h_total);
         h_total = nullptr;
-        dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total); dev_free(d_xticket);
+        dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total);
         dev_free(d_hdr);
         if (h_hdr) (void)hipHostFree(h_hdr);
         h_hdr = nullptr;
@@ -2124,16 +2123,14 @@ struct tm_engine {
         {   // the first static_frac of the tiles round-robin, the tail by per-XCD tickets
             const uint64_t ntiles = ((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics;
             a.static_rounds = std::max<uint32_t>(1, (uint32_t)(static_frac * (double)ntiles / std::max(a.grid, 1u)));
-            if (!b->d_xticket) HIP_OK(hipMalloc((void**)&b->d_xticket, TICKET_GROUPS * TICKET_STRIDE * 4));
-            if ((uint64_t)a.static_rounds * a.grid < ntiles)   // the tail is scheduled by tickets
-                HIP_OK(hipMemsetAsync(b->d_xticket, 0, TICKET_GROUPS * TICKET_STRIDE * 4, S));
-            a.xtickets = b->d_xticket;
         }
         if ((uint64_t)a.grid * a.tile_topics * row_cap > b->c_rows) {
             snprintf(last_error(), 512, "emission rows sized for fewer waves than the launch");
             return TM_EIO;
         }
         a.sfids = b->d_sfids; a.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
+        a.rcap = a.sfids_cap / TICKET_GROUPS;
+        a.xg = b->d_ctrl + XG_WORD;
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
         a.s_qparent = b->d_sqpar; a.s_qpw = b->d_sqpw; a.s_qmeta = b->d_sqmeta; a.s_qkey = b->d_sqkey;
@@ -2170,12 +2167,18 @@ struct tm_engine {
     // retry reasons in *err (0 = clean)
     int check_ctrl(const uint32_t* ctrl, const unsigned long long* stats, uint32_t* err, uint64_t* need) {
         *err = ctrl[CTRL_ERR];
-        *need = (uint64_t)ctrl[CTRL_STAGING64] | ((uint64_t)ctrl[CTRL_STAGING64 + 1] << 32);
+        uint64_t staged = 0, top = 0;
+        for (uint32_t g = 0; g < TICKET_GROUPS; ++g) {
+            const uint64_t t = xg_top_read(ctrl, g);
+            staged += t;
+            top = std::max(top, t);
+        }
+        *need = top * TICKET_GROUPS;   // staging capacity that holds every region's reservation
         const uint64_t nmatch = stats[ST_MATCHES];
         // a CSR with u32 offsets cannot hold more (tm_result): refuse, never wrap
-        if ((*err & ERR_CSR_RANGE) || *need > result_limit || nmatch > result_limit) {
+        if ((*err & ERR_CSR_RANGE) || staged > result_limit || nmatch > result_limit) {
             snprintf(last_error(), 512, "batch result too large: %llu staged / %llu matched > limit %llu",
-                     (unsigned long long)*need, (unsigned long long)nmatch, (unsigned long long)result_limit);
+                     (unsigned long long)staged, (unsigned long long)nmatch, (unsigned long long)result_limit);
             return TM_EOVERFLOW;
         }
         return TM_OK;
@@ -2475,6 +2478,7 @@ struct tm_engine {
         x.rows = b->d_sfids;
         x.h_rows = reinterpret_cast<uint32_t*>(d_rows);
         x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
+        x.rcap = std::min<uint64_t>(b->c_sfids, MAX_RESULT) / TICKET_GROUPS;
         HIP_OK(launch_export_host(x, S));
         HIP_OK(hipEventRecord(sl->ev_done, S));
         return TM_OK;

@@ -84,18 +84,21 @@ __host__ __device__ inline uint32_t home_bucket(uint32_t parent, uint32_t word, 
 }
 
 // Control words of one batch launch (device memory, zeroed per launch).
+// Walk groups: one per XCD (blockIdx % 8 on the round-robin dispatch), each
+// with its own 128-B header line, so no two groups ever contend for one
+// address.  Group g hands out the tail tiles g, g + 8, g + 16, ... from its
+// ticket and reserves staging entries in its own region of sfids[] (region g
+// = [g * rcap, (g + 1) * rcap)): a single device-wide counter per tile
+// serialises at one L2 line and its return stalls every in-order vmcnt wait.
+constexpr uint32_t TICKET_GROUPS = 8, TICKET_STRIDE = 32;
+
 enum Ctrl : uint32_t {
     CTRL_NOVF = 1,          // topics appended to the ovf list
     CTRL_ERR = 2,           // error bits
     CTRL_SLOW_DONE = 3,
     CTRL_TILE_NEXT = 4,     // (unused: tail tickets live in MatchArgs.xtickets)
-    CTRL_STAGING64 = 6,     // words 6-7: u64 staging entries reserved (may exceed capacity -> rerun)
     CTRL_WORDS = 16
 };
-// Tail tickets of the tile walk: one counter per XCD (blockIdx % 8 on the
-// round-robin dispatch), each on its own 128-B line, so the 8 groups never
-// contend for one address; group g hands out tail tiles g, g + 8, g + 16, ...
-constexpr uint32_t TICKET_GROUPS = 8, TICKET_STRIDE = 32;
 constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
 constexpr uint32_t ERR_SLOW_SCRATCH = 2; // slow-path scratch exceeded
 constexpr uint32_t ERR_OVF_LIST = 4;
@@ -104,11 +107,21 @@ constexpr uint32_t ERR_CSR_RANGE = 8;    // the batch's match count does not fit
 // matches than this fails with TM_EOVERFLOW instead of wrapping.
 constexpr uint64_t MAX_RESULT = 0xFFFFFFF0ull;
 
-__device__ __forceinline__ unsigned long long* ctrl_staging(uint32_t* ctrl) {
-    return reinterpret_cast<unsigned long long*>(ctrl + CTRL_STAGING64);
-}
 
 enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_PROBES = 5, ST_N = 8 };
+
+// The batch header block: ctrl (CTRL_WORDS u32) | stats (ST_N u64) | one
+// 128-B line per walk group (see TICKET_GROUPS): u32 tail ticket at +0, u64
+// staging top at +8 | per-topic src / count.  Zeroed per launch.
+constexpr uint32_t XG_WORD = CTRL_WORDS + ST_N * 2;   // first group line, in u32 of the header
+// staging entries group g reserved (u64; may exceed the region -> rerun)
+__host__ __device__ __forceinline__ unsigned long long* xg_top(uint32_t* xg, uint32_t g) {
+    return reinterpret_cast<unsigned long long*>(xg + g * TICKET_STRIDE + 2);
+}
+__host__ __device__ __forceinline__ uint64_t xg_top_read(const uint32_t* hdr, uint32_t g) {
+    const uint32_t* w = hdr + XG_WORD + g * TICKET_STRIDE + 2;
+    return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+}
 
 struct MatchArgs {
     // trie replica
@@ -137,7 +150,8 @@ struct MatchArgs {
     uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
     uint32_t qcap;            // LDS probe-stack entries per wave (384 or 512)
     uint32_t static_rounds;   // round-robin tiles per wave before tickets (>= 1)
-    uint32_t* xtickets;       // TICKET_GROUPS counters, TICKET_STRIDE u32 apart (zeroed per launch)
+    uint32_t* xg;             // the header's group lines (header + XG_WORD)
+    uint64_t rcap;            // staging entries per group region (sfids_cap / TICKET_GROUPS)
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;
@@ -370,6 +384,7 @@ struct ExportArgs {
     const uint32_t* rows;     // staging area
     uint32_t* h_rows;
     uint64_t rows_cap;        // entries h_rows holds
+    uint64_t rcap;            // entries per group region of the staging area
 };
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
 // dirty cuckoo slots -> the device table

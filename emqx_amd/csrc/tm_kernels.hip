@@ -584,18 +584,11 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     // u64 ticket: a batch may reserve more than 2^32 entries; the host then
     // fails it with TM_EOVERFLOW (sfids_cap < 2^32, so dst below never wraps)
     unsigned long long base64 = 0;
-#ifdef TM_EXPERIMENT_XSTAGE   // (timing experiments only: per-group staging regions, results not exported)
-    const uint64_t rcap = a.sfids_cap / TICKET_GROUPS, g = blockIdx.x % TICKET_GROUPS;
-    if (lane == 0 && tot)
-        base64 = g * rcap + atomicAdd(reinterpret_cast<unsigned long long*>(&a.xtickets[g * TICKET_STRIDE + 2]),
-                                      (unsigned long long)tot);
+    const uint32_t g = blockIdx.x % TICKET_GROUPS;   // my group's staging region
+    if (lane == 0 && tot) base64 = atomicAdd(xg_top(a.xg, g), (unsigned long long)tot);
     base64 = __shfl(base64, 0, 64);
-    const bool fits = base64 + tot <= (g + 1) * rcap;
-#else
-    if (lane == 0 && tot) base64 = atomicAdd(ctrl_staging(a.ctrl), (unsigned long long)tot);
-    base64 = __shfl(base64, 0, 64);
-    const bool fits = base64 + tot <= a.sfids_cap;
-#endif
+    const bool fits = base64 + tot <= a.rcap;
+    base64 += (uint64_t)g * a.rcap;
     const uint32_t base = (uint32_t)base64;
     const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
@@ -636,7 +629,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
         // wait of the tile, so only the tail balances by tickets, per XCD)
         uint32_t ticket = 0;
         if (round + 1 >= a.static_rounds && lane == 0)
-            ticket = atomicAdd(&a.xtickets[(blockIdx.x % TICKET_GROUPS) * TICKET_STRIDE], 1u);
+            ticket = atomicAdd(&a.xg[(blockIdx.x % TICKET_GROUPS) * TICKET_STRIDE], 1u);
         const uint32_t t0 = tile * tt;
         const uint32_t tend = min(t0 + tt, a.n);
         const uint32_t t = t0 + lane;
@@ -845,9 +838,12 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             __syncthreads();
         }
         unsigned long long base = 0;
-        if (lane == 0 && on) base = atomicAdd(ctrl_staging(a.ctrl), (unsigned long long)on);
+        const uint32_t g = blockIdx.x % TICKET_GROUPS;
+        if (lane == 0 && on) base = atomicAdd(xg_top(a.xg, g), (unsigned long long)on);
         base = __shfl(base, 0, 64);
-        if (base + on <= a.sfids_cap) {
+        const bool fits = base + on <= a.rcap;
+        base += (uint64_t)g * a.rcap;
+        if (fits) {
             for (uint32_t i = lane; i < on; i += 64) a.sfids[CK_(base + i, a.sfids_cap, 30)] = ofid[i];
         } else if (lane == 0) {
             atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);
@@ -1806,9 +1802,11 @@ __global__ __launch_bounds__(256) void tm_export_host(ExportArgs a) {
     const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     for (uint64_t i = i0; i < a.hdr_words; i += stride) a.h_hdr[i] = a.hdr[i];
     for (uint64_t i = i0; i < a.n; i += stride) a.h_count[i] = a.count[i];
-    const uint64_t top = *reinterpret_cast<const unsigned long long*>(a.hdr + CTRL_STAGING64);
-    const uint64_t rows = top < a.rows_cap ? top : a.rows_cap;
-    for (uint64_t i = i0; i < rows; i += stride) a.h_rows[i] = a.rows[i];
+    for (uint32_t g = 0; g < TICKET_GROUPS; ++g) {   // each group region's reserved entries
+        const uint64_t top = xg_top_read(a.hdr, g);
+        const uint64_t lo = g * a.rcap, hi = lo + (top < a.rcap ? top : a.rcap);
+        for (uint64_t i = lo + i0; i < hi && i < a.rows_cap; i += stride) a.h_rows[i] = a.rows[i];
+    }
 }
 
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s) {
