@@ -163,6 +163,23 @@ def c1_leg(host, device=0):
     return out
 
 
+def pmc_traffic(workload, topics, filters=None):
+    """HBM bytes per walk launch from the committed PMC pass of this workload
+    (tools/pmc_traffic.sh -> profiles/pmc_latest.json for C2,
+    tools/pmc_traffic_c4.sh -> profiles/pmc_c4.json for C4), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json" if workload == "C2" else "pmc_c4.json")
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if pmc.get("workload") != workload or pmc.get("topics") != topics:
+        return None
+    if filters is not None and pmc.get("filters") not in (None, filters):
+        return None
+    return pmc.get("hbm_bytes_per_launch")
+
+
 def run_c4(args, ws, rank, local, pg):
     """Config C4: IoT filters partitioned over the WORLD_SIZE GPUs by their literal
     (w0, w1) prefix (root-wildcard filters replicated), each rank publishing its
@@ -240,8 +257,8 @@ def run_c4(args, ws, rank, local, pg):
                    "filters_on_rank0_shard": inserted, "mode": "filter-sharded",
                    "parallelism": f"filters sharded x{ws}, all_to_all exchange"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tm_match_tiles",
-                     "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("C4", n, p.n_filters),
+                     "kernel": "tm_match_tiles", "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes,
                      "per_publish": {k: st[v] / max(st["topics"], 1) for k, v in
                                      (("V", "visits"), ("H", "hash_hits"), ("d", "words"), ("M", "matches"))}},
         "matches_per_step": int(gids.numel()),
@@ -716,16 +733,7 @@ def main():
                  + 4 * st["matches"] + 4 * n)
     k_ms = float(np.mean(ms_match))
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            if pmc.get("workload") == "C2" and pmc.get("topics") == n:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic = pmc_traffic("C2", n)
 
     out = {
         "metric": "publishes matched/sec (node) at 1M wildcard subs; p99 batch match latency",

@@ -368,6 +368,9 @@ struct tm_batch {
     size_t ch_rtotal = 0, ch_rrow = 0, ch_rfid = 0, ch_rdest = 0;
     // subscriber fan-out (tm_batch_dispatch)
     uint64_t *d_moff = nullptr, *d_fbsums = nullptr, *d_ftotal = nullptr, *d_drow = nullptr, *d_ftile = nullptr;
+    uint32_t* d_moff32 = nullptr;
+    uint8_t* d_fbig = nullptr;
+    size_t c_moff32 = 0, c_fbig = 0;
     uint64_t *h_ftotal = nullptr, *h_drow = nullptr, *h_moff = nullptr;
     uint32_t *d_fout = nullptr, *h_fout = nullptr;
     size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0, c_ftile = 0;
@@ -375,7 +378,7 @@ struct tm_batch {
     hipEvent_t fev0 = nullptr, fev1 = nullptr;
 
     void release() {
-        dev_free(d_moff); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
+        dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
         dev_free(d_ftile);
         for (uint64_t** h : {&h_ftotal, &h_drow, &h_moff}) {
             if (*h) (void)hipHostFree(*h);
@@ -575,6 +578,7 @@ struct tm_engine {
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
     uint32_t qcap = 384;           // LDS probe stack per wave, 384 or 512 (TM_QCAP); C2 tiles peak at ~340
     double static_frac = 0.5;       // share of tiles scheduled round-robin before tickets (TM_STATIC_FRAC)
+    uint64_t fan_big_limit = 0xFFFFFFFFull;   // fan-out scan blocks above this use u64 offsets (TM_FAN_BIG: tests)
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
     uint32_t* d_dbg = nullptr;
@@ -1301,6 +1305,8 @@ struct tm_engine {
         const uint32_t nb = (uint32_t)((nm + 1 + fan_scan_tile() - 1) / fan_scan_tile());
         if ((rc = dev_reserve(b->d_moff, b->c_moff, nm + 1))) return rc;
         if ((rc = dev_reserve(b->d_fbsums, b->c_fbsums, nb))) return rc;
+        if ((rc = dev_reserve(b->d_moff32, b->c_moff32, nm + 1))) return rc;
+        if ((rc = dev_reserve(b->d_fbig, b->c_fbig, nb))) return rc;
         if ((rc = dev_reserve(b->d_ftotal, b->c_ftotal, 1))) return rc;
         if ((rc = dev_reserve(b->d_drow, b->c_drow, (size_t)n + 1))) return rc;
         if ((rc = host_reserve(b->h_ftotal, b->ch_ftotal, 1))) return rc;
@@ -1311,7 +1317,8 @@ struct tm_engine {
         FanArgs fa{};
         fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
         fa.soff = d_soff; fa.scnt = d_scnt; fa.subs = d_subs; fa.nnodes = subs_nn;
-        fa.moff = b->d_moff; fa.bsums = b->d_fbsums; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
+        fa.moff = b->d_moff; fa.moff32 = b->d_moff32; fa.bbig = b->d_fbig; fa.bsums = b->d_fbsums;
+        fa.big_limit = fan_big_limit; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
         HIP_OK(launch_fan_scan(fa, stream));
         HIP_OK(hipMemcpyAsync(b->h_ftotal, b->d_ftotal, 8, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -2592,6 +2599,7 @@ struct tm_engine {
         if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
         if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
         if (const char* sf = getenv("TM_STATIC_FRAC")) static_frac = std::min(1.0, std::max(0.0, atof(sf)));
+        if (const char* fb = getenv("TM_FAN_BIG")) fan_big_limit = std::min<uint64_t>(0xFFFFFFFFull, strtoull(fb, nullptr, 10));
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         if (const char* rl = getenv("TM_RESULT_LIMIT"))
             result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));

@@ -217,7 +217,11 @@ struct FanArgs {
     const uint8_t* scnt;      // per node id: min(soff[f + 1] - soff[f], 255); 255 = read soff
     const uint32_t* subs;
     uint32_t nnodes;
-    uint64_t* moff;           // n_matches + 1: first delivery of match entry j (block-relative until globalized)
+    uint64_t* moff;           // n_matches + 1: u64 first delivery of entry j (block-relative in "big"
+                              // scan blocks; all entries, global, after tm_fan_scan_add)
+    uint32_t* moff32;         // n_matches + 1: the same, u32 block-relative, in blocks under 2^32 deliveries
+    uint8_t* bbig;            // per scan block: 1 = its deliveries exceed u32, read moff instead of moff32
+    uint64_t big_limit;       // a block delivering more takes the u64 path (u32 max; TM_FAN_BIG test knob)
     uint64_t* bsums;          // scan block sums (FAN_SCAN_TILE entries per block)
     uint64_t* d_total;
     uint64_t* drow;           // n + 1: deliveries of publish i

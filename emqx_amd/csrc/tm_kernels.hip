@@ -1052,8 +1052,11 @@ constexpr uint32_t FAN_FILL_PER = TM_FAN_FILL_PER;         // deliveries per fil
 constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * FAN_FILL_PER;
 constexpr uint32_t FAN_LDS_ENTRIES = FAN_FILL_TILE * 3 / 4;  // match entries a fill tile can stage
 
+// first delivery of match entry j: the block's offset plus the block-relative
+// u32 (u64 only in scan blocks with 2^32 deliveries or more)
 __device__ inline uint64_t fan_moff(const FanArgs& a, uint64_t j) {
-    return a.moff[j] + a.bsums[j / FAN_SCAN_TILE];
+    const uint64_t b = j / FAN_SCAN_TILE;
+    return (a.bbig[b] ? a.moff[j] : (uint64_t)a.moff32[j]) + a.bsums[b];
 }
 
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
@@ -1084,23 +1087,37 @@ __device__ inline uint64_t fan_block_scan(uint64_t v, uint64_t* lds, uint64_t& t
 
 // A block scans FAN_SCAN_TILE entries as FAN_PER striped chunks of FAN_BLOCK
 // (coalesced ids loads and moff stores); all chunks' run lengths are gathered
-// before the first scan so the soff loads overlap.
+// before the first scan so the soff loads overlap.  The block's total decides
+// the width of its offsets: u32 (half the bytes every reader moves) unless the
+// block delivers 2^32 or more (a hot filter with millions of subscribers).
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
     __shared__ uint64_t lds[4];
     const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + threadIdx.x;
-    uint64_t c[FAN_PER];
+    uint64_t c[FAN_PER], mine = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < FAN_PER; ++k) c[k] = fan_count(a, j0 + (uint64_t)k * FAN_BLOCK);
+    for (uint32_t k = 0; k < FAN_PER; ++k) {
+        c[k] = fan_count(a, j0 + (uint64_t)k * FAN_BLOCK);
+        mine += c[k];
+    }
+    uint64_t total;
+    (void)fan_block_scan(mine, lds, total);
+    const bool big = total > a.big_limit;
     uint64_t carry = 0;
 #pragma unroll
     for (uint32_t k = 0; k < FAN_PER; ++k) {
         uint64_t tot;
         const uint64_t e = fan_block_scan(c[k], lds, tot);
         const uint64_t j = j0 + (uint64_t)k * FAN_BLOCK;
-        if (j <= a.n_matches) a.moff[j] = carry + e;
+        if (j <= a.n_matches) {
+            if (big) a.moff[j] = carry + e;
+            else a.moff32[j] = (uint32_t)(carry + e);
+        }
         carry += tot;
     }
-    if (threadIdx.x == 0) a.bsums[blockIdx.x] = carry;
+    if (threadIdx.x == 0) {
+        a.bsums[blockIdx.x] = carry;
+        a.bbig[blockIdx.x] = big ? 1 : 0;
+    }
 }
 
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_t nb) {
@@ -1117,14 +1134,14 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_
     if (threadIdx.x == 0) *a.d_total = carry;
 }
 
-// After scan_local + scan_sums, moff[j] is relative to its scan block and
-// bsums[b] is the block's exclusive offset: rows, tiles and fill read the sum
-// (bsums is small and cache-resident).  tm_fan_scan_add makes moff global in
-// place -- only when the caller asks for the match offsets, and only after the
-// fill, which no longer needs it.
+// After scan_local + scan_sums, moff32[j] (or moff[j] in a big block) is
+// relative to its scan block and bsums[b] is the block's exclusive offset:
+// rows, tiles and fill read the sum (bsums is small and cache-resident).
+// tm_fan_scan_add writes the global u64 offsets into moff -- only when the
+// caller asks for the match offsets, and only after the fill.
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_add(FanArgs a) {
     const uint64_t j = (uint64_t)blockIdx.x * FAN_BLOCK + threadIdx.x;
-    if (j <= a.n_matches) a.moff[j] += a.bsums[j / FAN_SCAN_TILE];
+    if (j <= a.n_matches) a.moff[j] = fan_moff(a, j);   // in place for big blocks: read, then write
 }
 
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_rows(FanArgs a) {

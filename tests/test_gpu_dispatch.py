@@ -52,9 +52,15 @@ def test_dispatch_random_churn_vs_oracle():
         assert sorted(B.topics()) == sorted(orc.routes)
 
 
-def test_dispatch_skewed_fanout_and_modes():
+@pytest.mark.parametrize("big", [None, "100000", "0"])
+def test_dispatch_skewed_fanout_and_modes(big, monkeypatch):
     """One '#' filter with 150k subscribers next to thousands of 1-subscriber
-    filters: the fill kernel's workgroups straddle both kinds of runs."""
+    filters: the fill kernel's workgroups straddle both kinds of runs.  `big`
+    lowers the per-scan-block delivery count above which match offsets are
+    kept as u64 instead of u32 (TM_FAN_BIG, normally 2^32 - 1): some blocks,
+    and then every block, take the u64 path."""
+    if big is not None:
+        monkeypatch.setenv("TM_FAN_BIG", big)
     p = replace(gen.C1, n_filters=4000)
     F = gen.gen_filters(p).tolist()
     T = gen.gen_topics(p, gen.Strings.from_list(F), 23, 3000).tolist()

@@ -50,6 +50,9 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--topics", type=int, default=10_000_000)
     ap.add_argument("--write", default=None)
+    ap.add_argument("--workload", default="C2")
+    ap.add_argument("--filters", type=int, default=0)
+    ap.add_argument("--kernel", default="tm_match_tiles")
     args = ap.parse_args()
     res = load(args.root)
     if not res:
@@ -60,16 +63,16 @@ def main():
         for c in sorted(res[k]):
             print(f"    {c:32s} {res[k][c]:.6g}")
     if args.write:
-        mt = [k for k in res if "tm_match_tiles" in k]
+        mt = [k for k in res if args.kernel in k]
         if not mt:
-            print("tm_match_tiles not found")
+            print(args.kernel, "not found")
             return 1
         r = res[mt[0]]
         fetch_kib = r.get("FETCH_SIZE")
         write_kib = r.get("WRITE_SIZE")
-        info = {"workload": "C2", "topics": args.topics, "kernel": short(mt[0]),
+        info = {"workload": args.workload, "topics": args.topics, "kernel": short(mt[0]),
                 "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
-                "hbm_bytes_per_launch": None,
+                "hbm_bytes_per_launch": None, "filters": args.filters or None,
                 "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes; "
                         "the 16-B bucket loads are the calibrated width, the 4/8-B stores are not"}
         if fetch_kib is not None and write_kib is not None:
