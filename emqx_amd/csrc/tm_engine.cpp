@@ -1191,6 +1191,9 @@ struct tm_engine {
     uint64_t* d_soff = nullptr;
     uint32_t* d_subs = nullptr;
     uint8_t* d_scnt = nullptr;    // per node: min(soff[f + 1] - soff[f], 255) (the scan's 1-B gather)
+    uint32_t* d_sone = nullptr;   // per node: its subscriber when it has exactly one (the fill's 4-B gather)
+    size_t c_sone = 0;
+    std::vector<uint32_t> h_sone;
     size_t c_soff = 0, c_subs = 0, c_scnt = 0;
     std::vector<uint8_t> h_scnt;
     uint32_t subs_nn = 0;
@@ -1280,12 +1283,17 @@ struct tm_engine {
         for (const auto& r : runs) std::copy(r.second->begin(), r.second->end(), h_subs.begin() + (long)h_soff[r.first]);
         h_scnt.resize(std::max<size_t>(nn, 1));
         for (size_t i = 0; i < nn; ++i) h_scnt[i] = (uint8_t)std::min<uint64_t>(h_soff[i + 1] - h_soff[i], 255);
+        h_sone.assign(std::max<size_t>(nn, 1), NONE);
+        for (size_t i = 0; i < nn; ++i)
+            if (h_soff[i + 1] - h_soff[i] == 1) h_sone[i] = h_subs[h_soff[i]];
         int rc;
         if ((rc = dev_reserve(d_soff, c_soff, nn + 1))) return rc;
         if ((rc = dev_reserve(d_scnt, c_scnt, std::max<size_t>(nn, 1)))) return rc;
+        if ((rc = dev_reserve(d_sone, c_sone, std::max<size_t>(nn, 1)))) return rc;
         if ((rc = dev_reserve(d_subs, c_subs, std::max<size_t>(h_subs.size(), 1)))) return rc;
         HIP_OK(hipMemcpyAsync(d_soff, h_soff.data(), (nn + 1) * 8, hipMemcpyHostToDevice, stream));
         if (nn) HIP_OK(hipMemcpyAsync(d_scnt, h_scnt.data(), nn, hipMemcpyHostToDevice, stream));
+        if (nn) HIP_OK(hipMemcpyAsync(d_sone, h_sone.data(), nn * 4, hipMemcpyHostToDevice, stream));
         if (!h_subs.empty())
             HIP_OK(hipMemcpyAsync(d_subs, h_subs.data(), h_subs.size() * 4, hipMemcpyHostToDevice, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -1316,7 +1324,7 @@ struct tm_engine {
         }
         FanArgs fa{};
         fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
-        fa.soff = d_soff; fa.scnt = d_scnt; fa.subs = d_subs; fa.nnodes = subs_nn;
+        fa.soff = d_soff; fa.scnt = d_scnt; fa.sone = d_sone; fa.subs = d_subs; fa.nnodes = subs_nn;
         fa.moff = b->d_moff; fa.moff32 = b->d_moff32; fa.bbig = b->d_fbig; fa.bsums = b->d_fbsums;
         fa.big_limit = fan_big_limit; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
         HIP_OK(launch_fan_scan(fa, stream));
@@ -2638,7 +2646,7 @@ struct tm_engine {
             if (h_dxidx) (void)hipHostFree(h_dxidx);
             if (h_dxval) (void)hipHostFree(h_dxval);
             dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
-            dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt);
+            dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt); dev_free(d_sone);
             if (h_dbg) (void)hipHostFree(h_dbg);
             if (h_didx) (void)hipHostFree(h_didx);
             if (h_dval) (void)hipHostFree(h_dval);

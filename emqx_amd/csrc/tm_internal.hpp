@@ -215,6 +215,7 @@ struct FanArgs {
     uint64_t n_matches;
     const uint64_t* soff;     // per node id: subscribers soff[f] .. soff[f+1] (nnodes + 1)
     const uint8_t* scnt;      // per node id: min(soff[f + 1] - soff[f], 255); 255 = read soff
+    const uint32_t* sone;     // per node id: the subscriber of a one-subscriber node
     const uint32_t* subs;
     uint32_t nnodes;
     uint64_t* moff;           // n_matches + 1: u64 first delivery of entry j (block-relative in "big"

@@ -1204,7 +1204,10 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
         const uint64_t j = jlo + e;
         const uint64_t m0 = fan_moff(a, j), m1 = fan_moff(a, j + 1);
         if (m1 > m0 && m1 > start && m0 < end) {
-            base[e] = (int64_t)a.soff[a.ids[j]] - (int64_t)m0;
+            // a one-delivery run keeps its subscriber inline (one 4-B gather,
+            // no dependent read of subs[]): INT64_MIN + id marks it
+            const uint32_t f = a.ids[j];
+            base[e] = m1 - m0 == 1 ? INT64_MIN + (int64_t)a.sone[f] : (int64_t)a.soff[f] - (int64_t)m0;
             own[m0 > start ? (uint32_t)(m0 - start) : 0u] = (uint16_t)(e + 1);
         }
     }
@@ -1244,7 +1247,9 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     __syncthreads();
     for (uint32_t i = t; i < len; i += FAN_BLOCK) {
         const uint32_t e = (uint32_t)own[i] - 1u;
-        a.out[start + i] = a.subs[(uint64_t)(base[e] + (int64_t)(start + i))];
+        const int64_t bs = base[e];
+        a.out[start + i] = bs < INT64_MIN + (1ll << 33) ? (uint32_t)(bs - INT64_MIN)
+                                                        : a.subs[(uint64_t)(bs + (int64_t)(start + i))];
     }
 }
 
