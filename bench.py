@@ -306,7 +306,7 @@ def run_c5(args, ws, rank, local, sync):
     for _ in range(args.steps):
         dels, adds = churn.step(args.c5_deltas)
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
-    ms_match, ms_churn = [], []
+    ms_match, ms_churn, ms_walk, ms_tok = [], [], [], []
     t0 = time.perf_counter()
     tc = time.perf_counter()
     Churn.apply(eng, *deltas[0])
@@ -318,7 +318,10 @@ def run_c5(args, ws, rank, local, sync):
             Churn.apply(eng, *deltas[i + 1])
             ms_churn.append(1e3 * (time.perf_counter() - tc))
         b.wait()
-        ms_match.append(b.stats()["ms_total"])
+        st = b.stats()
+        ms_match.append(st["ms_total"])
+        ms_walk.append(st["ms_match"])
+        ms_tok.append(st["ms_tokenize"])
         if i + 1 < args.steps:
             b.launch()
     elapsed = time.perf_counter() - t0
@@ -347,6 +350,8 @@ def run_c5(args, ws, rank, local, sync):
                                f"{n} publishes per GPU (90% hot, Zipf 1.0), {args.c5_deltas} deltas per step",
                    "filters": len(allf), "distinct_topics": int(n_rows), "mode": "replicated, dedup batches"},
         "device_pipeline_ms": float(np.mean(ms_match)),
+        "device_walk_ms": float(np.mean(ms_walk)),
+        "device_tokenize_ms": float(np.mean(ms_tok)),
         "churn_apply_ms": float(np.mean(ms_churn)),
         "churn_overlapped_with_device": True,
         "matches_delivered_per_step": delivered,
@@ -756,7 +761,8 @@ def main():
                      "kernel": "tm_match_tiles", "kernel_ms": k_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "per_publish": {"V": st["visits"] / n, "H": st["hash_hits"] / n,
-                                     "d": st["words"] / n, "M": st["matches"] / n}},
+                                     "d": st["words"] / n, "M": st["matches"] / n,
+                                     "bucket_reads": st["probes"] / n}},
         "pipeline_ms": float(np.mean(ms_total)),
         "pipeline_fresh_ms": float(np.median(fresh_ms)),
         "tokenize_ms": float(np.median(fresh_tok)),

@@ -495,10 +495,23 @@ struct tm_engine {
     WordDict dict;
     tm_batch tokb;   // staging of tm_tokenize_device
 
-    // node table (host)
-    std::vector<uint32_t> n_parent, n_word, n_ec, n_plus, n_hash, n_inslot, n_flen;
+    // node table (host): the fields a mutation touches in one 32-B record
+    // (one cache line per node on the churn path), the filter-bytes index
+    // (uploads, tm_filter_bytes) apart
+    struct alignas(32) NodeRec {
+        uint32_t parent = 0, word = 0;   // incoming edge
+        uint32_t ec = 0;                 // edge_count (src/emqx_trie.erl:145-158)
+        uint32_t plus = NONE, hash = NONE;   // '+' / '#' child
+        uint32_t inslot = NONE;          // edge-hash slot of the incoming edge
+        uint8_t live = 0, topic = 0;
+        uint8_t hasbytes = 0;            // n_foff / n_flen name this id's filter (until the id is reused)
+        uint8_t pad = 0;
+        uint32_t pad2 = 0;
+    };
+    static_assert(sizeof(NodeRec) == 32, "two node records per cache line");
+    std::vector<NodeRec> nd;
+    std::vector<uint32_t> n_flen;
     std::vector<uint64_t> n_foff;
-    std::vector<uint8_t> n_live, n_topic;
     std::vector<uint32_t> free_nodes;
     // A freed node id (== filter id) is not reused while a batch launched
     // before the free may still hand it out: results are read (ids mapped to
@@ -509,7 +522,6 @@ struct tm_engine {
     std::deque<std::pair<uint64_t, uint32_t>> pending_free;
     std::multiset<uint64_t> live_launches;
     uint64_t launch_seq = 0;
-    std::vector<uint8_t> n_hasbytes;   // n_foff / n_flen name this id's filter (until the id is reused)
     uint64_t live_nodes = 0, live_edges = 0, n_filters = 0;
     std::vector<uint8_t> fbytes;
 
@@ -648,7 +660,7 @@ struct tm_engine {
             bool was_empty;
             uint32_t i = place_slot(tab, e.parent, e.word, disp, was_empty);
             tab[i] = e;
-            n_inslot[e.child & ID_MASK] = i;
+            nd[e.child & ID_MASK].inslot = i;
             md = std::max(md, disp);
             ++used;
         }
@@ -675,7 +687,7 @@ struct tm_engine {
         max_disp = std::max(max_disp, disp);
         Slot& e = slots[i];
         e.parent = p; e.word = w; e.child = c;
-        n_inslot[c] = i;
+        nd[c].inslot = i;
         write_summary(c);
         ++live_edges;
         return i;
@@ -692,7 +704,7 @@ struct tm_engine {
     // tombstones until a full rebuild.
     void move_slot(uint32_t to, uint32_t from) {
         slots[to] = slots[from];
-        n_inslot[slots[to].child & ID_MASK] = to;
+        nd[slots[to].child & ID_MASK].inslot = to;
         Slot& e = slots[from];
         memset(&e, 0, sizeof(e));
         e.parent = SLOT_EMPTY;
@@ -713,8 +725,8 @@ struct tm_engine {
     }
 
     void delete_edge_of(uint32_t c) {
-        uint32_t i = n_inslot[c];
-        n_inslot[c] = NONE;
+        uint32_t i = nd[c].inslot;
+        nd[c].inslot = NONE;
         --live_edges;
         --used_slots;
         const uint32_t nb = nbuckets();
@@ -756,7 +768,7 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------ nodes
-    bool node_capacity_left() const { return !free_nodes.empty() || n_parent.size() < MAX_NODES; }
+    bool node_capacity_left() const { return !free_nodes.empty() || nd.size() < MAX_NODES; }
 
     void release_pending_ids() {
         const uint64_t watermark = live_launches.empty() ? ~0ull : *live_launches.begin();
@@ -785,16 +797,16 @@ struct tm_engine {
         if (!free_nodes.empty()) {
             id = free_nodes.back();
             free_nodes.pop_back();
-            n_hasbytes[id] = 0;
+            nd[id].hasbytes = 0;
         }
         else {
-            id = (uint32_t)n_parent.size();
-            n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
-            n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
-            n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0); n_hasbytes.push_back(0);
+            id = (uint32_t)nd.size();
+            nd.push_back(NodeRec{});
+            n_flen.push_back(0);
+            n_foff.push_back(0);
         }
-        n_parent[id] = parent; n_word[id] = word; n_ec[id] = 0; n_plus[id] = NONE; n_hash[id] = NONE;
-        n_inslot[id] = NONE; n_live[id] = 1; n_topic[id] = 0;
+        nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
+        nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
         ++live_nodes;
         return id;
     }
@@ -806,36 +818,36 @@ struct tm_engine {
             n_nroutes[id] = 0;
             routes_dirty = true;
         }
-        n_live[id] = 0;
-        n_topic[id] = 0;
-        n_ec[id] = 0;
+        nd[id].live = 0;
+        nd[id].topic = 0;
+        nd[id].ec = 0;
         --live_nodes;
         if (id != ROOT) pending_free.emplace_back(launch_seq, id);
     }
 
     uint32_t summary_flags(uint32_t c) const {
-        return (n_plus[c] != NONE ? NF_PLUS : 0) | (n_hash[c] != NONE ? NF_HASH : 0);
+        return (nd[c].plus != NONE ? NF_PLUS : 0) | (nd[c].hash != NONE ? NF_HASH : 0);
     }
     uint32_t hterm_of(uint32_t c) const {
-        const uint32_t h = n_hash[c];
-        return (h != NONE && n_topic[h]) ? h : NONE;
+        const uint32_t h = nd[c].hash;
+        return (h != NONE && nd[h].topic) ? h : NONE;
     }
 
     // rewrite c's summary into its incoming slot (or the root record)
     void write_summary(uint32_t c) {
         if (c == ROOT) return;   // root record is rebuilt at every launch
-        const uint32_t i = n_inslot[c];
+        const uint32_t i = nd[c].inslot;
         if (i == NONE) return;
         Slot& e = slots[i];
-        e.child = c | (n_topic[c] ? B_TOPIC : 0u) | (n_plus[c] != NONE ? B_PLUS : 0u);
-        const uint32_t h = n_hash[c];
-        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && n_topic[h]) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
+        e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
+        const uint32_t h = nd[c].hash;
+        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
         mark_dirty(i);
     }
 
     RootRec root_rec() const {
         RootRec r;
-        r.live = n_live[ROOT];
+        r.live = nd[ROOT].live;
         r.hterm = hterm_of(ROOT);
         r.flags = summary_flags(ROOT);
         r.pad = 0;
@@ -843,26 +855,26 @@ struct tm_engine {
     }
 
     void set_topic(uint32_t c, const uint8_t* bytes, size_t len) {
-        n_topic[c] = 1;
-        n_hasbytes[c] = 1;
+        nd[c].topic = 1;
+        nd[c].hasbytes = 1;
         ++n_filters;
         n_foff[c] = fbytes.size();
         n_flen[c] = (uint32_t)len;
         fbytes.insert(fbytes.end(), bytes, bytes + len);
         if (!full_f_dirty) {
-            if (dirty_f_mark.size() < n_parent.size()) dirty_f_mark.resize(n_parent.size(), 0);
+            if (dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
             if (!dirty_f_mark[c]) { dirty_f_mark[c] = 1; dirty_f.push_back(c); }
         }
         write_summary(c);
-        if (c != ROOT && n_word[c] == W_HASH) write_summary(n_parent[c]);
+        if (c != ROOT && nd[c].word == W_HASH) write_summary(nd[c].parent);
     }
 
     void clear_topic(uint32_t c) {
-        if (!n_topic[c]) return;
-        n_topic[c] = 0;
+        if (!nd[c].topic) return;
+        nd[c].topic = 0;
         --n_filters;
         write_summary(c);
-        if (c != ROOT && n_word[c] == W_HASH) write_summary(n_parent[c]);
+        if (c != ROOT && nd[c].word == W_HASH) write_summary(nd[c].parent);
     }
 
     // intern (insert=true) or look up the words of a filter / node id
@@ -880,52 +892,6 @@ struct tm_engine {
             ids.push_back(id);
         }
         return true;
-    }
-
-    // Bulk mutations (tm_trie_insert_many / delete_many, the churn path) walk
-    // a chunk of filters level by level first, every probe of a level
-    // prefetched before any is read, so the chunk's cache misses on the
-    // (hundreds-of-MB) edge hash overlap instead of costing one memory round
-    // trip per level per filter; the sequential insert / delete pass that
-    // follows finds the lines in cache.  Read-only: results are discarded.
-    static constexpr uint32_t WARM = 32;
-    void warm_paths(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi) {
-        static thread_local std::vector<uint32_t> ids[WARM];
-        uint32_t node[WARM], depth[WARM];
-        const uint32_t m = std::min<uint32_t>(hi - lo, WARM);
-        if (!n_live[ROOT]) return;
-        for (uint32_t i = 0; i < m; ++i) {
-            const uint8_t* f = buf + offs[lo + i];
-            filter_words_prefix(f, offs[lo + i + 1] - offs[lo + i], ids[i]);
-            node[i] = ROOT;
-            depth[i] = 0;
-        }
-        const uint32_t nb = nbuckets();
-        for (bool any = true; any;) {
-            any = false;
-            for (uint32_t i = 0; i < m; ++i)
-                if (node[i] != NONE && depth[i] < ids[i].size())
-                    __builtin_prefetch(&slots[(size_t)home_bucket(node[i], ids[i][depth[i]], nb) * BUCKET]);
-            for (uint32_t i = 0; i < m; ++i) {
-                if (node[i] == NONE || depth[i] >= ids[i].size()) continue;
-                const uint32_t sl = find_slot(node[i], ids[i][depth[i]]);
-                node[i] = sl == NONE ? NONE : (slots[sl].child & ID_MASK);
-                ++depth[i];
-                any = true;
-            }
-        }
-    }
-
-    // word ids of a filter up to its first word absent from the dictionary
-    void filter_words_prefix(const uint8_t* t, size_t len, std::vector<uint32_t>& ids) {
-        static thread_local std::vector<TWord> ws;
-        split_words(t, len, ws);
-        ids.clear();
-        for (const TWord& w : ws) {
-            const uint32_t id = w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find(w.p, w.n);
-            if (id == W_UNKNOWN) return;
-            ids.push_back(id);
-        }
     }
 
     // tm_dict_load: intern words in order ('', '+', '#' have fixed ids)
@@ -956,7 +922,7 @@ struct tm_engine {
     }
 
     uint32_t walk(const std::vector<uint32_t>& ids) const {
-        if (!n_live[ROOT]) return NONE;
+        if (!nd[ROOT].live) return NONE;
         uint32_t n = ROOT;
         for (uint32_t w : ids) {
             const uint32_t s = find_slot(n, w);
@@ -970,13 +936,21 @@ struct tm_engine {
     int trie_insert(const uint8_t* t, size_t len) {
         static thread_local std::vector<uint32_t> ids;
         if (!filter_words(t, len, true, ids)) return TM_ENOENT;   // frozen dictionary only
+        return trie_insert_ids(t, len, ids.data(), (uint32_t)ids.size(), ROOT, 0);
+    }
+
+    // insert/1 with the word ids known and the path known to exist down to
+    // `from` at level k0 (ROOT, 0 for a full walk)
+    int trie_insert_ids(const uint8_t* t, size_t len, const uint32_t* ids_p, uint32_t nids, uint32_t from,
+                        uint32_t k0) {
+        struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
         // add_path/1 for every triple (:145-158), in one walk: existing edges
         // are followed, the missing suffix is created
-        uint32_t p = ROOT;
+        uint32_t p = from;
         bool created = false;
-        for (size_t k = 0; k < ids.size(); ++k) {
+        for (size_t k = k0; k < ids.size(); ++k) {
             const uint32_t w = ids[k];
-            const uint32_t s = n_live[p] ? find_slot(p, w) : NONE;
+            const uint32_t s = nd[p].live ? find_slot(p, w) : NONE;
             uint32_t c;
             if (s != NONE) {
                 c = slots[s].child & ID_MASK;
@@ -984,23 +958,23 @@ struct tm_engine {
                 if (!created) {
                     // node ids are 30-bit (two flag bits ride in the slot's id words)
                     const size_t need = ids.size() - k;
-                    if (n_parent.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
+                    if (nd.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
                         return TM_ENOMEM;
                     created = true;
                 }
-                if (!n_live[p]) {               // only the root can be absent here
-                    n_live[p] = 1; n_ec[p] = 0; ++live_nodes;
+                if (!nd[p].live) {               // only the root can be absent here
+                    nd[p].live = 1; nd[p].ec = 0; ++live_nodes;
                 }
                 c = new_node(p, w);
-                ++n_ec[p];
-                if (w == W_PLUS) n_plus[p] = c;
-                else if (w == W_HASH) n_hash[p] = c;
+                ++nd[p].ec;
+                if (w == W_PLUS) nd[p].plus = c;
+                else if (w == W_HASH) nd[p].hash = c;
                 insert_edge(p, w, c);
                 write_summary(p);
             }
             p = c;
         }
-        if (!created && n_topic[p]) return TM_OK;   // inserted already: idempotent
+        if (!created && nd[p].topic) return TM_OK;   // inserted already: idempotent
         set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
         ++version;
         return TM_OK;
@@ -1012,8 +986,14 @@ struct tm_engine {
         if (!filter_words(t, len, false, ids)) return TM_OK;
         const uint32_t n = walk(ids);
         if (n == NONE) return TM_OK;
-        if (n_ec[n] != 0) {
-            if (n_topic[n]) { clear_topic(n); ++version; }
+        return trie_delete_at(n, ids.data(), (uint32_t)ids.size());
+    }
+
+    // delete/1 of the filter whose words are ids and whose node is n
+    int trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids) {
+        struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
+        if (nd[n].ec != 0) {
+            if (nd[n].topic) { clear_topic(n); ++version; }
             return TM_OK;
         }
         clear_topic(n);
@@ -1021,26 +1001,145 @@ struct tm_engine {
         int rc = TM_OK;
         bool child_dead = false;
         for (size_t k = ids.size(); k-- > 0;) {
-            const uint32_t p = n_parent[child];
+            const uint32_t p = nd[child].parent;
             const uint32_t w = ids[k];
             delete_edge_of(child);
             if (!child_dead) { kill_node(child); child_dead = true; }
-            if (w == W_PLUS) n_plus[p] = NONE;
-            else if (w == W_HASH) n_hash[p] = NONE;
-            if (!n_live[p]) { rc = TM_EABORT; break; }
-            if (n_ec[p] == 1 && !n_topic[p]) {
-                n_ec[p] = 0;
+            if (w == W_PLUS) nd[p].plus = NONE;
+            else if (w == W_HASH) nd[p].hash = NONE;
+            if (!nd[p].live) { rc = TM_EABORT; break; }
+            if (nd[p].ec == 1 && !nd[p].topic) {
+                nd[p].ec = 0;
                 if (p == ROOT) { kill_node(p); break; }
                 kill_node(p);
                 child = p;
                 continue;
             }
-            --n_ec[p];
+            --nd[p].ec;
             write_summary(p);
             break;
         }
         ++version;
         return rc;
+    }
+
+    // ------------------------------------------------------------ bulk plan
+    // Bulk mutations (tm_trie_insert_many / delete_many: subscribe churn, C5)
+    // split into a read-only PLAN over the whole batch, run by `threads`
+    // workers -- split into words, dictionary lookups, and the walk down the
+    // existing path (the edge-hash misses) -- and a serial pass that only
+    // mutates.  The plan stays valid through the serial pass: insert_many never
+    // removes a node, so a planned prefix still exists (the pass resumes the
+    // walk from it and sees edges earlier filters of the batch created);
+    // delete_many never creates one, and a node is only killed once no live
+    // filter lies below it, so a planned node that is still live is the
+    // filter's node (killed ids are not reused before the pass ends).
+    struct PlanEnt {
+        uint32_t node;    // deepest existing node (insert) / the filter's node or NONE (delete)
+        uint32_t depth;   // levels walked (insert)
+        uint32_t woff, nw;
+        uint32_t part;    // worker whose word vector holds the ids
+    };
+    std::vector<PlanEnt> plan;
+    std::vector<std::vector<uint32_t>> plan_words;
+
+    void plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part) {
+        std::vector<uint32_t>& W = plan_words[part];
+        W.clear();
+        std::vector<TWord> ws;
+        const bool root_live = nd[ROOT].live != 0;
+        for (uint32_t i = lo; i < hi; ++i) {
+            PlanEnt& pe = plan[i];
+            split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
+            pe.woff = (uint32_t)W.size();
+            pe.nw = (uint32_t)ws.size();
+            pe.part = part;
+            bool known = true;
+            for (const TWord& w : ws) {
+                const uint32_t id = w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find(w.p, w.n);
+                known &= id != W_UNKNOWN;
+                W.push_back(id);
+            }
+            // walk the existing path (words up to the first unknown one)
+            uint32_t n = ROOT, k = 0;
+            if (root_live) {
+                const uint32_t nb = nbuckets();
+                for (; k < pe.nw; ++k) {
+                    const uint32_t w = W[pe.woff + k];
+                    if (w == W_UNKNOWN) break;
+                    if (k + 1 < pe.nw) __builtin_prefetch(&slots[(size_t)home_bucket(n, w, nb) * BUCKET]);
+                    const uint32_t sl = find_slot(n, w);
+                    if (sl == NONE) break;
+                    n = slots[sl].child & ID_MASK;
+                }
+            }
+            if (del) pe.node = (root_live && known && k == pe.nw) ? n : NONE;
+            else { pe.node = n; pe.depth = k; }
+        }
+    }
+
+    void make_plan(const uint8_t* buf, const uint64_t* offs, uint32_t n, bool del) {
+        plan.resize(n);
+        const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 512));
+        if (plan_words.size() < nt) plan_words.resize(nt);
+        if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
+        std::vector<std::thread> th;
+        for (unsigned i = 0; i < nt; ++i) {
+            const uint32_t lo = (uint32_t)((uint64_t)n * i / nt), hi = (uint32_t)((uint64_t)n * (i + 1) / nt);
+            th.emplace_back([this, buf, offs, lo, hi, del, i] { plan_range(buf, offs, lo, hi, del, i); });
+        }
+        for (auto& x : th) x.join();
+    }
+
+    // the serial passes prefetch what filter i + PF_FAR / i + PF_NEAR will
+    // touch: their node records first, then the lines those records point at
+    static constexpr uint32_t PF_FAR = 16, PF_NEAR = 8;
+    void prefetch_insert(uint32_t i, uint32_t n) {
+        if (i + PF_FAR < n) __builtin_prefetch(&nd[plan[i + PF_FAR].node]);
+        if (i + PF_NEAR < n) {
+            const PlanEnt& q = plan[i + PF_NEAR];
+            if (q.depth < q.nw) {
+                const uint32_t w = plan_words[q.part][q.woff + q.depth];
+                if (w != W_UNKNOWN) __builtin_prefetch(&slots[(size_t)home_bucket(q.node, w, nbuckets()) * BUCKET]);
+            }
+            const size_t nf = free_nodes.size();
+            if (nf > PF_NEAR) __builtin_prefetch(&nd[free_nodes[nf - 1 - PF_NEAR]]);
+        }
+    }
+    void prefetch_delete(uint32_t i, uint32_t n) {
+        if (i + PF_FAR < n && plan[i + PF_FAR].node != NONE) __builtin_prefetch(&nd[plan[i + PF_FAR].node]);
+        if (i + PF_NEAR < n && plan[i + PF_NEAR].node != NONE) {
+            const NodeRec& r = nd[plan[i + PF_NEAR].node];
+            __builtin_prefetch(&nd[r.parent]);
+            if (r.inslot != NONE) {
+                __builtin_prefetch(&slots[r.inslot]);
+                if (r.inslot < dirty_mark.size()) __builtin_prefetch(&dirty_mark[r.inslot]);
+            }
+        }
+    }
+
+    int insert_planned(const uint8_t* buf, const uint64_t* offs, uint32_t i) {
+        PlanEnt& pe = plan[i];
+        uint32_t* ids = plan_words[pe.part].data() + pe.woff;
+        for (uint32_t k = pe.depth; k < pe.nw; ++k)
+            if (ids[k] == W_UNKNOWN) {   // new word (or interned by an earlier filter of the batch)
+                if (frozen) return TM_ENOENT;
+                const uint8_t* f = buf + offs[i];
+                static thread_local std::vector<TWord> ws;
+                split_words(f, offs[i + 1] - offs[i], ws);
+                for (uint32_t j = k; j < pe.nw; ++j)
+                    if (ids[j] == W_UNKNOWN) ids[j] = dict.intern(ws[j].p, ws[j].n);
+                break;
+            }
+        // the planned prefix was walked with the root live; a root created since
+        // (empty trie at plan time) restarts at ROOT, level 0
+        return trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i], ids, pe.nw, pe.node, pe.depth);
+    }
+
+    int delete_planned(uint32_t i) {
+        const PlanEnt& pe = plan[i];
+        if (pe.node == NONE || !nd[pe.node].live) return TM_OK;   // absent, or removed earlier in the batch
+        return trie_delete_at(pe.node, plan_words[pe.part].data() + pe.woff, pe.nw);
     }
 
     // ------------------------------------------------------------ device sync
@@ -1056,7 +1155,7 @@ struct tm_engine {
         static thread_local std::vector<uint32_t> ids;
         if (!filter_words(t, len, false, ids)) return NONE;
         const uint32_t n = walk(ids);
-        return (n != NONE && n_topic[n]) ? n : NONE;
+        return (n != NONE && nd[n].topic) ? n : NONE;
     }
 
     // emqx_router:do_add_route/2 (src/emqx_router.erl:113-124, 229-234)
@@ -1068,9 +1167,9 @@ struct tm_engine {
             n = node_of(t, len);
             if (n == NONE) return TM_EIO;
         }
-        if (n_dests.size() < n_parent.size()) {
-            n_dests.resize(n_parent.size());
-            n_nroutes.resize(n_parent.size(), 0);
+        if (n_dests.size() < nd.size()) {
+            n_dests.resize(nd.size());
+            n_nroutes.resize(nd.size(), 0);
         }
         auto& v = n_dests[n];
         bool found = false;
@@ -1107,8 +1206,8 @@ struct tm_engine {
 
     // dests CSR by node id -> HBM (rebuilt whole when routes changed)
     int sync_routes() {
-        if (!routes_dirty && c_roff >= n_parent.size() + 1) return TM_OK;
-        const size_t nn = n_parent.size();
+        if (!routes_dirty && c_roff >= nd.size() + 1) return TM_OK;
+        const size_t nn = nd.size();
         h_roff.assign(nn + 1, 0);
         h_rdest.clear();
         h_rdest.reserve(route_entries);
@@ -1143,7 +1242,7 @@ struct tm_engine {
         if ((rc = host_reserve(b->h_rtotal, b->ch_rtotal, 1))) return rc;
         RouteArgs r{};
         r.row_off = b->d_rowoff; r.ids = b->d_ids; r.n = n;
-        r.roff = d_roff; r.rdest = d_rdest; r.nnodes = (uint32_t)n_parent.size();
+        r.roff = d_roff; r.rdest = d_rdest; r.nnodes = (uint32_t)nd.size();
         r.rcount = b->d_rcount; r.r_rowoff = b->d_rrow; r.bsums = b->d_rbsums;
         HIP_OK(launch_route_count(r, stream));
         ScanArgs sa{};
@@ -1267,7 +1366,7 @@ struct tm_engine {
     // subscriber runs by node id -> HBM (rebuilt whole after subscription or
     // trie changes: a topic's node id is looked up at build time)
     int sync_subs() {
-        const size_t nn = n_parent.size();
+        const size_t nn = nd.size();
         if (!subs_dirty && subs_version == version && subs_nn == nn && d_soff) return TM_OK;
         h_soff.assign(nn + 1, 0);
         std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> runs;
@@ -1452,7 +1551,7 @@ struct tm_engine {
     bool upload_pending() {
         if (full_dirty || !dirty.empty() || d_nslots != slots.size() || needs_repack()) return true;
         if (full_f_dirty || !dirty_f.empty() || fbytes.size() > fbytes_uploaded) return true;
-        if (c_foff < n_parent.size() || c_flen < n_parent.size() || c_fbytes < fbytes.size() + 1) return true;
+        if (c_foff < nd.size() || c_flen < nd.size() || c_fbytes < fbytes.size() + 1) return true;
         if (dev_tok && (d_dict_n != dict.keys().size() || d_dict_gen != dict.gen() || !dict.dirty().empty() ||
                         dict.tails().size() > tails_uploaded || dict.arena().size() > arena_uploaded ||
                         c_arena < dict.arena().size() + 1))
@@ -1506,7 +1605,7 @@ struct tm_engine {
             async_used = true;
         }
         // filter bytes (slow-path sort) : arena + per-node (off, len)
-        const size_t nn = n_parent.size();
+        const size_t nn = nd.size();
         if (c_foff < nn || c_flen < nn) {
             if ((rc = dev_reserve(d_foff, c_foff, nn))) return rc;
             if ((rc = dev_reserve(d_flen, c_flen, nn))) return rc;
@@ -1625,10 +1724,11 @@ struct tm_engine {
     }
 
     // generic-path scratch of a batch: one frontier + match area per slow wave;
-    // 64 waves for small batches, up to 512 for large ones
+    // 64 waves for small batches (<= 16k topics), 512 from 128k topics up: a
+    // deduplicated skewed batch can send tens of thousands of long rows here
     int ensure_slow_scratch(tm_batch* b) {
         int rc;
-        if (!b->s_waves) b->s_waves = std::min<uint32_t>(512, std::max<uint32_t>(64, b->n / 2048));
+        if (!b->s_waves) b->s_waves = std::min<uint32_t>(512, std::max<uint32_t>(64, b->n / 256));
         const size_t q = (size_t)b->s_waves * b->s_qcap, o = (size_t)b->s_waves * b->s_ocap;
         if ((rc = dev_reserve(b->d_sqpar, b->c_sq, q))) return rc;
         if ((rc = dev_reserve(b->d_sqpw, b->c_sq2, q))) return rc;
@@ -1844,7 +1944,7 @@ struct tm_engine {
     // tm_batch_export
     int export_batch(tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
         if (!b->done) return TM_EINVAL;
-        const uint64_t top = (uint64_t)(n_parent.size() ? n_parent.size() - 1 : 0) * mul + add;
+        const uint64_t top = (uint64_t)(nd.size() ? nd.size() - 1 : 0) * mul + add;
         if (top > 0xFFFFFFFFull) return TM_EOVERFLOW;
         HIP_OK(launch_export(b->d_rowoff, b->d_ids, b->n, b->total, d_counts, d_ids, mul, add, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -2153,7 +2253,7 @@ struct tm_engine {
         a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;
         a.nwords = (uint32_t)std::max<uint64_t>(b->nwords, 1);
         a.nslots = (uint32_t)slots.size();
-        a.nnodes = (uint32_t)n_parent.size();
+        a.nnodes = (uint32_t)nd.size();
         a.nfbytes = fbytes.size();
         a.dbg = checked ? d_dbg : nullptr;
         HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
@@ -2615,9 +2715,9 @@ struct tm_engine {
         dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
         if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');
         // root node id 0 (absent until the first add_path, like the reference)
-        n_parent.push_back(0); n_word.push_back(0); n_ec.push_back(0); n_plus.push_back(NONE);
-        n_hash.push_back(NONE); n_inslot.push_back(NONE); n_flen.push_back(0);
-        n_foff.push_back(0); n_live.push_back(0); n_topic.push_back(0); n_hasbytes.push_back(0);
+        nd.push_back(NodeRec{});
+        n_flen.push_back(0);
+        n_foff.push_back(0);
         slots.clear();
         slots.resize(1024);
         for (Slot& s : slots) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
@@ -2785,16 +2885,16 @@ int tm_trie_lookup(tm_engine* e, const uint8_t* id, size_t len, int is_root, tm_
     std::lock_guard<std::recursive_mutex> g(e->mu);
     uint32_t n;
     if (is_root) {
-        n = e->n_live[ROOT] ? ROOT : NONE;
+        n = e->nd[ROOT].live ? ROOT : NONE;
     } else {
         std::vector<uint32_t> ids;
         if (!e->filter_words(id, len, false, ids)) return 0;
         n = e->walk(ids);
     }
     if (n == NONE) return 0;
-    out->edge_count = e->n_ec[n];
-    out->has_topic = e->n_topic[n];
-    out->filter_id = e->n_topic[n] ? n : TM_NONE;
+    out->edge_count = e->nd[n].ec;
+    out->has_topic = e->nd[n].topic;
+    out->filter_id = e->nd[n].topic ? n : TM_NONE;
     return 1;
 }
 
@@ -3168,10 +3268,19 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     for (uint32_t i = 0; i < n; ++i)
         if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
+        if (nshards <= 1) {
+            e->make_plan(filters, offsets, n, false);
+            for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
+                e->prefetch_insert(i, n);
+                rc = e->insert_planned(filters, offsets, i);
+                if (rc == TM_OK) ++done;
+            }
+            if (n_inserted) *n_inserted = done;
+            return rc;
+        }
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
             const uint8_t* f = filters + offsets[i];
             const size_t len = offsets[i + 1] - offsets[i];
-            if (i % tm_engine::WARM == 0 && nshards <= 1) e->warm_paths(filters, offsets, i, n);
             if (nshards > 1) {
                 const int s = e->filter_shard(f, len, nshards);
                 if (s < 0) { rc = s; break; }
@@ -3193,11 +3302,13 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     std::lock_guard<std::recursive_mutex> g(e->mu);
     uint64_t done = 0;
     int rc = TM_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
+        e->make_plan(filters, offsets, n, true);
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
-            if (offsets[i + 1] < offsets[i]) { rc = TM_EINVAL; break; }
-            if (i % tm_engine::WARM == 0) e->warm_paths(filters, offsets, i, n);
-            rc = e->trie_delete(filters + offsets[i], offsets[i + 1] - offsets[i]);
+            e->prefetch_delete(i, n);
+            rc = e->delete_planned(i);
             if (rc == TM_OK) ++done;
         }
     } catch (...) {
@@ -3308,7 +3419,7 @@ int tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_i
 const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
     if (!e) return nullptr;
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) return nullptr;   // matched ids keep their bytes
+    if (id >= e->nd.size() || !e->nd[id].hasbytes) return nullptr;   // matched ids keep their bytes
     if (len) *len = e->n_flen[id];
     static const uint8_t empty = 0;
     return e->n_flen[id] ? e->fbytes.data() + e->n_foff[id] : &empty;
@@ -3317,7 +3428,7 @@ const uint8_t* tm_filter_bytes(tm_engine* e, uint32_t id, size_t* len) {
 int tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* len) {
     if (!e || !len || (cap && !buf)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) return TM_ENOENT;
+    if (id >= e->nd.size() || !e->nd[id].hasbytes) return TM_ENOENT;
     *len = e->n_flen[id];
     if (*len <= cap && *len) memcpy(buf, e->fbytes.data() + e->n_foff[id], *len);
     return TM_OK;
@@ -3329,7 +3440,7 @@ int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf,
     std::lock_guard<std::recursive_mutex> g(e->mu);
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i)
-        if (ids[i] < e->n_hasbytes.size() && e->n_hasbytes[ids[i]]) total += e->n_flen[ids[i]];
+        if (ids[i] < e->nd.size() && e->nd[ids[i]].hasbytes) total += e->n_flen[ids[i]];
     *need = total;
     if (total > cap) return TM_OK;   // nothing copied: the caller grows buf and asks again
     uint32_t k = 0;
@@ -3337,7 +3448,7 @@ int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf,
     offs[0] = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t id = ids[i];
-        if (id >= e->n_hasbytes.size() || !e->n_hasbytes[id]) continue;
+        if (id >= e->nd.size() || !e->nd[id].hasbytes) continue;
         const uint32_t len = e->n_flen[id];
         if (len) memcpy(buf + at, e->fbytes.data() + e->n_foff[id], len);
         at += len;
@@ -3354,7 +3465,7 @@ int tm_filter_id(tm_engine* e, const uint8_t* f, size_t len, uint32_t* id) {
     std::vector<uint32_t> ids;
     if (!e->filter_words(f, len, false, ids)) return TM_ENOENT;
     const uint32_t n = e->walk(ids);
-    if (n == NONE || !e->n_topic[n]) return TM_ENOENT;
+    if (n == NONE || !e->nd[n].topic) return TM_ENOENT;
     *id = n;
     return TM_OK;
 }
@@ -3436,7 +3547,7 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
                     snprintf(last_error(), 512, "run of slot %u (home %u) broken at bucket %u", b * BUCKET + k, h, x);
                     return TM_EIO;
                 }
-            if (e->find_slot(sl.parent, sl.word) != b * BUCKET + k || e->n_inslot[sl.child & ID_MASK] != b * BUCKET + k) {
+            if (e->find_slot(sl.parent, sl.word) != b * BUCKET + k || e->nd[sl.child & ID_MASK].inslot != b * BUCKET + k) {
                 snprintf(last_error(), 512, "slot %u not found by its key", b * BUCKET + k);
                 return TM_EIO;
             }

@@ -34,12 +34,14 @@ from __future__ import annotations
 
 from typing import Callable, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 from .engine import Batch, Engine
 
 META_SHIFT = 2            # meta = depth << 2 | tflags (TF_DOLLAR = 1, TF_SLOW = 2)
+WID_MASK = (1 << 29) - 1  # word id bits of a token (tm_internal.hpp WID_BITS)
 
 
 def excl_cumsum(x: torch.Tensor) -> torch.Tensor:
@@ -89,6 +91,50 @@ class ShardedMatcher:
         """Shared dictionary, then this shard's filters + the replicated ones."""
         self.eng.dict_load(vocab)
         return self.eng.insert_many(filters, self.rank, self.world)
+
+    # ---- online subscribe / unsubscribe ---------------------------------------
+    # Word ids must agree on every shard, so new literal words cannot be
+    # interned by whichever rank happens to insert a filter first.  Every rank
+    # applies the same subscribe stream (the replicated route table's events,
+    # src/emqx_router_helper.erl / emqx_trie:insert/1 on each node), so the
+    # words a batch introduces -- collected in first-appearance order -- are
+    # appended to each rank's dictionary before its filters go in: an
+    # append-only dictionary delta that gives every rank the same new ids
+    # (tm_dict_load assigns ids in order), then each rank keeps its own shard.
+    def missing_words(self, filters) -> list:
+        """Literal words of `filters` absent from the shared dictionary, in
+        first-appearance order (tm_tokenize marks them UNKNOWN)."""
+        fl = list(filters)
+        if not fl:
+            return []
+        tok = self.eng.tokenize(fl)
+        ids = tok.words & WID_MASK
+        unknown = np.nonzero(ids == 0)[0]
+        if unknown.size == 0:
+            return []
+        toff = tok.toff.astype(np.int64)
+        which = np.searchsorted(toff, unknown, side="right") - 1   # filter of each unknown word
+        out, seen = [], set()
+        for i, w in zip(which.tolist(), unknown.tolist()):
+            word = fl[i].split(b"/")[w - int(toff[i])]
+            if word not in seen:
+                seen.add(word)
+                out.append(word)
+        return out
+
+    def subscribe(self, filters) -> int:
+        """emqx_trie:insert/1 of a subscribe batch, called with the same batch on
+        every rank: dictionary delta first, then this shard's filters and the
+        replicated ones.  Returns how many this rank inserted."""
+        new = self.missing_words(filters)
+        if new:
+            self.eng.dict_load(new)
+        return self.eng.insert_many(filters, self.rank, self.world)
+
+    def unsubscribe(self, filters) -> int:
+        """emqx_trie:delete/1 of an unsubscribe batch on every rank (filters of
+        other shards are absent here: no-ops).  Words stay interned."""
+        return self.eng.delete_many(filters)
 
     # ---- device pieces -------------------------------------------------------
     def _shards(self, words: torch.Tensor, toff: torch.Tensor, n: int) -> torch.Tensor:

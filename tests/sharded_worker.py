@@ -136,7 +136,50 @@ def main(rank, world, port, seed, mode="cpu"):
         sm = ShardedMatcher(eng, rank, world)
     else:
         sm = ShardedMatcher(eng, rank, world, shard_fn=shard_fn, local_match=local_match)
-    # each rank publishes its own slice of the topics
+    check_step(sm, eng, F, T_all, mine, rank, world, gpu)
+
+    # online churn under the frozen dictionary: subscribes that bring new
+    # literal words (in levels 0/1, so they pick a shard, and deeper), and
+    # unsubscribes; every rank applies the same batches
+    rng = random.Random(seed + 7)
+    new_f = sorted({b"/".join([b"nw%d" % rng.randrange(40), rng.choice([b"d1", b"nx%d" % rng.randrange(9), b"+"]),
+                               rng.choice([b"#", b"k%d" % rng.randrange(5), b"sensor"])]) for _ in range(300)}
+                   | {b"device/nz%d/#" % k for k in range(20)} | {b"+/+/q%d" % k for k in range(10)})
+    new_f = [f for f in new_f if f not in set(F)]
+    gone = F[::7]
+    new_words = sm.missing_words(new_f)
+    assert new_words and len(set(new_words)) == len(new_words)
+    n_new = sm.subscribe(new_f)
+    sm.unsubscribe(gone)
+    F2 = [f for f in F if f not in set(gone)] + new_f
+    # the appended words got the same ids on every rank
+    wid = torch.from_numpy(eng.tokenize(new_words).words.view(np.int32).copy())
+    all_wid = [torch.empty_like(wid) for _ in range(world)]
+    dist.all_gather(all_wid, wid)
+    assert all(torch.equal(all_wid[0], x) for x in all_wid), "dictionary deltas diverged"
+    assert (wid & WID_MASK).min() >= W_FIRST + len(vocab)
+    for k, w in enumerate(new_words):
+        words_of[W_FIRST + len(vocab) + k] = w
+    mine2 = [f for f in F2 if eng.filter_shard(f, G) in (rank, G)]
+    assert n_new == sum(1 for f in new_f if f in set(mine2))
+    assert eng.stats()["filters"] == len(mine2)
+    mine[:] = mine2
+    orc.__init__()
+    for f in mine:
+        orc.register(f)
+        orc.insert(f)
+    T2 = T_all + [b"/".join([b"nw%d" % rng.randrange(40), rng.choice([b"d1", b"nx%d" % rng.randrange(9), b"zz"]),
+                             rng.choice([b"k%d" % rng.randrange(5), b"sensor", b"zz"])]) for _ in range(600)]
+    T2 += [b"device/nz%d/a/b" % k for k in range(20)] + [b"x/y/q%d" % k for k in range(10)]
+    check_step(sm, eng, F2, T2, mine, rank, world, gpu)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def check_step(sm, eng, F, T_all, mine, rank, world, gpu):
+    """One exchange step over this rank's slice of T_all; rows must equal the
+    oracle's over the full filter set F."""
+    G = world
     T = T_all[rank::world]
     tok = eng.tokenize(T)
     words = torch.from_numpy(tok.words.view(np.int32).copy())
@@ -176,8 +219,6 @@ def main(rank, world, port, seed, mode="cpu"):
     stats = torch.tensor([moved, len(T)], dtype=torch.int64)
     dist.all_reduce(stats)
     assert stats[0] > 0
-    dist.barrier()
-    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -10,10 +10,15 @@ from emqx_amd.engine import Engine
 from oracle import oracle as O
 
 
-def _churn(seed, n_words, pool_n, live_n, steps, check_every):
+def _churn(seed, n_words, pool_n, live_n, steps, check_every, wild=False):
     rng = random.Random(seed)
     words = [b"w%d" % i for i in range(n_words)]
-    pool = list({b"/".join(rng.choice(words) for _ in range(rng.randint(1, 3))) for _ in range(pool_n)})
+    if wild:   # '+' chains and '#' leaves: wildcard edges of every depth
+        words += [b"+"] * (n_words // 2)
+        pool = {b"/".join(rng.choice(words) for _ in range(rng.randint(1, 5))) for _ in range(pool_n)}
+        pool = list(pool | {p + b"/#" for p in list(pool)[: pool_n // 8]})
+    else:
+        pool = list({b"/".join(rng.choice(words) for _ in range(rng.randint(1, 3))) for _ in range(pool_n)})
     e, t = Engine(device=-1), O.Trie()
     live = set()
     for f in pool[:live_n]:
@@ -52,3 +57,11 @@ def test_churn_keeps_every_probe_run_intact():
 def test_churn_small_tables_many_seeds():
     for seed in range(12):
         _churn(seed=100 + seed, n_words=40, pool_n=3000, live_n=1500, steps=6000, check_every=97)
+
+
+def test_churn_plus_chains():
+    # wildcard-heavy churn: '+' chains, '#' leaves, shared prefixes
+    worst = _churn(seed=7, n_words=60, pool_n=30000, live_n=15000, steps=30000, check_every=499, wild=True)
+    assert worst >= 2
+    for seed in range(6):
+        _churn(seed=300 + seed, n_words=8, pool_n=3000, live_n=1500, steps=6000, check_every=97, wild=True)
