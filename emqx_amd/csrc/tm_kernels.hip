@@ -50,6 +50,8 @@ constexpr uint32_t M_DSTART = 1u << 12;  // $-rooted start probe: the node was a
 static_assert(FAST_MAX_DEPTH <= (int)M_LVL_MASK, "level field too narrow");
 constexpr uint32_t M_DISP_SHIFT = 13;    // bucket displacement of a continued probe (<= max_probe <= 48)
 constexpr uint32_t M_DISP_MASK = 0x3F;
+constexpr uint32_t Q_FOUND = 0xFFFFFFFFu;   // probe-entry marks written by the quad (parent / word fields)
+constexpr uint32_t Q_TAIL = 0xFFFFFFFFu;
 
 // digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
 //   L = literal branch, H = '#' terminal, P = '+' branch; E = 0, L_lo = 1.
@@ -220,15 +222,18 @@ __device__ __forceinline__ uint4 q_pack(uint64_t key, uint32_t meta, uint32_t pa
 }
 
 // Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
+// wrows = this wave's rows (rows + blockIdx.x * tile_topics * K), hoisted by the caller.
 template <bool CK>
-__device__ __forceinline__ void emit_row(const MatchArgs& a, uint32_t tl, uint32_t slot, uint64_t key, uint32_t fid) {
+__device__ __forceinline__ void emit_row(const MatchArgs& a, unsigned long long* wrows, uint32_t tl, uint32_t slot,
+                                         uint64_t key, uint32_t fid) {
 #ifdef TM_EXPERIMENT_NO_EMIT   // timing experiments only
     if (slot < a.row_cap && fid == 0xFFFFFFF0u) {
 #else
     if (slot < a.row_cap) {
 #endif
-        const uint64_t i = ((uint64_t)blockIdx.x * a.tile_topics + tl) * a.row_cap + slot;
-        a.rows[CK_(i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13)] = (key & KEY_MASK) | fid;
+        const uint32_t i = tl * a.row_cap + slot;   // < tile_topics * K <= 2^16
+        if (CK) (void)CK_((uint64_t)blockIdx.x * a.tile_topics * a.row_cap + i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13);
+        wrows[i] = (key & KEY_MASK) | fid;
     }
 }
 
@@ -416,6 +421,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     uint32_t qn = 0;
     bool ovf = false;
     const bool active = !(fl & TF_SLOW);
+    unsigned long long* const wrows = a.rows + (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
     uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
     const uint32_t d_me = L.depth[lane];
 
@@ -440,7 +446,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         qn += __popcll(b0) + __popcll(b1);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
-            emit_row<CK>(a, lane, 0, x.ek0, x.ef0);
+            emit_row<CK>(a, wrows, lane, 0, x.ek0, x.ef0);
         }
     }
 
@@ -505,56 +511,81 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
                 sl[r] = v ? reinterpret_cast<const uint4*>(a.slots)[si] : uint4{0u, 0u, 0u, 0u};
             }
         }
-        uint64_t mm[4], te[4];
+        // The quad reports to the owner through the owner's LDS entry, not
+        // through ballots: the matching lane writes the child summary and a
+        // FOUND mark, the lane of the bucket's last slot a TAIL mark when that
+        // slot is free (the probe run ends in this bucket).  Parent ids and
+        // word ids never equal the marks.
 #pragma unroll
         for (uint32_t r = 0; r < 4; ++r) {
             const bool m = rp[r] != SLOT_EMPTY && sl[r].x == rp[r] && sl[r].y == rw[r];
-            mm[r] = __ballot(m);
-            te[r] = __ballot(qs == 3 && sl[r].x == SLOT_EMPTY);   // bucket has a free tail: the run ends here
             if (m) {
                 L.q[qn + 16 * r + qd].x = sl[r].z;
                 L.q[qn + 16 * r + qd].y = sl[r].w;
+                L.q[qn + 16 * r + qd].z = Q_FOUND;
             }
+            if (qs == 3 && sl[r].x == SLOT_EMPTY) L.q[qn + 16 * r + qd].w = Q_TAIL;   // out-of-range loads read 0
         }
-        const uint32_t myr = lane >> 4, myq = lane & 15;
-        const uint64_t mym = myr == 0 ? mm[0] : myr == 1 ? mm[1] : myr == 2 ? mm[2] : mm[3];
-        const uint64_t myt = myr == 0 ? te[0] : myr == 1 ? te[1] : myr == 2 ? te[2] : te[3];
-        const bool found = has && ((mym >> (4 * myq)) & 0xF) != 0;
-        const bool cont = has && !found && !((myt >> (4 * myq + 3)) & 1) && disp < a.max_probe;
+        uint4 res = uint4{0u, 0u, 0u, 0u};
+        if (has) res = L.q[idx];
+        const bool found = has && res.z == Q_FOUND;
+        const bool cont = has && !found && res.w != Q_TAIL && disp < a.max_probe;
         Node s;
         s.child = 0; s.term = NONE; s.hterm = NONE; s.flags = 0;
         if (found) {
-            const uint4 res = L.q[idx];
             const uint32_t hz = res.x, hw = res.y;
             s.child = hz & ID_MASK;
             s.term = (hz & B_TOPIC) ? s.child : NONE;
             s.hterm = (hw & B_HTERM) ? (hw & ID_MASK) : NONE;
             s.flags = ((hz & B_PLUS) ? NF_PLUS : 0u) | ((hw & B_HASH) ? NF_HASH : 0u);
         }
-        Expand x; x.ne = 0; x.np = 0;
+        // Expansion of the found node, match_node/3 (src/emqx_trie.erl:168-177),
+        // with fixed roles instead of expand()'s packed lists: emissions A, B;
+        // push L (the literal word, or the continuation) and push P ('+').
+        // lc <= FAST_MAX_DEPTH here, so every level has a digit position.
+        const bool at_end = lc == d;
+        const uint32_t cls = w_here >> WID_BITS, id = w_here & WID_MASK;
+        const int sh = key_shift(lc);
+        bool eA = false, eB = false, pL = false, pP = false;
+        uint32_t fA = 0;
+        uint64_t kA = key;
         if (found) {
             if (!(meta & M_DSTART)) tV += 1;
             if (s.flags & NF_HASH) tH += 1;
-            expand(s, lc, d, meta, key, w_here, w_prev, x);
+            if (at_end) {   // end of the words: own topic, then the '#' child's
+                eA = !(meta & M_SKIPE) && s.term != NONE;
+                fA = s.term;
+                // '' word at level lc-1 followed by the end: "P/" sorts before "P/#"
+                if ((w_prev >> WID_BITS) == C_EMPTY) {
+                    const int sp = key_shift(lc - 1);
+                    if (((kA >> sp) & 7) == 4) kA = (kA & ~(7ull << sp)) | (1ull << sp);
+                }
+                eB = s.hterm != NONE;
+            } else {        // '#' child's topic, then the literal and '+' edges
+                eA = s.hterm != NONE;
+                fA = s.hterm;
+                kA = key | ((uint64_t)dig_H(cls) << sh);
+                pL = id == W_HASH ? (s.flags & NF_HASH) != 0 : (id != W_UNKNOWN && id != W_PLUS);
+                pP = (s.flags & NF_PLUS) != 0;
+            }
         }
-        const uint32_t np = cont ? 1u : x.np;
-        const uint64_t b0 = __ballot(np >= 1), b1 = __ballot(np >= 2);
-        const uint32_t ptot = __popcll(b0) + __popcll(b1);
+        const bool sL = cont || pL;
+        const uint64_t bL = __ballot(sL), bP = __ballot(pP);
+        const uint32_t ptot = __popcll(bL) + __popcll(bP);
         if (qn + ptot > (uint32_t)LT::QCAP) { ovf = true; break; }
-        const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+        const uint32_t pre = qn + prefix_count(bL) + prefix_count(bP);
         const uint32_t nmeta = tl | ((lc + 1) << M_LVL_SHIFT);
-        const uint32_t wid = w_here & WID_MASK;
-        if (cont) {
-            L.q[qn + pre] = q_pack(key, meta + (1u << M_DISP_SHIFT), parent, pw);
-        } else {
-            if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, nmeta | x.pf0, s.child, (x.pf0 & M_PLUS) ? W_PLUS : wid);
-            if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, nmeta | x.pf1, s.child, (x.pf1 & M_PLUS) ? W_PLUS : wid);
+        if (sL) {
+            const uint32_t lfl = (id == W_HASH && lc + 1 == d) ? M_SKIPE : 0u;
+            L.q[pre] = cont ? q_pack(key, meta + (1u << M_DISP_SHIFT), parent, pw)
+                            : q_pack(key | ((uint64_t)dig_L(cls) << sh), nmeta | lfl, s.child, id);
         }
+        if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key | ((uint64_t)dig_P(cls) << sh), nmeta | M_PLUS, s.child, W_PLUS);
         qn += ptot;
-        if (x.ne) {
-            const uint32_t slot = atomicAdd(&L.cnt[tl], x.ne);
-            emit_row<CK>(a, tl, slot, x.ek0, x.ef0);
-            if (x.ne >= 2) emit_row<CK>(a, tl, slot + 1, x.ek1, x.ef1);
+        if (eA | eB) {
+            const uint32_t slot = atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));
+            if (eA) emit_row<CK>(a, wrows, tl, slot, kA, fA);
+            if (eB) emit_row<CK>(a, wrows, tl, slot + (eA ? 1u : 0u), key | (2ull << sh), s.hterm);
         }
     }
     __syncthreads();
