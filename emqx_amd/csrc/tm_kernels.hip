@@ -487,14 +487,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             if (hb >= a.nbuckets) hb -= a.nbuckets;
             L.q[idx].x = hb;
         }
-        // the topic's words are read while the buckets are in flight
-        uint32_t d = 0, w_here = 0, w_prev = 0;
-        if (has) {
-            const uint32_t base = L.toff[tl];
-            d = L.depth[tl];
-            w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
-            w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
-        }
         uint32_t rp[4], rw[4];
         uint4 sl[4];
 #pragma unroll
@@ -510,6 +502,17 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             } else {
                 sl[r] = v ? reinterpret_cast<const uint4*>(a.slots)[si] : uint4{0u, 0u, 0u, 0u};
             }
+        }
+        // the topic's words are read while the buckets are in flight (the
+        // barrier keeps the compiler from hoisting these LDS reads, and their
+        // waits, above the bucket loads)
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t d = 0, w_here = 0, w_prev = 0;
+        if (has) {
+            const uint32_t base = L.toff[tl];
+            d = L.depth[tl];
+            w_here = lc < d ? wsrc[CK_(base + lc, wlim, 11)] : 0u;
+            w_prev = wsrc[CK_(base + lc - 1, wlim, 10)];
         }
         // The quad reports to the owner through the owner's LDS entry, not
         // through ballots: the matching lane writes the child summary and a
