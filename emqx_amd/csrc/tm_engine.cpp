@@ -363,6 +363,8 @@ struct tm_batch {
     size_t c_nslow = 0, ch_bad = 0;
     // route resolution (tm_batch_routes)
     uint32_t *d_rcount = nullptr, *d_rrow = nullptr, *d_rbsums = nullptr, *d_rfid = nullptr, *d_rdest = nullptr;
+    uint32_t* d_reoff = nullptr;   // route scan over match entries
+    size_t c_reoff = 0;
     uint32_t *d_rtotal = nullptr, *h_rtotal = nullptr, *h_rrow = nullptr, *h_rfid = nullptr, *h_rdest = nullptr;
     size_t c_rcount = 0, c_rrow = 0, c_rbsums = 0, c_rfid = 0, c_rdest = 0, c_rtotal = 0;
     size_t ch_rtotal = 0, ch_rrow = 0, ch_rfid = 0, ch_rdest = 0;
@@ -389,6 +391,7 @@ struct tm_batch {
         if (fev0) (void)hipEventDestroy(fev0);
         if (fev1) (void)hipEventDestroy(fev1);
         fev0 = fev1 = nullptr;
+        dev_free(d_reoff);
         dev_free(d_rcount); dev_free(d_rrow); dev_free(d_rbsums); dev_free(d_rfid); dev_free(d_rdest); dev_free(d_rtotal);
         for (uint32_t** h : {&h_rtotal, &h_rrow, &h_rfid, &h_rdest}) {
             if (*h) (void)hipHostFree(*h);
@@ -1235,19 +1238,29 @@ struct tm_engine {
         if ((rc = sync_routes())) return rc;
         const uint32_t n = b->n;
         const size_t nn = std::max<size_t>(n, 1);
-        if ((rc = dev_reserve(b->d_rcount, b->c_rcount, nn))) return rc;
+        const uint64_t m64 = b->total;   // match entries (< 2^32: u32 result CSR)
+        if (m64 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        const uint32_t m = (uint32_t)m64;
+        if ((rc = dev_reserve(b->d_rcount, b->c_rcount, (size_t)m + 1))) return rc;    // per-entry counts
+        if ((rc = dev_reserve(b->d_reoff, b->c_reoff, (size_t)m + 1))) return rc;
         if ((rc = dev_reserve(b->d_rrow, b->c_rrow, nn + 1))) return rc;
-        if ((rc = dev_reserve(b->d_rbsums, b->c_rbsums, (size_t)scan_block_count(n) + 1))) return rc;
+        if ((rc = dev_reserve(b->d_rbsums, b->c_rbsums, (size_t)scan_block_count(m) + 1))) return rc;
         if ((rc = dev_reserve(b->d_rtotal, b->c_rtotal, 1))) return rc;
         if ((rc = host_reserve(b->h_rtotal, b->ch_rtotal, 1))) return rc;
         RouteArgs r{};
-        r.row_off = b->d_rowoff; r.ids = b->d_ids; r.n = n;
+        r.row_off = b->d_rowoff; r.ids = b->d_ids; r.n = n; r.m = m;
         r.roff = d_roff; r.rdest = d_rdest; r.nnodes = (uint32_t)nd.size();
-        r.rcount = b->d_rcount; r.r_rowoff = b->d_rrow; r.bsums = b->d_rbsums;
+        r.ecount = b->d_rcount; r.eoff = b->d_reoff; r.bsums = b->d_rbsums; r.total = b->d_rtotal;
+        r.r_rowoff = b->d_rrow;
         HIP_OK(launch_route_count(r, stream));
         ScanArgs sa{};
-        sa.count = b->d_rcount; sa.row_off = b->d_rrow; sa.block_sums = b->d_rbsums; sa.n = n;
-        HIP_OK(launch_scan(sa, stream, b->d_rtotal));
+        sa.count = b->d_rcount; sa.row_off = b->d_reoff; sa.block_sums = b->d_rbsums; sa.n = m;
+        if (m) {
+            HIP_OK(launch_scan(sa, stream, b->d_rtotal));
+        } else {
+            HIP_OK(hipMemsetAsync(b->d_rtotal, 0, 4, stream));
+        }
+        HIP_OK(launch_route_rows(r, stream));
         HIP_OK(hipMemcpyAsync(b->h_rtotal, b->d_rtotal, 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
         const uint64_t total = b->h_rtotal[0];

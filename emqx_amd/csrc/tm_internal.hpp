@@ -191,16 +191,21 @@ struct ScanArgs {
 };
 
 // Route resolution over a batch's match CSR (tm_batch_routes).
+// Entry-parallel: one thread per match entry, so a topic matching thousands of
+// filters (C5 skew) costs no more per thread than one matching a few.
 struct RouteArgs {
-    const uint32_t* row_off;  // match CSR (n + 1) and filter ids
+    const uint32_t* row_off;  // match CSR (n + 1) and filter ids (m entries)
     const uint32_t* ids;
     uint32_t n;
+    uint32_t m;
     const uint32_t* roff;     // per node id: dests roff[f] .. roff[f+1] (nnodes + 1)
     const uint32_t* rdest;
     uint32_t nnodes;
-    uint32_t* rcount;         // per topic: number of routes
-    uint32_t* r_rowoff;       // n + 1: route CSR offsets (block-local until tm_route_fill)
-    uint32_t* bsums;          // scan block sums
+    uint32_t* ecount;         // per match entry: dests of its filter
+    uint32_t* eoff;           // m + 1: exclusive scan of ecount (block-local + bsums)
+    uint32_t* bsums;          // scan block sums (SCAN_TILE entries per block)
+    const uint32_t* total;    // routes in the batch (scan total)
+    uint32_t* r_rowoff;       // n + 1: route CSR offsets
     uint32_t* out_fid;        // route i: filter id, dest
     uint32_t* out_dest;
     uint64_t cap;             // capacity of out_fid / out_dest
@@ -251,6 +256,7 @@ hipError_t launch_rules_match(const RulesArgs& a, hipStream_t s);
 hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const int64_t* idx, uint32_t n,
                               const int64_t* dst_off, uint32_t* dst, hipStream_t s);
 hipError_t launch_route_count(const RouteArgs& a, hipStream_t s);
+hipError_t launch_route_rows(const RouteArgs& a, hipStream_t s);
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s);
 // fan-out: per-match delivery counts + u64 scan (moff, d_total), publish row
 // offsets (drow), then the load-balanced subscriber copy (out[total])

@@ -1035,31 +1035,33 @@ __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
 // Routes per topic = sum over its matched filters of their dest counts
 // (lookup_routes/1 for every To in [Topic | Matched], src/emqx_router.erl:132;
 // the topic itself is in the trie, so Matched already holds an exact route).
+// Routes of a batch = for every match entry, the dests of its filter, in
+// match order (emqx_router:match_routes/1 + aggre/1 per publish,
+// src/emqx_router.erl:127-133, src/emqx_broker.erl:250-261): the route CSR is
+// an exclusive scan of per-ENTRY dest counts, and a topic's first route is its
+// first entry's offset.  One thread per entry in each kernel.
 __global__ __launch_bounds__(256) void tm_route_count(RouteArgs a) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.n) return;
-    uint32_t c = 0;
-    for (uint32_t i = a.row_off[t], e = a.row_off[t + 1]; i < e; ++i) {
-        const uint32_t f = a.ids[i];
-        if (f < a.nnodes) c += a.roff[f + 1] - a.roff[f];
-    }
-    a.rcount[t] = c;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.m) return;
+    const uint32_t f = a.ids[i];
+    a.ecount[i] = f < a.nnodes ? a.roff[f + 1] - a.roff[f] : 0u;
 }
-
-// Writes each topic's (filter, dest) pairs at its global route offset
-// (finishes the block-local scan of rcount, like tm_finalize does for ids).
-__global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
+__device__ __forceinline__ uint32_t route_eoff(const RouteArgs& a, uint32_t j) {
+    return j < a.m ? a.eoff[j] + a.bsums[j / SCAN_TILE] : *a.total;
+}
+__global__ __launch_bounds__(256) void tm_route_rows(RouteArgs a) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.n) return;
-    uint64_t o = (uint64_t)a.r_rowoff[t] + a.bsums[t / SCAN_TILE];
-    a.r_rowoff[t] = (uint32_t)o;
-    for (uint32_t i = a.row_off[t], e = a.row_off[t + 1]; i < e; ++i) {
-        const uint32_t f = a.ids[i];
-        if (f >= a.nnodes) continue;
-        for (uint32_t k = a.roff[f], ke = a.roff[f + 1]; k < ke && o < a.cap; ++k, ++o) {
-            a.out_fid[o] = f;
-            a.out_dest[o] = a.rdest[k];
-        }
+    if (t <= a.n) a.r_rowoff[t] = route_eoff(a, a.row_off[t]);
+}
+__global__ __launch_bounds__(256) void tm_route_fill(RouteArgs a) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.m) return;
+    const uint32_t f = a.ids[i];
+    if (f >= a.nnodes) return;
+    uint64_t o = route_eoff(a, i);
+    for (uint32_t k = a.roff[f], ke = a.roff[f + 1]; k < ke && o < a.cap; ++k, ++o) {
+        a.out_fid[o] = f;
+        a.out_dest[o] = a.rdest[k];
     }
 }
 
@@ -1957,12 +1959,17 @@ hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked) {
 }
 
 hipError_t launch_route_count(const RouteArgs& a, hipStream_t s) {
-    if (a.n) hipLaunchKernelGGL(tm_route_count, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    if (a.m) hipLaunchKernelGGL(tm_route_count, dim3((a.m + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_rows(const RouteArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(tm_route_rows, dim3((a.n + 1 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_route_fill(const RouteArgs& a, hipStream_t s) {
-    if (a.n) hipLaunchKernelGGL(tm_route_fill, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    if (a.m) hipLaunchKernelGGL(tm_route_fill, dim3((a.m + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
