@@ -75,3 +75,33 @@ def test_routes_random_with_groups_and_churn():
             exp = [(live[int(j)], a) for j in idx[cut[t]:cut[t + 1]] for a in bag[live[int(j)]]]
             got = [(eng.filter_bytes(int(fids[k])), inv[int(dests[k])]) for k in range(offs[t], offs[t + 1])]
             assert got == exp, (rnd, T[t])
+
+
+def test_routes_skewed_rows_entry_parallel():
+    """C5-style skew: hot topics matched by hundreds of filters (rows past the
+    fast path's K, generic kernel) next to cold ones, every filter routed to
+    1-3 destinations: the entry-parallel route kernels (per-entry counts, a
+    multi-block scan over the entries, per-entry fill) against the oracle."""
+    hot, derived = gen.gen_skew(gen.SkewParams(n_hot=40, k_per_hot=400, seed=13))
+    F = sorted(set(derived.tolist()))
+    T = hot.tolist() + gen.gen_topics(replace(gen.C1, n_filters=2000), gen.Strings.from_list(F), 4, 2000).tolist()
+    eng = Engine(device=0)
+    ndest = {}
+    for i, f in enumerate(F):
+        ndest[f] = 1 + i % 3
+        for d in range(ndest[f]):
+            eng.route_add(f, d)
+    offs, fids, dests = eng.match_routes_batch(T)
+    orc = P.Oracle()
+    for f in F:
+        orc.register(f)
+        orc.insert(f)
+    buf, o = P.pack(T)
+    counts, idx, _ = orc.match_batch(buf, o)
+    assert int(counts[:len(hot)].max()) > 128          # rows past K took the generic path
+    assert int(counts.sum()) > 4 * 4096                # the entry scan spans several blocks
+    cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    for t in range(len(T)):
+        exp = [(F[int(j)], d) for j in idx[cut[t]:cut[t + 1]] for d in range(ndest[F[int(j)]])]
+        got = [(eng.filter_bytes(int(fids[k])), int(dests[k])) for k in range(offs[t], offs[t + 1])]
+        assert got == exp, T[t]
