@@ -1235,16 +1235,53 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     }
     uint4* own4 = reinterpret_cast<uint4*>(own);
     for (uint32_t i = t; i < FAN_FILL_TILE / 8; i += FAN_BLOCK) own4[i] = make_uint4(0, 0, 0, 0);
+    // The entries [jlo, jhi + 1] lie in at most two scan blocks (ne + 1 <=
+    // FAN_LDS_ENTRIES + 1 < FAN_SCAN_TILE): their "big" flags and offsets are
+    // read once, so an entry's delivery offset is one load, not a flag load
+    // and then the offset load.
+    const uint64_t sb0 = jlo / FAN_SCAN_TILE;
+    const uint64_t nsb = a.n_matches / FAN_SCAN_TILE + 1;   // scan blocks over n_matches + 1 entries
+    const bool big0 = a.bbig[sb0], big1 = sb0 + 1 < nsb ? a.bbig[sb0 + 1] != 0 : false;
+    const uint64_t bs0 = a.bsums[sb0], bs1 = sb0 + 1 < nsb ? a.bsums[sb0 + 1] : 0;
+    auto moff_at = [&](uint64_t j) -> uint64_t {
+        const bool hi = j / FAN_SCAN_TILE != sb0;
+        return ((hi ? big1 : big0) ? a.moff[j] : (uint64_t)a.moff32[j]) + (hi ? bs1 : bs0);
+    };
     __syncthreads();
-    for (uint32_t e = t; e < (uint32_t)ne; e += FAN_BLOCK) {
-        const uint64_t j = jlo + e;
-        const uint64_t m0 = fan_moff(a, j), m1 = fan_moff(a, j + 1);
-        if (m1 > m0 && m1 > start && m0 < end) {
+    // staging, FAN_STG entries per thread with every load of a step in flight
+    // (the offsets and filter ids, then the dependent sone / soff gathers)
+    constexpr uint32_t FAN_STG = 4;
+    for (uint32_t e0 = t; e0 < (uint32_t)ne; e0 += FAN_BLOCK * FAN_STG) {
+        uint64_t m0[FAN_STG], m1[FAN_STG];
+        uint32_t f[FAN_STG];
+        bool act[FAN_STG];
+#pragma unroll
+        for (uint32_t u = 0; u < FAN_STG; ++u) {
+            const uint32_t e = e0 + u * FAN_BLOCK;
+            m0[u] = 0; m1[u] = 0; f[u] = 0;
+            if (e < (uint32_t)ne) {
+                const uint64_t j = jlo + e;
+                m0[u] = moff_at(j);
+                m1[u] = moff_at(j + 1);
+                f[u] = a.ids[j];
+            }
+        }
+        int64_t v[FAN_STG];
+#pragma unroll
+        for (uint32_t u = 0; u < FAN_STG; ++u) {
+            act[u] = m1[u] > m0[u] && m1[u] > start && m0[u] < end;
+            v[u] = 0;
             // a one-delivery run keeps its subscriber inline (one 4-B gather,
             // no dependent read of subs[]): INT64_MIN + id marks it
-            const uint32_t f = a.ids[j];
-            base[e] = m1 - m0 == 1 ? INT64_MIN + (int64_t)a.sone[f] : (int64_t)a.soff[f] - (int64_t)m0;
-            own[m0 > start ? (uint32_t)(m0 - start) : 0u] = (uint16_t)(e + 1);
+            if (act[u]) v[u] = m1[u] - m0[u] == 1 ? INT64_MIN + (int64_t)a.sone[f[u]]
+                                                  : (int64_t)a.soff[f[u]] - (int64_t)m0[u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < FAN_STG; ++u) {
+            if (!act[u]) continue;
+            const uint32_t e = e0 + u * FAN_BLOCK;
+            base[e] = v[u];
+            own[m0[u] > start ? (uint32_t)(m0[u] - start) : 0u] = (uint16_t)(e + 1);
         }
     }
     __syncthreads();
@@ -1281,11 +1318,22 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
         own4[NQ * t + q] = make_uint4(o[0], o[1], o[2], o[3]);
     }
     __syncthreads();
-    for (uint32_t i = t; i < len; i += FAN_BLOCK) {
-        const uint32_t e = (uint32_t)own[i] - 1u;
-        const int64_t bs = base[e];
-        a.out[start + i] = bs < INT64_MIN + (1ll << 33) ? (uint32_t)(bs - INT64_MIN)
-                                                        : a.subs[(uint64_t)(bs + (int64_t)(start + i))];
+    // the copy: every delivery's subscriber load of this thread in flight at once
+    uint32_t r[FAN_FILL_PER];
+#pragma unroll
+    for (uint32_t u = 0; u < FAN_FILL_PER; ++u) {
+        const uint32_t i = t + u * FAN_BLOCK;
+        r[u] = 0;
+        if (i < len) {
+            const int64_t bs = base[(uint32_t)own[i] - 1u];
+            r[u] = bs < INT64_MIN + (1ll << 33) ? (uint32_t)(bs - INT64_MIN)
+                                                : a.subs[(uint64_t)(bs + (int64_t)(start + i))];
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < FAN_FILL_PER; ++u) {
+        const uint32_t i = t + u * FAN_BLOCK;
+        if (i < len) a.out[start + i] = r[u];
     }
 }
 
