@@ -1085,6 +1085,7 @@ constexpr uint32_t FAN_SCAN_TILE = FAN_BLOCK * FAN_PER;
 #define TM_FAN_FILL_PER 8
 #endif
 constexpr uint32_t FAN_FILL_PER = TM_FAN_FILL_PER;         // deliveries per fill thread (8 or 16)
+static_assert(FAN_FILL_PER % 8 == 0 && FAN_FILL_PER >= 8, "the fill's max-scan reads its marks as uint4 words (8 per thread)");
 constexpr uint32_t FAN_FILL_TILE = FAN_BLOCK * FAN_FILL_PER;
 constexpr uint32_t FAN_LDS_ENTRIES = FAN_FILL_TILE * 3 / 4;  // match entries a fill tile can stage
 
