@@ -1013,16 +1013,21 @@ __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
             const uint32_t hi = __shfl(off + c, last, 64);
             const uint64_t sb = (uint64_t)lo + d0;
             if ((uint64_t)hi > a.ids_cap || sb + (hi - lo) > a.sfids_cap) continue;   // rerun path
-            for (uint32_t i = lo + lane; i < hi; i += 256) {
-                const uint32_t i1 = i + 64, i2 = i + 128, i3 = i + 192;
-                const uint32_t v0 = a.sfids[CK_(sb + (i - lo), a.sfids_cap, 30)];
-                const uint32_t v1 = i1 < hi ? a.sfids[CK_(sb + (i1 - lo), a.sfids_cap, 31)] : 0u;
-                const uint32_t v2 = i2 < hi ? a.sfids[CK_(sb + (i2 - lo), a.sfids_cap, 32)] : 0u;
-                const uint32_t v3 = i3 < hi ? a.sfids[CK_(sb + (i3 - lo), a.sfids_cap, 33)] : 0u;
-                a.ids[CK_(i, a.ids_cap, 34)] = v0;
-                if (i1 < hi) a.ids[CK_(i1, a.ids_cap, 35)] = v1;
-                if (i2 < hi) a.ids[CK_(i2, a.ids_cap, 36)] = v2;
-                if (i3 < hi) a.ids[CK_(i3, a.ids_cap, 37)] = v3;
+            // FIN_U loads per lane in flight before the stores: a tile's run
+            // (~1,500 ids at C2) is one or two memory round trips
+            constexpr uint32_t FIN_U = 16;
+            for (uint32_t i = lo + lane; i < hi; i += 64 * FIN_U) {
+                uint32_t v[FIN_U];
+#pragma unroll
+                for (uint32_t u = 0; u < FIN_U; ++u) {
+                    const uint32_t iu = i + 64 * u;
+                    v[u] = iu < hi ? a.sfids[CK_(sb + (iu - lo), a.sfids_cap, 30)] : 0u;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < FIN_U; ++u) {
+                    const uint32_t iu = i + 64 * u;
+                    if (iu < hi) a.ids[CK_(iu, a.ids_cap, 34)] = v[u];
+                }
             }
         } else if (any && s + c <= a.sfids_cap && (uint64_t)off + c <= a.ids_cap) {
             for (uint32_t i = 0; i < c; ++i) a.ids[CK_((uint64_t)off + i, a.ids_cap, 38)] = a.sfids[CK_(s + i, a.sfids_cap, 39)];
