@@ -1134,30 +1134,59 @@ __device__ inline uint64_t fan_block_scan(uint64_t v, uint64_t* lds, uint64_t& t
 // block delivers 2^32 or more (a hot filter with millions of subscribers).
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
     __shared__ uint64_t lds[4];
-    const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + threadIdx.x;
+    // thread t owns FAN_PER consecutive entries: a serial prefix in registers
+    // and ONE block scan of the per-thread sums (striped chunks needed one
+    // block scan per chunk); ids and offsets move as 16-B vectors
+    const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + (uint64_t)threadIdx.x * FAN_PER;
+    uint32_t f[FAN_PER];
+    if (j0 + FAN_PER <= a.n_matches) {
+        const uint4* q = reinterpret_cast<const uint4*>(a.ids + j0);   // j0 % 16 == 0: 64-B aligned
+#pragma unroll
+        for (uint32_t k = 0; k < FAN_PER / 4; ++k) {
+            const uint4 v = q[k];
+            f[4 * k] = v.x; f[4 * k + 1] = v.y; f[4 * k + 2] = v.z; f[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < FAN_PER; ++k) f[k] = j0 + k < a.n_matches ? a.ids[j0 + k] : a.nnodes;
+    }
     uint64_t c[FAN_PER], mine = 0;
 #pragma unroll
     for (uint32_t k = 0; k < FAN_PER; ++k) {
-        c[k] = fan_count(a, j0 + (uint64_t)k * FAN_BLOCK);
+        c[k] = 0;
+        if (f[k] < a.nnodes) {
+            const uint32_t s1 = a.scnt[f[k]];   // 1 B per node: the gather's footprint stays L2-sized
+            c[k] = s1 < 255 ? s1 : a.soff[f[k] + 1] - a.soff[f[k]];
+        }
         mine += c[k];
     }
     uint64_t total;
-    (void)fan_block_scan(mine, lds, total);
+    uint64_t run = fan_block_scan(mine, lds, total);
     const bool big = total > a.big_limit;
-    uint64_t carry = 0;
+    if (!big && j0 + FAN_PER <= a.n_matches + 1) {
+        uint4* q = reinterpret_cast<uint4*>(a.moff32 + j0);
 #pragma unroll
-    for (uint32_t k = 0; k < FAN_PER; ++k) {
-        uint64_t tot;
-        const uint64_t e = fan_block_scan(c[k], lds, tot);
-        const uint64_t j = j0 + (uint64_t)k * FAN_BLOCK;
-        if (j <= a.n_matches) {
-            if (big) a.moff[j] = carry + e;
-            else a.moff32[j] = (uint32_t)(carry + e);
+        for (uint32_t k = 0; k < FAN_PER / 4; ++k) {
+            uint4 v;
+            v.x = (uint32_t)run; run += c[4 * k];
+            v.y = (uint32_t)run; run += c[4 * k + 1];
+            v.z = (uint32_t)run; run += c[4 * k + 2];
+            v.w = (uint32_t)run; run += c[4 * k + 3];
+            q[k] = v;
         }
-        carry += tot;
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < FAN_PER; ++k) {
+            const uint64_t j = j0 + k;
+            if (j <= a.n_matches) {
+                if (big) a.moff[j] = run;
+                else a.moff32[j] = (uint32_t)run;
+            }
+            run += c[k];
+        }
     }
     if (threadIdx.x == 0) {
-        a.bsums[blockIdx.x] = carry;
+        a.bsums[blockIdx.x] = total;
         a.bbig[blockIdx.x] = big ? 1 : 0;
     }
 }
