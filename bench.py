@@ -180,6 +180,24 @@ def pmc_traffic(workload, topics, filters=None):
     return pmc.get("hbm_bytes_per_launch")
 
 
+def timed_steps(bs, steps, ms_match=None, ms_total=None):
+    """steps launches cycling over the batches in bs: batch i + len(bs) - 1 is
+    launched before batch i is waited for (each on its own stream when
+    len(bs) > 1); ends on a wait, so the device is idle at both ends."""
+    nb = len(bs)
+    for i in range(min(nb - 1, steps)):
+        bs[i].launch()
+    for i in range(steps):
+        if i + nb - 1 < steps:
+            bs[(i + nb - 1) % nb].launch()
+        cur = bs[i % nb]
+        cur.wait()
+        if ms_match is not None:
+            s = cur.stats()
+            ms_match.append(s["ms_match"])
+            ms_total.append(s["ms_total"])
+
+
 def run_c4(args, ws, rank, local, pg):
     """Config C4: IoT filters partitioned over the WORLD_SIZE GPUs by their literal
     (w0, w1) prefix (root-wildcard filters replicated), each rank publishing its
@@ -623,6 +641,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--topics", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="C2: batches in flight in the headline steps, each on its own stream (1 = one "
+                         "batch on the engine stream: walk events and rocprof durations stay un-overlapped)")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--latency-batches", type=int, default=200)
     ap.add_argument("--e2e-topics", type=int, default=10_000_000,
@@ -691,28 +712,31 @@ def main():
     log(f"[rank {rank}] trie built+uploaded in {time.time() - t0:.1f}s: {est}")
 
     t0 = time.time()
-    b = eng.prepare(topics)
-    log(f"[rank {rank}] batch bytes resident in HBM in {time.time() - t0:.1f}s")
+    # args.inflight batches of the same publishes, each on a stream of its own
+    # (TM_BATCH_STREAM): batch i + 1 is launched before batch i is waited for,
+    # so one batch's CSR pass overlaps the next one's walk
+    nb = max(1, args.inflight)
+    bs = [eng.prepare(topics, stream=nb > 1) for _ in range(nb)]
+    b = bs[0]
+    log(f"[rank {rank}] {nb} batch(es) resident in HBM in {time.time() - t0:.1f}s")
 
     # the first launch tokenises the resident bytes on the device (tm_tok_*);
     # the timed steps reuse the tokens (the dictionary does not change), so a
     # step is the trie walk + CSR over a tokenised batch already in HBM
     for _ in range(max(args.warmup, 1)):
-        b.launch().wait()
+        for x in bs:
+            x.launch().wait()
     st = b.stats()
     if st["topics"] != len(topics):
         raise RuntimeError(f"batch stats inconsistent: {st}")
 
-    # wait() drains the engine's stream, the only stream this process uses
+    # every step's wait() drains that batch's stream; the loop ends on a wait,
+    # so the device is idle at both ends of the timed region
     if sync is not None:
         sync.barrier()
     ms_match, ms_total = [], []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.launch().wait()
-        s = b.stats()
-        ms_match.append(s["ms_match"])
-        ms_total.append(s["ms_total"])
+    timed_steps(bs, args.steps, ms_match, ms_total)
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if sync is not None:
@@ -755,7 +779,8 @@ def main():
         "data": "synthetic (seeded generator, SURVEY.md §8d C2)",
         "config": {"workload": "C2: 1M wildcard filters depth<=7, 10M-publish batch per GPU",
                    "filters": len(filters), "publishes_per_gpu": n, "mode": "replicated",
-                   "parallelism": f"replicated trie x{ws}, batches split per GPU"},
+                   "parallelism": f"replicated trie x{ws}, batches split per GPU",
+                   "batches_in_flight": nb},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "tm_match_tiles", "kernel_ms": k_ms,
@@ -770,6 +795,26 @@ def main():
         "matches_per_step": st["matches"],
         "slow_path_topics": st["slow_topics"],
     }
+
+    if nb == 1 and not args.profile:
+        # two batches in flight on streams of their own (TM_BATCH_STREAM): one
+        # batch's CSR pass and walk tail overlap the next one's walk.  Beside
+        # the headline, which keeps one batch so its walk events and rocprof
+        # durations are un-overlapped
+        b2 = [eng.prepare(topics, stream=True) for _ in range(2)]
+        for x in b2:
+            x.launch().wait()
+        if sync is not None:
+            sync.barrier()
+        t2 = time.perf_counter()
+        timed_steps(b2, args.steps)
+        e2 = time.perf_counter() - t2
+        if sync is not None:
+            sync.barrier()
+            e2 = sync.allmax(e2)
+        out["two_in_flight"] = {"publishes_per_s": ws * n * args.steps / e2, "ms_per_step": 1e3 * e2 / args.steps}
+        for x in b2:
+            x.free()
 
     if args.profile:
         args.no_cpu = True
@@ -806,7 +851,8 @@ def main():
         out["e2e"] = e2e_rate(eng, topics.slice(0, min(n, args.e2e_topics)))
         out["e2e_host_publishes_per_s"] = out["e2e"]["publishes_per_s"]
 
-    b.free()
+    for x in bs:
+        x.free()
 
     if rank == 0 and ws == 1 and not args.no_cpu:
         host = host_cpu_share()

@@ -27,6 +27,7 @@ TM_MAX_TOPIC_LEN = 4096
 TM_CFG_FROZEN_DICT = 1
 TM_CFG_HOST_TOKENIZE = 2
 TM_BATCH_DEDUP = 1
+TM_BATCH_STREAM = 2
 TM_ROUTE_DELETE = 0
 TM_ROUTE_WRITE = 1
 

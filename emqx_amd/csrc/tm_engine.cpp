@@ -323,6 +323,7 @@ struct tm_batch {
     size_t ch_rowoff = 0, ch_ids = 0;
     // the stream the batch runs on: async slots own one, other batches use the engine's
     hipStream_t own = nullptr;
+    bool own_user = false;   // TM_BATCH_STREAM: a caller's batch on a stream of its own (async slots: false)
     // generic-path scratch, per batch (batches on different streams run concurrently)
     uint32_t s_waves = 0, s_qcap = 1u << 13, s_ocap = 1u << 14;
     uint32_t *d_sqpar = nullptr, *d_sqpw = nullptr, *d_sqmeta = nullptr, *d_sofid = nullptr;
@@ -2125,6 +2126,14 @@ struct tm_engine {
 
     hipStream_t st(const tm_batch* b) const { return b->own ? b->own : stream; }
 
+    // a TM_BATCH_STREAM batch goes away: no longer a reader, stream destroyed
+    void drop_user_stream(tm_batch* b) {
+        readers.erase(std::remove(readers.begin(), readers.end(), b), readers.end());
+        if (b->own) (void)hipStreamDestroy(b->own);
+        b->own = nullptr;
+        b->own_user = false;
+    }
+
     // device tokenisation: the caller's bytes and offsets go to HBM now (the
     // caller's buffers are only borrowed for the call); words are produced at launch
     int upload_bytes(tm_batch* b, const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
@@ -2472,7 +2481,8 @@ struct tm_engine {
         }
         a_slots.clear();
         a_free.clear();
-        readers.clear();
+        readers.erase(std::remove_if(readers.begin(), readers.end(), [](tm_batch* r) { return !r->own_user; }),
+                      readers.end());
         a_started = false;
     }
 
@@ -3041,7 +3051,7 @@ int tm_async_stats_get(tm_engine* e, tm_async_stats* out) {
 
 int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
                         tm_batch** out) {
-    if (!e || !offsets || !out || (!topics && n) || (flags & ~TM_BATCH_DEDUP)) return TM_EINVAL;
+    if (!e || !offsets || !out || (!topics && n) || (flags & ~(TM_BATCH_DEDUP | TM_BATCH_STREAM))) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
     if (e->device >= 0) {
         int rc = e->set_device();
@@ -3050,18 +3060,38 @@ int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* off
     const bool fresh = *out == nullptr;   // non-NULL: re-prepared in place (buffers only grow)
     tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *out;
     if (!b) return TM_ENOMEM;
+    bool made_stream = false;
+    if ((flags & TM_BATCH_STREAM) && e->device >= 0 && !b->own) {
+        // a stream of its own: its launches overlap other batches' (a CSR
+        // pass with the next walk); trie uploads wait for it (readers)
+        if (hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) != hipSuccess) {
+            b->own = nullptr;
+            if (fresh) delete b;
+            return TM_EIO;
+        }
+        b->own_user = true;
+        e->readers.push_back(b);
+        made_stream = true;
+    }
     int rc;
     try {
-        rc = e->prepare(b, topics, offsets, n, flags);
+        rc = e->prepare(b, topics, offsets, n, flags & TM_BATCH_DEDUP);
     } catch (...) {
         rc = TM_ENOMEM;
     }
     if (rc) {
-        if (fresh) { b->release(); delete b; }
-        else { b->launched = b->done = false; }
+        if (b->own) (void)hipStreamSynchronize(b->own);
+        if (fresh) {
+            if (made_stream) e->drop_user_stream(b);
+            b->release();
+            delete b;
+        } else {
+            b->launched = b->done = false;
+        }
         return rc;
     }
     if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
+    if (b->own) HIP_OK(hipStreamSynchronize(b->own));   // the caller's buffers were only borrowed
     *out = b;
     return TM_OK;
 }
@@ -3134,6 +3164,10 @@ void tm_batch_free(tm_engine* e, tm_batch* b) {
             (void)hipStreamSynchronize(e->stream);
         }
         e->forget_launch(b);
+        if (b->own_user) {
+            (void)hipStreamSynchronize(b->own);
+            e->drop_user_stream(b);
+        }
         b->release();
     } else {
         b->release();

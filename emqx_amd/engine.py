@@ -40,7 +40,7 @@ class Tokens:
 class Batch:
     """A device-resident publish batch (tm_batch_prepare / launch / wait / result)."""
 
-    def __init__(self, eng: "Engine", topics=None, handle=None, n=0, dedup=False):
+    def __init__(self, eng: "Engine", topics=None, handle=None, n=0, dedup=False, stream=False):
         self.eng = eng
         if handle is not None:          # built by Engine.prepare_tokens
             self.h = handle
@@ -52,8 +52,9 @@ class Batch:
         self._buf = np.ascontiguousarray(buf)
         self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
         h = C.c_void_p()
+        flags = (N.TM_BATCH_DEDUP if dedup else 0) | (N.TM_BATCH_STREAM if stream else 0)
         N.check(eng.L.tm_batch_prepare_ex(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
-                                          N.TM_BATCH_DEDUP if dedup else 0, C.byref(h)), "tm_batch_prepare_ex")
+                                          flags, C.byref(h)), "tm_batch_prepare_ex")
         self.h = h
 
     def row_map(self):
@@ -391,9 +392,11 @@ class Engine:
                 "tm_match_batch")
         return _result_arrays(r)
 
-    def prepare(self, topics, dedup: bool = False) -> Batch:
-        """Device-resident batch; dedup=True matches identical topics once (TM_BATCH_DEDUP)."""
-        return Batch(self, topics, dedup=dedup)
+    def prepare(self, topics, dedup: bool = False, stream: bool = False) -> Batch:
+        """Device-resident batch; dedup=True matches identical topics once (TM_BATCH_DEDUP);
+        stream=True gives it a HIP stream of its own, so launches of several
+        batches overlap on the device (TM_BATCH_STREAM)."""
+        return Batch(self, topics, dedup=dedup, stream=stream)
 
     # ---- routes (emqx_router + emqx_broker:aggre/1) -------------------------
     def route_add(self, topic: bytes, dest: int):

@@ -207,6 +207,12 @@ TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t
  * one row per DISTINCT topic (tm_result.n_topics = distinct count) and
  * tm_batch_row_map gives the row of every publish. */
 #define TM_BATCH_DEDUP 1u
+/* TM_BATCH_STREAM: the batch runs on a HIP stream of its own, so launches of
+ * different batches overlap on the device (one batch's CSR pass with the
+ * next batch's walk); trie updates still reach a launch that follows them
+ * (read-your-writes) and wait for the batch's walk before changing the
+ * tables.  Every call on the batch stays synchronous for the caller. */
+#define TM_BATCH_STREAM 2u
 TM_API int  tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                 uint32_t flags, tm_batch** out);
 /* row_of[i] = result row of publish i (identity for batches without

@@ -288,3 +288,46 @@ def test_publish_batcher_emqx_batch_semantics():
     exp, _ = oracle_rows(F, T)
     for t, e in zip(T, exp):
         assert out[t] == e
+
+
+def test_stream_batches_overlap_and_read_your_writes():
+    """TM_BATCH_STREAM: two batches on streams of their own, launched back to
+    back (the second launched before the first is waited for), with trie
+    inserts and deletes between rounds: every row equals the oracle's on the
+    trie as it stood at that batch's launch."""
+    p = replace(gen.C1, n_filters=4000)
+    F = gen.gen_filters(p).tolist()
+    T = gen.gen_topics(p, gen.Strings.from_list(F), 21, 20000).tolist()
+    eng = Engine(device=0)
+    live = set(F[:3000])
+    eng.insert_many(sorted(live))
+    a, b = eng.prepare(T[:10000], stream=True), eng.prepare(T[10000:], stream=True)
+    rng = random.Random(4)
+    for rnd in range(4):
+        snap = sorted(live)
+        a.launch()
+        b.launch()
+        a.wait()
+        b.wait()
+        orc = P.Oracle()
+        for f in snap:
+            orc.register(f)
+            orc.insert(f)
+        for batch, part in ((a, T[:10000]), (b, T[10000:])):
+            offs, ids = batch.result()
+            buf, o = P.pack(part)
+            counts, idx, _ = orc.match_batch(buf, o)
+            cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+            for t in range(0, len(part), 7):
+                exp = [snap[int(j)] for j in idx[cut[t]:cut[t + 1]]]
+                got = [eng.filter_bytes(int(x)) for x in ids[offs[t]:offs[t + 1]]]
+                assert got == exp, (rnd, part[t])
+        # churn between rounds: reaches the next launches (read-your-writes)
+        add = rng.sample([f for f in F if f not in live], 200)
+        rem = rng.sample(sorted(live), 200)
+        eng.insert_many(add)
+        eng.delete_many(rem)
+        live |= set(add)
+        live -= set(rem)
+    a.free()
+    b.free()
