@@ -176,13 +176,14 @@ class ShardedMatcher:
         dist.all_to_all_single(out, x.contiguous(), recv, send, group=self.group)
         return out
 
-    def _gather(self, src: torch.Tensor, src_off: torch.Tensor, idx: torch.Tensor, lens: torch.Tensor):
-        """Rows src[src_off[idx[i]] .. src_off[idx[i]+1]) concatenated -> (dst, dst_off int64 [n+1])."""
+    def _gather(self, src: torch.Tensor, src_off: torch.Tensor, idx: torch.Tensor, lens: torch.Tensor,
+                total: int):
+        """Rows src[src_off[idx[i]] .. src_off[idx[i]+1]) concatenated -> (dst, dst_off int64 [n+1]);
+        total = sum(lens), known on the host from the exchanged sizes (no sync here)."""
         n = idx.numel()
         dst_off = torch.zeros(n + 1, dtype=torch.int64, device=src.device)
         if n:
             dst_off[1:] = torch.cumsum(lens, 0)
-        total = int(dst_off[-1].item())
         if self._local_match is not None or src.device.type != "cuda":   # CPU tests
             return gather_segments(src, src_off[idx], lens), dst_off
         dst = torch.empty(total, dtype=src.dtype, device=src.device)
@@ -208,22 +209,27 @@ class ShardedMatcher:
             return row_off, gids
         shard = self._shards(words, toff, n).to(torch.int64)
         owner = torch.where(shard == G, torch.full_like(shard, self.rank), shard)
-        # counting sort by owner (G is small): publishes grouped per destination
-        order = torch.cat([torch.nonzero(owner == g).flatten() for g in range(G)])
+        # publishes grouped per destination: a stable sort by owner keeps the
+        # publish order within each group (no per-owner host round trip)
+        order = torch.argsort(owner, stable=True)
         toff64 = toff.to(torch.int64)
         depth = toff64[1:] - toff64[:-1]
         depth_o = depth[order]
         send_t = torch.bincount(owner, minlength=G)
         send_w = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, owner, depth)
         meta_o = ((depth_o << META_SHIFT) | tflags[order].to(torch.int64)).to(torch.int32)
-        words_o, _ = self._gather(words, toff64, order, depth_o)
 
+        # the split sizes must be host values for all_to_all: one copy out for
+        # ours, one back for the peers'
         sizes = torch.stack([send_t, send_w], 1)
-        hs = sizes.cpu() if self._stage else sizes
+        hsz = sizes.cpu()
+        st, sw = hsz[:, 0].tolist(), hsz[:, 1].tolist()
+        words_o, _ = self._gather(words, toff64, order, depth_o, sum(sw))
+        hs = hsz if self._stage else sizes
         rsizes = torch.empty_like(hs)
         dist.all_to_all_single(rsizes, hs, group=self.group)
-        st, sw = send_t.tolist(), send_w.tolist()
-        rt, rw = rsizes[:, 0].tolist(), rsizes[:, 1].tolist()
+        hr = rsizes.cpu()
+        rt, rw = hr[:, 0].tolist(), hr[:, 1].tolist()
         r_meta = self._a2a(meta_o, st, rt)
         r_words = self._a2a(words_o, sw, rw)
 
@@ -240,7 +246,8 @@ class ShardedMatcher:
         counts_o = self._a2a(counts, rt, st)
         c_o = counts_o.to(torch.int64)
         recv_g = torch.zeros(G, dtype=torch.int64, device=dev).scatter_add_(0, owner[order], c_o)
-        gids_o = self._a2a(gids, back_g.tolist(), recv_g.tolist())
+        bg, rg = torch.stack([back_g, recv_g]).cpu().tolist()   # one copy out for both splits
+        gids_o = self._a2a(gids, bg, rg)
 
         # publish order
         counts_orig = torch.empty(n, dtype=torch.int64, device=dev)
@@ -250,7 +257,7 @@ class ShardedMatcher:
         off_o = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         if n:
             off_o[1:] = torch.cumsum(c_o, 0)
-        gids_final, row_off = self._gather(gids_o, off_o, inv, counts_orig)
+        gids_final, row_off = self._gather(gids_o, off_o, inv, counts_orig, sum(rg))
         self.last.update(sent_topics=st, recv_topics=rt, local_matches=int(gids.numel()))
         return row_off, gids_final
 
