@@ -1285,7 +1285,10 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     __syncthreads();
     // staging, FAN_STG entries per thread with every load of a step in flight
     // (the offsets and filter ids, then the dependent sone / soff gathers)
-    constexpr uint32_t FAN_STG = 4;
+#ifndef TM_FAN_STG
+#define TM_FAN_STG 8
+#endif
+    constexpr uint32_t FAN_STG = TM_FAN_STG;
     for (uint32_t e0 = t; e0 < (uint32_t)ne; e0 += FAN_BLOCK * FAN_STG) {
         uint64_t m0[FAN_STG], m1[FAN_STG];
         uint32_t f[FAN_STG];
