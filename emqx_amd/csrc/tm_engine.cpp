@@ -487,7 +487,7 @@ struct tm_engine {
     // a batch launches when a slot is free and either nothing is in flight or
     // at least a_busy_min calls queued: under load, calls accumulate while the
     // device works instead of trickling out as tiny batches
-    uint32_t a_max = 16384, a_linger_us = 0, a_depth = 3, a_busy_min = 128, a_ncompleters = 2;
+    uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // tools/ab_async.sh
     uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0;
     // where the pipeline's time goes (host microseconds, summed over batches)
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;

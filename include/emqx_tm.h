@@ -173,7 +173,7 @@ typedef struct {
     uint64_t requests;      /* calls completed */
     uint64_t recoveries;    /* batches re-run through the CSR path (capacity misses) */
     uint64_t max_batch;     /* largest batch formed */
-    uint32_t depth;         /* batches in flight at most (TM_ASYNC_DEPTH, default 3) */
+    uint32_t depth;         /* batches in flight at most (TM_ASYNC_DEPTH, default 4) */
     uint32_t queued;        /* calls waiting for a batch now */
     double   us_launch;     /* host time forming + enqueueing batches (launcher thread) */
     double   us_wait;       /* completer time blocked on device batches */
