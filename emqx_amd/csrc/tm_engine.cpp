@@ -12,6 +12,7 @@
 // node record's edge_count is kept so that emqx_trie:lookup/1 answers match
 // the reference's tests (test/emqx_trie_SUITE.erl:49-142).
 #include <linux/futex.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -273,6 +274,41 @@ int host_reserve_coherent(uint8_t*& p, size_t& cap, size_t bytes) {
     return TM_OK;
 }
 
+// Allocator of the host mirror's big random-access tables (edge hash, node
+// records): blocks of 4 MB and more are mapped 2-MB aligned with
+// MADV_HUGEPAGE before first touch, so a churn delta's random lines do not
+// each cost a page walk (THP is "madvise" on these hosts).
+template <class T>
+struct HugeAlloc {
+    using value_type = T;
+    static constexpr size_t HUGE = 2u << 20, MIN_BYTES = 4u << 20;
+    HugeAlloc() = default;
+    template <class U>
+    HugeAlloc(const HugeAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < MIN_BYTES) return std::allocator<T>().allocate(n);
+        const size_t span = (bytes + HUGE - 1) / HUGE * HUGE;
+        const size_t len = span + HUGE;   // room to align
+        void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        const uintptr_t p0 = (uintptr_t)p, a = (p0 + HUGE - 1) & ~(uintptr_t)(HUGE - 1);
+        if (a > p0) munmap(p, a - p0);                                  // head before the aligned start
+        if (p0 + len > a + span) munmap((void*)(a + span), p0 + len - (a + span));   // and the tail
+        (void)madvise((void*)a, span, MADV_HUGEPAGE);
+        return reinterpret_cast<T*>(a);
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < MIN_BYTES) { std::allocator<T>().deallocate(p, n); return; }
+        munmap(p, (bytes + HUGE - 1) / HUGE * HUGE);   // exactly the mapping allocate() kept
+    }
+    template <class U>
+    bool operator==(const HugeAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+
 unsigned default_threads() {
     unsigned h = std::thread::hardware_concurrency();
     return std::max(1u, std::min(h ? h : 1u, 16u));
@@ -513,7 +549,7 @@ struct tm_engine {
         uint32_t pad2 = 0;
     };
     static_assert(sizeof(NodeRec) == 32, "two node records per cache line");
-    std::vector<NodeRec> nd;
+    std::vector<NodeRec, HugeAlloc<NodeRec>> nd;
     std::vector<uint32_t> n_flen;
     std::vector<uint64_t> n_foff;
     std::vector<uint32_t> free_nodes;
@@ -530,7 +566,7 @@ struct tm_engine {
     std::vector<uint8_t> fbytes;
 
     // edge hash (host mirror of the HBM replica)
-    std::vector<Slot> slots;
+    std::vector<Slot, HugeAlloc<Slot>> slots;
     uint64_t used_slots = 0;   // live + tombstones
     uint32_t max_disp = 0;
 
@@ -634,7 +670,8 @@ struct tm_engine {
 
     // first free slot (empty or tombstone) along the probe sequence; slots of a
     // bucket are taken in order, so "last slot empty" <=> "bucket has a hole"
-    uint32_t place_slot(std::vector<Slot>& tab, uint32_t p, uint32_t w, uint32_t& disp, bool& was_empty) const {
+    uint32_t place_slot(std::vector<Slot, HugeAlloc<Slot>>& tab, uint32_t p, uint32_t w, uint32_t& disp,
+                        bool& was_empty) const {
         const uint32_t nb = (uint32_t)(tab.size() / BUCKET);
         uint32_t b = home_bucket(p, w, nb);
         for (uint32_t i = 0;; ++i) {
@@ -654,7 +691,7 @@ struct tm_engine {
     void rehash(size_t want_slots) {
         size_t nb = std::max<size_t>((want_slots + BUCKET - 1) / BUCKET, 256);
         const size_t ns = nb * BUCKET;
-        std::vector<Slot> tab(ns);
+        std::vector<Slot, HugeAlloc<Slot>> tab(ns);
         for (Slot& s : tab) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
         uint32_t md = 0;
         uint64_t used = 0;
