@@ -316,6 +316,10 @@ unsigned default_threads() {
 
 }  // namespace
 
+#ifndef TM_SLOW_WAVES_MAX
+#define TM_SLOW_WAVES_MAX 4096   // C5 K=1000 device: 512 waves 7.75 ms, 2048 4.54, 4096 4.03 (tools/ab_slow.sh)
+#endif
+
 // ===================================================================== batch
 
 struct tm_batch {
@@ -1781,7 +1785,14 @@ struct tm_engine {
     // deduplicated skewed batch can send tens of thousands of long rows here
     int ensure_slow_scratch(tm_batch* b) {
         int rc;
-        if (!b->s_waves) b->s_waves = std::min<uint32_t>(512, std::max<uint32_t>(64, b->n / 256));
+        if (!b->s_waves) {
+            // one wave per generic-path topic at a time, latency-bound: a
+            // skewed batch (C5: ~28k rows of ~1,000 matches) needs several
+            // waves per CU; idle waves exit at once (scratch ~350 KB each)
+            uint32_t w = b->n < 65536 ? 64u : std::min<uint32_t>(TM_SLOW_WAVES_MAX, b->n / 32);
+            if (const char* v = getenv("TM_SLOW_WAVES")) w = std::max(1, atoi(v));
+            b->s_waves = w;
+        }
         const size_t q = (size_t)b->s_waves * b->s_qcap, o = (size_t)b->s_waves * b->s_ocap;
         if ((rc = dev_reserve(b->d_sqpar, b->c_sq, q))) return rc;
         if ((rc = dev_reserve(b->d_sqpw, b->c_sq2, q))) return rc;
