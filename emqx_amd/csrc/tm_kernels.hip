@@ -1192,17 +1192,22 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
 }
 
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_t nb) {
+    // each thread owns a contiguous chunk of the block sums: a serial sum, ONE
+    // block scan of the chunk sums, then a serial exclusive pass (one block
+    // scan per 256 sums made this a long chain of barriers at 60k blocks)
     __shared__ uint64_t lds[4];
-    uint64_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += FAN_BLOCK) {
-        const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < nb ? a.bsums[i] : 0;
-        uint64_t tot;
-        const uint64_t e = fan_block_scan(v, lds, tot);
-        if (i < nb) a.bsums[i] = carry + e;
-        carry += tot;
+    const uint32_t per = (nb + FAN_BLOCK - 1) / FAN_BLOCK;
+    const uint32_t lo = min(nb, threadIdx.x * per), hi = min(nb, lo + per);
+    uint64_t mine = 0;
+    for (uint32_t i = lo; i < hi; ++i) mine += a.bsums[i];
+    uint64_t total;
+    uint64_t run = fan_block_scan(mine, lds, total);
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint64_t v = a.bsums[i];
+        a.bsums[i] = run;
+        run += v;
     }
-    if (threadIdx.x == 0) *a.d_total = carry;
+    if (threadIdx.x == 0) *a.d_total = total;
 }
 
 // After scan_local + scan_sums, moff32[j] (or moff[j] in a big block) is
