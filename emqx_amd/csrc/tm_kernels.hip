@@ -1097,8 +1097,14 @@ constexpr uint32_t FAN_LDS_ENTRIES = FAN_FILL_TILE * 3 / 4;  // match entries a 
 // first delivery of match entry j: the block's offset plus the block-relative
 // u32 (u64 only in scan blocks with 2^32 deliveries or more)
 __device__ inline uint64_t fan_moff(const FanArgs& a, uint64_t j) {
+    // the u32 offset, the block flag and the block sum are loaded together
+    // (moff32 spans every entry, so the speculative read is in bounds); only a
+    // block past 2^32 deliveries reads the u64 offset after the flag
     const uint64_t b = j / FAN_SCAN_TILE;
-    return (a.bbig[b] ? a.moff[j] : (uint64_t)a.moff32[j]) + a.bsums[b];
+    const uint32_t m32 = a.moff32[j];
+    const bool big = a.bbig[b] != 0;
+    const uint64_t bs = a.bsums[b];
+    return (big ? a.moff[j] : (uint64_t)m32) + bs;
 }
 
 __device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
