@@ -1204,14 +1204,29 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_sums(FanArgs a, uint32_
     __shared__ uint64_t lds[4];
     const uint32_t per = (nb + FAN_BLOCK - 1) / FAN_BLOCK;
     const uint32_t lo = min(nb, threadIdx.x * per), hi = min(nb, lo + per);
+    // 8 loads of a chunk in flight at a time (a dependent chain of 230 loads
+    // per thread was the cost); the chunk is kept in registers for pass 2 when
+    // it fits
+    constexpr uint32_t U = 8;
     uint64_t mine = 0;
-    for (uint32_t i = lo; i < hi; ++i) mine += a.bsums[i];
+    for (uint32_t i0 = lo; i0 < hi; i0 += U) {
+        uint64_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = i0 + u < hi ? a.bsums[i0 + u] : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) mine += v[u];
+    }
     uint64_t total;
     uint64_t run = fan_block_scan(mine, lds, total);
-    for (uint32_t i = lo; i < hi; ++i) {
-        const uint64_t v = a.bsums[i];
-        a.bsums[i] = run;
-        run += v;
+    for (uint32_t i0 = lo; i0 < hi; i0 += U) {
+        uint64_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = i0 + u < hi ? a.bsums[i0 + u] : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (i0 + u < hi) a.bsums[i0 + u] = run;
+            run += v[u];
+        }
     }
     if (threadIdx.x == 0) *a.d_total = total;
 }
