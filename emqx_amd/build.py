@@ -5,6 +5,7 @@
 
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -20,11 +21,28 @@ TM_SOURCES = ["tm_engine.cpp", "tm_group.cpp", "tm_kernels.hip"]
 TM_HEADERS = ["tm_internal.hpp", os.path.join("..", "..", "include", "emqx_tm.h")]
 
 
-def _stale(out, deps):
-    if not os.path.exists(out):
+def _digest(deps, extra=""):
+    h = hashlib.sha256(extra.encode())
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def _stale(out, deps, extra=""):
+    """A built library is reused only if its stamp names the digest of exactly
+    these sources (and flags): a snapshot copied to another machine keeps no
+    trustworthy mtimes, and a stale .so must never pass for the current code."""
+    stamp = out + ".srchash"
+    if not os.path.exists(out) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(deps, extra)
+
+
+def _stamp(out, deps, extra=""):
+    with open(out + ".srchash", "w") as f:
+        f.write(_digest(deps, extra) + "\n")
 
 
 def _run(cmd):
@@ -35,13 +53,21 @@ def _run(cmd):
 def build_tm(force=False):
     out = os.path.join(HERE, "libemqx_tm.so")
     deps = [os.path.join(CSRC, f) for f in TM_SOURCES + TM_HEADERS]
-    if force or _stale(out, deps):
+    if force or _stale(out, deps, ARCH):
         tmp = out + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-fvisibility=hidden", "-Wall", "-Wl,-soname,libemqx_tm.so", "-o", tmp]
+              "-fvisibility=hidden", "-Wall", "-Wl,-soname,libemqx_tm.so",
+              f'-DTM_SRC_HASH="{_digest(deps, ARCH)}"', "-o", tmp]
              + [os.path.join(CSRC, f) for f in TM_SOURCES] + ["-lpthread"])
         os.replace(tmp, out)
+        _stamp(out, deps, ARCH)
     return out
+
+
+def source_hash():
+    """Digest of the engine's sources: tm_build_info() of a library built from
+    them ends with it (tests check the loaded .so is the current code)."""
+    return _digest([os.path.join(CSRC, f) for f in TM_SOURCES + TM_HEADERS], ARCH)
 
 
 def build_gen(force=False):
@@ -49,6 +75,7 @@ def build_gen(force=False):
     src = os.path.join(CSRC, "tm_gen.c")
     if force or _stale(out, [src]):
         _run(["gcc", "-O2", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall", "-o", out, src, "-lm"])
+        _stamp(out, [src])
     return out
 
 
@@ -60,6 +87,7 @@ def build_load(force=False):
     if force or _stale(out, deps):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall", "-o", out, src,
               "-L" + HERE, "-lemqx_tm", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+        _stamp(out, deps)
     return out
 
 
@@ -75,6 +103,7 @@ def build_nif_mock(force=False):
         _run(["gcc", "-O1", "-g", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror",
               "-I" + mock, "-I" + os.path.join(ROOT, "include"), "-o", out] + srcs +
              ["-L" + HERE, "-lemqx_tm", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+        _stamp(out, deps)
     return out
 
 

@@ -3666,8 +3666,12 @@ int tm_device_count(void) {
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+#ifndef TM_SRC_HASH
+#define TM_SRC_HASH "unstamped"
+#endif
+// ends with the digest of the sources it was built from (emqx_amd/build.py source_hash)
 const char* tm_build_info(void) {
-    return "emqx_tm gfx950 frontier-tile kernel; slots=32B buckets=64B; path-code sort; " __DATE__;
+    return "emqx_tm gfx950 frontier-tile kernel; 16-B slots, 64-B buckets; path-code sort; src " TM_SRC_HASH;
 }
 
 }  // extern "C"

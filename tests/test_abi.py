@@ -33,6 +33,9 @@ def test_library_exports_every_declared_symbol():
 
 def test_build_info_and_no_device_match_fails_loudly():
     assert b"gfx950" in N.lib().tm_build_info()
+    # the loaded library was built from the sources in this tree (not a stale .so)
+    from emqx_amd import build as B
+    assert N.lib().tm_build_info().decode().endswith("src " + B.source_hash())
     e = Engine(device=-1)
     e.insert(b"a/+")
     with pytest.raises(N.TmError) as ei:
