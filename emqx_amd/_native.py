@@ -107,6 +107,9 @@ SZ = C.c_size_t
 U8P = C.c_char_p
 SIGNATURES = {
     "tm_create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+    "tm_create_replicated": (C.c_int, [C.POINTER(Config), P, C.c_uint32, C.POINTER(P)]),
+    "tm_replica_count": (C.c_uint32, [P]),
+    "tm_async_start": (C.c_int, [P]),
     "tm_destroy": (None, [P]),
     "tm_version": (C.c_uint64, [P]),
     "tm_stats": (C.c_int, [P, C.POINTER(EngineStats)]),
@@ -123,6 +126,8 @@ SIGNATURES = {
     "tm_async_stats_get": (C.c_int, [P, C.POINTER(AsyncStats)]),
     "tm_batch_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
     "tm_batch_prepare_ex": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "tm_batch_prepare_on": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "tm_batch_replica": (C.c_uint32, [P, P]),
     "tm_batch_row_map": (C.c_int, [P, P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint32)]),
     "tm_batch_launch": (C.c_int, [P, P]),
     "tm_batch_wait": (C.c_int, [P, P]),
@@ -174,6 +179,11 @@ SIGNATURES = {
     "tm_group_batch_stats": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_group_batch_free": (None, [P, P]),
     "tm_group_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_group_dispatch": (C.c_int, [P, P, C.POINTER(Deliveries)]),
+    "tm_group_match_async": (C.c_int, [P, U8P, SZ, MATCH_CB, P]),
+    "tm_group_match_coalesced": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "tm_group_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
+    "tm_group_rules_match": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P]),
     "tm_debug_check": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),

@@ -44,8 +44,34 @@ static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_UNDEFINED, 
 /* set while a match callback runs on the engine's completion thread */
 static __thread int in_engine_callback;
 
-static void* destroy_engine(void* e) {
-    tm_destroy((tm_engine*)e);
+/* Engines whose last reference went away inside a match callback cannot be
+ * destroyed there (tm_destroy joins the completion thread that runs the
+ * callback): they go to the library's reaper thread, started by load/3 and
+ * joined by unload/2, so no engine outlives the module and none leaks. */
+typedef struct reap_node {
+    tm_engine* e;
+    struct reap_node* next;
+} reap_node;
+static pthread_mutex_t reap_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t reap_cv = PTHREAD_COND_INITIALIZER;
+static reap_node* reap_head;
+static int reap_stop, reap_running;
+static pthread_t reap_thread;
+
+static void* reaper(void* arg) {
+    (void)arg;
+    pthread_mutex_lock(&reap_mu);
+    for (;;) {
+        while (!reap_head && !reap_stop) pthread_cond_wait(&reap_cv, &reap_mu);
+        if (!reap_head) break;   /* stopping and drained */
+        reap_node* n = reap_head;
+        reap_head = n->next;
+        pthread_mutex_unlock(&reap_mu);
+        tm_destroy(n->e);
+        enif_free(n);
+        pthread_mutex_lock(&reap_mu);
+    }
+    pthread_mutex_unlock(&reap_mu);
     return NULL;
 }
 
@@ -53,10 +79,16 @@ static void engine_dtor(ErlNifEnv* env, void* obj) {
     (void)env;
     engine_res* r = (engine_res*)obj;
     if (r->e && in_engine_callback) {
-        /* the last reference went away in a match callback: tm_destroy joins
-         * the completion thread, so it runs on a thread of its own */
-        pthread_t t;
-        if (pthread_create(&t, NULL, destroy_engine, r->e) == 0) pthread_detach(t);
+        reap_node* n = enif_alloc(sizeof(reap_node));
+        if (n) {
+            n->e = r->e;
+            pthread_mutex_lock(&reap_mu);
+            n->next = reap_head;
+            reap_head = n;
+            pthread_cond_signal(&reap_cv);
+            pthread_mutex_unlock(&reap_mu);
+        }
+        /* (allocation failure: the engine leaks rather than deadlocking here) */
     } else if (r->e) {
         tm_destroy(r->e);
     }
@@ -86,15 +118,38 @@ static ERL_NIF_TERM make_bin(ErlNifEnv* env, const uint8_t* p, size_t n) {
     return t;
 }
 
-/* new(Device) -> {ok, Engine} | {error, Reason} */
+/* new(Device | [Device]) -> {ok, Engine} | {error, Reason}
+ * A list makes one engine over those GPUs (tm_create_replicated): one host
+ * trie, an HBM replica per device, per-publish matches dealt over them and
+ * batch calls spread over them -- a broker node uses every GPU through the
+ * same Engine term.  The async pipeline starts here (a dirty scheduler), so
+ * match_async/3 on a normal scheduler never pays its setup. */
+#define MAX_DEVICES 64
 static ERL_NIF_TERM nif_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+    int32_t devs[MAX_DEVICES];
+    unsigned ndev = 0;
     int dev;
     (void)argc;
-    if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
-    tm_config cfg = {dev, 0, 0, 0};
+    if (enif_get_int(env, argv[0], &dev)) {
+        devs[0] = dev;
+        ndev = dev >= 0 ? 1 : 0;   /* -1: host-only engine (trie ops, no match) */
+    } else {
+        ERL_NIF_TERM head, tail = argv[0];
+        if (!enif_get_list_length(env, tail, &ndev) || ndev == 0 || ndev > MAX_DEVICES) return enif_make_badarg(env);
+        for (unsigned i = 0; i < ndev; i++)
+            if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_int(env, head, &dev))
+                return enif_make_badarg(env);
+            else
+                devs[i] = dev;
+    }
+    tm_config cfg = {devs[0], 0, 0, 0};
     tm_engine* e = NULL;
-    int rc = tm_create(&cfg, &e);
+    int rc = tm_create_replicated(&cfg, devs, ndev, &e);
     if (rc) return err(env, rc);
+    if (tm_replica_count(e) && (rc = tm_async_start(e))) {   /* (device -1: host-only engine, no pipeline) */
+        tm_destroy(e);
+        return err(env, rc);
+    }
     engine_res* r = enif_alloc_resource(ENGINE_RT, sizeof(engine_res));
     r->e = e;
     ERL_NIF_TERM t = enif_make_resource(env, r);
@@ -539,6 +594,9 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
     (void)priv; (void)info;
     ENGINE_RT = enif_open_resource_type(env, NULL, "tm_engine", engine_dtor, ERL_NIF_RT_CREATE, NULL);
     if (!ENGINE_RT) return -1;
+    reap_stop = 0;
+    if (pthread_create(&reap_thread, NULL, reaper, NULL) != 0) return -1;
+    reap_running = 1;
     ATOM_OK = enif_make_atom(env, "ok");
     ATOM_ERROR = enif_make_atom(env, "error");
     ATOM_TRUE = enif_make_atom(env, "true");
@@ -579,4 +637,16 @@ static ErlNifFunc funcs[] = {
     {"topic_match", 2, nif_topic_match, 0},
 };
 
-ERL_NIF_INIT(emqx_tm, funcs, load, NULL, NULL, NULL)
+/* the reaper destroys what is queued, then exits */
+static void unload(ErlNifEnv* env, void* priv) {
+    (void)env; (void)priv;
+    if (!reap_running) return;
+    pthread_mutex_lock(&reap_mu);
+    reap_stop = 1;
+    pthread_cond_signal(&reap_cv);
+    pthread_mutex_unlock(&reap_mu);
+    pthread_join(reap_thread, NULL);
+    reap_running = 0;
+}
+
+ERL_NIF_INIT(emqx_tm, funcs, load, NULL, NULL, unload)

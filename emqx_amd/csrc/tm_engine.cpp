@@ -361,8 +361,12 @@ struct tm_batch {
     uint32_t* h_rowoff = nullptr;
     uint32_t* h_ids = nullptr;
     size_t ch_rowoff = 0, ch_ids = 0;
-    // the stream the batch runs on: async slots own one, other batches use the engine's
+    // the replica (device copy of the trie) the batch runs on; fixed for the
+    // batch's life: its buffers live on that replica's device
+    struct Replica* rep = nullptr;
+    // the stream the batch runs on: async slots own one, other batches use the replica's
     hipStream_t own = nullptr;
+    hipEvent_t ev_read = nullptr;   // own-stream batches: marks their walk for the replica's next upload
     bool own_user = false;   // TM_BATCH_STREAM: a caller's batch on a stream of its own (async slots: false)
     // generic-path scratch, per batch (batches on different streams run concurrently)
     uint32_t s_waves = 0, s_qcap = 1u << 13, s_ocap = 1u << 14;
@@ -464,7 +468,8 @@ struct tm_batch {
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev2) (void)hipEventDestroy(ev2);
         if (evt) (void)hipEventDestroy(evt);
-        ev0 = ev1 = ev2 = evt = nullptr;
+        if (ev_read) (void)hipEventDestroy(ev_read);
+        ev0 = ev1 = ev2 = evt = ev_read = nullptr;
     }
 };
 
@@ -496,12 +501,78 @@ struct AsyncSlot {
     bool claimed = false;                // a completer is delivering it
 };
 
-struct tm_engine {
-    std::recursive_mutex mu;
+// One device copy of the trie (a replica): the HBM tables, the stream the
+// engine's own work runs on, the batches that read the tables from streams of
+// their own, and the async per-publish pipeline that feeds this device.  An
+// engine owns one replica per device it was created on (tm_create: one;
+// tm_create_replicated: one per listed device, a device may repeat); they all
+// mirror the engine's ONE host trie, so a mutation is made once on the host
+// and its delta uploaded to every replica (sync_device), and node / filter
+// ids are the same on every device by construction.
+struct Replica {
+    uint32_t index = 0;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_delta = nullptr;       // end of the last async delta upload (staging reusable after it)
+    hipEvent_t ev_sync = nullptr;        // end of the delta uploads, waited for by own-stream batches
+    bool delta_inflight = false;
+    uint64_t upload_seq = 0;             // async trie uploads recorded on ev_sync
+    // batches on streams of their own (async slots, TM_BATCH_STREAM) read the
+    // tables concurrently with the replica stream: uploads wait for their walks
+    std::vector<tm_batch*> readers;
+    tm_batch scratch;   // tm_match_batch / tm_trie_match / tm_match_routes_batch slices
+    tm_batch tokb;      // staging of tm_tokenize_device
+
+    // trie tables
+    Slot* d_slots = nullptr;
+    size_t d_nslots = 0;
+    uint64_t* d_foff = nullptr;
+    uint32_t* d_flen = nullptr;
+    size_t c_foff = 0, c_flen = 0;
+    uint8_t* d_fbytes = nullptr;
+    size_t c_fbytes = 0;
+    uint64_t fbytes_uploaded = 0;
+    uint32_t* d_didx = nullptr;
+    Slot* d_dval = nullptr;
+    size_t cd_didx = 0, cd_dval = 0;
+    uint32_t* d_fidx = nullptr;
+    uint64_t* d_foffv = nullptr;
+    uint32_t* d_flenv = nullptr;
+    size_t cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
+    // word dictionary mirror (device tokeniser): cuckoo key table, tails, arena
+    DictKey* d_dkey = nullptr;
+    size_t d_dict_n = 0;            // cuckoo slots on the device
+    uint64_t d_dict_gen = ~0ull;    // dict.gen() of the device table
+    DictTail* d_tail = nullptr;
+    size_t c_tail = 0, tails_uploaded = 0;
+    uint8_t* d_arena = nullptr;
+    size_t c_arena = 0, arena_uploaded = 0;
+    uint32_t* d_dxidx = nullptr;
+    DictKey* d_dxval = nullptr;
+    size_t cd_dxidx = 0, cd_dxval = 0;
+    // bounds-checked variant's report
+    uint32_t* d_dbg = nullptr;
+    uint32_t* h_dbg = nullptr;
+    size_t c_dbg = 0, ch_dbg = 0;
+    // routes: dests CSR by node id (engine routes_gen when uploaded)
+    uint32_t *d_roff = nullptr, *d_rdest = nullptr;
+    size_t c_roff = 0, c_rdest = 0;
+    uint64_t routes_gen = ~0ull;
+    // subscribers: soff / subs / scnt / sone by node id (engine subs_gen when uploaded)
+    uint64_t* d_soff = nullptr;
+    uint32_t* d_subs = nullptr;
+    uint8_t* d_scnt = nullptr;
+    uint32_t* d_sone = nullptr;
+    size_t c_soff = 0, c_subs = 0, c_scnt = 0, c_sone = 0;
+    uint64_t subs_gen = ~0ull;
+    // tm_rules_match
+    uint32_t* d_rl = nullptr;
+    size_t c_rl = 0;
+
     // async pipeline (tm_match_async / tm_match_coalesced): calls queue on amu;
     // the launcher thread turns the queue into a device batch on a free slot
-    // (under mu, like every other engine operation), the completer thread
-    // waits for slots in launch order and delivers the rows
+    // (under the engine mutex, like every other engine operation), the
+    // completer threads wait for slots in launch order and deliver the rows
     std::mutex amu;
     std::condition_variable a_work, a_done;
     // submissions go to one of QSHARDS queues picked by the calling thread, so
@@ -531,13 +602,17 @@ struct tm_engine {
     uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0;
     // where the pipeline's time goes (host microseconds, summed over batches)
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
+};
+
+struct tm_engine {
+    std::recursive_mutex mu;
+    std::vector<Replica*> reps;   // empty: host-only engine (trie ops, no match)
     bool upload_nosync = false;   // set by tm_match_batch (prepare -> launch -> wait in one call)
-    int device = -1;
+    int device = -1;              // the first replica's device, -1 = host-only
     unsigned threads = 1;
-    hipStream_t stream = nullptr;
+    std::atomic<uint32_t> rr{0};  // round-robin over replicas for calls that pick one
 
     WordDict dict;
-    tm_batch tokb;   // staging of tm_tokenize_device
 
     // node table (host): the fields a mutation touches in one 32-B record
     // (one cache line per node on the churn path), the filter-bytes index
@@ -581,49 +656,17 @@ struct tm_engine {
     std::vector<uint8_t> dirty_f_mark;
     bool full_dirty = true;
     bool full_f_dirty = true;
-    uint64_t fbytes_uploaded = 0;
-
-    // device replica
-    Slot* d_slots = nullptr;
-    size_t d_nslots = 0;
-    uint64_t* d_foff = nullptr;
-    uint32_t* d_flen = nullptr;
-    size_t c_foff = 0, c_flen = 0;
-    uint8_t* d_fbytes = nullptr;
-    size_t c_fbytes = 0;
-    // delta staging
+    // delta staging in pinned host memory, filled once per upload and copied to every replica
     uint32_t* h_didx = nullptr;
     Slot* h_dval = nullptr;
-    uint32_t* d_didx = nullptr;
-    Slot* d_dval = nullptr;
-    size_t ch_didx = 0, ch_dval = 0, cd_didx = 0, cd_dval = 0;
+    size_t ch_didx = 0, ch_dval = 0;
     uint32_t* h_fidx = nullptr;
     uint64_t* h_foffv = nullptr;
     uint32_t* h_flenv = nullptr;
-    uint32_t* d_fidx = nullptr;
-    uint64_t* d_foffv = nullptr;
-    uint32_t* d_flenv = nullptr;
-    size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0, cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
-    hipEvent_t ev_delta = nullptr;
-    hipEvent_t ev_sync = nullptr;        // end of the delta uploads, waited for by own-stream batches
-    // batches on streams of their own (async slots) read the replica
-    // concurrently with the engine stream: uploads wait for their walks first
-    std::vector<tm_batch*> readers;
-    uint64_t upload_seq = 0;             // async trie uploads recorded on ev_sync
-    bool delta_inflight = false;
-    // device word dictionary (device tokeniser): cuckoo key table, tails, arena
-    DictKey* d_dkey = nullptr;
-    size_t d_dict_n = 0;            // cuckoo slots on the device
-    uint64_t d_dict_gen = ~0ull;    // dict.gen() of the device table
-    DictTail* d_tail = nullptr;
-    size_t c_tail = 0, tails_uploaded = 0;
-    uint8_t* d_arena = nullptr;
-    size_t c_arena = 0, arena_uploaded = 0;
+    size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0;
     uint32_t* h_dxidx = nullptr;
     DictKey* h_dxval = nullptr;
-    uint32_t* d_dxidx = nullptr;
-    DictKey* d_dxval = nullptr;
-    size_t ch_dxidx = 0, ch_dxval = 0, cd_dxidx = 0, cd_dxval = 0;
+    size_t ch_dxidx = 0, ch_dxval = 0;
     bool dev_tok = true;            // TM_CFG_HOST_TOKENIZE / TM_HOST_TOKENIZE=1: tokenise on the host
 
 
@@ -637,11 +680,6 @@ struct tm_engine {
     uint64_t fan_big_limit = 0xFFFFFFFFull;   // fan-out scan blocks above this use u64 offsets (TM_FAN_BIG: tests)
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
-    uint32_t* d_dbg = nullptr;
-    uint32_t* h_dbg = nullptr;
-    size_t c_dbg = 0, ch_dbg = 0;
-
-    tm_batch scratch;   // reused by tm_match_batch / tm_trie_match
 
     // routes (the emqx_route bag, aggregated per destination by the caller):
     // node id -> [(dest, count)] in first-added order; total routes per node
@@ -649,8 +687,7 @@ struct tm_engine {
     std::vector<uint32_t> n_nroutes;
     bool routes_dirty = true;
     uint64_t route_entries = 0;
-    uint32_t *d_roff = nullptr, *d_rdest = nullptr;
-    size_t c_roff = 0, c_rdest = 0;
+    uint64_t routes_gen = 0;   // bumped when h_roff / h_rdest are rebuilt
     std::vector<uint32_t> h_roff, h_rdest;
 
     // ------------------------------------------------------------ hash
@@ -1190,13 +1227,6 @@ struct tm_engine {
     }
 
     // ------------------------------------------------------------ device sync
-    int ensure_delta_idle() {
-        if (delta_inflight) {
-            HIP_OK(hipEventSynchronize(ev_delta));
-            delta_inflight = false;
-        }
-        return TM_OK;
-    }
 
     uint32_t node_of(const uint8_t* t, size_t len) {
         static thread_local std::vector<uint32_t> ids;
@@ -1251,35 +1281,43 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // dests CSR by node id -> HBM (rebuilt whole when routes changed)
-    int sync_routes() {
-        if (!routes_dirty && c_roff >= nd.size() + 1) return TM_OK;
-        const size_t nn = nd.size();
-        h_roff.assign(nn + 1, 0);
-        h_rdest.clear();
-        h_rdest.reserve(route_entries);
-        for (size_t i = 0; i < nn; ++i) {
-            h_roff[i] = (uint32_t)h_rdest.size();
-            if (i < n_dests.size())
-                for (const auto& e : n_dests[i]) h_rdest.push_back(e.first);
+    // dests CSR by node id: built on the host when routes changed (routes_gen),
+    // uploaded to a replica that has an older one
+    int sync_routes(Replica& R) {
+        if (routes_dirty || h_roff.size() < nd.size() + 1) {
+            const size_t nn = nd.size();
+            h_roff.assign(nn + 1, 0);
+            h_rdest.clear();
+            h_rdest.reserve(route_entries);
+            for (size_t i = 0; i < nn; ++i) {
+                h_roff[i] = (uint32_t)h_rdest.size();
+                if (i < n_dests.size())
+                    for (const auto& e : n_dests[i]) h_rdest.push_back(e.first);
+            }
+            h_roff[nn] = (uint32_t)h_rdest.size();
+            routes_dirty = false;
+            ++routes_gen;
         }
-        h_roff[nn] = (uint32_t)h_rdest.size();
+        if (R.routes_gen == routes_gen) return TM_OK;
+        const size_t nn = h_roff.size() - 1;
         int rc;
-        if ((rc = dev_reserve(d_roff, c_roff, nn + 1))) return rc;
-        if ((rc = dev_reserve(d_rdest, c_rdest, std::max<size_t>(h_rdest.size(), 1)))) return rc;
-        HIP_OK(hipMemcpyAsync(d_roff, h_roff.data(), (nn + 1) * 4, hipMemcpyHostToDevice, stream));
+        if ((rc = dev_reserve(R.d_roff, R.c_roff, nn + 1))) return rc;
+        if ((rc = dev_reserve(R.d_rdest, R.c_rdest, std::max<size_t>(h_rdest.size(), 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(R.d_roff, h_roff.data(), (nn + 1) * 4, hipMemcpyHostToDevice, R.stream));
         if (!h_rdest.empty())
-            HIP_OK(hipMemcpyAsync(d_rdest, h_rdest.data(), h_rdest.size() * 4, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipStreamSynchronize(stream));
-        routes_dirty = false;
+            HIP_OK(hipMemcpyAsync(R.d_rdest, h_rdest.data(), h_rdest.size() * 4, hipMemcpyHostToDevice, R.stream));
+        HIP_OK(hipStreamSynchronize(R.stream));
+        R.routes_gen = routes_gen;
         return TM_OK;
     }
 
     // tm_batch_routes: route CSR of a waited batch, resolved on the device
     int batch_routes(tm_batch* b, tm_routes* out) {
         if (!b->done) return TM_EINVAL;
+        Replica& R = *b->rep;
+        const hipStream_t stream = R.stream;
         int rc;
-        if ((rc = sync_routes())) return rc;
+        if ((rc = sync_routes(R))) return rc;
         const uint32_t n = b->n;
         const size_t nn = std::max<size_t>(n, 1);
         const uint64_t m64 = b->total;   // match entries (< 2^32: u32 result CSR)
@@ -1293,7 +1331,7 @@ struct tm_engine {
         if ((rc = host_reserve(b->h_rtotal, b->ch_rtotal, 1))) return rc;
         RouteArgs r{};
         r.row_off = b->d_rowoff; r.ids = b->d_ids; r.n = n; r.m = m;
-        r.roff = d_roff; r.rdest = d_rdest; r.nnodes = (uint32_t)nd.size();
+        r.roff = R.d_roff; r.rdest = R.d_rdest; r.nnodes = (uint32_t)(h_roff.size() - 1);
         r.ecount = b->d_rcount; r.eoff = b->d_reoff; r.bsums = b->d_rbsums; r.total = b->d_rtotal;
         r.r_rowoff = b->d_rrow;
         HIP_OK(launch_route_count(r, stream));
@@ -1344,13 +1382,11 @@ struct tm_engine {
     std::unordered_map<uint32_t, std::vector<std::string>> topics_of;
     bool subs_dirty = true;
     uint64_t sub_entries = 0, subs_version = 0;
-    uint64_t* d_soff = nullptr;
-    uint32_t* d_subs = nullptr;
-    uint8_t* d_scnt = nullptr;    // per node: min(soff[f + 1] - soff[f], 255) (the scan's 1-B gather)
-    uint32_t* d_sone = nullptr;   // per node: its subscriber when it has exactly one (the fill's 4-B gather)
-    size_t c_sone = 0;
+    uint64_t subs_gen = 0;         // bumped when the host arrays below are rebuilt
+    // host image of the device arrays: soff (u64), subs, scnt = per node
+    // min(soff[f + 1] - soff[f], 255) (the scan's 1-B gather), sone = the
+    // subscriber of a one-subscriber node (the fill's 4-B gather)
     std::vector<uint32_t> h_sone;
-    size_t c_soff = 0, c_subs = 0, c_scnt = 0;
     std::vector<uint8_t> h_scnt;
     uint32_t subs_nn = 0;
     std::vector<uint64_t> h_soff;
@@ -1420,50 +1456,58 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // subscriber runs by node id -> HBM (rebuilt whole after subscription or
-    // trie changes: a topic's node id is looked up at build time)
-    int sync_subs() {
+    // subscriber runs by node id: rebuilt on the host after subscription or
+    // trie changes (a topic's node id is looked up at build time), uploaded to
+    // a replica holding an older build
+    int sync_subs(Replica& R) {
         const size_t nn = nd.size();
-        if (!subs_dirty && subs_version == version && subs_nn == nn && d_soff) return TM_OK;
-        h_soff.assign(nn + 1, 0);
-        std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> runs;
-        runs.reserve(subs_of.size());
-        for (const auto& kv : subs_of) {
-            const uint32_t n = node_of((const uint8_t*)kv.first.data(), kv.first.size());
-            if (n == NONE || n >= nn) continue;   // not in the trie: no route, no dispatch
-            runs.emplace_back(n, &kv.second);
-            h_soff[n + 1] += kv.second.size();
+        if (subs_dirty || subs_version != version || subs_nn != nn || h_soff.empty()) {
+            h_soff.assign(nn + 1, 0);
+            std::vector<std::pair<uint32_t, const std::vector<uint32_t>*>> runs;
+            runs.reserve(subs_of.size());
+            for (const auto& kv : subs_of) {
+                const uint32_t n = node_of((const uint8_t*)kv.first.data(), kv.first.size());
+                if (n == NONE || n >= nn) continue;   // not in the trie: no route, no dispatch
+                runs.emplace_back(n, &kv.second);
+                h_soff[n + 1] += kv.second.size();
+            }
+            for (size_t i = 0; i < nn; ++i) h_soff[i + 1] += h_soff[i];
+            h_subs.resize(h_soff[nn]);
+            for (const auto& r : runs) std::copy(r.second->begin(), r.second->end(), h_subs.begin() + (long)h_soff[r.first]);
+            h_scnt.resize(std::max<size_t>(nn, 1));
+            for (size_t i = 0; i < nn; ++i) h_scnt[i] = (uint8_t)std::min<uint64_t>(h_soff[i + 1] - h_soff[i], 255);
+            h_sone.assign(std::max<size_t>(nn, 1), NONE);
+            for (size_t i = 0; i < nn; ++i)
+                if (h_soff[i + 1] - h_soff[i] == 1) h_sone[i] = h_subs[h_soff[i]];
+            subs_dirty = false;
+            subs_version = version;
+            subs_nn = (uint32_t)nn;
+            ++subs_gen;
         }
-        for (size_t i = 0; i < nn; ++i) h_soff[i + 1] += h_soff[i];
-        h_subs.resize(h_soff[nn]);
-        for (const auto& r : runs) std::copy(r.second->begin(), r.second->end(), h_subs.begin() + (long)h_soff[r.first]);
-        h_scnt.resize(std::max<size_t>(nn, 1));
-        for (size_t i = 0; i < nn; ++i) h_scnt[i] = (uint8_t)std::min<uint64_t>(h_soff[i + 1] - h_soff[i], 255);
-        h_sone.assign(std::max<size_t>(nn, 1), NONE);
-        for (size_t i = 0; i < nn; ++i)
-            if (h_soff[i + 1] - h_soff[i] == 1) h_sone[i] = h_subs[h_soff[i]];
+        if (R.subs_gen == subs_gen) return TM_OK;
+        const size_t sn = subs_nn;
         int rc;
-        if ((rc = dev_reserve(d_soff, c_soff, nn + 1))) return rc;
-        if ((rc = dev_reserve(d_scnt, c_scnt, std::max<size_t>(nn, 1)))) return rc;
-        if ((rc = dev_reserve(d_sone, c_sone, std::max<size_t>(nn, 1)))) return rc;
-        if ((rc = dev_reserve(d_subs, c_subs, std::max<size_t>(h_subs.size(), 1)))) return rc;
-        HIP_OK(hipMemcpyAsync(d_soff, h_soff.data(), (nn + 1) * 8, hipMemcpyHostToDevice, stream));
-        if (nn) HIP_OK(hipMemcpyAsync(d_scnt, h_scnt.data(), nn, hipMemcpyHostToDevice, stream));
-        if (nn) HIP_OK(hipMemcpyAsync(d_sone, h_sone.data(), nn * 4, hipMemcpyHostToDevice, stream));
+        if ((rc = dev_reserve(R.d_soff, R.c_soff, sn + 1))) return rc;
+        if ((rc = dev_reserve(R.d_scnt, R.c_scnt, std::max<size_t>(sn, 1)))) return rc;
+        if ((rc = dev_reserve(R.d_sone, R.c_sone, std::max<size_t>(sn, 1)))) return rc;
+        if ((rc = dev_reserve(R.d_subs, R.c_subs, std::max<size_t>(h_subs.size(), 1)))) return rc;
+        HIP_OK(hipMemcpyAsync(R.d_soff, h_soff.data(), (sn + 1) * 8, hipMemcpyHostToDevice, R.stream));
+        if (sn) HIP_OK(hipMemcpyAsync(R.d_scnt, h_scnt.data(), sn, hipMemcpyHostToDevice, R.stream));
+        if (sn) HIP_OK(hipMemcpyAsync(R.d_sone, h_sone.data(), sn * 4, hipMemcpyHostToDevice, R.stream));
         if (!h_subs.empty())
-            HIP_OK(hipMemcpyAsync(d_subs, h_subs.data(), h_subs.size() * 4, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipStreamSynchronize(stream));
-        subs_dirty = false;
-        subs_version = version;
-        subs_nn = (uint32_t)nn;
+            HIP_OK(hipMemcpyAsync(R.d_subs, h_subs.data(), h_subs.size() * 4, hipMemcpyHostToDevice, R.stream));
+        HIP_OK(hipStreamSynchronize(R.stream));
+        R.subs_gen = subs_gen;
         return TM_OK;
     }
 
     // tm_batch_dispatch: deliveries of a waited batch, resolved on the device
     int batch_dispatch(tm_batch* b, uint32_t flags, tm_deliveries* out) {
         if (!b->done) return TM_EINVAL;
+        Replica& R = *b->rep;
+        const hipStream_t stream = R.stream;
         int rc;
-        if ((rc = sync_subs())) return rc;
+        if ((rc = sync_subs(R))) return rc;
         const uint32_t n = b->n;
         const uint64_t nm = b->total;
         const uint32_t nb = (uint32_t)((nm + 1 + fan_scan_tile() - 1) / fan_scan_tile());
@@ -1480,7 +1524,7 @@ struct tm_engine {
         }
         FanArgs fa{};
         fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
-        fa.soff = d_soff; fa.scnt = d_scnt; fa.sone = d_sone; fa.subs = d_subs; fa.nnodes = subs_nn;
+        fa.soff = R.d_soff; fa.scnt = R.d_scnt; fa.sone = R.d_sone; fa.subs = R.d_subs; fa.nnodes = subs_nn;
         fa.moff = b->d_moff; fa.moff32 = b->d_moff32; fa.bbig = b->d_fbig; fa.bsums = b->d_fbsums;
         fa.big_limit = fan_big_limit; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
         HIP_OK(launch_fan_scan(fa, stream));
@@ -1536,10 +1580,9 @@ struct tm_engine {
     }
 
     // tm_rules_match: rules tokenised with their own dictionary, names against it
-    uint32_t *d_rl = nullptr;
-    size_t c_rl = 0;
-    int rules_match(const uint8_t* names, const uint64_t* noffs, uint32_t n, const uint8_t* rules,
+    int rules_match(Replica& R, const uint8_t* names, const uint64_t* noffs, uint32_t n, const uint8_t* rules,
                     const uint64_t* roffs, uint32_t r, bool dollar_rule, uint32_t* bits) {
+        const hipStream_t stream = R.stream;
         WordDict rd;
         std::vector<TWord> ws;
         std::vector<uint32_t> rw, ro(1, 0), nw, no(1, 0);
@@ -1577,8 +1620,8 @@ struct tm_engine {
         const size_t nbits = (size_t)n * wpr;
         const size_t words = rw.size() + ro.size() + nw.size() + no.size() + nbits + (r + n + 3) / 4 + 4;
         int rc;
-        if ((rc = dev_reserve(d_rl, c_rl, words))) return rc;
-        uint32_t* d = d_rl;
+        if ((rc = dev_reserve(R.d_rl, R.c_rl, words))) return rc;
+        uint32_t* d = R.d_rl;
         uint32_t *d_rw = d, *d_ro = d_rw + rw.size(), *d_nw = d_ro + ro.size(), *d_no = d_nw + nw.size();
         uint32_t* d_bits = d_no + no.size();
         uint8_t* d_rf = reinterpret_cast<uint8_t*>(d_bits + nbits);
@@ -1604,178 +1647,258 @@ struct tm_engine {
                                       slots.size() * target_load * 1.5 < live_edges);
     }
 
-    // anything for sync_device to upload?
-    bool upload_pending() {
-        if (full_dirty || !dirty.empty() || d_nslots != slots.size() || needs_repack()) return true;
-        if (full_f_dirty || !dirty_f.empty() || fbytes.size() > fbytes_uploaded) return true;
-        if (c_foff < nd.size() || c_flen < nd.size() || c_fbytes < fbytes.size() + 1) return true;
-        if (dev_tok && (d_dict_n != dict.keys().size() || d_dict_gen != dict.gen() || !dict.dirty().empty() ||
-                        dict.tails().size() > tails_uploaded || dict.arena().size() > arena_uploaded ||
-                        c_arena < dict.arena().size() + 1))
+    // anything for sync_device to upload to replica R?
+    bool upload_pending(const Replica& R) {
+        if (full_dirty || !dirty.empty() || R.d_nslots != slots.size() || needs_repack()) return true;
+        if (full_f_dirty || !dirty_f.empty() || fbytes.size() > R.fbytes_uploaded) return true;
+        if (R.c_foff < nd.size() || R.c_flen < nd.size() || R.c_fbytes < fbytes.size() + 1) return true;
+        if (dev_tok && (R.d_dict_n != dict.keys().size() || R.d_dict_gen != dict.gen() || !dict.dirty().empty() ||
+                        dict.tails().size() > R.tails_uploaded || dict.arena().size() > R.arena_uploaded ||
+                        R.c_arena < dict.arena().size() + 1))
             return true;
         return false;
     }
 
-    int sync_device() {
-        if (device < 0) return TM_ENODEV;
-        int rc = ensure_delta_idle();
-        if (rc) return rc;
-        if (!readers.empty() && upload_pending())
-            for (tm_batch* r : readers)   // batches on other streams finish before the tables change
-                if (r->launched) HIP_OK(hipStreamSynchronize(r->own));
-        // after a bulk build or heavy churn, re-pack the replica to load ~0.55 so
-        // the walk's working set stays small (it is a full upload anyway)
-        if (needs_repack()) rehash((size_t)(live_edges / target_load));
-        // edge hash
-        if (d_nslots != slots.size()) {
-            dev_free(d_slots);
-            HIP_OK(hipMalloc((void**)&d_slots, slots.size() * sizeof(Slot)));
-            d_nslots = slots.size();
-            full_dirty = true;
-        }
-        bool async_used = false, pageable_used = false;
-        if (full_dirty || dirty.size() > slots.size() / 8) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_slots, slots.data(), slots.size() * sizeof(Slot), hipMemcpyHostToDevice, stream));
-            ++uploads_full;
-            full_dirty = false;
-            for (uint32_t i : dirty) dirty_mark[i >> 6] = 0;   // every set bit is in `dirty`
-            dirty.clear();
-            if (dirty_mark.size() != (slots.size() + 63) / 64) dirty_mark.assign((slots.size() + 63) / 64, 0);
-        } else if (!dirty.empty()) {
-            const size_t nd = dirty.size();
-            if ((rc = host_reserve(h_didx, ch_didx, nd))) return rc;
-            if ((rc = host_reserve(h_dval, ch_dval, nd))) return rc;
-            if ((rc = dev_reserve(d_didx, cd_didx, nd))) return rc;
-            if ((rc = dev_reserve(d_dval, cd_dval, nd))) return rc;
-            for (size_t k = 0; k < nd; ++k) {
-                h_didx[k] = dirty[k];
-                h_dval[k] = slots[dirty[k]];
-                dirty_mark[dirty[k] >> 6] = 0;
+    int ensure_delta_idle() {
+        for (Replica* R : reps)
+            if (R->delta_inflight) {
+                HIP_OK(hipSetDevice(R->device));
+                HIP_OK(hipEventSynchronize(R->ev_delta));
+                R->delta_inflight = false;
             }
-            HIP_OK(hipMemcpyAsync(d_didx, h_didx, nd * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_dval, h_dval, nd * sizeof(Slot), hipMemcpyHostToDevice, stream));
-            HIP_OK(launch_scatter_slots(d_slots, d_didx, d_dval, (uint32_t)nd, stream));
-            ++uploads_delta;
-            delta_slots += nd;
-            dirty.clear();
-            async_used = true;
-        }
-        // filter bytes (slow-path sort) : arena + per-node (off, len)
-        const size_t nn = nd.size();
-        if (c_foff < nn || c_flen < nn) {
-            if ((rc = dev_reserve(d_foff, c_foff, nn))) return rc;
-            if ((rc = dev_reserve(d_flen, c_flen, nn))) return rc;
-            full_f_dirty = true;
-        }
-        if (c_fbytes < fbytes.size() + 1) {
-            if ((rc = dev_reserve(d_fbytes, c_fbytes, fbytes.size() + 1))) return rc;
-            fbytes_uploaded = 0;
-        }
-        if (fbytes.size() > fbytes_uploaded) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_fbytes + fbytes_uploaded, fbytes.data() + fbytes_uploaded,
-                                  fbytes.size() - fbytes_uploaded, hipMemcpyHostToDevice, stream));
-            fbytes_uploaded = fbytes.size();
-        }
-        if (full_f_dirty) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_foff, n_foff.data(), nn * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_flen, n_flen.data(), nn * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-            full_f_dirty = false;
-            dirty_f.clear();
-            dirty_f_mark.assign(nn, 0);
-        } else if (!dirty_f.empty()) {
-            const size_t nd = dirty_f.size();
-            if ((rc = host_reserve(h_fidx, ch_fidx, nd))) return rc;
-            if ((rc = host_reserve(h_foffv, ch_foffv, nd))) return rc;
-            if ((rc = host_reserve(h_flenv, ch_flenv, nd))) return rc;
-            if ((rc = dev_reserve(d_fidx, cd_fidx, nd))) return rc;
-            if ((rc = dev_reserve(d_foffv, cd_foffv, nd))) return rc;
-            if ((rc = dev_reserve(d_flenv, cd_flenv, nd))) return rc;
-            for (size_t k = 0; k < nd; ++k) {
-                const uint32_t c = dirty_f[k];
-                h_fidx[k] = c; h_foffv[k] = n_foff[c]; h_flenv[k] = n_flen[c];
-                dirty_f_mark[c] = 0;
-            }
-            HIP_OK(hipMemcpyAsync(d_fidx, h_fidx, nd * 4, hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_foffv, h_foffv, nd * 8, hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_flenv, h_flenv, nd * 4, hipMemcpyHostToDevice, stream));
-            HIP_OK(launch_scatter_fmeta(d_foff, d_flen, d_fidx, d_foffv, d_flenv, (uint32_t)nd, stream));
-            dirty_f.clear();
-            async_used = true;
-        }
-        if (dev_tok && (rc = sync_dict(pageable_used, async_used))) return rc;
-        if (pageable_used) {
-            // host vectors may be mutated / reallocated right after we return
-            HIP_OK(hipStreamSynchronize(stream));
-        } else if (async_used) {
-            HIP_OK(hipEventRecord(ev_delta, stream));
-            delta_inflight = true;
-            if (!readers.empty()) {   // own-stream batches launched from now on wait for this upload
-                HIP_OK(hipEventRecord(ev_sync, stream));
-                ++upload_seq;
-            }
-        }
         return TM_OK;
     }
 
-    // word dictionary -> HBM: the whole cuckoo table after a rebuild, else the
-    // slots written since the last upload; the tails' and the arena's new ends
-    int sync_dict(bool& pageable_used, bool& async_used) {
+    // Brings every replica up to the host trie: the dirty slots, filter
+    // metadata and dictionary slots are gathered ONCE into pinned staging and
+    // each replica gets the same copies + scatter kernels on its own stream
+    // (full uploads where a replica's table was reallocated or most of it
+    // changed).  Uploads to a replica wait on the device for the walks of its
+    // own-stream batches in flight; those batches' next launches wait for the
+    // upload (ev_sync), so read-your-writes holds on every device.  Returns
+    // with the calling thread's device set to `back` (or the first replica's).
+    int sync_device(const Replica* back = nullptr) {
+        if (reps.empty()) return TM_ENODEV;
+        int rc = ensure_delta_idle();
+        if (rc) return rc;
+        bool any = false;
+        for (Replica* R : reps) any = any || upload_pending(*R);
+        if (!any) {
+            HIP_OK(hipSetDevice(back ? back->device : device));
+            return TM_OK;
+        }
+        // after a bulk build or heavy churn, re-pack the host table to the
+        // target load so the walk's working set stays small (a full upload)
+        if (needs_repack()) rehash((size_t)(live_edges / target_load));
+        const size_t nn = nd.size();
+        // gather the deltas once
+        const bool slots_full = full_dirty || dirty.size() > slots.size() / 8;
+        if (!slots_full && !dirty.empty()) {
+            const size_t k = dirty.size();
+            if ((rc = host_reserve(h_didx, ch_didx, k))) return rc;
+            if ((rc = host_reserve(h_dval, ch_dval, k))) return rc;
+            for (size_t i = 0; i < k; ++i) {
+                h_didx[i] = dirty[i];
+                h_dval[i] = slots[dirty[i]];
+            }
+        }
+        if (!full_f_dirty && !dirty_f.empty()) {
+            const size_t k = dirty_f.size();
+            if ((rc = host_reserve(h_fidx, ch_fidx, k))) return rc;
+            if ((rc = host_reserve(h_foffv, ch_foffv, k))) return rc;
+            if ((rc = host_reserve(h_flenv, ch_flenv, k))) return rc;
+            for (size_t i = 0; i < k; ++i) {
+                const uint32_t c = dirty_f[i];
+                h_fidx[i] = c; h_foffv[i] = n_foff[c]; h_flenv[i] = n_flen[c];
+            }
+        }
+        std::vector<uint32_t>& dx = dict.dirty();
+        const bool keys_full = dx.size() > dict.keys().size() / 8;
+        if (dev_tok && !keys_full && !dx.empty()) {
+            std::sort(dx.begin(), dx.end());
+            dx.erase(std::unique(dx.begin(), dx.end()), dx.end());   // a slot may move twice: scatter it once
+            const size_t k = dx.size();
+            if ((rc = host_reserve(h_dxidx, ch_dxidx, k))) return rc;
+            if ((rc = host_reserve(h_dxval, ch_dxval, k))) return rc;
+            for (size_t i = 0; i < k; ++i) {
+                h_dxidx[i] = dx[i];
+                h_dxval[i] = dict.keys()[dx[i]];
+            }
+        }
+        // apply to every replica (different devices run their copies concurrently)
+        std::vector<uint8_t> pageable(reps.size(), 0), async(reps.size(), 0);
+        for (size_t r = 0; r < reps.size(); ++r) {
+            Replica& R = *reps[r];
+            bool pg = false, as = false;
+            if ((rc = upload_to(R, slots_full, keys_full, nn, pg, as))) return rc;
+            pageable[r] = pg;
+            async[r] = as;
+        }
+        // the dirty sets are consumed: every replica has them now
+        if (slots_full) {
+            full_dirty = false;
+            for (uint32_t i : dirty) dirty_mark[i >> 6] = 0;   // every set bit is in `dirty`
+            if (dirty_mark.size() != (slots.size() + 63) / 64) dirty_mark.assign((slots.size() + 63) / 64, 0);
+        } else {
+            for (uint32_t i : dirty) dirty_mark[i >> 6] = 0;
+        }
+        dirty.clear();
+        if (full_f_dirty) {
+            full_f_dirty = false;
+            dirty_f_mark.assign(nn, 0);
+        } else {
+            for (uint32_t c : dirty_f) dirty_f_mark[c] = 0;
+        }
+        dirty_f.clear();
+        if (dev_tok) dx.clear();
+        for (size_t r = 0; r < reps.size(); ++r) {
+            Replica& R = *reps[r];
+            HIP_OK(hipSetDevice(R.device));
+            if (pageable[r]) {
+                // host vectors may be mutated / reallocated right after we return
+                HIP_OK(hipStreamSynchronize(R.stream));
+            } else if (async[r]) {
+                HIP_OK(hipEventRecord(R.ev_delta, R.stream));
+                R.delta_inflight = true;
+                if (!R.readers.empty()) {   // own-stream batches launched from now on wait for this upload
+                    HIP_OK(hipEventRecord(R.ev_sync, R.stream));
+                    ++R.upload_seq;
+                }
+            }
+        }
+        HIP_OK(hipSetDevice(back ? back->device : device));
+        return TM_OK;
+    }
+
+    // one replica's share of sync_device: the staged deltas (or full tables)
+    int upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn, bool& pageable_used, bool& async_used) {
         int rc;
+        HIP_OK(hipSetDevice(R.device));
+        const hipStream_t stream = R.stream;
+        // tables change under the walks of this replica's own-stream batches in
+        // flight: the uploads wait for them on the device, or on the host when
+        // a table is reallocated (its old buffer is freed here)
+        const bool realloc = R.d_nslots != slots.size() || R.c_foff < nn || R.c_flen < nn ||
+                             R.c_fbytes < fbytes.size() + 1 ||
+                             (dev_tok && (R.d_dict_n != dict.keys().size() || R.c_tail < dict.tails().size() + 1 ||
+                                          R.c_arena < dict.arena().size() + 1));
+        for (tm_batch* r : R.readers)
+            if (r->launched) {
+                if (realloc) {
+                    HIP_OK(hipStreamSynchronize(r->own));
+                    continue;
+                }
+                if (!r->ev_read) HIP_OK(hipEventCreateWithFlags(&r->ev_read, hipEventDisableTiming));
+                HIP_OK(hipEventRecord(r->ev_read, r->own));
+                HIP_OK(hipStreamWaitEvent(stream, r->ev_read, 0));
+            }
+        // edge hash
+        bool full = slots_full;
+        if (R.d_nslots != slots.size()) {
+            dev_free(R.d_slots);
+            HIP_OK(hipMalloc((void**)&R.d_slots, slots.size() * sizeof(Slot)));
+            R.d_nslots = slots.size();
+            full = true;
+        }
+        if (full) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(R.d_slots, slots.data(), slots.size() * sizeof(Slot), hipMemcpyHostToDevice, stream));
+            ++uploads_full;
+        } else if (!dirty.empty()) {
+            const size_t k = dirty.size();
+            if ((rc = dev_reserve(R.d_didx, R.cd_didx, k))) return rc;
+            if ((rc = dev_reserve(R.d_dval, R.cd_dval, k))) return rc;
+            HIP_OK(hipMemcpyAsync(R.d_didx, h_didx, k * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(R.d_dval, h_dval, k * sizeof(Slot), hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_slots(R.d_slots, R.d_didx, R.d_dval, (uint32_t)k, stream));
+            ++uploads_delta;
+            delta_slots += k;
+            async_used = true;
+        }
+        // filter bytes (slow-path sort): arena + per-node (off, len)
+        bool f_full = full_f_dirty;
+        if (R.c_foff < nn || R.c_flen < nn) {
+            if ((rc = dev_reserve(R.d_foff, R.c_foff, nn))) return rc;
+            if ((rc = dev_reserve(R.d_flen, R.c_flen, nn))) return rc;
+            f_full = true;
+        }
+        if (R.c_fbytes < fbytes.size() + 1) {
+            if ((rc = dev_reserve(R.d_fbytes, R.c_fbytes, fbytes.size() + 1))) return rc;
+            R.fbytes_uploaded = 0;
+        }
+        if (fbytes.size() > R.fbytes_uploaded) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(R.d_fbytes + R.fbytes_uploaded, fbytes.data() + R.fbytes_uploaded,
+                                  fbytes.size() - R.fbytes_uploaded, hipMemcpyHostToDevice, stream));
+            R.fbytes_uploaded = fbytes.size();
+        }
+        if (f_full) {
+            pageable_used = true;
+            HIP_OK(hipMemcpyAsync(R.d_foff, n_foff.data(), nn * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(R.d_flen, n_flen.data(), nn * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+        } else if (!dirty_f.empty()) {
+            const size_t k = dirty_f.size();
+            if ((rc = dev_reserve(R.d_fidx, R.cd_fidx, k))) return rc;
+            if ((rc = dev_reserve(R.d_foffv, R.cd_foffv, k))) return rc;
+            if ((rc = dev_reserve(R.d_flenv, R.cd_flenv, k))) return rc;
+            HIP_OK(hipMemcpyAsync(R.d_fidx, h_fidx, k * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(R.d_foffv, h_foffv, k * 8, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(R.d_flenv, h_flenv, k * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_fmeta(R.d_foff, R.d_flen, R.d_fidx, R.d_foffv, R.d_flenv, (uint32_t)k, stream));
+            async_used = true;
+        }
+        if (dev_tok && (rc = sync_dict(R, keys_full, pageable_used, async_used))) return rc;
+        return TM_OK;
+    }
+
+    // word dictionary -> one replica: the whole cuckoo table after a rebuild
+    // (or when most of it changed), else the staged dirty slots; the tails'
+    // and the arena's new ends
+    int sync_dict(Replica& R, bool keys_full, bool& pageable_used, bool& async_used) {
+        int rc;
+        const hipStream_t stream = R.stream;
         const std::vector<DictKey>& tab = dict.keys();
         const std::vector<DictTail>& tl = dict.tails();
         const std::vector<uint8_t>& ar = dict.arena();
-        std::vector<uint32_t>& dx = dict.dirty();
-        if (d_dict_n != tab.size()) {
-            dev_free(d_dkey);
-            HIP_OK(hipMalloc((void**)&d_dkey, tab.size() * sizeof(DictKey)));
-            d_dict_n = tab.size();
-            d_dict_gen = ~0ull;
+        const std::vector<uint32_t>& dx = dict.dirty();
+        if (R.d_dict_n != tab.size()) {
+            dev_free(R.d_dkey);
+            HIP_OK(hipMalloc((void**)&R.d_dkey, tab.size() * sizeof(DictKey)));
+            R.d_dict_n = tab.size();
+            R.d_dict_gen = ~0ull;
         }
-        if (d_dict_gen != dict.gen() || dx.size() > tab.size() / 8) {
+        if (R.d_dict_gen != dict.gen() || keys_full) {
             pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_dkey, tab.data(), tab.size() * sizeof(DictKey), hipMemcpyHostToDevice, stream));
-            d_dict_gen = dict.gen();
-            dx.clear();
+            HIP_OK(hipMemcpyAsync(R.d_dkey, tab.data(), tab.size() * sizeof(DictKey), hipMemcpyHostToDevice, stream));
+            R.d_dict_gen = dict.gen();
         } else if (!dx.empty()) {
-            std::sort(dx.begin(), dx.end());
-            dx.erase(std::unique(dx.begin(), dx.end()), dx.end());   // a slot may move twice: scatter it once
-            const size_t nd = dx.size();
-            if ((rc = host_reserve(h_dxidx, ch_dxidx, nd))) return rc;
-            if ((rc = host_reserve(h_dxval, ch_dxval, nd))) return rc;
-            if ((rc = dev_reserve(d_dxidx, cd_dxidx, nd))) return rc;
-            if ((rc = dev_reserve(d_dxval, cd_dxval, nd))) return rc;
-            for (size_t k = 0; k < nd; ++k) {
-                h_dxidx[k] = dx[k];
-                h_dxval[k] = tab[dx[k]];
-            }
-            HIP_OK(hipMemcpyAsync(d_dxidx, h_dxidx, nd * 4, hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_dxval, h_dxval, nd * sizeof(DictKey), hipMemcpyHostToDevice, stream));
-            HIP_OK(launch_scatter_keys(d_dkey, d_dxidx, d_dxval, (uint32_t)nd, stream));
-            dx.clear();
+            const size_t k = dx.size();
+            if ((rc = dev_reserve(R.d_dxidx, R.cd_dxidx, k))) return rc;
+            if ((rc = dev_reserve(R.d_dxval, R.cd_dxval, k))) return rc;
+            HIP_OK(hipMemcpyAsync(R.d_dxidx, h_dxidx, k * 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(R.d_dxval, h_dxval, k * sizeof(DictKey), hipMemcpyHostToDevice, stream));
+            HIP_OK(launch_scatter_keys(R.d_dkey, R.d_dxidx, R.d_dxval, (uint32_t)k, stream));
             async_used = true;
         }
-        if (c_tail < tl.size() + 1) {
-            if ((rc = dev_reserve(d_tail, c_tail, tl.size() + tl.size() / 2 + 64))) return rc;
-            tails_uploaded = 0;
+        if (R.c_tail < tl.size() + 1) {
+            if ((rc = dev_reserve(R.d_tail, R.c_tail, tl.size() + tl.size() / 2 + 64))) return rc;
+            R.tails_uploaded = 0;
         }
-        if (tl.size() > tails_uploaded) {
+        if (tl.size() > R.tails_uploaded) {
             pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_tail + tails_uploaded, tl.data() + tails_uploaded,
-                                  (tl.size() - tails_uploaded) * sizeof(DictTail), hipMemcpyHostToDevice, stream));
-            tails_uploaded = tl.size();
+            HIP_OK(hipMemcpyAsync(R.d_tail + R.tails_uploaded, tl.data() + R.tails_uploaded,
+                                  (tl.size() - R.tails_uploaded) * sizeof(DictTail), hipMemcpyHostToDevice, stream));
+            R.tails_uploaded = tl.size();
         }
-        if (c_arena < ar.size() + 1) {
-            if ((rc = dev_reserve(d_arena, c_arena, ar.size() + 1))) return rc;
-            arena_uploaded = 0;
+        if (R.c_arena < ar.size() + 1) {
+            if ((rc = dev_reserve(R.d_arena, R.c_arena, ar.size() + 1))) return rc;
+            R.arena_uploaded = 0;
         }
-        if (ar.size() > arena_uploaded) {
+        if (ar.size() > R.arena_uploaded) {
             pageable_used = true;
-            HIP_OK(hipMemcpyAsync(d_arena + arena_uploaded, ar.data() + arena_uploaded, ar.size() - arena_uploaded,
+            HIP_OK(hipMemcpyAsync(R.d_arena + R.arena_uploaded, ar.data() + R.arena_uploaded, ar.size() - R.arena_uploaded,
                                   hipMemcpyHostToDevice, stream));
-            arena_uploaded = ar.size();
+            R.arena_uploaded = ar.size();
         }
         return TM_OK;
     }
@@ -1920,12 +2043,14 @@ struct tm_engine {
     // tm_tokenize_device: the device tokeniser into caller device arrays
     int tokenize_device(const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* d_words, uint64_t cap,
                         uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords) {
-        if (device < 0) return TM_ENODEV;
+        if (reps.empty()) return TM_ENODEV;
         int rc;
-        tm_batch* b = &tokb;
+        Replica& R = *reps[0];   // the caller's device buffers are on the first replica's device
+        const hipStream_t stream = R.stream;
+        tm_batch* b = &R.tokb;
         const uint64_t base = offsets[0], nbytes = offsets[n] - base;
         if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
-        if ((rc = sync_device())) return rc;
+        if ((rc = sync_device(&R))) return rc;
         if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;
         if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
@@ -1938,7 +2063,7 @@ struct tm_engine {
         if (!n) HIP_OK(hipMemsetAsync(d_toff, 0, 4, stream));
         TokArgs t{};
         t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
-        t.keys = d_dkey; t.tails = d_tail; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+        t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
         t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
         t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
         t.tile_topics = tok_tile_topics(n, nbytes);
@@ -1955,6 +2080,7 @@ struct tm_engine {
     int prepare_tokens(tm_batch* b, const uint32_t* words, const uint32_t* toff, const uint8_t* tflags, uint32_t n,
                        uint64_t nwords, bool on_device) {
         if (nwords > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        const hipStream_t stream = b->rep ? st(b) : nullptr;   // (host-only engine: none)
         b->n = n;
         b->nwords = nwords;
         b->tokens_only = true;
@@ -2010,8 +2136,8 @@ struct tm_engine {
         if (!b->done) return TM_EINVAL;
         const uint64_t top = (uint64_t)(nd.size() ? nd.size() - 1 : 0) * mul + add;
         if (top > 0xFFFFFFFFull) return TM_EOVERFLOW;
-        HIP_OK(launch_export(b->d_rowoff, b->d_ids, b->n, b->total, d_counts, d_ids, mul, add, stream));
-        HIP_OK(hipStreamSynchronize(stream));
+        HIP_OK(launch_export(b->d_rowoff, b->d_ids, b->n, b->total, d_counts, d_ids, mul, add, st(b)));
+        HIP_OK(hipStreamSynchronize(st(b)));
         return TM_OK;
     }
 
@@ -2064,7 +2190,7 @@ struct tm_engine {
     int reserve_rows(tm_batch* b) {
         int rc;
         const uint64_t fast =
-            std::max<uint64_t>((uint64_t)match_waves(b->n, device, qcap) * tile_topics(b->n) * row_cap, 1);
+            std::max<uint64_t>((uint64_t)match_waves(b->n, b->rep->device, qcap) * tile_topics(b->n) * row_cap, 1);
         if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
         if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
@@ -2172,11 +2298,12 @@ struct tm_engine {
         return upload_batch(b);
     }
 
-    hipStream_t st(const tm_batch* b) const { return b->own ? b->own : stream; }
+    hipStream_t st(const tm_batch* b) const { return b->own ? b->own : b->rep->stream; }
 
     // a TM_BATCH_STREAM batch goes away: no longer a reader, stream destroyed
     void drop_user_stream(tm_batch* b) {
-        readers.erase(std::remove(readers.begin(), readers.end(), b), readers.end());
+        auto& rd = b->rep->readers;
+        rd.erase(std::remove(rd.begin(), rd.end(), b), rd.end());
         if (b->own) (void)hipStreamDestroy(b->own);
         b->own = nullptr;
         b->own_user = false;
@@ -2257,23 +2384,24 @@ struct tm_engine {
     // per-topic (src, count) of the header block, and the caller enqueues its
     // own read-back; ev2 then marks the end of the walk.
     int launch(tm_batch* b, bool csr = true) {
-        if (device < 0) return TM_ENODEV;
+        if (reps.empty()) return TM_ENODEV;
         int rc;
+        Replica& R = *b->rep;
         const hipStream_t S = st(b);
         if (!b->tokens_only && !b->dev_tok && b->dict_size != dict.size()) {   // new words since tokenisation
             if ((rc = tokenize(b))) return rc;
             if ((rc = upload_batch(b))) return rc;
         }
-        if ((rc = sync_device())) return rc;
-        if (b->own && b->seen_upload != upload_seq) {   // trie deltas still in flight on the engine stream land first
-            HIP_OK(hipStreamWaitEvent(S, ev_sync, 0));
-            b->seen_upload = upload_seq;
+        if ((rc = sync_device(&R))) return rc;
+        if (b->own && b->seen_upload != R.upload_seq) {   // trie deltas still in flight on the replica stream land first
+            HIP_OK(hipStreamWaitEvent(S, R.ev_sync, 0));
+            b->seen_upload = R.upload_seq;
         }
         if ((rc = ensure_slow_scratch(b))) return rc;
         if (checked) {
-            if ((rc = dev_reserve(d_dbg, c_dbg, 8))) return rc;
-            if ((rc = host_reserve(h_dbg, ch_dbg, 8))) return rc;
-            HIP_OK(hipMemsetAsync(d_dbg, 0, 8 * 4, S));
+            if ((rc = dev_reserve(R.d_dbg, R.c_dbg, 8))) return rc;
+            if ((rc = host_reserve(R.h_dbg, R.ch_dbg, 8))) return rc;
+            HIP_OK(hipMemsetAsync(R.d_dbg, 0, 8 * 4, S));
         }
         const bool tokenize_now = b->dev_tok && b->tok_dict != dict.size();
         if (!tokenize_now) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
@@ -2285,7 +2413,7 @@ struct tm_engine {
             t.zero = reinterpret_cast<uint32_t*>(b->d_hdr);   // the tokeniser's first kernel clears ctrl + stats
             t.zero_words = tm_batch::HDR_FIXED / 4;
             t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
-            t.keys = d_dkey; t.tails = d_tail; t.dict_mask = d_dict_n - 1; t.arena = d_arena;
+            t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
             t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
@@ -2295,16 +2423,16 @@ struct tm_engine {
             HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
         }
         MatchArgs a{};
-        a.slots = d_slots;
+        a.slots = R.d_slots;
         a.nbuckets = nbuckets();
         a.max_probe = max_disp;
         a.root = root_rec();
-        a.foff = d_foff; a.flen = d_flen; a.fbytes = d_fbytes;
+        a.foff = R.d_foff; a.flen = R.d_flen; a.fbytes = R.d_fbytes;
         a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
         a.slow_list = b->d_slow; a.n_slow = b->dev_slow ? 0u : (uint32_t)b->h_slow.size();
         a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
-        a.grid = match_waves(b->n, device, qcap);
+        a.grid = match_waves(b->n, R.device, qcap);
         a.tile_topics = tile_topics(b->n);
         a.qcap = qcap;
         {   // the first static_frac of the tiles round-robin, the tail by per-XCD tickets
@@ -2327,7 +2455,7 @@ struct tm_engine {
         a.nslots = (uint32_t)slots.size();
         a.nnodes = (uint32_t)nd.size();
         a.nfbytes = fbytes.size();
-        a.dbg = checked ? d_dbg : nullptr;
+        a.dbg = checked ? R.d_dbg : nullptr;
         HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
         note_launch(b);
         b->launched = true;
@@ -2339,14 +2467,14 @@ struct tm_engine {
         s.sfids = b->d_sfids; s.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
-        s.dbg = checked ? d_dbg : nullptr;
+        s.dbg = checked ? R.d_dbg : nullptr;
         HIP_OK(launch_scan(s, S, b->d_total));
         HIP_OK(launch_finalize(s, S, checked));
         b->scan_args = s;
         HIP_OK(hipEventRecord(b->ev2, S));
         HIP_OK(hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S));   // ctrl + stats
         HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S));
-        if (checked) HIP_OK(hipMemcpyAsync(h_dbg, d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
+        if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
         return TM_OK;
     }
 
@@ -2412,6 +2540,7 @@ struct tm_engine {
         }
         for (int attempt = 0;; ++attempt) {
             HIP_OK(hipStreamSynchronize(S));
+            const uint32_t* h_dbg = b->rep->h_dbg;
             if (checked && h_dbg[0]) {
                 snprintf(last_error(), 512, "bounds check %u failed: index %u bound %u (count %u, extra %u)",
                          h_dbg[0], h_dbg[1], h_dbg[2], h_dbg[3], h_dbg[4]);
@@ -2473,50 +2602,53 @@ struct tm_engine {
 
 
     // ------------------------------------------------------------ async pipeline
-    // Slots are created on first use (under amu; takes mu).
-    int async_start() {
-        if (a_started) return TM_OK;
-        if (device < 0) return TM_ENODEV;
-        if (const char* d = getenv("TM_ASYNC_DEPTH")) a_depth = (uint32_t)std::min(16, std::max(1, atoi(d)));
-        if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) a_busy_min = (uint32_t)std::max(1, atoi(d));
-        if (const char* d = getenv("TM_ASYNC_COMPLETERS")) a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
+    // Every replica runs a pipeline of its own (slots, launcher, completers);
+    // tm_match_async deals the calls over them.  Slots are created on first
+    // use or by tm_async_start (under R.amu; takes mu).
+    int async_start(Replica& R) {
+        if (R.a_started) return TM_OK;
+        if (reps.empty()) return TM_ENODEV;
+        if (const char* d = getenv("TM_ASYNC_DEPTH")) R.a_depth = (uint32_t)std::min(16, std::max(1, atoi(d)));
+        if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) R.a_busy_min = (uint32_t)std::max(1, atoi(d));
+        if (const char* d = getenv("TM_ASYNC_COMPLETERS")) R.a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
         {
             std::lock_guard<std::recursive_mutex> g(mu);
-            HIP_OK(hipSetDevice(device));
-            for (uint32_t i = 0; i < a_depth; ++i) {
+            HIP_OK(hipSetDevice(R.device));
+            for (uint32_t i = 0; i < R.a_depth; ++i) {
                 AsyncSlot* sl = new AsyncSlot();
-                a_slots.push_back(sl);
+                R.a_slots.push_back(sl);
+                sl->b.rep = &R;
                 HIP_OK(hipStreamCreateWithFlags(&sl->b.own, hipStreamNonBlocking));
                 HIP_OK(hipEventCreateWithFlags(&sl->ev_done, hipEventDisableTiming));
-                a_free.push_back(sl);
-                readers.push_back(&sl->b);
+                R.a_free.push_back(sl);
+                R.readers.push_back(&sl->b);
             }
         }
-        a_stop = false;
-        a_launcher_done = false;
-        a_launcher = std::thread([this] { launcher_loop(); });
-        for (uint32_t i = 0; i < a_ncompleters; ++i) a_completers.emplace_back([this] { completer_loop(); });
-        a_started = true;
-        a_live.store(true, std::memory_order_release);
+        R.a_stop = false;
+        R.a_launcher_done = false;
+        R.a_launcher = std::thread([this, &R] { launcher_loop(R); });
+        for (uint32_t i = 0; i < R.a_ncompleters; ++i) R.a_completers.emplace_back([this, &R] { completer_loop(R); });
+        R.a_started = true;
+        R.a_live.store(true, std::memory_order_release);
         return TM_OK;
     }
 
-    void async_stop() {
+    void async_stop(Replica& R) {
         {
-            std::lock_guard<std::mutex> lk(amu);
-            if (!a_started && a_slots.empty()) return;
-            a_stop = true;
-            a_live.store(false, std::memory_order_release);
+            std::lock_guard<std::mutex> lk(R.amu);
+            if (!R.a_started && R.a_slots.empty()) return;
+            R.a_stop = true;
+            R.a_live.store(false, std::memory_order_release);
         }
-        a_work.notify_all();
-        a_done.notify_all();
-        if (a_launcher.joinable()) a_launcher.join();
-        for (auto& t : a_completers)
+        R.a_work.notify_all();
+        R.a_done.notify_all();
+        if (R.a_launcher.joinable()) R.a_launcher.join();
+        for (auto& t : R.a_completers)
             if (t.joinable()) t.join();
-        a_completers.clear();
+        R.a_completers.clear();
         std::lock_guard<std::recursive_mutex> g(mu);
-        (void)hipSetDevice(device);
-        for (AsyncSlot* sl : a_slots) {
+        (void)hipSetDevice(R.device);
+        for (AsyncSlot* sl : R.a_slots) {
             if (sl->b.own) (void)hipStreamSynchronize(sl->b.own);
             forget_launch(&sl->b);
             sl->b.release();
@@ -2527,47 +2659,60 @@ struct tm_engine {
             if (sl->h_out) (void)hipHostFree(sl->h_out);
             delete sl;
         }
-        a_slots.clear();
-        a_free.clear();
-        readers.erase(std::remove_if(readers.begin(), readers.end(), [](tm_batch* r) { return !r->own_user; }),
-                      readers.end());
-        a_started = false;
+        R.a_slots.clear();
+        R.a_free.clear();
+        R.readers.erase(std::remove_if(R.readers.begin(), R.readers.end(), [](tm_batch* r) { return !r->own_user; }),
+                        R.readers.end());
+        R.a_started = false;
     }
 
+    // Deals calls over the replicas: a submitting thread goes round-robin,
+    // starting from a replica of its own, so a few busy submitters spread
+    // evenly and each replica's batches still form from whole queue shards.
     int match_async(const uint8_t* t, size_t len, tm_match_cb cb, void* ctx) {
-        if (!a_live.load(std::memory_order_acquire)) {
-            std::lock_guard<std::mutex> lk(amu);
-            if (a_stop) return TM_ENODEV;
-            if (!a_started) {
-                int rc = async_start();
+        if (reps.empty()) return TM_ENODEV;
+        static std::atomic<uint32_t> next_sub{0};
+        static thread_local uint32_t my_sub = next_sub.fetch_add(1);
+        static thread_local uint32_t my_calls = 0;
+        Replica& R = *reps[(my_sub + my_calls++) % reps.size()];
+        return match_async(R, t, len, cb, ctx);
+    }
+
+    int match_async(Replica& R, const uint8_t* t, size_t len, tm_match_cb cb, void* ctx) {
+        if (!R.a_live.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> lk(R.amu);
+            if (R.a_stop) return TM_ENODEV;
+            if (!R.a_started) {
+                int rc = async_start(R);
                 if (rc) return rc;
             }
         }
         static std::atomic<uint32_t> next_shard{0};
-        static thread_local uint32_t my_shard = next_shard.fetch_add(1) % QSHARDS;
-        QShard& sh = qs[my_shard];
+        static thread_local uint32_t my_shard = next_shard.fetch_add(1) % Replica::QSHARDS;
+        Replica::QShard& sh = R.qs[my_shard];
         {
             std::lock_guard<std::mutex> g(sh.mu);
             if (len) sh.bytes.insert(sh.bytes.end(), t, t + len);
             sh.lens.push_back((uint32_t)len);
             sh.calls.push_back(AsyncCall{cb, ctx});
         }
-        const uint64_t q = q_count.fetch_add(1, std::memory_order_acq_rel) + 1;
-        if (q == 1 || q == a_busy_min || q == a_max) {   // the launcher may be waiting for this
-            std::lock_guard<std::mutex> lk(amu);
-            a_work.notify_one();
+        const uint64_t q = R.q_count.fetch_add(1, std::memory_order_acq_rel) + 1;
+        if (q == 1 || q == R.a_busy_min || q == R.a_max) {   // the launcher may be waiting for this
+            std::lock_guard<std::mutex> lk(R.amu);
+            R.a_work.notify_one();
         }
         return TM_OK;
     }
 
     // moves exactly `take` queued calls (at least that many are queued) into the slot
-    void drain_queue(AsyncSlot* sl, size_t take) {
+    void drain_queue(Replica& R, AsyncSlot* sl, size_t take) {
+        constexpr uint32_t QSHARDS = Replica::QSHARDS;
         sl->calls.clear();
         sl->bytes.clear();
         sl->offs.assign(1, 0);
         static thread_local uint32_t start = 0;
         for (uint32_t k = 0; k < QSHARDS && sl->calls.size() < take; ++k) {
-            QShard& sh = qs[(start + k) % QSHARDS];
+            Replica::QShard& sh = R.qs[(start + k) % QSHARDS];
             std::lock_guard<std::mutex> g(sh.mu);
             size_t h = sh.head, hb = sh.head_bytes;
             while (h < sh.calls.size() && sl->calls.size() < take) {
@@ -2589,30 +2734,30 @@ struct tm_engine {
             }
         }
         start = (start + 1) % QSHARDS;   // no shard is always last
-        q_count.fetch_sub(sl->calls.size(), std::memory_order_acq_rel);
+        R.q_count.fetch_sub(sl->calls.size(), std::memory_order_acq_rel);
     }
 
     // Forms batches from the queue: everything queued while the pipeline was
-    // busy (up to a_max), optionally after a linger, on the next free slot.
-    void launcher_loop() {
-        (void)hipSetDevice(device);
-        std::unique_lock<std::mutex> lk(amu);
+    // busy (up to R.a_max), optionally after a linger, on the next free slot.
+    void launcher_loop(Replica& R) {
+        (void)hipSetDevice(R.device);
+        std::unique_lock<std::mutex> lk(R.amu);
         for (;;) {
-            a_work.wait(lk, [&] {
-                const uint64_t q = q_count.load(std::memory_order_acquire);
-                if (a_stop) return q == 0 || !a_free.empty();
-                const bool idle = a_free.size() == a_slots.size();
-                return q && !a_free.empty() && (idle || q >= a_busy_min);
+            R.a_work.wait(lk, [&] {
+                const uint64_t q = R.q_count.load(std::memory_order_acquire);
+                if (R.a_stop) return q == 0 || !R.a_free.empty();
+                const bool idle = R.a_free.size() == R.a_slots.size();
+                return q && !R.a_free.empty() && (idle || q >= R.a_busy_min);
             });
-            if (q_count.load(std::memory_order_acquire) == 0) break;   // stopping, queue drained
-            if (a_linger_us && !a_stop && q_count.load() < a_max)
-                a_work.wait_for(lk, std::chrono::microseconds(a_linger_us),
-                                [&] { return a_stop || q_count.load() >= a_max; });
-            AsyncSlot* sl = a_free.back();
-            a_free.pop_back();
-            const size_t take = std::min<uint64_t>(q_count.load(std::memory_order_acquire), std::max<uint32_t>(a_max, 1));
+            if (R.q_count.load(std::memory_order_acquire) == 0) break;   // stopping, queue drained
+            if (R.a_linger_us && !R.a_stop && R.q_count.load() < R.a_max)
+                R.a_work.wait_for(lk, std::chrono::microseconds(R.a_linger_us),
+                                [&] { return R.a_stop || R.q_count.load() >= R.a_max; });
+            AsyncSlot* sl = R.a_free.back();
+            R.a_free.pop_back();
+            const size_t take = std::min<uint64_t>(R.q_count.load(std::memory_order_acquire), std::max<uint32_t>(R.a_max, 1));
             lk.unlock();
-            drain_queue(sl, take);
+            drain_queue(R, sl, take);
             const auto t0 = std::chrono::steady_clock::now();
             try {
                 sl->rc = slot_launch(sl);
@@ -2621,13 +2766,13 @@ struct tm_engine {
             }
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             lk.lock();
-            a_max_seen = std::max<uint64_t>(a_max_seen, sl->calls.size());
-            a_us_launch += us;
-            a_inflight.push_back(sl);
-            a_done.notify_all();
+            R.a_max_seen = std::max<uint64_t>(R.a_max_seen, sl->calls.size());
+            R.a_us_launch += us;
+            R.a_inflight.push_back(sl);
+            R.a_done.notify_all();
         }
-        a_launcher_done = true;
-        a_done.notify_all();
+        R.a_launcher_done = true;
+        R.a_done.notify_all();
     }
 
     // H2D of the slot's topics (one copy), device tokeniser, walk, and one
@@ -2641,7 +2786,7 @@ struct tm_engine {
         memcpy(sl->h_in, sl->offs.data(), ((size_t)n + 1) * 8);
         if (nb) memcpy(sl->h_in + head, sl->bytes.data(), nb);
         std::lock_guard<std::recursive_mutex> g(mu);
-        HIP_OK(hipSetDevice(device));
+        HIP_OK(hipSetDevice(sl->b.rep->device));
         tm_batch* b = &sl->b;
         const hipStream_t S = b->own;
         rc = dev_tok ? upload_packed(b, sl->h_in, n, nb)
@@ -2675,18 +2820,18 @@ struct tm_engine {
     // Each completer claims the oldest in-flight slot nobody delivers yet,
     // waits for it and runs its callbacks; several completers deliver
     // consecutive batches concurrently.
-    void completer_loop() {
-        (void)hipSetDevice(device);
-        std::unique_lock<std::mutex> lk(amu);
+    void completer_loop(Replica& R) {
+        (void)hipSetDevice(R.device);
+        std::unique_lock<std::mutex> lk(R.amu);
         for (;;) {
             AsyncSlot* sl = nullptr;
-            a_done.wait(lk, [&] {
-                for (AsyncSlot* x : a_inflight)
+            R.a_done.wait(lk, [&] {
+                for (AsyncSlot* x : R.a_inflight)
                     if (!x->claimed) {
                         sl = x;
                         return true;
                     }
-                return a_launcher_done;
+                return R.a_launcher_done;
             });
             if (!sl) break;
             sl->claimed = true;
@@ -2698,17 +2843,17 @@ struct tm_engine {
             } catch (...) {
             }
             lk.lock();
-            a_inflight.erase(std::find(a_inflight.begin(), a_inflight.end(), sl));
-            a_us_wait += us_wait;
-            a_us_deliver += us_deliver;
-            ++a_batches;
-            a_recoveries += recovered ? 1 : 0;
-            a_requests += sl->calls.size();
+            R.a_inflight.erase(std::find(R.a_inflight.begin(), R.a_inflight.end(), sl));
+            R.a_us_wait += us_wait;
+            R.a_us_deliver += us_deliver;
+            ++R.a_batches;
+            R.a_recoveries += recovered ? 1 : 0;
+            R.a_requests += sl->calls.size();
             sl->calls.clear();
             sl->claimed = false;
-            a_free.push_back(sl);
-            a_work.notify_all();
-            a_done.notify_all();
+            R.a_free.push_back(sl);
+            R.a_work.notify_all();
+            R.a_done.notify_all();
         }
     }
 
@@ -2750,7 +2895,7 @@ struct tm_engine {
             tm_result r{};
             {
                 std::lock_guard<std::recursive_mutex> g(mu);
-                (void)hipSetDevice(device);
+                (void)hipSetDevice(b->rep->device);
                 rc = grow_for(b, err, need);
                 if (!rc) rc = wait(b);
                 if (!rc) rc = result(b, &r);
@@ -2772,8 +2917,8 @@ struct tm_engine {
         return false;
     }
 
-    int init(const tm_config* cfg) {
-        device = cfg ? cfg->device : -1;
+    // devices[ndev]: one replica per entry (ndev = 0: host-only engine)
+    int init(const tm_config* cfg, const int32_t* devices, uint32_t ndev) {
         frozen = cfg && (cfg->flags & TM_CFG_FROZEN_DICT);
         const char* ck = getenv("TM_CHECKED");
         checked = ck && ck[0] == '1';
@@ -2796,45 +2941,199 @@ struct tm_engine {
         for (Slot& s : slots) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
         if (cfg && cfg->init_slots) rehash(cfg->init_slots);
         dirty_mark.assign((slots.size() + 63) / 64, 0);
-        if (device >= 0) {
-            int ndev = 0;
-            if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return TM_ENODEV;
+        if (ndev) {
+            int count = 0;
+            if (hipGetDeviceCount(&count) != hipSuccess) return TM_ENODEV;
+            for (uint32_t i = 0; i < ndev; ++i)
+                if (devices[i] < 0 || devices[i] >= count) return TM_ENODEV;
+            device = devices[0];
+            for (uint32_t i = 0; i < ndev; ++i) {
+                Replica* R = new Replica();
+                R->index = i;
+                R->device = devices[i];
+                R->scratch.rep = R;
+                R->tokb.rep = R;
+                reps.push_back(R);
+                HIP_OK(hipSetDevice(R->device));
+                HIP_OK(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+                HIP_OK(hipEventCreateWithFlags(&R->ev_delta, hipEventDisableTiming));
+                HIP_OK(hipEventCreateWithFlags(&R->ev_sync, hipEventDisableTiming));
+            }
             HIP_OK(hipSetDevice(device));
-            HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-            HIP_OK(hipEventCreateWithFlags(&ev_delta, hipEventDisableTiming));
-            HIP_OK(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
         }
         return TM_OK;
     }
 
     void destroy() {
-        async_stop();
-        if (device >= 0) {
-            (void)hipSetDevice(device);
-            if (stream) (void)hipStreamSynchronize(stream);
-            scratch.release();
-            tokb.release();
-            dev_free(d_slots); dev_free(d_foff); dev_free(d_flen); dev_free(d_fbytes);
-            dev_free(d_dkey); dev_free(d_tail); dev_free(d_arena); dev_free(d_dxidx); dev_free(d_dxval);
-            if (h_dxidx) (void)hipHostFree(h_dxidx);
-            if (h_dxval) (void)hipHostFree(h_dxval);
-            dev_free(d_didx); dev_free(d_dval); dev_free(d_fidx); dev_free(d_foffv); dev_free(d_flenv);
-            dev_free(d_dbg); dev_free(d_roff); dev_free(d_rdest); dev_free(d_rl); dev_free(d_soff); dev_free(d_subs); dev_free(d_scnt); dev_free(d_sone);
-            if (h_dbg) (void)hipHostFree(h_dbg);
-            if (h_didx) (void)hipHostFree(h_didx);
-            if (h_dval) (void)hipHostFree(h_dval);
-            if (h_fidx) (void)hipHostFree(h_fidx);
-            if (h_foffv) (void)hipHostFree(h_foffv);
-            if (h_flenv) (void)hipHostFree(h_flenv);
-            if (ev_delta) (void)hipEventDestroy(ev_delta);
-            if (ev_sync) (void)hipEventDestroy(ev_sync);
-            if (stream) (void)hipStreamDestroy(stream);
+        for (Replica* R : reps) async_stop(*R);
+        for (Replica* R : reps) {
+            (void)hipSetDevice(R->device);
+            if (R->stream) (void)hipStreamSynchronize(R->stream);
+            R->scratch.release();
+            R->tokb.release();
+            dev_free(R->d_slots); dev_free(R->d_foff); dev_free(R->d_flen); dev_free(R->d_fbytes);
+            dev_free(R->d_dkey); dev_free(R->d_tail); dev_free(R->d_arena); dev_free(R->d_dxidx); dev_free(R->d_dxval);
+            dev_free(R->d_didx); dev_free(R->d_dval); dev_free(R->d_fidx); dev_free(R->d_foffv); dev_free(R->d_flenv);
+            dev_free(R->d_dbg); dev_free(R->d_roff); dev_free(R->d_rdest); dev_free(R->d_rl);
+            dev_free(R->d_soff); dev_free(R->d_subs); dev_free(R->d_scnt); dev_free(R->d_sone);
+            if (R->h_dbg) (void)hipHostFree(R->h_dbg);
+            if (R->ev_delta) (void)hipEventDestroy(R->ev_delta);
+            if (R->ev_sync) (void)hipEventDestroy(R->ev_sync);
+            if (R->stream) (void)hipStreamDestroy(R->stream);
+            delete R;
         }
+        reps.clear();
+        for (void* h : {(void*)h_dxidx, (void*)h_dxval, (void*)h_didx, (void*)h_dval, (void*)h_fidx, (void*)h_foffv,
+                        (void*)h_flenv})
+            if (h) (void)hipHostFree(h);
+        h_dxidx = nullptr; h_dxval = nullptr; h_didx = nullptr; h_dval = nullptr;
+        h_fidx = nullptr; h_foffv = nullptr; h_flenv = nullptr;
     }
 
-    int set_device() {
-        if (device < 0) return TM_ENODEV;
-        HIP_OK(hipSetDevice(device));
+    // the calling thread's HIP device := replica R's (the first one by default)
+    int use(const Replica* R = nullptr) {
+        if (reps.empty()) return TM_ENODEV;
+        HIP_OK(hipSetDevice(R ? R->device : device));
+        return TM_OK;
+    }
+    int set_device() { return use(); }
+    // the replica a call that may run anywhere takes (round-robin)
+    Replica& pick() { return *reps[rr.fetch_add(1, std::memory_order_relaxed) % reps.size()]; }
+
+    // ---- whole-batch calls over every replica: a batch is split into
+    // contiguous slices, one per replica, run concurrently (launched by one
+    // thread: every replica's work is asynchronous until the waits), and the
+    // slices' results concatenate in publish order.  No data-path collective.
+    std::vector<uint32_t> m_rowoff, m_ids, m_dests;   // merged results (valid like tm_result)
+
+    static uint32_t slice_lo(uint32_t n, size_t k, size_t i) { return (uint32_t)((uint64_t)n * i / k); }
+
+    template <class F>
+    void each_rep(F f) {
+        const size_t k = reps.size();
+        if (k == 1) { f(0); return; }
+        std::vector<std::thread> th;
+        th.reserve(k);
+        for (size_t i = 0; i < k; ++i) th.emplace_back([&f, i] { f(i); });
+        for (auto& t : th) t.join();
+    }
+
+    // prepare + launch every slice (scratch batches), then wait each
+    int run_slices(const uint8_t* topics, const uint64_t* offsets, uint32_t n) {
+        const size_t k = reps.size();
+        int rc = TM_OK;
+        upload_nosync = true;   // every slice's stream is drained by its wait below (or on failure)
+        for (size_t i = 0; i < k; ++i) {
+            Replica& R = *reps[i];
+            const uint32_t lo = slice_lo(n, k, i), hi = slice_lo(n, k, i + 1);
+            if ((rc = use(&R))) break;
+            if ((rc = prepare(&R.scratch, topics, offsets + lo, hi - lo))) break;
+            if ((rc = launch(&R.scratch))) break;
+        }
+        upload_nosync = false;
+        int first = rc;
+        for (size_t i = 0; i < k; ++i) {   // every slice is drained, even after an error
+            Replica& R = *reps[i];
+            (void)use(&R);
+            if (R.scratch.launched && !R.scratch.done) rc = wait(&R.scratch);
+            if (rc && !first) first = rc;
+            (void)hipStreamSynchronize(R.stream);
+        }
+        return first;
+    }
+
+    // tm_match_batch over every replica: merged CSR in m_rowoff / m_ids
+    int match_batch_split(const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_result* out) {
+        for (Replica* R : reps) R->scratch.launched = R->scratch.done = false;
+        int rc = run_slices(topics, offsets, n);
+        if (rc) return rc;
+        const size_t k = reps.size();
+        std::vector<tm_result> r(k);
+        uint64_t total = 0;
+        for (size_t i = 0; i < k; ++i) {
+            if ((rc = use(reps[i]))) return rc;
+            if ((rc = result(&reps[i]->scratch, &r[i]))) return rc;
+            total += r[i].n_matches;
+        }
+        if (total > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
+        m_rowoff.resize((size_t)n + 1);
+        m_ids.resize(std::max<uint64_t>(total, 1));
+        std::vector<uint64_t> base(k + 1, 0);
+        for (size_t i = 0; i < k; ++i) base[i + 1] = base[i] + r[i].n_matches;
+        each_rep([&](size_t i) {
+            const uint32_t lo = slice_lo(n, k, i), cnt = slice_lo(n, k, i + 1) - lo, add = (uint32_t)base[i];
+            for (uint32_t t = 0; t < cnt; ++t) m_rowoff[lo + t] = r[i].row_offsets[t] + add;
+            if (r[i].n_matches) memcpy(m_ids.data() + base[i], r[i].filter_ids, r[i].n_matches * sizeof(uint32_t));
+        });
+        m_rowoff[n] = (uint32_t)total;
+        out->n_topics = n;
+        out->n_matches = total;
+        out->row_offsets = m_rowoff.data();
+        out->filter_ids = m_ids.data();
+        return TM_OK;
+    }
+
+    // tm_match_routes_batch over every replica: merged route CSR
+    int match_routes_split(const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_routes* out) {
+        for (Replica* R : reps) R->scratch.launched = R->scratch.done = false;
+        int rc = run_slices(topics, offsets, n);
+        if (rc) return rc;
+        const size_t k = reps.size();
+        std::vector<tm_routes> r(k);
+        uint64_t total = 0;
+        for (size_t i = 0; i < k; ++i) {
+            if ((rc = use(reps[i]))) return rc;
+            if ((rc = batch_routes(&reps[i]->scratch, &r[i]))) return rc;
+            total += r[i].n_routes;
+        }
+        if (total > MAX_RESULT) return TM_EOVERFLOW;
+        m_rowoff.resize((size_t)n + 1);
+        m_ids.resize(std::max<uint64_t>(total, 1));
+        m_dests.resize(std::max<uint64_t>(total, 1));
+        std::vector<uint64_t> base(k + 1, 0);
+        for (size_t i = 0; i < k; ++i) base[i + 1] = base[i] + r[i].n_routes;
+        each_rep([&](size_t i) {
+            const uint32_t lo = slice_lo(n, k, i), cnt = slice_lo(n, k, i + 1) - lo, add = (uint32_t)base[i];
+            for (uint32_t t = 0; t < cnt; ++t) m_rowoff[lo + t] = r[i].row_offsets[t] + add;
+            if (r[i].n_routes) {
+                memcpy(m_ids.data() + base[i], r[i].filter_ids, r[i].n_routes * sizeof(uint32_t));
+                memcpy(m_dests.data() + base[i], r[i].dests, r[i].n_routes * sizeof(uint32_t));
+            }
+        });
+        m_rowoff[n] = (uint32_t)total;
+        out->n_topics = n;
+        out->n_routes = total;
+        out->row_offsets = m_rowoff.data();
+        out->filter_ids = m_ids.data();
+        out->dests = m_dests.data();
+        return TM_OK;
+    }
+
+    // tm_rules_match over every replica: names split, each replica writes its
+    // rows of the bitmap (disjoint)
+    int rules_match_split(const uint8_t* names, const uint64_t* noffs, uint32_t n, const uint8_t* rules,
+                          const uint64_t* roffs, uint32_t r, bool dollar_rule, uint32_t* bits) {
+        const size_t k = std::min<size_t>(reps.size(), std::max<uint32_t>(1, n / 4096));   // small: one replica
+        const uint32_t wpr = (r + 31) / 32;
+        std::vector<int> rc(k, TM_OK);
+        auto one = [&](size_t i) {
+            Replica& R = *reps[i];
+            const uint32_t lo = slice_lo(n, k, i), hi = slice_lo(n, k, i + 1);
+            if (hipSetDevice(R.device) != hipSuccess) { rc[i] = TM_EIO; return; }
+            try {
+                rc[i] = rules_match(R, names, noffs + lo, hi - lo, rules, roffs, r, dollar_rule, bits + (size_t)lo * wpr);
+            } catch (...) {
+                rc[i] = TM_ENOMEM;
+            }
+        };
+        if (k == 1) one(0);
+        else {
+            std::vector<std::thread> th;
+            for (size_t i = 0; i < k; ++i) th.emplace_back(one, i);
+            for (auto& t : th) t.join();
+        }
+        for (int x : rc)
+            if (x) return x;
         return TM_OK;
     }
 };
@@ -2884,14 +3183,43 @@ size_t utf8_char(const uint8_t* p, size_t n, uint32_t& cp) {
 
 extern "C" {
 
-int tm_create(const tm_config* cfg, tm_engine** out) {
-    if (!out) return TM_EINVAL;
+int tm_create_replicated(const tm_config* cfg, const int32_t* devices, uint32_t n_devices, tm_engine** out) {
+    if (!out || (n_devices && !devices)) return TM_EINVAL;
     if (cfg && (cfg->flags & ~(TM_CFG_FROZEN_DICT | TM_CFG_HOST_TOKENIZE))) return TM_EINVAL;
     tm_engine* e = new (std::nothrow) tm_engine();
     if (!e) return TM_ENOMEM;
-    int rc = e->init(cfg);
+    int rc;
+    try {
+        rc = e->init(cfg, devices, n_devices);
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
     if (rc) { e->destroy(); delete e; return rc; }
     *out = e;
+    return TM_OK;
+}
+
+int tm_create(const tm_config* cfg, tm_engine** out) {
+    const int32_t dev = cfg ? cfg->device : -1;
+    return tm_create_replicated(cfg, &dev, dev >= 0 ? 1u : 0u, out);
+}
+
+uint32_t tm_replica_count(tm_engine* e) { return e ? (uint32_t)e->reps.size() : 0; }
+
+int tm_async_start(tm_engine* e) {
+    if (!e) return TM_EINVAL;
+    if (e->reps.empty()) return TM_ENODEV;
+    for (Replica* R : e->reps) {
+        std::lock_guard<std::mutex> lk(R->amu);
+        if (R->a_stop) return TM_ENODEV;
+        int rc;
+        try {
+            rc = e->async_start(*R);
+        } catch (...) {
+            rc = TM_ENOMEM;
+        }
+        if (rc) return rc;
+    }
     return TM_OK;
 }
 
@@ -2915,7 +3243,12 @@ int tm_stats(tm_engine* e, tm_engine_stats* o) {
     o->filters = e->n_filters;
     o->words = e->dict.size();
     o->slots = e->slots.size();
-    o->device_bytes = e->d_nslots * sizeof(Slot) + e->c_foff * 8 + e->c_flen * 4 + e->c_fbytes;
+    if (!e->reps.empty()) {   // per replica (each device holds the same)
+        const Replica& R = *e->reps[0];
+        o->device_bytes = R.d_nslots * sizeof(Slot) + R.c_foff * 8 + R.c_flen * 4 + R.c_fbytes;
+    } else {
+        o->device_bytes = 0;
+    }
     o->uploads_full = e->uploads_full;
     o->uploads_delta = e->uploads_delta;
     o->delta_slots = e->delta_slots;
@@ -2928,9 +3261,12 @@ int tm_sync(tm_engine* e) {
     int rc = e->set_device();
     if (rc) return rc;
     if ((rc = e->sync_device())) return rc;
-    HIP_OK(hipStreamSynchronize(e->stream));
-    e->delta_inflight = false;
-    return TM_OK;
+    for (Replica* R : e->reps) {
+        HIP_OK(hipSetDevice(R->device));
+        HIP_OK(hipStreamSynchronize(R->stream));
+        R->delta_inflight = false;
+    }
+    return e->set_device();
 }
 
 int tm_trie_insert(tm_engine* e, const uint8_t* t, size_t len) {
@@ -2981,25 +3317,37 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
     std::lock_guard<std::recursive_mutex> g(e->mu);
     int rc = e->set_device();
     if (rc) return rc;
+    // a large batch is split over every replica (no collective); a small one
+    // runs on one of them, round-robin
+    if (e->reps.size() > 1 && n >= 65536) {
+        try {
+            return e->match_batch_split(topics, offsets, n, out);
+        } catch (...) {
+            return TM_ENOMEM;
+        }
+    }
+    Replica& R = e->pick();
+    if ((rc = e->use(&R))) return rc;
     // prepare's H2D of the caller's buffers is not waited for (the pipeline is,
     // below); on any early exit the stream is drained before returning, so
     // the borrowed buffers are never read after the caller frees them
     struct Drain {
         tm_engine* e;
+        Replica& R;
         bool armed = true;
         ~Drain() {
             e->upload_nosync = false;
-            if (armed) (void)hipStreamSynchronize(e->stream);
+            if (armed) (void)hipStreamSynchronize(R.stream);
         }
-    } drain{e};
+    } drain{e, R};
     try {
         e->upload_nosync = true;
-        rc = e->prepare(&e->scratch, topics, offsets, n);
+        rc = e->prepare(&R.scratch, topics, offsets, n);
         e->upload_nosync = false;
         if (rc) return rc;
-        if ((rc = e->launch(&e->scratch))) return rc;
-        if ((rc = e->wait(&e->scratch))) return rc;
-        rc = e->result(&e->scratch, out);
+        if ((rc = e->launch(&R.scratch))) return rc;
+        if ((rc = e->wait(&R.scratch))) return rc;
+        rc = e->result(&R.scratch, out);
         drain.armed = rc != TM_OK;   // result() synchronised the stream
         return rc;
     } catch (...) {
@@ -3074,42 +3422,58 @@ int tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len, uint32_t*
 
 int tm_coalesce_config(tm_engine* e, uint32_t max_batch, uint32_t linger_us, uint64_t* batches, uint64_t* requests) {
     if (!e) return TM_EINVAL;
-    std::lock_guard<std::mutex> lk(e->amu);
-    if (max_batch) e->a_max = max_batch;
-    if (linger_us != TM_NONE) e->a_linger_us = linger_us;
-    if (batches) *batches = e->a_batches;
-    if (requests) *requests = e->a_requests;
+    uint64_t nb = 0, nr = 0;
+    for (Replica* R : e->reps) {
+        std::lock_guard<std::mutex> lk(R->amu);
+        if (max_batch) R->a_max = max_batch;
+        if (linger_us != TM_NONE) R->a_linger_us = linger_us;
+        nb += R->a_batches;
+        nr += R->a_requests;
+    }
+    if (batches) *batches = nb;
+    if (requests) *requests = nr;
     return TM_OK;
 }
 
 int tm_async_stats_get(tm_engine* e, tm_async_stats* out) {
     if (!e || !out) return TM_EINVAL;
-    std::lock_guard<std::mutex> lk(e->amu);
-    out->batches = e->a_batches;
-    out->requests = e->a_requests;
-    out->recoveries = e->a_recoveries;
-    out->max_batch = e->a_max_seen;
-    out->depth = e->a_depth;
-    out->queued = (uint32_t)e->q_count.load();
-    out->us_launch = e->a_us_launch;
-    out->us_wait = e->a_us_wait;
-    out->us_deliver = e->a_us_deliver;
+    *out = tm_async_stats{};
+    for (Replica* R : e->reps) {   // summed over the replicas' pipelines
+        std::lock_guard<std::mutex> lk(R->amu);
+        out->batches += R->a_batches;
+        out->requests += R->a_requests;
+        out->recoveries += R->a_recoveries;
+        out->max_batch = std::max<uint64_t>(out->max_batch, R->a_max_seen);
+        out->depth += R->a_depth;
+        out->queued += (uint32_t)R->q_count.load();
+        out->us_launch += R->a_us_launch;
+        out->us_wait += R->a_us_wait;
+        out->us_deliver += R->a_us_deliver;
+    }
     return TM_OK;
 }
 
-int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
-                        tm_batch** out) {
+namespace {
+int prepare_on(tm_engine* e, Replica* R, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
+               tm_batch** out) {
     if (!e || !offsets || !out || (!topics && n) || (flags & ~(TM_BATCH_DEDUP | TM_BATCH_STREAM))) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    if (e->device >= 0) {
-        int rc = e->set_device();
+    const bool fresh = *out == nullptr;   // non-NULL: re-prepared in place (buffers only grow)
+    if (!fresh) {
+        if (R && (*out)->rep != R) return TM_EINVAL;   // a batch's buffers live on its replica's device
+        R = (*out)->rep;
+    } else if (!R && !e->reps.empty()) {
+        R = &e->pick();   // a fresh batch goes to the next replica, round-robin
+    }
+    if (R) {
+        int rc = e->use(R);
         if (rc) return rc;
     }
-    const bool fresh = *out == nullptr;   // non-NULL: re-prepared in place (buffers only grow)
     tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *out;
     if (!b) return TM_ENOMEM;
+    b->rep = R;
     bool made_stream = false;
-    if ((flags & TM_BATCH_STREAM) && e->device >= 0 && !b->own) {
+    if ((flags & TM_BATCH_STREAM) && R && !b->own) {
         // a stream of its own: its launches overlap other batches' (a CSR
         // pass with the next walk); trie uploads wait for it (readers)
         if (hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) != hipSuccess) {
@@ -3118,7 +3482,7 @@ int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* off
             return TM_EIO;
         }
         b->own_user = true;
-        e->readers.push_back(b);
+        R->readers.push_back(b);
         made_stream = true;
     }
     int rc;
@@ -3138,10 +3502,26 @@ int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* off
         }
         return rc;
     }
-    if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
+    if (R) HIP_OK(hipStreamSynchronize(R->stream));
     if (b->own) HIP_OK(hipStreamSynchronize(b->own));   // the caller's buffers were only borrowed
     *out = b;
     return TM_OK;
+}
+}  // namespace
+
+int tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t flags,
+                        tm_batch** out) {
+    return prepare_on(e, nullptr, topics, offsets, n, flags, out);
+}
+
+int tm_batch_prepare_on(tm_engine* e, uint32_t replica, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                        uint32_t flags, tm_batch** out) {
+    if (!e || replica >= e->reps.size()) return TM_EINVAL;
+    return prepare_on(e, e->reps[replica], topics, offsets, n, flags, out);
+}
+
+uint32_t tm_batch_replica(tm_engine* e, tm_batch* b) {
+    return (e && b && b->rep) ? b->rep->index : TM_NONE;
 }
 
 int tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_t* n_rows) {
@@ -3159,24 +3539,34 @@ int tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_
 
 int tm_batch_launch(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     return e->launch(b);
 }
 
 int tm_batch_wait(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
+    // the device wait itself runs without the engine lock, so other replicas'
+    // launches (async pipelines, other callers' batches) proceed meanwhile;
+    // the caller owns b, and wait() below finds its stream drained
+    if (b->launched && !b->done) {
+        HIP_OK(hipSetDevice(b->rep->device));
+        HIP_OK(hipStreamSynchronize(b->own ? b->own : b->rep->stream));
+    }
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     return e->wait(b);
 }
 
 int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {
     if (!e || !b || !out) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     return e->result(b, out);
 }
@@ -3207,9 +3597,9 @@ void tm_batch_free(tm_engine* e, tm_batch* b) {
     if (!b) return;
     if (e) {
         std::lock_guard<std::recursive_mutex> g(e->mu);
-        if (e->device >= 0) {
-            (void)hipSetDevice(e->device);
-            (void)hipStreamSynchronize(e->stream);
+        if (b->rep) {
+            (void)hipSetDevice(b->rep->device);
+            (void)hipStreamSynchronize(b->rep->stream);
         }
         e->forget_launch(b);
         if (b->own_user) {
@@ -3304,8 +3694,9 @@ int tm_subscriber_down(tm_engine* e, uint32_t subscriber, uint32_t node_dest, ui
 
 int tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deliveries* out) {
     if (!e || !b || !out) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     try {
         return e->batch_dispatch(b, flags, out);
@@ -3316,8 +3707,9 @@ int tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deliveries* 
 
 int tm_batch_routes(tm_engine* e, tm_batch* b, tm_routes* out) {
     if (!e || !b || !out) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     try {
         return e->batch_routes(b, out);
@@ -3332,10 +3724,13 @@ int tm_match_routes_batch(tm_engine* e, const uint8_t* topics, const uint64_t* o
     int rc = e->set_device();
     if (rc) return rc;
     try {
-        if ((rc = e->prepare(&e->scratch, topics, offsets, n))) return rc;
-        if ((rc = e->launch(&e->scratch))) return rc;
-        if ((rc = e->wait(&e->scratch))) return rc;
-        return e->batch_routes(&e->scratch, out);
+        if (e->reps.size() > 1 && n >= 65536) return e->match_routes_split(topics, offsets, n, out);
+        Replica& R = e->pick();
+        if ((rc = e->use(&R))) return rc;
+        if ((rc = e->prepare(&R.scratch, topics, offsets, n))) return rc;
+        if ((rc = e->launch(&R.scratch))) return rc;
+        if ((rc = e->wait(&R.scratch))) return rc;
+        return e->batch_routes(&R.scratch, out);
     } catch (...) {
         return TM_ENOMEM;
     }
@@ -3349,10 +3744,12 @@ int tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* name_offs
     if (rc) return rc;
     if (!n || !r) return TM_OK;
     try {
-        return e->rules_match(names, name_offsets, n, rules, rule_offsets, r, dollar_rule != 0, bits);
+        rc = e->rules_match_split(names, name_offsets, n, rules, rule_offsets, r, dollar_rule != 0, bits);
     } catch (...) {
-        return TM_ENOMEM;
+        rc = TM_ENOMEM;
     }
+    (void)e->set_device();
+    return rc;
 }
 
 int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n, uint32_t shard,
@@ -3467,6 +3864,8 @@ int tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t*
     const bool fresh = *out == nullptr;   // a non-NULL *out is reused (its buffers only grow)
     tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *out;
     if (!b) return TM_ENOMEM;
+    if (fresh) b->rep = e->reps.empty() ? nullptr : e->reps[0];   // device tokens live on the first replica's device
+    if (b->rep) (void)e->use(b->rep);
     int rc;
     try {
         rc = e->prepare_tokens(b, words, toff, tflags, n, nwords, on_device != 0);
@@ -3478,7 +3877,7 @@ int tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t*
         else b->launched = b->done = false;
         return rc;
     }
-    if (e->device >= 0) HIP_OK(hipStreamSynchronize(e->stream));
+    if (b->rep) HIP_OK(hipStreamSynchronize(b->rep->stream));
     *out = b;
     return TM_OK;
 }
@@ -3489,8 +3888,8 @@ int tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d_src_off
     std::lock_guard<std::recursive_mutex> g(e->mu);
     int rc = e->set_device();
     if (rc) return rc;
-    HIP_OK(launch_gather_rows(d_src, d_src_off, d_idx, n, d_dst_off, d_dst, e->stream));
-    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(launch_gather_rows(d_src, d_src_off, d_idx, n, d_dst_off, d_dst, e->reps[0]->stream));
+    HIP_OK(hipStreamSynchronize(e->reps[0]->stream));
     return TM_OK;
 }
 
@@ -3500,15 +3899,16 @@ int tm_tokens_shard(tm_engine* e, const uint32_t* d_words, const uint32_t* d_tof
     std::lock_guard<std::recursive_mutex> g(e->mu);
     int rc = e->set_device();
     if (rc) return rc;
-    HIP_OK(launch_tokens_shard(d_words, d_toff, n, nshards, d_shard, e->stream));
-    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(launch_tokens_shard(d_words, d_toff, n, nshards, d_shard, e->reps[0]->stream));
+    HIP_OK(hipStreamSynchronize(e->reps[0]->stream));
     return TM_OK;
 }
 
 int tm_batch_export(tm_engine* e, tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
     if (!e || !b || (!d_counts && b->n) || (!d_ids && b->total)) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    int rc = e->set_device();
+    int rc = e->use(b->rep);
     if (rc) return rc;
     return e->export_batch(b, d_counts, d_ids, mul, add);
 }

@@ -1,13 +1,17 @@
-// tm_group.cpp -- replicated multi-device matching in one process (BASELINE
-// config C3: "1M filters replicated, publish batches split across 2/4/8
-// MI355X, no collective").
+// tm_group.cpp -- the replicated multi-device group (BASELINE config C3: "1M
+// filters replicated, publish batches split across 2/4/8 MI355X, no
+// collective") as a view of ONE replicated engine.
 //
-// A group owns one engine (trie replica) per listed device.  The reference
-// keeps a full copy of the emqx_trie tables on every node
-// (src/emqx_trie.erl:53-74); here every mutation is applied to every replica
-// in the same order, so node / filter ids agree across replicas and a batch
-// split into contiguous slices (one per replica, no data-path collective)
-// concatenates back into one CSR.  Built only on the engine's public C ABI.
+// The reference keeps a full copy of the emqx_trie tables on every node
+// (src/emqx_trie.erl:53-74).  Here the group's engine holds one host trie and
+// one HBM replica per listed device (tm_create_replicated): a mutation is made
+// once on the host and its delta uploaded to every device, so node / filter
+// ids agree across devices by construction, and a batch split into contiguous
+// slices (one per replica, no data-path collective) concatenates back into one
+// CSR.  Every tm_* call on tm_group_engine(g, i) already spans the replicas
+// (per-publish calls are dealt over them, whole batches split); the tm_group_*
+// split form below keeps one slice per device explicit for callers that
+// pipeline batches themselves.  Built only on the engine's public C ABI.
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -22,68 +26,30 @@ struct tm_group_batch {
     std::vector<tm_batch*> parts;          // one per replica
     std::vector<uint32_t> row_offsets;     // merged CSR
     std::vector<uint32_t> filter_ids;
+    std::vector<uint64_t> d_rows;          // merged deliveries (tm_group_dispatch)
+    std::vector<uint32_t> d_subs;
 };
 
 struct tm_group {
-    std::vector<tm_engine*> engines;
-    std::mutex mu;                         // orders mutations: the replicas see one sequence
-    bool diverged = false;                 // a mutation returned different codes on two replicas
-    tm_group_batch* last = nullptr;        // tm_group_match_batch's batch (its CSR outlives the call)
+    tm_engine* e = nullptr;
+    std::mutex mu;                         // g->last is reused: one tm_group_match_batch at a time
+    tm_group_batch* last = nullptr;
 };
-
-namespace {
-
-// Runs f(engine index) on every replica, in parallel when there are several.
-template <class F>
-void each(tm_group* g, F f) {
-    const size_t k = g->engines.size();
-    if (k == 1) {
-        f(0);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(k);
-    for (size_t i = 0; i < k; ++i) th.emplace_back([&f, i] { f(i); });
-    for (auto& t : th) t.join();
-}
-
-// Same mutation on every replica; replicas are identical, so the codes agree.
-template <class F>
-int mutate(tm_group* g, F f) {
-    std::lock_guard<std::mutex> lk(g->mu);
-    if (g->diverged) return TM_EIO;
-    std::vector<int> rc(g->engines.size(), TM_OK);
-    each(g, [&](size_t i) { rc[i] = f(i); });
-    for (int r : rc)
-        if (r != rc[0]) {
-            g->diverged = true;
-            return TM_EIO;
-        }
-    return rc[0];
-}
-
-}  // namespace
 
 extern "C" {
 
 int tm_group_create(const int32_t* devices, uint32_t n, const tm_config* cfg, tm_group** out) {
     if (!devices || !n || !out) return TM_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (devices[i] < 0) return TM_EINVAL;
     tm_group* g = new (std::nothrow) tm_group();
     if (!g) return TM_ENOMEM;
-    for (uint32_t i = 0; i < n; ++i) {
-        tm_config c = cfg ? *cfg : tm_config{0, 0, 0, 0};
-        c.device = devices[i];
-        if (c.device < 0) {
-            tm_group_destroy(g);
-            return TM_EINVAL;
-        }
-        tm_engine* e = nullptr;
-        int rc = tm_create(&c, &e);
-        if (rc) {
-            tm_group_destroy(g);
-            return rc;
-        }
-        g->engines.push_back(e);
+    tm_config c = cfg ? *cfg : tm_config{0, 0, 0, 0};
+    c.device = devices[0];
+    int rc = tm_create_replicated(&c, devices, n, &g->e);
+    if (rc) {
+        delete g;
+        return rc;
     }
     *out = g;
     return TM_OK;
@@ -92,57 +58,40 @@ int tm_group_create(const int32_t* devices, uint32_t n, const tm_config* cfg, tm
 void tm_group_destroy(tm_group* g) {
     if (!g) return;
     if (g->last) tm_group_batch_free(g, g->last);
-    for (tm_engine* e : g->engines) tm_destroy(e);
+    tm_destroy(g->e);
     delete g;
 }
 
-uint32_t tm_group_size(tm_group* g) { return g ? (uint32_t)g->engines.size() : 0; }
+uint32_t tm_group_size(tm_group* g) { return g ? tm_replica_count(g->e) : 0; }
 
 tm_engine* tm_group_engine(tm_group* g, uint32_t i) {
-    return (g && i < g->engines.size()) ? g->engines[i] : nullptr;
+    return (g && i < tm_replica_count(g->e)) ? g->e : nullptr;
 }
 
 int tm_group_trie_insert(tm_group* g, const uint8_t* t, size_t len) {
-    if (!g) return TM_EINVAL;
-    return mutate(g, [&](size_t i) { return tm_trie_insert(g->engines[i], t, len); });
+    return g ? tm_trie_insert(g->e, t, len) : TM_EINVAL;
 }
 
 int tm_group_trie_delete(tm_group* g, const uint8_t* t, size_t len) {
-    if (!g) return TM_EINVAL;
-    return mutate(g, [&](size_t i) { return tm_trie_delete(g->engines[i], t, len); });
+    return g ? tm_trie_delete(g->e, t, len) : TM_EINVAL;
 }
 
 int tm_group_insert_many(tm_group* g, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                          uint64_t* n_inserted) {
-    if (!g) return TM_EINVAL;
-    std::vector<uint64_t> done(g->engines.size(), 0);
-    int rc = mutate(g, [&](size_t i) { return tm_trie_insert_many(g->engines[i], filters, offsets, n, 0, 1, &done[i]); });
-    if (n_inserted) *n_inserted = done[0];
-    return rc;
+    return g ? tm_trie_insert_many(g->e, filters, offsets, n, 0, 1, n_inserted) : TM_EINVAL;
 }
 
 int tm_group_route_apply(tm_group* g, const uint8_t* topics, const uint64_t* offsets, const uint32_t* dests,
                          const uint8_t* ops, uint32_t n, uint64_t* n_changed) {
-    if (!g) return TM_EINVAL;
-    std::vector<uint64_t> ch(g->engines.size(), 0);
-    int rc = mutate(g, [&](size_t i) { return tm_route_apply(g->engines[i], topics, offsets, dests, ops, n, &ch[i]); });
-    if (n_changed) *n_changed = ch[0];
-    return rc;
+    return g ? tm_route_apply(g->e, topics, offsets, dests, ops, n, n_changed) : TM_EINVAL;
 }
 
-int tm_group_sync(tm_group* g) {
-    if (!g) return TM_EINVAL;
-    std::vector<int> rc(g->engines.size(), TM_OK);
-    each(g, [&](size_t i) { rc[i] = tm_sync(g->engines[i]); });
-    for (int r : rc)
-        if (r) return r;
-    return TM_OK;
-}
+int tm_group_sync(tm_group* g) { return g ? tm_sync(g->e) : TM_EINVAL; }
 
 int tm_group_prepare(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                      tm_group_batch** out) {
     if (!g || !offsets || !out || (!topics && n)) return TM_EINVAL;
-    const size_t k = g->engines.size();
+    const size_t k = tm_replica_count(g->e);
     const bool fresh = *out == nullptr;
     tm_group_batch* b = fresh ? new (std::nothrow) tm_group_batch() : *out;
     if (!b) return TM_ENOMEM;
@@ -150,16 +99,14 @@ int tm_group_prepare(tm_group* g, const uint8_t* topics, const uint64_t* offsets
     b->n = n;
     b->lo.assign(k + 1, 0);
     for (size_t i = 0; i <= k; ++i) b->lo[i] = (uint32_t)((uint64_t)n * i / k);
-    std::vector<int> rc(k, TM_OK);
-    each(g, [&](size_t i) {
+    for (size_t i = 0; i < k; ++i) {
         const uint32_t lo = b->lo[i], cnt = b->lo[i + 1] - lo;
-        rc[i] = tm_batch_prepare(g->engines[i], topics, offsets + lo, cnt, &b->parts[i]);
-    });
-    for (int r : rc)
-        if (r) {
+        int rc = tm_batch_prepare_on(g->e, (uint32_t)i, topics, offsets + lo, cnt, 0, &b->parts[i]);
+        if (rc) {
             if (fresh) tm_group_batch_free(g, b);
-            return r;
+            return rc;
         }
+    }
     b->row_offsets.clear();
     b->filter_ids.clear();
     *out = b;
@@ -167,34 +114,33 @@ int tm_group_prepare(tm_group* g, const uint8_t* topics, const uint64_t* offsets
 }
 
 int tm_group_launch(tm_group* g, tm_group_batch* b) {
-    if (!g || !b || b->parts.size() != g->engines.size()) return TM_EINVAL;
-    // launches are asynchronous (one stream per replica): one thread issues all
-    for (size_t i = 0; i < g->engines.size(); ++i) {
-        int rc = tm_batch_launch(g->engines[i], b->parts[i]);
+    if (!g || !b || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
+    // launches are asynchronous (each replica's stream): one thread issues all
+    for (tm_batch* p : b->parts) {
+        int rc = tm_batch_launch(g->e, p);
         if (rc) return rc;
     }
     return TM_OK;
 }
 
 int tm_group_wait(tm_group* g, tm_group_batch* b) {
-    if (!g || !b || b->parts.size() != g->engines.size()) return TM_EINVAL;
+    if (!g || !b || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
     int first = TM_OK;
-    for (size_t i = 0; i < g->engines.size(); ++i) {   // every slice is drained, even after an error
-        int rc = tm_batch_wait(g->engines[i], b->parts[i]);
+    for (tm_batch* p : b->parts) {   // every slice is drained, even after an error
+        int rc = tm_batch_wait(g->e, p);
         if (rc && !first) first = rc;
     }
     return first;
 }
 
 int tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out) {
-    if (!g || !b || !out || b->parts.size() != g->engines.size()) return TM_EINVAL;
-    const size_t k = g->engines.size();
+    if (!g || !b || !out || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
+    const size_t k = b->parts.size();
     std::vector<tm_result> r(k);
-    std::vector<int> rc(k, TM_OK);
-    each(g, [&](size_t i) { rc[i] = tm_batch_result(g->engines[i], b->parts[i], &r[i]); });
     uint64_t total = 0;
     for (size_t i = 0; i < k; ++i) {
-        if (rc[i]) return rc[i];
+        int rc = tm_batch_result(g->e, b->parts[i], &r[i]);
+        if (rc) return rc;
         total += r[i].n_matches;
     }
     if (total > 0xFFFFFFF0ull) return TM_EOVERFLOW;   // u32 CSR offsets
@@ -202,12 +148,15 @@ int tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out) {
     b->filter_ids.resize(std::max<uint64_t>(total, 1));
     std::vector<uint64_t> base(k + 1, 0);
     for (size_t i = 0; i < k; ++i) base[i + 1] = base[i] + r[i].n_matches;
-    each(g, [&](size_t i) {
-        const uint32_t lo = b->lo[i], cnt = b->lo[i + 1] - lo, add = (uint32_t)base[i];
-        for (uint32_t t = 0; t < cnt; ++t) b->row_offsets[lo + t] = r[i].row_offsets[t] + add;
-        if (r[i].n_matches)
-            memcpy(b->filter_ids.data() + base[i], r[i].filter_ids, r[i].n_matches * sizeof(uint32_t));
-    });
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < k; ++i)
+        th.emplace_back([&, i] {
+            const uint32_t lo = b->lo[i], cnt = b->lo[i + 1] - lo, add = (uint32_t)base[i];
+            for (uint32_t t = 0; t < cnt; ++t) b->row_offsets[lo + t] = r[i].row_offsets[t] + add;
+            if (r[i].n_matches)
+                memcpy(b->filter_ids.data() + base[i], r[i].filter_ids, r[i].n_matches * sizeof(uint32_t));
+        });
+    for (auto& t : th) t.join();
     b->row_offsets[b->n] = (uint32_t)total;
     out->n_topics = b->n;
     out->n_matches = total;
@@ -216,12 +165,46 @@ int tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out) {
     return TM_OK;
 }
 
+int tm_group_dispatch(tm_group* g, tm_group_batch* b, tm_deliveries* out) {
+    if (!g || !b || !out || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
+    const size_t k = b->parts.size();
+    std::vector<tm_deliveries> d(k);
+    uint64_t total = 0, nm = 0;
+    float fill = 0.f;
+    for (size_t i = 0; i < k; ++i) {
+        int rc = tm_batch_dispatch(g->e, b->parts[i], 0, &d[i]);
+        if (rc) return rc;
+        total += d[i].n_deliveries;
+        nm += d[i].n_matches;
+        fill = std::max(fill, d[i].fill_ms);
+    }
+    b->d_rows.resize((size_t)b->n + 1);
+    b->d_subs.resize(std::max<uint64_t>(total, 1));
+    uint64_t base = 0;
+    for (size_t i = 0; i < k; ++i) {
+        const uint32_t lo = b->lo[i], cnt = b->lo[i + 1] - lo;
+        for (uint32_t t = 0; t < cnt; ++t) b->d_rows[lo + t] = d[i].row_offsets[t] + base;
+        if (d[i].n_deliveries)
+            memcpy(b->d_subs.data() + base, d[i].subscribers, d[i].n_deliveries * sizeof(uint32_t));
+        base += d[i].n_deliveries;
+    }
+    b->d_rows[b->n] = total;
+    out->n_topics = b->n;
+    out->n_matches = nm;
+    out->n_deliveries = total;
+    out->row_offsets = b->d_rows.data();
+    out->match_offsets = nullptr;
+    out->subscribers = b->d_subs.data();
+    out->fill_ms = fill;
+    return TM_OK;
+}
+
 int tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out) {
-    if (!g || !b || !out || b->parts.size() != g->engines.size()) return TM_EINVAL;
+    if (!g || !b || !out || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
     tm_batch_stats s{};
-    for (size_t i = 0; i < g->engines.size(); ++i) {
+    for (tm_batch* part : b->parts) {
         tm_batch_stats p{};
-        int rc = tm_batch_stats_get(g->engines[i], b->parts[i], &p);
+        int rc = tm_batch_stats_get(g->e, part, &p);
         if (rc) return rc;
         s.topics += p.topics; s.visits += p.visits; s.hash_hits += p.hash_hits; s.words += p.words;
         s.matches += p.matches; s.slow_topics += p.slow_topics; s.overflow_tiles += p.overflow_tiles;
@@ -236,8 +219,8 @@ int tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out) {
 
 void tm_group_batch_free(tm_group* g, tm_group_batch* b) {
     if (!b) return;
-    for (size_t i = 0; i < b->parts.size(); ++i)
-        if (b->parts[i]) tm_batch_free(g && i < g->engines.size() ? g->engines[i] : nullptr, b->parts[i]);
+    for (tm_batch* p : b->parts)
+        if (p) tm_batch_free(g ? g->e : nullptr, p);
     delete b;
 }
 
@@ -248,6 +231,26 @@ int tm_group_match_batch(tm_group* g, const uint8_t* topics, const uint64_t* off
     if (rc) return rc;
     if (!(rc = tm_group_launch(g, g->last)) && !(rc = tm_group_wait(g, g->last))) rc = tm_group_result(g, g->last, out);
     return rc;
+}
+
+int tm_group_match_async(tm_group* g, const uint8_t* topic, size_t len, tm_match_cb cb, void* ctx) {
+    return g ? tm_match_async(g->e, topic, len, cb, ctx) : TM_EINVAL;
+}
+
+int tm_group_match_coalesced(tm_group* g, const uint8_t* topic, size_t len, uint32_t* ids, uint32_t cap,
+                             uint32_t* n_out) {
+    return g ? tm_match_coalesced(g->e, topic, len, ids, cap, n_out) : TM_EINVAL;
+}
+
+int tm_group_match_routes_batch(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                tm_routes* out) {
+    return g ? tm_match_routes_batch(g->e, topics, offsets, n, out) : TM_EINVAL;
+}
+
+int tm_group_rules_match(tm_group* g, const uint8_t* names, const uint64_t* name_offsets, uint32_t n,
+                         const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule,
+                         uint32_t* bits) {
+    return g ? tm_rules_match(g->e, names, name_offsets, n, rules, rule_offsets, r, dollar_rule, bits) : TM_EINVAL;
 }
 
 }  // extern "C"

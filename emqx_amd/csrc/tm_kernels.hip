@@ -231,7 +231,11 @@ __device__ __forceinline__ void emit_row(const MatchArgs& a, unsigned long long*
 #else
     if (slot < a.row_cap) {
 #endif
+#ifdef TM_EXPERIMENT_EMIT_HOT   // timing only: same stores, 4 slots per topic (L2-resident rows)
+        const uint32_t i = tl * a.row_cap + (slot & 3);
+#else
         const uint32_t i = tl * a.row_cap + slot;   // < tile_topics * K <= 2^16
+#endif
         if (CK) (void)CK_((uint64_t)blockIdx.x * a.tile_topics * a.row_cap + i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13);
         wrows[i] = (key & KEY_MASK) | fid;
     }

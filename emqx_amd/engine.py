@@ -1,6 +1,8 @@
-"""Pythonic wrapper of one tm_engine (one trie replica on one MI355X).
+"""Pythonic wrapper of one tm_engine (one host trie mirrored into an HBM
+replica on each of its MI355X devices).
 
-    eng = Engine(device=0)
+    eng = Engine(device=0)                       # one GPU
+    eng = Engine(devices=[0, 1, 2, 3])           # one engine over four GPUs
     eng.insert(b"sensor/+/#")
     eng.match(b"sensor/1/temp")                  # -> [b"sensor/+/#"]
     offs, ids = eng.match_batch(topics)          # CSR over a whole batch
@@ -40,7 +42,7 @@ class Tokens:
 class Batch:
     """A device-resident publish batch (tm_batch_prepare / launch / wait / result)."""
 
-    def __init__(self, eng: "Engine", topics=None, handle=None, n=0, dedup=False, stream=False):
+    def __init__(self, eng: "Engine", topics=None, handle=None, n=0, dedup=False, stream=False, replica=None):
         self.eng = eng
         if handle is not None:          # built by Engine.prepare_tokens
             self.h = handle
@@ -53,9 +55,17 @@ class Batch:
         self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
         h = C.c_void_p()
         flags = (N.TM_BATCH_DEDUP if dedup else 0) | (N.TM_BATCH_STREAM if stream else 0)
-        N.check(eng.L.tm_batch_prepare_ex(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
-                                          flags, C.byref(h)), "tm_batch_prepare_ex")
+        if replica is None:
+            N.check(eng.L.tm_batch_prepare_ex(eng.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
+                                              flags, C.byref(h)), "tm_batch_prepare_ex")
+        else:
+            N.check(eng.L.tm_batch_prepare_on(eng.h, replica, self._buf.ctypes.data, self._offs.ctypes.data,
+                                              self.n, flags, C.byref(h)), "tm_batch_prepare_on")
         self.h = h
+
+    @property
+    def replica(self) -> int:
+        return int(self.eng.L.tm_batch_replica(self.eng.h, self.h))
 
     def row_map(self):
         """-> (row_of uint32[n publishes], n_rows): result row of every publish."""
@@ -187,6 +197,15 @@ class GroupBatch:
         N.check(self.grp.L.tm_group_result(self.grp.h, self.h, C.byref(r)), "tm_group_result")
         return _result_arrays(r)
 
+    def dispatch(self):
+        """tm_group_dispatch -> (row_offsets u64[n+1], subscribers u32[deliveries])."""
+        d = N.Deliveries()
+        N.check(self.grp.L.tm_group_dispatch(self.grp.h, self.h, C.byref(d)), "tm_group_dispatch")
+        n, t = d.n_topics, int(d.n_deliveries)
+        offs = np.ctypeslib.as_array(d.row_offsets, shape=(n + 1,)).copy()
+        subs = np.ctypeslib.as_array(d.subscribers, shape=(t,)).copy() if t else np.zeros(0, np.uint32)
+        return offs, subs
+
     def stats(self) -> dict:
         st = N.BatchStats()
         N.check(self.grp.L.tm_group_batch_stats(self.grp.h, self.h, C.byref(st)), "tm_group_batch_stats")
@@ -206,8 +225,9 @@ class GroupBatch:
 
 class Group:
     """Replicated multi-device matching in one process (tm_group_*, config C3):
-    one trie replica per listed device, mutations applied to all, batches split
-    into one contiguous slice per replica."""
+    a view of one replicated engine -- one host trie, one HBM replica per
+    listed device, a mutation made once and uploaded to every replica, batches
+    split into one contiguous slice per replica."""
 
     def __init__(self, devices, host_threads: int = 0):
         self.L = N.lib()
@@ -264,6 +284,11 @@ class Group:
     def prepare(self, topics) -> GroupBatch:
         return GroupBatch(self, topics)
 
+    def engine(self) -> "Engine":
+        """The group's engine (every tm_* call on it spans the replicas); the
+        Group keeps ownership."""
+        return Engine._borrow(self.L.tm_group_engine(self.h, 0), self.devices)
+
     def match_batch(self, topics):
         s = _pack(topics)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
@@ -284,18 +309,40 @@ class Group:
 
 class Engine:
     def __init__(self, device: int = 0, init_slots: int = 0, host_threads: int = 0, frozen_dict: bool = False,
-                 host_tokenize: bool = False):
+                 host_tokenize: bool = False, devices=None):
         self.L = N.lib()
         flags = (N.TM_CFG_FROZEN_DICT if frozen_dict else 0) | (N.TM_CFG_HOST_TOKENIZE if host_tokenize else 0)
         cfg = N.Config(device, init_slots, host_threads, flags)
         h = C.c_void_p()
-        N.check(self.L.tm_create(C.byref(cfg), C.byref(h)), "tm_create")
+        self._owned = True
+        if devices is None:
+            N.check(self.L.tm_create(C.byref(cfg), C.byref(h)), "tm_create")
+            self.devices = [device] if device >= 0 else []
+        else:
+            devs = (C.c_int32 * max(len(devices), 1))(*devices)
+            N.check(self.L.tm_create_replicated(C.byref(cfg), devs, len(devices), C.byref(h)), "tm_create_replicated")
+            self.devices = list(devices)
         self.h = h
-        self.device = device
+        self.device = self.devices[0] if self.devices else -1
+
+    @classmethod
+    def _borrow(cls, handle, devices) -> "Engine":
+        e = cls.__new__(cls)
+        e.L, e.h, e._owned = N.lib(), C.c_void_p(handle), False
+        e.devices, e.device = list(devices), devices[0]
+        return e
+
+    @property
+    def replicas(self) -> int:
+        return int(self.L.tm_replica_count(self.h))
+
+    def async_start(self):
+        N.check(self.L.tm_async_start(self.h), "tm_async_start")
 
     def close(self):
         if getattr(self, "h", None):
-            self.L.tm_destroy(self.h)
+            if getattr(self, "_owned", True):
+                self.L.tm_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -392,11 +439,12 @@ class Engine:
                 "tm_match_batch")
         return _result_arrays(r)
 
-    def prepare(self, topics, dedup: bool = False, stream: bool = False) -> Batch:
+    def prepare(self, topics, dedup: bool = False, stream: bool = False, replica=None) -> Batch:
         """Device-resident batch; dedup=True matches identical topics once (TM_BATCH_DEDUP);
         stream=True gives it a HIP stream of its own, so launches of several
-        batches overlap on the device (TM_BATCH_STREAM)."""
-        return Batch(self, topics, dedup=dedup, stream=stream)
+        batches overlap on the device (TM_BATCH_STREAM); replica = the device
+        replica it runs on (default: the next one, round-robin)."""
+        return Batch(self, topics, dedup=dedup, stream=stream, replica=replica)
 
     # ---- routes (emqx_router + emqx_broker:aggre/1) -------------------------
     def route_add(self, topic: bytes, dest: int):

@@ -11,11 +11,13 @@
  *   - plain pointers + sizes; caller-owned inputs are borrowed for the call;
  *   - return codes: 0 = ok, negative errno-style values (TM_E*) on error;
  *     predicates return 0/1; no C++ exceptions cross this boundary;
- *   - one engine = one trie replica on one HIP device.  Calls on one engine are
- *     serialised by an internal mutex (readers and the single writer of the
- *     reference's mnesia tables become ordered operations on one HIP stream, so
- *     a match issued after tm_trie_insert returns always sees the filter:
- *     read-your-writes, src/emqx_broker.erl:150-158).
+ *   - one engine = one host trie mirrored into one HBM replica per device it
+ *     was created on (tm_create: one device; tm_create_replicated: a list).
+ *     Calls on one engine are serialised by an internal mutex (readers and the
+ *     single writer of the reference's mnesia tables become ordered operations
+ *     on each replica's HIP stream, so a match issued after tm_trie_insert
+ *     returns always sees the filter on every device: read-your-writes,
+ *     src/emqx_broker.erl:150-158).
  */
 #ifndef EMQX_TM_H
 #define EMQX_TM_H
@@ -113,6 +115,25 @@ typedef struct {
 
 /* ---- engine ---------------------------------------------------------- */
 TM_API int  tm_create(const tm_config* cfg, tm_engine** out);
+/* One engine over several devices (a node's GPUs): every node of the
+ * reference cluster holds the whole emqx_trie (src/emqx_trie.erl:53-74), so
+ * the engine keeps ONE host trie and an HBM replica of it on each listed
+ * device (a device may be listed twice); cfg->device is ignored.  A mutation
+ * is made once and its delta uploaded to every replica, so filter ids are the
+ * same everywhere.  Per-publish calls (tm_match_async / tm_match_coalesced)
+ * are dealt over the replicas; whole-batch calls (tm_match_batch,
+ * tm_match_routes_batch, tm_rules_match) of 65,536+ publishes are split into
+ * one contiguous slice per replica and their results concatenated (no
+ * collective); a fresh tm_batch goes to the next replica round-robin, or to
+ * the one named by tm_batch_prepare_on.  n_devices = 0: host-only engine. */
+TM_API int  tm_create_replicated(const tm_config* cfg, const int32_t* devices, uint32_t n_devices,
+                                 tm_engine** out);
+/* Number of device replicas (0 for a host-only engine). */
+TM_API uint32_t tm_replica_count(tm_engine* e);
+/* Starts the async pipeline (tm_match_async) of every replica now instead of
+ * at the first call -- a NIF calls it from new/1, which runs on a dirty
+ * scheduler, so the first match_async/3 never pays thread and stream setup. */
+TM_API int  tm_async_start(tm_engine* e);
 TM_API void tm_destroy(tm_engine* e);
 TM_API uint64_t tm_version(tm_engine* e);
 TM_API int  tm_stats(tm_engine* e, tm_engine_stats* out);
@@ -215,6 +236,12 @@ TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t
 #define TM_BATCH_STREAM 2u
 TM_API int  tm_batch_prepare_ex(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                 uint32_t flags, tm_batch** out);
+/* tm_batch_prepare_ex on replica `replica` (< tm_replica_count) of the engine.
+ * A batch stays on the replica it was created on (re-preparing it on another
+ * is TM_EINVAL); tm_batch_replica names it. */
+TM_API int  tm_batch_prepare_on(tm_engine* e, uint32_t replica, const uint8_t* topics, const uint64_t* offsets,
+                                uint32_t n, uint32_t flags, tm_batch** out);
+TM_API uint32_t tm_batch_replica(tm_engine* e, tm_batch* b);
 /* row_of[i] = result row of publish i (identity for batches without
  * TM_BATCH_DEDUP); *n_rows = number of result rows.  Engine-owned memory,
  * valid until the batch is re-prepared or freed. */
@@ -436,13 +463,14 @@ TM_API int  tm_rules_match(tm_engine* e, const uint8_t* names, const uint64_t* n
                            uint32_t* bits);
 
 /* ---- replicated multi-device group (BASELINE config C3) --------------- */
-/* One process drives one trie replica per listed device (a device may be
- * listed twice: two replicas on one GPU).  Every mutation is applied to every
- * replica in the same order, so node / filter ids are identical everywhere
- * (the reference replicates emqx_trie to every node the same way,
- * src/emqx_trie.erl:53-74); a publish batch is split into contiguous slices,
- * one per replica, matched concurrently with no collective, and the slices'
- * CSRs concatenate into the batch's CSR. */
+/* A view of one tm_create_replicated engine (tm_group_engine(g, i) returns it
+ * for every i < tm_group_size): one host trie, one HBM replica per listed
+ * device (a device may be listed twice: two replicas on one GPU), so node /
+ * filter ids are identical everywhere (the reference replicates emqx_trie to
+ * every node, src/emqx_trie.erl:53-74).  The split form keeps one slice per
+ * replica explicit: a publish batch is split into contiguous slices matched
+ * concurrently with no collective, and the slices' CSRs concatenate into the
+ * batch's CSR. */
 typedef struct tm_group tm_group;
 typedef struct tm_group_batch tm_group_batch;
 TM_API int  tm_group_create(const int32_t* devices, uint32_t n_devices, const tm_config* cfg, tm_group** out);
@@ -471,6 +499,20 @@ TM_API void tm_group_batch_free(tm_group* g, tm_group_batch* b);
 /* prepare + launch + wait + result in one call. */
 TM_API int  tm_group_match_batch(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                  tm_result* out);
+/* Deliveries of a waited group batch (tm_batch_dispatch per slice, merged in
+ * publish order into group-owned memory valid like tm_group_result's). */
+TM_API int  tm_group_dispatch(tm_group* g, tm_group_batch* b, tm_deliveries* out);
+/* The per-publish and whole-batch calls of the group's engine (each spans the
+ * replicas, see tm_create_replicated): tm_match_async, tm_match_coalesced,
+ * tm_match_routes_batch, tm_rules_match. */
+TM_API int  tm_group_match_async(tm_group* g, const uint8_t* topic, size_t len, tm_match_cb cb, void* ctx);
+TM_API int  tm_group_match_coalesced(tm_group* g, const uint8_t* topic, size_t len, uint32_t* ids, uint32_t cap,
+                                     uint32_t* n_out);
+TM_API int  tm_group_match_routes_batch(tm_group* g, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                        tm_routes* out);
+TM_API int  tm_group_rules_match(tm_group* g, const uint8_t* names, const uint64_t* name_offsets, uint32_t n,
+                                 const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule,
+                                 uint32_t* bits);
 
 /* ---- diagnostics ------------------------------------------------------ */
 /* Consistency check of the host edge hash (tests): slots of a bucket filled

@@ -37,6 +37,7 @@ typedef struct {
     int num_of_funcs;
     ErlNifFunc* funcs;
     int (*load)(ErlNifEnv*, void**, ERL_NIF_TERM);
+    void (*unload)(ErlNifEnv*, void*);
 } ErlNifEntry;
 
 #define ERL_NIF_DIRTY_JOB_CPU_BOUND 1
@@ -44,7 +45,7 @@ typedef struct {
 
 #define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                                      \
     ErlNifEntry* nif_init(void) {                                                                     \
-        static ErlNifEntry entry = {#NAME, (int)(sizeof(FUNCS) / sizeof(FUNCS[0])), FUNCS, LOAD};    \
+        static ErlNifEntry entry = {#NAME, (int)(sizeof(FUNCS) / sizeof(FUNCS[0])), FUNCS, LOAD, UNLOAD}; \
         return &entry;                                                                                \
     }
 

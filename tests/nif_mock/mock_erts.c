@@ -297,6 +297,11 @@ API int mock_load(void) {
     return rc;
 }
 
+API void mock_unload(void) {
+    ErlNifEntry* en = nif_init();
+    if (en->unload) en->unload(NULL, NULL);
+}
+
 /* flags of the NIF (its scheduler class), -1 if absent */
 API int mock_nif_flags(const char* name, unsigned arity) {
     ErlNifEntry* en = nif_init();
