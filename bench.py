@@ -289,6 +289,82 @@ def run_c4(args, ws, rank, local, pg):
         pg.destroy_process_group()
 
 
+def run_c4_group(args):
+    """Config C4 in ONE process (tm_sharded_*, no torch, no collective): the IoT
+    filters partitioned over shard engines on the listed devices (default
+    0..N-1; 0,0 rehearses two shards on one GPU), one batch of --topics
+    publishes per shard.  One step = owner per publish + device partition by
+    owner + every shard matching its part + rows restored to publish order, all
+    in HBM (tm_sharded_run)."""
+    from emqx_amd import gen
+    from emqx_amd.engine import ShardedGroup
+
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    G = len(devs)
+    p = gen.IotParams(n_filters=args.c4_filters) if args.c4_filters else gen.C4
+    t0 = time.time()
+    grp = ShardedGroup(devs)
+    grp.dict_load(gen.gen_iot_vocab(p))
+    inserted = 0
+    chunk = 5_000_000
+    for lo in range(0, p.n_filters, chunk):
+        inserted += grp.insert_many(gen.gen_iot_filters(p, lo, min(p.n_filters, lo + chunk)))
+        log(f"[c4 group] filters {min(p.n_filters, lo + chunk)}/{p.n_filters} over {G} shard(s), "
+            f"{time.time() - t0:.0f}s")
+    n = args.topics * G
+    parts = [gen.gen_iot_topics(p, 4000 + k, args.topics) for k in range(G)]
+    topics = gen.Strings.concat(parts) if G > 1 else parts[0]
+    del parts
+    b = grp.prepare(topics)
+    del topics
+    for _ in range(max(args.warmup, 1)):
+        b.run()
+    ms_match, phases = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.run()
+        st = b.stats()
+        ms_match.append(st["ms_match"])
+        phases.append((st["ms_partition"], st["ms_parts"], st["ms_unpartition"]))
+    elapsed = time.perf_counter() - t0
+    st = b.stats()
+    alg_bytes = (ALG_BYTES_PER_VISIT * (st["visits"] + st["hash_hits"]) + 4 * st["words"]
+                 + 4 * st["matches"] + 4 * st["topics"]) / G      # per shard (device)
+    k_ms = float(np.mean(ms_match))                                 # slowest part per step
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    ph = np.mean(np.array(phases), 0).tolist()
+    out = {
+        "metric": "publishes matched/sec (node) at 100M IoT filters, filter-sharded",
+        "value": n * args.steps / elapsed,
+        "unit": "publishes/s",
+        "n_gpus": len(set(devs)),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded IoT generator, SURVEY.md §8d C4)",
+        "config": {"workload": f"C4: {p.n_filters} IoT filters sharded over {G} shard(s) on devices {devs}, "
+                               f"{args.topics} publishes per shard, one process (tm_sharded)", "filters": p.n_filters,
+                   "filters_inserted_over_shards": inserted, "mode": "filter-sharded, in-process",
+                   "parallelism": f"filters sharded x{G}, device partition by owner (no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("C4", args.topics, p.n_filters) if G == 1
+                     else None, "kernel": "tm_match_tiles", "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes,
+                     "per_publish": {k: st[v] / max(st["topics"], 1) for k, v in
+                                     (("V", "visits"), ("H", "hash_hits"), ("d", "words"), ("M", "matches"))}},
+        "matches_per_step": st["matches"],
+        "device_match_ms": k_ms,
+        "phase_ms": {"partition": ph[0], "parts": ph[1], "unpartition": ph[2]},
+        "part_topics": st["part_topics"],
+    }
+    b.free()
+    grp.close()
+    print(json.dumps(out), flush=True)
+
+
 def run_c5(args, ws, rank, local, sync):
     """Config C5: 10k hot topics take 90% of the publishes, each matched by ~K
     filters derived from it (+ 100k background C2-style filters); one step =
@@ -670,6 +746,8 @@ def main():
     if ws > 1 and ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {ws}; using WORLD_SIZE")
     pg = None
+    if ws == 1 and args.workload == "c4":
+        return run_c4_group(args)   # one process, torch-free (tm_sharded)
     if ws > 1 and args.workload == "c4":
         # the filter-sharded exchange is RCCL: torch (and its HIP runtime) is
         # initialised before the engine library loads, so both share one runtime

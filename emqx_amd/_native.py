@@ -98,6 +98,11 @@ class AsyncStats(C.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class ShardedStats(C.Structure):
+    _fields_ = [("match", BatchStats), ("ms_partition", C.c_float), ("ms_parts", C.c_float),
+                ("ms_unpartition", C.c_float), ("part_topics", C.c_uint32 * 64)]
+
+
 # void (*tm_match_cb)(void* ctx, int rc, const uint32_t* ids, uint32_t n)
 MATCH_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(C.c_uint32), C.c_uint32)
 
@@ -184,6 +189,21 @@ SIGNATURES = {
     "tm_group_match_coalesced": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_group_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
     "tm_group_rules_match": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P]),
+    "tm_sharded_create": (C.c_int, [P, C.c_uint32, C.POINTER(Config), C.POINTER(P)]),
+    "tm_sharded_destroy": (None, [P]),
+    "tm_sharded_size": (C.c_uint32, [P]),
+    "tm_sharded_engine": (P, [P, C.c_uint32]),
+    "tm_sharded_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
+    "tm_sharded_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_sharded_delete_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_sharded_prepare": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(P)]),
+    "tm_sharded_run": (C.c_int, [P, P]),
+    "tm_sharded_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_sharded_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
+    "tm_sharded_batch_stats": (C.c_int, [P, P, C.POINTER(ShardedStats)]),
+    "tm_sharded_batch_free": (None, [P, P]),
+    "tm_sharded_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_sharded_filter_copy": (C.c_int, [P, C.c_uint32, P, SZ, C.POINTER(SZ)]),
     "tm_debug_check": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),

@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
-TM_SOURCES = ["tm_engine.cpp", "tm_group.cpp", "tm_kernels.hip"]
+TM_SOURCES = ["tm_engine.cpp", "tm_group.cpp", "tm_shard.cpp", "tm_kernels.hip"]
 TM_HEADERS = ["tm_internal.hpp", os.path.join("..", "..", "include", "emqx_tm.h")]
 
 

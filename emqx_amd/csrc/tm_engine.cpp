@@ -4061,6 +4061,12 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
 
 const char* tm_last_error(void) { return last_error(); }
 
+}  // extern "C"
+
+char* etm::error_buf() { return last_error(); }
+
+extern "C" {
+
 int tm_device_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;

@@ -251,6 +251,9 @@ struct RulesArgs {
     uint32_t* bits;
 };
 
+// text of the last TM_EIO on this thread (tm_last_error), shared by the C++ modules
+char* error_buf();
+
 // kernel launchers (tm_kernels.hip)
 hipError_t launch_rules_match(const RulesArgs& a, hipStream_t s);
 hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const int64_t* idx, uint32_t n,
@@ -280,6 +283,42 @@ hipError_t launch_tokens_shard(const uint32_t* words, const uint32_t* toff, uint
                                uint32_t* shard, hipStream_t s);
 hipError_t launch_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
                          uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add, hipStream_t s);
+
+// In-process filter-sharded group (tm_sharded, BASELINE config C4 without a
+// collective): a tokenised batch on the home device is partitioned by owner
+// shard (a stable counting sort: each owner's publishes contiguous, in publish
+// order), every shard matches its part, and the rows come back in publish order.
+constexpr uint32_t PART_BLOCK = 1024;   // publishes per partition block (one per thread)
+constexpr uint32_t PART_MAX_G = 64;     // shards
+struct PartArgs {
+    const uint32_t* owner;    // n: tm_tokens_shard's shard, or G = any shard
+    const uint32_t* words;
+    const uint32_t* toff;     // n + 1
+    const uint8_t* tflags;
+    uint32_t n, G, nb;        // nb = partition blocks
+    uint32_t* cnt;            // [G * nb]: publishes of owner g in block b (g-major), scanned by launch_scan
+    uint32_t* wcnt;           // [G * nb]: their words
+    const uint32_t* cnt_off;  // scans of cnt / wcnt (two-level: off[i] + bsums[i / SCAN_TILE], total at [G * nb])
+    const uint32_t* cnt_bs;
+    const uint32_t* w_off;
+    const uint32_t* w_bs;
+    uint32_t* segs;           // [2 * (G + 1)]: first publish / first word of every owner's part, then the totals
+    uint32_t* order;          // n: publish index at each partitioned position
+    uint32_t* ptoff;          // n + G: owner g's word offsets (relative to its part) at [tseg[g] + g ..]
+    uint8_t* ptflags;         // n
+    uint32_t* pwords;
+};
+hipError_t launch_part_count(const PartArgs& a, hipStream_t s);
+hipError_t launch_part_segs(const PartArgs& a, hipStream_t s);
+hipError_t launch_part_scatter(const PartArgs& a, hipStream_t s);
+// un-partition: counts_o[order[p]] = counts_p[p]
+hipError_t launch_unpart_counts(const uint32_t* order, const uint32_t* counts_p, uint32_t n, uint32_t* counts_o,
+                                hipStream_t s);
+// rows back in publish order: row p of ids_p (at scan(counts_p)[p]) -> out[scan(counts_o)[order[p]]],
+// and the global CSR offsets rowg[order[p]] (rowg[n] = total)
+hipError_t launch_unpart_rows(const uint32_t* order, const uint32_t* counts_p, uint32_t n, const uint32_t* src_off,
+                              const uint32_t* src_bs, const uint32_t* dst_off, const uint32_t* dst_bs,
+                              const uint32_t* ids_p, uint32_t* out, uint32_t* rowg, hipStream_t s);
 
 // ------------------------------------------------------------ word dictionary
 // One entry of the word interner's open-addressed table (emqx_topic:words/1

@@ -1499,6 +1499,127 @@ __global__ __launch_bounds__(256) void tm_tokens_shard(const uint32_t* words, co
     shard[t] = s;
 }
 
+// ---------------------------------------- in-process filter-sharded group
+
+// The publish's owner: its shard, or (G = any shard resolves it: only
+// replicated filters can match) spread round-robin by publish index.
+__device__ __forceinline__ uint32_t part_owner(const PartArgs& a, uint32_t t) {
+    const uint32_t o = a.owner[t];
+    return o < a.G ? o : t % a.G;
+}
+
+__device__ __forceinline__ uint32_t scan_at(const uint32_t* off, const uint32_t* bs, uint32_t i) {
+    return off[i] + bs[i / SCAN_TILE];
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Pass 1: per block and owner, publishes and words -> cnt / wcnt (g-major, so
+// one scan over them numbers each owner's publishes contiguously).
+__global__ __launch_bounds__(PART_BLOCK) void tm_part_count(PartArgs a) {
+    __shared__ uint32_t sc[PART_BLOCK / 64][PART_MAX_G], sw[PART_BLOCK / 64][PART_MAX_G];
+    const uint32_t t = blockIdx.x * PART_BLOCK + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const bool valid = t < a.n;
+    const uint32_t g_me = valid ? part_owner(a, t) : a.G;
+    const uint32_t depth = valid ? a.toff[t + 1] - a.toff[t] : 0u;
+    for (uint32_t g = 0; g < a.G; ++g) {
+        const uint64_t m = __ballot(g_me == g);
+        const uint32_t w = wave_sum(g_me == g ? depth : 0u);
+        if (lane == 0) { sc[wid][g] = (uint32_t)__popcll(m); sw[wid][g] = w; }
+    }
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < a.G; g += PART_BLOCK) {
+        uint32_t c = 0, w = 0;
+        for (uint32_t k = 0; k < PART_BLOCK / 64; ++k) { c += sc[k][g]; w += sw[k][g]; }
+        a.cnt[g * a.nb + blockIdx.x] = c;
+        a.wcnt[g * a.nb + blockIdx.x] = w;
+    }
+}
+
+// segs[g] = first partitioned position of owner g (segs[G] = n), segs[G + 1 + g]
+// = its first word (segs[2G + 1] = all words): the host sizes each shard's part.
+__global__ void tm_part_segs(PartArgs a) {
+    const uint32_t g = threadIdx.x;
+    if (g > a.G) return;
+    const uint32_t i = g * a.nb;
+    a.segs[g] = g < a.G ? scan_at(a.cnt_off, a.cnt_bs, i) : a.cnt_off[a.G * a.nb];
+    a.segs[a.G + 1 + g] = g < a.G ? scan_at(a.w_off, a.w_bs, i) : a.w_off[a.G * a.nb];
+}
+
+// Pass 3: every publish to its place in its owner's part, with its words; the
+// part's word offsets restart at 0 (each part is a token batch of its own,
+// tm_batch_prepare_tokens), so part g's offsets sit at ptoff[segs[g] + g ..].
+__global__ __launch_bounds__(PART_BLOCK) void tm_part_scatter(PartArgs a) {
+    __shared__ uint32_t sc[PART_BLOCK / 64][PART_MAX_G], sw[PART_BLOCK / 64][PART_MAX_G];
+    const uint32_t t = blockIdx.x * PART_BLOCK + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const bool valid = t < a.n;
+    const uint32_t g_me = valid ? part_owner(a, t) : a.G;
+    const uint32_t depth = valid ? a.toff[t + 1] - a.toff[t] : 0u;
+    uint32_t rank = 0, wpre = 0;
+    for (uint32_t g = 0; g < a.G; ++g) {
+        const bool mine = g_me == g;
+        const uint64_t m = __ballot(mine);
+        // inclusive scan of this owner's depths across the wave
+        uint32_t incl = mine ? depth : 0u;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += u;
+        }
+        if (mine) { rank = prefix_count(m); wpre = incl - depth; }
+        if (lane == 63) { sc[wid][g] = (uint32_t)__popcll(m); sw[wid][g] = incl; }
+    }
+    __syncthreads();
+    // each part's closing offset (its word count)
+    if (blockIdx.x == 0 && threadIdx.x < a.G) {
+        const uint32_t g = threadIdx.x;
+        const uint32_t tend = g + 1 < a.G ? scan_at(a.cnt_off, a.cnt_bs, (g + 1) * a.nb) : a.cnt_off[a.G * a.nb];
+        const uint32_t wend = g + 1 < a.G ? scan_at(a.w_off, a.w_bs, (g + 1) * a.nb) : a.w_off[a.G * a.nb];
+        a.ptoff[tend + g] = wend - scan_at(a.w_off, a.w_bs, g * a.nb);
+    }
+    if (!valid) return;
+    uint32_t bt = 0, bw = 0;   // earlier waves of the block, same owner
+    for (uint32_t k = 0; k < wid; ++k) { bt += sc[k][g_me]; bw += sw[k][g_me]; }
+    const uint32_t i = g_me * a.nb + blockIdx.x;
+    const uint32_t p = scan_at(a.cnt_off, a.cnt_bs, i) + bt + rank;
+    const uint32_t w = scan_at(a.w_off, a.w_bs, i) + bw + wpre;
+    const uint32_t wseg = scan_at(a.w_off, a.w_bs, g_me * a.nb);
+    a.order[p] = t;
+    a.ptflags[p] = a.tflags[t];
+    a.ptoff[p + g_me] = w - wseg;
+    const uint32_t src = a.toff[t];
+    for (uint32_t k = 0; k < depth; ++k) a.pwords[w + k] = a.words[src + k];
+}
+
+__global__ __launch_bounds__(256) void tm_unpart_counts(const uint32_t* order, const uint32_t* counts_p, uint32_t n,
+                                                         uint32_t* counts_o) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p < n) counts_o[order[p]] = counts_p[p];
+}
+
+// 16 lanes per row (rows are short lists of filter ids; lanes stride long ones)
+__global__ __launch_bounds__(256) void tm_unpart_rows(const uint32_t* order, const uint32_t* counts_p, uint32_t n,
+                                                       const uint32_t* src_off, const uint32_t* src_bs,
+                                                       const uint32_t* dst_off, const uint32_t* dst_bs,
+                                                       const uint32_t* ids_p, uint32_t* out, uint32_t* rowg) {
+    const uint64_t p = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const uint32_t sub = threadIdx.x & 15;
+    if (p > n) return;
+    if (p == n) {   // the closing offset
+        if (sub == 0) rowg[n] = dst_off[n];
+        return;
+    }
+    const uint32_t t = order[p];
+    const uint32_t len = counts_p[p];
+    const uint32_t src = scan_at(src_off, src_bs, (uint32_t)p), dst = scan_at(dst_off, dst_bs, t);
+    if (sub == 0) rowg[t] = dst;
+    for (uint32_t k = sub; k < len; k += 16) out[dst + k] = ids_p[src + k];
+}
+
 // counts[t] = |row t|; gids[i] = ids[i] * mul + add (a shard's global ids).
 __global__ __launch_bounds__(256) void tm_export(const uint32_t* row_off, const uint32_t* ids, uint32_t n, uint64_t total,
                                                   uint32_t* counts, uint32_t* gids, uint32_t mul, uint32_t add) {
@@ -2139,6 +2260,32 @@ hipError_t launch_token_check(const uint32_t* toff, const uint8_t* tflags, uint3
 hipError_t launch_tokens_shard(const uint32_t* words, const uint32_t* toff, uint32_t n, uint32_t nshards,
                                uint32_t* shard, hipStream_t s) {
     if (n) hipLaunchKernelGGL(tm_tokens_shard, dim3((n + 255) / 256), dim3(256), 0, s, words, toff, n, nshards, shard);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_count(const PartArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_part_count, dim3(a.nb), dim3(PART_BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_part_segs(const PartArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(tm_part_segs, dim3(1), dim3(PART_MAX_G + 1), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_part_scatter(const PartArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_part_scatter, dim3(a.nb), dim3(PART_BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_unpart_counts(const uint32_t* order, const uint32_t* counts_p, uint32_t n, uint32_t* counts_o,
+                                hipStream_t s) {
+    if (n) hipLaunchKernelGGL(tm_unpart_counts, dim3((n + 255) / 256), dim3(256), 0, s, order, counts_p, n, counts_o);
+    return hipGetLastError();
+}
+hipError_t launch_unpart_rows(const uint32_t* order, const uint32_t* counts_p, uint32_t n, const uint32_t* src_off,
+                              const uint32_t* src_bs, const uint32_t* dst_off, const uint32_t* dst_bs,
+                              const uint32_t* ids_p, uint32_t* out, uint32_t* rowg, hipStream_t s) {
+    const uint64_t threads = ((uint64_t)n + 1) * 16;
+    hipLaunchKernelGGL(tm_unpart_rows, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, order, counts_p, n,
+                       src_off, src_bs, dst_off, dst_bs, ids_p, out, rowg);
     return hipGetLastError();
 }
 

@@ -668,3 +668,122 @@ class Engine:
         md = C.c_uint64()
         N.check(self.L.tm_debug_check(self.h, C.byref(md)), "tm_debug_check")
         return int(md.value)
+
+
+class ShardedBatch:
+    """A publish batch of a ShardedGroup (tm_sharded_prepare / run / result)."""
+
+    def __init__(self, grp: "ShardedGroup", topics):
+        self.grp = grp
+        s = _pack(topics)
+        self.n = len(s)
+        self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        h = C.c_void_p()
+        N.check(grp.L.tm_sharded_prepare(grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n, C.byref(h)),
+                "tm_sharded_prepare")
+        self.h = h
+
+    def run(self):
+        N.check(self.grp.L.tm_sharded_run(self.grp.h, self.h), "tm_sharded_run")
+        return self
+
+    def result(self):
+        r = N.Result()
+        N.check(self.grp.L.tm_sharded_result(self.grp.h, self.h, C.byref(r)), "tm_sharded_result")
+        return _result_arrays(r)
+
+    def stats(self) -> dict:
+        st = N.ShardedStats()
+        N.check(self.grp.L.tm_sharded_batch_stats(self.grp.h, self.h, C.byref(st)), "tm_sharded_batch_stats")
+        out = st.match.asdict()
+        out.update(ms_partition=st.ms_partition, ms_parts=st.ms_parts, ms_unpartition=st.ms_unpartition,
+                   part_topics=list(st.part_topics)[:len(self.grp)])
+        return out
+
+    def free(self):
+        if self.h:
+            self.grp.L.tm_sharded_batch_free(self.grp.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class ShardedGroup:
+    """Filter-sharded matching in one process (tm_sharded_*, config C4 without
+    torch or a collective): G shard engines, filters partitioned by their
+    literal (w0, w1) prefix, publishes matched by their owner shard, rows in
+    publish order with global ids (local id * G + shard)."""
+
+    def __init__(self, devices, host_threads: int = 0):
+        self.L = N.lib()
+        devs = (C.c_int32 * len(devices))(*devices)
+        cfg = N.Config(0, 0, host_threads, 0)
+        h = C.c_void_p()
+        N.check(self.L.tm_sharded_create(devs, len(devices), C.byref(cfg), C.byref(h)), "tm_sharded_create")
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tm_sharded_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self.L.tm_sharded_size(self.h))
+
+    def dict_load(self, words):
+        s = _pack(words)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        N.check(self.L.tm_sharded_dict_load(self.h, buf.ctypes.data, offs.ctypes.data, len(s)), "tm_sharded_dict_load")
+
+    def insert_many(self, filters) -> int:
+        s = _pack(filters)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        done = C.c_uint64()
+        N.check(self.L.tm_sharded_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
+                "tm_sharded_insert_many")
+        return int(done.value)
+
+    def delete_many(self, filters) -> int:
+        s = _pack(filters)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        done = C.c_uint64()
+        N.check(self.L.tm_sharded_delete_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
+                "tm_sharded_delete_many")
+        return int(done.value)
+
+    def prepare(self, topics) -> ShardedBatch:
+        return ShardedBatch(self, topics)
+
+    def match_batch(self, topics):
+        s = _pack(topics)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        r = N.Result()
+        N.check(self.L.tm_sharded_match_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
+                "tm_sharded_match_batch")
+        return _result_arrays(r)
+
+    def filter_bytes(self, gid: int) -> bytes:
+        cap = 4096
+        buf = C.create_string_buffer(cap)
+        n = C.c_size_t()
+        N.check(self.L.tm_sharded_filter_copy(self.h, gid, buf, cap, C.byref(n)), "tm_sharded_filter_copy")
+        return buf.raw[:n.value]
+
+    def engine(self, shard: int) -> "Engine":
+        return Engine._borrow(self.L.tm_sharded_engine(self.h, shard), [self.devices[shard]])

@@ -514,6 +514,63 @@ TM_API int  tm_group_rules_match(tm_group* g, const uint8_t* names, const uint64
                                  const uint8_t* rules, const uint64_t* rule_offsets, uint32_t r, int dollar_rule,
                                  uint32_t* bits);
 
+/* ---- filter-sharded group in one process (BASELINE config C4) -------- */
+/* Subscription sets too large to replicate, partitioned over G shard engines
+ * (one per listed device; a device may repeat), no collective: a filter whose
+ * first two levels are literal lives on shard tm_filter_shard(); all others
+ * are replicated on every shard.  A publish is matched completely by its
+ * owner shard (the shard of its first two words, or any shard when only
+ * replicated filters can match it), so rows stay bit-exact.  One step over a
+ * batch tokenised on the home device (devices[0]): owner per publish, a
+ * stable partition by owner on the device, every shard matching its part,
+ * and the rows restored to publish order with global filter ids (local id *
+ * G + shard).  The shards' dictionaries grow only by the deltas of
+ * tm_sharded_insert_many, so word ids agree everywhere.  Reference: the
+ * replicated emqx_trie (src/emqx_trie.erl:53-74) matched in full by
+ * match_routes/1 (src/emqx_router.erl:127-141); sharding it is new. */
+typedef struct tm_sharded tm_sharded;
+typedef struct tm_sharded_batch tm_sharded_batch;
+typedef struct {
+    tm_batch_stats match;     /* summed over the parts; ms_* = the slowest part */
+    float ms_partition;       /* host wall time: owner + partition kernels */
+    float ms_parts;           /* host wall time: parts prepared, matched, exported */
+    float ms_unpartition;     /* host wall time: rows back in publish order */
+    uint32_t part_topics[64]; /* publishes each shard matched */
+} tm_sharded_stats;
+TM_API int  tm_sharded_create(const int32_t* devices, uint32_t n_shards, const tm_config* cfg, tm_sharded** out);
+TM_API void tm_sharded_destroy(tm_sharded* s);
+TM_API uint32_t tm_sharded_size(tm_sharded* s);
+/* Shard g's engine (read-only use: stats, filter bytes of its local ids). */
+TM_API tm_engine* tm_sharded_engine(tm_sharded* s, uint32_t shard);
+/* Interns n words in order on every shard (tm_dict_load). */
+TM_API int  tm_sharded_dict_load(tm_sharded* s, const uint8_t* words, const uint64_t* offsets, uint32_t n);
+/* emqx_trie:insert/1 of a subscribe batch: the batch's literal words no shard
+ * knows are appended to every shard's dictionary in first-appearance order,
+ * then every shard inserts its filters and the replicated ones.
+ * *n_inserted = insertions summed over the shards. */
+TM_API int  tm_sharded_insert_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
+                                   uint64_t* n_inserted);
+/* emqx_trie:delete/1 of an unsubscribe batch on every shard (absent: no-op). */
+TM_API int  tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
+                                   uint64_t* n_deleted);
+/* A publish batch: bytes copied and tokenised on the home device.  A non-NULL
+ * *out is re-prepared in place. */
+TM_API int  tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                               tm_sharded_batch** out);
+/* One step (returns with the rows in the home device's HBM). */
+TM_API int  tm_sharded_run(tm_sharded* s, tm_sharded_batch* b);
+/* D2H of the step's CSR of global filter ids (memory valid like tm_result). */
+TM_API int  tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out);
+TM_API int  tm_sharded_device_csr(tm_sharded* s, tm_sharded_batch* b, const uint32_t** d_row_offsets,
+                                  const uint32_t** d_ids, uint64_t* n_matches);
+TM_API int  tm_sharded_batch_stats(tm_sharded* s, tm_sharded_batch* b, tm_sharded_stats* out);
+TM_API void tm_sharded_batch_free(tm_sharded* s, tm_sharded_batch* b);
+/* prepare + run + result in one call. */
+TM_API int  tm_sharded_match_batch(tm_sharded* s, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                                   tm_result* out);
+/* Bytes of global filter id gid (tm_filter_copy on its shard). */
+TM_API int  tm_sharded_filter_copy(tm_sharded* s, uint32_t gid, uint8_t* buf, size_t cap, size_t* len);
+
 /* ---- diagnostics ------------------------------------------------------ */
 /* Consistency check of the host edge hash (tests): slots of a bucket filled
  * in order, every key's probe run unbroken and within max_disp, every key
