@@ -46,3 +46,43 @@ def test_churn_keeps_live_set_consistent():
     assert len(dels) == 25 and len(adds) == 25
     assert len(c.live) == n0 and len(c.live_set) == n0
     assert not (set(dels) & c.live_set) and set(adds) <= c.live_set
+
+
+def test_c5_checker_equals_the_trie_oracle_under_churn():
+    """tests/c5_checker.py (the full-scale C5 test's expected rows) against the
+    trie oracle over the whole snapshot, on a small C5 workload with churn."""
+    import random
+
+    from c5_checker import SnapshotOracle
+    from oracle import pyoracle as P
+
+    p = gen.SkewParams(seed=12, n_hot=60, k_per_hot=80, vocab=8)   # small vocab: many cross-family matches
+    allf, derived, hot, pubs = workload(p, 2000, 5000, seed=12, background_pool=800)
+    background = allf.tolist()[len(derived):]
+    chk = SnapshotOracle(derived, background)
+    live = set(derived.tolist())
+    churn = Churn(hot, derived.tolist(), seed=5)
+    T = sorted(set(pubs.tolist()))[:400] + hot.tolist()
+    for rnd in range(3):
+        if rnd:
+            dels, adds = churn.step(400)
+            for f in dels:
+                chk.delete(f)
+                live.discard(f)
+            for f in adds:
+                chk.insert(f)
+                live.add(f)
+        orc = P.Oracle()
+        F = sorted(live) + background
+        for f in F:
+            orc.register(f)
+            orc.insert(f)
+        buf, offs = P.pack(T)
+        counts, idx, _ = orc.match_batch(buf, offs)
+        orc.close()
+        cut = [0]
+        for c in counts.tolist():
+            cut.append(cut[-1] + c)
+        exp = [[F[int(j)] for j in idx[cut[i]:cut[i + 1]]] for i in range(len(T))]
+        assert chk.rows(T) == exp, rnd
+    chk.close()

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r3b
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_replicated.py tests/test_gpu_sharded_group.py -x -v --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_replicated.py tests/test_gpu_sharded_group.py tests/test_gpu_skew_full.py -x -v --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?
 tail -12 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
