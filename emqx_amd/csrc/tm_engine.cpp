@@ -23,7 +23,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <deque>
+#include <functional>
 #include <set>
 #include <mutex>
 #include <string>
@@ -604,6 +606,114 @@ struct Replica {
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
 };
 
+// Persistent host workers of the bulk mutations: run(f) calls f(0..n-1) with
+// f(0) on the calling thread, so a delta batch pays no thread start-up for
+// each of its phases.
+struct WorkPool {
+    unsigned n = 1;
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, cv_done;
+    const std::function<void(unsigned)>* job = nullptr;
+    uint64_t gen = 0;
+    unsigned busy = 0;
+    bool stop = false;
+
+    void start(unsigned k) {
+        n = std::max(1u, k);
+        for (unsigned i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
+    }
+    void loop(unsigned i) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            const std::function<void(unsigned)>* f = job;
+            lk.unlock();
+            (*f)(i);
+            lk.lock();
+            if (--busy == 0) cv_done.notify_all();
+        }
+    }
+    void run(const std::function<void(unsigned)>& f) {
+        if (n <= 1) { f(0); return; }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = &f;
+            busy = n - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu);
+        cv_done.wait(lk, [&] { return busy == 0; });
+    }
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
+// One worker's share of a parallel bulk mutation (tm_engine::mutate_parallel).
+// Phase 1 (defer): node records change in place -- each worker owns the
+// subtrees of its first words, ROOT is shared under root_mu -- while the
+// edge-hash work (insert / delete an edge, rewrite a child summary) is only
+// recorded; the counters, dirty lists, filter bytes and freed ids collect
+// here and are merged afterwards.  Phase 2 applies the recorded edge work by
+// bucket ranges.
+struct Mut {
+    bool defer = false;
+    std::vector<uint32_t>* ids = nullptr;               // the batch's node ids: free ones, then fresh ones
+    std::atomic<size_t>* next_id = nullptr;             //   (shared by the workers)
+    size_t n_free = 0, fresh_base = 0;
+    std::vector<std::array<uint32_t, 3>> ins;           // deferred insert_edge(p, w, c)
+    std::vector<std::pair<uint32_t, uint32_t>> del;     // deferred delete_edge_of(c): (c, its slot then)
+    std::vector<uint32_t> sum;                          // deferred write_summary(c)
+    // (parent << 32 | word) -> child made in phase 1: open addressing, keys + 1
+    std::vector<std::pair<uint64_t, uint32_t>> made;
+    size_t made_n = 0;
+    uint32_t made_get(uint64_t k) const {
+        if (made.empty()) return NONE;
+        const size_t m = made.size() - 1;
+        for (size_t i = (size_t)((k * 0x9E3779B97F4A7C15ull) >> 20) & m;; i = (i + 1) & m) {
+            if (made[i].first == 0) return NONE;
+            if (made[i].first == k + 1) return made[i].second;
+        }
+    }
+    void made_put(uint64_t k, uint32_t c) {
+        if ((made_n + 1) * 2 > made.size()) {
+            std::vector<std::pair<uint64_t, uint32_t>> old;
+            old.swap(made);
+            made.assign(std::max<size_t>(1024, old.size() * 2), {0, 0});
+            made_n = 0;
+            for (const auto& e : old)
+                if (e.first) made_put(e.first - 1, e.second);
+        }
+        const size_t m = made.size() - 1;
+        size_t i = (size_t)((k * 0x9E3779B97F4A7C15ull) >> 20) & m;
+        while (made[i].first && made[i].first != k + 1) i = (i + 1) & m;
+        if (!made[i].first) ++made_n;
+        made[i] = {k + 1, c};
+    }
+    std::vector<uint8_t> fb;                            // filter bytes appended
+    std::vector<std::pair<uint32_t, uint64_t>> foff;    // (node, offset into fb)
+    std::vector<uint32_t> dirty, dirty_f;
+    std::vector<std::pair<uint64_t, uint32_t>> pend;    // freed ids (pending_free)
+    int64_t live_nodes = 0, n_filters = 0, live_edges = 0, used_slots = 0, route_entries = 0;
+    uint32_t max_disp = 0;
+    uint64_t version = 0, done = 0;
+    bool routes_dirty = false;
+    int rc = TM_OK;
+    std::vector<uint32_t> items;                        // phase 1: the batch entries of this worker
+};
+thread_local Mut* tl_mut = nullptr;
+
 struct tm_engine {
     std::recursive_mutex mu;
     std::vector<Replica*> reps;   // empty: host-only engine (trie ops, no match)
@@ -758,22 +868,34 @@ struct tm_engine {
         if (full_dirty) return;
         uint64_t& w = dirty_mark[i >> 6];
         const uint64_t m = 1ull << (i & 63);
-        if (!(w & m)) { w |= m; dirty.push_back(i); }
+        if (!(w & m)) { w |= m; (tl_mut ? tl_mut->dirty : dirty).push_back(i); }
     }
 
     uint32_t insert_edge(uint32_t p, uint32_t w, uint32_t c) {
-        if ((used_slots + 1) * 4 > slots.size() * 3 || max_disp > 48)
+        Mut* M = tl_mut;
+        if (M && M->defer) {   // phase 1 of a parallel batch: recorded, placed in phase 2
+            M->ins.push_back({p, w, c});
+            M->made_put((uint64_t)p << 32 | w, c);
+            return NONE;
+        }
+        if (!M && ((used_slots + 1) * 4 > slots.size() * 3 || max_disp > 48))   // (phase 2 checks capacity first)
             rehash(std::max<size_t>((size_t)((live_edges + 1) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
         uint32_t disp;
         bool was_empty;
         uint32_t i = place_slot(slots, p, w, disp, was_empty);
-        if (was_empty) ++used_slots;
-        max_disp = std::max(max_disp, disp);
+        if (M) {
+            if (was_empty) ++M->used_slots;
+            M->max_disp = std::max(M->max_disp, disp);
+            ++M->live_edges;
+        } else {
+            if (was_empty) ++used_slots;
+            max_disp = std::max(max_disp, disp);
+            ++live_edges;
+        }
         Slot& e = slots[i];
         e.parent = p; e.word = w; e.child = c;
         nd[c].inslot = i;
         write_summary(c);
-        ++live_edges;
         return i;
     }
 
@@ -809,10 +931,20 @@ struct tm_engine {
     }
 
     void delete_edge_of(uint32_t c) {
+        Mut* M = tl_mut;
+        if (M && M->defer) {   // phase 1 of a parallel batch: recorded, removed in phase 2
+            M->del.emplace_back(c, nd[c].inslot);
+            return;
+        }
         uint32_t i = nd[c].inslot;
         nd[c].inslot = NONE;
-        --live_edges;
-        --used_slots;
+        if (M) {
+            --M->live_edges;
+            --M->used_slots;
+        } else {
+            --live_edges;
+            --used_slots;
+        }
         const uint32_t nb = nbuckets();
         uint32_t hb = i / BUCKET;
         const bool was_full = slots[hb * BUCKET + BUCKET - 1].parent != SLOT_EMPTY;
@@ -877,6 +1009,15 @@ struct tm_engine {
 
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
+        if (Mut* M = tl_mut) {   // a parallel batch: the free ids of the batch first, then fresh ones
+            const size_t k = M->next_id->fetch_add(1, std::memory_order_relaxed);
+            id = k < M->n_free ? (*M->ids)[k] : (uint32_t)(M->fresh_base + (k - M->n_free));
+            nd[id].hasbytes = 0;
+            nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
+            nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
+            ++M->live_nodes;
+            return id;
+        }
         if (free_nodes.empty()) release_pending_ids();
         if (!free_nodes.empty()) {
             id = free_nodes.back();
@@ -896,17 +1037,28 @@ struct tm_engine {
     }
 
     void kill_node(uint32_t id) {
+        Mut* M = tl_mut;
         if (id < n_dests.size() && !n_dests[id].empty()) {
-            route_entries -= n_dests[id].size();
+            if (M) {
+                M->route_entries -= (int64_t)n_dests[id].size();
+                M->routes_dirty = true;
+            } else {
+                route_entries -= n_dests[id].size();
+                routes_dirty = true;
+            }
             n_dests[id].clear();
             n_nroutes[id] = 0;
-            routes_dirty = true;
         }
         nd[id].live = 0;
         nd[id].topic = 0;
         nd[id].ec = 0;
-        --live_nodes;
-        if (id != ROOT) pending_free.emplace_back(launch_seq, id);
+        if (M) {
+            --M->live_nodes;
+            if (id != ROOT) M->pend.emplace_back(launch_seq, id);
+        } else {
+            --live_nodes;
+            if (id != ROOT) pending_free.emplace_back(launch_seq, id);
+        }
     }
 
     uint32_t summary_flags(uint32_t c) const {
@@ -920,6 +1072,10 @@ struct tm_engine {
     // rewrite c's summary into its incoming slot (or the root record)
     void write_summary(uint32_t c) {
         if (c == ROOT) return;   // root record is rebuilt at every launch
+        if (tl_mut && tl_mut->defer) {   // phase 1 of a parallel batch: rewritten in phase 2
+            tl_mut->sum.push_back(c);
+            return;
+        }
         const uint32_t i = nd[c].inslot;
         if (i == NONE) return;
         Slot& e = slots[i];
@@ -941,13 +1097,20 @@ struct tm_engine {
     void set_topic(uint32_t c, const uint8_t* bytes, size_t len) {
         nd[c].topic = 1;
         nd[c].hasbytes = 1;
-        ++n_filters;
-        n_foff[c] = fbytes.size();
         n_flen[c] = (uint32_t)len;
-        fbytes.insert(fbytes.end(), bytes, bytes + len);
-        if (!full_f_dirty) {
-            if (dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
-            if (!dirty_f_mark[c]) { dirty_f_mark[c] = 1; dirty_f.push_back(c); }
+        if (Mut* M = tl_mut) {   // bytes land in the arena at the merge (n_foff fixed up there)
+            ++M->n_filters;
+            M->foff.emplace_back(c, M->fb.size());
+            M->fb.insert(M->fb.end(), bytes, bytes + len);
+            if (!full_f_dirty && !dirty_f_mark[c]) { dirty_f_mark[c] = 1; M->dirty_f.push_back(c); }   // (pre-sized)
+        } else {
+            ++n_filters;
+            n_foff[c] = fbytes.size();
+            fbytes.insert(fbytes.end(), bytes, bytes + len);
+            if (!full_f_dirty) {
+                if (dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
+                if (!dirty_f_mark[c]) { dirty_f_mark[c] = 1; dirty_f.push_back(c); }
+            }
         }
         write_summary(c);
         if (c != ROOT && nd[c].word == W_HASH) write_summary(nd[c].parent);
@@ -956,7 +1119,8 @@ struct tm_engine {
     void clear_topic(uint32_t c) {
         if (!nd[c].topic) return;
         nd[c].topic = 0;
-        --n_filters;
+        if (tl_mut) --tl_mut->n_filters;
+        else --n_filters;
         write_summary(c);
         if (c != ROOT && nd[c].word == W_HASH) write_summary(nd[c].parent);
     }
@@ -1032,22 +1196,33 @@ struct tm_engine {
         // are followed, the missing suffix is created
         uint32_t p = from;
         bool created = false;
+        Mut* const M = tl_mut;
         for (size_t k = k0; k < ids.size(); ++k) {
             const uint32_t w = ids[k];
-            const uint32_t s = nd[p].live ? find_slot(p, w) : NONE;
-            uint32_t c;
-            if (s != NONE) {
-                c = slots[s].child & ID_MASK;
-            } else {
+            // (a parallel batch: the nodes of depth < 2 are shared by workers)
+            std::unique_lock<std::recursive_mutex> rl;
+            if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+            uint32_t c = NONE;
+            if (M && M->defer) {   // an edge made earlier in this batch is not in the hash yet
+                c = M->made_get((uint64_t)p << 32 | w);
+            }
+            if (c == NONE) {
+                const uint32_t s = nd[p].live ? find_slot(p, w) : NONE;
+                if (s != NONE) c = slots[s].child & ID_MASK;
+            }
+            if (c == NONE) {
                 if (!created) {
-                    // node ids are 30-bit (two flag bits ride in the slot's id words)
+                    // node ids are 30-bit (two flag bits ride in the slot's id words); a
+                    // parallel batch checked its whole need up front
                     const size_t need = ids.size() - k;
-                    if (nd.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
+                    if (!M && nd.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
                         return TM_ENOMEM;
                     created = true;
                 }
                 if (!nd[p].live) {               // only the root can be absent here
-                    nd[p].live = 1; nd[p].ec = 0; ++live_nodes;
+                    nd[p].live = 1; nd[p].ec = 0;
+                    if (M) ++M->live_nodes;
+                    else ++live_nodes;
                 }
                 c = new_node(p, w);
                 ++nd[p].ec;
@@ -1058,9 +1233,12 @@ struct tm_engine {
             }
             p = c;
         }
+        std::unique_lock<std::recursive_mutex> tl;
+        if (M && ids.size() < 2) tl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
         if (!created && nd[p].topic) return TM_OK;   // inserted already: idempotent
         set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
-        ++version;
+        if (M) ++M->version;
+        else ++version;
         return TM_OK;
     }
 
@@ -1076,8 +1254,15 @@ struct tm_engine {
     // delete/1 of the filter whose words are ids and whose node is n
     int trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids) {
         struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
+        Mut* const M = tl_mut;
+        std::unique_lock<std::recursive_mutex> nl;
+        if (M && ids.size() < 2) nl = std::unique_lock<std::recursive_mutex>(shared_mu(n));
         if (nd[n].ec != 0) {
-            if (nd[n].topic) { clear_topic(n); ++version; }
+            if (nd[n].topic) {
+                clear_topic(n);
+                if (M) ++M->version;
+                else ++version;
+            }
             return TM_OK;
         }
         clear_topic(n);
@@ -1089,6 +1274,9 @@ struct tm_engine {
             const uint32_t w = ids[k];
             delete_edge_of(child);
             if (!child_dead) { kill_node(child); child_dead = true; }
+            // (a parallel batch: the nodes of depth < 2 are shared by workers)
+            std::unique_lock<std::recursive_mutex> rl;
+            if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
             if (w == W_PLUS) nd[p].plus = NONE;
             else if (w == W_HASH) nd[p].hash = NONE;
             if (!nd[p].live) { rc = TM_EABORT; break; }
@@ -1103,7 +1291,8 @@ struct tm_engine {
             write_summary(p);
             break;
         }
-        ++version;
+        if (M) ++M->version;
+        else ++version;
         return rc;
     }
 
@@ -1118,6 +1307,11 @@ struct tm_engine {
     // delete_many never creates one, and a node is only killed once no live
     // filter lies below it, so a planned node that is still live is the
     // filter's node (killed ids are not reused before the pass ends).
+    std::recursive_mutex shared_mus[64];   // the records of depth < 2 during a parallel batch, striped by node id
+    std::recursive_mutex& shared_mu(uint32_t id) { return shared_mus[id & 63]; }
+    WorkPool pool;            // workers of parallel batches (started at the first one)
+    bool pool_started = false;
+
     struct PlanEnt {
         uint32_t node;    // deepest existing node (insert) / the filter's node or NONE (delete)
         uint32_t depth;   // levels walked (insert)
@@ -1167,12 +1361,13 @@ struct tm_engine {
         const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 512));
         if (plan_words.size() < nt) plan_words.resize(nt);
         if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
-        std::vector<std::thread> th;
-        for (unsigned i = 0; i < nt; ++i) {
-            const uint32_t lo = (uint32_t)((uint64_t)n * i / nt), hi = (uint32_t)((uint64_t)n * (i + 1) / nt);
-            th.emplace_back([this, buf, offs, lo, hi, del, i] { plan_range(buf, offs, lo, hi, del, i); });
-        }
-        for (auto& x : th) x.join();
+        ensure_pool();   // the engine's workers (no thread start-up per batch)
+        pool.run([&](unsigned i) {
+            for (unsigned j = i; j < nt; j += pool.n) {
+                const uint32_t lo = (uint32_t)((uint64_t)n * j / nt), hi = (uint32_t)((uint64_t)n * (j + 1) / nt);
+                plan_range(buf, offs, lo, hi, del, j);
+            }
+        });
     }
 
     // the serial passes prefetch what filter i + PF_FAR / i + PF_NEAR will
@@ -1224,6 +1419,300 @@ struct tm_engine {
         const PlanEnt& pe = plan[i];
         if (pe.node == NONE || !nd[pe.node].live) return TM_OK;   // absent, or removed earlier in the batch
         return trie_delete_at(pe.node, plan_words[pe.part].data() + pe.woff, pe.nw);
+    }
+
+    // ------------------------------------------------------------ parallel batches
+    // A bulk insert / delete of PAR_MIN+ filters (subscribe churn, C5) runs
+    // its serial mutation pass on the engine's workers instead of one thread:
+    //   phase 1: the batch is dealt by first word (a worker owns the subtrees
+    //            of its first words; ROOT is shared under root_mu) and every
+    //            worker mutates node records in place, in batch order, while
+    //            the edge-hash work is recorded (Mut);
+    //   phase 2: the recorded edge deletes, then inserts, run by bucket range:
+    //            2T ranges, the even ones in parallel, then the odd ones, so
+    //            two workers never touch neighbouring buckets (a backward-shift
+    //            chain or a probe run crosses into at most the next range);
+    //            a delete whose slot moved into a range of the wrong parity
+    //            meanwhile runs serially at the end; then the recorded summary
+    //            rewrites, by slot range.
+    // Node ids are handed out per worker up front (the free list first), and
+    // the counters, dirty lists, freed ids and filter bytes are merged after.
+    // Filter / node ids therefore differ from a serial run's (ids are the
+    // engine's own), the trie and its HBM image are the same.
+    static constexpr uint32_t PAR_MIN = 2048;
+    static constexpr uint32_t PAR_RANGE_MIN = 65536;   // buckets per phase-2 range at least
+
+    static uint32_t mix_word(uint32_t w) {
+        uint64_t k = (uint64_t)w * 0x9E3779B97F4A7C15ull;
+        return (uint32_t)(k >> 32);
+    }
+
+    void ensure_pool() {
+        if (!pool_started) {
+            pool.start(threads);
+            pool_started = true;
+        }
+    }
+
+    // Phase 2: the recorded edge work of W, by bucket range (see above).
+    void edge_phase(std::vector<Mut>& W) {
+        const unsigned T = (unsigned)W.size();
+        auto merge_edges = [&](std::vector<Mut>& X) {
+            for (Mut& m : X) {
+                live_edges += m.live_edges; used_slots += m.used_slots; max_disp = std::max(max_disp, m.max_disp);
+                dirty.insert(dirty.end(), m.dirty.begin(), m.dirty.end());
+                m.live_edges = m.used_slots = 0; m.max_disp = 0; m.dirty.clear();
+            }
+        };
+        auto ranges = [&](unsigned& T2, uint32_t& RS, uint32_t& R) {
+            const uint32_t nb = nbuckets();
+            T2 = std::min<unsigned>(T, nb / (2 * PAR_RANGE_MIN));
+            if (T2 < 2) { T2 = 0; return; }
+            RS = ((nb + 2 * T2 - 1) / (2 * T2) + 15) / 16 * 16;   // whole 16-bucket groups: dirty-mark words stay per range
+            R = (nb + RS - 1) / RS;
+        };
+        for (Mut& m : W) m.defer = false;
+        const bool trace = getenv("TM_PAR_TRACE") != nullptr;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        const auto e0 = now();
+        unsigned T2 = 0;
+        uint32_t RS = 0, R = 0;
+        // ---- deletes, bucketed by the slot recorded in phase 1 (nothing has moved since)
+        ranges(T2, RS, R);
+        if (!T2) {
+            for (Mut& m : W)
+                for (const auto& d : m.del) delete_edge_of(d.first);
+        } else {
+            std::vector<std::vector<uint32_t>> per(2 * T2);
+            std::vector<uint32_t> tail;
+            for (Mut& m : W)
+                for (const auto& d : m.del) {
+                    const uint32_t r = d.second / BUCKET / RS;
+                    if (R % 2 && r == R - 1) tail.push_back(d.first);   // (R odd: the last range wraps onto range 0)
+                    else per[r].push_back(d.first);
+                }
+            std::vector<Mut> X(T2);
+            std::vector<std::vector<uint32_t>> late(T2);
+            for (uint32_t par = 0; par < 2; ++par)
+                pool.run([&](unsigned t) {
+                    if (t >= T2) return;
+                    const uint32_t r = 2 * t + par;
+                    tl_mut = &X[t];
+                    for (uint32_t c : per[r]) {
+                        // an odd range's slot may have been pulled back into the even range before it
+                        if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
+                        delete_edge_of(c);
+                    }
+                    tl_mut = nullptr;
+                });
+            merge_edges(X);
+            for (auto& l : late) tail.insert(tail.end(), l.begin(), l.end());
+            for (uint32_t c : tail) delete_edge_of(c);   // serially, global counters
+        }
+        // ---- inserts: room first (the serial insert_edge's rehash rule, for the whole batch)
+        const auto e1 = now();
+        size_t nins = 0;
+        for (Mut& m : W) nins += m.ins.size();
+        bool rehashed = false;
+        if ((used_slots + nins) * 4 > slots.size() * 3 || max_disp > 48) {
+            rehash(std::max<size_t>((size_t)((live_edges + nins) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
+            rehashed = true;
+        }
+        const auto e2 = now();
+        ranges(T2, RS, R);
+        if (!T2) {
+            for (Mut& m : W)
+                for (const auto& e : m.ins) insert_edge(e[0], e[1], e[2]);
+        } else {
+            std::vector<std::vector<std::array<uint32_t, 3>>> per(2 * T2);
+            std::vector<std::array<uint32_t, 3>> tail;
+            const uint32_t nb = nbuckets();
+            for (Mut& m : W)
+                for (const auto& e : m.ins) {
+                    const uint32_t r = home_bucket(e[0], e[1], nb) / RS;
+                    if (R % 2 && r == R - 1) tail.push_back(e);
+                    else per[r].push_back(e);
+                }
+            std::vector<Mut> X(T2);
+            for (uint32_t par = 0; par < 2; ++par)
+                pool.run([&](unsigned t) {
+                    if (t >= T2) return;
+                    tl_mut = &X[t];
+                    for (const auto& e : per[2 * t + par]) insert_edge(e[0], e[1], e[2]);
+                    tl_mut = nullptr;
+                });
+            merge_edges(X);
+            for (const auto& e : tail) insert_edge(e[0], e[1], e[2]);
+        }
+        if (max_disp > 48) rehash(std::max<size_t>((size_t)(live_edges / 0.55), slots.size() * 2));
+        const auto e3 = now();
+        // ---- summaries of the nodes whose record changed: by node (a node's
+        // records are rewritten by one worker; dirty marks set atomically)
+        const unsigned TS = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));
+        std::vector<std::vector<uint32_t>> per(TS);
+        for (Mut& m : W)
+            for (uint32_t c : m.sum) per[mix_word(c) % TS].push_back(c);
+        std::vector<Mut> X(TS);
+        pool.run([&](unsigned t) {
+            if (t >= TS) return;
+            std::vector<uint32_t>& v = per[t];
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            for (uint32_t c : v) {
+                if (!nd[c].live || nd[c].inslot == NONE) continue;
+                write_summary_at(c, X[t].dirty);
+            }
+        });
+        merge_edges(X);
+        if (trace)
+            fprintf(stderr, "[par edges T2=%u nb=%u] del %.2f rehash %d %.2f ins %.2f sum %.2f ms\n", T2, nbuckets(),
+                    ms(e0, e1), (int)rehashed, ms(e1, e2), ms(e2, e3), ms(e3, now()));
+    }
+
+    // write_summary for a parallel pass: the dirty mark set atomically (another
+    // worker may mark a slot of the same 64-slot word)
+    void write_summary_at(uint32_t c, std::vector<uint32_t>& dl) {
+        const uint32_t i = nd[c].inslot;
+        Slot& e = slots[i];
+        e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
+        const uint32_t h = nd[c].hash;
+        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
+        if (full_dirty) return;
+        const uint64_t m = 1ull << (i & 63);
+        if (!(__atomic_fetch_or(&dirty_mark[i >> 6], m, __ATOMIC_RELAXED) & m)) dl.push_back(i);
+    }
+
+    // tm_trie_insert_many / delete_many of n >= PAR_MIN planned filters (make_plan ran).
+    // Returns 1 when the batch must run serially instead (nothing changed then).
+    int mutate_parallel(bool del, const uint8_t* buf, const uint64_t* offs, uint32_t n, uint64_t* done_out,
+                        int* rc_out) {
+        const unsigned T = std::max(1u, threads);
+        if (T < 2 || (uint64_t)n * 4 > n_filters) return 1;   // bulk builds stay serial: churn on a big trie only
+        if (!del) {
+            // new words are interned first, serially (the dictionary is not thread-safe)
+            for (uint32_t i = 0; i < n; ++i) {
+                PlanEnt& pe = plan[i];
+                uint32_t* ids = plan_words[pe.part].data() + pe.woff;
+                bool unknown = false;
+                for (uint32_t k = pe.depth; k < pe.nw; ++k) unknown |= ids[k] == W_UNKNOWN;
+                if (!unknown) continue;
+                if (frozen) return 1;   // TM_ENOENT semantics of the serial pass (stop at the first)
+                static thread_local std::vector<TWord> ws;
+                split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
+                for (uint32_t k = pe.depth; k < pe.nw; ++k)
+                    if (ids[k] == W_UNKNOWN) ids[k] = dict.intern(ws[k].p, ws[k].n);
+            }
+        }
+        ensure_pool();
+        std::vector<Mut> W(T);
+        for (uint32_t i = 0; i < n; ++i) {   // by the first two words: a worker owns those subtrees
+            const PlanEnt& pe = plan[i];
+            const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+            const uint32_t key = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
+            W[mix_word(key) % T].items.push_back(i);
+        }
+        // node ids: at most the levels the batch's filters lack, the free ids first
+        std::vector<uint32_t> ids;
+        std::atomic<size_t> next_id{0};
+        size_t fresh = 0;
+        const size_t base = nd.size();
+        if (!del) {
+            release_pending_ids();
+            uint64_t total = 0;
+            for (uint32_t i = 0; i < n; ++i) total += plan[i].nw - plan[i].depth;
+            const size_t take = std::min<size_t>(total, free_nodes.size());
+            fresh = total - take;
+            if (base + fresh >= MAX_NODES) return 1;
+            ids.assign(free_nodes.end() - (long)take, free_nodes.end());
+            free_nodes.resize(free_nodes.size() - take);
+            if (fresh) {
+                nd.resize(base + fresh);   // dead records until handed out; the unused tail is cut after
+                n_flen.resize(base + fresh, 0);
+                n_foff.resize(base + fresh, 0);
+            }
+            if (!full_f_dirty && dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
+        }
+        for (Mut& m : W) {
+            m.ids = &ids;
+            m.next_id = &next_id;
+            m.n_free = ids.size();
+            m.fresh_base = base;
+        }
+        const auto tp0 = std::chrono::steady_clock::now();
+        // phase 1: node records, by first word
+        pool.run([&](unsigned t) {
+            Mut& m = W[t];
+            m.defer = true;
+            tl_mut = &m;
+            try {
+                const size_t ni = m.items.size();
+                for (size_t q = 0; q < ni; ++q) {
+                    const uint32_t i = m.items[q];
+                    if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
+                        const uint32_t f = plan[m.items[q + 8]].node;
+                        if (f != NONE) __builtin_prefetch(&nd[f]);
+                    }
+                    const PlanEnt& pe = plan[i];
+                    int rc;
+                    if (del) {
+                        rc = delete_planned(i);
+                    } else {
+                        rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
+                                             plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth);
+                    }
+                    if (rc) { m.rc = rc; break; }
+                    ++m.done;
+                }
+            } catch (...) {
+                m.rc = TM_ENOMEM;
+            }
+            tl_mut = nullptr;
+        });
+        const auto tp1 = std::chrono::steady_clock::now();
+        // phase 2: the edge hash
+        edge_phase(W);
+        const auto tp2 = std::chrono::steady_clock::now();
+        // merge the rest
+        uint64_t done = 0;
+        int rc = TM_OK;
+        for (Mut& m : W) {
+            live_nodes += m.live_nodes;
+            n_filters += m.n_filters;
+            route_entries += m.route_entries;
+            routes_dirty = routes_dirty || m.routes_dirty;
+            version += m.version;
+            done += m.done;
+            if (m.rc && !rc) rc = m.rc;
+            m.fresh_base = fbytes.size();   // (reused: this worker's bytes start here)
+            fbytes.insert(fbytes.end(), m.fb.begin(), m.fb.end());
+            dirty_f.insert(dirty_f.end(), m.dirty_f.begin(), m.dirty_f.end());
+            for (const auto& q : m.pend) pending_free.push_back(q);
+        }
+        pool.run([&](unsigned t) {   // filter byte offsets: distinct nodes per worker
+            for (unsigned j = t; j < T; j += pool.n)
+                for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+        });
+        if (!del) {   // ids not handed out: free ones back to the list, the fresh tail cut off
+            const size_t used = next_id.load();
+            for (size_t k = used; k < ids.size(); ++k) free_nodes.push_back(ids[k]);
+            const size_t fresh_used = used > ids.size() ? used - ids.size() : 0;
+            if (fresh_used < fresh) {
+                nd.resize(base + fresh_used);
+                n_flen.resize(base + fresh_used);
+                n_foff.resize(base + fresh_used);
+                if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
+            }
+        }
+        *done_out = done;
+        *rc_out = rc;
+        if (getenv("TM_PAR_TRACE")) {
+            const auto tp3 = std::chrono::steady_clock::now();
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "[par %s n=%u T=%u] phase1 %.2f ms edges %.2f ms merge %.2f ms\n", del ? "del" : "ins", n, T,
+                    ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
+        }
+        return 0;
     }
 
     // ------------------------------------------------------------ device sync
@@ -3764,6 +4253,10 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     try {
         if (nshards <= 1) {
             e->make_plan(filters, offsets, n, false);
+            if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(false, filters, offsets, n, &done, &rc)) {
+                if (n_inserted) *n_inserted = done;
+                return rc;
+            }
             for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
                 e->prefetch_insert(i, n);
                 rc = e->insert_planned(filters, offsets, i);
@@ -3800,6 +4293,10 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
         if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
         e->make_plan(filters, offsets, n, true);
+        if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(true, filters, offsets, n, &done, &rc)) {
+            if (n_deleted) *n_deleted = done;
+            return rc;
+        }
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
             e->prefetch_delete(i, n);
             rc = e->delete_planned(i);

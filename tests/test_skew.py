@@ -86,3 +86,40 @@ def test_c5_checker_equals_the_trie_oracle_under_churn():
         exp = [[F[int(j)] for j in idx[cut[i]:cut[i + 1]]] for i in range(len(T))]
         assert chk.rows(T) == exp, rnd
     chk.close()
+
+
+def test_parallel_churn_builds_the_same_trie_as_the_serial_pass():
+    """tm_trie_insert_many / delete_many of 2,048+ filters on a big trie run
+    their mutation pass on the engine's workers (first-two-word subtrees, then
+    the edge hash by bucket ranges).  The result must be the serial pass's
+    trie: same nodes, edges and filters, the same edge_count of every node on
+    the churned paths, and a consistent edge hash (tm_debug_check)."""
+    import random
+
+    p = gen.SkewParams(seed=21, n_hot=2500, k_per_hot=100)
+    allf, derived, hot, _ = workload(p, 60_000, 100, seed=21, background_pool=500)
+    A = Engine(device=-1, host_threads=1)      # one thread: the serial pass
+    B = Engine(device=-1, host_threads=8)
+    for e in (A, B):
+        e.insert_many(allf)
+
+    def same():
+        a, b = A.stats(), B.stats()
+        assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+        B.debug_check()
+
+    same()
+    churn = Churn(hot, derived.tolist(), seed=3)
+    touched = []
+    for _ in range(4):
+        dels, adds = churn.step(10_000)
+        for e in (A, B):
+            Churn.apply(e, gen.Strings.from_list(dels), gen.Strings.from_list(adds))
+        touched += dels[:300] + adds[:300]
+        same()
+    rng = random.Random(4)
+    for f in touched + rng.sample(sorted(churn.live_set), 1000):
+        ws = f.split(b"/")
+        for k in range(1, len(ws) + 1):
+            pre = b"/".join(ws[:k])
+            assert A.lookup(pre) == B.lookup(pre), pre
