@@ -2680,7 +2680,8 @@ struct tm_engine {
         int rc;
         const uint64_t fast =
             std::max<uint64_t>((uint64_t)match_waves(b->n, b->rep->device, qcap) * tile_topics(b->n) * row_cap, 1);
-        if ((rc = dev_reserve(b->d_rows, b->c_rows, fast))) return rc;
+        // + a byte per entry past the rows: the emission-log variant's lanes (TM_EMIT_LOG)
+        if ((rc = dev_reserve(b->d_rows, b->c_rows, fast + fast / 8 + 8))) return rc;
         if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;

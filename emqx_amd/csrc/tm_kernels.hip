@@ -396,6 +396,65 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
     }
 }
 
+#ifdef TM_EMIT_LOG
+// Emission log variant of the tile epilogue: the tile's matches were appended
+// to a wave-private log in iteration order (coalesced: one store of <= 64
+// consecutive entries per emission role per iteration), each with its topic
+// lane in a parallel byte log.  The rows are rebuilt in LDS a chunk of whole
+// rows at a time -- the log is streamed (L2-resident: written moments ago)
+// and every entry of a chunk's rows goes to its row's next free place -- and
+// sorted as before.
+template <bool CK, class LT>
+__device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst,
+                                              const unsigned long long* wlog, const uint8_t* wlane, uint32_t lcount) {
+    constexpr uint32_t STAGE = LT::STAGE;
+    const uint32_t lane = threadIdx.x;
+    unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
+    const uint32_t cw = keep ? c : 0u;
+    uint32_t incl = cw;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += u;
+    }
+    const uint32_t pos = incl - cw;
+    uint32_t rs = 0;
+    while (rs < a.tile_topics) {
+        const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
+        const uint64_t beyond = __ballot(lane >= rs && pos + cw - p0 > STAGE);
+        const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : a.tile_topics;
+        const bool in_chunk = keep && lane >= rs && lane < re;
+        L.depth[lane] = in_chunk ? pos - p0 : NONE;   // (free after the frontier loop) row base in the stage
+        L.toff[lane] = 0;                            // row fill cursor
+        __syncthreads();
+        for (uint32_t k0 = 0; k0 < lcount; k0 += 256) {
+            unsigned long long e[4];
+            uint32_t r[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + lane + 64 * u;
+                r[u] = 64;
+                if (k < lcount) {
+                    e[u] = wlog[k];
+                    r[u] = wlane[k];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                if (r[u] >= 64) continue;
+                const uint32_t base = L.depth[r[u]];
+                if (base == NONE) continue;
+                const uint32_t at = base + atomicAdd(&L.toff[r[u]], 1u);
+                stg[CK_(at, STAGE, 49)] = e[u];
+            }
+        }
+        __syncthreads();
+        sort_classes<CK, LT>(a, L, in_chunk, c, pos - p0, dst);
+        __syncthreads();
+        rs = re;
+    }
+}
+#endif
+
 template <bool CK>
 __device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint32_t t) {
     const uint64_t m = __ballot(mine);
@@ -426,6 +485,14 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     bool ovf = false;
     const bool active = !(fl & TF_SLOW);
     unsigned long long* const wrows = a.rows + (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
+#ifdef TM_EMIT_LOG
+    // the wave's log: its rows region (entries) + a byte per entry (topic lane)
+    // past the whole rows array
+    const uint32_t lcap = a.tile_topics * a.row_cap;
+    uint8_t* const wlane =
+        reinterpret_cast<uint8_t*>(a.rows + (uint64_t)a.grid * lcap) + (uint64_t)blockIdx.x * lcap;
+    uint32_t lcount = 0;
+#endif
     uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
     const uint32_t d_me = L.depth[lane];
 
@@ -448,10 +515,21 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, meta | x.pf0, ROOT, (x.pf0 & M_PLUS) ? W_PLUS : wid);
         if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, meta | x.pf1, ROOT, (x.pf1 & M_PLUS) ? W_PLUS : wid);
         qn += __popcll(b0) + __popcll(b1);
+#ifdef TM_EMIT_LOG
+        const uint64_t mr = __ballot(x.ne != 0);
+        if (x.ne) {   // at most one emission at the root ('#')
+            L.cnt[lane] = 1;
+            const uint32_t i = prefix_count(mr);
+            wrows[i] = (x.ek0 & KEY_MASK) | x.ef0;
+            wlane[i] = (uint8_t)lane;
+        }
+        lcount = (uint32_t)__popcll(mr);
+#else
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
             emit_row<CK>(a, wrows, lane, 0, x.ek0, x.ef0);
         }
+#endif
     }
 
     // ---- frontier loop: LIFO stack, up to 64 probes per iteration
@@ -589,11 +667,31 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         }
         if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key | ((uint64_t)dig_P(cls) << sh), nmeta | M_PLUS, s.child, W_PLUS);
         qn += ptot;
+#ifdef TM_EMIT_LOG
+        {
+            if (eA | eB) atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));   // row sizes
+            const uint64_t mA = __ballot(eA), mB = __ballot(eB);
+            const uint32_t nA = (uint32_t)__popcll(mA), nE = nA + (uint32_t)__popcll(mB);
+            if (lcount + nE > lcap) { ovf = true; break; }   // log full: the tile goes to the generic path
+            if (eA) {
+                const uint32_t i = lcount + prefix_count(mA);
+                wrows[i] = (kA & KEY_MASK) | fA;
+                wlane[i] = (uint8_t)tl;
+            }
+            if (eB) {
+                const uint32_t i = lcount + nA + prefix_count(mB);
+                wrows[i] = ((key | (2ull << sh)) & KEY_MASK) | s.hterm;
+                wlane[i] = (uint8_t)tl;
+            }
+            lcount += nE;
+        }
+#else
         if (eA | eB) {
             const uint32_t slot = atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));
             if (eA) emit_row<CK>(a, wrows, tl, slot, kA, fA);
             if (eB) emit_row<CK>(a, wrows, tl, slot + (eA ? 1u : 0u), key | (2ull << sh), s.hterm);
         }
+#endif
     }
     __syncthreads();
 #ifdef TM_EXPERIMENT_PHASES
@@ -631,7 +729,11 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if (fits) {
+#ifdef TM_EMIT_LOG
+        sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount);
+#else
         sort_rows<CK, LT>(a, L, keep, c, dst);
+#endif
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
     }
