@@ -35,8 +35,11 @@ init() ->
           end,
     erlang:load_nif(filename:join(Dir, "emqx_tm_nif"), 0).
 
--spec(new(non_neg_integer()) -> {ok, reference()} | {error, term()}).
-new(_Device) -> erlang:nif_error(nif_not_loaded).
+%% new(Device) binds one GPU; new([Device]) one engine over several GPUs (one
+%% host trie, an HBM replica on each, per-publish matches dealt over them and
+%% batch calls spread over them).  The async pipelines start here.
+-spec(new(non_neg_integer() | [non_neg_integer()]) -> {ok, reference()} | {error, term()}).
+new(_Devices) -> erlang:nif_error(nif_not_loaded).
 
 %% emqx_trie:insert/1
 -spec(insert(reference(), binary()) -> ok | {error, term()}).
