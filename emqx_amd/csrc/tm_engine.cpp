@@ -369,6 +369,13 @@ struct tm_batch {
     // the stream the batch runs on: async slots own one, other batches use the replica's
     hipStream_t own = nullptr;
     hipEvent_t ev_read = nullptr;   // own-stream batches: marks their walk for the replica's next upload
+    // the batch's whole pipeline (header clear, walk, generic path, scan,
+    // finalize, read-back of the control words) captured as a HIP graph and
+    // replayed while its launch arguments stay the same (small batches: one
+    // launch instead of ten API calls and their gaps)
+    hipGraphExec_t gexec = nullptr;
+    std::vector<uint8_t> gkey;      // the arguments gexec was captured with, or of the last direct launch
+    bool gbad = false;              // capture failed once: this batch launches directly
     bool own_user = false;   // TM_BATCH_STREAM: a caller's batch on a stream of its own (async slots: false)
     // generic-path scratch, per batch (batches on different streams run concurrently)
     uint32_t s_waves = 0, s_qcap = 1u << 13, s_ocap = 1u << 14;
@@ -472,6 +479,9 @@ struct tm_batch {
         if (evt) (void)hipEventDestroy(evt);
         if (ev_read) (void)hipEventDestroy(ev_read);
         ev0 = ev1 = ev2 = evt = ev_read = nullptr;
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        gexec = nullptr;
+        gkey.clear();
     }
 };
 
@@ -2894,7 +2904,8 @@ struct tm_engine {
             HIP_OK(hipMemsetAsync(R.d_dbg, 0, 8 * 4, S));
         }
         const bool tokenize_now = b->dev_tok && b->tok_dict != dict.size();
-        if (!tokenize_now) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
+        const bool graph = csr && !checked && !tokenize_now && use_graphs && !b->gbad && b->n <= GRAPH_MAX;
+        if (!tokenize_now && !graph) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
         b->tok_timed = tokenize_now && csr;
         if (b->tok_timed) HIP_OK(hipEventRecord(b->evt, S));
         if (tokenize_now) {
@@ -2946,25 +2957,86 @@ struct tm_engine {
         a.nnodes = (uint32_t)nd.size();
         a.nfbytes = fbytes.size();
         a.dbg = checked ? R.d_dbg : nullptr;
-        HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
-        note_launch(b);
-        b->launched = true;
-        b->done = false;
-        b->csr = csr;
-        if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
         ScanArgs s{};
         s.count = b->d_count; s.src = b->d_src;
         s.sfids = b->d_sfids; s.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? R.d_dbg : nullptr;
-        HIP_OK(launch_scan(s, S, b->d_total));
-        HIP_OK(launch_finalize(s, S, checked));
+        if (graph) {
+            int rc2 = launch_graph(b, a, s, S);
+            if (rc2 != 1) {
+                if (rc2) return rc2;
+                note_launch(b);
+                b->launched = true;
+                b->done = false;
+                b->csr = true;
+                b->scan_args = s;
+                return TM_OK;
+            }
+            HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
+        }
+        HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        note_launch(b);
+        b->launched = true;
+        b->done = false;
+        b->csr = csr;
+        if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
+        HIP_OK(enqueue_csr(b, s, S));
         b->scan_args = s;
-        HIP_OK(hipEventRecord(b->ev2, S));
-        HIP_OK(hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S));   // ctrl + stats
-        HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
+        return TM_OK;
+    }
+
+    // scan + finalize + the read-back of the control words (after the walk)
+    hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S) {
+        hipError_t e;
+        if ((e = launch_scan(s, S, b->d_total)) != hipSuccess) return e;
+        if ((e = launch_finalize(s, S, false)) != hipSuccess) return e;
+        if ((e = hipEventRecord(b->ev2, S)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S)) != hipSuccess)
+            return e;   // ctrl + stats
+        return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
+    }
+
+    // Replays the batch's captured pipeline, capturing it first when its
+    // arguments changed (tables moved or grew, the root record, the staging
+    // capacity...).  1: capture is unavailable, launch the direct way.
+    static constexpr uint32_t GRAPH_MAX = 1u << 20;
+    bool use_graphs = true;
+    int launch_graph(tm_batch* b, const MatchArgs& a, const ScanArgs& s, hipStream_t S) {
+        std::vector<uint8_t> key(sizeof(MatchArgs) + sizeof(ScanArgs));
+        memcpy(key.data(), &a, sizeof a);
+        memcpy(key.data() + sizeof a, &s, sizeof s);
+        if (!b->gexec || b->gkey != key) {
+            if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
+            b->gexec = nullptr;
+            if (b->gkey != key) {   // captured only when a launch repeats the last one's arguments
+                b->gkey.swap(key);
+                return 1;
+            }
+            hipGraph_t g = nullptr;
+            if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) != hipSuccess) {
+                (void)hipGetLastError();
+                b->gbad = true;
+                return 1;
+            }
+            hipError_t e = hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S);
+            if (e == hipSuccess) e = launch_match(a, S, b->ev0, b->ev1, false);
+            if (e == hipSuccess) e = enqueue_csr(b, s, S);
+            const hipError_t e2 = hipStreamEndCapture(S, &g);
+            if (e != hipSuccess || e2 != hipSuccess || !g ||
+                hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                (void)hipGetLastError();
+                b->gexec = nullptr;
+                b->gbad = true;
+                return 1;
+            }
+            (void)hipGraphDestroy(g);
+            b->gkey.swap(key);
+        }
+        HIP_OK(hipGraphLaunch(b->gexec, S));
         return TM_OK;
     }
 
@@ -3422,6 +3494,7 @@ struct tm_engine {
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
         if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');
+        if (const char* ng = getenv("TM_NO_GRAPH")) use_graphs = ng[0] != '1';
         // root node id 0 (absent until the first add_path, like the reference)
         nd.push_back(NodeRec{});
         n_flen.push_back(0);
