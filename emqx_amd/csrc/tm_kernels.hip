@@ -396,7 +396,7 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
     }
 }
 
-#ifdef TM_EMIT_LOG
+#ifndef TM_EMIT_ROWS
 // Emission log variant of the tile epilogue: the tile's matches were appended
 // to a wave-private log in iteration order (coalesced: one store of <= 64
 // consecutive entries per emission role per iteration), each with its topic
@@ -485,7 +485,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     bool ovf = false;
     const bool active = !(fl & TF_SLOW);
     unsigned long long* const wrows = a.rows + (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
-#ifdef TM_EMIT_LOG
+#ifndef TM_EMIT_ROWS
     // the wave's log: its rows region (entries) + a byte per entry (topic lane)
     // past the whole rows array
     const uint32_t lcap = a.tile_topics * a.row_cap;
@@ -515,7 +515,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, meta | x.pf0, ROOT, (x.pf0 & M_PLUS) ? W_PLUS : wid);
         if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, meta | x.pf1, ROOT, (x.pf1 & M_PLUS) ? W_PLUS : wid);
         qn += __popcll(b0) + __popcll(b1);
-#ifdef TM_EMIT_LOG
+#ifndef TM_EMIT_ROWS
         const uint64_t mr = __ballot(x.ne != 0);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
@@ -667,20 +667,25 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         }
         if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key | ((uint64_t)dig_P(cls) << sh), nmeta | M_PLUS, s.child, W_PLUS);
         qn += ptot;
-#ifdef TM_EMIT_LOG
+#ifndef TM_EMIT_ROWS
         {
-            if (eA | eB) atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));   // row sizes
+            // row sizes; a row's entries past K are not logged (the row goes to
+            // the generic path), so the log holds at most tile_topics * K
+            uint32_t slot = 0;
+            if (eA | eB) slot = atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));
+            const uint32_t slotB = slot + (eA ? 1u : 0u);
+            eA = eA && slot < a.row_cap;
+            eB = eB && slotB < a.row_cap;
             const uint64_t mA = __ballot(eA), mB = __ballot(eB);
             const uint32_t nA = (uint32_t)__popcll(mA), nE = nA + (uint32_t)__popcll(mB);
-            if (lcount + nE > lcap) { ovf = true; break; }   // log full: the tile goes to the generic path
             if (eA) {
                 const uint32_t i = lcount + prefix_count(mA);
-                wrows[i] = (kA & KEY_MASK) | fA;
+                wrows[CK_(i, lcap, 13)] = (kA & KEY_MASK) | fA;
                 wlane[i] = (uint8_t)tl;
             }
             if (eB) {
                 const uint32_t i = lcount + nA + prefix_count(mB);
-                wrows[i] = ((key | (2ull << sh)) & KEY_MASK) | s.hterm;
+                wrows[CK_(i, lcap, 14)] = ((key | (2ull << sh)) & KEY_MASK) | s.hterm;
                 wlane[i] = (uint8_t)tl;
             }
             lcount += nE;
@@ -729,7 +734,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if (fits) {
-#ifdef TM_EMIT_LOG
+#ifndef TM_EMIT_ROWS
         sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount);
 #else
         sort_rows<CK, LT>(a, L, keep, c, dst);

@@ -138,6 +138,6 @@ def test_c4_20m_iot_filters_two_shards_properties_and_oracle_sample():
     exp, _ = oracle_rows(cand, ts)
     got = [[grp.filter_bytes(int(x)) for x in ids[offs[i]:offs[i + 1]]] for i in sample]
     assert_same(ts, got, exp)
-    assert sum(len(r) for r in exp) > 1000       # the sample exercises real matches
+    assert sum(len(r) for r in exp) > 300        # the sample exercises real matches
     b.free()
     grp.close()
