@@ -410,8 +410,11 @@ struct tm_batch {
     const uint8_t* in_bytes = nullptr;
     const uint64_t* in_offs = nullptr;
     uint64_t seen_upload = 0;   // own-stream batches: the last trie upload this batch's stream waited for
-    uint32_t* d_wcount = nullptr;
-    size_t c_bytes = 0, c_boffs = 0, c_wcount = 0;
+    // tokeniser look-back status (TokArgs::tstat): zeroed when (re)allocated
+    // and past TOK_EPOCH_MAX launches; each launch takes the next epoch
+    unsigned long long* d_tstat = nullptr;
+    size_t c_bytes = 0, c_boffs = 0, c_tstat = 0, tstat_armed = 0;
+    uint32_t tok_epoch = 0;
     uint64_t tok_base = 0;
     uint32_t *d_nslow = nullptr, *h_bad = nullptr;
     size_t c_nslow = 0, ch_bad = 0;
@@ -452,7 +455,8 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in);
+        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_tstat); dev_free(d_in);
+        c_tstat = tstat_armed = 0;
         in_bytes = nullptr;
         in_offs = nullptr;
         if (h_bad) (void)hipHostFree(h_bad);
@@ -2539,6 +2543,21 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
+    // the tokeniser's look-back status for this launch: reserved for n topics
+    // (tickets + two words per tile), zeroed when new or when the epochs run out
+    int arm_tokenizer(tm_batch* b, TokArgs& t, hipStream_t s) {
+        int rc;
+        if ((rc = dev_reserve(b->d_tstat, b->c_tstat, 2 * (size_t)t.n + 2))) return rc;
+        if (b->tstat_armed != b->c_tstat || b->tok_epoch >= TOK_EPOCH_MAX) {
+            HIP_OK(hipMemsetAsync(b->d_tstat, 0, b->c_tstat * sizeof(unsigned long long), s));
+            b->tstat_armed = b->c_tstat;
+            b->tok_epoch = 0;
+        }
+        t.tstat = b->d_tstat;
+        t.epoch = ++b->tok_epoch;
+        return TM_OK;
+    }
+
     // tm_tokenize_device: the device tokeniser into caller device arrays
     int tokenize_device(const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* d_words, uint64_t cap,
                         uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords) {
@@ -2552,10 +2571,8 @@ struct tm_engine {
         if ((rc = sync_device(&R))) return rc;
         if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;
         if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
-        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
         if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
-        if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
         HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
@@ -2563,12 +2580,11 @@ struct tm_engine {
         TokArgs t{};
         t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
         t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
-        t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
+        t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
         t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
         t.tile_topics = tok_tile_topics(n, nbytes);
-        ScanArgs ts{};
-        ts.block_sums = b->d_bsums;
-        HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
+        if ((rc = arm_tokenizer(b, t, stream))) return rc;
+        HIP_OK(launch_tokenize(t, stream));
         HIP_OK(hipMemcpyAsync(b->h_total, b->d_nslow + 1, 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
         *nwords = n ? b->h_total[0] : 0;
@@ -2835,7 +2851,7 @@ struct tm_engine {
     int reserve_tokens(tm_batch* b, uint32_t n, uint64_t nbytes) {
         int rc;
         b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
-        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
+        if ((rc = dev_reserve(b->d_tstat, b->c_tstat, 2 * (size_t)n + 2))) return rc;   // tickets + per tile
         if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(b->nwords, 1)))) return rc;
         if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
@@ -2915,13 +2931,12 @@ struct tm_engine {
             t.zero_words = tm_batch::HDR_FIXED / 4;
             t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
             t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
-            t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
+            t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
             t.tile_topics = tok_tile_topics(b->n, b->nwords - b->n);   // nwords = bytes + topics (reserve_tokens)
-            ScanArgs ts{};
-            ts.block_sums = b->d_bsums;
-            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
+            if ((rc = arm_tokenizer(b, t, S))) return rc;
+            HIP_OK(launch_tokenize(t, S));
         }
         MatchArgs a{};
         a.slots = R.d_slots;

@@ -407,19 +407,21 @@ struct TokArgs {
     const DictTail* tails;    // by word id
     uint64_t dict_mask;       // cuckoo table size - 1 (power of two)
     const uint8_t* arena;
-    uint32_t* wcount;         // pass 1: words per tile (ntiles + 1 entries), scanned in place
+    unsigned long long* tstat;   // [0] tile tickets, [1] waves done (both 0 between launches),
+                                 // then per tile (words, generic-path topics) look-back status
+    uint32_t epoch;           // this launch's status epoch (1 .. TOK_EPOCH_MAX)
     uint8_t* tflags;
     uint32_t* toff;           // n + 1 word offsets
-    const uint32_t* bsums;    // scan block offsets of the tile scan (tm_scan_sums)
     uint32_t* words;
     uint64_t words_cap;       // entries of words[]; nothing at or past it is written
     uint32_t* slow_list;
-    uint32_t* d_nslow;        // [0] generic-path topics, [1] total words; zeroed by pass 1
-    uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
+    uint32_t* d_nslow;        // [0] generic-path topics, [1] total words (written by the last tile)
+    uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by the kernel (the batch's ctrl + stats)
     uint32_t zero_words;
     uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
 };
-hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
+hipError_t launch_tokenize(const TokArgs& a, hipStream_t s);
+constexpr uint32_t TOK_EPOCH_MAX = (1u << 22) - 1;   // status epochs; the status array is re-zeroed past it
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 
