@@ -2543,18 +2543,26 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
-    // the tokeniser's look-back status for this launch: reserved for n topics
-    // (tickets + two words per tile), zeroed when new or when the epochs run out
+    // a ticket / look-back status array (tb_* in tm_kernels.hip) for `words`
+    // per-tile words: zeroed when (re)allocated and before its epochs wrap
+    static int arm_status(unsigned long long*& p, size_t& cap, size_t& armed, uint32_t& launches, size_t words,
+                          hipStream_t s) {
+        int rc;
+        if ((rc = dev_reserve(p, cap, words + TB_HEAD_WORDS))) return rc;
+        if (armed != cap || launches >= TB_EPOCH_LAUNCHES) {
+            HIP_OK(hipMemsetAsync(p, 0, cap * sizeof(unsigned long long), s));
+            armed = cap;
+            launches = 0;
+        }
+        ++launches;
+        return TM_OK;
+    }
+
     int arm_tokenizer(tm_batch* b, TokArgs& t, hipStream_t s) {
         int rc;
-        if ((rc = dev_reserve(b->d_tstat, b->c_tstat, 2 * (size_t)t.n + 2))) return rc;
-        if (b->tstat_armed != b->c_tstat || b->tok_epoch >= TOK_EPOCH_MAX) {
-            HIP_OK(hipMemsetAsync(b->d_tstat, 0, b->c_tstat * sizeof(unsigned long long), s));
-            b->tstat_armed = b->c_tstat;
-            b->tok_epoch = 0;
-        }
+        const size_t ntiles = ((size_t)t.n + t.tile_topics - 1) / std::max<uint32_t>(t.tile_topics, 1);
+        if ((rc = arm_status(b->d_tstat, b->c_tstat, b->tstat_armed, b->tok_epoch, 2 * ntiles, s))) return rc;
         t.tstat = b->d_tstat;
-        t.epoch = ++b->tok_epoch;
         return TM_OK;
     }
 
@@ -2851,7 +2859,6 @@ struct tm_engine {
     int reserve_tokens(tm_batch* b, uint32_t n, uint64_t nbytes) {
         int rc;
         b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
-        if ((rc = dev_reserve(b->d_tstat, b->c_tstat, 2 * (size_t)n + 2))) return rc;   // tickets + per tile
         if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(b->nwords, 1)))) return rc;
         if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;

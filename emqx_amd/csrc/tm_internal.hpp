@@ -407,9 +407,8 @@ struct TokArgs {
     const DictTail* tails;    // by word id
     uint64_t dict_mask;       // cuckoo table size - 1 (power of two)
     const uint8_t* arena;
-    unsigned long long* tstat;   // [0] tile tickets, [1] waves done (both 0 between launches),
-                                 // then per tile (words, generic-path topics) look-back status
-    uint32_t epoch;           // this launch's status epoch (1 .. TOK_EPOCH_MAX)
+    unsigned long long* tstat;   // ticket / look-back status array (tb_* in tm_kernels.hip):
+                                 // 4 header words, then (words, generic-path topics) per tile
     uint8_t* tflags;
     uint32_t* toff;           // n + 1 word offsets
     uint32_t* words;
@@ -421,7 +420,10 @@ struct TokArgs {
     uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
 };
 hipError_t launch_tokenize(const TokArgs& a, hipStream_t s);
-constexpr uint32_t TOK_EPOCH_MAX = (1u << 22) - 1;   // status epochs; the status array is re-zeroed past it
+// launches of a ticket / look-back kernel on one status array before the host
+// zeroes it again (the device-held epoch has 22 bits)
+constexpr uint32_t TB_EPOCH_LAUNCHES = (1u << 22) - 2;
+constexpr uint32_t TB_HEAD_WORDS = 4;
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 

@@ -69,6 +69,50 @@ __device__ __forceinline__ uint32_t prefix_count(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// ---- ticket-ordered tiles with a decoupled look-back (tm_tok_tiles, tm_csr)
+//
+// A wave takes tiles by ticket (one atomic per tile), so every tile a wave
+// waits for was taken by a wave that is running and that publishes its
+// aggregate before waiting for anything: no residency assumption, no
+// deadlock, whatever else shares the GPU.  A tile publishes its aggregate,
+// then sums its predecessors back to the nearest inclusive prefix (64 per
+// step, one per lane) and publishes that.  Status array (u64):
+//   [0] tickets  [1] waves done  [2] epoch  [3] -  [TB_HEAD ..] per-tile words
+// A status word is epoch (22 bits) | flag (2) | value (40).  The epoch lives
+// in device memory and the last wave out advances it (and clears the ticket
+// counters), so the previous launch's words read as "not yet", nothing is
+// cleared per launch, and the kernel's arguments stay the same from launch to
+// launch (a captured graph replays it).  The host zeroes the array when it is
+// allocated and again before the epochs wrap (TB_EPOCH_LAUNCHES).
+constexpr uint32_t TB_AGG = 1, TB_INCL = 2, TB_HEAD = 4;
+constexpr unsigned long long TB_VALUE = (1ull << 40) - 1;
+
+__device__ __forceinline__ unsigned long long tb_pack(uint32_t epoch, uint32_t flag, uint64_t v) {
+    return ((unsigned long long)epoch << 42) | ((unsigned long long)flag << 40) | (v & TB_VALUE);
+}
+__device__ __forceinline__ uint32_t tb_flag(unsigned long long w, uint32_t epoch) {
+    return (uint32_t)(w >> 42) == epoch ? (uint32_t)(w >> 40) & 3u : 0u;
+}
+__device__ __forceinline__ void tb_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long tb_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t tb_ticket(unsigned long long* ctr) {
+    uint32_t t = 0;
+    if (threadIdx.x == 0) t = (uint32_t)atomicAdd(ctr, 1ull);
+    return __shfl(t, 0, 64);
+}
+// the last wave out (every wave has taken its last ticket) rearms the counters
+__device__ __forceinline__ void tb_exit(unsigned long long* ctr, uint32_t epoch) {
+    if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
+        ctr[0] = 0;
+        ctr[1] = 0;
+        ctr[2] = epoch + 1u < (1u << 22) ? epoch + 1u : 1u;   // 22 bits
+    }
+}
+
 // Bounds-checked debug variant: an out-of-range index is recorded (first
 // failing check id, index, bound) and clamped to 0 instead of faulting.
 template <bool CK>
@@ -2007,52 +2051,38 @@ __device__ __forceinline__ uint32_t topic_words_global(const uint8_t* p, uint64_
     return nw;
 }
 
-// ---- tile order and offsets: tickets + decoupled look-back
-//
-// Tiles are taken in ticket order (one atomic per tile), so any tile a wave
-// waits for belongs to a wave that is running and waits for nothing later:
-// no residency assumption, no deadlock.  A tile publishes its word and
-// generic-path counts as soon as its topics are split (an aggregate); after
-// its dictionary lookups it sums its predecessors back to the nearest
-// inclusive prefix (64 per step, one per lane) and publishes its own.  A
-// status word is epoch (22 bits) | flag (2) | value (40): the previous
-// launch's words carry another epoch and read as "not yet", so nothing is
-// cleared per launch.
-constexpr uint32_t TS_AGG = 1, TS_INCL = 2;
-constexpr unsigned long long TS_VALUE = (1ull << 40) - 1;
+// ---- tile order and offsets: tickets + decoupled look-back (see tb_* above).
+// A tile publishes its word and generic-path counts as soon as its topics are
+// split (an aggregate); after its dictionary lookups it sums its predecessors
+// back to the nearest inclusive prefix and publishes its own.
 
-__device__ __forceinline__ unsigned long long ts_pack(uint32_t epoch, uint32_t flag, uint64_t v) {
-    return ((unsigned long long)epoch << 42) | ((unsigned long long)flag << 40) | (v & TS_VALUE);
-}
-
-__device__ __forceinline__ void tok_publish(const TokArgs& a, uint32_t tile, uint32_t flag, uint64_t w, uint64_t s) {
+__device__ __forceinline__ void tok_publish(const TokArgs& a, uint32_t epoch, uint32_t tile, uint32_t flag, uint64_t w,
+                                            uint64_t s) {
     if (threadIdx.x == 0) {
-        unsigned long long* st = a.tstat + 2 + 2 * (uint64_t)tile;
-        __hip_atomic_store(st, ts_pack(a.epoch, flag, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(st + 1, ts_pack(a.epoch, flag, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long* st = a.tstat + TB_HEAD + 2 * (uint64_t)tile;
+        tb_store(st, tb_pack(epoch, flag, w));
+        tb_store(st + 1, tb_pack(epoch, flag, s));
     }
 }
 
 // exclusive (words, generic-path topics) prefixes of `tile` (> 0)
-__device__ __forceinline__ void tok_lookback(const TokArgs& a, uint32_t tile, uint64_t& pw, uint64_t& ps) {
+__device__ __forceinline__ void tok_lookback(const TokArgs& a, uint32_t epoch, uint32_t tile, uint64_t& pw, uint64_t& ps) {
     const uint32_t lane = threadIdx.x;
     uint64_t aw = 0, as = 0;
     int64_t j = (int64_t)tile - 1;   // lane i reads tile j - i
     for (;;) {
         const int64_t k = j - (int64_t)lane;
-        uint32_t f = TS_INCL;   // before tile 0: an inclusive 0
+        uint32_t f = TB_INCL;   // before tile 0: an inclusive 0
         uint64_t vw = 0, vs = 0;
         if (k >= 0) {
-            const unsigned long long* st = a.tstat + 2 + 2 * (uint64_t)k;
-            const unsigned long long w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long s = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t fw = (uint32_t)(w >> 42) == a.epoch ? (uint32_t)(w >> 40) & 3u : 0u;
-            const uint32_t fs = (uint32_t)(s >> 42) == a.epoch ? (uint32_t)(s >> 40) & 3u : 0u;
+            const unsigned long long* st = a.tstat + TB_HEAD + 2 * (uint64_t)k;
+            const unsigned long long w = tb_load(st), s = tb_load(st + 1);
+            const uint32_t fw = tb_flag(w, epoch), fs = tb_flag(s, epoch);
             f = fw == fs ? fw : 0u;   // a pair caught between its two stores reads as "not yet"
-            vw = w & TS_VALUE;
-            vs = s & TS_VALUE;
+            vw = w & TB_VALUE;
+            vs = s & TB_VALUE;
         }
-        const uint64_t inc = __ballot(f == TS_INCL);
+        const uint64_t inc = __ballot(f == TB_INCL);
         const uint32_t lim = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;   // lanes 0..lim are summed
         if (__ballot(f == 0u && lane <= lim)) {   // a predecessor has not published yet
             __builtin_amdgcn_s_sleep(2);
@@ -2090,7 +2120,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;
     const uint32_t ntiles = (a.n + tt - 1) / tt;
-    unsigned long long* const ctr = a.tstat;   // [0] tickets, [1] waves done
+    unsigned long long* const ctr = a.tstat;   // tb_* layout
+    const uint32_t epoch = (uint32_t)tb_load(ctr + 2);
     if (ntiles == 0 && blockIdx.x == 0) {   // empty batch: control words and totals only
         for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
         if (lane < 2) a.d_nslow[lane] = 0;
@@ -2216,14 +2247,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
         const bool slow = (fl & TF_SLOW) != 0;
         const uint64_t smask = __ballot(slow);
         const uint32_t ns = (uint32_t)__popcll(smask);
-        tok_publish(a, tile, tile == 0 ? TS_INCL : TS_AGG, tw, ns);
+        tok_publish(a, epoch, tile, tile == 0 ? TB_INCL : TB_AGG, tw, ns);
 #ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
         if (lds) tok_lookup(a, L, tw, wend);   // the tile's words, round-robin over lanes -> L.went
 #endif
         uint64_t pw = 0, ps = 0;
         if (tile) {
-            tok_lookback(a, tile, pw, ps);
-            tok_publish(a, tile, TS_INCL, pw + tw, ps + ns);
+            tok_lookback(a, epoch, tile, pw, ps);
+            tok_publish(a, epoch, tile, TB_INCL, pw + tw, ps + ns);
         }
         if (tend == a.n && lane == 0) {   // the batch's totals
             a.toff[a.n] = (uint32_t)(pw + tw);
@@ -2247,10 +2278,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             tok_fill_topic_global(a, t, o, sl);
         }
     }
-    if (lane == 0 && atomicAdd(ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
-        ctr[0] = 0;   // every wave has taken its last ticket: rearm for the next launch
-        ctr[1] = 0;
-    }
+    tb_exit(ctr, epoch);
 }
 
 
