@@ -410,11 +410,8 @@ struct tm_batch {
     const uint8_t* in_bytes = nullptr;
     const uint64_t* in_offs = nullptr;
     uint64_t seen_upload = 0;   // own-stream batches: the last trie upload this batch's stream waited for
-    // tokeniser look-back status (TokArgs::tstat): zeroed when (re)allocated
-    // and past TOK_EPOCH_MAX launches; each launch takes the next epoch
-    unsigned long long* d_tstat = nullptr;
-    size_t c_bytes = 0, c_boffs = 0, c_tstat = 0, tstat_armed = 0;
-    uint32_t tok_epoch = 0;
+    uint32_t* d_wcount = nullptr;
+    size_t c_bytes = 0, c_boffs = 0, c_wcount = 0;
     uint64_t tok_base = 0;
     uint32_t *d_nslow = nullptr, *h_bad = nullptr;
     size_t c_nslow = 0, ch_bad = 0;
@@ -455,8 +452,7 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_tstat); dev_free(d_in);
-        c_tstat = tstat_armed = 0;
+        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in);
         in_bytes = nullptr;
         in_offs = nullptr;
         if (h_bad) (void)hipHostFree(h_bad);
@@ -2543,29 +2539,6 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
-    // a ticket / look-back status array (tb_* in tm_kernels.hip) for `words`
-    // per-tile words: zeroed when (re)allocated and before its epochs wrap
-    static int arm_status(unsigned long long*& p, size_t& cap, size_t& armed, uint32_t& launches, size_t words,
-                          hipStream_t s) {
-        int rc;
-        if ((rc = dev_reserve(p, cap, words + TB_HEAD_WORDS))) return rc;
-        if (armed != cap || launches >= TB_EPOCH_LAUNCHES) {
-            HIP_OK(hipMemsetAsync(p, 0, cap * sizeof(unsigned long long), s));
-            armed = cap;
-            launches = 0;
-        }
-        ++launches;
-        return TM_OK;
-    }
-
-    int arm_tokenizer(tm_batch* b, TokArgs& t, hipStream_t s) {
-        int rc;
-        const size_t ntiles = ((size_t)t.n + t.tile_topics - 1) / std::max<uint32_t>(t.tile_topics, 1);
-        if ((rc = arm_status(b->d_tstat, b->c_tstat, b->tstat_armed, b->tok_epoch, 2 * ntiles, s))) return rc;
-        t.tstat = b->d_tstat;
-        return TM_OK;
-    }
-
     // tm_tokenize_device: the device tokeniser into caller device arrays
     int tokenize_device(const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint32_t* d_words, uint64_t cap,
                         uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords) {
@@ -2579,8 +2552,10 @@ struct tm_engine {
         if ((rc = sync_device(&R))) return rc;
         if ((rc = dev_reserve(b->d_bytes, b->c_bytes, nbytes + 16))) return rc;
         if ((rc = dev_reserve(b->d_boffs, b->c_boffs, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
         if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
+        if ((rc = dev_reserve(b->d_bsums, b->c_bsums, (size_t)scan_block_count(n) + 1))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         if (nbytes) HIP_OK(hipMemcpyAsync(b->d_bytes, topics + base, nbytes, hipMemcpyHostToDevice, stream));
         HIP_OK(hipMemcpyAsync(b->d_boffs, offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, stream));
@@ -2588,11 +2563,12 @@ struct tm_engine {
         TokArgs t{};
         t.bytes = b->d_bytes; t.offs = b->d_boffs; t.base = base; t.n = n;
         t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
-        t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
+        t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
         t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
         t.tile_topics = tok_tile_topics(n, nbytes);
-        if ((rc = arm_tokenizer(b, t, stream))) return rc;
-        HIP_OK(launch_tokenize(t, stream));
+        ScanArgs ts{};
+        ts.block_sums = b->d_bsums;
+        HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
         HIP_OK(hipMemcpyAsync(b->h_total, b->d_nslow + 1, 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
         *nwords = n ? b->h_total[0] : 0;
@@ -2859,6 +2835,7 @@ struct tm_engine {
     int reserve_tokens(tm_batch* b, uint32_t n, uint64_t nbytes) {
         int rc;
         b->nwords = nbytes + n;                  // bound: one word per byte + 1 per topic
+        if ((rc = dev_reserve(b->d_wcount, b->c_wcount, (size_t)n + 2))) return rc;   // per tile + total
         if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(b->nwords, 1)))) return rc;
         if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
         if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
@@ -2938,12 +2915,13 @@ struct tm_engine {
             t.zero_words = tm_batch::HDR_FIXED / 4;
             t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
             t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
-            t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
+            t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
             t.tile_topics = tok_tile_topics(b->n, b->nwords - b->n);   // nwords = bytes + topics (reserve_tokens)
-            if ((rc = arm_tokenizer(b, t, S))) return rc;
-            HIP_OK(launch_tokenize(t, S));
+            ScanArgs ts{};
+            ts.block_sums = b->d_bsums;
+            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
         }
         MatchArgs a{};
         a.slots = R.d_slots;

@@ -407,23 +407,19 @@ struct TokArgs {
     const DictTail* tails;    // by word id
     uint64_t dict_mask;       // cuckoo table size - 1 (power of two)
     const uint8_t* arena;
-    unsigned long long* tstat;   // ticket / look-back status array (tb_* in tm_kernels.hip):
-                                 // 4 header words, then (words, generic-path topics) per tile
+    uint32_t* wcount;         // pass 1: words per tile (ntiles + 1 entries), scanned in place
     uint8_t* tflags;
     uint32_t* toff;           // n + 1 word offsets
+    const uint32_t* bsums;    // scan block offsets of the tile scan (tm_scan_sums)
     uint32_t* words;
     uint64_t words_cap;       // entries of words[]; nothing at or past it is written
     uint32_t* slow_list;
-    uint32_t* d_nslow;        // [0] generic-path topics, [1] total words (written by the last tile)
-    uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by the kernel (the batch's ctrl + stats)
+    uint32_t* d_nslow;        // [0] generic-path topics, [1] total words; zeroed by pass 1
+    uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
     uint32_t zero_words;
     uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
 };
-hipError_t launch_tokenize(const TokArgs& a, hipStream_t s);
-// launches of a ticket / look-back kernel on one status array before the host
-// zeroes it again (the device-held epoch has 22 bits)
-constexpr uint32_t TB_EPOCH_LAUNCHES = (1u << 22) - 2;
-constexpr uint32_t TB_HEAD_WORDS = 4;
+hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 

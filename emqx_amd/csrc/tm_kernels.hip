@@ -69,50 +69,6 @@ __device__ __forceinline__ uint32_t prefix_count(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// ---- ticket-ordered tiles with a decoupled look-back (tm_tok_tiles, tm_csr)
-//
-// A wave takes tiles by ticket (one atomic per tile), so every tile a wave
-// waits for was taken by a wave that is running and that publishes its
-// aggregate before waiting for anything: no residency assumption, no
-// deadlock, whatever else shares the GPU.  A tile publishes its aggregate,
-// then sums its predecessors back to the nearest inclusive prefix (64 per
-// step, one per lane) and publishes that.  Status array (u64):
-//   [0] tickets  [1] waves done  [2] epoch  [3] -  [TB_HEAD ..] per-tile words
-// A status word is epoch (22 bits) | flag (2) | value (40).  The epoch lives
-// in device memory and the last wave out advances it (and clears the ticket
-// counters), so the previous launch's words read as "not yet", nothing is
-// cleared per launch, and the kernel's arguments stay the same from launch to
-// launch (a captured graph replays it).  The host zeroes the array when it is
-// allocated and again before the epochs wrap (TB_EPOCH_LAUNCHES).
-constexpr uint32_t TB_AGG = 1, TB_INCL = 2, TB_HEAD = 4;
-constexpr unsigned long long TB_VALUE = (1ull << 40) - 1;
-
-__device__ __forceinline__ unsigned long long tb_pack(uint32_t epoch, uint32_t flag, uint64_t v) {
-    return ((unsigned long long)epoch << 42) | ((unsigned long long)flag << 40) | (v & TB_VALUE);
-}
-__device__ __forceinline__ uint32_t tb_flag(unsigned long long w, uint32_t epoch) {
-    return (uint32_t)(w >> 42) == epoch ? (uint32_t)(w >> 40) & 3u : 0u;
-}
-__device__ __forceinline__ void tb_store(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long tb_load(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t tb_ticket(unsigned long long* ctr) {
-    uint32_t t = 0;
-    if (threadIdx.x == 0) t = (uint32_t)atomicAdd(ctr, 1ull);
-    return __shfl(t, 0, 64);
-}
-// the last wave out (every wave has taken its last ticket) rearms the counters
-__device__ __forceinline__ void tb_exit(unsigned long long* ctr, uint32_t epoch) {
-    if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
-        ctr[0] = 0;
-        ctr[1] = 0;
-        ctr[2] = epoch + 1u < (1u << 22) ? epoch + 1u : 1u;   // 22 bits
-    }
-}
-
 // Bounds-checked debug variant: an out-of-range index is recorded (first
 // failing check id, index, bound) and clamped to 0 instead of faulting.
 template <bool CK>
@@ -591,10 +547,14 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const uint32_t qd = lane >> 2, qs = lane & 3;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<Slot*>(a.slots), 0, BIG ? 0u : a.nslots * 16u, 0x00020000);
-#ifdef TM_EXPERIMENT_PHASES   // (timing experiments only: cycles per phase into the H / W stats)
+#ifdef TM_EXPERIMENT_PHASES   // (timing experiments only: cycles per phase into the H / W stats, iterations into V)
     const uint64_t ph0 = __builtin_amdgcn_s_memtime();
+    uint32_t iters = 0;
 #endif
     while (qn > 0) {
+#ifdef TM_EXPERIMENT_PHASES
+        ++iters;
+#endif
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         qn -= k;
@@ -746,6 +706,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
 #ifdef TM_EXPERIMENT_PHASES
     tW = 0;
     tH = lane == 0 ? (uint32_t)(__builtin_amdgcn_s_memtime() - ph0) : 0u;   // frontier loop
+    tV = lane == 0 ? iters : 0u;
 #endif
 
     if (ovf) {
@@ -1794,16 +1755,20 @@ __global__ void tm_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t*
 // emqx_topic:words/1 (src/emqx_topic.erl:150-164: binary:split on "/", '' / '+'
 // / '#' as their atoms) plus the engine's interning, on the device: the same
 // word entries (class << 29 | id), flags and generic-path list as the host
-// tokeniser (tm_engine.cpp tokenize_range).  ONE kernel, tm_tok_tiles: a
-// wavefront per tile of 64 topics (bytes contiguous in the batch), tiles taken
-// by ticket.  The tile's bytes are staged in LDS by coalesced loads; word
-// starts come from bit masks ('/' bytes, topic starts) and one wave scan;
-// then the lanes take the tile's WORDS round-robin -- class, reserved atoms,
-// dictionary probe with the first 8 bytes compared inline.  The tile's output
-// offsets (words, generic-path list) come from a decoupled look-back over the
-// tiles before it, so there is no count pass and no scan kernel, and the
-// words leave LDS as one coalesced run.  Tiles too long for the LDS budget
-// take a lane-per-topic path that reads the bytes from HBM.
+// tokeniser (tm_engine.cpp tokenize_range).  One wavefront per tile of 64
+// topics, whose bytes are contiguous in the batch:
+//   tm_tok_count  words per tile = '/' bytes in the tile's range + topics,
+//                 counted from coalesced dword loads (bit tricks, no per-byte
+//                 loop); also clears the launch's control words;
+//   (scan of the tile counts)
+//   tm_tok_fill   the tile's bytes are staged in LDS by coalesced loads; each
+//                 lane splits its own topic there (word starts / lengths into
+//                 an LDS list, flags, in-tile word offsets by a wave scan);
+//                 then the lanes take the tile's WORDS round-robin -- class,
+//                 reserved atoms, dictionary probe with the first 8 bytes
+//                 compared inline -- and the tile's words leave LDS as one
+//                 coalesced run.  Tiles too long for the LDS budget take a
+//                 lane-per-topic path that reads the bytes from HBM.
 
 constexpr uint32_t TOK_LANE_BYTES = 48;                 // bytes of the window each lane splits
 constexpr uint32_t TOK_BYTES = 64 * TOK_LANE_BYTES;     // LDS bytes per tile (16-B aligned window)
@@ -1900,6 +1865,70 @@ __device__ __forceinline__ uint32_t slash_mask16(const uint4& x) {
            (gather4(byte_eq(x.w, '/')) << 12);
 }
 
+constexpr uint32_t TOK_RUN = 63;   // tiles per count run (their 64 boundaries: one per lane)
+
+// pass 1: words per tile = '/' bytes + topics.  Each wave takes a contiguous
+// run of tiles (a slice of the grid's share, TOK_RUN at a time): their
+// boundaries in one vector load, then the run's bytes streamed with four
+// 16-B loads per lane in flight; each lane walks a cursor over the boundaries
+// and adds its chunks' '/' counts to the tiles' LDS counters.  Block 0 also
+// clears the launch's control words.
+__global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
+    __shared__ uint64_t bnd[TOK_RUN + 1];
+    __shared__ uint32_t cnt[TOK_RUN];
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x == 0) {   // the launch's control words (kernels after this one use them)
+        if (lane < 2) a.d_nslow[lane] = 0;
+        for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
+    }
+    const uint32_t tt = a.tile_topics;
+    const uint32_t ntiles = (a.n + tt - 1) / tt;
+    const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    const uint32_t first = blockIdx.x * per, last = min(first + per, ntiles);
+    for (uint32_t run = first; run < last; run += TOK_RUN) {
+        const uint32_t K = min(TOK_RUN, last - run);
+        if (lane <= K) bnd[lane] = a.offs[min((run + lane) * tt, a.n)] - a.base;
+        if (lane < K) cnt[lane] = 0;
+        __syncthreads();
+        const uint64_t B0 = bnd[0], BK = bnd[K], a0 = B0 & ~15ull;
+        uint32_t j = 0;   // my cursor: the tile of my current chunk
+        for (uint64_t p0 = a0 + 16u * lane; p0 < BK; p0 += 4096) {
+            uint4 x[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint64_t p = p0 + 1024u * u;
+                x[u] = p < BK ? *reinterpret_cast<const uint4*>(a.bytes + p) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint64_t p = p0 + 1024u * u;
+                if (p >= BK) break;
+                uint32_t m = slash_mask16(x[u]);
+                if (p < B0) m &= ~0u << (uint32_t)(B0 - p);
+                if (p + 16 > BK) m &= (1u << (uint32_t)(BK - p)) - 1u;
+                while (j + 1 < K && bnd[j + 1] <= p) ++j;
+                while (m) {   // bits up to the next boundary belong to tile j
+                    const uint64_t lim = j + 1 < K ? bnd[j + 1] - p : 16u;
+                    if (lim >= 16) {
+                        atomicAdd(&cnt[j], (uint32_t)__popc(m));
+                        break;
+                    }
+                    const uint32_t below = m & ((1u << (uint32_t)lim) - 1u);
+                    if (below) atomicAdd(&cnt[j], (uint32_t)__popc(below));
+                    m &= ~((1u << (uint32_t)lim) - 1u);
+                    ++j;
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < K) {
+            const uint32_t t0 = (run + lane) * tt;
+            a.wcount[run + lane] = cnt[lane] + (min(t0 + tt, a.n) - t0);
+        }
+        __syncthreads();
+    }
+}
+
 struct alignas(16) TokLds {
     uint8_t bytes[TOK_BYTES + 32];      // the tile's window; + 32: 8-byte reads past a word stay inside
     uint64_t tsb[TOK_BYTES / 64 + 1];   // topic-start bitmap of the window (+1: a lane's bits may straddle)
@@ -1907,7 +1936,6 @@ struct alignas(16) TokLds {
     uint8_t wtop[TOK_WORDS];            // tile-local topic of each word
     uint32_t ttoff[TILE + 1];           // tile-local first word of each topic; [cnt] = words
     uint32_t tirr[TILE];                // a word of the topic starts with '+' but is not '+'
-    uint32_t went[TOK_WORDS];           // the tile's word entries, written out once its offset is known
 };
 
 // 8 bytes at byte offset s of a 4-aligned LDS array (any alignment of s)
@@ -1938,8 +1966,9 @@ constexpr uint32_t TOK_WPL = TM_TOK_WPL;   // words per lane per lookup round (r
 // primary holds another word (cuckoo slots never empty again once filled, so
 // an empty primary slot means the word is absent).  Lookups are bound by L2
 // requests, not instructions: one per word is the point.
-// Entries (class << 29 | id) go to L.went.
-__device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw, uint32_t wend) {
+// Entries (class << 29 | id) go straight to words[].
+__device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw, uint32_t wend,
+                                           uint64_t tile_base) {
     const uint32_t lane = threadIdx.x;
     const uint32_t mask = (uint32_t)a.dict_mask;
     for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
@@ -1959,7 +1988,8 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
             const uint32_t n = (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u);
             const uint8_t c0 = n ? L.bytes[s0] : 0;
             bool irr = false;
-            ent[k] = tok_class(c0, n, irr) << WID_BITS;   // (irregular words: the tile's pre-pass marks them)
+            ent[k] = tok_class(c0, n, irr) << WID_BITS;
+            if (irr) L.tirr[L.wtop[w]] = 1;
             if (n == 0) { ent[k] |= W_EMPTY; continue; }
             if (n == 1 && c0 == '+') { ent[k] |= W_PLUS; continue; }
             if (n == 1 && c0 == '#') { ent[k] |= W_HASH; continue; }
@@ -2006,7 +2036,7 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
             if ((pend >> k & 1u) && ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) ent[k] |= e[k].w;
             const uint32_t w = base + lane + 64 * k;
-            if (w < tw) L.went[w] = ent[k];
+            if (w < tw && tile_base + w < a.words_cap) a.words[tile_base + w] = ent[k];
         }
     }
 }
@@ -2035,111 +2065,24 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
     slow = (fl & TF_SLOW) != 0;
 }
 
-// words of topic [b, e) read from HBM (long tiles), and whether one of them
-// starts with '+' but is longer (the topic then takes the generic path)
-__device__ __forceinline__ uint32_t topic_words_global(const uint8_t* p, uint64_t b, uint64_t e, bool& irregular) {
-    uint32_t nw = 1;
-    uint64_t ws = b;
-    for (uint64_t i = b; i < e; ++i) {
-        if (p[i] == '/') {
-            if (i - ws > 1 && p[ws] == '+') irregular = true;
-            ++nw;
-            ws = i + 1;
-        }
-    }
-    if (e - ws > 1 && p[ws] == '+') irregular = true;
-    return nw;
-}
-
-// ---- tile order and offsets: tickets + decoupled look-back (see tb_* above).
-// A tile publishes its word and generic-path counts as soon as its topics are
-// split (an aggregate); after its dictionary lookups it sums its predecessors
-// back to the nearest inclusive prefix and publishes its own.
-
-__device__ __forceinline__ void tok_publish(const TokArgs& a, uint32_t epoch, uint32_t tile, uint32_t flag, uint64_t w,
-                                            uint64_t s) {
-    if (threadIdx.x == 0) {
-        unsigned long long* st = a.tstat + TB_HEAD + 2 * (uint64_t)tile;
-        tb_store(st, tb_pack(epoch, flag, w));
-        tb_store(st + 1, tb_pack(epoch, flag, s));
-    }
-}
-
-// exclusive (words, generic-path topics) prefixes of `tile` (> 0)
-__device__ __forceinline__ void tok_lookback(const TokArgs& a, uint32_t epoch, uint32_t tile, uint64_t& pw, uint64_t& ps) {
-    const uint32_t lane = threadIdx.x;
-    uint64_t aw = 0, as = 0;
-    int64_t j = (int64_t)tile - 1;   // lane i reads tile j - i
-    for (;;) {
-        const int64_t k = j - (int64_t)lane;
-        uint32_t f = TB_INCL;   // before tile 0: an inclusive 0
-        uint64_t vw = 0, vs = 0;
-        if (k >= 0) {
-            const unsigned long long* st = a.tstat + TB_HEAD + 2 * (uint64_t)k;
-            const unsigned long long w = tb_load(st), s = tb_load(st + 1);
-            const uint32_t fw = tb_flag(w, epoch), fs = tb_flag(s, epoch);
-            f = fw == fs ? fw : 0u;   // a pair caught between its two stores reads as "not yet"
-            vw = w & TB_VALUE;
-            vs = s & TB_VALUE;
-        }
-        const uint64_t inc = __ballot(f == TB_INCL);
-        const uint32_t lim = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;   // lanes 0..lim are summed
-        if (__ballot(f == 0u && lane <= lim)) {   // a predecessor has not published yet
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        if (lane > lim) {
-            vw = 0;
-            vs = 0;
-        }
-        for (int o = 32; o; o >>= 1) {
-            vw += __shfl_xor(vw, o, 64);
-            vs += __shfl_xor(vs, o, 64);
-        }
-        aw += vw;
-        as += vs;
-        if (inc) break;
-        j -= 64;
-    }
-    pw = aw;
-    ps = as;
-}
-
-// One pass: a wave takes tiles by ticket; per tile it splits the topics
-// (LDS path: the tile's bytes staged by coalesced loads, word starts from bit
-// masks and one wave scan), publishes its counts, looks its words up in the
-// dictionary, takes its offsets from the look-back, and writes words, word
-// offsets, flags and generic-path entries in place.  No count pass, no scan
-// kernels.  The wave holding tile 0 clears the launch's control words; the
-// last wave out rearms the ticket counters for the next launch.
+// pass 2 (after the scan of the tile counts): word entries, offsets, flags
 #ifndef TM_TOK_WPE
 #define TM_TOK_WPE 5
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_tiles(TokArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
     __shared__ TokLds L;
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;
     const uint32_t ntiles = (a.n + tt - 1) / tt;
-    unsigned long long* const ctr = a.tstat;   // tb_* layout
-    const uint32_t epoch = (uint32_t)tb_load(ctr + 2);
-    if (ntiles == 0 && blockIdx.x == 0) {   // empty batch: control words and totals only
-        for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
-        if (lane < 2) a.d_nslow[lane] = 0;
-        if (lane == 0) a.toff[0] = 0;
-    }
-    for (;;) {
-        uint32_t tile = 0;
-        if (lane == 0) tile = (uint32_t)atomicAdd(ctr, 1ull);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= ntiles) break;
-        if (tile == 0)
-            for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n), cnt = tend - t0;
         const uint32_t t = t0 + lane;
         const bool valid = lane < cnt;
         const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
         const uint64_t my_b = valid ? a.offs[t] - a.base : 0, my_e = valid ? a.offs[t + 1] - a.base : 0;
         const uint64_t a0 = b0 & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
+        const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
+        bool slow = false;
         // the LDS path: the window fits and no topic is empty (an empty topic
         // starts where the next one does: one bit cannot mark both)
         bool lds = b1 - a0 <= TOK_BYTES && !__any(valid && my_b == my_e);
@@ -2194,7 +2137,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             }
         }
         uint32_t nw = 0, tincl = 0;
-        uint8_t fl = 0;
+        if (!lds) {
+            // long tile: one lane per topic, bytes from HBM; in-tile offsets by
+            // a wave scan of the per-topic word counts ('/' + 1)
+            if (valid) {
+                nw = 1;
+                for (uint64_t i = my_b; i < my_e; ++i) nw += a.bytes[i] == '/';
+            }
+            tincl = nw;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(tincl, o, 64);
+                if (lane >= (uint32_t)o) tincl += u;
+            }
+            tw = __shfl(tincl, 63, 64);
+        }
+        if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
         if (lds) {
             uint32_t wi = (incl - mine) & 0xFFFFu;            // my first word
             int32_t tc = (int32_t)((incl - mine) >> 16) - 1;   // the topic my first byte is in
@@ -2216,71 +2173,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             }
             if (lane == 0) L.ttoff[cnt] = tw;
             __syncthreads();
-            // a word that starts with '+' but is longer sends its topic to the generic path
-            for (uint32_t w = lane; w < tw; w += 64) {
-                const uint32_t s0 = L.wst[w] & 0x7FFFu;
-                const uint32_t nx = w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u);
-                const uint32_t n = (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u);
-                if (n > 1 && L.bytes[s0] == '+') L.tirr[L.wtop[w]] = 1;
-            }
+#ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
+            tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
+#endif
             __syncthreads();
             if (valid) {
+                const uint32_t w0 = L.ttoff[lane], tn = L.ttoff[lane + 1] - w0;
+                uint8_t fl = 0;
                 if (L.bytes[my_b - a0] == '$') fl |= TF_DOLLAR;
-                if (L.tirr[lane] || L.ttoff[lane + 1] - L.ttoff[lane] > FAST_MAX_DEPTH) fl |= TF_SLOW;
-            }
-        } else {
-            // long tile: one lane per topic, bytes from HBM; in-tile offsets by
-            // a wave scan of the per-topic word counts
-            if (valid) {
-                bool irr = false;
-                nw = topic_words_global(a.bytes, my_b, my_e, irr);
-                if (my_e > my_b && a.bytes[my_b] == '$') fl |= TF_DOLLAR;
-                if (irr || nw > FAST_MAX_DEPTH) fl |= TF_SLOW;
-            }
-            tincl = nw;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(tincl, o, 64);
-                if (lane >= (uint32_t)o) tincl += u;
-            }
-            tw = __shfl(tincl, 63, 64);
-        }
-        const bool slow = (fl & TF_SLOW) != 0;
-        const uint64_t smask = __ballot(slow);
-        const uint32_t ns = (uint32_t)__popcll(smask);
-        tok_publish(a, epoch, tile, tile == 0 ? TB_INCL : TB_AGG, tw, ns);
-#ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
-        if (lds) tok_lookup(a, L, tw, wend);   // the tile's words, round-robin over lanes -> L.went
-#endif
-        uint64_t pw = 0, ps = 0;
-        if (tile) {
-            tok_lookback(a, epoch, tile, pw, ps);
-            tok_publish(a, epoch, tile, TB_INCL, pw + tw, ps + ns);
-        }
-        if (tend == a.n && lane == 0) {   // the batch's totals
-            a.toff[a.n] = (uint32_t)(pw + tw);
-            a.d_nslow[0] = (uint32_t)(ps + ns);
-            a.d_nslow[1] = (uint32_t)(pw + tw);
-        }
-        if (slow) a.slow_list[ps + prefix_count(smask)] = t;
-        if (lds) {
-            __syncthreads();   // every lane's entries are in L.went
-            for (uint32_t w = lane; w < tw; w += 64)
-                if (pw + w < a.words_cap) a.words[pw + w] = L.went[w];
-            if (valid) {
+                if (L.tirr[lane] || tn > FAST_MAX_DEPTH) fl |= TF_SLOW;
                 a.tflags[t] = fl;
-                a.toff[t] = (uint32_t)(pw + L.ttoff[lane]);
+                a.toff[t] = (uint32_t)(tile_base + w0);
+                slow = (fl & TF_SLOW) != 0;
             }
-            __syncthreads();   // the LDS is the next tile's
-        } else if (valid) {
-            const uint64_t o = pw + tincl - nw;
-            a.toff[t] = (uint32_t)o;
-            bool sl = false;
-            tok_fill_topic_global(a, t, o, sl);
+            tok_append_slow(a, slow, t);
+            __syncthreads();
+        } else {
+            const uint64_t o = tile_base + tincl - nw;
+            if (valid) {
+                a.toff[t] = (uint32_t)o;
+                tok_fill_topic_global(a, t, o, slow);
+            }
+            tok_append_slow(a, slow, t);
         }
     }
-    tb_exit(ctr, epoch);
 }
-
 
 // Read-back of an async batch in ONE kernel, written straight into pinned host
 // memory: the header block's first hdr_words (ctrl + stats + src), the counts,
@@ -2523,10 +2440,20 @@ static uint32_t resident_blocks(K kernel, int block) {
     return (uint32_t)(cus * per);
 }
 
-hipError_t launch_tokenize(const TokArgs& a, hipStream_t s) {
-    static const uint32_t cap = resident_blocks(tm_tok_tiles, 64);
+hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
+    static const uint32_t cap_count = resident_blocks(tm_tok_count, 64);
+    static const uint32_t cap_fill = resident_blocks(tm_tok_fill, 64);
     const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
-    hipLaunchKernelGGL(tm_tok_tiles, dim3(ntiles ? min(ntiles, cap) : 1u), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(tm_tok_count, dim3(ntiles ? min(ntiles, cap_count) : 1u), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
+    if (!a.n) return hipGetLastError();
+    scan.count = a.wcount;
+    scan.row_off = a.wcount;   // in place: tile counts -> block-local tile offsets
+    scan.n = ntiles;
+    const hipError_t e = launch_scan(scan, s, d_nwords);
+    if (e != hipSuccess) return e;
+    TokArgs f = a;
+    f.bsums = scan.block_sums;
+    hipLaunchKernelGGL(tm_tok_fill, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
     return hipGetLastError();
 }
 

@@ -1,0 +1,32 @@
+"""C5 churn apply on the host mirror alone (dev tool; TM_PAR_TRACE=1 prints
+the parallel phases): 10k deltas per step, K filters per hot topic.
+
+    python tools/churn_prof.py [K] [steps]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from emqx_amd import gen  # noqa: E402
+from emqx_amd.engine import Engine  # noqa: E402
+from emqx_amd.skew import Churn, workload  # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+p = gen.SkewParams(k_per_hot=K)
+allf, derived, hot, pubs = workload(p, 100_000, 100_000, seed=5)
+eng = Engine(device=-1)
+eng.insert_many(allf)
+churn = Churn(hot, derived.tolist(), seed=11)
+deltas = []
+for _ in range(steps):
+    dels, adds = churn.step(10_000)
+    deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
+for d, a in deltas:
+    t = time.perf_counter()
+    eng.delete_many(d)
+    t1 = time.perf_counter()
+    eng.insert_many(a)
+    t2 = time.perf_counter()
+    print(f"K={K} del {1e3 * (t1 - t):.2f} ms  ins {1e3 * (t2 - t1):.2f} ms  total {1e3 * (t2 - t):.2f}", flush=True)
