@@ -7,8 +7,12 @@ Workload: 1,000,000 distinct wildcard filters
 the HBM trie replica; a batch of 10,000,000 synthetic publishes per GPU
 (seed 1000 + rank), tokenised + interned on the host and resident in HBM before
 timing.  One step = the whole device pipeline over the batch: frontier-walk
-kernel, generic slow path, CSR scan and sorted-row finalize -- every topic's
-complete, byte-sorted match set lands in HBM.
+kernel and generic slow path -- every topic's complete, byte-sorted,
+deduplicated match set lands in HBM as the walk's rows (tm_batch_rows: per
+topic a count and a start in the staging array; the per-publish path consumes
+them there).  The dense CSR (row offsets + ids in topic order: scan + one copy,
+built on request by tm_batch_result / routes / dispatch / export) is timed
+beside it as "dense_csr".
 
 Multi-GPU: one process per GPU (torchrun), the trie replicated on every GPU,
 each rank matching its own 10M batch (replicated mode, no data-path
@@ -873,6 +877,22 @@ def main():
         "matches_per_step": st["matches"],
         "slow_path_topics": st["slow_topics"],
     }
+
+    # the same steps with the dense CSR built after every wait (scan + copy
+    # of every row into topic order, tm_batch_device_csr): what a consumer
+    # that indexes the result by offsets pays per batch
+    if nb == 1:
+        csr_ms = []
+        t2 = time.perf_counter()
+        for _ in range(args.steps):
+            b.launch().wait()
+            b.device_csr()
+            csr_ms.append(b.stats()["ms_csr"])
+        e2 = time.perf_counter() - t2
+        if sync is not None:
+            e2 = sync.allmax(e2)
+        out["dense_csr"] = {"publishes_per_s": ws * n * args.steps / e2, "ms_per_step": 1e3 * e2 / args.steps,
+                            "csr_ms": float(np.mean(csr_ms))}
 
     if nb == 1 and not args.profile:
         # two batches in flight on streams of their own (TM_BATCH_STREAM): one

@@ -75,7 +75,8 @@ class BatchStats(C.Structure):
     _fields_ = [("topics", C.c_uint64), ("visits", C.c_uint64), ("hash_hits", C.c_uint64),
                 ("words", C.c_uint64), ("matches", C.c_uint64), ("slow_topics", C.c_uint64),
                 ("overflow_tiles", C.c_uint64), ("ms_match", C.c_float), ("ms_total", C.c_float),
-                ("ms_tokenize", C.c_float), ("probes", C.c_uint64)]
+                ("ms_tokenize", C.c_float), ("probes", C.c_uint64),
+                ("ms_csr", C.c_float)]
 
     def asdict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -139,6 +140,7 @@ SIGNATURES = {
     "tm_batch_result": (C.c_int, [P, P, C.POINTER(Result)]),
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
+    "tm_batch_rows": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_free": (None, [P, P]),
     "tm_batch_retokenize": (C.c_int, [P, P]),
     "tm_route_add": (C.c_int, [P, U8P, SZ, C.c_uint32]),

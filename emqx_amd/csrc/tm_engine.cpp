@@ -101,13 +101,31 @@ class WordDict {
         ck_rebuild(1024);
     }
 
-    uint32_t find(const uint8_t* p, size_t n) const {
+    uint32_t find(const uint8_t* p, size_t n) const { return find_h(p, n, hash_word(p, n)); }
+
+    // the hash of a word, its home entry prefetched (batched lookups: hash
+    // and prefetch a group of words, then find_h each)
+    uint64_t prefetch(const uint8_t* p, size_t n) const {
         const uint64_t h = hash_word(p, n);
+        __builtin_prefetch(&tab_[h & mask_]);
+        return h;
+    }
+
+    uint32_t find_h(const uint8_t* p, size_t n, uint64_t h) const {
         size_t i = h & mask_;
         for (;;) {
             const DictEnt& e = tab_[i];
             if (e.h == 0) return W_UNKNOWN;
-            if (e.h == h && e.len == n && memcmp(arena_.data() + e.off, p, n) == 0) return e.id;
+            if (e.h == h && e.len == n) {
+                // up to 16 bytes compare inline (head, head2), longer words in the arena
+                if (n <= 16) {
+                    if (e.head == le_bytes(p, (uint32_t)std::min<size_t>(n, 8)) &&
+                        e.head2 == (n > 8 ? le_bytes(p + 8, (uint32_t)(n - 8)) : 0))
+                        return e.id;
+                } else if (memcmp(arena_.data() + e.off, p, n) == 0) {
+                    return e.id;
+                }
+            }
             i = (i + 1) & mask_;
         }
     }
@@ -384,6 +402,10 @@ struct tm_batch {
     size_t c_sq = 0, c_so = 0, c_sq2 = 0, c_sq3 = 0, c_so2 = 0, c_sq4 = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     hipEvent_t evt = nullptr;   // before the device tokeniser (fresh launches)
+    hipEvent_t evc0 = nullptr, evc1 = nullptr;   // around the dense-CSR pass (ensure_dense)
+    // the waited result is the walk's own: row i = sfids[src[i] .. + count[i]);
+    // dense = the CSR (row_off, ids) has been built from it since the last launch
+    bool dense = false;
     bool tok_timed = false;     // the last launch tokenised: evt..ev0 is its time
     bool launched = false, done = false;
     bool csr = true;   // the last launch built the CSR (false: async, rows left in staging)
@@ -478,7 +500,9 @@ struct tm_batch {
         if (ev2) (void)hipEventDestroy(ev2);
         if (evt) (void)hipEventDestroy(evt);
         if (ev_read) (void)hipEventDestroy(ev_read);
-        ev0 = ev1 = ev2 = evt = ev_read = nullptr;
+        if (evc0) (void)hipEventDestroy(evc0);
+        if (evc1) (void)hipEventDestroy(evc1);
+        ev0 = ev1 = ev2 = evt = ev_read = evc0 = evc1 = nullptr;
         if (gexec) (void)hipGraphExecDestroy(gexec);
         gexec = nullptr;
         gkey.clear();
@@ -619,53 +643,60 @@ struct Replica {
 // Persistent host workers of the bulk mutations: run(f) calls f(0..n-1) with
 // f(0) on the calling thread, so a delta batch pays no thread start-up for
 // each of its phases.
+// The engine's host workers (bulk plans and parallel churn).  A bulk call
+// runs several short jobs back to back (plan, node records, edge ranges,
+// summaries, merges: 0.1-1 ms each), so starting a job must be cheap: the
+// workers sleep on a futex over the job counter (one FUTEX_WAKE starts them
+// all, no mutex for them to queue on after waking) and the caller sleeps on
+// the busy count.  Only a short spin before each sleep: the box runs under a
+// CFS CPU quota, where spinning threads would burn the quota and throttle.
 struct WorkPool {
     unsigned n = 1;
     std::vector<std::thread> th;
-    std::mutex mu;
-    std::condition_variable cv, cv_done;
     const std::function<void(unsigned)>* job = nullptr;
-    uint64_t gen = 0;
-    unsigned busy = 0;
-    bool stop = false;
+    std::atomic<uint32_t> gen{0};
+    std::atomic<uint32_t> busy{0};
+    std::atomic<bool> stop{false};
 
+    static long futex(std::atomic<uint32_t>* a, int op, uint32_t v) {
+        return syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), op | FUTEX_PRIVATE_FLAG, v, nullptr, nullptr, 0);
+    }
+    static bool spin_until_changed(const std::atomic<uint32_t>& a, uint32_t v) {
+        for (int i = 0; i < 2048; ++i) {
+            if (a.load(std::memory_order_acquire) != v) return true;
+            __builtin_ia32_pause();
+        }
+        return false;
+    }
     void start(unsigned k) {
         n = std::max(1u, k);
         for (unsigned i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
     }
     void loop(unsigned i) {
-        uint64_t seen = 0;
-        std::unique_lock<std::mutex> lk(mu);
+        uint32_t seen = 0;
         for (;;) {
-            cv.wait(lk, [&] { return stop || gen != seen; });
-            if (stop) return;
-            seen = gen;
-            const std::function<void(unsigned)>* f = job;
-            lk.unlock();
-            (*f)(i);
-            lk.lock();
-            if (--busy == 0) cv_done.notify_all();
+            while (gen.load(std::memory_order_acquire) == seen && !stop.load(std::memory_order_acquire))
+                if (!spin_until_changed(gen, seen)) futex(&gen, FUTEX_WAIT, seen);
+            if (stop.load(std::memory_order_acquire)) return;
+            seen = gen.load(std::memory_order_acquire);
+            (*job)(i);
+            if (busy.fetch_sub(1, std::memory_order_acq_rel) == 1) futex(&busy, FUTEX_WAKE, 1);
         }
     }
     void run(const std::function<void(unsigned)>& f) {
         if (n <= 1) { f(0); return; }
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            job = &f;
-            busy = n - 1;
-            ++gen;
-        }
-        cv.notify_all();
+        job = &f;
+        busy.store(n - 1, std::memory_order_release);
+        gen.fetch_add(1, std::memory_order_acq_rel);
+        futex(&gen, FUTEX_WAKE, INT32_MAX);
         f(0);
-        std::unique_lock<std::mutex> lk(mu);
-        cv_done.wait(lk, [&] { return busy == 0; });
+        for (uint32_t b; (b = busy.load(std::memory_order_acquire)) != 0;)
+            if (!spin_until_changed(busy, b)) futex(&busy, FUTEX_WAIT, b);
     }
     ~WorkPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            stop = true;
-        }
-        cv.notify_all();
+        stop.store(true, std::memory_order_release);
+        gen.fetch_add(1, std::memory_order_acq_rel);
+        futex(&gen, FUTEX_WAKE, INT32_MAX);
         for (auto& t : th) t.join();
     }
 };
@@ -681,7 +712,9 @@ struct Mut {
     bool defer = false;
     std::vector<uint32_t>* ids = nullptr;               // the batch's node ids: free ones, then fresh ones
     std::atomic<size_t>* next_id = nullptr;             //   (shared by the workers)
-    size_t n_free = 0, fresh_base = 0;
+    size_t n_free = 0, fresh_base = 0, n_fresh = 0;
+    static constexpr size_t ID_CHUNK = 16;
+    size_t id_lo = 0, id_hi = 0;                        // this worker's current chunk of the batch's ids
     std::vector<std::array<uint32_t, 3>> ins;           // deferred insert_edge(p, w, c)
     std::vector<std::pair<uint32_t, uint32_t>> del;     // deferred delete_edge_of(c): (c, its slot then)
     std::vector<uint32_t> sum;                          // deferred write_summary(c)
@@ -718,9 +751,10 @@ struct Mut {
     int64_t live_nodes = 0, n_filters = 0, live_edges = 0, used_slots = 0, route_entries = 0;
     uint32_t max_disp = 0;
     uint64_t version = 0, done = 0;
+    double t_us = 0;                                    // phase-1 time (TM_PAR_TRACE)
+    size_t n_items = 0;
     bool routes_dirty = false;
     int rc = TM_OK;
-    std::vector<uint32_t> items;                        // phase 1: the batch entries of this worker
 };
 thread_local Mut* tl_mut = nullptr;
 
@@ -1020,7 +1054,21 @@ struct tm_engine {
     uint32_t new_node(uint32_t parent, uint32_t word) {
         uint32_t id;
         if (Mut* M = tl_mut) {   // a parallel batch: the free ids of the batch first, then fresh ones
-            const size_t k = M->next_id->fetch_add(1, std::memory_order_relaxed);
+            if (M->id_lo == M->id_hi) {
+                // a chunk of ids at a time (no line shared with another worker's
+                // fresh records), their records prefetched when taken
+                M->id_lo = M->next_id->fetch_add(Mut::ID_CHUNK, std::memory_order_relaxed);
+                M->id_hi = M->id_lo + Mut::ID_CHUNK;
+                for (size_t k = M->id_lo; k < M->id_hi; ++k) {
+                    const size_t j = k < M->n_free ? (*M->ids)[k] : M->fresh_base + (k - M->n_free);
+                    if (j >= nd.size()) break;
+                    __builtin_prefetch(&nd[j], 1);
+                    __builtin_prefetch(&n_flen[j], 1);
+                    if (j < dirty_f_mark.size()) __builtin_prefetch(&dirty_f_mark[j], 1);
+                }
+            }
+            const size_t k = M->id_lo++;
+            if (k >= M->n_free + M->n_fresh) throw std::bad_alloc();   // (the batch's need was counted up front)
             id = k < M->n_free ? (*M->ids)[k] : (uint32_t)(M->fresh_base + (k - M->n_free));
             nd[id].hasbytes = 0;
             nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
@@ -1214,9 +1262,19 @@ struct tm_engine {
             if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
             uint32_t c = NONE;
             if (M && M->defer) {   // an edge made earlier in this batch is not in the hash yet
-                c = M->made_get((uint64_t)p << 32 | w);
+                // (levels 0-1: made by any worker, held in the stripe's shared map)
+                if (k < 2) {
+                    const auto& sm = shared_made[p & 63];
+                    const auto it = sm.find((uint64_t)p << 32 | w);
+                    if (it != sm.end()) c = it->second;
+                } else {
+                    c = M->made_get((uint64_t)p << 32 | w);
+                }
             }
-            if (c == NONE) {
+            // The edge hash is frozen during phase 1 of a parallel insert and the
+            // plan's walk stopped at level k0 on a miss, so every deeper parent
+            // is a node of this batch: only the made maps can hold its edges.
+            if (c == NONE && !(M && M->defer) && !created) {
                 const uint32_t s = nd[p].live ? find_slot(p, w) : NONE;
                 if (s != NONE) c = slots[s].child & ID_MASK;
             }
@@ -1239,6 +1297,7 @@ struct tm_engine {
                 if (w == W_PLUS) nd[p].plus = c;
                 else if (w == W_HASH) nd[p].hash = c;
                 insert_edge(p, w, c);
+                if (M && M->defer && k < 2) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
                 write_summary(p);
             }
             p = c;
@@ -1319,6 +1378,10 @@ struct tm_engine {
     // filter's node (killed ids are not reused before the pass ends).
     std::recursive_mutex shared_mus[64];   // the records of depth < 2 during a parallel batch, striped by node id
     std::recursive_mutex& shared_mu(uint32_t id) { return shared_mus[id & 63]; }
+    // edges of levels 0-1 created in phase 1 of a parallel insert, by any
+    // worker: (parent << 32 | word) -> child, striped like shared_mus (a
+    // worker reads and writes stripe p & 63 only under shared_mu(p))
+    std::unordered_map<uint64_t, uint32_t> shared_made[64];
     WorkPool pool;            // workers of parallel batches (started at the first one)
     bool pool_started = false;
 
@@ -1330,39 +1393,78 @@ struct tm_engine {
     };
     std::vector<PlanEnt> plan;
     std::vector<std::vector<uint32_t>> plan_words;
+    std::vector<std::vector<TWord>> plan_tw;   // a plan group's words, per part
 
+    // Plans filters lo..hi-1 in groups of PLAN_G: the group's words are split
+    // and hashed with their dictionary entries prefetched, then resolved; the
+    // existing paths are walked level by level for the whole group, every
+    // filter's next bucket prefetched before any is probed -- PLAN_G
+    // independent cache misses in flight instead of one chain per filter.
+    static constexpr uint32_t PLAN_G = 16;
     void plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part) {
         std::vector<uint32_t>& W = plan_words[part];
         W.clear();
         std::vector<TWord> ws;
+        std::vector<uint64_t> hs;
         const bool root_live = nd[ROOT].live != 0;
-        for (uint32_t i = lo; i < hi; ++i) {
-            PlanEnt& pe = plan[i];
-            split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
-            pe.woff = (uint32_t)W.size();
-            pe.nw = (uint32_t)ws.size();
-            pe.part = part;
-            bool known = true;
-            for (const TWord& w : ws) {
-                const uint32_t id = w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find(w.p, w.n);
-                known &= id != W_UNKNOWN;
-                W.push_back(id);
-            }
-            // walk the existing path (words up to the first unknown one)
-            uint32_t n = ROOT, k = 0;
-            if (root_live) {
-                const uint32_t nb = nbuckets();
-                for (; k < pe.nw; ++k) {
-                    const uint32_t w = W[pe.woff + k];
-                    if (w == W_UNKNOWN) break;
-                    if (k + 1 < pe.nw) __builtin_prefetch(&slots[(size_t)home_bucket(n, w, nb) * BUCKET]);
-                    const uint32_t sl = find_slot(n, w);
-                    if (sl == NONE) break;
-                    n = slots[sl].child & ID_MASK;
+        const uint32_t nb = nbuckets();
+        for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
+            const uint32_t g1 = std::min(hi, g0 + PLAN_G);
+            // words and their dictionary entries
+            const uint32_t wbase = (uint32_t)W.size();
+            hs.clear();
+            std::vector<TWord>& all = plan_tw[part];
+            all.clear();
+            for (uint32_t i = g0; i < g1; ++i) {
+                PlanEnt& pe = plan[i];
+                split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
+                pe.woff = wbase + (uint32_t)all.size();
+                pe.nw = (uint32_t)ws.size();
+                pe.part = part;
+                for (const TWord& w : ws) {
+                    all.push_back(w);
+                    hs.push_back(w.n == 0 || is_plus(w) || is_hash(w) ? 0 : dict.prefetch(w.p, w.n));
                 }
             }
-            if (del) pe.node = (root_live && known && k == pe.nw) ? n : NONE;
-            else { pe.node = n; pe.depth = k; }
+            for (size_t j = 0; j < all.size(); ++j) {
+                const TWord& w = all[j];
+                W.push_back(w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find_h(w.p, w.n, hs[j]));
+            }
+            // the existing paths, level by level over the group
+            uint32_t node[PLAN_G], k[PLAN_G];
+            bool run[PLAN_G], known[PLAN_G];
+            const uint32_t G = g1 - g0;
+            for (uint32_t q = 0; q < G; ++q) {
+                const PlanEnt& pe = plan[g0 + q];
+                node[q] = ROOT;
+                k[q] = 0;
+                known[q] = true;
+                for (uint32_t j = 0; j < pe.nw; ++j) known[q] &= W[pe.woff + j] != W_UNKNOWN;
+                run[q] = root_live;
+            }
+            for (bool any = root_live; any;) {
+                any = false;
+                for (uint32_t q = 0; q < G; ++q) {
+                    const PlanEnt& pe = plan[g0 + q];
+                    if (!run[q]) continue;
+                    if (k[q] >= pe.nw || W[pe.woff + k[q]] == W_UNKNOWN) { run[q] = false; continue; }
+                    __builtin_prefetch(&slots[(size_t)home_bucket(node[q], W[pe.woff + k[q]], nb) * BUCKET]);
+                }
+                for (uint32_t q = 0; q < G; ++q) {
+                    if (!run[q]) continue;
+                    const PlanEnt& pe = plan[g0 + q];
+                    const uint32_t sl = find_slot(node[q], W[pe.woff + k[q]]);
+                    if (sl == NONE) { run[q] = false; continue; }
+                    node[q] = slots[sl].child & ID_MASK;
+                    ++k[q];
+                    any = true;
+                }
+            }
+            for (uint32_t q = 0; q < G; ++q) {
+                PlanEnt& pe = plan[g0 + q];
+                if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
+                else { pe.node = node[q]; pe.depth = k[q]; }
+            }
         }
     }
 
@@ -1370,6 +1472,7 @@ struct tm_engine {
         plan.resize(n);
         const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 512));
         if (plan_words.size() < nt) plan_words.resize(nt);
+        if (plan_tw.size() < nt) plan_tw.resize(nt);
         if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
         ensure_pool();   // the engine's workers (no thread start-up per batch)
         pool.run([&](unsigned i) {
@@ -1616,12 +1719,21 @@ struct tm_engine {
         }
         ensure_pool();
         std::vector<Mut> W(T);
-        for (uint32_t i = 0; i < n; ++i) {   // by the first two words: a worker owns those subtrees
+        // by the first two words: one worker owns those subtrees; 8 parts per
+        // worker, taken largest first by whichever worker is free (skewed
+        // churn clusters under a few first words)
+        const uint32_t P = 8 * T;
+        std::vector<std::vector<uint32_t>> parts(P);
+        for (uint32_t i = 0; i < n; ++i) {
             const PlanEnt& pe = plan[i];
             const uint32_t* w = plan_words[pe.part].data() + pe.woff;
             const uint32_t key = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
-            W[mix_word(key) % T].items.push_back(i);
+            parts[mix_word(key) % P].push_back(i);
         }
+        std::vector<uint32_t> porder(P);
+        for (uint32_t q = 0; q < P; ++q) porder[q] = q;
+        std::sort(porder.begin(), porder.end(), [&](uint32_t a, uint32_t b) { return parts[a].size() > parts[b].size(); });
+        std::atomic<uint32_t> next_part{0};
         // node ids: at most the levels the batch's filters lack, the free ids first
         std::vector<uint32_t> ids;
         std::atomic<size_t> next_id{0};
@@ -1632,7 +1744,7 @@ struct tm_engine {
             uint64_t total = 0;
             for (uint32_t i = 0; i < n; ++i) total += plan[i].nw - plan[i].depth;
             const size_t take = std::min<size_t>(total, free_nodes.size());
-            fresh = total - take;
+            fresh = total - take + (size_t)T * Mut::ID_CHUNK;   // + slack: ids are taken a chunk per worker
             if (base + fresh >= MAX_NODES) return 1;
             ids.assign(free_nodes.end() - (long)take, free_nodes.end());
             free_nodes.resize(free_nodes.size() - take);
@@ -1647,36 +1759,44 @@ struct tm_engine {
             m.ids = &ids;
             m.next_id = &next_id;
             m.n_free = ids.size();
+            m.n_fresh = fresh;
             m.fresh_base = base;
         }
+        for (auto& sm : shared_made) sm.clear();
         const auto tp0 = std::chrono::steady_clock::now();
         // phase 1: node records, by first word
         pool.run([&](unsigned t) {
             Mut& m = W[t];
             m.defer = true;
             tl_mut = &m;
+            const auto tw0 = std::chrono::steady_clock::now();
             try {
-                const size_t ni = m.items.size();
-                for (size_t q = 0; q < ni; ++q) {
-                    const uint32_t i = m.items[q];
-                    if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
-                        const uint32_t f = plan[m.items[q + 8]].node;
-                        if (f != NONE) __builtin_prefetch(&nd[f]);
+                for (uint32_t pi; !m.rc && (pi = next_part.fetch_add(1)) < P;) {
+                    const std::vector<uint32_t>& items = parts[porder[pi]];
+                    const size_t ni = items.size();
+                    m.n_items += ni;
+                    for (size_t q = 0; q < ni; ++q) {
+                        const uint32_t i = items[q];
+                        if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
+                            const uint32_t f = plan[items[q + 8]].node;
+                            if (f != NONE) __builtin_prefetch(&nd[f]);
+                        }
+                        const PlanEnt& pe = plan[i];
+                        int rc;
+                        if (del) {
+                            rc = delete_planned(i);
+                        } else {
+                            rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
+                                                 plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth);
+                        }
+                        if (rc) { m.rc = rc; break; }
+                        ++m.done;
                     }
-                    const PlanEnt& pe = plan[i];
-                    int rc;
-                    if (del) {
-                        rc = delete_planned(i);
-                    } else {
-                        rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
-                                             plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth);
-                    }
-                    if (rc) { m.rc = rc; break; }
-                    ++m.done;
                 }
             } catch (...) {
                 m.rc = TM_ENOMEM;
             }
+            m.t_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
             tl_mut = nullptr;
         });
         const auto tp1 = std::chrono::steady_clock::now();
@@ -1704,7 +1824,15 @@ struct tm_engine {
                 for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
         });
         if (!del) {   // ids not handed out: free ones back to the list, the fresh tail cut off
-            const size_t used = next_id.load();
+            // (the rest of each worker's last chunk: free-list ids go back; fresh
+            // ids below the highest one handed out stay as free dead records)
+            size_t used = 0;
+            for (const Mut& m : W) used = std::max(used, m.id_lo);   // highest id index handed out + 1
+            const size_t avail = ids.size() + fresh;
+            if (used > avail) used = avail;
+            for (const Mut& m : W)
+                for (size_t k = m.id_lo; k < std::min(m.id_hi, used); ++k)
+                    free_nodes.push_back(k < ids.size() ? ids[k] : (uint32_t)(base + (k - ids.size())));
             for (size_t k = used; k < ids.size(); ++k) free_nodes.push_back(ids[k]);
             const size_t fresh_used = used > ids.size() ? used - ids.size() : 0;
             if (fresh_used < fresh) {
@@ -1719,8 +1847,10 @@ struct tm_engine {
         if (getenv("TM_PAR_TRACE")) {
             const auto tp3 = std::chrono::steady_clock::now();
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "[par %s n=%u T=%u] phase1 %.2f ms edges %.2f ms merge %.2f ms\n", del ? "del" : "ins", n, T,
+            fprintf(stderr, "[par %s n=%u T=%u] phase1 %.2f ms edges %.2f ms merge %.2f ms; workers (items, us):", del ? "del" : "ins", n, T,
                     ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
+            for (const Mut& m : W) fprintf(stderr, " (%zu, %.0f)", m.n_items, m.t_us);
+            fprintf(stderr, "\n");
         }
         return 0;
     }
@@ -1816,6 +1946,7 @@ struct tm_engine {
         Replica& R = *b->rep;
         const hipStream_t stream = R.stream;
         int rc;
+        if ((rc = ensure_dense(b))) return rc;
         if ((rc = sync_routes(R))) return rc;
         const uint32_t n = b->n;
         const size_t nn = std::max<size_t>(n, 1);
@@ -2006,6 +2137,7 @@ struct tm_engine {
         Replica& R = *b->rep;
         const hipStream_t stream = R.stream;
         int rc;
+        if ((rc = ensure_dense(b))) return rc;
         if ((rc = sync_subs(R))) return rc;
         const uint32_t n = b->n;
         const uint64_t nm = b->total;
@@ -2633,6 +2765,7 @@ struct tm_engine {
     // tm_batch_export
     int export_batch(tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
         if (!b->done) return TM_EINVAL;
+        if (int rc = ensure_dense(b)) return rc;
         const uint64_t top = (uint64_t)(nd.size() ? nd.size() - 1 : 0) * mul + add;
         if (top > 0xFFFFFFFFull) return TM_EOVERFLOW;
         HIP_OK(launch_export(b->d_rowoff, b->d_ids, b->n, b->total, d_counts, d_ids, mul, add, st(b)));
@@ -2679,6 +2812,8 @@ struct tm_engine {
             HIP_OK(hipEventCreate(&b->ev1));
             HIP_OK(hipEventCreate(&b->ev2));
             HIP_OK(hipEventCreate(&b->evt));
+            HIP_OK(hipEventCreate(&b->evc0));
+            HIP_OK(hipEventCreate(&b->evc1));
         }
         return TM_OK;
     }
@@ -2970,6 +3105,7 @@ struct tm_engine {
                 note_launch(b);
                 b->launched = true;
                 b->done = false;
+                b->dense = false;
                 b->csr = true;
                 b->scan_args = s;
                 return TM_OK;
@@ -2980,6 +3116,7 @@ struct tm_engine {
         note_launch(b);
         b->launched = true;
         b->done = false;
+        b->dense = false;
         b->csr = csr;
         if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
         HIP_OK(enqueue_csr(b, s, S));
@@ -2988,15 +3125,58 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // scan + finalize + the read-back of the control words (after the walk)
+    // the read-back of the control words after the walk.  The batch's result is
+    // then what the walk left in HBM -- row i = sfids[src[i] .. + count[i]),
+    // sorted and deduplicated -- and the dense CSR (scan + finalize copy) is
+    // built only for a consumer that asks for offsets (ensure_dense).
+    // TM_EAGER_CSR=1 builds it in every launch (round-2 behaviour, for A/B).
+    bool eager_csr = getenv("TM_EAGER_CSR") && atoi(getenv("TM_EAGER_CSR")) != 0;
     hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S) {
         hipError_t e;
-        if ((e = launch_scan(s, S, b->d_total)) != hipSuccess) return e;
-        if ((e = launch_finalize(s, S, false)) != hipSuccess) return e;
+        if (eager_csr) {
+            if ((e = launch_scan(s, S, b->d_total)) != hipSuccess) return e;
+            if ((e = launch_finalize(s, S, false)) != hipSuccess) return e;
+        }
         if ((e = hipEventRecord(b->ev2, S)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S)) != hipSuccess)
             return e;   // ctrl + stats
-        return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
+        if (eager_csr) return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
+        return hipSuccess;
+    }
+
+    // The dense CSR of a waited batch (row_off[n + 1], ids[total] in topic
+    // order) from the walk's rows: exclusive scan of the counts, then one copy
+    // of every row from staging (tm_finalize).  Built once per launch, on the
+    // batch's stream, for the consumers that index the result by offsets: the
+    // host copy (tm_batch_result), routes, fan-out, the sharded export and
+    // tm_batch_device_csr.  The per-publish path reads the rows where the walk
+    // wrote them and never builds it.
+    int ensure_dense(tm_batch* b) {
+        if (!b->done) return TM_EINVAL;
+        if (b->dense) return TM_OK;
+        const hipStream_t S = st(b);
+        int rc;
+        if (b->total > b->c_ids) {
+            if ((rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->total + b->total / 4))) return rc;
+        }
+        b->scan_args.ids = b->d_ids;
+        b->scan_args.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
+        HIP_OK(hipEventRecord(b->evc0, S));
+        HIP_OK(launch_scan(b->scan_args, S, b->d_total));
+        HIP_OK(launch_finalize(b->scan_args, S, checked));
+        HIP_OK(hipEventRecord(b->evc1, S));
+        HIP_OK(hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S));
+        HIP_OK(hipStreamSynchronize(S));
+        if (b->h_total[0] != b->total) {
+            snprintf(last_error(), 512, "inconsistent CSR: scanned %u entries, kernel count %llu", b->h_total[0],
+                     (unsigned long long)b->total);
+            return TM_EIO;
+        }
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, b->evc0, b->evc1);
+        b->st.ms_csr = ms;
+        b->dense = true;
+        return TM_OK;
     }
 
     // Replays the batch's captured pipeline, capturing it first when its
@@ -3080,6 +3260,7 @@ struct tm_engine {
         (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
         if (b->tok_timed) (void)hipEventElapsedTime(&ms_tok, b->evt, b->ev0);
         b->st.ms_tokenize = ms_tok;
+        b->st.ms_csr = 0;   // set by ensure_dense
         b->st.topics = b->n;
         b->st.visits = b->h_stats[ST_VISITS];
         b->st.hash_hits = b->h_stats[ST_HASH];
@@ -3117,8 +3298,8 @@ struct tm_engine {
             if ((rc = grow_for(b, err, need))) return rc;
             if ((rc = launch(b))) return rc;
         }
-        // CSR capacity: the finalize pass is rerun alone when ids[] was too small
-        if (b->h_total[0] > b->c_ids) {
+        // eager CSR (TM_EAGER_CSR): the finalize pass is rerun alone when ids[] was too small
+        if (eager_csr && b->h_total[0] > b->c_ids) {
             int rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->h_total[0] + b->h_total[0] / 4);
             if (rc) return rc;
             b->scan_args.ids = b->d_ids;
@@ -3131,12 +3312,14 @@ struct tm_engine {
         }
         fill_stats(b);
         b->done = true;
+        b->dense = eager_csr;
         return TM_OK;
     }
 
     int result(tm_batch* b, tm_result* out) {
         if (!b->done) return TM_EINVAL;
         int rc;
+        if ((rc = ensure_dense(b))) return rc;
         const hipStream_t S = st(b);
         // the match count is known since wait(): both copies go out behind one sync
         const uint64_t total = b->total;
@@ -4142,9 +4325,25 @@ int tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out) {
 
 int tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row, const uint32_t** d_ids, uint64_t* n) {
     if (!e || !b || !b->done) return TM_EINVAL;
+    {
+        std::lock_guard<std::recursive_mutex> g(e->mu);
+        int rc = e->use(b->rep);
+        if (rc) return rc;
+        if ((rc = e->ensure_dense(b))) return rc;
+    }
     if (d_row) *d_row = b->d_rowoff;
     if (d_ids) *d_ids = b->d_ids;
     if (n) *n = b->total;
+    return TM_OK;
+}
+
+int tm_batch_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uint64_t** d_start,
+                  const uint32_t** d_ids, uint64_t* n_matches) {
+    if (!e || !b || !b->done || !b->csr) return TM_EINVAL;
+    if (d_count) *d_count = b->d_count;
+    if (d_start) *d_start = reinterpret_cast<const uint64_t*>(b->d_src);
+    if (d_ids) *d_ids = b->d_sfids;
+    if (n_matches) *n_matches = b->total;
     return TM_OK;
 }
 
@@ -4326,7 +4525,11 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
         if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
         if (nshards <= 1) {
+            const auto tq0 = std::chrono::steady_clock::now();
             e->make_plan(filters, offsets, n, false);
+            if (getenv("TM_PAR_TRACE"))
+                fprintf(stderr, "[plan ins n=%u] %.2f ms\n", n,
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
             if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(false, filters, offsets, n, &done, &rc)) {
                 if (n_inserted) *n_inserted = done;
                 return rc;
@@ -4366,7 +4569,11 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     for (uint32_t i = 0; i < n; ++i)
         if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     try {
+        const auto tq0 = std::chrono::steady_clock::now();
         e->make_plan(filters, offsets, n, true);
+        if (getenv("TM_PAR_TRACE"))
+            fprintf(stderr, "[plan del n=%u] %.2f ms\n", n,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
         if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(true, filters, offsets, n, &done, &rc)) {
             if (n_deleted) *n_deleted = done;
             return rc;

@@ -140,6 +140,28 @@ class Batch:
                 "tm_batch_device_csr")
         return row.value, ids.value, n.value
 
+    def device_rows(self):
+        """Device pointers of the result as the walk left it (tm_batch_rows):
+        (count u32[n], start u64[n], ids u32[...], n_matches); no CSR pass."""
+        cnt, start, ids, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_uint64()
+        N.check(self.eng.L.tm_batch_rows(self.eng.h, self.h, C.byref(cnt), C.byref(start), C.byref(ids),
+                                         C.byref(n)), "tm_batch_rows")
+        return cnt.value, start.value, ids.value, n.value
+
+    def rows(self, n_rows: int):
+        """Host copy of the walk's rows (tm_batch_rows + hipMemcpy, for tests):
+        (count u32[n_rows], start u64[n_rows], staging u32[max end])."""
+        cnt, start, ids, _ = self.device_rows()
+        c = np.zeros(n_rows, np.uint32)
+        s = np.zeros(n_rows, np.uint64)
+        _d2h(c, cnt)
+        _d2h(s, start)
+        end = int((s + c).max()) if n_rows else 0
+        stg = np.zeros(max(end, 1), np.uint32)
+        if end:
+            _d2h(stg, ids)
+        return c, s, stg[:end]
+
     def free(self):
         if self.h:
             self.eng.L.tm_batch_free(self.eng.h, self.h)
@@ -150,6 +172,23 @@ class Batch:
             self.free()
         except Exception:
             pass
+
+
+_hip = None
+
+
+def _d2h(dst: np.ndarray, src_ptr: int):
+    """hipMemcpy device -> host through the HIP runtime the engine already
+    loaded (same soname, so the same copy): test/diagnostic use only."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+    if dst.nbytes:
+        rc = _hip.hipMemcpy(dst.ctypes.data, src_ptr, dst.nbytes, 2)   # hipMemcpyDeviceToHost
+        if rc:
+            raise RuntimeError(f"hipMemcpy D2H failed: {rc}")
 
 
 def _result_arrays(r: N.Result):

@@ -98,6 +98,7 @@ typedef struct {
     float    ms_total;      /* device time of the whole batch pipeline (last launch) */
     float    ms_tokenize;   /* device tokeniser time of the last launch (0: tokens reused) */
     uint64_t probes;        /* 64-B edge-hash bucket reads of the tile walk (hits + misses) */
+    float    ms_csr;        /* device time of the last dense-CSR build (scan + copy; 0: not built) */
 } tm_batch_stats;
 
 typedef struct {
@@ -250,7 +251,18 @@ TM_API int  tm_batch_launch(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_wait(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out);
 TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
-/* Device pointers of the batch's CSR (valid after wait): row_offsets, ids. */
+/* A waited batch's result is the rows as the walk wrote them to HBM: row i
+ * (one per topic, or per distinct topic with TM_BATCH_DEDUP) is
+ * d_ids[d_start[i] .. d_start[i] + d_count[i]), sorted (Erlang binary order)
+ * and deduplicated; rows of different topics are not adjacent.  Device
+ * pointers of the batch, valid until its next launch or re-prepare; no copy,
+ * no extra pass.  *n_matches = sum of the counts. */
+TM_API int  tm_batch_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uint64_t** d_start,
+                          const uint32_t** d_ids, uint64_t* n_matches);
+/* Device pointers of the batch's dense CSR: row_offsets[n + 1], ids[total]
+ * in topic order.  Built from the rows on first request after a launch
+ * (scan + one copy, on the batch's stream; tm_batch_result, routes, dispatch
+ * and export build it too); valid until the next launch. */
 TM_API int  tm_batch_device_csr(tm_engine* e, tm_batch* b, const uint32_t** d_row_offsets,
                          const uint32_t** d_ids, uint64_t* n_matches);
 TM_API void tm_batch_free(tm_engine* e, tm_batch* b);

@@ -132,6 +132,51 @@ def test_c1_full_parity_and_walk_counters():
     b.free()
 
 
+@pytest.mark.parametrize("rowcap", [None, "4"])
+def test_walk_rows_are_the_result_without_a_csr_pass(rowcap):
+    """wait() leaves the result where the walk wrote it (tm_batch_rows: row i =
+    ids[start[i] .. + count[i]), rows of different tiles in any order); the
+    dense CSR is built only on request.  Both equal the oracle's rows; with a
+    4-entry row cap most rows come from the generic path's runs instead."""
+    if rowcap:
+        os.environ["TM_ROWCAP"] = rowcap
+    try:
+        eng = Engine(device=0)
+    finally:
+        os.environ.pop("TM_ROWCAP", None)
+    p = replace(gen.C1, n_filters=4000)
+    F = gen.gen_filters(p).tolist()
+    Ts = gen.gen_topics(p, gen.Strings.from_list(F), 77, 30000)
+    T = Ts.tolist()
+    for f in F:
+        eng.insert(f)
+    exp, _ = oracle_rows(F, T)
+    b = eng.prepare(Ts)
+    b.launch().wait()
+    st = b.stats()
+    assert st["ms_csr"] == 0.0   # no CSR pass in launch + wait
+    cnt, start, stg = b.rows(len(T))
+    assert int(cnt.sum()) == st["matches"]
+    cache = {}
+    got = [[cache.setdefault(int(i), eng.filter_bytes(int(i))) for i in stg[int(start[k]):int(start[k]) + int(cnt[k])]]
+           for k in range(len(T))]
+    assert_same(T, got, exp)
+    if rowcap:
+        assert st["slow_topics"] > 1000
+    # the dense CSR, built on request, holds the same rows in topic order
+    offs, ids = b.result()
+    assert b.stats()["ms_csr"] > 0.0
+    assert np.array_equal(np.diff(offs.astype(np.int64)), cnt.astype(np.int64))
+    for k in range(0, len(T), 97):
+        assert np.array_equal(ids[offs[k]:offs[k + 1]], stg[int(start[k]):int(start[k]) + int(cnt[k])])
+    # a relaunch drops the dense CSR; asking again rebuilds it
+    b.launch().wait()
+    assert b.stats()["ms_csr"] == 0.0
+    offs2, ids2 = b.result()
+    assert np.array_equal(offs, offs2) and np.array_equal(ids, ids2)
+    b.free()
+
+
 def test_c2_parity_sample():
     F = gen.gen_filters(gen.C2).tolist()
     T = gen.gen_topics(gen.C2, gen.Strings.from_list(F), 2002, 200_000).tolist()

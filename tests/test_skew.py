@@ -123,3 +123,29 @@ def test_parallel_churn_builds_the_same_trie_as_the_serial_pass():
         for k in range(1, len(ws) + 1):
             pre = b"/".join(ws[:k])
             assert A.lookup(pre) == B.lookup(pre), pre
+
+
+def test_parallel_insert_creates_a_shared_first_level_edge_once():
+    """A bulk insert whose filters share a NEW first word but differ in the
+    second word is dealt to different workers (first-two-word subtrees): the
+    level-0 edge they all need must be created once, not once per worker."""
+    p = gen.SkewParams(seed=22, n_hot=500, k_per_hot=40)
+    allf, _, _, _ = workload(p, 20_000, 100, seed=22, background_pool=500)
+    A = Engine(device=-1, host_threads=1)
+    B = Engine(device=-1, host_threads=8)
+    adds = [b"nw%d/%d/x" % (i % 5, i) for i in range(3000)] + [b"nw%d" % (i % 3) for i in range(6)]
+    adds += [b"+/nz%d/%d" % (i % 4, i) for i in range(2500)]
+    for e in (A, B):
+        e.insert_many(allf)
+        e.insert_many(gen.Strings.from_list(adds))
+    a, b = A.stats(), B.stats()
+    assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+    B.debug_check()
+    for f in adds[::7] + [b"nw0", b"nw1", b"+/nz1"]:
+        assert A.lookup(f) == B.lookup(f), f
+    # and the deletes of the same filters leave both tries equal again
+    for e in (A, B):
+        e.delete_many(gen.Strings.from_list(adds))
+    a, b = A.stats(), B.stats()
+    assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+    B.debug_check()
