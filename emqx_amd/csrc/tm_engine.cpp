@@ -408,6 +408,9 @@ struct tm_batch {
     bool dense = false;
     bool tok_timed = false;     // the last launch tokenised: evt..ev0 is its time
     bool launched = false, done = false;
+    // staging as one region shared by every walk group (set when one group's
+    // reservation alone would need more than the staging limit / TICKET_GROUPS)
+    bool one_region = false;
     bool csr = true;   // the last launch built the CSR (false: async, rows left in staging)
     uint64_t seq = 0;  // launch sequence number while its results may be read (0: none)
     uint64_t total = 0;
@@ -834,6 +837,7 @@ struct tm_engine {
     uint64_t fan_big_limit = 0xFFFFFFFFull;   // fan-out scan blocks above this use u64 offsets (TM_FAN_BIG: tests)
     double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
     uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
+    uint64_t staging_min = 1u << 16;      // initial staging entries of a batch (TM_STAGING_MIN: test-only)
 
     // routes (the emqx_route bag, aggregated per destination by the caller):
     // node id -> [(dest, count)] in first-added order; total routes per node
@@ -2827,7 +2831,7 @@ struct tm_engine {
             std::max<uint64_t>((uint64_t)match_waves(b->n, b->rep->device, qcap) * tile_topics(b->n) * row_cap, 1);
         // + a byte per entry past the rows: the emission-log variant's lanes (TM_EMIT_LOG)
         if ((rc = dev_reserve(b->d_rows, b->c_rows, fast + fast / 8 + 8))) return rc;
-        if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
+        if ((rc = dev_reserve(b->d_sfids, b->c_sfids, std::max<uint64_t>((uint64_t)b->n * 32, staging_min)))) return rc;
         if ((rc = dev_reserve(b->d_ids, b->c_ids, std::max<uint64_t>((uint64_t)b->n * 32, 1u << 16)))) return rc;
         if ((rc = host_reserve(b->h_total, b->ch_total, 4))) return rc;
         return TM_OK;
@@ -3080,7 +3084,8 @@ struct tm_engine {
             return TM_EIO;
         }
         a.sfids = b->d_sfids; a.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
-        a.rcap = a.sfids_cap / TICKET_GROUPS;
+        a.rcap = b->one_region ? a.sfids_cap : a.sfids_cap / TICKET_GROUPS;
+        a.sgmask = b->one_region ? 0u : TICKET_GROUPS - 1;
         a.xg = b->d_ctrl + XG_WORD;
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
         a.stats = b->d_stats;
@@ -3222,7 +3227,8 @@ struct tm_engine {
 
     // control words of a finished launch: TM_EOVERFLOW past the u32 CSR, the
     // retry reasons in *err (0 = clean)
-    int check_ctrl(const uint32_t* ctrl, const unsigned long long* stats, uint32_t* err, uint64_t* need) {
+    int check_ctrl(const uint32_t* ctrl, const unsigned long long* stats, uint32_t* err, uint64_t* need,
+                   uint64_t* staged_out = nullptr) {
         *err = ctrl[CTRL_ERR];
         uint64_t staged = 0, top = 0;
         for (uint32_t g = 0; g < TICKET_GROUPS; ++g) {
@@ -3231,6 +3237,7 @@ struct tm_engine {
             top = std::max(top, t);
         }
         *need = top * TICKET_GROUPS;   // staging capacity that holds every region's reservation
+        if (staged_out) *staged_out = staged;
         const uint64_t nmatch = stats[ST_MATCHES];
         // a CSR with u32 offsets cannot hold more (tm_result): refuse, never wrap
         if ((*err & ERR_CSR_RANGE) || staged > result_limit || nmatch > result_limit) {
@@ -3242,9 +3249,15 @@ struct tm_engine {
     }
 
     // capacity misses of the last launch: grow what overflowed (the caller relaunches)
-    int grow_for(tm_batch* b, uint32_t err, uint64_t need) {
+    int grow_for(tm_batch* b, uint32_t err, uint64_t need, uint64_t staged) {
         if (err & ERR_STAGING) {
-            int rc = dev_reserve(b->d_sfids, b->c_sfids, std::min<uint64_t>(need + need / 4 + 1024, MAX_RESULT));
+            // per-group regions of the largest group's size: unless that exceeds
+            // the limit while the batch as a whole fits (skew concentrated in one
+            // walk group) -- then one region for all groups, sized by the total
+            const uint64_t limit = std::min<uint64_t>(MAX_RESULT, result_limit + 1024);
+            if (!b->one_region && need + need / 4 + 1024 > limit && staged <= result_limit) b->one_region = true;
+            if (b->one_region) need = staged;
+            int rc = dev_reserve(b->d_sfids, b->c_sfids, std::min<uint64_t>(need + need / 4 + 1024, limit));
             if (rc) return rc;
         }
         if (err & ERR_SLOW_SCRATCH) {
@@ -3290,12 +3303,16 @@ struct tm_engine {
                 return TM_EIO;
             }
             uint32_t err;
-            uint64_t need;
-            int rc = check_ctrl(b->h_ctrl, b->h_stats, &err, &need);
+            uint64_t need, staged;
+            int rc = check_ctrl(b->h_ctrl, b->h_stats, &err, &need, &staged);
             if (rc) return rc;
             if (!err) break;
-            if (attempt >= 6) return TM_EOVERFLOW;
-            if ((rc = grow_for(b, err, need))) return rc;
+            if (attempt >= 6) {
+                snprintf(last_error(), 512, "capacity misses did not settle after %d relaunches (err %#x, %llu staged)",
+                         attempt, err, (unsigned long long)staged);
+                return TM_EOVERFLOW;
+            }
+            if ((rc = grow_for(b, err, need, staged))) return rc;
             if ((rc = launch(b))) return rc;
         }
         // eager CSR (TM_EAGER_CSR): the finalize pass is rerun alone when ids[] was too small
@@ -3556,7 +3573,7 @@ struct tm_engine {
         x.rows = b->d_sfids;
         x.h_rows = reinterpret_cast<uint32_t*>(d_rows);
         x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
-        x.rcap = std::min<uint64_t>(b->c_sfids, MAX_RESULT) / TICKET_GROUPS;
+        x.rcap = std::min<uint64_t>(b->c_sfids, MAX_RESULT) / (b->one_region ? 1 : TICKET_GROUPS);
         HIP_OK(launch_export_host(x, S));
         HIP_OK(hipEventRecord(sl->ev_done, S));
         return TM_OK;
@@ -3627,12 +3644,13 @@ struct tm_engine {
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(sl->h_out + tm_batch::HDR_FIXED);
         const uint32_t* count = reinterpret_cast<const uint32_t*>(sl->h_out + hdr_bytes);
         uint32_t err = 0;
-        uint64_t need = 0;
-        int rc = check_ctrl(ctrl, stats, &err, &need);
+        uint64_t need = 0, staged = 0;
+        int rc = check_ctrl(ctrl, stats, &err, &need, &staged);
         if (rc) {
             fail_all(rc);
             return false;
         }
+        if (b->one_region) need = staged;
         if (!err && need > sl->c_rows / 4) err = ERR_STAGING;   // (cannot happen: rows hold the staging area)
         if (err) {
             // capacity miss (staging, generic-path scratch): the CSR path grows
@@ -3641,7 +3659,7 @@ struct tm_engine {
             {
                 std::lock_guard<std::recursive_mutex> g(mu);
                 (void)hipSetDevice(b->rep->device);
-                rc = grow_for(b, err, need);
+                rc = grow_for(b, err, need, staged);
                 if (!rc) rc = wait(b);
                 if (!rc) rc = result(b, &r);
             }
@@ -3674,6 +3692,7 @@ struct tm_engine {
         if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
         if (const char* rl = getenv("TM_RESULT_LIMIT"))
             result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));
+        if (const char* sm = getenv("TM_STAGING_MIN")) staging_min = std::max<uint64_t>(64, strtoull(sm, nullptr, 10));
         threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
         dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
         if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');

@@ -152,6 +152,8 @@ struct MatchArgs {
     uint32_t static_rounds;   // round-robin tiles per wave before tickets (>= 1)
     uint32_t* xg;             // the header's group lines (header + XG_WORD)
     uint64_t rcap;            // staging entries per group region (sfids_cap / TICKET_GROUPS)
+    uint32_t sgmask;          // staging group of a wave = (blockIdx % TICKET_GROUPS) & sgmask
+                              // (TICKET_GROUPS - 1; 0 = one region for all: a skewed batch)
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;

@@ -682,6 +682,9 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             eB = eB && slotB < a.row_cap;
             const uint64_t mA = __ballot(eA), mB = __ballot(eB);
             const uint32_t nA = (uint32_t)__popcll(mA), nE = nA + (uint32_t)__popcll(mB);
+#ifdef TM_EXPERIMENT_NO_LOG   // (timing experiments only: counts kept, log stores dropped)
+            eA = eB = false;
+#endif
             if (eA) {
                 const uint32_t i = lcount + prefix_count(mA);
                 wrows[CK_(i, lcap, 13)] = (kA & KEY_MASK) | fA;
@@ -730,7 +733,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     // u64 ticket: a batch may reserve more than 2^32 entries; the host then
     // fails it with TM_EOVERFLOW (sfids_cap < 2^32, so dst below never wraps)
     unsigned long long base64 = 0;
-    const uint32_t g = blockIdx.x % TICKET_GROUPS;   // my group's staging region
+    const uint32_t g = (blockIdx.x % TICKET_GROUPS) & a.sgmask;   // my group's staging region
     if (lane == 0 && tot) base64 = atomicAdd(xg_top(a.xg, g), (unsigned long long)tot);
     base64 = __shfl(base64, 0, 64);
     const bool fits = base64 + tot <= a.rcap;
@@ -988,7 +991,7 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
             __syncthreads();
         }
         unsigned long long base = 0;
-        const uint32_t g = blockIdx.x % TICKET_GROUPS;
+        const uint32_t g = (blockIdx.x % TICKET_GROUPS) & a.sgmask;
         if (lane == 0 && on) base = atomicAdd(xg_top(a.xg, g), (unsigned long long)on);
         base = __shfl(base, 0, 64);
         const bool fits = base + on <= a.rcap;

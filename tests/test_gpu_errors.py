@@ -71,3 +71,31 @@ def test_topic_longer_than_max_topic_len_is_einval():
             eng.prepare(topics)
         assert ei.value.rc == N.TM_EINVAL
     assert eng.match(b"a/b") == [b"+/#"]               # still usable
+
+
+def test_staging_skew_in_one_walk_group_falls_back_to_one_region():
+    """Every match of a batch reserved by waves of one walk group (1-topic
+    tiles: topic t -> wave t -> group t % 8; only topics t % 8 == 0 match):
+    that group's region overflows while the batch fits the limit.  The engine
+    must not retry per-group regions sized 8x the group (they exceed the
+    limit) but stage the batch as one region, and return exact rows."""
+    import itertools
+    os.environ["TM_RESULT_LIMIT"] = "2000"
+    os.environ["TM_STAGING_MIN"] = "64"
+    try:
+        eng = Engine(device=0)
+    finally:
+        del os.environ["TM_RESULT_LIMIT"]
+        del os.environ["TM_STAGING_MIN"]
+    words = [b"a", b"b", b"c", b"d", b"e", b"f"]
+    F = [b"/".join(c) for c in itertools.product(*[(w, b"+") for w in words])]     # 64 filters
+    F += [b"/".join(words[:k] + [b"#"]) for k in range(len(words) + 1)]          # 7 more
+    for f in F:
+        eng.insert(f)
+    # 64 topics, one per tile; the 8 of group 0 match 71 filters each: 568
+    # entries in a 256-entry region, 8 x 568 > the 2,000 limit, 568 < it
+    T = [b"a/b/c/d/e/f" if t % 8 == 0 else b"q%d" % t for t in range(64)]
+    exp, _ = oracle_rows(F, T)
+    assert len(exp[0]) == 71
+    for _ in range(2):   # and again on the grown batch
+        assert_same(T, engine_rows(eng, T), exp)
