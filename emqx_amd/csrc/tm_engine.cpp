@@ -593,6 +593,11 @@ struct Replica {
     uint32_t* d_dbg = nullptr;
     uint32_t* h_dbg = nullptr;
     size_t c_dbg = 0, ch_dbg = 0;
+    // pinned staging of the appended tails (filter bytes, dictionary tails and
+    // arena) of one delta upload: small appends go out asynchronously instead
+    // of as pageable copies the host must wait for
+    uint8_t* h_app = nullptr;
+    size_t ch_app = 0;
     // routes: dests CSR by node id (engine routes_gen when uploaded)
     uint32_t *d_roff = nullptr, *d_rdest = nullptr;
     size_t c_roff = 0, c_rdest = 0;
@@ -760,6 +765,34 @@ struct Mut {
     int rc = TM_OK;
 };
 thread_local Mut* tl_mut = nullptr;
+
+// Wake-ups of blocked tm_match_coalesced callers.  A caller that stops
+// spinning sleeps on one of WAKE_WORDS shared futex words (chosen by its
+// thread); a completer delivering a batch marks each call done without a
+// syscall and notes the words whose sleepers it finished, then wakes each
+// noted word once after the batch (~8-16 FUTEX_WAKEs instead of one per
+// call; a woken caller whose call is not done yet sleeps again).  Callbacks
+// run outside a completer's batch wake their caller at once.
+namespace syncwake {
+constexpr uint32_t WAKE_WORDS = 16;
+struct alignas(64) Word {
+    std::atomic<uint32_t> seq{0};
+};
+inline Word words[WAKE_WORDS];
+inline thread_local bool in_batch = false;        // a completer is delivering a batch
+inline thread_local uint32_t pending = 0;         // words to wake at the batch's end
+inline long futex(std::atomic<uint32_t>* a, int op, uint32_t v) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), op | FUTEX_PRIVATE_FLAG, v, nullptr, nullptr, 0);
+}
+inline void wake(uint32_t k) {
+    words[k].seq.fetch_add(1, std::memory_order_acq_rel);
+    futex(&words[k].seq, FUTEX_WAKE, INT32_MAX);
+}
+inline void flush() {
+    for (uint32_t m = pending; m; m &= m - 1) wake((uint32_t)__builtin_ctz(m));
+    pending = 0;
+}
+}  // namespace syncwake
 
 struct tm_engine {
     std::recursive_mutex mu;
@@ -1412,7 +1445,10 @@ struct tm_engine {
         std::vector<uint64_t> hs;
         const bool root_live = nd[ROOT].live != 0;
         const uint32_t nb = nbuckets();
+        static const bool ptrace = getenv("TM_PLAN_TRACE") != nullptr;
+        std::chrono::steady_clock::duration d_split{}, d_dict{}, d_walk{};
         for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
+            const auto c0 = std::chrono::steady_clock::now();
             const uint32_t g1 = std::min(hi, g0 + PLAN_G);
             // words and their dictionary entries
             const uint32_t wbase = (uint32_t)W.size();
@@ -1430,10 +1466,14 @@ struct tm_engine {
                     hs.push_back(w.n == 0 || is_plus(w) || is_hash(w) ? 0 : dict.prefetch(w.p, w.n));
                 }
             }
+            const auto c1 = std::chrono::steady_clock::now();
             for (size_t j = 0; j < all.size(); ++j) {
                 const TWord& w = all[j];
                 W.push_back(w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find_h(w.p, w.n, hs[j]));
             }
+            const auto c2 = std::chrono::steady_clock::now();
+            d_split += c1 - c0;
+            d_dict += c2 - c1;
             // the existing paths, level by level over the group
             uint32_t node[PLAN_G], k[PLAN_G];
             bool run[PLAN_G], known[PLAN_G];
@@ -1469,6 +1509,12 @@ struct tm_engine {
                 if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
                 else { pe.node = node[q]; pe.depth = k[q]; }
             }
+            d_walk += std::chrono::steady_clock::now() - c2;
+        }
+        if (ptrace) {
+            auto us = [](auto d) { return std::chrono::duration<double, std::micro>(d).count(); };
+            fprintf(stderr, "  [plan part %u: %u filters] split+hash %.0f us, dict %.0f us, walk %.0f us\n", part, hi - lo,
+                    us(d_split), us(d_dict), us(d_walk));
         }
     }
 
@@ -2450,6 +2496,35 @@ struct tm_engine {
             delta_slots += k;
             async_used = true;
         }
+        // appended tails up to APP_MAX bytes in all go through the replica's
+        // pinned staging (reserved once here: copies queued below read it until
+        // the upload's event, and ensure_delta_idle waits for that before the
+        // next upload reuses it)
+        size_t app_need = 0, app_used = 0;
+        {
+            const uint64_t fb_from = R.c_fbytes < fbytes.size() + 1 ? 0 : R.fbytes_uploaded;
+            app_need += fbytes.size() > fb_from ? fbytes.size() - fb_from : 0;
+            if (dev_tok) {
+                const size_t t_from = R.c_tail < dict.tails().size() + 1 ? 0 : R.tails_uploaded;
+                const size_t a_from = R.c_arena < dict.arena().size() + 1 ? 0 : R.arena_uploaded;
+                if (dict.tails().size() > t_from) app_need += (dict.tails().size() - t_from) * sizeof(DictTail) + 16;
+                if (dict.arena().size() > a_from) app_need += dict.arena().size() - a_from + 16;
+            }
+        }
+        const bool app_pinned = app_need > 0 && app_need <= APP_MAX;
+        if (app_pinned && (rc = host_reserve(R.h_app, R.ch_app, app_need))) return rc;
+        // a host range -> device, through the pinned staging when it fits
+        auto h2d_tail = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+            if (app_pinned && app_used + bytes <= R.ch_app) {
+                uint8_t* stg = R.h_app + app_used;
+                memcpy(stg, src, bytes);
+                app_used = (app_used + bytes + 15) & ~(size_t)15;
+                async_used = true;
+                return hipMemcpyAsync(dst, stg, bytes, hipMemcpyHostToDevice, stream);
+            }
+            pageable_used = true;
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream);
+        };
         // filter bytes (slow-path sort): arena + per-node (off, len)
         bool f_full = full_f_dirty;
         if (R.c_foff < nn || R.c_flen < nn) {
@@ -2462,9 +2537,8 @@ struct tm_engine {
             R.fbytes_uploaded = 0;
         }
         if (fbytes.size() > R.fbytes_uploaded) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(R.d_fbytes + R.fbytes_uploaded, fbytes.data() + R.fbytes_uploaded,
-                                  fbytes.size() - R.fbytes_uploaded, hipMemcpyHostToDevice, stream));
+            HIP_OK(h2d_tail(R.d_fbytes + R.fbytes_uploaded, fbytes.data() + R.fbytes_uploaded,
+                            fbytes.size() - R.fbytes_uploaded));
             R.fbytes_uploaded = fbytes.size();
         }
         if (f_full) {
@@ -2482,14 +2556,16 @@ struct tm_engine {
             HIP_OK(launch_scatter_fmeta(R.d_foff, R.d_flen, R.d_fidx, R.d_foffv, R.d_flenv, (uint32_t)k, stream));
             async_used = true;
         }
-        if (dev_tok && (rc = sync_dict(R, keys_full, pageable_used, async_used))) return rc;
+        if (dev_tok && (rc = sync_dict(R, keys_full, pageable_used, async_used, h2d_tail))) return rc;
         return TM_OK;
     }
+    static constexpr size_t APP_MAX = 8u << 20;
 
     // word dictionary -> one replica: the whole cuckoo table after a rebuild
     // (or when most of it changed), else the staged dirty slots; the tails'
     // and the arena's new ends
-    int sync_dict(Replica& R, bool keys_full, bool& pageable_used, bool& async_used) {
+    template <class H2D>
+    int sync_dict(Replica& R, bool keys_full, bool& pageable_used, bool& async_used, H2D&& h2d_tail) {
         int rc;
         const hipStream_t stream = R.stream;
         const std::vector<DictKey>& tab = dict.keys();
@@ -2520,9 +2596,8 @@ struct tm_engine {
             R.tails_uploaded = 0;
         }
         if (tl.size() > R.tails_uploaded) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(R.d_tail + R.tails_uploaded, tl.data() + R.tails_uploaded,
-                                  (tl.size() - R.tails_uploaded) * sizeof(DictTail), hipMemcpyHostToDevice, stream));
+            HIP_OK(h2d_tail(R.d_tail + R.tails_uploaded, tl.data() + R.tails_uploaded,
+                            (tl.size() - R.tails_uploaded) * sizeof(DictTail)));
             R.tails_uploaded = tl.size();
         }
         if (R.c_arena < ar.size() + 1) {
@@ -2530,9 +2605,7 @@ struct tm_engine {
             R.arena_uploaded = 0;
         }
         if (ar.size() > R.arena_uploaded) {
-            pageable_used = true;
-            HIP_OK(hipMemcpyAsync(R.d_arena + R.arena_uploaded, ar.data() + R.arena_uploaded, ar.size() - R.arena_uploaded,
-                                  hipMemcpyHostToDevice, stream));
+            HIP_OK(h2d_tail(R.d_arena + R.arena_uploaded, ar.data() + R.arena_uploaded, ar.size() - R.arena_uploaded));
             R.arena_uploaded = ar.size();
         }
         return TM_OK;
@@ -3600,10 +3673,13 @@ struct tm_engine {
             lk.unlock();
             bool recovered = false;
             double us_wait = 0, us_deliver = 0;
+            syncwake::in_batch = true;
             try {
                 recovered = slot_deliver(sl, us_wait, us_deliver);
             } catch (...) {
             }
+            syncwake::in_batch = false;
+            syncwake::flush();
             lk.lock();
             R.a_inflight.erase(std::find(R.a_inflight.begin(), R.a_inflight.end(), sl));
             R.a_us_wait += us_wait;
@@ -3742,6 +3818,7 @@ struct tm_engine {
             dev_free(R->d_dbg); dev_free(R->d_roff); dev_free(R->d_rdest); dev_free(R->d_rl);
             dev_free(R->d_soff); dev_free(R->d_subs); dev_free(R->d_scnt); dev_free(R->d_sone);
             if (R->h_dbg) (void)hipHostFree(R->h_dbg);
+            if (R->h_app) (void)hipHostFree(R->h_app);
             if (R->ev_delta) (void)hipEventDestroy(R->ev_delta);
             if (R->ev_sync) (void)hipEventDestroy(R->ev_sync);
             if (R->stream) (void)hipStreamDestroy(R->stream);
@@ -4146,6 +4223,7 @@ struct SyncWait {
     uint32_t cap;
     uint32_t n = 0;
     int rc = TM_OK;
+    uint32_t word = 0;           // the caller's syncwake word
 };
 
 void sync_cb(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
@@ -4153,8 +4231,11 @@ void sync_cb(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
     w->rc = rc;
     w->n = n;
     if (rc == TM_OK && n && w->cap) memcpy(w->ids, ids, (size_t)std::min(n, w->cap) * 4);
-    if (w->state.exchange(1, std::memory_order_acq_rel) == 2)
-        syscall(SYS_futex, reinterpret_cast<int*>(&w->state), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    const uint32_t k = w->word;   // (w is the caller's: gone once state reads 1)
+    if (w->state.exchange(1, std::memory_order_acq_rel) == 2) {
+        if (syncwake::in_batch) syncwake::pending |= 1u << k;
+        else syncwake::wake(k);
+    }
 }
 }  // namespace
 
@@ -4174,13 +4255,21 @@ int tm_match_coalesced(tm_engine* e, const uint8_t* topic, size_t len, uint32_t*
     SyncWait w;
     w.ids = ids;
     w.cap = cap;
+    static std::atomic<uint32_t> next_word{0};
+    static thread_local uint32_t my_word = next_word.fetch_add(1) % syncwake::WAKE_WORDS;
+    w.word = my_word;
     int rc = tm_match_async(e, topic, len, sync_cb, &w);
     if (rc) return rc;
     for (int i = 0; i < 4000 && w.state.load(std::memory_order_acquire) != 1; ++i) __builtin_ia32_pause();
     int expect = 0;
-    if (w.state.compare_exchange_strong(expect, 2, std::memory_order_acq_rel))
-        while (w.state.load(std::memory_order_acquire) == 2)
-            syscall(SYS_futex, reinterpret_cast<int*>(&w.state), FUTEX_WAIT_PRIVATE, 2, nullptr, nullptr, 0);
+    if (w.state.compare_exchange_strong(expect, 2, std::memory_order_acq_rel)) {
+        std::atomic<uint32_t>& seq = syncwake::words[w.word].seq;
+        for (;;) {
+            const uint32_t s0 = seq.load(std::memory_order_acquire);   // before the state check: no lost wake-up
+            if (w.state.load(std::memory_order_acquire) != 2) break;
+            syncwake::futex(&seq, FUTEX_WAIT, s0);
+        }
+    }
     *n_out = w.n;
     return w.rc;
 }

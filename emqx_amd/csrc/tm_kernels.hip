@@ -396,6 +396,9 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
     }
 }
 
+#ifndef TM_LOG_U
+#define TM_LOG_U 12  // log entries per lane per read-back step, all in flight (4 / 8 / 12 / 16: 5.10 / 5.07 / 5.04 / 5.05 ms)
+#endif
 #ifndef TM_EMIT_ROWS
 // Emission log variant of the tile epilogue: the tile's matches were appended
 // to a wave-private log in iteration order (coalesced: one store of <= 64
@@ -426,11 +429,11 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
         L.depth[lane] = in_chunk ? pos - p0 : NONE;   // (free after the frontier loop) row base in the stage
         L.toff[lane] = 0;                            // row fill cursor
         __syncthreads();
-        for (uint32_t k0 = 0; k0 < lcount; k0 += 256) {
-            unsigned long long e[4];
-            uint32_t r[4];
+        for (uint32_t k0 = 0; k0 < lcount; k0 += 64 * TM_LOG_U) {
+            unsigned long long e[TM_LOG_U];
+            uint32_t r[TM_LOG_U];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < TM_LOG_U; ++u) {
                 const uint32_t k = k0 + lane + 64 * u;
                 r[u] = 64;
                 if (k < lcount) {
@@ -439,7 +442,7 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
                 }
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < TM_LOG_U; ++u) {
                 if (r[u] >= 64) continue;
                 const uint32_t base = L.depth[r[u]];
                 if (base == NONE) continue;
@@ -2237,9 +2240,12 @@ __global__ void tm_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKe
 // fewer per wave so that they spread over >= ~2048 waves -- a tile's latency
 // is its probe count / 64 iterations, so one topic per wave walks in about
 // depth dependent rounds instead of the 64 topics' combined frontier.
+#ifndef TM_MIN_TILES
+#define TM_MIN_TILES 2048   // small batches: tiles shrink until there are this many
+#endif
 uint32_t tile_topics(uint32_t n) {
     uint32_t tt = 64;
-    while (tt > 1 && (n + tt - 1) / tt < 2048) tt >>= 1;
+    while (tt > 1 && (n + tt - 1) / tt < TM_MIN_TILES) tt >>= 1;
     return tt;
 }
 
@@ -2429,6 +2435,10 @@ uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes) {
     // the most topics (64 at most) whose average bytes fill ~3/4 of the LDS window
     uint32_t tt = TILE;
     while (tt > 1 && (uint64_t)tt * nbytes > (uint64_t)(TOK_BYTES * 3 / 4) * (n ? n : 1)) tt >>= 1;
+    // small batches (per-publish calls): at least 32 tiles down to 4 topics a
+    // tile -- one wave walking a whole 64-topic tile's lookups is a chain of
+    // dependent rounds; several short tiles run them side by side
+    while (tt > 4 && (n + tt - 1) / tt < 32) tt >>= 1;
     return tt;
 }
 
