@@ -117,6 +117,7 @@ struct tm_sharded_batch {
     std::vector<uint64_t> mseg;           // first match of each part's rows (+ total)
     uint64_t total = 0;
     bool done = false;
+    bool direct = false;   // one shard: the result is the part's own CSR (no partition, no reorder)
     // host result
     uint32_t *h_row = nullptr, *h_ids = nullptr;
     size_t ch_row = 0, ch_ids = 0;
@@ -180,11 +181,50 @@ struct tm_sharded {
         return TM_OK;
     }
 
+    // One shard: every publish is its own part and the rows come back in
+    // publish order -- no owner kernel, no partition, no reorder; global ids
+    // are the local ones (local * 1 + 0).
+    int step_one(tm_sharded_batch* b) {
+        int rc;
+        const uint32_t n = b->n;
+        const double t1 = now_ms();
+        if (b->part.size() != 1) b->part.assign(1, nullptr);
+        static const uint32_t zero_off = 0;
+        if (!n) {
+            SH_HIP(hipSetDevice(home));
+            SH_HIP(hipMemcpy(b->toff.p, &zero_off, 4, hipMemcpyHostToDevice));
+        }
+        if ((rc = tm_batch_prepare_tokens(sh[0], b->words.p, b->toff.p, b->tflags.p, n, b->nwords, 1, &b->part[0])))
+            return rc;
+        if ((rc = tm_batch_launch(sh[0], b->part[0]))) return rc;
+        if ((rc = tm_batch_wait(sh[0], b->part[0]))) return rc;
+        tm_batch_stats p{};
+        if ((rc = tm_batch_stats_get(sh[0], b->part[0], &p))) return rc;
+        if (p.matches > MAX_RESULT) return TM_EOVERFLOW;
+        b->st = p;
+        b->st.topics = n;
+        b->tseg.assign(2, 0);
+        b->tseg[1] = n;
+        b->wseg.assign(2, 0);
+        b->wseg[1] = (uint32_t)b->nwords;
+        b->mseg.assign(2, 0);
+        b->mseg[1] = p.matches;
+        b->ms_partition = 0;
+        b->ms_parts = (float)(now_ms() - t1);
+        b->ms_unpartition = 0;
+        b->total = p.matches;
+        b->direct = true;
+        b->done = true;
+        return TM_OK;
+    }
+
     int step(tm_sharded_batch* b) {
         int rc;
         const uint32_t n = b->n;
         b->done = false;
+        b->direct = false;
         if (b->dict_words != dict_words() && (rc = tokenize(b))) return rc;   // new words since tokenisation
+        if (G == 1) return step_one(b);
         const double t0 = now_ms();
         // ---- owner and partition (home device)
         const uint32_t nb = std::max<uint32_t>(1, (n + PART_BLOCK - 1) / PART_BLOCK);
@@ -516,9 +556,15 @@ int tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out) {
     int rc;
     if ((rc = host_pinned(b->h_row, b->ch_row, (size_t)b->n + 1))) return rc;
     if ((rc = host_pinned(b->h_ids, b->ch_ids, std::max<uint64_t>(b->total, 1)))) return rc;
+    const uint32_t* d_row = b->rowg.p;
+    const uint32_t* d_ids = b->out.p;
+    if (b->direct) {   // one shard: the part's CSR (built here on first use)
+        uint64_t m = 0;
+        if ((rc = tm_batch_device_csr(s->sh[0], b->part[0], &d_row, &d_ids, &m))) return rc;
+    }
     SH_HIP(hipSetDevice(s->home));
-    SH_HIP(hipMemcpyAsync(b->h_row, b->rowg.p, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, s->s));
-    if (b->total) SH_HIP(hipMemcpyAsync(b->h_ids, b->out.p, b->total * 4, hipMemcpyDeviceToHost, s->s));
+    SH_HIP(hipMemcpyAsync(b->h_row, d_row, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, s->s));
+    if (b->total) SH_HIP(hipMemcpyAsync(b->h_ids, d_ids, b->total * 4, hipMemcpyDeviceToHost, s->s));
     SH_HIP(hipStreamSynchronize(s->s));
     if (b->h_row[b->n] != b->total) {
         snprintf(error_buf(), 512, "inconsistent sharded CSR: %u vs %llu", b->h_row[b->n], (unsigned long long)b->total);
@@ -534,6 +580,10 @@ int tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out) {
 int tm_sharded_device_csr(tm_sharded* s, tm_sharded_batch* b, const uint32_t** d_row_offsets, const uint32_t** d_ids,
                           uint64_t* n_matches) {
     if (!s || !b || !b->done) return TM_EINVAL;
+    if (b->direct) {
+        std::lock_guard<std::mutex> lk(s->mu);
+        return tm_batch_device_csr(s->sh[0], b->part[0], d_row_offsets, d_ids, n_matches);
+    }
     if (d_row_offsets) *d_row_offsets = b->rowg.p;
     if (d_ids) *d_ids = b->out.p;
     if (n_matches) *n_matches = b->total;

@@ -34,7 +34,7 @@ def rows_of(grp, offs, ids):
     return [[fb(x) for x in ids[offs[i]:offs[i + 1]]] for i in range(len(offs) - 1)]
 
 
-@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("G", [1, 2, 3])
 def test_shards_on_one_device_with_online_dictionary_deltas(G):
     """The IoT workload plus irregular filters and topics ('$', '' levels,
     deep, root wildcards); the dictionary starts EMPTY and grows only by the
