@@ -61,23 +61,6 @@ __device__ __forceinline__ uint32_t dig_P(uint32_t c) { return (0x3344u >> (4 * 
 
 __device__ __forceinline__ int key_shift(uint32_t level) { return 61 - 3 * (int)level; }
 
-// The tile kernel's path code, packed (k5): the digits (0..4) of levels 0..9
-// in pairs, each pair 5 * d(2j) + d(2j+1) in 5 bits, pair 0 highest; level
-// 10's digit in the lowest 3 bits: 28 bits in all, ordered like the digit
-// string, so the probe entries carry it in one u32 and an emission is ONE u64
-//   k5 << 36 | topic lane << 30 | filter id (30 bits)
-// (no separate lane log).  A digit at level l adds d * k5w(l).
-constexpr uint32_t K5_LANE_SHIFT = 30, K5_KEY_SHIFT = 36;
-constexpr uint64_t K5_FID_MASK = (1ull << K5_LANE_SHIFT) - 1;
-__device__ __forceinline__ uint32_t k5w(uint32_t l) {
-    const uint32_t w = ((l & 1u) ? 1u : 5u) << ((23u - 5u * (l >> 1)) & 31u);
-    return l >= 10u ? 1u : w;
-}
-__device__ __forceinline__ uint64_t k5_entry(uint32_t k5, uint32_t lane, uint32_t fid) {
-    return ((uint64_t)k5 << K5_KEY_SHIFT) | ((uint64_t)lane << K5_LANE_SHIFT) | fid;
-}
-static_assert(FAST_MAX_DEPTH <= 10, "k5 holds the digits of levels 0..10");
-
 __device__ __forceinline__ uint64_t put_digit(uint64_t key, uint32_t level, uint32_t d) {
     return level <= FAST_MAX_DEPTH ? (key | ((uint64_t)d << key_shift(level))) : key;
 }
@@ -217,29 +200,6 @@ __device__ __forceinline__ void expand_root(const RootRec& r, bool dollar, uint3
     if (!dollar && (r.flags & NF_PLUS)) add_p(x, (uint64_t)dig_P(cls) << 61, M_PLUS);
 }
 
-// expand_root with k5 keys (the tile kernel)
-struct Expand5 {
-    uint32_t ne, np;
-    uint32_t ef0, ek0;
-    uint32_t pf0, pf1, pk0, pk1;
-};
-__device__ __forceinline__ void expand_root5(const RootRec& r, bool dollar, uint32_t d, uint32_t w0, Expand5& x) {
-    x.ne = 0; x.np = 0;
-    const uint32_t cls = w0 >> WID_BITS, id = w0 & WID_MASK;
-    const uint32_t w = k5w(0);
-    auto add_p5 = [&](uint32_t key, uint32_t fl) {
-        if (x.np == 0) { x.pk0 = key; x.pf0 = fl; } else { x.pk1 = key; x.pf1 = fl; }
-        x.np++;
-    };
-    if (!dollar && r.hterm != NONE) { x.ef0 = r.hterm; x.ek0 = dig_H(cls) * w; x.ne = 1; }
-    if (id == W_HASH) {
-        if (!dollar && (r.flags & NF_HASH)) add_p5(dig_L(cls) * w, (d == 1) ? M_SKIPE : 0u);
-    } else if (id != W_UNKNOWN && id != W_PLUS) {
-        add_p5(dig_L(cls) * w, dollar ? M_DSTART : 0u);
-    }
-    if (!dollar && (r.flags & NF_PLUS)) add_p5(dig_P(cls) * w, M_PLUS);
-}
-
 // Per-wave LDS of the tile kernel.  The probe stack holds QC 16-B entries
 // {key lo | meta, key hi, parent, word to probe (the literal w[lc-1] or
 // W_PLUS / W_HASH)}: one ds_write_b128 per push, one ds_read_b128 per pop.
@@ -257,15 +217,15 @@ struct alignas(16) TileLds {
     static constexpr uint32_t STAGE = (QC * 16 + WCAP * 4) / 8;
 };
 
-__device__ __forceinline__ uint4 q_pack(uint32_t k5, uint32_t meta, uint32_t parent, uint32_t pw) {
-    return uint4{meta, k5, parent, pw};
+__device__ __forceinline__ uint4 q_pack(uint64_t key, uint32_t meta, uint32_t parent, uint32_t pw) {
+    return uint4{(uint32_t)key | meta, (uint32_t)(key >> 32), parent, pw};
 }
 
 // Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
 // wrows = this wave's rows (rows + blockIdx.x * tile_topics * K), hoisted by the caller.
 template <bool CK>
 __device__ __forceinline__ void emit_row(const MatchArgs& a, unsigned long long* wrows, uint32_t tl, uint32_t slot,
-                                         uint32_t key, uint32_t fid) {
+                                         uint64_t key, uint32_t fid) {
 #ifdef TM_EXPERIMENT_NO_EMIT   // timing experiments only
     if (slot < a.row_cap && fid == 0xFFFFFFF0u) {
 #else
@@ -277,7 +237,7 @@ __device__ __forceinline__ void emit_row(const MatchArgs& a, unsigned long long*
         const uint32_t i = tl * a.row_cap + slot;   // < tile_topics * K <= 2^16
 #endif
         if (CK) (void)CK_((uint64_t)blockIdx.x * a.tile_topics * a.row_cap + i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13);
-        wrows[i] = k5_entry(key, tl, fid);
+        wrows[i] = (key & KEY_MASK) | fid;
     }
 }
 
@@ -327,7 +287,7 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
     constexpr uint32_t STAGE = LT::STAGE;
     const uint32_t lane = threadIdx.x;
     const unsigned long long* stg = reinterpret_cast<const unsigned long long*>(L.q);
-    if (keep && c == 1) a.sfids[CK_(dst, a.sfids_cap, 40)] = (uint32_t)(stg[CK_(pos, STAGE, 41)] & K5_FID_MASK);
+    if (keep && c == 1) a.sfids[CK_(dst, a.sfids_cap, 40)] = (uint32_t)(stg[CK_(pos, STAGE, 41)] & ~KEY_MASK);
 #pragma unroll
     for (uint32_t W = 2; W <= 64; W <<= 1) {
         const bool mine = keep && c > W / 2 && c <= W;
@@ -359,7 +319,7 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
                     key = (lower == up) ? lo : hi;
                 }
             }
-            if (rv && e < cr) a.sfids[CK_((uint64_t)dr + e, a.sfids_cap, 44)] = (uint32_t)(key & K5_FID_MASK);
+            if (rv && e < cr) a.sfids[CK_((uint64_t)dr + e, a.sfids_cap, 44)] = (uint32_t)(key & ~KEY_MASK);
         }
         __syncthreads();
     }
@@ -386,8 +346,8 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
                 r0 += kj < k0 ? 1u : 0u;
                 r1 += kj < k1 ? 1u : 0u;
             }
-            if (lane < cr) a.sfids[CK_((uint64_t)dr + r0, a.sfids_cap, 47)] = (uint32_t)(k0 & K5_FID_MASK);
-            if (lane + 64 < cr) a.sfids[CK_((uint64_t)dr + r1, a.sfids_cap, 48)] = (uint32_t)(k1 & K5_FID_MASK);
+            if (lane < cr) a.sfids[CK_((uint64_t)dr + r0, a.sfids_cap, 47)] = (uint32_t)(k0 & ~KEY_MASK);
+            if (lane + 64 < cr) a.sfids[CK_((uint64_t)dr + r1, a.sfids_cap, 48)] = (uint32_t)(k1 & ~KEY_MASK);
         }
     }
 }
@@ -449,7 +409,7 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
 // sorted as before.
 template <bool CK, class LT>
 __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst,
-                                              const unsigned long long* wlog, uint32_t lcount) {
+                                              const unsigned long long* wlog, const uint8_t* wlane, uint32_t lcount) {
     constexpr uint32_t STAGE = LT::STAGE;
     const uint32_t lane = threadIdx.x;
     unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
@@ -476,12 +436,10 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
             for (uint32_t u = 0; u < TM_LOG_U; ++u) {
                 const uint32_t k = k0 + lane + 64 * u;
                 r[u] = 64;
-                if (k < lcount) e[u] = wlog[k];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < TM_LOG_U; ++u) {
-                const uint32_t k = k0 + lane + 64 * u;
-                if (k < lcount) r[u] = (uint32_t)(e[u] >> K5_LANE_SHIFT) & 63u;
+                if (k < lcount) {
+                    e[u] = wlog[k];
+                    r[u] = wlane[k];
+                }
             }
 #pragma unroll
             for (uint32_t u = 0; u < TM_LOG_U; ++u) {
@@ -531,8 +489,11 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const bool active = !(fl & TF_SLOW);
     unsigned long long* const wrows = a.rows + (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
 #ifndef TM_EMIT_ROWS
-    // the wave's log: its rows region, k5 entries (the topic lane inside)
+    // the wave's log: its rows region (entries) + a byte per entry (topic lane)
+    // past the whole rows array
     const uint32_t lcap = a.tile_topics * a.row_cap;
+    uint8_t* const wlane =
+        reinterpret_cast<uint8_t*>(a.rows + (uint64_t)a.grid * lcap) + (uint64_t)blockIdx.x * lcap;
     uint32_t lcount = 0;
 #endif
     uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
@@ -540,7 +501,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
 
     // ---- level 0: root expansion, one topic per lane
     {
-        Expand5 x; x.ne = 0; x.np = 0;
+        Expand x; x.ne = 0; x.np = 0;
         uint32_t w0 = 0;
         if (active && d_me > 0) {
             const bool dollar = fl & TF_DOLLAR;
@@ -548,7 +509,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             if (!dollar && (a.root.flags & NF_HASH)) tH += 1;
             tW += d_me;
             w0 = wsrc[CK_(L.toff[lane], wlim, 9)];
-            expand_root5(a.root, dollar, d_me, w0, x);
+            expand_root(a.root, dollar, d_me, w0, x);
         }
         const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
         const uint32_t pre = prefix_count(b0) + prefix_count(b1);
@@ -561,7 +522,9 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         const uint64_t mr = __ballot(x.ne != 0);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
-            wrows[prefix_count(mr)] = k5_entry(x.ek0, lane, x.ef0);
+            const uint32_t i = prefix_count(mr);
+            wrows[i] = (x.ek0 & KEY_MASK) | x.ef0;
+            wlane[i] = (uint8_t)lane;
         }
         lcount = (uint32_t)__popcll(mr);
 #else
@@ -602,8 +565,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         const uint32_t idx = qn + lane;
         uint4 e = uint4{0u, 0u, 0u, 0u};
         if (has) e = L.q[idx];
-        const uint32_t meta = e.x;
-        const uint32_t key = e.y;   // k5
+        const uint32_t meta = e.x & 0x7FFFFFFFu;
+        const uint64_t key = ((uint64_t)e.y << 32) | (e.x & 0x80000000u);
         const uint32_t parent = e.z, pw = e.w;
         const uint32_t tl = meta & 63;
         const uint32_t lc = (meta >> M_LVL_SHIFT) & M_LVL_MASK;
@@ -674,10 +637,10 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         // lc <= FAST_MAX_DEPTH here, so every level has a digit position.
         const bool at_end = lc == d;
         const uint32_t cls = w_here >> WID_BITS, id = w_here & WID_MASK;
-        const uint32_t kw = k5w(lc);   // a digit at level lc adds d * kw
+        const int sh = key_shift(lc);
         bool eA = false, eB = false, pL = false, pP = false;
         uint32_t fA = 0;
-        uint32_t kA = key;
+        uint64_t kA = key;
         if (found) {
             if (!(meta & M_DSTART)) tV += 1;
             if (s.flags & NF_HASH) tH += 1;
@@ -686,17 +649,14 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
                 fA = s.term;
                 // '' word at level lc-1 followed by the end: "P/" sorts before "P/#"
                 if ((w_prev >> WID_BITS) == C_EMPTY) {
-                    // level lc - 1 (<= 9) chose L (digit 4 for this class): L_lo = 1
-                    const uint32_t p = lc - 1;
-                    const uint32_t f = (kA >> (23u - 5u * (p >> 1))) & 31u;
-                    const uint32_t hi = (f * 13u) >> 6;   // f / 5 for f <= 24
-                    if (((p & 1u) ? f - 5u * hi : hi) == 4u) kA -= 3u * k5w(p);
+                    const int sp = key_shift(lc - 1);
+                    if (((kA >> sp) & 7) == 4) kA = (kA & ~(7ull << sp)) | (1ull << sp);
                 }
                 eB = s.hterm != NONE;
             } else {        // '#' child's topic, then the literal and '+' edges
                 eA = s.hterm != NONE;
                 fA = s.hterm;
-                kA = key + dig_H(cls) * kw;
+                kA = key | ((uint64_t)dig_H(cls) << sh);
                 pL = id == W_HASH ? (s.flags & NF_HASH) != 0 : (id != W_UNKNOWN && id != W_PLUS);
                 pP = (s.flags & NF_PLUS) != 0;
             }
@@ -710,9 +670,9 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         if (sL) {
             const uint32_t lfl = (id == W_HASH && lc + 1 == d) ? M_SKIPE : 0u;
             L.q[pre] = cont ? q_pack(key, meta + (1u << M_DISP_SHIFT), parent, pw)
-                            : q_pack(key + dig_L(cls) * kw, nmeta | lfl, s.child, id);
+                            : q_pack(key | ((uint64_t)dig_L(cls) << sh), nmeta | lfl, s.child, id);
         }
-        if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key + dig_P(cls) * kw, nmeta | M_PLUS, s.child, W_PLUS);
+        if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key | ((uint64_t)dig_P(cls) << sh), nmeta | M_PLUS, s.child, W_PLUS);
         qn += ptot;
 #ifndef TM_EMIT_ROWS
         {
@@ -728,15 +688,23 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
 #ifdef TM_EXPERIMENT_NO_LOG   // (timing experiments only: counts kept, log stores dropped)
             eA = eB = false;
 #endif
-            if (eA) wrows[CK_(lcount + prefix_count(mA), lcap, 13)] = k5_entry(kA, tl, fA);
-            if (eB) wrows[CK_(lcount + nA + prefix_count(mB), lcap, 14)] = k5_entry(key + 2u * kw, tl, s.hterm);
+            if (eA) {
+                const uint32_t i = lcount + prefix_count(mA);
+                wrows[CK_(i, lcap, 13)] = (kA & KEY_MASK) | fA;
+                wlane[i] = (uint8_t)tl;
+            }
+            if (eB) {
+                const uint32_t i = lcount + nA + prefix_count(mB);
+                wrows[CK_(i, lcap, 14)] = ((key | (2ull << sh)) & KEY_MASK) | s.hterm;
+                wlane[i] = (uint8_t)tl;
+            }
             lcount += nE;
         }
 #else
         if (eA | eB) {
             const uint32_t slot = atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));
             if (eA) emit_row<CK>(a, wrows, tl, slot, kA, fA);
-            if (eB) emit_row<CK>(a, wrows, tl, slot + (eA ? 1u : 0u), key + 2u * kw, s.hterm);
+            if (eB) emit_row<CK>(a, wrows, tl, slot + (eA ? 1u : 0u), key | (2ull << sh), s.hterm);
         }
 #endif
     }
@@ -778,7 +746,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if (fits) {
 #ifndef TM_EMIT_ROWS
-        sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, lcount);
+        sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount);
 #else
         sort_rows<CK, LT>(a, L, keep, c, dst);
 #endif
@@ -2273,7 +2241,7 @@ __global__ void tm_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKe
 // is its probe count / 64 iterations, so one topic per wave walks in about
 // depth dependent rounds instead of the 64 topics' combined frontier.
 #ifndef TM_MIN_TILES
-#define TM_MIN_TILES 512    // small batches: tiles shrink until there are this many (4,096-topic batch p50: 2048 -> 0.16 ms, 1024 -> 0.10, 512 -> 0.07)
+#define TM_MIN_TILES 256    // small batches: tiles shrink until there are this many (4,096-topic batch p50: 2048 / 1024 / 512 / 256 / 128 -> 0.16 / 0.10 / 0.07 / 0.063 / 0.082 ms)
 #endif
 uint32_t tile_topics(uint32_t n) {
     uint32_t tt = 64;

@@ -68,34 +68,3 @@ def test_model_overflow_tiles_still_exact():
         tr.insert(f)
     for t, row in zip(T, rows):
         assert row == sorted(set(tr.match(t)))
-
-
-def test_k5_packed_path_code_keeps_digit_order():
-    """The tile kernel carries path codes packed (tm_kernels.hip k5w /
-    k5_entry): digits 0..4 of levels 0..9 in pairs 5*d(2j) + d(2j+1) of 5
-    bits, level 10 in the low 3 bits -- 28 bits, so an emission is one u64
-    with the topic lane inside.  The packing must order like the digit
-    strings, and a digit must decode back ((f * 13) >> 6 = f / 5 for the
-    L_lo patch)."""
-    import random
-
-    def k5w(level):
-        return 1 if level >= 10 else (1 if level & 1 else 5) << (23 - 5 * (level >> 1))
-
-    def pack(ds):
-        return sum(d * k5w(lv) for lv, d in enumerate(ds))
-
-    assert all(((f * 13) >> 6) == f // 5 for f in range(25))
-    rng = random.Random(5)
-    for _ in range(50_000):
-        a = [rng.randint(0, 4) for _ in range(11)]
-        b = [rng.randint(0, 4) for _ in range(11)]
-        if rng.random() < 0.5:
-            k = rng.randint(0, 10)
-            b[:k] = a[:k]
-        assert (a < b) == (pack(a) < pack(b)) and (a == b) == (pack(a) == pack(b))
-        assert pack(a) < 1 << 28
-        p = rng.randint(0, 9)
-        f = (pack(a) >> (23 - 5 * (p >> 1))) & 31
-        hi = (f * 13) >> 6
-        assert (f - 5 * hi if p & 1 else hi) == a[p]
