@@ -716,7 +716,7 @@ struct WorkPool {
 // recorded; the counters, dirty lists, filter bytes and freed ids collect
 // here and are merged afterwards.  Phase 2 applies the recorded edge work by
 // bucket ranges.
-struct Mut {
+struct alignas(64) Mut {   // (one cache line boundary per worker: no false sharing of counters)
     bool defer = false;
     std::vector<uint32_t>* ids = nullptr;               // the batch's node ids: free ones, then fresh ones
     std::atomic<size_t>* next_id = nullptr;             //   (shared by the workers)
@@ -1439,21 +1439,29 @@ struct tm_engine {
     // independent cache misses in flight instead of one chain per filter.
     static constexpr uint32_t PLAN_G = 16;
     void plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part) {
-        std::vector<uint32_t>& W = plan_words[part];
+        // the part's vectors are worked on as locals and put back at the end:
+        // the per-part vector headers share cache lines, and a push_back per
+        // word on them from 8-16 threads was a false-sharing storm (plan of
+        // 5,000 filters: 0.45 us per filter on one thread, 3-5x that per
+        // thread on eight)
+        std::vector<uint32_t> W;
+        W.swap(plan_words[part]);
         W.clear();
+        std::vector<TWord> all;
+        all.swap(plan_tw[part]);
         std::vector<TWord> ws;
         std::vector<uint64_t> hs;
         const bool root_live = nd[ROOT].live != 0;
         const uint32_t nb = nbuckets();
         static const bool ptrace = getenv("TM_PLAN_TRACE") != nullptr;
         std::chrono::steady_clock::duration d_split{}, d_dict{}, d_walk{};
+        using clk = std::chrono::steady_clock;
         for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
-            const auto c0 = std::chrono::steady_clock::now();
+            const auto c0 = ptrace ? clk::now() : clk::time_point{};
             const uint32_t g1 = std::min(hi, g0 + PLAN_G);
             // words and their dictionary entries
             const uint32_t wbase = (uint32_t)W.size();
             hs.clear();
-            std::vector<TWord>& all = plan_tw[part];
             all.clear();
             for (uint32_t i = g0; i < g1; ++i) {
                 PlanEnt& pe = plan[i];
@@ -1466,12 +1474,12 @@ struct tm_engine {
                     hs.push_back(w.n == 0 || is_plus(w) || is_hash(w) ? 0 : dict.prefetch(w.p, w.n));
                 }
             }
-            const auto c1 = std::chrono::steady_clock::now();
+            const auto c1 = ptrace ? clk::now() : clk::time_point{};
             for (size_t j = 0; j < all.size(); ++j) {
                 const TWord& w = all[j];
                 W.push_back(w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find_h(w.p, w.n, hs[j]));
             }
-            const auto c2 = std::chrono::steady_clock::now();
+            const auto c2 = ptrace ? clk::now() : clk::time_point{};
             d_split += c1 - c0;
             d_dict += c2 - c1;
             // the existing paths, level by level over the group
@@ -1509,8 +1517,10 @@ struct tm_engine {
                 if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
                 else { pe.node = node[q]; pe.depth = k[q]; }
             }
-            d_walk += std::chrono::steady_clock::now() - c2;
+            if (ptrace) d_walk += clk::now() - c2;
         }
+        plan_words[part].swap(W);
+        plan_tw[part].swap(all);
         if (ptrace) {
             auto us = [](auto d) { return std::chrono::duration<double, std::micro>(d).count(); };
             fprintf(stderr, "  [plan part %u: %u filters] split+hash %.0f us, dict %.0f us, walk %.0f us\n", part, hi - lo,
@@ -1768,6 +1778,7 @@ struct tm_engine {
             }
         }
         ensure_pool();
+        const auto ts0 = std::chrono::steady_clock::now();
         std::vector<Mut> W(T);
         // by the first two words: one worker owns those subtrees; 8 parts per
         // worker, taken largest first by whichever worker is free (skewed
@@ -1897,8 +1908,8 @@ struct tm_engine {
         if (getenv("TM_PAR_TRACE")) {
             const auto tp3 = std::chrono::steady_clock::now();
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "[par %s n=%u T=%u] phase1 %.2f ms edges %.2f ms merge %.2f ms; workers (items, us):", del ? "del" : "ins", n, T,
-                    ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
+            fprintf(stderr, "[par %s n=%u T=%u] setup %.2f ms phase1 %.2f ms edges %.2f ms merge %.2f ms; workers (items, us):",
+                    del ? "del" : "ins", n, T, ms(ts0, tp0), ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
             for (const Mut& m : W) fprintf(stderr, " (%zu, %.0f)", m.n_items, m.t_us);
             fprintf(stderr, "\n");
         }
@@ -4640,6 +4651,9 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
             if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(false, filters, offsets, n, &done, &rc)) {
                 if (n_inserted) *n_inserted = done;
+                if (getenv("TM_PAR_TRACE"))
+                    fprintf(stderr, "[insert_many n=%u] %.2f ms in the call\n", n,
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
                 return rc;
             }
             for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
@@ -4684,6 +4698,9 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
         if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(true, filters, offsets, n, &done, &rc)) {
             if (n_deleted) *n_deleted = done;
+            if (getenv("TM_PAR_TRACE"))
+                fprintf(stderr, "[delete_many n=%u] %.2f ms in the call\n", n,
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
             return rc;
         }
         for (uint32_t i = 0; i < n && rc == TM_OK; ++i) {
