@@ -407,9 +407,12 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
 // rows at a time -- the log is streamed (L2-resident: written moments ago)
 // and every entry of a chunk's rows goes to its row's next free place -- and
 // sorted as before.
+#ifndef TM_LOG_REM
+#define TM_LOG_REM 1   // passes after the first read only the entries of rows not yet done (compacted in place)
+#endif
 template <bool CK, class LT>
 __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst,
-                                              const unsigned long long* wlog, const uint8_t* wlane, uint32_t lcount) {
+                                              unsigned long long* wlog, uint8_t* wlane, uint32_t lcount) {
     constexpr uint32_t STAGE = LT::STAGE;
     const uint32_t lane = threadIdx.x;
     unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
@@ -420,15 +423,23 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
         if (lane >= (uint32_t)o) incl += u;
     }
     const uint32_t pos = incl - cw;
+    constexpr uint32_t REM = NONE - 1;   // a kept row of a later chunk
     uint32_t rs = 0;
     while (rs < a.tile_topics) {
         const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
         const uint64_t beyond = __ballot(lane >= rs && pos + cw - p0 > STAGE);
         const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : a.tile_topics;
         const bool in_chunk = keep && lane >= rs && lane < re;
-        L.depth[lane] = in_chunk ? pos - p0 : NONE;   // (free after the frontier loop) row base in the stage
+        // (depth / toff are free after the frontier loop) row base in the stage,
+        // REM for rows of later chunks, NONE for rows not staged here
+        L.depth[lane] = in_chunk ? pos - p0 : ((TM_LOG_REM && keep && lane >= re) ? REM : NONE);
         L.toff[lane] = 0;                            // row fill cursor
         __syncthreads();
+        // With a later chunk, this pass also moves the entries of the later
+        // chunks' rows to the front of the log (positions already read: the
+        // remainder never outruns the reads), so the next pass reads only them.
+        const bool more = TM_LOG_REM && re < a.tile_topics;
+        uint32_t wr = 0;
         for (uint32_t k0 = 0; k0 < lcount; k0 += 64 * TM_LOG_U) {
             unsigned long long e[TM_LOG_U];
             uint32_t r[TM_LOG_U];
@@ -443,16 +454,26 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
             }
 #pragma unroll
             for (uint32_t u = 0; u < TM_LOG_U; ++u) {
-                if (r[u] >= 64) continue;
-                const uint32_t base = L.depth[r[u]];
-                if (base == NONE) continue;
+                const uint32_t base = r[u] < 64 ? L.depth[r[u]] : NONE;
+                if (more) {
+                    const bool rem = base == REM;
+                    const uint64_t m = __ballot(rem);
+                    if (rem) {
+                        const uint32_t at = wr + prefix_count(m);
+                        wlog[at] = e[u];
+                        wlane[at] = (uint8_t)r[u];
+                    }
+                    wr += (uint32_t)__popcll(m);
+                }
+                if (base >= REM) continue;
                 const uint32_t at = base + atomicAdd(&L.toff[r[u]], 1u);
                 stg[CK_(at, STAGE, 49)] = e[u];
             }
         }
-        __syncthreads();
+        __syncthreads();   // (also: the moved entries are visible to the next pass's loads)
         sort_classes<CK, LT>(a, L, in_chunk, c, pos - p0, dst);
         __syncthreads();
+        if (more) lcount = wr;
         rs = re;
     }
 }
