@@ -411,10 +411,8 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
 #define TM_LOG_REM 0   // 1: passes after the first read only the entries of rows not yet done, compacted in place (A/B: 5.037 -> 5.027 ms, WRITE_SIZE +0.8 GB: off)
 #endif
 template <bool CK, class LT>
-__device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t& dst,
-                                              unsigned long long* wlog, uint8_t* wlane, uint32_t lcount,
-                                              const unsigned long long& base_lane0, uint32_t tot, uint32_t g,
-                                              uint32_t excl) {
+__device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst,
+                                              unsigned long long* wlog, uint8_t* wlane, uint32_t lcount) {
     constexpr uint32_t STAGE = LT::STAGE;
     const uint32_t lane = threadIdx.x;
     unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
@@ -473,18 +471,6 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
             }
         }
         __syncthreads();   // (also: the moved entries are visible to the next pass's loads)
-        if (rs == 0) {
-            // the staging reservation was issued before the read-back: its
-            // return is needed only now
-            unsigned long long b64 = __shfl(base_lane0, 0, 64);
-            const bool fits = b64 + tot <= a.rcap;
-            b64 += (uint64_t)g * a.rcap;
-            dst = fits ? (uint32_t)b64 + excl : NONE;
-            if (!fits) {
-                if (lane == 0) atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
-                return;
-            }
-        }
         sort_classes<CK, LT>(a, L, in_chunk, c, pos - p0, dst);
         __syncthreads();
         if (more) lcount = wr;
@@ -773,21 +759,21 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     unsigned long long base64 = 0;
     const uint32_t g = (blockIdx.x % TICKET_GROUPS) & a.sgmask;   // my group's staging region
     if (lane == 0 && tot) base64 = atomicAdd(xg_top(a.xg, g), (unsigned long long)tot);
-#if !defined(TM_EMIT_ROWS) && !defined(TM_EXPERIMENT_NO_EPILOGUE)
-    uint32_t dst = 0;
-    sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount, base64, tot, g, incl - c);
-#else
     base64 = __shfl(base64, 0, 64);
     const bool fits = base64 + tot <= a.rcap;
     base64 += (uint64_t)g * a.rcap;
-    const uint32_t dst = (uint32_t)base64 + incl - c;
+    const uint32_t base = (uint32_t)base64;
+    const uint32_t dst = base + incl - c;
 #ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if (fits) {
+#ifndef TM_EMIT_ROWS
+        sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount);
+#else
         sort_rows<CK, LT>(a, L, keep, c, dst);
+#endif
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
     }
-#endif
 #endif
     if (keep) {
         a.count[CK_(t, a.n, 16)] = c_me;
@@ -1837,6 +1823,9 @@ __device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint32_t n, bool& irre
 template <class P>
 __device__ __forceinline__ bool ck_match(const TokArgs& a, const uint4& e, uint64_t head, uint32_t n, P p) {
     if (e.z != n || e.x != (uint32_t)head || e.y != (uint32_t)(head >> 32)) return false;
+#ifdef TM_EXPERIMENT_TOK_NO_TAIL   // (timing experiments only: words over 8 bytes match on head + length)
+    return true;
+#endif
     if (n <= 8) return true;
     const DictTail t = a.tails[e.w];
     uint64_t h2 = 0;
