@@ -397,9 +397,10 @@ def run_c5(args, ws, rank, local, sync):
     # route_apply hands over).  Step i applies deltas i (emqx_trie:delete/1 and
     # insert/1 on the host mirror) and matches batch i against the result.
     # Pipelined: the host applies deltas i + 1 while the device walks batch i
-    # -- the host mirror and the HBM replica are separate, and launch i + 1
-    # uploads deltas i + 1 (read-your-writes) -- so the step costs
-    # max(apply, device) rather than their sum.
+    # -- the host mirror and the HBM replica are separate, and the upload of
+    # deltas i + 1 is queued behind walk i on the engine stream, ahead of
+    # launch i + 1 (read-your-writes) -- so the step costs max(apply, device)
+    # rather than their sum.
     deltas = []
     for _ in range(args.steps):
         dels, adds = churn.step(args.c5_deltas)
@@ -415,6 +416,10 @@ def run_c5(args, ws, rank, local, sync):
             tc = time.perf_counter()
             Churn.apply(eng, *deltas[i + 1])
             ms_churn.append(1e3 * (time.perf_counter() - tc))
+            # the deltas' upload is gathered and enqueued now, behind batch i's
+            # walk on the engine stream (pinned staging: no host wait), so
+            # launch i + 1 has nothing left to upload
+            eng.sync_async()
         b.wait()
         st = b.stats()
         ms_match.append(st["ms_total"])

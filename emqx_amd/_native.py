@@ -120,6 +120,7 @@ SIGNATURES = {
     "tm_version": (C.c_uint64, [P]),
     "tm_stats": (C.c_int, [P, C.POINTER(EngineStats)]),
     "tm_sync": (C.c_int, [P]),
+    "tm_sync_async": (C.c_int, [P]),
     "tm_trie_insert": (C.c_int, [P, U8P, SZ]),
     "tm_trie_delete": (C.c_int, [P, U8P, SZ]),
     "tm_trie_lookup": (C.c_int, [P, U8P, SZ, C.c_int, C.POINTER(TrieNode)]),

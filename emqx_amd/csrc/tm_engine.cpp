@@ -4122,6 +4122,15 @@ int tm_sync(tm_engine* e) {
     return e->set_device();
 }
 
+int tm_sync_async(tm_engine* e) {
+    if (!e) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    if ((rc = e->sync_device())) return rc;
+    return e->set_device();
+}
+
 int tm_trie_insert(tm_engine* e, const uint8_t* t, size_t len) {
     if (!e || (!t && len)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);

@@ -702,6 +702,10 @@ class Engine:
     def sync(self):
         N.check(self.L.tm_sync(self.h), "tm_sync")
 
+    def sync_async(self):
+        """Queue the pending deltas' upload now, without waiting (tm_sync_async)."""
+        N.check(self.L.tm_sync_async(self.h), "tm_sync_async")
+
     def debug_check(self) -> int:
         """tm_debug_check: edge-hash invariants; -> largest displacement."""
         md = C.c_uint64()

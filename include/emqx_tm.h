@@ -141,6 +141,10 @@ TM_API int  tm_stats(tm_engine* e, tm_engine_stats* out);
 /* Applies pending trie deltas to the device replica (also done implicitly by
  * every match call). */
 TM_API int  tm_sync(tm_engine* e);
+/* tm_sync without the wait: the pending deltas are gathered now and their
+ * upload is queued on every replica's stream, behind the work already there
+ * (a walk in flight keeps its snapshot) and ahead of the next launch. */
+TM_API int  tm_sync_async(tm_engine* e);
 
 /* ---- emqx_trie (src/emqx_trie.erl) ----------------------------------- */
 /* emqx_trie:insert/1 (:81-93): idempotent; add_path/1 (:145-158) semantics. */

@@ -376,3 +376,33 @@ def test_stream_batches_overlap_and_read_your_writes():
         live -= set(rem)
     a.free()
     b.free()
+
+
+def test_sync_async_queues_the_upload_behind_a_walk_in_flight():
+    """tm_sync_async: deltas applied while a batch walks are uploaded behind it
+    on the engine stream -- the walk in flight keeps its snapshot, the next
+    launch sees the new filters."""
+    p = replace(gen.C1, n_filters=3000)
+    F = gen.gen_filters(p).tolist()
+    Ts = gen.gen_topics(p, gen.Strings.from_list(F), 31, 50_000)
+    T = Ts.tolist()
+    eng = Engine(device=0)
+    eng.insert_many(F[:2000])
+    eng.sync()
+    b = eng.prepare(Ts)
+    b.launch()
+    eng.insert_many(F[2000:])       # while the walk is in flight
+    eng.delete_many(F[:100])
+    eng.sync_async()
+    b.wait()
+    cache = {}
+
+    def rows():
+        offs, ids = b.result()
+        return [[cache.setdefault(int(i), eng.filter_bytes(int(i))) for i in r] for r in rows_of(offs, ids)]
+    exp_old, _ = oracle_rows(F[:2000], T)
+    assert_same(T, rows(), exp_old)
+    b.launch().wait()
+    exp_new, _ = oracle_rows(F[100:], T)
+    assert_same(T, rows(), exp_new)
+    b.free()
