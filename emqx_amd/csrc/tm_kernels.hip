@@ -890,7 +890,10 @@ __device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp
     }
 }
 
-constexpr uint32_t SORT_LDS = 2048;
+#ifndef TM_SORT_LDS
+#define TM_SORT_LDS 2048   // generic path: rows up to this many are sorted in LDS (12 B each: it bounds waves per CU)
+#endif
+constexpr uint32_t SORT_LDS = TM_SORT_LDS;
 constexpr uint32_t SM_PLUS = 1u << 29;
 constexpr uint32_t SM_SKIPE = 1u << 30;
 constexpr uint32_t SM_DSTART = 1u << 31;
