@@ -396,9 +396,6 @@ __device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, 
     }
 }
 
-#ifndef TM_SCALAR_STATS
-#define TM_SCALAR_STATS 1   // the frontier loop counts V / H / bucket reads by ballots (SALU), not per lane
-#endif
 #ifndef TM_LOG_U
 #define TM_LOG_U 12  // log entries per lane per read-back step, all in flight (4 / 8 / 12 / 16: 5.10 / 5.07 / 5.04 / 5.05 ms)
 #endif
@@ -521,9 +518,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     uint32_t lcount = 0;
 #endif
     uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
-#if TM_SCALAR_STATS
-    uint32_t uV = 0, uH = 0, uP = 0;            // the frontier loop's counts, wave-uniform (SALU)
-#endif
     const uint32_t d_me = L.depth[lane];
 
     // ---- level 0: root expansion, one topic per lane
@@ -588,11 +582,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         qn -= k;
-#if TM_SCALAR_STATS
-        uP += k;                    // bucket reads (hits, misses, continuations)
-#else
         tP += lane == 0 ? k : 0u;   // bucket reads (hits, misses, continuations)
-#endif
         const uint32_t idx = qn + lane;
         uint4 e = uint4{0u, 0u, 0u, 0u};
         if (has) e = L.q[idx];
@@ -673,10 +663,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         uint32_t fA = 0;
         uint64_t kA = key;
         if (found) {
-#if !TM_SCALAR_STATS
             if (!(meta & M_DSTART)) tV += 1;
             if (s.flags & NF_HASH) tH += 1;
-#endif
             if (at_end) {   // end of the words: own topic, then the '#' child's
                 eA = !(meta & M_SKIPE) && s.term != NONE;
                 fA = s.term;
@@ -694,10 +682,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
                 pP = (s.flags & NF_PLUS) != 0;
             }
         }
-#if TM_SCALAR_STATS
-        uV += (uint32_t)__popcll(__ballot(found && !(meta & M_DSTART)));
-        uH += (uint32_t)__popcll(__ballot(found && (s.flags & NF_HASH)));
-#endif
         const bool sL = cont || pL;
         const uint64_t bL = __ballot(sL), bP = __ballot(pP);
         const uint32_t ptot = __popcll(bL) + __popcll(bP);
@@ -757,9 +741,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         send_to_slow<CK>(a, valid && active, t);
         return;
     }
-#if TM_SCALAR_STATS && !defined(TM_EXPERIMENT_PHASES)
-    if (lane == 0) { tV += uV; tH += uH; tP += uP; }
-#endif
     sV += tV; sH += tH; sW += tW; sP += tP;
     const uint32_t c_me = L.cnt[lane];
     const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
