@@ -131,3 +131,33 @@ def test_words_cap_overflow_is_reported():
         eng.tokenize_device(topics, words_cap=399)
     w, t, f = eng.tokenize_device(topics, words_cap=400)
     assert int(t[-1]) == 400
+
+
+def test_flat_tokeniser_on_large_batches_equals_host_tokens():
+    """From 65,536 topics the device tokeniser splits in tiles but looks every
+    word up in a flat pass, one thread per word, its bytes read from HBM
+    around its start: same tokens as the host on the generated workload plus
+    the edge cases (empty and separator-only topics, 7-24-byte words across
+    the 8/16-byte boundaries, a 4,096-byte topic on the lane-per-topic path,
+    UTF-8, unknown words), and the words-cap overflow still reported."""
+    p = replace(gen.C1, n_filters=20000)
+    filters = gen.gen_filters(p).tolist()
+    adv = load_golden("synth_adversarial.json")
+    filters += [lb(f) for f in adv["filters"]]
+    eng = Engine(device=0)
+    for f in filters:
+        eng.insert(f)
+    for n in (7, 8, 9, 15, 16, 17, 24):
+        eng.insert(b"k" * n + b"/" + b"z" * n)
+    words = sorted({w for f in filters for w in f.split(b"/")})
+    topics = gen.gen_topics(p, gen.Strings.from_list(filters[:20000]), 9, 70000).tolist()
+    edge = [lb(t) for t in adv["topics"]] + edge_topics(words)
+    edge += [b"k" * n + b"/" + b"z" * n for n in (7, 8, 9, 15, 16, 17, 24)]
+    topics = topics[:30000] + edge + topics[30000:] + edge
+    assert len(topics) >= 65536
+    assert_tokens_equal(eng, topics)
+    big = [b"a/b/c/d"] * 70000
+    with pytest.raises(Exception):
+        eng.tokenize_device(big, words_cap=279999)
+    w, t, f = eng.tokenize_device(big, words_cap=280000)
+    assert int(t[-1]) == 280000
