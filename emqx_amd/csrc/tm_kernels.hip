@@ -2275,50 +2275,80 @@ __device__ __forceinline__ uint32_t dw_of(uint64_t lo, uint64_t hi, uint32_t k) 
     return (uint32_t)(v >> (32 * (k & 1)));
 }
 
+#ifndef TM_TOK_LU
+#define TM_TOK_LU 4   // words per thread per round of the flat lookup, every load of a round in flight
+#endif
 __global__ __launch_bounds__(256) void tm_tok_lookup(TokArgs a) {
-    const uint32_t total = *a.d_total;
+    constexpr uint32_t U = TM_TOK_LU;
+    const uint32_t total = min<uint64_t>(*a.d_total, a.words_cap);
     const uint32_t mask = (uint32_t)a.dict_mask;
-    for (uint32_t w = blockIdx.x * 256 + threadIdx.x; w < total && w < a.words_cap;
-         w += gridDim.x * 256) {
-        const uint32_t p0 = a.wpos[w], p1 = a.wpos[w + 1];
-        const uint32_t s = p0 & ~WPOS_FIRST;
-        const uint32_t n = (p1 & ~WPOS_FIRST) - s - ((p1 & WPOS_FIRST) ? 0u : 1u);
-        // bytes s .. s + 15 (the batch's buffer has 16 bytes of slack past its end)
-        const uint64_t* q = reinterpret_cast<const uint64_t*>(a.bytes + (s & ~7u));
-        const uint32_t sh = (s & 7u) * 8u;
-        const uint64_t x0 = q[0], x1 = q[1];
-        const uint64_t x2 = ((s & 7u) + n > 16u) ? q[2] : 0ull;
-        uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-        uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
-        if (n < 8) { lo &= (1ull << (8u * n)) - 1ull; hi = 0; }
-        else if (n < 16) hi &= (1ull << (8u * (n - 8u))) - 1ull;
-        const uint8_t c0 = (uint8_t)lo;
-        bool irr = false;
-        const uint32_t cls = tok_class(c0, n, irr);
-        uint32_t id;
-        if (n == 0) id = W_EMPTY;
-        else if (n == 1 && c0 == '+') id = W_PLUS;
-        else if (n == 1 && c0 == '#') id = W_HASH;
-        else if (n > 16) id = dict_find(a, a.bytes + s, n);   // (rare: bytes 16.. live in the arena)
-        else {
-            uint32_t h1 = HW_SEED, h2 = HW_SEED2;
-            for (uint32_t k = 0; 4 * k < n; ++k) {   // dwords of the word, the tail zero-padded
-                const uint32_t d = dw_of(lo, hi, k);
-                h1 = hw_step(h1, d);
-                h2 = hw_step(h2, d);
-            }
-            const uint4 e1 = *reinterpret_cast<const uint4*>(a.keys + (hw_final(h1, n) & mask));
-            id = W_UNKNOWN;
-            if (e1.w != 0) {   // an empty primary slot: absent (slots are never emptied)
-                if (ck_match16(a, e1, lo, hi, n)) {
-                    id = e1.w;
-                } else {
-                    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (hw_final(h2, n) & mask));
-                    if (ck_match16(a, e2, lo, hi, n)) id = e2.w;
+    const uint32_t stride = gridDim.x * 256 * U;
+    for (uint32_t w0 = blockIdx.x * 256 * U + threadIdx.x; w0 < total; w0 += stride) {
+        // word w0 + 256 k: coalesced wpos loads, then every word's bytes
+        uint32_t s[U], n[U];
+        uint64_t lo[U], hi[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k) {
+            const uint32_t w = w0 + 256 * k;
+            const uint32_t p0 = w < total ? a.wpos[w] : 0u, p1 = w < total ? a.wpos[w + 1] : 0u;
+            s[k] = p0 & ~WPOS_FIRST;
+            n[k] = w < total ? (p1 & ~WPOS_FIRST) - s[k] - ((p1 & WPOS_FIRST) ? 0u : 1u) : 0u;
+        }
+        uint64_t x0[U], x1[U], x2[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k) {
+            // bytes s .. s + 15 (the batch's buffer has 16 bytes of slack past its end)
+            const uint64_t* q = reinterpret_cast<const uint64_t*>(a.bytes + (s[k] & ~7u));
+            x0[k] = q[0];
+            x1[k] = q[1];
+            x2[k] = ((s[k] & 7u) + n[k] > 16u) ? q[2] : 0ull;
+        }
+        uint32_t cls[U], id[U], h1[U];
+        bool look[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k) {
+            const uint32_t sh = (s[k] & 7u) * 8u;
+            lo[k] = sh ? (x0[k] >> sh) | (x1[k] << (64u - sh)) : x0[k];
+            hi[k] = sh ? (x1[k] >> sh) | (x2[k] << (64u - sh)) : x1[k];
+            const uint32_t nk = n[k];
+            if (nk < 8) { lo[k] &= (1ull << (8u * nk)) - 1ull; hi[k] = 0; }
+            else if (nk < 16) hi[k] &= (1ull << (8u * (nk - 8u))) - 1ull;
+            const uint8_t c0 = (uint8_t)lo[k];
+            bool irr = false;
+            cls[k] = tok_class(c0, nk, irr);
+            id[k] = nk == 0 ? W_EMPTY : (nk == 1 && c0 == '+') ? W_PLUS : (nk == 1 && c0 == '#') ? W_HASH : W_UNKNOWN;
+            look[k] = w0 + 256 * k < total && id[k] == W_UNKNOWN;
+            uint32_t h = HW_SEED;
+            for (uint32_t j = 0; 4 * j < nk && j < 4; ++j) h = hw_step(h, dw_of(lo[k], hi[k], j));   // dwords, tail zero-padded
+            h1[k] = h;
+        }
+        uint4 e[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k)   // every primary slot in flight at once
+            e[k] = look[k] && n[k] <= 16 ? *reinterpret_cast<const uint4*>(a.keys + (hw_final(h1[k], n[k]) & mask))
+                                         : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k) {
+            if (!look[k]) continue;
+            const uint32_t nk = n[k];
+            if (nk > 16) {   // (rare: bytes 16.. live in the arena)
+                id[k] = dict_find(a, a.bytes + s[k], nk);
+            } else if (e[k].w != 0) {   // an empty primary slot: absent (slots are never emptied)
+                if (ck_match16(a, e[k], lo[k], hi[k], nk)) {
+                    id[k] = e[k].w;
+                } else {   // the alternate slot: the second hash, only here
+                    uint32_t g = HW_SEED2;
+                    for (uint32_t j = 0; 4 * j < nk && j < 4; ++j) g = hw_step(g, dw_of(lo[k], hi[k], j));
+                    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (hw_final(g, nk) & mask));
+                    if (ck_match16(a, e2, lo[k], hi[k], nk)) id[k] = e2.w;
                 }
             }
         }
-        a.words[w] = (cls << WID_BITS) | id;
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k) {
+            const uint32_t w = w0 + 256 * k;
+            if (w < total) a.words[w] = (cls[k] << WID_BITS) | id[k];
+        }
     }
 }
 
@@ -2590,7 +2620,7 @@ hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, 
         f.d_total = d_nwords;
         hipLaunchKernelGGL(tm_tok_fill<true>, dim3(min(ntiles, cap_fill_flat)), dim3(64), 0, s, f);
         // one thread per word (the total is on the device): a full chip's worth of blocks, grid-stride
-        hipLaunchKernelGGL(tm_tok_lookup, dim3(2048), dim3(256), 0, s, f);
+        hipLaunchKernelGGL(tm_tok_lookup, dim3(1536), dim3(256), 0, s, f);   // 6 waves / SIMD at 77 VGPRs
     } else {
         hipLaunchKernelGGL(tm_tok_fill<false>, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
     }
