@@ -436,8 +436,7 @@ struct tm_batch {
     const uint64_t* in_offs = nullptr;
     uint64_t seen_upload = 0;   // own-stream batches: the last trie upload this batch's stream waited for
     uint32_t* d_wcount = nullptr;
-    uint32_t* d_wpos = nullptr;   // flat tokeniser: word starts (large batches)
-    size_t c_bytes = 0, c_boffs = 0, c_wcount = 0, c_wpos = 0;
+    size_t c_bytes = 0, c_boffs = 0, c_wcount = 0;
     uint64_t tok_base = 0;
     uint32_t *d_nslow = nullptr, *h_bad = nullptr;
     size_t c_nslow = 0, ch_bad = 0;
@@ -478,7 +477,7 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in); dev_free(d_wpos);
+        dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in);
         in_bytes = nullptr;
         in_offs = nullptr;
         if (h_bad) (void)hipHostFree(h_bad);
@@ -2787,11 +2786,6 @@ struct tm_engine {
         t.wcount = b->d_wcount; t.tflags = d_tflags; t.toff = d_toff; t.words = d_words; t.words_cap = cap;
         t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
         t.tile_topics = tok_tile_topics(n, nbytes);
-        t.offs_nbytes = nbytes;
-        if (tok_flat(n, nbytes)) {
-            if ((rc = dev_reserve(b->d_wpos, b->c_wpos, cap + 1))) return rc;
-            t.wpos = b->d_wpos;
-        }
         ScanArgs ts{};
         ts.block_sums = b->d_bsums;
         HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, stream));
@@ -3146,11 +3140,6 @@ struct tm_engine {
             t.keys = R.d_dkey; t.tails = R.d_tail; t.dict_mask = R.d_dict_n - 1; t.arena = R.d_arena;
             t.wcount = b->d_wcount; t.tflags = b->d_tflags; t.toff = b->d_toff; t.words = b->d_words;
             t.words_cap = b->c_words;
-            t.offs_nbytes = b->nwords - b->n;   // nwords = bytes + topics (reserve_tokens)
-            if (tok_flat(b->n, t.offs_nbytes)) {
-                if ((rc = dev_reserve(b->d_wpos, b->c_wpos, b->c_words + 1))) return rc;
-                t.wpos = b->d_wpos;
-            }
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
             t.tile_topics = tok_tile_topics(b->n, b->nwords - b->n);   // nwords = bytes + topics (reserve_tokens)
             ScanArgs ts{};

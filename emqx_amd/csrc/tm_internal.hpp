@@ -420,17 +420,7 @@ struct TokArgs {
     uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
     uint32_t zero_words;
     uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
-    // large batches (tok_flat): pass 2 only splits -- every word's byte start
-    // (from base) | FIRST-of-its-topic into wpos[], plus a sentinel at the
-    // end -- and pass 3 looks every word up, one thread per word
-    uint32_t* wpos;           // words_cap + 1 entries (nullptr: never flat)
-    const uint32_t* d_total;  // the word total (the tile scan's)
-    uint64_t offs_nbytes;     // the batch's bytes (offs[n] - base): flat only under 2 GB
 };
-constexpr uint32_t WPOS_FIRST = 0x80000000u;
-// the flat split + lookup is used from this many topics up (and batches under 2 GB)
-constexpr uint32_t TOK_FLAT_MIN = 65536;
-inline bool tok_flat(uint32_t n, uint64_t nbytes) { return n >= TOK_FLAT_MIN && nbytes < WPOS_FIRST; }
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);

@@ -2074,23 +2074,7 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
     }
 }
 
-// FLAT pass 2, LDS path: the tile's words w = lane + 64 k, each its byte
-// start (from base) | FIRST into wpos[], coalesced; the irregular-word mark
-// ('+' followed by more bytes) for its topic.  No dictionary work here.
-__device__ __forceinline__ void tok_mark(const TokArgs& a, TokLds& L, uint32_t tw, uint32_t wend, uint64_t tile_base,
-                                         uint32_t a0) {
-    for (uint32_t w = threadIdx.x; w < tw; w += 64) {
-        const uint32_t st = L.wst[w];
-        const uint32_t s0 = st & 0x7FFFu;
-        const uint32_t nx = w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u);
-        const uint32_t n = (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u);
-        if (n > 1 && L.bytes[s0] == '+') L.tirr[L.wtop[w]] = 1;
-        if (tile_base + w < a.words_cap) a.wpos[tile_base + w] = (a0 + s0) | ((st & 0x8000u) ? WPOS_FIRST : 0u);
-    }
-}
-
 // lane-per-topic path of a tile too long for the LDS budget: bytes from HBM
-template <bool FLAT>
 __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t t, uint64_t o, bool& slow) {
     const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
     const uint8_t* p = a.bytes;
@@ -2099,13 +2083,8 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
     uint64_t ws = b;
     for (uint64_t i = b;; ++i) {
         if (i == e || p[i] == '/') {
-            if (FLAT) {   // the word's start; its lookup is pass 3's
-                if (o < a.words_cap) a.wpos[o] = (uint32_t)ws | (ws == b ? WPOS_FIRST : 0u);
-                if (i - ws > 1 && p[ws] == '+') irregular = true;
-            } else {
-                const uint32_t w = word_entry(a, p + ws, (uint32_t)(i - ws), irregular);
-                if (o < a.words_cap) a.words[o] = w;
-            }
+            const uint32_t w = word_entry(a, p + ws, (uint32_t)(i - ws), irregular);
+            if (o < a.words_cap) a.words[o] = w;
             ++o;
             ++nw;
             if (i == e) break;
@@ -2123,7 +2102,6 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
 #ifndef TM_TOK_WPE
 #define TM_TOK_WPE 5
 #endif
-template <bool FLAT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
     __shared__ TokLds L;
     const uint32_t lane = threadIdx.x;
@@ -2206,10 +2184,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             }
             tw = __shfl(tincl, 63, 64);
         }
-        if (tend == a.n && lane == 0) {
-            a.toff[a.n] = (uint32_t)(tile_base + tw);
-            if (FLAT && tile_base + tw < a.words_cap + 1) a.wpos[tile_base + tw] = (uint32_t)b1 | WPOS_FIRST;   // sentinel
-        }
+        if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
         if (lds) {
             uint32_t wi = (incl - mine) & 0xFFFFu;            // my first word
             int32_t tc = (int32_t)((incl - mine) >> 16) - 1;   // the topic my first byte is in
@@ -2232,8 +2207,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             if (lane == 0) L.ttoff[cnt] = tw;
             __syncthreads();
 #ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
-            if (FLAT) tok_mark(a, L, tw, wend, tile_base, (uint32_t)a0);
-            else tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
+            tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
 #endif
             __syncthreads();
             if (valid) {
@@ -2251,103 +2225,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             const uint64_t o = tile_base + tincl - nw;
             if (valid) {
                 a.toff[t] = (uint32_t)o;
-                tok_fill_topic_global<FLAT>(a, t, o, slow);
+                tok_fill_topic_global(a, t, o, slow);
             }
             tok_append_slow(a, slow, t);
-        }
-    }
-}
-
-// FLAT pass 3: one thread per word.  Its bytes come from HBM as (up to)
-// three aligned u64 loads around its start -- consecutive words are
-// consecutive bytes, so a wave's loads stay within a few lines -- then the
-// same class, reserved atoms and dictionary probe as tok_lookup: the primary
-// cuckoo slot for every word at once, the alternate only where the primary
-// holds another word.  No tile rounds, no LDS, no per-tile divergence.
-// does cuckoo key e hold the word of <= 16 bytes (lo, hi) of length n?
-__device__ __forceinline__ bool ck_match16(const TokArgs& a, const uint4& e, uint64_t lo, uint64_t hi, uint32_t n) {
-    if (e.z != n || e.x != (uint32_t)lo || e.y != (uint32_t)(lo >> 32)) return false;
-    return n <= 8 || a.tails[e.w].head2 == hi;
-}
-
-__device__ __forceinline__ uint32_t dw_of(uint64_t lo, uint64_t hi, uint32_t k) {   // dword k (< 4) of 16 bytes
-    const uint64_t v = k < 2 ? lo : hi;
-    return (uint32_t)(v >> (32 * (k & 1)));
-}
-
-#ifndef TM_TOK_LU
-#define TM_TOK_LU 4   // words per thread per round of the flat lookup, every load of a round in flight
-#endif
-__global__ __launch_bounds__(256) void tm_tok_lookup(TokArgs a) {
-    constexpr uint32_t U = TM_TOK_LU;
-    const uint32_t total = min<uint64_t>(*a.d_total, a.words_cap);
-    const uint32_t mask = (uint32_t)a.dict_mask;
-    const uint32_t stride = gridDim.x * 256 * U;
-    for (uint32_t w0 = blockIdx.x * 256 * U + threadIdx.x; w0 < total; w0 += stride) {
-        // word w0 + 256 k: coalesced wpos loads, then every word's bytes
-        uint32_t s[U], n[U];
-        uint64_t lo[U], hi[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t w = w0 + 256 * k;
-            const uint32_t p0 = w < total ? a.wpos[w] : 0u, p1 = w < total ? a.wpos[w + 1] : 0u;
-            s[k] = p0 & ~WPOS_FIRST;
-            n[k] = w < total ? (p1 & ~WPOS_FIRST) - s[k] - ((p1 & WPOS_FIRST) ? 0u : 1u) : 0u;
-        }
-        uint64_t x0[U], x1[U], x2[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            // bytes s .. s + 15 (the batch's buffer has 16 bytes of slack past its end)
-            const uint64_t* q = reinterpret_cast<const uint64_t*>(a.bytes + (s[k] & ~7u));
-            x0[k] = q[0];
-            x1[k] = q[1];
-            x2[k] = ((s[k] & 7u) + n[k] > 16u) ? q[2] : 0ull;
-        }
-        uint32_t cls[U], id[U], h1[U];
-        bool look[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t sh = (s[k] & 7u) * 8u;
-            lo[k] = sh ? (x0[k] >> sh) | (x1[k] << (64u - sh)) : x0[k];
-            hi[k] = sh ? (x1[k] >> sh) | (x2[k] << (64u - sh)) : x1[k];
-            const uint32_t nk = n[k];
-            if (nk < 8) { lo[k] &= (1ull << (8u * nk)) - 1ull; hi[k] = 0; }
-            else if (nk < 16) hi[k] &= (1ull << (8u * (nk - 8u))) - 1ull;
-            const uint8_t c0 = (uint8_t)lo[k];
-            bool irr = false;
-            cls[k] = tok_class(c0, nk, irr);
-            id[k] = nk == 0 ? W_EMPTY : (nk == 1 && c0 == '+') ? W_PLUS : (nk == 1 && c0 == '#') ? W_HASH : W_UNKNOWN;
-            look[k] = w0 + 256 * k < total && id[k] == W_UNKNOWN;
-            uint32_t h = HW_SEED;
-            for (uint32_t j = 0; 4 * j < nk && j < 4; ++j) h = hw_step(h, dw_of(lo[k], hi[k], j));   // dwords, tail zero-padded
-            h1[k] = h;
-        }
-        uint4 e[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k)   // every primary slot in flight at once
-            e[k] = look[k] && n[k] <= 16 ? *reinterpret_cast<const uint4*>(a.keys + (hw_final(h1[k], n[k]) & mask))
-                                         : uint4{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            if (!look[k]) continue;
-            const uint32_t nk = n[k];
-            if (nk > 16) {   // (rare: bytes 16.. live in the arena)
-                id[k] = dict_find(a, a.bytes + s[k], nk);
-            } else if (e[k].w != 0) {   // an empty primary slot: absent (slots are never emptied)
-                if (ck_match16(a, e[k], lo[k], hi[k], nk)) {
-                    id[k] = e[k].w;
-                } else {   // the alternate slot: the second hash, only here
-                    uint32_t g = HW_SEED2;
-                    for (uint32_t j = 0; 4 * j < nk && j < 4; ++j) g = hw_step(g, dw_of(lo[k], hi[k], j));
-                    const uint4 e2 = *reinterpret_cast<const uint4*>(a.keys + (hw_final(g, nk) & mask));
-                    if (ck_match16(a, e2, lo[k], hi[k], nk)) id[k] = e2.w;
-                }
-            }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t w = w0 + 256 * k;
-            if (w < total) a.words[w] = (cls[k] << WID_BITS) | id[k];
         }
     }
 }
@@ -2602,7 +2482,7 @@ static uint32_t resident_blocks(K kernel, int block) {
 
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
     static const uint32_t cap_count = resident_blocks(tm_tok_count, 64);
-    static const uint32_t cap_fill = resident_blocks(tm_tok_fill<false>, 64);
+    static const uint32_t cap_fill = resident_blocks(tm_tok_fill, 64);
     const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
     hipLaunchKernelGGL(tm_tok_count, dim3(ntiles ? min(ntiles, cap_count) : 1u), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
     if (!a.n) return hipGetLastError();
@@ -2613,17 +2493,7 @@ hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, 
     if (e != hipSuccess) return e;
     TokArgs f = a;
     f.bsums = scan.block_sums;
-    static const bool flat_on = getenv("TM_TOK_NO_FLAT") == nullptr;   // (A/B knob)
-    const bool flat = flat_on && a.wpos && tok_flat(a.n, a.offs_nbytes);
-    if (flat) {
-        static const uint32_t cap_fill_flat = resident_blocks(tm_tok_fill<true>, 64);
-        f.d_total = d_nwords;
-        hipLaunchKernelGGL(tm_tok_fill<true>, dim3(min(ntiles, cap_fill_flat)), dim3(64), 0, s, f);
-        // one thread per word (the total is on the device): a full chip's worth of blocks, grid-stride
-        hipLaunchKernelGGL(tm_tok_lookup, dim3(1536), dim3(256), 0, s, f);   // 6 waves / SIMD at 77 VGPRs
-    } else {
-        hipLaunchKernelGGL(tm_tok_fill<false>, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
-    }
+    hipLaunchKernelGGL(tm_tok_fill, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
     return hipGetLastError();
 }
 

@@ -133,13 +133,13 @@ def test_words_cap_overflow_is_reported():
     assert int(t[-1]) == 400
 
 
-def test_flat_tokeniser_on_large_batches_equals_host_tokens():
-    """From 65,536 topics the device tokeniser splits in tiles but looks every
-    word up in a flat pass, one thread per word, its bytes read from HBM
-    around its start: same tokens as the host on the generated workload plus
-    the edge cases (empty and separator-only topics, 7-24-byte words across
-    the 8/16-byte boundaries, a 4,096-byte topic on the lane-per-topic path,
-    UTF-8, unknown words), and the words-cap overflow still reported."""
+def test_large_batch_tokens_equal_host_tokens():
+    """A batch past 65,536 topics (multi-block tile scan, full-size tiles):
+    the same tokens as the host on the generated workload plus the edge cases
+    (empty and separator-only topics, 7-24-byte words across the 8/16-byte
+    boundaries, a 4,096-byte topic on the lane-per-topic path, UTF-8, unknown
+    words) placed mid-batch and at its end, and the words-cap overflow still
+    reported."""
     p = replace(gen.C1, n_filters=20000)
     filters = gen.gen_filters(p).tolist()
     adv = load_golden("synth_adversarial.json")
