@@ -536,6 +536,12 @@ struct AsyncSlot {
     uint32_t* h_rows = nullptr;
     size_t c_rows = 0;
     hipEvent_t ev_done = nullptr;
+    // polled completion (TM_ASYNC_SPIN_US): the stream writes seq into this
+    // pinned word after the export, the completer spins on it before it
+    // falls back to the event
+    uint32_t* h_flag = nullptr;
+    uint32_t* d_flag = nullptr;
+    uint32_t seq = 0;
     int rc = TM_OK;                      // launch failure (delivered to every call)
     bool claimed = false;                // a completer is delivering it
 };
@@ -643,6 +649,7 @@ struct Replica {
     // at least a_busy_min calls queued: under load, calls accumulate while the
     // device works instead of trickling out as tiny batches
     uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // tools/ab_async.sh
+    uint32_t a_spin_us = 0;   // completers poll a pinned flag this long before blocking on the event (0: off)
     uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0;
     // where the pipeline's time goes (host microseconds, summed over batches)
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
@@ -3457,6 +3464,7 @@ struct tm_engine {
         if (const char* d = getenv("TM_ASYNC_DEPTH")) R.a_depth = (uint32_t)std::min(16, std::max(1, atoi(d)));
         if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) R.a_busy_min = (uint32_t)std::max(1, atoi(d));
         if (const char* d = getenv("TM_ASYNC_COMPLETERS")) R.a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
+        if (const char* d = getenv("TM_ASYNC_SPIN_US")) R.a_spin_us = (uint32_t)std::min(10000, std::max(0, atoi(d)));
         {
             std::lock_guard<std::recursive_mutex> g(mu);
             HIP_OK(hipSetDevice(R.device));
@@ -3503,6 +3511,7 @@ struct tm_engine {
             if (sl->h_in) (void)hipHostFree(sl->h_in);
             if (sl->h_rows) (void)hipHostFree(sl->h_rows);
             if (sl->h_out) (void)hipHostFree(sl->h_out);
+            if (sl->h_flag) (void)hipHostFree(sl->h_flag);
             delete sl;
         }
         R.a_slots.clear();
@@ -3659,6 +3668,14 @@ struct tm_engine {
         x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
         x.rcap = std::min<uint64_t>(b->c_sfids, MAX_RESULT) / (b->one_region ? 1 : TICKET_GROUPS);
         HIP_OK(launch_export_host(x, S));
+        if (b->rep->a_spin_us) {
+            if (!sl->h_flag) {
+                HIP_OK(hipHostMalloc((void**)&sl->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+                *sl->h_flag = 0;
+                HIP_OK(hipHostGetDevicePointer((void**)&sl->d_flag, sl->h_flag, 0));
+            }
+            HIP_OK(hipStreamWriteValue32(S, sl->d_flag, ++sl->seq, 0));
+        }
         HIP_OK(hipEventRecord(sl->ev_done, S));
         return TM_OK;
     }
@@ -3719,6 +3736,18 @@ struct tm_engine {
             return false;
         }
         const auto tw = std::chrono::steady_clock::now();
+        if (sl->h_flag && b->rep->a_spin_us) {   // poll the pinned flag first (no interrupt wake-up)
+            const volatile uint32_t* f = sl->h_flag;
+            const auto lim = tw + std::chrono::microseconds(b->rep->a_spin_us);
+            for (uint32_t it = 0; *f != sl->seq; ++it) {
+                __builtin_ia32_pause();
+                if ((it & 255) == 0 && std::chrono::steady_clock::now() > lim) break;
+            }
+            // the flag follows the export in stream order; the event right after it
+            if (*f == sl->seq)
+                while (hipEventQuery(sl->ev_done) == hipErrorNotReady && std::chrono::steady_clock::now() < lim)
+                    __builtin_ia32_pause();
+        }
         if (hipEventSynchronize(sl->ev_done) != hipSuccess) {
             fail_all(TM_EIO);
             return false;
