@@ -12,11 +12,14 @@
 // node record's edge_count is kept so that emqx_trie:lookup/1 answers match
 // the reference's tests (test/emqx_trie_SUITE.erl:49-142).
 #include <linux/futex.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -329,9 +332,60 @@ struct HugeAlloc {
     bool operator!=(const HugeAlloc<U>&) const { return false; }
 };
 
+// host worker threads when tm_config.host_threads is 0: TM_HOST_THREADS, else
+// min(hardware threads, 16) -- the GPU box leases 16 CPUs of cgroup bandwidth
+// out of 256 hardware threads, so hardware_concurrency() alone overcounts.
 unsigned default_threads() {
+    if (const char* v = getenv("TM_HOST_THREADS")) {
+        const int t = atoi(v);
+        if (t > 0) return (unsigned)std::min(t, 64);
+    }
     unsigned h = std::thread::hardware_concurrency();
     return std::max(1u, std::min(h ? h : 1u, 16u));
+}
+
+// The CPUs of the NUMA node `device` is attached to (sysfs), within this
+// process's affinity: the churn workers run there, so the host mirror's pages
+// they first-touch and their random reads stay on one socket instead of
+// crossing to the other at the scheduler's whim.  False (no pinning) for a
+// host-only engine, a node-less device, fewer CPUs than `need`, or
+// TM_POOL_PIN=0.
+bool device_node_cpus(int device, unsigned need, cpu_set_t& out) {
+    if (device < 0) return false;
+    if (const char* v = getenv("TM_POOL_PIN"))
+        if (v[0] == '0') return false;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus - 1, device) != hipSuccess) return false;
+    for (char* c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
+    auto read_line = [](const std::string& path) {
+        std::string s;
+        if (FILE* f = fopen(path.c_str(), "r")) {
+            char buf[4096];
+            if (fgets(buf, sizeof buf, f)) s = buf;
+            fclose(f);
+        }
+        return s;
+    };
+    const std::string nodes = read_line(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+    if (nodes.empty()) return false;
+    const int node = atoi(nodes.c_str());
+    if (node < 0) return false;
+    const std::string list = read_line("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+    cpu_set_t mine;
+    CPU_ZERO(&mine);
+    if (list.empty() || sched_getaffinity(0, sizeof mine, &mine) != 0) return false;
+    CPU_ZERO(&out);
+    for (const char* p = list.c_str(); *p && *p != '\n';) {   // "0-63,128-191"
+        char* e;
+        const long a = strtol(p, &e, 10);
+        long b = a;
+        if (e == p) return false;
+        if (*e == '-') b = strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c >= 0 && CPU_ISSET(c, &mine)) CPU_SET(c, &out);
+        p = *e == ',' ? e + 1 : e;
+    }
+    return (unsigned)CPU_COUNT(&out) >= need;
 }
 
 }  // namespace
@@ -683,9 +737,13 @@ struct WorkPool {
         }
         return false;
     }
-    void start(unsigned k) {
+    // `cpus` (may be null): the CPUs the workers run on
+    void start(unsigned k, const cpu_set_t* cpus) {
         n = std::max(1u, k);
-        for (unsigned i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
+        for (unsigned i = 1; i < n; ++i) {
+            th.emplace_back([this, i] { loop(i); });
+            if (cpus) (void)pthread_setaffinity_np(th.back().native_handle(), sizeof(cpu_set_t), cpus);
+        }
     }
     void loop(unsigned i) {
         uint32_t seen = 0;
@@ -1629,7 +1687,8 @@ struct tm_engine {
 
     void ensure_pool() {
         if (!pool_started) {
-            pool.start(threads);
+            cpu_set_t cpus;
+            pool.start(threads, device_node_cpus(device, threads, cpus) ? &cpus : nullptr);
             pool_started = true;
         }
     }
