@@ -828,6 +828,17 @@ struct alignas(64) Mut {   // (one cache line boundary per worker: no false shar
     size_t n_items = 0;
     bool routes_dirty = false;
     int rc = TM_OK;
+    // back to a fresh worker state for the next batch, keeping the vectors'
+    // capacity: no allocation, page faults or table growth per churn batch
+    void reset() {
+        if (made_n) std::fill(made.begin(), made.end(), std::pair<uint64_t, uint32_t>{0, 0});
+        Mut n;
+        n.ins.swap(ins); n.del.swap(del); n.sum.swap(sum); n.made.swap(made); n.fb.swap(fb);
+        n.foff.swap(foff); n.dirty.swap(dirty); n.dirty_f.swap(dirty_f); n.pend.swap(pend);
+        n.ins.clear(); n.del.clear(); n.sum.clear(); n.fb.clear();
+        n.foff.clear(); n.dirty.clear(); n.dirty_f.clear(); n.pend.clear();
+        *this = std::move(n);
+    }
 };
 thread_local Mut* tl_mut = nullptr;
 
@@ -1485,6 +1496,7 @@ struct tm_engine {
     // worker reads and writes stripe p & 63 only under shared_mu(p))
     std::unordered_map<uint64_t, uint32_t> shared_made[64];
     WorkPool pool;            // workers of parallel batches (started at the first one)
+    std::vector<Mut> mut_w;   // their states (reset per batch, capacity kept)
     bool pool_started = false;
 
     struct PlanEnt {
@@ -1693,6 +1705,16 @@ struct tm_engine {
         }
     }
 
+    // a pass over node ids v touching each node's record and its slot: the
+    // record 16 nodes ahead, the slot (from the record, by then in cache) 8 ahead
+    void prefetch_edge_of(const std::vector<uint32_t>& v, size_t q) const {
+        if (q + 16 < v.size()) __builtin_prefetch(&nd[v[q + 16]]);
+        if (q + 8 < v.size()) {
+            const uint32_t s = nd[v[q + 8]].inslot;
+            if (s != NONE && s < slots.size()) __builtin_prefetch(&slots[s], 1);
+        }
+    }
+
     // Phase 2: the recorded edge work of W, by bucket range (see above).
     void edge_phase(std::vector<Mut>& W) {
         const unsigned T = (unsigned)W.size();
@@ -1738,7 +1760,10 @@ struct tm_engine {
                     if (t >= T2) return;
                     const uint32_t r = 2 * t + par;
                     tl_mut = &X[t];
-                    for (uint32_t c : per[r]) {
+                    const std::vector<uint32_t>& v = per[r];
+                    for (size_t q = 0; q < v.size(); ++q) {
+                        prefetch_edge_of(v, q);
+                        const uint32_t c = v[q];
                         // an odd range's slot may have been pulled back into the even range before it
                         if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
                         delete_edge_of(c);
@@ -1778,7 +1803,14 @@ struct tm_engine {
                 pool.run([&](unsigned t) {
                     if (t >= T2) return;
                     tl_mut = &X[t];
-                    for (const auto& e : per[2 * t + par]) insert_edge(e[0], e[1], e[2]);
+                    const auto& v = per[2 * t + par];
+                    for (size_t q = 0; q < v.size(); ++q) {
+                        if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
+                            __builtin_prefetch(&slots[(size_t)home_bucket(v[q + 8][0], v[q + 8][1], nb) * BUCKET], 1);
+                            __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                        }
+                        insert_edge(v[q][0], v[q][1], v[q][2]);
+                    }
                     tl_mut = nullptr;
                 });
             merge_edges(X);
@@ -1798,7 +1830,9 @@ struct tm_engine {
             std::vector<uint32_t>& v = per[t];
             std::sort(v.begin(), v.end());
             v.erase(std::unique(v.begin(), v.end()), v.end());
-            for (uint32_t c : v) {
+            for (size_t q = 0; q < v.size(); ++q) {
+                prefetch_edge_of(v, q);
+                const uint32_t c = v[q];
                 if (!nd[c].live || nd[c].inslot == NONE) continue;
                 write_summary_at(c, X[t].dirty);
             }
@@ -1845,7 +1879,9 @@ struct tm_engine {
         }
         ensure_pool();
         const auto ts0 = std::chrono::steady_clock::now();
-        std::vector<Mut> W(T);
+        if (mut_w.size() != T) mut_w.resize(T);
+        for (Mut& m : mut_w) m.reset();
+        std::vector<Mut>& W = mut_w;
         // by the first two words: one worker owns those subtrees; 8 parts per
         // worker, taken largest first by whichever worker is free (skewed
         // churn clusters under a few first words)
