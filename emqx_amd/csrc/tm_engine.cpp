@@ -1360,8 +1360,10 @@ struct tm_engine {
 
     // insert/1 with the word ids known and the path known to exist down to
     // `from` at level k0 (ROOT, 0 for a full walk)
+    // (sd: in a parallel batch, the nodes of depth < sd are shared by workers --
+    // 2, or 3 for the filters of a split part, see mutate_parallel)
     int trie_insert_ids(const uint8_t* t, size_t len, const uint32_t* ids_p, uint32_t nids, uint32_t from,
-                        uint32_t k0) {
+                        uint32_t k0, uint32_t sd = 2) {
         struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
         // add_path/1 for every triple (:145-158), in one walk: existing edges
         // are followed, the missing suffix is created
@@ -1370,13 +1372,13 @@ struct tm_engine {
         Mut* const M = tl_mut;
         for (size_t k = k0; k < ids.size(); ++k) {
             const uint32_t w = ids[k];
-            // (a parallel batch: the nodes of depth < 2 are shared by workers)
+            // (a parallel batch: the nodes of depth < sd are shared by workers)
             std::unique_lock<std::recursive_mutex> rl;
-            if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+            if (M && k < sd) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
             uint32_t c = NONE;
             if (M && M->defer) {   // an edge made earlier in this batch is not in the hash yet
-                // (levels 0-1: made by any worker, held in the stripe's shared map)
-                if (k < 2) {
+                // (levels < sd: made by any worker, held in the stripe's shared map)
+                if (k < sd) {
                     const auto& sm = shared_made[p & 63];
                     const auto it = sm.find((uint64_t)p << 32 | w);
                     if (it != sm.end()) c = it->second;
@@ -1410,13 +1412,13 @@ struct tm_engine {
                 if (w == W_PLUS) nd[p].plus = c;
                 else if (w == W_HASH) nd[p].hash = c;
                 insert_edge(p, w, c);
-                if (M && M->defer && k < 2) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
+                if (M && M->defer && k < sd) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
                 write_summary(p);
             }
             p = c;
         }
         std::unique_lock<std::recursive_mutex> tl;
-        if (M && ids.size() < 2) tl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+        if (M && ids.size() < sd) tl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
         if (!created && nd[p].topic) return TM_OK;   // inserted already: idempotent
         set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
         if (M) ++M->version;
@@ -1893,8 +1895,30 @@ struct tm_engine {
             const uint32_t key = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
             parts[mix_word(key) % P].push_back(i);
         }
-        std::vector<uint32_t> porder(P);
-        for (uint32_t q = 0; q < P; ++q) porder[q] = q;
+        // An insert part far above a worker's share (a hot first-two-words
+        // prefix, e.g. 10% of C5's churn under "+/+") is split by its third
+        // word: its filters then share the depth-2 nodes too, under the same
+        // striped locks and shared made map (parts split_from.. are those).
+        const uint32_t split_from = P;
+        if (!del) {
+            const size_t big = std::max<size_t>(64, n / (2 * T));
+            constexpr uint32_t SPLIT = 8;
+            for (uint32_t q = 0; q < split_from; ++q) {
+                if (parts[q].size() <= big) continue;
+                std::vector<uint32_t> whole;
+                whole.swap(parts[q]);
+                const size_t first = parts.size();
+                parts.resize(first + SPLIT);
+                for (uint32_t i : whole) {
+                    const PlanEnt& pe = plan[i];
+                    const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+                    parts[first + (pe.nw > 2 ? mix_word(w[2] * 0xC2B2AE35u + 7) % SPLIT : 0)].push_back(i);
+                }
+            }
+        }
+        const uint32_t NP = (uint32_t)parts.size();
+        std::vector<uint32_t> porder(NP);
+        for (uint32_t q = 0; q < NP; ++q) porder[q] = q;
         std::sort(porder.begin(), porder.end(), [&](uint32_t a, uint32_t b) { return parts[a].size() > parts[b].size(); });
         std::atomic<uint32_t> next_part{0};
         // node ids: at most the levels the batch's filters lack, the free ids first
@@ -1934,8 +1958,9 @@ struct tm_engine {
             tl_mut = &m;
             const auto tw0 = std::chrono::steady_clock::now();
             try {
-                for (uint32_t pi; !m.rc && (pi = next_part.fetch_add(1)) < P;) {
+                for (uint32_t pi; !m.rc && (pi = next_part.fetch_add(1)) < NP;) {
                     const std::vector<uint32_t>& items = parts[porder[pi]];
+                    const uint32_t sd = porder[pi] >= split_from ? 3 : 2;
                     const size_t ni = items.size();
                     m.n_items += ni;
                     for (size_t q = 0; q < ni; ++q) {
@@ -1950,7 +1975,7 @@ struct tm_engine {
                             rc = delete_planned(i);
                         } else {
                             rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
-                                                 plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth);
+                                                 plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth, sd);
                         }
                         if (rc) { m.rc = rc; break; }
                         ++m.done;

@@ -149,3 +149,29 @@ def test_parallel_insert_creates_a_shared_first_level_edge_once():
     a, b = A.stats(), B.stats()
     assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
     B.debug_check()
+
+
+def test_parallel_insert_splits_a_hot_two_word_prefix():
+    """A bulk insert with most of its filters under one first-two-words prefix
+    (C5's "+/+" share) splits that part by the third word: the prefix's
+    depth-2 node is then shared by workers, so its new children, its own
+    filter and the new nodes above it must each come out once."""
+    p = gen.SkewParams(seed=23, n_hot=500, k_per_hot=40)
+    allf, _, _, _ = workload(p, 20_000, 100, seed=23, background_pool=500)
+    A = Engine(device=-1, host_threads=1)
+    B = Engine(device=-1, host_threads=8)
+    adds = [b"hp/hq/%d/%d" % (i % 50, i) for i in range(3000)] + [b"hp/hq", b"hp/hq/#", b"hp/hq/+"]
+    adds += [b"+/+/w%d/%d/#" % (i % 7, i) for i in range(1500)] + [b"other%d/x" % i for i in range(500)]
+    for e in (A, B):
+        e.insert_many(allf)
+        e.insert_many(gen.Strings.from_list(adds))
+    a, b = A.stats(), B.stats()
+    assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+    B.debug_check()
+    for f in adds[::5] + [b"hp/hq", b"hp/hq/7", b"+/+/w3"]:
+        assert A.lookup(f) == B.lookup(f), f
+    for e in (A, B):
+        e.delete_many(gen.Strings.from_list(adds[::2]))
+    a, b = A.stats(), B.stats()
+    assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+    B.debug_check()
