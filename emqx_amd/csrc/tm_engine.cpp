@@ -2488,6 +2488,17 @@ struct tm_engine {
         return TM_OK;
     }
 
+    // f(i0, i1) over [0, k): in contiguous chunks on the churn workers when k
+    // is large (a churn batch's delta gather: random reads of lines the
+    // workers just wrote), else inline.  Only under mu, like every pool use.
+    template <class F>
+    void par_chunks(size_t k, const F& f) {
+        if (k < 8192 || threads < 2) { f(0, k); return; }
+        ensure_pool();
+        const size_t W = pool.n;
+        pool.run([&](unsigned t) { f(k * t / W, k * (t + 1) / W); });
+    }
+
     // Brings every replica up to the host trie: the dirty slots, filter
     // metadata and dictionary slots are gathered ONCE into pinned staging and
     // each replica gets the same copies + scatter kernels on its own stream
@@ -2516,20 +2527,25 @@ struct tm_engine {
             const size_t k = dirty.size();
             if ((rc = host_reserve(h_didx, ch_didx, k))) return rc;
             if ((rc = host_reserve(h_dval, ch_dval, k))) return rc;
-            for (size_t i = 0; i < k; ++i) {
-                h_didx[i] = dirty[i];
-                h_dval[i] = slots[dirty[i]];
-            }
+            par_chunks(k, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) {
+                    if (i + 16 < i1) __builtin_prefetch(&slots[dirty[i + 16]]);
+                    h_didx[i] = dirty[i];
+                    h_dval[i] = slots[dirty[i]];
+                }
+            });
         }
         if (!full_f_dirty && !dirty_f.empty()) {
             const size_t k = dirty_f.size();
             if ((rc = host_reserve(h_fidx, ch_fidx, k))) return rc;
             if ((rc = host_reserve(h_foffv, ch_foffv, k))) return rc;
             if ((rc = host_reserve(h_flenv, ch_flenv, k))) return rc;
-            for (size_t i = 0; i < k; ++i) {
-                const uint32_t c = dirty_f[i];
-                h_fidx[i] = c; h_foffv[i] = n_foff[c]; h_flenv[i] = n_flen[c];
-            }
+            par_chunks(k, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) {
+                    const uint32_t c = dirty_f[i];
+                    h_fidx[i] = c; h_foffv[i] = n_foff[c]; h_flenv[i] = n_flen[c];
+                }
+            });
         }
         std::vector<uint32_t>& dx = dict.dirty();
         const bool keys_full = dx.size() > dict.keys().size() / 8;
