@@ -674,9 +674,64 @@ def run_group(args):
                      "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes},
         "matches_per_step": st["matches"],
     }
+    # self-check: >= 3,000 sampled rows of every device's slice against one
+    # replica on device 0 (a separate engine over the same filters)
+    from emqx_amd import selfcheck as SC
+    from emqx_amd.engine import Engine
+    offs, ids = b.result()
+    rep = grp.engine()
+    lo = [n * k // ng for k in range(ng + 1)]
+    ref = Engine(device=0)
+    ref.insert_many(filters)
+    sc = group_selfcheck(lambda idx: SC.rows_from_csr(offs, ids, idx, SC.engine_names(rep)), topics, lo,
+                         [f"slice {k} (device {d})" for k, d in enumerate(devs)], ref)
+    ref.close()
+    out["selfcheck"] = sc
+    out["parity_sample_ok"] = sc["parity_sample_ok"]
+    out["devices"] = devs
     b.free()
     grp.close()
     print(json.dumps(out), flush=True)
+
+
+def replica_selfcheck(eng, b, topics, sync, rank, label) -> dict:
+    """After the timed region: this rank's waited batch b gives an evenly
+    spaced sample of >= 3,000 rows (as filter bytes, digested); rank 0's engine
+    -- one replica on device 0 -- matches every rank's sampled publishes and
+    compares bit-exactly.  Rank 0 returns the verdict, every rank the same."""
+    from emqx_amd import selfcheck as SC
+    offs, ids = b.result()
+    idx = SC.sample_index(len(topics))
+    sample = [topics[int(i)] for i in idx]
+    rows = SC.rows_from_csr(offs, ids, idx, SC.engine_names(eng))
+    del offs, ids
+    payloads = sync.allgather(SC.payload(sample, rows, label))
+    verdict = "{}"
+    if rank == 0:
+        names = SC.engine_names(eng)
+
+        def match_rows(ts):
+            o, i = eng.match_batch(ts)
+            return SC.rows_from_csr(o, i, np.arange(len(ts)), names)
+        verdict = json.dumps(SC.check(payloads, match_rows))
+    return json.loads(sync.allgather(verdict)[0])
+
+
+def group_selfcheck(grp_rows, topics, lo, labels, ref_engine) -> dict:
+    """In-process groups: slice k = publishes [lo[k], lo[k+1]) of the batch;
+    grp_rows(idx) -> rows (filter bytes) of those publishes from the group's
+    result; ref_engine = one replica on device 0 over the same filters."""
+    from emqx_amd import selfcheck as SC
+    payloads = []
+    for k in range(len(lo) - 1):
+        idx = lo[k] + SC.sample_index(lo[k + 1] - lo[k])
+        payloads.append(SC.payload([topics[int(i)] for i in idx], grp_rows(idx), labels[k]))
+    names = SC.engine_names(ref_engine)
+
+    def match_rows(ts):
+        o, i = ref_engine.match_batch(ts)
+        return SC.rows_from_csr(o, i, np.arange(len(ts)), names)
+    return SC.check(payloads, match_rows)
 
 
 def e2e_rate(eng, sub, reps: int = 3) -> dict:
@@ -918,6 +973,16 @@ def main():
         out["two_in_flight"] = {"publishes_per_s": ws * n * args.steps / e2, "ms_per_step": 1e3 * e2 / args.steps}
         for x in b2:
             x.free()
+
+    if ws > 1:
+        # self-check of the multi-GPU run: every rank's sampled rows (as filter
+        # bytes) must equal what rank 0's replica on device 0 returns for the
+        # same publishes (emqx_amd/selfcheck.py)
+        out["devices"] = [int(x) for x in sync.allgather(str(local))]
+        out["selfcheck"] = replica_selfcheck(eng, b, topics, sync, rank, f"rank {rank} (device {local})")
+        out["parity_sample_ok"] = out["selfcheck"]["parity_sample_ok"]
+        if rank == 0 and not out["parity_sample_ok"]:
+            log(f"[rank 0] PARITY SAMPLE FAILED: {out['selfcheck']}")
 
     if args.profile:
         args.no_cpu = True

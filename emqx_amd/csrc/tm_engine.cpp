@@ -1921,6 +1921,9 @@ struct tm_engine {
         for (uint32_t q = 0; q < NP; ++q) porder[q] = q;
         std::sort(porder.begin(), porder.end(), [&](uint32_t a, uint32_t b) { return parts[a].size() > parts[b].size(); });
         std::atomic<uint32_t> next_part{0};
+        // the first error stops every worker (not just the one that hit it):
+        // the filters applied are then those finished before it, see the header
+        std::atomic<bool> failed{false};
         // node ids: at most the levels the batch's filters lack, the free ids first
         std::vector<uint32_t> ids;
         std::atomic<size_t> next_id{0};
@@ -1958,12 +1961,13 @@ struct tm_engine {
             tl_mut = &m;
             const auto tw0 = std::chrono::steady_clock::now();
             try {
-                for (uint32_t pi; !m.rc && (pi = next_part.fetch_add(1)) < NP;) {
+                for (uint32_t pi; !m.rc && !failed.load(std::memory_order_relaxed) && (pi = next_part.fetch_add(1)) < NP;) {
                     const std::vector<uint32_t>& items = parts[porder[pi]];
                     const uint32_t sd = porder[pi] >= split_from ? 3 : 2;
                     const size_t ni = items.size();
                     m.n_items += ni;
                     for (size_t q = 0; q < ni; ++q) {
+                        if ((q & 63) == 63 && failed.load(std::memory_order_relaxed)) break;
                         const uint32_t i = items[q];
                         if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
                             const uint32_t f = plan[items[q + 8]].node;
@@ -1977,12 +1981,13 @@ struct tm_engine {
                             rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
                                                  plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth, sd);
                         }
-                        if (rc) { m.rc = rc; break; }
+                        if (rc) { m.rc = rc; failed.store(true, std::memory_order_relaxed); break; }
                         ++m.done;
                     }
                 }
             } catch (...) {
                 m.rc = TM_ENOMEM;
+                failed.store(true, std::memory_order_relaxed);
             }
             m.t_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
             tl_mut = nullptr;
@@ -3363,13 +3368,13 @@ struct tm_engine {
     // built only for a consumer that asks for offsets (ensure_dense).
     // TM_EAGER_CSR=1 builds it in every launch (round-2 behaviour, for A/B).
     bool eager_csr = getenv("TM_EAGER_CSR") && atoi(getenv("TM_EAGER_CSR")) != 0;
-    hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S) {
+    hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S, unsigned ev_flags = 0) {
         hipError_t e;
         if (eager_csr) {
             if ((e = launch_scan(s, S, b->d_total)) != hipSuccess) return e;
             if ((e = launch_finalize(s, S, false)) != hipSuccess) return e;
         }
-        if ((e = hipEventRecord(b->ev2, S)) != hipSuccess) return e;
+        if ((e = hipEventRecordWithFlags(b->ev2, S, ev_flags)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S)) != hipSuccess)
             return e;   // ctrl + stats
         if (eager_csr) return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
@@ -3434,8 +3439,9 @@ struct tm_engine {
                 return 1;
             }
             hipError_t e = hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S);
-            if (e == hipSuccess) e = launch_match(a, S, b->ev0, b->ev1, false);
-            if (e == hipSuccess) e = enqueue_csr(b, s, S);
+            // timing events as external nodes: every replay re-records them
+            if (e == hipSuccess) e = launch_match(a, S, b->ev0, b->ev1, false, hipEventRecordExternal);
+            if (e == hipSuccess) e = enqueue_csr(b, s, S, hipEventRecordExternal);
             const hipError_t e2 = hipStreamEndCapture(S, &g);
             if (e != hipSuccess || e2 != hipSuccess || !g ||
                 hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0) != hipSuccess) {
@@ -4588,12 +4594,15 @@ int tm_batch_launch(tm_engine* e, tm_batch* b) {
 int tm_batch_wait(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
     if (!b->rep) return TM_ENODEV;   // host-only engine
-    // the device wait itself runs without the engine lock, so other replicas'
-    // launches (async pipelines, other callers' batches) proceed meanwhile;
-    // the caller owns b, and wait() below finds its stream drained
-    if (b->launched && !b->done) {
+    // A batch on a stream of its own is waited for without the engine lock,
+    // so other replicas' launches (async pipelines, other callers' batches)
+    // proceed meanwhile; the caller owns b, and wait() below finds its stream
+    // drained.  A batch on the replica's shared stream is waited for under the
+    // lock (in wait()): another thread may be capturing a graph on that stream,
+    // and a synchronize on a capturing stream is refused (and breaks the capture).
+    if (b->launched && !b->done && b->own) {
         HIP_OK(hipSetDevice(b->rep->device));
-        HIP_OK(hipStreamSynchronize(b->own ? b->own : b->rep->stream));
+        HIP_OK(hipStreamSynchronize(b->own));
     }
     std::lock_guard<std::recursive_mutex> g(e->mu);
     int rc = e->use(b->rep);

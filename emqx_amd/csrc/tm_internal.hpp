@@ -270,7 +270,8 @@ hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s);
 hipError_t launch_fan_globalize(const FanArgs& a, hipStream_t s);   // block-relative moff -> global
 uint32_t fan_scan_tile();   // match entries per scan block
 uint32_t fan_fill_tile();   // deliveries per fill block
-hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked);
+hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked,
+                        unsigned ev_flags = 0);
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, uint32_t* d_total);
 hipError_t launch_finalize(const ScanArgs& a, hipStream_t s, bool checked);
 hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* vals, uint32_t n,

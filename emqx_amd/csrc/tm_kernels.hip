@@ -2303,23 +2303,35 @@ uint32_t match_waves(uint32_t n, int device, uint32_t qcap) {
 }
 
 template <bool CK, bool BIG>
-static void launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
+static hipError_t launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b,
+                                 unsigned ev_flags) {
     const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
-    if (ev_a) (void)hipEventRecord(ev_a, s);
+    hipError_t e;
+    if (ev_a && (e = hipEventRecordWithFlags(ev_a, s, ev_flags)) != hipSuccess) return e;
     if (ntiles) {
         const uint32_t grid = a.grid;
         if (a.qcap <= 384) hipLaunchKernelGGL((tm_match_tiles<CK, BIG, 384>), dim3(grid), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((tm_match_tiles<CK, BIG, 512>), dim3(grid), dim3(64), 0, s, a);
     }
-    if (ev_b) (void)hipEventRecord(ev_b, s);
+    if (ev_b && (e = hipEventRecordWithFlags(ev_b, s, ev_flags)) != hipSuccess) return e;
     hipLaunchKernelGGL((tm_match_slow<CK, BIG>), dim3(a.s_waves), dim3(64), 0, s, a);
+    return hipSuccess;
 }
 
-hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked) {
+// ev_flags: hipEventRecordExternal while the stream is being captured into a
+// graph, so that every replay re-records the timing events (a plain record in
+// a capture only adds a dependency, and the events would keep the times of the
+// last direct launch)
+hipError_t launch_match(const MatchArgs& a, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b, bool checked,
+                        unsigned ev_flags) {
     // the edge hash is read with 32-bit-offset buffer loads unless it exceeds 4 GiB
     const bool big = (uint64_t)a.nslots * sizeof(Slot) > 0xFFFFFFFFull;
-    if (checked) { if (big) launch_match_t<true, true>(a, s, ev_a, ev_b); else launch_match_t<true, false>(a, s, ev_a, ev_b); }
-    else { if (big) launch_match_t<false, true>(a, s, ev_a, ev_b); else launch_match_t<false, false>(a, s, ev_a, ev_b); }
+    hipError_t e;
+    if (checked) e = big ? launch_match_t<true, true>(a, s, ev_a, ev_b, ev_flags)
+                         : launch_match_t<true, false>(a, s, ev_a, ev_b, ev_flags);
+    else e = big ? launch_match_t<false, true>(a, s, ev_a, ev_b, ev_flags)
+                 : launch_match_t<false, false>(a, s, ev_a, ev_b, ev_flags);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

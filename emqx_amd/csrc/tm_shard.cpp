@@ -501,12 +501,33 @@ int tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t
                            uint64_t* n_deleted) {
     if (n_deleted) *n_deleted = 0;
     if (!s || !offsets || (!filters && n)) return TM_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i]) return TM_EINVAL;
     std::lock_guard<std::mutex> lk(s->mu);
-    std::vector<int> rcs(s->G, TM_OK);
-    s->each([&](uint32_t g) { rcs[g] = tm_trie_delete_many(s->sh[g], filters, offsets, n, nullptr); });
-    for (int rc : rcs)
-        if (rc) return rc;
-    if (n_deleted) *n_deleted = n;
+    // counted like tm_sharded_insert_many: one deletion per shard a present
+    // filter lives on (its owner, or every shard for a replicated one)
+    uint64_t tot = 0;
+    try {
+        std::unordered_set<std::string> seen;   // a filter listed twice is deleted once
+        for (uint32_t i = 0; i < n; ++i) {
+            if (!seen.insert(std::string((const char*)filters + offsets[i], offsets[i + 1] - offsets[i])).second) continue;
+            const int o = tm_filter_shard(s->sh[0], filters + offsets[i], offsets[i + 1] - offsets[i], s->G);
+            if (o == TM_ENOENT) continue;   // a word no shard knows: the filter is nowhere
+            if (o < 0) return o;
+            const bool repl = (uint32_t)o >= s->G;
+            uint32_t id;   // absent filters are no-ops, not deletions
+            if (tm_filter_id(s->sh[repl ? 0 : o], filters + offsets[i], offsets[i + 1] - offsets[i], &id) != TM_OK)
+                continue;
+            tot += repl ? s->G : 1;
+        }
+        std::vector<int> rcs(s->G, TM_OK);
+        s->each([&](uint32_t g) { rcs[g] = tm_trie_delete_many(s->sh[g], filters, offsets, n, nullptr); });
+        for (int rc : rcs)
+            if (rc) return rc;
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+    if (n_deleted) *n_deleted = tot;
     return TM_OK;
 }
 

@@ -11,6 +11,7 @@ replica on each of its MI355X devices).
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -209,6 +210,12 @@ def _routes_arrays(r: N.Routes):
     return offs, fids, dests
 
 
+def _invalidate(owner):
+    """Borrowed Engine views of an owner that is being closed lose their handle."""
+    for e in list(getattr(owner, "_borrowed", ())):
+        e._h = None
+
+
 class GroupBatch:
     """A publish batch split over a Group's replicas (tm_group_prepare ...)."""
 
@@ -276,9 +283,11 @@ class Group:
         N.check(self.L.tm_group_create(devs, len(devices), C.byref(cfg), C.byref(h)), "tm_group_create")
         self.h = h
         self.devices = list(devices)
+        self._borrowed = weakref.WeakSet()
 
     def close(self):
         if getattr(self, "h", None):
+            _invalidate(self)
             self.L.tm_group_destroy(self.h)
             self.h = None
 
@@ -326,7 +335,7 @@ class Group:
     def engine(self) -> "Engine":
         """The group's engine (every tm_* call on it spans the replicas); the
         Group keeps ownership."""
-        return Engine._borrow(self.L.tm_group_engine(self.h, 0), self.devices)
+        return Engine._borrow(self.L.tm_group_engine(self.h, 0), self.devices, owner=self)
 
     def match_batch(self, topics):
         s = _pack(topics)
@@ -361,15 +370,30 @@ class Engine:
             devs = (C.c_int32 * max(len(devices), 1))(*devices)
             N.check(self.L.tm_create_replicated(C.byref(cfg), devs, len(devices), C.byref(h)), "tm_create_replicated")
             self.devices = list(devices)
-        self.h = h
+        self._h = h
         self.device = self.devices[0] if self.devices else -1
 
     @classmethod
-    def _borrow(cls, handle, devices) -> "Engine":
+    def _borrow(cls, handle, devices, owner=None) -> "Engine":
+        """A view of an engine another object owns: it keeps the owner alive,
+        and the owner's close() invalidates it (calls then raise instead of
+        reaching freed native memory)."""
+        if not handle:
+            raise ValueError("no such engine")
         e = cls.__new__(cls)
-        e.L, e.h, e._owned = N.lib(), C.c_void_p(handle), False
+        e.L, e._h, e._owned = N.lib(), C.c_void_p(handle), False
         e.devices, e.device = list(devices), devices[0]
+        e._owner = owner
+        if owner is not None:
+            owner._borrowed.add(e)
         return e
+
+    @property
+    def h(self):
+        h = getattr(self, "_h", None)
+        if h is None:
+            raise RuntimeError("engine is closed (or its owner was)")
+        return h
 
     @property
     def replicas(self) -> int:
@@ -379,10 +403,10 @@ class Engine:
         N.check(self.L.tm_async_start(self.h), "tm_async_start")
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "_h", None):
             if getattr(self, "_owned", True):
-                self.L.tm_destroy(self.h)
-            self.h = None
+                self.L.tm_destroy(self._h)
+            self._h = None
 
     def __del__(self):
         try:
@@ -770,9 +794,11 @@ class ShardedGroup:
         N.check(self.L.tm_sharded_create(devs, len(devices), C.byref(cfg), C.byref(h)), "tm_sharded_create")
         self.h = h
         self.devices = list(devices)
+        self._borrowed = weakref.WeakSet()
 
     def close(self):
         if getattr(self, "h", None):
+            _invalidate(self)
             self.L.tm_sharded_destroy(self.h)
             self.h = None
 
@@ -829,4 +855,4 @@ class ShardedGroup:
         return buf.raw[:n.value]
 
     def engine(self, shard: int) -> "Engine":
-        return Engine._borrow(self.L.tm_sharded_engine(self.h, shard), [self.devices[shard]])
+        return Engine._borrow(self.L.tm_sharded_engine(self.h, shard), [self.devices[shard]], owner=self)

@@ -56,6 +56,13 @@ class FileGroup:
         self._post(tag, repr(float(value)))
         return max(float(v) for v in self._collect(tag, timeout))
 
+    def allgather(self, payload: str, timeout: float = 600.0) -> list:
+        """Every rank's payload (a string), in rank order."""
+        self._n += 1
+        tag = f"g{self._n}"
+        self._post(tag, payload)
+        return self._collect(tag, timeout)
+
     def close(self):
         """Every rank reports it is done reading; then rank 0 removes the directory."""
         self._post("done", "")

@@ -374,11 +374,17 @@ TM_API int  tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deli
 /* emqx_trie:insert/1 over n filters (filters = concatenated bytes, offsets[n+1]).
  * nshards <= 1: every filter.  Otherwise only the filters whose
  * tm_filter_shard() is `shard` or nshards (replicated); *n_inserted (may be
- * NULL) counts them.  Stops at the first error. */
+ * NULL) counts them.  Stops at the first error.  A batch of >= 2,048
+ * filters on a big trie is applied by parallel workers: after an error the
+ * filters applied are each worker's finished ones (every filter is applied
+ * whole or not at all, the trie stays consistent), so a subset of the batch
+ * that need not be a prefix; *n_inserted counts them and re-applying the
+ * batch is idempotent (emqx_trie:insert/1 is). */
 TM_API int  tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets,
                                 uint32_t n, uint32_t shard, uint32_t nshards, uint64_t* n_inserted);
 /* emqx_trie:delete/1 over n filters; *n_deleted (may be NULL) counts the calls
- * made.  Stops at the first error. */
+ * made.  Stops at the first error (subset semantics of a parallel batch as
+ * for tm_trie_insert_many). */
 TM_API int  tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                 uint64_t* n_deleted);
 /* Interns n words in order (the shared dictionary of the sharded mode).  Words
@@ -566,7 +572,9 @@ TM_API int  tm_sharded_dict_load(tm_sharded* s, const uint8_t* words, const uint
  * *n_inserted = insertions summed over the shards. */
 TM_API int  tm_sharded_insert_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                    uint64_t* n_inserted);
-/* emqx_trie:delete/1 of an unsubscribe batch on every shard (absent: no-op). */
+/* emqx_trie:delete/1 of an unsubscribe batch on every shard (absent: no-op).
+ * *n_deleted = deletions summed over the shards each filter lives on (its
+ * owner, or all G for a replicated filter), as tm_sharded_insert_many counts. */
 TM_API int  tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                    uint64_t* n_deleted);
 /* A publish batch: bytes copied and tokenised on the home device.  A non-NULL

@@ -37,6 +37,26 @@ def native_built():
     yield
 
 
+def gpu_count() -> int:
+    """HIP devices visible to this process (0 without a GPU)."""
+    try:
+        from emqx_amd import _native as N
+        return int(N.lib().tm_device_count())
+    except Exception:   # noqa: BLE001
+        return 0
+
+
+@pytest.fixture(params=["dev00", "dev01"])
+def device_pair(request):
+    """Two devices for the multi-device paths: [0, 0] (two replicas / shards on
+    one GPU: always) and [0, 1] (two physical GPUs: skipped on a 1-GPU box)."""
+    if request.param == "dev01":
+        if gpu_count() < 2:
+            pytest.skip("needs two HIP devices")
+        return [0, 1]
+    return [0, 0]
+
+
 def load_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

@@ -43,8 +43,8 @@ def _recv_all(nif, pid, refs, timeout_s=60):
     return got
 
 
-def test_nif_engine_over_two_replicas_async_under_concurrent_subscribes(nif):
-    """new([0, 0]): match_async calls from 16 processes are dealt over both
+def test_nif_engine_over_two_replicas_async_under_concurrent_subscribes(nif, device_pair):
+    """new([0, 0]) (and new([0, 1]) on a box with two GPUs): match_async calls from 16 processes are dealt over both
     replicas while a writer keeps subscribing; every reply equals the oracle's
     set, and a match issued after an insert returned sees the filter whichever
     replica serves it (read-your-writes through the shared host trie)."""
@@ -55,7 +55,7 @@ def test_nif_engine_over_two_replicas_async_under_concurrent_subscribes(nif):
         ws = [rng.choice(words) for _ in range(rng.randint(1, 5))]
         if b"#" not in ws[:-1]:
             filters.add(b"/".join(ws))
-    e, t = nif.new([0, 0]), O.Trie()
+    e, t = nif.new(device_pair), O.Trie()
     for f in sorted(filters):
         assert nif.call("insert", e, f) == "ok"
         t.insert(f)
@@ -121,11 +121,11 @@ def _c2_small(n_filters=100_000, n_topics=100_000, seed=2201):
     return F, T
 
 
-def test_replicated_engine_splits_large_batches_like_one_engine():
+def test_replicated_engine_splits_large_batches_like_one_engine(device_pair):
     F, T = _c2_small()
     one = Engine(device=0)
     one.insert_many(F)
-    rep = Engine(devices=[0, 0])
+    rep = Engine(devices=device_pair)
     assert rep.replicas == 2
     assert rep.insert_many(F) == len(F)
     o1, i1 = one.match_batch(T)

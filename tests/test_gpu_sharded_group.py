@@ -82,12 +82,12 @@ def test_shards_on_one_device_with_online_dictionary_deltas(G):
     grp.close()
 
 
-def test_sharded_rows_equal_one_engine():
+def test_sharded_rows_equal_one_engine(device_pair):
     F, T, vocab = workload(42)
     one = Engine(device=0, frozen_dict=True)
     one.dict_load(vocab)
     one.insert_many(F)
-    grp = ShardedGroup([0, 0])
+    grp = ShardedGroup(device_pair)
     grp.dict_load(vocab)
     grp.insert_many(F)
     o1, i1 = one.match_batch(T)
