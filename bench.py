@@ -296,47 +296,87 @@ def run_c4(args, ws, rank, local, pg):
 def run_c4_group(args):
     """Config C4 in ONE process (tm_sharded_*, no torch, no collective): the IoT
     filters partitioned over shard engines on the listed devices (default
-    0..N-1; 0,0 rehearses two shards on one GPU), one batch of --topics
-    publishes per shard.  One step = owner per publish + device partition by
-    owner + every shard matching its part + rows restored to publish order, all
-    in HBM (tm_sharded_run)."""
+    0..N-1; 0,0 rehearses two shards on one GPU), one slice of --topics
+    publishes per shard, tokenised on its shard's device at prepare.  One step
+    = every slice partitioned by owner on its own device + every shard
+    receiving its parts and walking them, one host wait (tm_sharded_run); the
+    rows stay in each shard's HBM.  The publish-order CSR (global ids) is built
+    on request and timed beside it; a fresh batch (tokenise + plan + step) too.
+    Self-check: >= 3,000 sampled rows of every slice against one engine on
+    device 0 over the filters that can match them (a topic
+    device/d<X>/sensor/... can only match filters whose second level is d<X>)."""
     from emqx_amd import gen
-    from emqx_amd.engine import ShardedGroup
+    from emqx_amd import selfcheck as SC
+    from emqx_amd.engine import Engine, ShardedGroup
 
     devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
     G = len(devs)
     p = gen.IotParams(n_filters=args.c4_filters) if args.c4_filters else gen.C4
     t0 = time.time()
-    grp = ShardedGroup(devs)
-    grp.dict_load(gen.gen_iot_vocab(p))
-    inserted = 0
-    chunk = 5_000_000
-    for lo in range(0, p.n_filters, chunk):
-        inserted += grp.insert_many(gen.gen_iot_filters(p, lo, min(p.n_filters, lo + chunk)))
-        log(f"[c4 group] filters {min(p.n_filters, lo + chunk)}/{p.n_filters} over {G} shard(s), "
-            f"{time.time() - t0:.0f}s")
     n = args.topics * G
     parts = [gen.gen_iot_topics(p, 4000 + k, args.topics) for k in range(G)]
     topics = gen.Strings.concat(parts) if G > 1 else parts[0]
     del parts
+    lo = [n * k // G for k in range(G + 1)]                         # the group's slices
+    sample = np.concatenate([lo[k] + SC.sample_index(lo[k + 1] - lo[k]) for k in range(G)])
+    want = np.unique(gen.iot_device_ids(gen.Strings.from_list([topics[int(i)] for i in sample])))
+    grp = ShardedGroup(devs)
+    vocab = gen.gen_iot_vocab(p)
+    grp.dict_load(vocab)
+    inserted, cand = 0, []
+    chunk = 5_000_000
+    for c0 in range(0, p.n_filters, chunk):
+        fl = gen.gen_iot_filters(p, c0, min(p.n_filters, c0 + chunk))
+        inserted += grp.insert_many(fl)
+        keep = np.flatnonzero(np.isin(gen.iot_device_ids(fl), want))
+        cand.extend(fl[int(i)] for i in keep)
+        log(f"[c4 group] filters {min(p.n_filters, c0 + chunk)}/{p.n_filters} over {G} shard(s), "
+            f"{time.time() - t0:.0f}s")
     b = grp.prepare(topics)
-    del topics
     for _ in range(max(args.warmup, 1)):
         b.run()
-    ms_match, phases = [], []
+    ms_match, phases, waits = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         b.run()
         st = b.stats()
         ms_match.append(st["ms_match"])
-        phases.append((st["ms_partition"], st["ms_parts"], st["ms_unpartition"]))
+        phases.append((st["ms_partition"], st["ms_exchange"], st["ms_step"]))
+        waits.append(st["host_waits"])
     elapsed = time.perf_counter() - t0
     st = b.stats()
+    # the publish-order CSR with global ids, built on request from the step's rows
+    tr = time.perf_counter()
+    offs, ids = b.result()
+    csr_ms = b.stats()["ms_unpartition"]
+    result_ms = 1e3 * (time.perf_counter() - tr)
+    # a fresh batch: slices tokenised on their devices + the plan + one step
+    fresh = []
+    for _ in range(3):
+        tf = time.perf_counter()
+        b.reprepare(topics).run()
+        fresh.append(1e3 * (time.perf_counter() - tf))
     alg_bytes = (ALG_BYTES_PER_VISIT * (st["visits"] + st["hash_hits"]) + 4 * st["words"]
                  + 4 * st["matches"] + 4 * st["topics"]) / G      # per shard (device)
     k_ms = float(np.mean(ms_match))                                 # slowest part per step
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     ph = np.mean(np.array(phases), 0).tolist()
+    # self-check against one engine on device 0 (fresh batch's rows = the timed batch's: same publishes)
+    ref = Engine(device=0, frozen_dict=True)
+    ref.dict_load(vocab)
+    ref.insert_many(cand)
+    cache = {}
+
+    def gname(g):
+        g = int(g)
+        if g not in cache:
+            cache[g] = grp.filter_bytes(g)
+        return cache[g]
+
+    def grp_rows(idx):
+        return [[gname(x) for x in ids[int(offs[i]):int(offs[i + 1])]] for i in idx]
+    sc = group_selfcheck(grp_rows, topics, lo, [f"slice {k} (device {d})" for k, d in enumerate(devs)], ref)
+    ref.close()
     out = {
         "metric": "publishes matched/sec (node) at 100M IoT filters, filter-sharded",
         "value": n * args.steps / elapsed,
@@ -353,7 +393,7 @@ def run_c4_group(args):
         "config": {"workload": f"C4: {p.n_filters} IoT filters sharded over {G} shard(s) on devices {devs}, "
                                f"{args.topics} publishes per shard, one process (tm_sharded)", "filters": p.n_filters,
                    "filters_inserted_over_shards": inserted, "mode": "filter-sharded, in-process",
-                   "parallelism": f"filters sharded x{G}, device partition by owner (no collective)"},
+                   "parallelism": f"filters sharded x{G}, per-device partition + part exchange (no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("C4", args.topics, p.n_filters) if G == 1
                      else None, "kernel": "tm_match_tiles", "kernel_ms": k_ms, "alg_bytes_per_launch": alg_bytes,
@@ -361,35 +401,45 @@ def run_c4_group(args):
                                      (("V", "visits"), ("H", "hash_hits"), ("d", "words"), ("M", "matches"))}},
         "matches_per_step": st["matches"],
         "device_match_ms": k_ms,
-        "phase_ms": {"partition": ph[0], "parts": ph[1], "unpartition": ph[2]},
+        "phase_ms": {"partition_device": ph[0], "exchange_device": ph[1], "step_host": ph[2]},
+        "host_waits_per_step": float(np.mean(waits)),
+        "publish_order_csr": {"ms": csr_ms, "with_d2h_ms": result_ms,
+                              "publishes_per_s_with_csr": n / (1e-3 * (1e3 * elapsed / args.steps + csr_ms))},
+        "fresh_publishes_per_s": n / (1e-3 * float(np.median(fresh))),
+        "fresh_ms": float(np.median(fresh)),
         "part_topics": st["part_topics"],
+        "links": [[grp.link(i, j) for j in range(G)] for i in range(G)],
+        "devices": devs,
+        "selfcheck": sc,
+        "parity_sample_ok": sc["parity_sample_ok"],
     }
     b.free()
     grp.close()
     print(json.dumps(out), flush=True)
 
 
-def run_c5(args, ws, rank, local, sync):
-    """Config C5: 10k hot topics take 90% of the publishes, each matched by ~K
+def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
+    """Config C5: 10k hot topics take 90% of the publishes, each matched by ~k
     filters derived from it (+ 100k background C2-style filters); one step =
-    10,000 subscribe/unsubscribe deltas applied to the trie and uploaded to the
-    device, then the deduplicated batch is matched (every distinct topic once;
-    rows longer than the fast path's K go to the generic kernel)."""
+    n_deltas subscribe/unsubscribe deltas applied to the trie and uploaded to
+    the device, then the deduplicated batch is matched (every distinct topic
+    once; rows longer than the fast path's K go to the generic kernel).
+    Returns the leg's measurements (publishes/s, churn and device ms)."""
     from emqx_amd import gen
     from emqx_amd.engine import Engine
     from emqx_amd.skew import Churn, workload
 
-    p = gen.SkewParams(k_per_hot=args.c5_k)
+    p = gen.SkewParams(k_per_hot=k)
     t0 = time.time()
-    allf, derived, hot, pubs = workload(p, 100_000, args.topics, seed=5 + rank)
-    log(f"[rank {rank}] C5 workload: {len(allf)} filters, {len(pubs)} publishes in {time.time() - t0:.1f}s")
-    eng = Engine(device=local)
+    allf, derived, hot, pubs = workload(p, 100_000, n_topics, seed=seed)
+    log(f"[c5 k={k}] workload: {len(allf)} filters, {len(pubs)} publishes in {time.time() - t0:.1f}s")
+    eng = Engine(device=device)
     eng.insert_many(allf)
     eng.sync()
-    churn = Churn(hot, derived.tolist(), seed=11 + rank)
+    churn = Churn(hot, derived.tolist(), seed=seed + 6)
     b = eng.prepare(pubs, dedup=True)
     row_of, n_rows = b.row_map()
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         b.launch().wait()
     if sync is not None:
         sync.barrier()
@@ -402,8 +452,8 @@ def run_c5(args, ws, rank, local, sync):
     # launch i + 1 (read-your-writes) -- so the step costs max(apply, device)
     # rather than their sum.
     deltas = []
-    for _ in range(args.steps):
-        dels, adds = churn.step(args.c5_deltas)
+    for _ in range(steps):
+        dels, adds = churn.step(n_deltas)
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
     ms_match, ms_churn, ms_walk, ms_tok = [], [], [], []
     t0 = time.perf_counter()
@@ -411,8 +461,8 @@ def run_c5(args, ws, rank, local, sync):
     Churn.apply(eng, *deltas[0])
     ms_churn.append(1e3 * (time.perf_counter() - tc))
     b.launch()
-    for i in range(args.steps):
-        if i + 1 < args.steps:
+    for i in range(steps):
+        if i + 1 < steps:
             tc = time.perf_counter()
             Churn.apply(eng, *deltas[i + 1])
             ms_churn.append(1e3 * (time.perf_counter() - tc))
@@ -425,7 +475,7 @@ def run_c5(args, ws, rank, local, sync):
         ms_match.append(st["ms_total"])
         ms_walk.append(st["ms_match"])
         ms_tok.append(st["ms_tokenize"])
-        if i + 1 < args.steps:
+        if i + 1 < steps:
             b.launch()
     elapsed = time.perf_counter() - t0
     if sync is not None:
@@ -437,29 +487,49 @@ def run_c5(args, ws, rank, local, sync):
     delivered = int(rowlen[row_of].sum())
     n = len(pubs)
     out = {
+        "k": k, "publishes_per_s": n * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "steps": steps,
+        "deltas_per_step": n_deltas, "filters": len(allf), "publishes": n, "distinct_topics": int(n_rows),
+        "device_ms": float(np.mean(ms_match)), "device_walk_ms": float(np.mean(ms_walk)),
+        "device_tokenize_ms": float(np.mean(ms_tok)),
+        "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
+        "churn_overlapped_with_device": True,
+        "matches_delivered_per_step": delivered, "generic_path_topics": int(st["slow_topics"]),
+        "uploads_delta": eng.stats()["uploads_delta"],
+    }
+    b.free()
+    eng.close()
+    return out
+
+
+def run_c5(args, ws, rank, local, sync):
+    """--workload c5: the C5 leg alone as the bench line (K = --c5-k)."""
+    leg = c5_leg(args.c5_k, args.steps, args.c5_deltas, args.topics, device=local, seed=5 + rank, sync=sync,
+                 warmup=args.warmup)
+    out = {
         "metric": "publishes matched/sec (node), hot-topic skew + churn (C5)",
-        "value": ws * n * args.steps / elapsed,
+        "value": ws * leg["publishes_per_s"],
         "unit": "publishes/s",
         "n_gpus": ws,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step": leg["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded skew generator, SURVEY.md §8d C5)",
         "config": {"workload": f"C5: 10k hot topics x ~{args.c5_k} filters + 100k background, "
-                               f"{n} publishes per GPU (90% hot, Zipf 1.0), {args.c5_deltas} deltas per step",
-                   "filters": len(allf), "distinct_topics": int(n_rows), "mode": "replicated, dedup batches"},
-        "device_pipeline_ms": float(np.mean(ms_match)),
-        "device_walk_ms": float(np.mean(ms_walk)),
-        "device_tokenize_ms": float(np.mean(ms_tok)),
-        "churn_apply_ms": float(np.mean(ms_churn)),
+                               f"{leg['publishes']} publishes per GPU (90% hot, Zipf 1.0), {args.c5_deltas} deltas per step",
+                   "filters": leg["filters"], "distinct_topics": leg["distinct_topics"],
+                   "mode": "replicated, dedup batches"},
+        "device_pipeline_ms": leg["device_ms"],
+        "device_walk_ms": leg["device_walk_ms"],
+        "device_tokenize_ms": leg["device_tokenize_ms"],
+        "churn_apply_ms": leg["churn_ms"],
         "churn_overlapped_with_device": True,
-        "matches_delivered_per_step": delivered,
-        "generic_path_topics": int(st["slow_topics"]),
-        "uploads_delta": eng.stats()["uploads_delta"],
+        "matches_delivered_per_step": leg["matches_delivered_per_step"],
+        "generic_path_topics": leg["generic_path_topics"],
+        "uploads_delta": leg["uploads_delta"],
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -734,6 +804,40 @@ def group_selfcheck(grp_rows, topics, lo, labels, ref_engine) -> dict:
     return SC.check(payloads, match_rows)
 
 
+def fresh_latency(eng, filters, topics, batches: int) -> dict:
+    """p50/p99 of tm_match_batch over `batches` never-repeated batches of B
+    publishes (B = 4,096 and 65,536): host bytes -> host CSR of sorted ids.
+    The batches are disjoint slices of the C2 publishes (more are generated
+    when the resident ones run out); slicing happens before timing."""
+    import ctypes as C
+
+    from emqx_amd import _native as N
+    from emqx_amd import gen
+    out = {}
+    pool = topics
+    for bsz in (4096, 65536):
+        need = bsz * (batches + 5)
+        if len(pool) < need:
+            extra = gen.gen_topics(gen.C2, filters, 7000 + len(pool), need - len(pool))
+            pool = gen.Strings.concat([pool, extra])
+        subs = []
+        for i in range(batches + 5):
+            sl = pool.slice(i * bsz, (i + 1) * bsz)
+            subs.append((np.ascontiguousarray(sl.buf), np.ascontiguousarray(sl.offs.astype(np.uint64))))
+        r = N.Result()
+        lat = []
+        for i, (buf, offs) in enumerate(subs):
+            t = time.perf_counter()
+            N.check(eng.L.tm_match_batch(eng.h, buf.ctypes.data, offs.ctypes.data, bsz, C.byref(r)), "tm_match_batch")
+            dt = 1e3 * (time.perf_counter() - t)
+            if i >= 5:                   # the first five size the pinned buffers
+                lat.append(dt)
+        out[str(bsz)] = {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+                         "batches": len(lat), "distinct_batches": True,
+                         "path": "host bytes -> tm_match_batch -> host CSR"}
+    return out
+
+
 def e2e_rate(eng, sub, reps: int = 3) -> dict:
     """tm_match_batch over `sub` from host bytes to the host CSR, best of `reps`
     after one warm-up call (pinned result buffers sized)."""
@@ -781,6 +885,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--topics", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="N = 1: skip the C5 legs of the default line")
     ap.add_argument("--inflight", type=int, default=1,
                     help="C2: batches in flight in the headline steps, each on its own stream (1 = one "
                          "batch on the engine stream: walk events and rocprof durations stay un-overlapped)")
@@ -1013,6 +1118,11 @@ def main():
         out["latency_sweep"] = sweep
         if "error" in main_lat:
             out["latency_error"] = main_lat["error"]
+        # fresh-batch latency (submit -> results ready): new
+        # topic bytes in host memory -> tm_match_batch (H2D, device tokeniser,
+        # walk, CSR, D2H) -> sorted ids in host memory, a different slice of
+        # publishes every batch
+        out["fresh_latency_sweep"] = fresh_latency(eng, filters, topics, args.latency_batches)
         # host-inclusive end to end, timed at the C ABI (tm_match_batch): topic
         # bytes in host RAM -> H2D -> device tokenise -> match -> sorted CSR in
         # the engine's pinned host buffers (what a NIF hands to the broker)
@@ -1027,6 +1137,10 @@ def main():
         out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), host)
         out["speedup_vs_cpu_allcore"] = value / out["cpu_baseline"]["value"]
         out["c1"] = c1_leg(host, device=local)
+    if rank == 0 and ws == 1 and not args.profile and not args.no_c5:
+        # config C5 in the driver's line: K = 100 and K = 10 filters per hot
+        # topic, 10k subscribe/unsubscribe deltas per step
+        out["c5"] = {f"k{k}": c5_leg(k, 5, 10_000, args.topics, device=local) for k in (100, 10)}
 
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -30,6 +30,9 @@ TM_BATCH_DEDUP = 1
 TM_BATCH_STREAM = 2
 TM_ROUTE_DELETE = 0
 TM_ROUTE_WRITE = 1
+TM_LINK_SAME = 0
+TM_LINK_PEER = 1
+TM_LINK_STAGED = 2
 
 _ERRNAMES = {TM_ENOENT: "ENOENT", TM_EIO: "EIO", TM_ENOMEM: "ENOMEM", TM_ENODEV: "ENODEV",
              TM_EINVAL: "EINVAL", TM_EOVERFLOW: "EOVERFLOW", TM_EABORT: "EABORT"}
@@ -100,8 +103,9 @@ class AsyncStats(C.Structure):
 
 
 class ShardedStats(C.Structure):
-    _fields_ = [("match", BatchStats), ("ms_partition", C.c_float), ("ms_parts", C.c_float),
-                ("ms_unpartition", C.c_float), ("part_topics", C.c_uint32 * 64)]
+    _fields_ = [("match", BatchStats), ("ms_partition", C.c_float), ("ms_exchange", C.c_float),
+                ("ms_step", C.c_float), ("ms_unpartition", C.c_float), ("host_waits", C.c_uint32),
+                ("part_topics", C.c_uint32 * 64)]
 
 
 # void (*tm_match_cb)(void* ctx, int rc, const uint32_t* ids, uint32_t n)
@@ -204,6 +208,7 @@ SIGNATURES = {
     "tm_sharded_result": (C.c_int, [P, P, C.POINTER(Result)]),
     "tm_sharded_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_sharded_batch_stats": (C.c_int, [P, P, C.POINTER(ShardedStats)]),
+    "tm_sharded_link": (C.c_int, [P, C.c_uint32, C.c_uint32]),
     "tm_sharded_batch_free": (None, [P, P]),
     "tm_sharded_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_sharded_filter_copy": (C.c_int, [P, C.c_uint32, P, SZ, C.POINTER(SZ)]),

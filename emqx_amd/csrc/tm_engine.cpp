@@ -474,6 +474,10 @@ struct tm_batch {
     // device-resident tokens the generic-path list is built on the device
     bool tokens_only = false;
     bool dev_slow = false;
+    // a part batch of the in-process sharded group: its token buffers are
+    // written by the group's copies, checked on the device by every launch
+    // (tm_token_check) and the verdict read back with the header
+    bool check_tokens = false;
     // device tokenisation: the topic bytes are uploaded by prepare and tokenised
     // on the engine stream by the first launch, after the dictionary deltas; a
     // later launch re-tokenises only if the dictionary grew meanwhile (ids of
@@ -2998,6 +3002,40 @@ struct tm_engine {
         return reserve_outputs(b);
     }
 
+    // A part batch of the in-process sharded group (tm_shard.cpp): token
+    // buffers for n topics / nwords words that the group's copies fill on the
+    // batch's stream; no staging copy and no host sync (the launch checks the
+    // tokens on the device).  The stream and buffers are returned.
+    int part_buffers(tm_batch* b, uint32_t n, uint64_t nwords, PartBuffers* out) {
+        if (nwords > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        int rc;
+        b->n = n;
+        b->nwords = nwords;
+        b->tokens_only = true;
+        b->dev_tok = false;
+        b->check_tokens = true;
+        b->gbad = true;   // launched directly: the token check belongs to every launch
+        b->launched = b->done = false;
+        b->bytes.clear(); b->offs.clear();
+        b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
+        if ((rc = dev_reserve(b->d_words, b->c_words, std::max<uint64_t>(nwords, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_toff, b->c_toff, (size_t)n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_tflags, b->c_tflags, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_slow, b->c_slow, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_nslow, b->c_nslow, 2))) return rc;
+        if ((rc = host_reserve(b->h_bad, b->ch_bad, 2))) return rc;
+        b->h_bad[0] = b->h_bad[1] = 0;
+        b->dev_slow = true;
+        if ((rc = reserve_outputs(b))) return rc;
+        out->words = b->d_words;
+        out->toff = b->d_toff;
+        out->tflags = b->d_tflags;
+        out->words_cap = b->c_words;
+        out->stream = st(b);
+        out->device = b->rep->device;
+        return TM_OK;
+    }
+
     // tm_batch_export
     int export_batch(tm_batch* b, uint32_t* d_counts, uint32_t* d_ids, uint32_t mul, uint32_t add) {
         if (!b->done) return TM_EINVAL;
@@ -3294,6 +3332,10 @@ struct tm_engine {
             ts.block_sums = b->d_bsums;
             HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
         }
+        if (b->check_tokens && b->n) {
+            HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, S));
+            HIP_OK(launch_token_check(b->d_toff, b->d_tflags, b->n, b->nwords, b->d_slow, b->d_nslow, b->d_nslow + 1, S));
+        }
         MatchArgs a{};
         a.slots = R.d_slots;
         a.nbuckets = nbuckets();
@@ -3358,6 +3400,7 @@ struct tm_engine {
         if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
         HIP_OK(enqueue_csr(b, s, S));
         b->scan_args = s;
+        if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
         return TM_OK;
     }
@@ -3520,15 +3563,24 @@ struct tm_engine {
         b->total = b->st.matches;
     }
 
-    int wait(tm_batch* b) {
+    // drained: the caller has already waited for the batch's stream (the
+    // sharded group joins all its streams in one host wait), so the first
+    // check needs no sync; *relaunched counts capacity-miss relaunches
+    int wait(tm_batch* b, bool drained = false, uint32_t* relaunched = nullptr) {
         if (!b->launched) return TM_EINVAL;
         const hipStream_t S = st(b);
         if (!b->csr) {   // an async launch stopped after the walk: redo it the CSR way
             int rc = launch(b, true);
             if (rc) return rc;
+            drained = false;
         }
         for (int attempt = 0;; ++attempt) {
-            HIP_OK(hipStreamSynchronize(S));
+            if (!drained || attempt) HIP_OK(hipStreamSynchronize(S));
+            if (attempt && relaunched) ++*relaunched;
+            if (b->check_tokens && b->n && b->h_bad[1]) {
+                snprintf(last_error(), 512, "token batch failed the device check (word offsets or flags)");
+                return TM_EINVAL;
+            }
             const uint32_t* h_dbg = b->rep->h_dbg;
             if (checked && h_dbg[0]) {
                 snprintf(last_error(), 512, "bounds check %u failed: index %u bound %u (count %u, extra %u)",
@@ -4967,6 +5019,47 @@ int tm_batch_prepare_tokens(tm_engine* e, const uint32_t* words, const uint32_t*
     *out = b;
     return TM_OK;
 }
+
+}  // extern "C"
+
+namespace etm {
+
+int part_batch_buffers(tm_engine* e, tm_batch** io, uint32_t n, uint64_t nwords, PartBuffers* out) {
+    if (!e || !io || !out) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (e->reps.empty()) return TM_ENODEV;
+    const bool fresh = *io == nullptr;
+    tm_batch* b = fresh ? new (std::nothrow) tm_batch() : *io;
+    if (!b) return TM_ENOMEM;
+    if (fresh) b->rep = e->reps[0];
+    int rc = e->use(b->rep);
+    if (!rc) {
+        try {
+            rc = e->part_buffers(b, n, nwords, out);
+        } catch (...) {
+            rc = TM_ENOMEM;
+        }
+    }
+    if (rc) {
+        if (fresh) { b->release(); delete b; }
+        else b->launched = b->done = false;
+        return rc;
+    }
+    *io = b;
+    return TM_OK;
+}
+
+int part_batch_finish(tm_engine* e, tm_batch* b, uint32_t* relaunched) {
+    if (!e || !b || !b->rep) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->use(b->rep);
+    if (rc) return rc;
+    return e->wait(b, true, relaunched);
+}
+
+}  // namespace etm
+
+extern "C" {
 
 int tm_gather_rows(tm_engine* e, const uint32_t* d_src, const int64_t* d_src_off, const int64_t* d_idx, uint32_t n,
                    const int64_t* d_dst_off, uint32_t* d_dst) {

@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct tm_engine;   // include/emqx_tm.h (opaque handles, defined in tm_engine.cpp)
+struct tm_batch;
+
 namespace etm {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -306,14 +309,41 @@ struct PartArgs {
     const uint32_t* w_off;
     const uint32_t* w_bs;
     uint32_t* segs;           // [2 * (G + 1)]: first publish / first word of every owner's part, then the totals
-    uint32_t* order;          // n: publish index at each partitioned position
-    uint32_t* ptoff;          // n + G: owner g's word offsets (relative to its part) at [tseg[g] + g ..]
+    uint32_t* order;          // n: publish index (+ tbase) at each partitioned position
+    uint32_t* ptoff;          // n + G: owner g's word offsets at [tseg[g] + g ..], relative to its part + wbase[g]
     uint8_t* ptflags;         // n
     uint32_t* pwords;
+    uint32_t tbase;           // added to every publish index in order[] (the slice's first publish)
+    uint32_t wbase[PART_MAX_G];   // added to owner g's word offsets (where its part lands in g's batch)
+    // Direct delivery: owner g's part is written straight into g's batch
+    // (same device, or a peer device over xGMI) at topic rbase[g] / word
+    // wbase[g] instead of into ptoff / ptflags / pwords; null = kept here
+    // (staged links, and the prepare-time plan)
+    uint32_t* dtoff[PART_MAX_G];
+    uint8_t* dflags[PART_MAX_G];
+    uint32_t* dwords[PART_MAX_G];
+    uint32_t rbase[PART_MAX_G];
 };
 hipError_t launch_part_count(const PartArgs& a, hipStream_t s);
 hipError_t launch_part_segs(const PartArgs& a, hipStream_t s);
 hipError_t launch_part_scatter(const PartArgs& a, hipStream_t s);
+// A part batch's token buffers (etm::part_batch_buffers): the group's copies
+// write a shard's part straight into them on `stream` (device `device`).
+struct PartBuffers {
+    uint32_t* words;
+    uint32_t* toff;
+    uint8_t* tflags;
+    size_t words_cap;
+    hipStream_t stream;
+    int device;
+};
+// engine internals the sharded group (tm_shard.cpp) drives: a part batch with
+// buffers of its own for n topics / nwords words (no host sync; the launch
+// checks the tokens on the device), and the finish of a launched part after the
+// caller has waited for its stream (*relaunched += capacity-miss relaunches,
+// each with its own wait)
+int part_batch_buffers(tm_engine* e, tm_batch** io, uint32_t n, uint64_t nwords, PartBuffers* out);
+int part_batch_finish(tm_engine* e, tm_batch* b, uint32_t* relaunched);
 // un-partition: counts_o[order[p]] = counts_p[p]
 hipError_t launch_unpart_counts(const uint32_t* order, const uint32_t* counts_p, uint32_t n, uint32_t* counts_o,
                                 hipStream_t s);

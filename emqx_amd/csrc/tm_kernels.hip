@@ -1693,8 +1693,9 @@ __global__ void tm_part_segs(PartArgs a) {
 }
 
 // Pass 3: every publish to its place in its owner's part, with its words; the
-// part's word offsets restart at 0 (each part is a token batch of its own,
-// tm_batch_prepare_tokens), so part g's offsets sit at ptoff[segs[g] + g ..].
+// part's word offsets restart at wbase[g] (where the part lands in owner g's
+// token batch, after the parts of earlier slices), so part g's offsets sit at
+// ptoff[segs[g] + g ..] ready to be copied.
 __global__ __launch_bounds__(PART_BLOCK) void tm_part_scatter(PartArgs a) {
     __shared__ uint32_t sc[PART_BLOCK / 64][PART_MAX_G], sw[PART_BLOCK / 64][PART_MAX_G];
     const uint32_t t = blockIdx.x * PART_BLOCK + threadIdx.x;
@@ -1721,7 +1722,7 @@ __global__ __launch_bounds__(PART_BLOCK) void tm_part_scatter(PartArgs a) {
         const uint32_t g = threadIdx.x;
         const uint32_t tend = g + 1 < a.G ? scan_at(a.cnt_off, a.cnt_bs, (g + 1) * a.nb) : a.cnt_off[a.G * a.nb];
         const uint32_t wend = g + 1 < a.G ? scan_at(a.w_off, a.w_bs, (g + 1) * a.nb) : a.w_off[a.G * a.nb];
-        a.ptoff[tend + g] = wend - scan_at(a.w_off, a.w_bs, g * a.nb);
+        a.ptoff[tend + g] = wend - scan_at(a.w_off, a.w_bs, g * a.nb) + a.wbase[g];
     }
     if (!valid) return;
     uint32_t bt = 0, bw = 0;   // earlier waves of the block, same owner
@@ -1730,10 +1731,20 @@ __global__ __launch_bounds__(PART_BLOCK) void tm_part_scatter(PartArgs a) {
     const uint32_t p = scan_at(a.cnt_off, a.cnt_bs, i) + bt + rank;
     const uint32_t w = scan_at(a.w_off, a.w_bs, i) + bw + wpre;
     const uint32_t wseg = scan_at(a.w_off, a.w_bs, g_me * a.nb);
-    a.order[p] = t;
-    a.ptflags[p] = a.tflags[t];
-    a.ptoff[p + g_me] = w - wseg;
+    a.order[p] = t + a.tbase;
     const uint32_t src = a.toff[t];
+    const uint32_t woff = w - wseg + a.wbase[g_me];   // in owner g's batch
+    if (a.dtoff[g_me]) {   // straight into the owner's batch (local, or a peer's HBM)
+        const uint32_t tseg = scan_at(a.cnt_off, a.cnt_bs, g_me * a.nb);
+        const uint32_t q = p - tseg + a.rbase[g_me];
+        a.dflags[g_me][q] = a.tflags[t];
+        a.dtoff[g_me][q] = woff;
+        uint32_t* dw = a.dwords[g_me] + woff;
+        for (uint32_t k = 0; k < depth; ++k) dw[k] = a.words[src + k];
+        return;
+    }
+    a.ptflags[p] = a.tflags[t];
+    a.ptoff[p + g_me] = woff;
     for (uint32_t k = 0; k < depth; ++k) a.pwords[w + k] = a.words[src + k];
 }
 

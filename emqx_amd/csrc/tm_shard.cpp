@@ -15,14 +15,30 @@
 //   * word ids mean the same on every shard: the engines run with a frozen
 //     dictionary that grows only by tm_sharded_insert_many's dictionary deltas
 //     (new literal words appended in first-appearance order on every shard).
-// One step over a batch tokenised on the home device (shard 0's):
-//   owner per publish (tm_tokens_shard) -> a stable counting sort by owner on
-//   the device (tm_part_*: each owner's publishes and words contiguous, in
-//   publish order) -> every owner matches its part (token batches of its
-//   engine, launched together) -> counts and global ids (local id * G + shard)
-//   back on the home device -> rows restored to publish order (tm_unpart_*).
-// The multi-process form with RCCL all_to_all is emqx_amd/sharded.py; in one
-// process the exchange is a device-to-device copy per part.
+//
+// A batch is cut into G contiguous slices; slice i lives on shard i's device
+// (its bytes tokenised there at prepare), so no device handles more than 1/G
+// of the batch outside its own walk.  One step, all of it queued before the
+// host waits once:
+//   source i (its own stream):  owner per publish (tm_tokens_shard) -> a
+//     stable counting sort by owner (tm_part_*) whose scatter writes every
+//     publish's tokens straight into its owner's batch, after the parts of
+//     slices < i (same device: local stores; another device: stores into the
+//     peer's HBM over xGMI); when peer access is unavailable the part of
+//     slice i owned by shard j is kept contiguous here and staged through
+//     pinned host memory;
+//   dest j (its part batch's stream): waits for every source (and copies in
+//     the staged parts), then walks its batch (the launch checks the tokens
+//     on the device);
+//   the home stream joins every part: ONE host wait, then each part's control
+//     words are checked (a capacity miss relaunches that part: another wait).
+// The sizes of the (slice i -> shard j) parts are the batch's plan, made at
+// prepare (the same kernels plus one read-back), and re-checked against the
+// device's counts after every step.  A step leaves each shard's rows where its
+// walk wrote them; the publish-order CSR with global ids (local id * G +
+// shard) is built on request (tm_sharded_result / device_csr), like the
+// single engine's dense CSR.
+// The multi-process form with RCCL all_to_all is emqx_amd/sharded.py.
 //
 // Reference: the filter set is the mnesia-replicated trie
 // (src/emqx_trie.erl:53-74) that every node matches in full
@@ -30,6 +46,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -96,46 +113,111 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
+}
+
+// Peer access between two devices, both ways: LINK_PEER when the runtime
+// grants it (xGMI on an MI355X node), LINK_STAGED otherwise (copies bounce
+// through pinned host memory).  TM_SHARD_STAGED=1 forces the staged path,
+// even on one device (tests exercise it on a one-GPU box).
+uint8_t open_link(int a, int b) {
+    const char* f = getenv("TM_SHARD_STAGED");
+    if (f && atoi(f) != 0) return TM_LINK_STAGED;
+    if (a == b) return TM_LINK_SAME;
+    int ab = 0, ba = 0;
+    if (hipDeviceCanAccessPeer(&ab, a, b) != hipSuccess || hipDeviceCanAccessPeer(&ba, b, a) != hipSuccess || !ab ||
+        !ba) {
+        (void)hipGetLastError();
+        return TM_LINK_STAGED;
+    }
+    const int pairs[2][2] = {{a, b}, {b, a}};
+    for (const auto& p : pairs) {
+        if (hipSetDevice(p[0]) != hipSuccess) {
+            (void)hipGetLastError();
+            return TM_LINK_STAGED;
+        }
+        const hipError_t e = hipDeviceEnablePeerAccess(p[1], 0);
+        (void)hipGetLastError();
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return TM_LINK_STAGED;
+    }
+    return TM_LINK_PEER;
+}
+
 }  // namespace
+
+// Slice i of a batch: its publishes, tokenised and partitioned on shard i's device.
+struct Slice {
+    uint32_t lo = 0, n = 0;        // publishes [lo, lo + n) of the batch
+    uint64_t nwords = 0;
+    DBuf<uint32_t> words, toff, owner, cnt, wcnt, cnt_off, cnt_bs, w_off, w_bs, segs, order, ptoff, pwords;
+    DBuf<uint8_t> tflags, ptflags;
+    uint32_t* h_segs = nullptr;    // the last step's partition counts (read back with its wait)
+    size_t ch_segs = 0;
+    std::vector<uint32_t> seg;     // the plan: [0..G] first publish of each owner's part, [G+1..2G+1] first word
+
+    void on(int d) {
+        for (DBuf<uint32_t>* x : {&words, &toff, &owner, &cnt, &wcnt, &cnt_off, &cnt_bs, &w_off, &w_bs, &segs, &order,
+                                  &ptoff, &pwords})
+            x->dev = d;
+        tflags.dev = ptflags.dev = d;
+    }
+    void release() {
+        for (DBuf<uint32_t>* x : {&words, &toff, &owner, &cnt, &wcnt, &cnt_off, &cnt_bs, &w_off, &w_bs, &segs, &order,
+                                  &ptoff, &pwords})
+            x->release();
+        tflags.release();
+        ptflags.release();
+        if (h_segs) (void)hipHostFree(h_segs);
+        h_segs = nullptr;
+        ch_segs = 0;
+    }
+    uint32_t part_n(uint32_t j) const { return seg[j + 1] - seg[j]; }
+    uint32_t part_w(uint32_t G, uint32_t j) const { return seg[G + 2 + j] - seg[G + 1 + j]; }
+};
 
 struct tm_sharded_batch {
     uint32_t n = 0;
-    uint64_t nwords = 0;
-    uint64_t dict_words = ~0ull;          // dictionary size the tokens were made with
-    std::vector<uint8_t> bytes;           // the publishes (re-tokenised if the dictionary grew)
+    uint64_t dict_words = ~0ull;          // dictionary size the plan was made with
+    std::vector<uint8_t> bytes;           // the publishes (re-planned if the dictionary grew)
     std::vector<uint64_t> offs;
-    // home device
-    DBuf<uint32_t> words, toff, owner, cnt, wcnt, cnt_off, cnt_bs, w_off, w_bs, segs, order, ptoff, pwords;
-    DBuf<uint32_t> counts_p, ids_p, counts_o, src_off, src_bs, dst_off, dst_bs, rowg, out;
-    DBuf<uint8_t> tflags, ptflags;
-    uint32_t* h_segs = nullptr;
-    size_t ch_segs = 0;
-    // per shard: its part (a token batch of its engine) and export staging on its device
-    std::vector<tm_batch*> part;
+    std::vector<Slice> src;               // G slices (G > 1)
+    std::vector<tm_batch*> part;          // shard j's part batch (its engine)
+    std::vector<PartBuffers> pb;
+    std::vector<uint32_t> pn;             // shard j: publishes it walks
+    std::vector<uint64_t> pw;             //          their words
+    std::vector<uint32_t> R, W;           // [i * G + j]: where slice i's part lands in shard j's batch
+    uint32_t* h_close = nullptr;          // pinned: shard j's closing word offset
+    size_t ch_close = 0;
+    std::vector<uint8_t*> bounce;         // staged links: [i * G + j] pinned [toff | words | tflags]
+    std::vector<size_t> cbounce;
+    // publish-order CSR with global ids on the home device (built on request)
+    DBuf<uint32_t> counts_p, ids_p, gorder, counts_o, src_off, src_bs, dst_off, dst_bs, rowg, out;
     std::vector<DBuf<uint32_t>> xcnt, xids;
-    std::vector<uint32_t> tseg, wseg;     // first publish / word of each part (+ totals)
-    std::vector<uint64_t> mseg;           // first match of each part's rows (+ total)
+    std::vector<uint64_t> mseg;           // first match of each part (+ total), in shard order
     uint64_t total = 0;
     bool done = false;
-    bool direct = false;   // one shard: the result is the part's own CSR (no partition, no reorder)
-    // host result
+    bool ordered = false;
     uint32_t *h_row = nullptr, *h_ids = nullptr;
     size_t ch_row = 0, ch_ids = 0;
     tm_batch_stats st{};
-    float ms_partition = 0, ms_parts = 0, ms_unpartition = 0;
+    float ms_partition = 0, ms_exchange = 0, ms_step = 0, ms_unpartition = 0;
+    uint32_t host_waits = 0;
 
     void release() {
-        for (DBuf<uint32_t>* b : {&words, &toff, &owner, &cnt, &wcnt, &cnt_off, &cnt_bs, &w_off, &w_bs, &segs, &order,
-                                  &ptoff, &pwords, &counts_p, &ids_p, &counts_o, &src_off, &src_bs, &dst_off, &dst_bs,
-                                  &rowg, &out})
+        for (auto& sl : src) sl.release();
+        for (DBuf<uint32_t>* b : {&counts_p, &ids_p, &gorder, &counts_o, &src_off, &src_bs, &dst_off, &dst_bs, &rowg,
+                                  &out})
             b->release();
-        tflags.release();
-        ptflags.release();
         for (auto& x : xcnt) x.release();
         for (auto& x : xids) x.release();
-        for (uint32_t* h : {h_segs, h_row, h_ids})
+        for (uint8_t* p : bounce)
+            if (p) (void)hipHostFree(p);
+        bounce.clear();
+        for (uint32_t* h : {h_row, h_ids, h_close})
             if (h) (void)hipHostFree(h);
-        h_segs = h_row = h_ids = nullptr;
+        h_row = h_ids = h_close = nullptr;
     }
 };
 
@@ -144,9 +226,15 @@ struct tm_sharded {
     std::vector<int32_t> dev;
     uint32_t G = 0;
     int home = -1;
-    hipStream_t s = nullptr;   // home device: partition / un-partition kernels
-    std::mutex mu;             // one step (and one mutation) at a time
+    hipStream_t s = nullptr;                 // home device: the step's join, the on-request reorder
+    std::vector<hipStream_t> ss;             // shard g's device: its slice's partition
+    std::vector<hipEvent_t> ev_p0, ev_p1, ev_x0, ev_x1, ev_done;   // per shard, on its device
+    std::vector<uint8_t> link;               // [i * G + j]: TM_LINK_*
+    std::mutex mu;                           // one step (and one mutation) at a time
     tm_sharded_batch* last = nullptr;
+    // TM_SHARD_COPY=1: sources keep their parts and the shards copy them in
+    // (DMA) instead of the scatter writing into the shards' batches (A/B)
+    const bool copy_parts = getenv("TM_SHARD_COPY") && atoi(getenv("TM_SHARD_COPY")) != 0;
 
     template <class F>
     void each(F f) {
@@ -161,217 +249,372 @@ struct tm_sharded {
         return tm_stats(sh[0], &st) == TM_OK ? st.words : 0;
     }
 
-    // publishes -> tokens on the home device (shard 0's device tokeniser)
-    int tokenize(tm_sharded_batch* b) {
-        const uint32_t n = b->n;
-        const uint64_t nbytes = b->offs[n];
-        int rc;
-        for (DBuf<uint32_t>* x : {&b->words, &b->toff}) x->dev = home;
-        b->tflags.dev = home;
-        if ((rc = b->words.reserve(std::max<uint64_t>(nbytes + n, 1)))) return rc;
-        if ((rc = b->toff.reserve((size_t)n + 1))) return rc;
-        if ((rc = b->tflags.reserve(std::max<size_t>(n, 1)))) return rc;
-        static const uint8_t zero = 0;
-        uint64_t nw = 0;
-        b->dict_words = dict_words();
-        if ((rc = tm_tokenize_device(sh[0], b->bytes.empty() ? &zero : b->bytes.data(), b->offs.data(), n, b->words.p,
-                                     b->words.cap, b->toff.p, b->tflags.p, &nw)))
-            return rc;
-        b->nwords = nw;
+    // bytes of slice i's memory -> shard j's device, enqueued on dest stream S
+    // (device dev[j] current): same device, or a peer copy (staged links copy
+    // from their bounce buffer instead, see step)
+    int copy_in(uint32_t i, uint32_t j, void* dst, const void* src, size_t bytes, hipStream_t S) {
+        if (!bytes) return TM_OK;
+        if (link[i * G + j] == TM_LINK_PEER) SH_HIP(hipMemcpyPeerAsync(dst, dev[j], src, dev[i], bytes, S));
+        else SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S));
         return TM_OK;
     }
 
-    // One shard: every publish is its own part and the rows come back in
-    // publish order -- no owner kernel, no partition, no reorder; global ids
-    // are the local ones (local * 1 + 0).
-    int step_one(tm_sharded_batch* b) {
+    // a blocking copy between shards' devices (the on-request reorder)
+    int copy_now(uint32_t i, uint32_t j, void* dst, const void* src, size_t bytes) {
+        if (!bytes) return TM_OK;
+        const uint8_t l = link[i * G + j];
+        if (l == TM_LINK_STAGED) {
+            std::vector<uint8_t> tmp(bytes);
+            SH_HIP(hipSetDevice(dev[i]));
+            SH_HIP(hipMemcpy(tmp.data(), src, bytes, hipMemcpyDeviceToHost));
+            SH_HIP(hipSetDevice(dev[j]));
+            SH_HIP(hipMemcpy(dst, tmp.data(), bytes, hipMemcpyHostToDevice));
+        } else if (l == TM_LINK_PEER) {
+            SH_HIP(hipSetDevice(dev[j]));
+            SH_HIP(hipMemcpyPeer(dst, dev[j], src, dev[i], bytes));
+        } else {
+            SH_HIP(hipSetDevice(dev[j]));
+            SH_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+        }
+        return TM_OK;
+    }
+
+    PartArgs part_args(Slice& S) {
+        PartArgs a{};
+        a.owner = S.owner.p; a.words = S.words.p; a.toff = S.toff.p; a.tflags = S.tflags.p;
+        a.n = S.n; a.G = G; a.nb = std::max<uint32_t>(1, (S.n + PART_BLOCK - 1) / PART_BLOCK);
+        a.cnt = S.cnt.p; a.wcnt = S.wcnt.p;
+        a.cnt_off = S.cnt_off.p; a.cnt_bs = S.cnt_bs.p; a.w_off = S.w_off.p; a.w_bs = S.w_bs.p;
+        a.segs = S.segs.p; a.order = S.order.p; a.ptoff = S.ptoff.p; a.ptflags = S.ptflags.p;
+        a.pwords = S.pwords.p;
+        return a;
+    }
+
+    // owner + counts of slice i's parts (no scatter), on shard i's stream
+    int enqueue_counts(Slice& S, const PartArgs& a, hipStream_t st) {
+        const uint32_t gb = G * a.nb;
+        SH_HIP(launch_tokens_shard(S.words.p, S.toff.p, S.n, G, S.owner.p, st));
+        SH_HIP(launch_part_count(a, st));
+        ScanArgs sc{};
+        sc.count = S.cnt.p; sc.row_off = S.cnt_off.p; sc.block_sums = S.cnt_bs.p; sc.n = gb;
+        SH_HIP(launch_scan(sc, st, nullptr));
+        ScanArgs sw{};
+        sw.count = S.wcnt.p; sw.row_off = S.w_off.p; sw.block_sums = S.w_bs.p; sw.n = gb;
+        SH_HIP(launch_scan(sw, st, nullptr));
+        SH_HIP(launch_part_segs(a, st));
+        return TM_OK;
+    }
+
+    // Prepare-time: every slice tokenised on its shard's device, its parts
+    // counted (the plan: how many publishes and words of slice i shard j
+    // walks, and where they land in shard j's batch), every shard's part batch
+    // sized.  One shard: the slice is tokenised straight into the part batch.
+    int plan(tm_sharded_batch* b) {
         int rc;
         const uint32_t n = b->n;
-        const double t1 = now_ms();
-        if (b->part.size() != 1) b->part.assign(1, nullptr);
-        static const uint32_t zero_off = 0;
-        if (!n) {
-            SH_HIP(hipSetDevice(home));
-            SH_HIP(hipMemcpy(b->toff.p, &zero_off, 4, hipMemcpyHostToDevice));
+        static const uint8_t zero = 0;
+        const uint8_t* bytes = b->bytes.empty() ? &zero : b->bytes.data();
+        b->dict_words = dict_words();
+        b->done = b->ordered = false;
+        if (b->part.size() != G) {
+            b->part.assign(G, nullptr);
+            b->pb.assign(G, PartBuffers{});
         }
-        if ((rc = tm_batch_prepare_tokens(sh[0], b->words.p, b->toff.p, b->tflags.p, n, b->nwords, 1, &b->part[0])))
-            return rc;
-        if ((rc = tm_batch_launch(sh[0], b->part[0]))) return rc;
-        if ((rc = tm_batch_wait(sh[0], b->part[0]))) return rc;
-        tm_batch_stats p{};
-        if ((rc = tm_batch_stats_get(sh[0], b->part[0], &p))) return rc;
-        if (p.matches > MAX_RESULT) return TM_EOVERFLOW;
-        b->st = p;
-        b->st.topics = n;
-        b->tseg.assign(2, 0);
-        b->tseg[1] = n;
-        b->wseg.assign(2, 0);
-        b->wseg[1] = (uint32_t)b->nwords;
-        b->mseg.assign(2, 0);
-        b->mseg[1] = p.matches;
-        b->ms_partition = 0;
-        b->ms_parts = (float)(now_ms() - t1);
-        b->ms_unpartition = 0;
-        b->total = p.matches;
-        b->direct = true;
-        b->done = true;
+        b->pn.assign(G, 0);
+        b->pw.assign(G, 0);
+        if (G == 1) {
+            const uint64_t cap = b->offs[n] + n + 1;
+            if ((rc = part_batch_buffers(sh[0], &b->part[0], n, cap, &b->pb[0]))) return rc;
+            uint64_t nw = 0;
+            if ((rc = tm_tokenize_device(sh[0], bytes, b->offs.data(), n, b->pb[0].words, b->pb[0].words_cap,
+                                         b->pb[0].toff, b->pb[0].tflags, &nw)))
+                return rc;
+            b->pn[0] = n;
+            b->pw[0] = nw;
+            return part_batch_buffers(sh[0], &b->part[0], n, nw, &b->pb[0]);
+        }
+        b->src.resize(G);
+        std::vector<int> rcs(G, TM_OK);
+        each([&](uint32_t i) {   // slices in parallel: each tokeniser waits on its own device
+            Slice& S = b->src[i];
+            S.lo = (uint32_t)((uint64_t)n * i / G);
+            S.n = (uint32_t)((uint64_t)n * (i + 1) / G) - S.lo;
+            S.on(dev[i]);
+            S.seg.assign(2 * ((size_t)G + 1), 0);
+            const uint64_t nbytes = b->offs[S.lo + S.n] - b->offs[S.lo];
+            int r;
+            const uint32_t nb = std::max<uint32_t>(1, (S.n + PART_BLOCK - 1) / PART_BLOCK), gb = G * nb;
+            if ((r = S.words.reserve(nbytes + S.n + 1)) || (r = S.toff.reserve((size_t)S.n + 1)) ||
+                (r = S.tflags.reserve(std::max<size_t>(S.n, 1))) || (r = S.owner.reserve(std::max<size_t>(S.n, 1))) ||
+                (r = S.cnt.reserve(gb)) || (r = S.wcnt.reserve(gb)) || (r = S.cnt_off.reserve((size_t)gb + 1)) ||
+                (r = S.w_off.reserve((size_t)gb + 1)) || (r = S.cnt_bs.reserve(scan_block_count(gb) + 1)) ||
+                (r = S.w_bs.reserve(scan_block_count(gb) + 1)) || (r = S.segs.reserve(2 * ((size_t)G + 1))) ||
+                (r = S.order.reserve(std::max<size_t>(S.n, 1))) || (r = S.ptoff.reserve((size_t)S.n + G)) ||
+                (r = S.ptflags.reserve(std::max<size_t>(S.n, 1))) ||
+                (r = host_pinned(S.h_segs, S.ch_segs, 2 * ((size_t)G + 1)))) {
+                rcs[i] = r;
+                return;
+            }
+            uint64_t nw = 0;
+            if ((r = tm_tokenize_device(sh[i], bytes, b->offs.data() + S.lo, S.n, S.words.p, S.words.cap, S.toff.p,
+                                        S.tflags.p, &nw))) {
+                rcs[i] = r;
+                return;
+            }
+            S.nwords = nw;
+            if ((r = S.pwords.reserve(std::max<uint64_t>(nw, 1)))) { rcs[i] = r; return; }
+            if (!S.n) return;
+            if (hipSetDevice(dev[i]) != hipSuccess) { rcs[i] = TM_EIO; return; }
+            const PartArgs a = part_args(S);
+            if ((r = enqueue_counts(S, a, ss[i]))) { rcs[i] = r; return; }
+            if (hipMemcpyAsync(S.h_segs, S.segs.p, 2 * ((size_t)G + 1) * 4, hipMemcpyDeviceToHost, ss[i]) !=
+                    hipSuccess ||
+                hipStreamSynchronize(ss[i]) != hipSuccess) {
+                snprintf(error_buf(), 512, "partition plan of slice %u failed", i);
+                rcs[i] = TM_EIO;
+                return;
+            }
+            S.seg.assign(S.h_segs, S.h_segs + 2 * ((size_t)G + 1));
+            if (S.seg[G] != S.n || S.seg[2 * G + 1] != nw) {
+                snprintf(error_buf(), 512, "partition of slice %u lost publishes: %u of %u, %u of %llu words", i,
+                         S.seg[G], S.n, S.seg[2 * G + 1], (unsigned long long)nw);
+                rcs[i] = TM_EIO;
+            }
+        });
+        for (int r : rcs)
+            if (r) return r;
+        // where slice i's part lands in shard j's batch: after the parts of slices < i
+        b->R.assign((size_t)G * G, 0);
+        b->W.assign((size_t)G * G, 0);
+        for (uint32_t j = 0; j < G; ++j) {
+            uint64_t rn = 0, rw = 0;
+            for (uint32_t i = 0; i < G; ++i) {
+                const Slice& S = b->src[i];
+                if (rw > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+                b->R[i * G + j] = (uint32_t)rn;
+                b->W[i * G + j] = (uint32_t)rw;
+                rn += S.n ? S.part_n(j) : 0;
+                rw += S.n ? S.part_w(G, j) : 0;
+            }
+            b->pn[j] = (uint32_t)rn;
+            b->pw[j] = rw;
+        }
+        if ((rc = host_pinned(b->h_close, b->ch_close, G))) return rc;
+        for (uint32_t j = 0; j < G; ++j) {
+            b->h_close[j] = (uint32_t)b->pw[j];
+            if ((rc = part_batch_buffers(sh[j], &b->part[j], b->pn[j], b->pw[j], &b->pb[j]))) return rc;
+        }
+        // staged links bounce through pinned host memory: [toff | words | tflags]
+        b->bounce.resize((size_t)G * G, nullptr);
+        b->cbounce.resize((size_t)G * G, 0);
+        for (uint32_t i = 0; i < G; ++i)
+            for (uint32_t j = 0; j < G; ++j) {
+                if (link[i * G + j] != TM_LINK_STAGED || !b->src[i].n) continue;
+                const Slice& S = b->src[i];
+                const size_t need = (size_t)S.part_n(j) * 5 + (size_t)S.part_w(G, j) * 4 + 16;
+                if ((rc = host_pinned(b->bounce[i * G + j], b->cbounce[i * G + j], need))) return rc;
+            }
         return TM_OK;
     }
 
     int step(tm_sharded_batch* b) {
         int rc;
-        const uint32_t n = b->n;
-        b->done = false;
-        b->direct = false;
-        if (b->dict_words != dict_words() && (rc = tokenize(b))) return rc;   // new words since tokenisation
-        if (G == 1) return step_one(b);
         const double t0 = now_ms();
-        // ---- owner and partition (home device)
-        const uint32_t nb = std::max<uint32_t>(1, (n + PART_BLOCK - 1) / PART_BLOCK);
-        const uint32_t gb = G * nb;
-        for (DBuf<uint32_t>* x : {&b->owner, &b->cnt, &b->wcnt, &b->cnt_off, &b->cnt_bs, &b->w_off, &b->w_bs, &b->segs,
-                                  &b->order, &b->ptoff, &b->pwords})
-            x->dev = home;
-        b->ptflags.dev = home;
-        if ((rc = b->owner.reserve(std::max<size_t>(n, 1)))) return rc;
-        if ((rc = b->cnt.reserve(gb))) return rc;
-        if ((rc = b->wcnt.reserve(gb))) return rc;
-        if ((rc = b->cnt_off.reserve((size_t)gb + 1))) return rc;
-        if ((rc = b->w_off.reserve((size_t)gb + 1))) return rc;
-        if ((rc = b->cnt_bs.reserve(scan_block_count(gb) + 1))) return rc;
-        if ((rc = b->w_bs.reserve(scan_block_count(gb) + 1))) return rc;
-        if ((rc = b->segs.reserve(2 * ((size_t)G + 1)))) return rc;
-        if ((rc = b->order.reserve(std::max<size_t>(n, 1)))) return rc;
-        if ((rc = b->ptoff.reserve((size_t)n + G))) return rc;
-        if ((rc = b->pwords.reserve(std::max<uint64_t>(b->nwords, 1)))) return rc;
-        if ((rc = b->ptflags.reserve(std::max<size_t>(n, 1)))) return rc;
-        if ((rc = host_pinned(b->h_segs, b->ch_segs, 2 * ((size_t)G + 1)))) return rc;
-        b->tseg.assign(G + 1, 0);
-        b->wseg.assign(G + 1, 0);
-        if (n) {
-            if ((rc = tm_tokens_shard(sh[0], b->words.p, b->toff.p, n, G, b->owner.p))) return rc;
-            SH_HIP(hipSetDevice(home));
-            PartArgs a{};
-            a.owner = b->owner.p; a.words = b->words.p; a.toff = b->toff.p; a.tflags = b->tflags.p;
-            a.n = n; a.G = G; a.nb = nb;
-            a.cnt = b->cnt.p; a.wcnt = b->wcnt.p;
-            a.cnt_off = b->cnt_off.p; a.cnt_bs = b->cnt_bs.p; a.w_off = b->w_off.p; a.w_bs = b->w_bs.p;
-            a.segs = b->segs.p; a.order = b->order.p; a.ptoff = b->ptoff.p; a.ptflags = b->ptflags.p;
-            a.pwords = b->pwords.p;
-            SH_HIP(launch_part_count(a, s));
-            ScanArgs sc{};
-            sc.count = b->cnt.p; sc.row_off = b->cnt_off.p; sc.block_sums = b->cnt_bs.p; sc.n = gb;
-            SH_HIP(launch_scan(sc, s, nullptr));
-            ScanArgs sw{};
-            sw.count = b->wcnt.p; sw.row_off = b->w_off.p; sw.block_sums = b->w_bs.p; sw.n = gb;
-            SH_HIP(launch_scan(sw, s, nullptr));
-            SH_HIP(launch_part_segs(a, s));
-            SH_HIP(launch_part_scatter(a, s));
-            SH_HIP(hipMemcpyAsync(b->h_segs, b->segs.p, 2 * ((size_t)G + 1) * 4, hipMemcpyDeviceToHost, s));
-            SH_HIP(hipStreamSynchronize(s));
-            for (uint32_t g = 0; g <= G; ++g) {
-                b->tseg[g] = b->h_segs[g];
-                b->wseg[g] = b->h_segs[G + 1 + g];
-            }
-            if (b->tseg[G] != n || b->wseg[G] != b->nwords) {
-                snprintf(error_buf(), 512, "partition lost publishes: %u of %u, %u of %llu words", b->tseg[G], n,
-                         b->wseg[G], (unsigned long long)b->nwords);
-                return TM_EIO;
+        b->done = b->ordered = false;
+        b->host_waits = 0;
+        if (b->dict_words != dict_words() && (rc = plan(b))) return rc;   // new words since the plan
+        uint32_t waits = 0;
+        // ---- sources: owner + partition of every slice on its own device
+        if (G > 1) {
+            for (uint32_t i = 0; i < G; ++i) {
+                Slice& S = b->src[i];
+                SH_HIP(hipSetDevice(dev[i]));
+                SH_HIP(hipEventRecord(ev_p0[i], ss[i]));
+                if (S.n) {
+                    PartArgs a = part_args(S);
+                    a.tbase = S.lo;
+                    for (uint32_t j = 0; j < G; ++j) {
+                        a.wbase[j] = b->W[i * G + j];
+                        if (link[i * G + j] == TM_LINK_STAGED || copy_parts) continue;
+                        // same device or a peer: the scatter writes into shard j's batch itself
+                        a.dtoff[j] = b->pb[j].toff;
+                        a.dflags[j] = b->pb[j].tflags;
+                        a.dwords[j] = b->pb[j].words;
+                        a.rbase[j] = b->R[i * G + j];
+                    }
+                    if ((rc = enqueue_counts(S, a, ss[i]))) return rc;
+                    SH_HIP(launch_part_scatter(a, ss[i]));
+                    SH_HIP(hipMemcpyAsync(S.h_segs, S.segs.p, 2 * ((size_t)G + 1) * 4, hipMemcpyDeviceToHost, ss[i]));
+                    for (uint32_t j = 0; j < G; ++j) {   // staged links: the part goes out to pinned memory
+                        if (link[i * G + j] != TM_LINK_STAGED) continue;
+                        const uint32_t pn = S.part_n(j), pw = S.part_w(G, j);
+                        uint8_t* bb = b->bounce[i * G + j];
+                        if (pn) SH_HIP(hipMemcpyAsync(bb, S.ptoff.p + S.seg[j] + j, (size_t)pn * 4, hipMemcpyDeviceToHost, ss[i]));
+                        if (pw) SH_HIP(hipMemcpyAsync(bb + (size_t)pn * 4, S.pwords.p + S.seg[G + 1 + j], (size_t)pw * 4,
+                                                      hipMemcpyDeviceToHost, ss[i]));
+                        if (pn) SH_HIP(hipMemcpyAsync(bb + (size_t)pn * 4 + (size_t)pw * 4, S.ptflags.p + S.seg[j], pn,
+                                                      hipMemcpyDeviceToHost, ss[i]));
+                    }
+                }
+                SH_HIP(hipEventRecord(ev_p1[i], ss[i]));
             }
         }
-        const double t1 = now_ms();
-        // ---- every owner matches its part (token batches of its engine)
-        if (b->part.size() != G) b->part.assign(G, nullptr);
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint32_t ng = b->tseg[g + 1] - b->tseg[g];
-            const uint64_t nw = b->wseg[g + 1] - b->wseg[g];
-            static const uint32_t zero_off = 0;
-            const uint32_t* w = n ? b->pwords.p + b->wseg[g] : b->words.p;
-            const uint32_t* o = n ? b->ptoff.p + b->tseg[g] + g : nullptr;
-            const uint8_t* f = n ? b->ptflags.p + b->tseg[g] : b->tflags.p;
-            if (!n) {   // an empty batch: one zero offset per part
-                SH_HIP(hipSetDevice(home));
-                SH_HIP(hipMemcpy(b->toff.p, &zero_off, 4, hipMemcpyHostToDevice));
-                o = b->toff.p;
+        // ---- shards: their parts land in their batches, which walk them
+        for (uint32_t j = 0; j < G; ++j) {
+            const PartBuffers& P = b->pb[j];
+            SH_HIP(hipSetDevice(dev[j]));
+            if (G > 1) {
+                for (uint32_t i = 0; i < G; ++i) SH_HIP(hipStreamWaitEvent(P.stream, ev_p1[i], 0));
+                SH_HIP(hipEventRecord(ev_x0[j], P.stream));
+                for (uint32_t i = 0; i < G; ++i) {
+                    const Slice& S = b->src[i];
+                    if (!S.n) continue;
+                    const uint32_t pn = S.part_n(j), pw = S.part_w(G, j);
+                    uint32_t* dtoff = P.toff + b->R[i * G + j];
+                    uint32_t* dwords = P.words + b->W[i * G + j];
+                    uint8_t* dflags = P.tflags + b->R[i * G + j];
+                    if (link[i * G + j] == TM_LINK_STAGED) {
+                        const uint8_t* bb = b->bounce[i * G + j];
+                        if (pn) SH_HIP(hipMemcpyAsync(dtoff, bb, (size_t)pn * 4, hipMemcpyHostToDevice, P.stream));
+                        if (pw) SH_HIP(hipMemcpyAsync(dwords, bb + (size_t)pn * 4, (size_t)pw * 4, hipMemcpyHostToDevice,
+                                                      P.stream));
+                        if (pn) SH_HIP(hipMemcpyAsync(dflags, bb + (size_t)pn * 4 + (size_t)pw * 4, pn,
+                                                      hipMemcpyHostToDevice, P.stream));
+                        continue;
+                    }
+                    if (!copy_parts) continue;   // written there by the source's scatter
+                    if ((rc = copy_in(i, j, dtoff, S.ptoff.p + S.seg[j] + j, (size_t)pn * 4, P.stream))) return rc;
+                    if ((rc = copy_in(i, j, dwords, S.pwords.p + S.seg[G + 1 + j], (size_t)pw * 4, P.stream))) return rc;
+                    if ((rc = copy_in(i, j, dflags, S.ptflags.p + S.seg[j], pn, P.stream))) return rc;
+                }
+                SH_HIP(hipMemcpyAsync(P.toff + b->pn[j], b->h_close + j, 4, hipMemcpyHostToDevice, P.stream));
+                SH_HIP(hipEventRecord(ev_x1[j], P.stream));
             }
-            if ((rc = tm_batch_prepare_tokens(sh[g], w, o, f, ng, nw, 1, &b->part[g]))) return rc;
+            if ((rc = tm_batch_launch(sh[j], b->part[j]))) return rc;
+            SH_HIP(hipSetDevice(dev[j]));
+            SH_HIP(hipEventRecord(ev_done[j], P.stream));
         }
-        for (uint32_t g = 0; g < G; ++g)
-            if ((rc = tm_batch_launch(sh[g], b->part[g]))) return rc;
+        // ---- one host wait: the home stream joins every part
+        SH_HIP(hipSetDevice(home));
+        for (uint32_t j = 0; j < G; ++j) SH_HIP(hipStreamWaitEvent(s, ev_done[j], 0));
+        SH_HIP(hipStreamSynchronize(s));
+        ++waits;
+        if (G > 1)
+            for (uint32_t i = 0; i < G; ++i) {   // the device's partition must be the plan
+                const Slice& S = b->src[i];
+                if (S.n && !std::equal(S.seg.begin(), S.seg.end(), S.h_segs)) {
+                    snprintf(error_buf(), 512, "slice %u partitioned differently from its plan", i);
+                    return TM_EIO;
+                }
+            }
         int first = TM_OK;
-        for (uint32_t g = 0; g < G; ++g) {   // every part is drained, even after an error
-            rc = tm_batch_wait(sh[g], b->part[g]);
+        for (uint32_t j = 0; j < G; ++j) {   // every part is checked, even after an error
+            rc = part_batch_finish(sh[j], b->part[j], &waits);
             if (rc && !first) first = rc;
         }
         if (first) return first;
-        b->mseg.assign(G + 1, 0);
         b->st = tm_batch_stats{};
-        for (uint32_t g = 0; g < G; ++g) {
+        b->mseg.assign(G + 1, 0);
+        for (uint32_t j = 0; j < G; ++j) {
             tm_batch_stats p{};
-            if ((rc = tm_batch_stats_get(sh[g], b->part[g], &p))) return rc;
-            b->mseg[g + 1] = b->mseg[g] + p.matches;
+            if ((rc = tm_batch_stats_get(sh[j], b->part[j], &p))) return rc;
+            b->mseg[j + 1] = b->mseg[j] + p.matches;
             b->st.topics += p.topics; b->st.visits += p.visits; b->st.hash_hits += p.hash_hits;
             b->st.words += p.words; b->st.matches += p.matches; b->st.slow_topics += p.slow_topics;
             b->st.overflow_tiles += p.overflow_tiles; b->st.probes += p.probes;
             b->st.ms_match = std::max(b->st.ms_match, p.ms_match);
             b->st.ms_total = std::max(b->st.ms_total, p.ms_total);
         }
-        const uint64_t total = b->mseg[G];
-        if (total > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
-        // counts and global ids of every part -> the home device, in partition order
-        for (DBuf<uint32_t>* x : {&b->counts_p, &b->ids_p, &b->counts_o, &b->src_off, &b->src_bs, &b->dst_off,
-                                  &b->dst_bs, &b->rowg, &b->out})
+        b->total = b->mseg[G];
+        if (b->total > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
+        b->ms_partition = b->ms_exchange = 0;
+        if (G > 1)
+            for (uint32_t g = 0; g < G; ++g) {
+                b->ms_partition = std::max(b->ms_partition, elapsed(ev_p0[g], ev_p1[g]));
+                b->ms_exchange = std::max(b->ms_exchange, elapsed(ev_x0[g], ev_x1[g]));
+            }
+        b->ms_step = (float)(now_ms() - t0);
+        b->host_waits = waits;
+        b->st.topics = b->n;
+        b->done = true;
+        return TM_OK;
+    }
+
+    // The publish-order CSR with global ids on the home device, from the
+    // shards' rows: each part's counts and ids (id * G + shard) to the home
+    // device, the slices' partition orders as one publish index per walked
+    // position, and the rows moved into publish order (tm_unpart_*).
+    int order_rows(tm_sharded_batch* b) {
+        if (b->ordered) return TM_OK;
+        int rc;
+        const double t0 = now_ms();
+        const uint32_t n = b->n;
+        const uint64_t total = b->total;
+        for (DBuf<uint32_t>* x : {&b->counts_p, &b->ids_p, &b->gorder, &b->counts_o, &b->src_off, &b->src_bs,
+                                  &b->dst_off, &b->dst_bs, &b->rowg, &b->out})
             x->dev = home;
-        if ((rc = b->counts_p.reserve(std::max<size_t>(n, 1)))) return rc;
-        if ((rc = b->ids_p.reserve(std::max<uint64_t>(total, 1)))) return rc;
+        if ((rc = b->counts_p.reserve(std::max<size_t>(n, 1))) || (rc = b->ids_p.reserve(std::max<uint64_t>(total, 1))) ||
+            (rc = b->gorder.reserve(std::max<size_t>(n, 1))) || (rc = b->counts_o.reserve(std::max<size_t>(n, 1))) ||
+            (rc = b->src_off.reserve((size_t)n + 1)) || (rc = b->dst_off.reserve((size_t)n + 1)) ||
+            (rc = b->src_bs.reserve(scan_block_count(n) + 1)) || (rc = b->dst_bs.reserve(scan_block_count(n) + 1)) ||
+            (rc = b->rowg.reserve((size_t)n + 1)) || (rc = b->out.reserve(std::max<uint64_t>(total, 1))))
+            return rc;
         if (b->xcnt.size() != G) {
             b->xcnt.resize(G);
             b->xids.resize(G);
         }
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint32_t ng = b->tseg[g + 1] - b->tseg[g];
-            const uint64_t mg = b->mseg[g + 1] - b->mseg[g];
-            if (!ng) continue;
-            if (dev[g] == home) {   // same device: export straight into place
-                if ((rc = tm_batch_export(sh[g], b->part[g], b->counts_p.p + b->tseg[g], b->ids_p.p + b->mseg[g], G, g)))
-                    return rc;
-                continue;
+        uint64_t pbase = 0;
+        for (uint32_t j = 0; j < G; ++j) {
+            const uint32_t nj = b->pn[j];
+            const uint64_t mj = b->mseg[j + 1] - b->mseg[j];
+            if (nj) {
+                if (dev[j] == home && link[j * G + 0] != TM_LINK_STAGED) {   // export straight into place
+                    if ((rc = tm_batch_export(sh[j], b->part[j], b->counts_p.p + pbase, b->ids_p.p + b->mseg[j], G, j)))
+                        return rc;
+                } else {
+                    b->xcnt[j].dev = b->xids[j].dev = dev[j];
+                    if ((rc = b->xcnt[j].reserve(nj)) || (rc = b->xids[j].reserve(std::max<uint64_t>(mj, 1)))) return rc;
+                    if ((rc = tm_batch_export(sh[j], b->part[j], b->xcnt[j].p, b->xids[j].p, G, j))) return rc;
+                    if ((rc = copy_now(j, 0, b->counts_p.p + pbase, b->xcnt[j].p, (size_t)nj * 4))) return rc;
+                    if ((rc = copy_now(j, 0, b->ids_p.p + b->mseg[j], b->xids[j].p, mj * 4))) return rc;
+                }
             }
-            b->xcnt[g].dev = b->xids[g].dev = dev[g];
-            if ((rc = b->xcnt[g].reserve(ng))) return rc;
-            if ((rc = b->xids[g].reserve(std::max<uint64_t>(mg, 1)))) return rc;
-            if ((rc = tm_batch_export(sh[g], b->part[g], b->xcnt[g].p, b->xids[g].p, G, g))) return rc;
-            SH_HIP(hipSetDevice(home));
-            SH_HIP(hipMemcpyAsync(b->counts_p.p + b->tseg[g], b->xcnt[g].p, (size_t)ng * 4, hipMemcpyDeviceToDevice, s));
-            if (mg) SH_HIP(hipMemcpyAsync(b->ids_p.p + b->mseg[g], b->xids[g].p, mg * 4, hipMemcpyDeviceToDevice, s));
+            // the publish walked at each position of shard j's batch
+            for (uint32_t i = 0; i < G; ++i) {
+                const Slice& S = b->src[i];
+                if (!S.n || !S.part_n(j)) continue;
+                if ((rc = copy_now(i, 0, b->gorder.p + pbase + b->R[i * G + j], S.order.p + S.seg[j],
+                                   (size_t)S.part_n(j) * 4)))
+                    return rc;
+            }
+            pbase += nj;
         }
-        const double t2 = now_ms();
-        // ---- rows back in publish order (home device)
-        if ((rc = b->counts_o.reserve(std::max<size_t>(n, 1)))) return rc;
-        if ((rc = b->src_off.reserve((size_t)n + 1))) return rc;
-        if ((rc = b->dst_off.reserve((size_t)n + 1))) return rc;
-        if ((rc = b->src_bs.reserve(scan_block_count(n) + 1))) return rc;
-        if ((rc = b->dst_bs.reserve(scan_block_count(n) + 1))) return rc;
-        if ((rc = b->rowg.reserve((size_t)n + 1))) return rc;
-        if ((rc = b->out.reserve(std::max<uint64_t>(total, 1)))) return rc;
         SH_HIP(hipSetDevice(home));
-        SH_HIP(launch_unpart_counts(b->order.p, b->counts_p.p, n, b->counts_o.p, s));
-        ScanArgs ss{};
-        ss.count = b->counts_p.p; ss.row_off = b->src_off.p; ss.block_sums = b->src_bs.p; ss.n = n;
-        SH_HIP(launch_scan(ss, s, nullptr));
+        SH_HIP(launch_unpart_counts(b->gorder.p, b->counts_p.p, n, b->counts_o.p, s));
+        ScanArgs ss_{};
+        ss_.count = b->counts_p.p; ss_.row_off = b->src_off.p; ss_.block_sums = b->src_bs.p; ss_.n = n;
+        SH_HIP(launch_scan(ss_, s, nullptr));
         ScanArgs sd{};
         sd.count = b->counts_o.p; sd.row_off = b->dst_off.p; sd.block_sums = b->dst_bs.p; sd.n = n;
         SH_HIP(launch_scan(sd, s, nullptr));
-        SH_HIP(launch_unpart_rows(b->order.p, b->counts_p.p, n, b->src_off.p, b->src_bs.p, b->dst_off.p, b->dst_bs.p,
+        SH_HIP(launch_unpart_rows(b->gorder.p, b->counts_p.p, n, b->src_off.p, b->src_bs.p, b->dst_off.p, b->dst_bs.p,
                                   b->ids_p.p, b->out.p, b->rowg.p, s));
         SH_HIP(hipStreamSynchronize(s));
-        const double t3 = now_ms();
-        b->ms_partition = (float)(t1 - t0);
-        b->ms_parts = (float)(t2 - t1);
-        b->ms_unpartition = (float)(t3 - t2);
-        b->st.topics = n;
-        b->total = total;
-        b->done = true;
+        b->ms_unpartition = (float)(now_ms() - t0);
+        b->ordered = true;
+        return TM_OK;
+    }
+
+    // device pointers of the publish-order CSR (built on first use)
+    int device_csr(tm_sharded_batch* b, const uint32_t** d_row, const uint32_t** d_ids) {
+        if (G == 1) {   // one shard: the part's own CSR, global id = local id
+            uint64_t m = 0;
+            return tm_batch_device_csr(sh[0], b->part[0], d_row, d_ids, &m);
+        }
+        int rc = order_rows(b);
+        if (rc) return rc;
+        *d_row = b->rowg.p;
+        *d_ids = b->out.p;
         return TM_OK;
     }
 };
@@ -386,6 +629,8 @@ int tm_sharded_create(const int32_t* devices, uint32_t n, const tm_config* cfg, 
     if (!s) return TM_ENOMEM;
     s->G = n;
     s->home = devices[0];
+    s->ss.assign(n, nullptr);
+    for (auto* v : {&s->ev_p0, &s->ev_p1, &s->ev_x0, &s->ev_x1, &s->ev_done}) v->assign(n, nullptr);
     for (uint32_t i = 0; i < n; ++i) {
         tm_config c = cfg ? *cfg : tm_config{0, 0, 0, 0};
         c.device = devices[i];
@@ -399,7 +644,19 @@ int tm_sharded_create(const int32_t* devices, uint32_t n, const tm_config* cfg, 
         s->sh.push_back(e);
         s->dev.push_back(devices[i]);
     }
-    if (hipSetDevice(s->home) != hipSuccess || hipStreamCreateWithFlags(&s->s, hipStreamNonBlocking) != hipSuccess) {
+    // every shard copies parts to every other: open the links both ways
+    s->link.assign((size_t)n * n, TM_LINK_SAME);
+    for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t j = i; j < n; ++j) s->link[i * n + j] = s->link[j * n + i] = open_link(devices[i], devices[j]);
+    bool ok = hipSetDevice(s->home) == hipSuccess && hipStreamCreateWithFlags(&s->s, hipStreamNonBlocking) == hipSuccess;
+    for (uint32_t g = 0; ok && g < n; ++g) {
+        ok = hipSetDevice(devices[g]) == hipSuccess &&
+             hipStreamCreateWithFlags(&s->ss[g], hipStreamNonBlocking) == hipSuccess;
+        for (auto* v : {&s->ev_p0, &s->ev_p1, &s->ev_x0, &s->ev_x1, &s->ev_done})
+            ok = ok && hipEventCreate(&(*v)[g]) == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
         tm_sharded_destroy(s);
         return TM_EIO;
     }
@@ -415,11 +672,25 @@ void tm_sharded_destroy(tm_sharded* s) {
         (void)hipStreamSynchronize(s->s);
         (void)hipStreamDestroy(s->s);
     }
+    for (size_t g = 0; g < s->ss.size() && g < s->dev.size(); ++g) {
+        (void)hipSetDevice(s->dev[g]);
+        if (s->ss[g]) {
+            (void)hipStreamSynchronize(s->ss[g]);
+            (void)hipStreamDestroy(s->ss[g]);
+        }
+        for (auto* v : {&s->ev_p0, &s->ev_p1, &s->ev_x0, &s->ev_x1, &s->ev_done})
+            if ((*v)[g]) (void)hipEventDestroy((*v)[g]);
+    }
     for (tm_engine* e : s->sh) tm_destroy(e);
     delete s;
 }
 
 uint32_t tm_sharded_size(tm_sharded* s) { return s ? s->G : 0; }
+
+int tm_sharded_link(tm_sharded* s, uint32_t i, uint32_t j) {
+    if (!s || i >= s->G || j >= s->G) return TM_EINVAL;
+    return s->link[i * s->G + j];
+}
 
 tm_engine* tm_sharded_engine(tm_sharded* s, uint32_t shard) {
     return (s && shard < s->G) ? s->sh[shard] : nullptr;
@@ -543,12 +814,12 @@ int tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* off
     int rc;
     try {
         b->n = n;
-        b->done = false;
+        b->done = b->ordered = false;
         const uint64_t base = offsets[0];
         b->offs.assign(offsets, offsets + (size_t)n + 1);
         for (auto& o : b->offs) o -= base;
         b->bytes.assign(topics + base, topics + base + b->offs[n]);
-        rc = s->tokenize(b);
+        rc = s->plan(b);
     } catch (...) {
         rc = TM_ENOMEM;
     }
@@ -577,11 +848,11 @@ int tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out) {
     int rc;
     if ((rc = host_pinned(b->h_row, b->ch_row, (size_t)b->n + 1))) return rc;
     if ((rc = host_pinned(b->h_ids, b->ch_ids, std::max<uint64_t>(b->total, 1)))) return rc;
-    const uint32_t* d_row = b->rowg.p;
-    const uint32_t* d_ids = b->out.p;
-    if (b->direct) {   // one shard: the part's CSR (built here on first use)
-        uint64_t m = 0;
-        if ((rc = tm_batch_device_csr(s->sh[0], b->part[0], &d_row, &d_ids, &m))) return rc;
+    const uint32_t *d_row = nullptr, *d_ids = nullptr;
+    try {
+        if ((rc = s->device_csr(b, &d_row, &d_ids))) return rc;
+    } catch (...) {
+        return TM_ENOMEM;
     }
     SH_HIP(hipSetDevice(s->home));
     SH_HIP(hipMemcpyAsync(b->h_row, d_row, ((size_t)b->n + 1) * 4, hipMemcpyDeviceToHost, s->s));
@@ -601,23 +872,31 @@ int tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out) {
 int tm_sharded_device_csr(tm_sharded* s, tm_sharded_batch* b, const uint32_t** d_row_offsets, const uint32_t** d_ids,
                           uint64_t* n_matches) {
     if (!s || !b || !b->done) return TM_EINVAL;
-    if (b->direct) {
-        std::lock_guard<std::mutex> lk(s->mu);
-        return tm_batch_device_csr(s->sh[0], b->part[0], d_row_offsets, d_ids, n_matches);
+    std::lock_guard<std::mutex> lk(s->mu);
+    const uint32_t *r = nullptr, *i = nullptr;
+    int rc;
+    try {
+        rc = s->device_csr(b, &r, &i);
+    } catch (...) {
+        rc = TM_ENOMEM;
     }
-    if (d_row_offsets) *d_row_offsets = b->rowg.p;
-    if (d_ids) *d_ids = b->out.p;
+    if (rc) return rc;
+    if (d_row_offsets) *d_row_offsets = r;
+    if (d_ids) *d_ids = i;
     if (n_matches) *n_matches = b->total;
     return TM_OK;
 }
 
 int tm_sharded_batch_stats(tm_sharded* s, tm_sharded_batch* b, tm_sharded_stats* out) {
     if (!s || !b || !out) return TM_EINVAL;
+    memset(out, 0, sizeof *out);
     out->match = b->st;
     out->ms_partition = b->ms_partition;
-    out->ms_parts = b->ms_parts;
+    out->ms_exchange = b->ms_exchange;
+    out->ms_step = b->ms_step;
     out->ms_unpartition = b->ms_unpartition;
-    for (uint32_t g = 0; g < 64; ++g) out->part_topics[g] = g < s->G && !b->tseg.empty() ? b->tseg[g + 1] - b->tseg[g] : 0;
+    out->host_waits = b->host_waits;
+    for (uint32_t g = 0; g < 64; ++g) out->part_topics[g] = g < s->G && g < b->pn.size() ? b->pn[g] : 0;
     return TM_OK;
 }
 

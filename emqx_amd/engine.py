@@ -755,6 +755,16 @@ class ShardedBatch:
         N.check(self.grp.L.tm_sharded_run(self.grp.h, self.h), "tm_sharded_run")
         return self
 
+    def reprepare(self, topics):
+        """tm_sharded_prepare in place: new publishes (or the same ones again)."""
+        s = _pack(topics)
+        self.n = len(s)
+        self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        N.check(self.grp.L.tm_sharded_prepare(self.grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
+                                              C.byref(self.h)), "tm_sharded_prepare")
+        return self
+
     def result(self):
         r = N.Result()
         N.check(self.grp.L.tm_sharded_result(self.grp.h, self.h, C.byref(r)), "tm_sharded_result")
@@ -764,7 +774,8 @@ class ShardedBatch:
         st = N.ShardedStats()
         N.check(self.grp.L.tm_sharded_batch_stats(self.grp.h, self.h, C.byref(st)), "tm_sharded_batch_stats")
         out = st.match.asdict()
-        out.update(ms_partition=st.ms_partition, ms_parts=st.ms_parts, ms_unpartition=st.ms_unpartition,
+        out.update(ms_partition=st.ms_partition, ms_exchange=st.ms_exchange, ms_step=st.ms_step,
+                   ms_unpartition=st.ms_unpartition, host_waits=st.host_waits,
                    part_topics=list(st.part_topics)[:len(self.grp)])
         return out
 
@@ -810,6 +821,11 @@ class ShardedGroup:
 
     def __len__(self):
         return int(self.L.tm_sharded_size(self.h))
+
+    def link(self, i: int, j: int) -> str:
+        """How shard i's memory reaches shard j's device: same / peer / staged."""
+        return {N.TM_LINK_SAME: "same", N.TM_LINK_PEER: "peer", N.TM_LINK_STAGED: "staged"}[
+            N.check(self.L.tm_sharded_link(self.h, i, j), "tm_sharded_link")]
 
     def dict_load(self, words):
         s = _pack(words)

@@ -346,6 +346,25 @@ def gen_iot_filters(p: IotParams, lo: int = 0, hi: int = None) -> Strings:
     return _take(cs)
 
 
+def iot_device_ids(s: Strings) -> np.ndarray:
+    """The <X> of the second level d<X> of every IoT filter or topic (both
+    generators put a literal d<X> there), vectorised: int64[len(s)]."""
+    n = len(s)
+    if n == 0:
+        return np.zeros(0, np.int64)
+    buf = s.buf
+    slash = np.flatnonzero(buf == ord("/"))
+    first = np.searchsorted(slash, s.offs[:-1])          # index of each string's first '/'
+    a = slash[first] + 2                                  # after "/d"
+    b = slash[first + 1]                                  # the second '/'
+    out = np.zeros(n, np.int64)
+    for k in range(int((b - a).max())):
+        live = a + k < b
+        digit = buf[np.minimum(a + k, len(buf) - 1)].astype(np.int64) - ord("0")
+        out = np.where(live, out * 10 + digit, out)
+    return out
+
+
 def gen_iot_topics(p: IotParams, tseed: int, n: int) -> Strings:
     cs = _CStrs()
     cp = _ciot(p)

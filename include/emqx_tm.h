@@ -542,11 +542,14 @@ TM_API int  tm_group_rules_match(tm_group* g, const uint8_t* names, const uint64
  * first two levels are literal lives on shard tm_filter_shard(); all others
  * are replicated on every shard.  A publish is matched completely by its
  * owner shard (the shard of its first two words, or any shard when only
- * replicated filters can match it), so rows stay bit-exact.  One step over a
- * batch tokenised on the home device (devices[0]): owner per publish, a
- * stable partition by owner on the device, every shard matching its part,
- * and the rows restored to publish order with global filter ids (local id *
- * G + shard).  The shards' dictionaries grow only by the deltas of
+ * replicated filters can match it), so rows stay bit-exact.  A batch is cut
+ * into G contiguous slices, slice i tokenised on shard i's device at prepare.
+ * One step: every slice partitioned by owner on its own device, every shard
+ * receiving its parts (D2D, xGMI peer copies, or staged through pinned host
+ * memory) and walking them -- all queued, then ONE host wait.  The rows stay
+ * where each shard's walk wrote them; the publish-order CSR with global
+ * filter ids (local id * G + shard) is built on request (tm_sharded_result /
+ * tm_sharded_device_csr).  The shards' dictionaries grow only by the deltas of
  * tm_sharded_insert_many, so word ids agree everywhere.  Reference: the
  * replicated emqx_trie (src/emqx_trie.erl:53-74) matched in full by
  * match_routes/1 (src/emqx_router.erl:127-141); sharding it is new. */
@@ -554,14 +557,22 @@ typedef struct tm_sharded tm_sharded;
 typedef struct tm_sharded_batch tm_sharded_batch;
 typedef struct {
     tm_batch_stats match;     /* summed over the parts; ms_* = the slowest part */
-    float ms_partition;       /* host wall time: owner + partition kernels */
-    float ms_parts;           /* host wall time: parts prepared, matched, exported */
-    float ms_unpartition;     /* host wall time: rows back in publish order */
+    float ms_partition;       /* device time: owner + partition of a slice (the slowest) */
+    float ms_exchange;        /* device time: a shard receiving its parts (the slowest) */
+    float ms_step;            /* host wall time of the last tm_sharded_run */
+    float ms_unpartition;     /* host wall time: the publish-order CSR (on request) */
+    uint32_t host_waits;      /* blocking host waits in the last step: 1, + 1 per capacity relaunch */
     uint32_t part_topics[64]; /* publishes each shard matched */
 } tm_sharded_stats;
+/* how shard i's memory reaches shard j's device */
+#define TM_LINK_SAME   0      /* same device: D2D copies */
+#define TM_LINK_PEER   1      /* peer access enabled both ways (xGMI): peer copies */
+#define TM_LINK_STAGED 2      /* no peer access: copies staged through pinned host memory */
 TM_API int  tm_sharded_create(const int32_t* devices, uint32_t n_shards, const tm_config* cfg, tm_sharded** out);
 TM_API void tm_sharded_destroy(tm_sharded* s);
 TM_API uint32_t tm_sharded_size(tm_sharded* s);
+/* TM_LINK_* between shards i and j (TM_EINVAL out of range). */
+TM_API int  tm_sharded_link(tm_sharded* s, uint32_t i, uint32_t j);
 /* Shard g's engine (read-only use: stats, filter bytes of its local ids). */
 TM_API tm_engine* tm_sharded_engine(tm_sharded* s, uint32_t shard);
 /* Interns n words in order on every shard (tm_dict_load). */
@@ -577,11 +588,12 @@ TM_API int  tm_sharded_insert_many(tm_sharded* s, const uint8_t* filters, const 
  * owner, or all G for a replicated filter), as tm_sharded_insert_many counts. */
 TM_API int  tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                    uint64_t* n_deleted);
-/* A publish batch: bytes copied and tokenised on the home device.  A non-NULL
- * *out is re-prepared in place. */
+/* A publish batch: bytes copied, slice i tokenised on shard i's device and
+ * its parts counted (the plan of the exchange).  A non-NULL *out is
+ * re-prepared in place. */
 TM_API int  tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                tm_sharded_batch** out);
-/* One step (returns with the rows in the home device's HBM). */
+/* One step (returns with every shard's rows in its HBM; one host wait). */
 TM_API int  tm_sharded_run(tm_sharded* s, tm_sharded_batch* b);
 /* D2H of the step's CSR of global filter ids (memory valid like tm_result). */
 TM_API int  tm_sharded_result(tm_sharded* s, tm_sharded_batch* b, tm_result* out);

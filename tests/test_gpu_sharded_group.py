@@ -23,6 +23,18 @@ pytestmark = pytest.mark.gpu
 # this module never imports torch: the in-process sharded group is torch-free
 
 
+def _iot_candidates(p, topics):
+    """The IoT filters that can match any of `topics`: those whose second level
+    d<X> is a topic's (every IoT filter's and topic's second level is literal,
+    so no other filter can match them)."""
+    want = np.unique(gen.iot_device_ids(gen.Strings.from_list(topics)))
+    cand = []
+    for lo in range(0, p.n_filters, 5_000_000):
+        fl = gen.gen_iot_filters(p, lo, min(p.n_filters, lo + 5_000_000))
+        cand.extend(fl[int(i)] for i in np.flatnonzero(np.isin(gen.iot_device_ids(fl), want)))
+    return cand
+
+
 def rows_of(grp, offs, ids):
     cache = {}
 
@@ -49,8 +61,9 @@ def test_shards_on_one_device_with_online_dictionary_deltas(G):
     assert all(np.array_equal(tok[0].words, x.words) for x in tok[1:])
     b = grp.prepare(T)
     b.run()
-    offs, ids = b.result()
     st = b.stats()
+    assert st["host_waits"] == 1                 # the whole step behind one host wait
+    offs, ids = b.result()
     assert sum(st["part_topics"]) == len(T) and st["matches"] == len(ids)
     assert min(st["part_topics"]) > 0            # every shard owned publishes
     exp, _ = oracle_rows(F, T)
@@ -115,8 +128,9 @@ def test_c4_20m_iot_filters_two_shards_properties_and_oracle_sample():
     Ts = gen.gen_iot_topics(p, 4242, n)
     b = grp.prepare(Ts)
     b.run()
-    offs, ids = b.result()
     st = b.stats()
+    assert st["host_waits"] == 1
+    offs, ids = b.result()
     lens = np.diff(offs.astype(np.int64))
     # every row: offsets consistent, at most one filter of each IoT kind
     assert offs[0] == 0 and int(offs[-1]) == len(ids) == st["matches"] and (lens >= 0).all() and (lens <= 3).all()
@@ -129,15 +143,71 @@ def test_c4_20m_iot_filters_two_shards_properties_and_oracle_sample():
     T = Ts.tolist()
     sample = list(range(0, n, n // 3000))[:3000]
     ts = [T[i] for i in sample]
-    want = {t.split(b"/")[1] for t in ts}
-    cand = []
-    for lo in range(0, p.n_filters, 5_000_000):
-        for f in gen.gen_iot_filters(p, lo, lo + 5_000_000).tolist():
-            if f.split(b"/", 2)[1] in want:
-                cand.append(f)
+    cand = _iot_candidates(p, ts)
     exp, _ = oracle_rows(cand, ts)
     got = [[grp.filter_bytes(int(x)) for x in ids[offs[i]:offs[i + 1]]] for i in sample]
     assert_same(ts, got, exp)
     assert sum(len(r) for r in exp) > 300        # the sample exercises real matches
+    b.free()
+    grp.close()
+
+
+def test_staged_links_and_three_shards(monkeypatch):
+    """Parts copied through pinned host memory (the path taken when two
+    devices cannot reach each other's memory), forced on one device by
+    TM_SHARD_STAGED; and three shards: every row equals the oracle's, one host
+    wait per step, the result identical to the same-device links'."""
+    F, T, vocab = workload(43)
+    exp, _ = oracle_rows(F, T)
+    res = {}
+    for mode in ("same", "staged"):
+        if mode == "staged":
+            monkeypatch.setenv("TM_SHARD_STAGED", "1")
+        grp = ShardedGroup([0, 0, 0])
+        monkeypatch.delenv("TM_SHARD_STAGED", raising=False)
+        assert grp.link(0, 1) == mode and grp.link(2, 2) == mode
+        grp.dict_load(vocab)
+        grp.insert_many(F)
+        b = grp.prepare(T)
+        for _ in range(2):                      # a second step over the same plan
+            b.run()
+            assert b.stats()["host_waits"] == 1
+        offs, ids = b.result()
+        got = rows_of(grp, offs, ids)
+        assert_same(T, got, exp)
+        res[mode] = got
+        b.free()
+        grp.close()
+    assert res["same"] == res["staged"]
+
+
+def test_c4_100m_iot_filters_one_shard_properties_and_oracle_sample():
+    """BASELINE config C4's full filter count (100M IoT filters) on one shard:
+    CSR properties on every row and 3,000 rows against the oracle over the
+    filters that can match them."""
+    p = gen.C4
+    grp = ShardedGroup([0])
+    grp.dict_load(gen.gen_iot_vocab(p))
+    inserted = 0
+    for lo in range(0, p.n_filters, 5_000_000):
+        inserted += grp.insert_many(gen.gen_iot_filters(p, lo, lo + 5_000_000))
+    assert inserted == p.n_filters
+    n = 2_000_000
+    Ts = gen.gen_iot_topics(p, 4343, n)
+    b = grp.prepare(Ts)
+    b.run()
+    st = b.stats()
+    assert st["host_waits"] == 1
+    offs, ids = b.result()
+    lens = np.diff(offs.astype(np.int64))
+    assert offs[0] == 0 and int(offs[-1]) == len(ids) == st["matches"] and (lens >= 0).all() and (lens <= 3).all()
+    assert st["matches"] > n // 2                 # 100M filters over 10M ids: most topics match something
+    T = Ts.tolist()
+    sample = list(range(0, n, n // 3000))[:3000]
+    ts = [T[i] for i in sample]
+    exp, _ = oracle_rows(_iot_candidates(p, ts), ts)
+    got = [[grp.filter_bytes(int(x)) for x in ids[offs[i]:offs[i + 1]]] for i in sample]
+    assert_same(ts, got, exp)
+    assert sum(len(r) for r in exp) > 1000
     b.free()
     grp.close()

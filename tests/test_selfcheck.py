@@ -90,3 +90,13 @@ def test_a_wrong_row_on_one_rank_is_caught():
     assert not v["parity_sample_ok"]
     assert v["slices"][0]["mismatches"] == 0 and v["slices"][1]["mismatches"] == 1
     assert v["mismatches"][0][0] == "rank 1"
+
+
+def test_iot_device_ids_vectorised():
+    """gen.iot_device_ids (the bench's and tests' candidate filter selection
+    for C4 samples) equals splitting every string in Python."""
+    p = replace(gen.C4, n_filters=50_000, n_ids=100_000)
+    for s in (gen.gen_iot_filters(p), gen.gen_iot_topics(p, 4001, 20_000)):
+        ids = gen.iot_device_ids(s)
+        assert ids.tolist() == [int(x.split(b"/")[1][1:]) for x in s.tolist()]
+    assert len(gen.iot_device_ids(gen.Strings.from_list([]))) == 0
