@@ -578,7 +578,8 @@ def run_coalesce(args, ws, rank, local, sync):
                       "mean_batch": (b1["requests"] - b0["requests"]) / max(b1["batches"] - b0["batches"], 1),
                       "recoveries": b1["recoveries"] - b0["recoveries"],
                       "host_us_per_batch": {k: (b1[k] - b0[k]) / max(b1["batches"] - b0["batches"], 1)
-                                            for k in ("us_launch", "us_wait", "us_deliver")}}
+                                            for k in ("us_launch", "us_wait", "us_deliver")},
+                      "inline_launches": b1["inline_launches"] - b0["inline_launches"]}
         log(f"[coalesce] {name}: {legs[name]}")
     out = {"metric": "emqx_trie:match/1 calls/sec, one call per publish (tm_match_async, 4096 in flight)",
            "value": legs["async"]["calls_per_s"], "unit": "calls/s", "n_gpus": 1, "steps": 1, "warmup": 1,
@@ -628,15 +629,18 @@ def run_dispatch(args, ws, rank, local, sync):
     b = eng.prepare(topics)
     for _ in range(max(args.warmup, 1)):
         b.launch().wait()
+        b.dispatch_rows_device()
         b.dispatch_device()
     if sync is not None:
         sync.barrier()
+    # one step = the match pipeline + the fan-out over the walk's rows as they
+    # lie in staging (TM_DISPATCH_ROWS: no dense CSR first), kept in HBM
     ms_match, ms_fill, ms_disp = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         b.launch().wait()
         td = time.perf_counter()
-        total, fill_ms, *_ = b.dispatch_device()
+        total, fill_ms = b.dispatch_rows_device()
         ms_disp.append(1e3 * (time.perf_counter() - td))
         ms_fill.append(fill_ms)
         ms_match.append(b.stats()["ms_total"])
@@ -644,6 +648,15 @@ def run_dispatch(args, ws, rank, local, sync):
     if sync is not None:
         sync.barrier()
         elapsed = sync.allmax(elapsed)
+    # the same with the publish-order CSR form (dense CSR built first)
+    csr_disp, csr_fill = [], []
+    for _ in range(args.steps):
+        b.launch().wait()
+        td = time.perf_counter()
+        tot2, f2, *_ = b.dispatch_device()
+        csr_disp.append(1e3 * (time.perf_counter() - td))
+        csr_fill.append(f2)
+    assert tot2 == total
     st = b.stats()
     n, m = len(topics), int(st["matches"])
     f_ms = float(np.mean(ms_fill))
@@ -673,6 +686,8 @@ def run_dispatch(args, ws, rank, local, sync):
         "deliveries_per_s": ws * total * args.steps / elapsed,
         "match_pipeline_ms": float(np.mean(ms_match)),
         "dispatch_ms": float(np.mean(ms_disp)),
+        "dispatch_form": "rows (TM_DISPATCH_ROWS: the walk's rows where they lie)",
+        "dispatch_csr": {"dispatch_ms": float(np.mean(csr_disp)), "fill_ms": float(np.mean(csr_fill))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "tm_fan_fill",
                      "kernel_ms": f_ms, "alg_bytes_per_launch": alg},

@@ -66,10 +66,12 @@ class Routes(C.Structure):
 class Deliveries(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_matches", C.c_uint64), ("n_deliveries", C.c_uint64),
                 ("row_offsets", C.POINTER(C.c_uint64)), ("match_offsets", C.POINTER(C.c_uint64)),
-                ("subscribers", C.POINTER(C.c_uint32)), ("fill_ms", C.c_float)]
+                ("subscribers", C.POINTER(C.c_uint32)), ("fill_ms", C.c_float),
+                ("row_counts", C.POINTER(C.c_uint32))]
 
 
 TM_DISPATCH_COUNT_ONLY = 1
+TM_DISPATCH_ROWS = 8
 TM_DISPATCH_MATCH_OFFSETS = 2
 TM_DISPATCH_DEVICE = 4
 
@@ -96,7 +98,8 @@ class EngineStats(C.Structure):
 class AsyncStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("requests", C.c_uint64), ("recoveries", C.c_uint64),
                 ("max_batch", C.c_uint64), ("depth", C.c_uint32), ("queued", C.c_uint32),
-                ("us_launch", C.c_double), ("us_wait", C.c_double), ("us_deliver", C.c_double)]
+                ("us_launch", C.c_double), ("us_wait", C.c_double), ("us_deliver", C.c_double),
+                ("inline_launches", C.c_uint64)]
 
     def asdict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

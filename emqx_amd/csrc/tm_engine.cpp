@@ -510,6 +510,8 @@ struct tm_batch {
     uint32_t* d_moff32 = nullptr;
     uint8_t* d_fbig = nullptr;
     size_t c_moff32 = 0, c_fbig = 0;
+    uint32_t* d_dcount = nullptr;   // TM_DISPATCH_ROWS: deliveries of each row
+    size_t c_dcount = 0;
     uint64_t *h_ftotal = nullptr, *h_drow = nullptr, *h_moff = nullptr;
     uint32_t *d_fout = nullptr, *h_fout = nullptr;
     size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0, c_ftile = 0;
@@ -517,7 +519,7 @@ struct tm_batch {
     hipEvent_t fev0 = nullptr, fev1 = nullptr;
 
     void release() {
-        dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
+        dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_dcount); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
         dev_free(d_ftile);
         for (uint64_t** h : {&h_ftotal, &h_drow, &h_moff}) {
             if (*h) (void)hipHostFree(*h);
@@ -708,7 +710,15 @@ struct Replica {
     // device works instead of trickling out as tiny batches
     uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // tools/ab_async.sh
     uint32_t a_spin_us = 0;   // completers poll a pinned flag this long before blocking on the event (0: off)
-    uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0;
+    // while batches are in flight and fewer than a_busy_min calls wait, the
+    // launcher gathers for at most this long, then launches what it has on a
+    // free slot (0: until the pipeline idles or a_busy_min calls queue).  Keeps
+    // a closed loop of blocking callers pipelined instead of one batch at a time.
+    uint32_t a_busy_wait_us = 40;
+    // a call that finds the queue empty and the whole pipeline idle launches
+    // its batch itself, on the calling thread (no launcher wake-up)
+    bool a_inline = true;
+    uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0, a_inline_launches = 0;
     // where the pipeline's time goes (host microseconds, summed over batches)
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
 };
@@ -2331,13 +2341,40 @@ struct tm_engine {
     // tm_batch_dispatch: deliveries of a waited batch, resolved on the device
     int batch_dispatch(tm_batch* b, uint32_t flags, tm_deliveries* out) {
         if (!b->done) return TM_EINVAL;
+        const bool rows = flags & TM_DISPATCH_ROWS;
+        if (rows && ((flags & TM_DISPATCH_MATCH_OFFSETS) || !b->csr)) return TM_EINVAL;
+        if (rows) flags |= TM_DISPATCH_DEVICE;
         Replica& R = *b->rep;
         const hipStream_t stream = R.stream;
         int rc;
-        if ((rc = ensure_dense(b))) return rc;
+        if (!rows && (rc = ensure_dense(b))) return rc;
         if ((rc = sync_subs(R))) return rc;
         const uint32_t n = b->n;
-        const uint64_t nm = b->total;
+        FanArgs fa{};
+        uint64_t nm = b->total;
+        if (rows) {   // the walk's staging regions as one virtual entry space (FanArgs)
+            const uint64_t cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
+            fa.nreg = b->one_region ? 1u : TICKET_GROUPS;
+            fa.rcap = region_cap(cap, b->one_region);
+            uint64_t v = 0, staged = 0;
+            for (uint32_t g = 0; g < fa.nreg; ++g) {
+                fa.vb[g] = v;
+                fa.rtop[g] = xg_top_read(b->h_ctrl, g);
+                staged += fa.rtop[g];
+                v += (fa.rtop[g] + 15) & ~15ull;
+            }
+            fa.vb[fa.nreg] = v;
+            if (staged != b->total) {
+                snprintf(last_error(), 512, "staging holds %llu entries, the walk matched %llu",
+                         (unsigned long long)staged, (unsigned long long)b->total);
+                return TM_EIO;
+            }
+            nm = v;
+            if ((rc = dev_reserve(b->d_dcount, b->c_dcount, std::max<size_t>(n, 1)))) return rc;
+            fa.rcount = b->d_count;
+            fa.rsrc = b->d_src;
+            fa.dcount = b->d_dcount;
+        }
         const uint32_t nb = (uint32_t)((nm + 1 + fan_scan_tile() - 1) / fan_scan_tile());
         if ((rc = dev_reserve(b->d_moff, b->c_moff, nm + 1))) return rc;
         if ((rc = dev_reserve(b->d_fbsums, b->c_fbsums, nb))) return rc;
@@ -2350,8 +2387,7 @@ struct tm_engine {
             HIP_OK(hipEventCreate(&b->fev0));
             HIP_OK(hipEventCreate(&b->fev1));
         }
-        FanArgs fa{};
-        fa.row_off = b->d_rowoff; fa.ids = b->d_ids; fa.n = n; fa.n_matches = nm;
+        fa.row_off = b->d_rowoff; fa.ids = rows ? b->d_sfids : b->d_ids; fa.n = n; fa.n_matches = nm;
         fa.soff = R.d_soff; fa.scnt = R.d_scnt; fa.sone = R.d_sone; fa.subs = R.d_subs; fa.nnodes = subs_nn;
         fa.moff = b->d_moff; fa.moff32 = b->d_moff32; fa.bbig = b->d_fbig; fa.bsums = b->d_fbsums;
         fa.big_limit = fan_big_limit; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
@@ -2372,8 +2408,9 @@ struct tm_engine {
         const bool want_moff = flags & TM_DISPATCH_MATCH_OFFSETS;
         if (want_moff) HIP_OK(launch_fan_globalize(fa, stream));   // moff is block-relative until now
         out->n_topics = n;
-        out->n_matches = nm;
+        out->n_matches = b->total;
         out->n_deliveries = total;
+        out->row_counts = nullptr;
         if (flags & TM_DISPATCH_DEVICE) {
             HIP_OK(hipStreamSynchronize(stream));
             if (!counts_only) HIP_OK(hipEventElapsedTime(&fill_ms, b->fev0, b->fev1));
@@ -2381,6 +2418,7 @@ struct tm_engine {
             out->match_offsets = want_moff ? b->d_moff : nullptr;
             out->subscribers = counts_only ? nullptr : b->d_fout;
             out->fill_ms = fill_ms;
+            out->row_counts = rows ? b->d_dcount : nullptr;
             return TM_OK;
         }
         if ((rc = host_reserve(b->h_drow, b->ch_drow, (size_t)n + 1))) return rc;
@@ -3358,7 +3396,7 @@ struct tm_engine {
             return TM_EIO;
         }
         a.sfids = b->d_sfids; a.sfids_cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
-        a.rcap = b->one_region ? a.sfids_cap : a.sfids_cap / TICKET_GROUPS;
+        a.rcap = region_cap(a.sfids_cap, b->one_region);
         a.sgmask = b->one_region ? 0u : TICKET_GROUPS - 1;
         a.xg = b->d_ctrl + XG_WORD;
         a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
@@ -3659,6 +3697,8 @@ struct tm_engine {
         if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) R.a_busy_min = (uint32_t)std::max(1, atoi(d));
         if (const char* d = getenv("TM_ASYNC_COMPLETERS")) R.a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
         if (const char* d = getenv("TM_ASYNC_SPIN_US")) R.a_spin_us = (uint32_t)std::min(10000, std::max(0, atoi(d)));
+        if (const char* d = getenv("TM_ASYNC_BUSY_WAIT_US")) R.a_busy_wait_us = (uint32_t)std::min(100000, std::max(0, atoi(d)));
+        if (const char* d = getenv("TM_ASYNC_INLINE")) R.a_inline = atoi(d) != 0;
         {
             std::lock_guard<std::recursive_mutex> g(mu);
             HIP_OK(hipSetDevice(R.device));
@@ -3746,6 +3786,15 @@ struct tm_engine {
             sh.calls.push_back(AsyncCall{cb, ctx});
         }
         const uint64_t q = R.q_count.fetch_add(1, std::memory_order_acq_rel) + 1;
+        if (q == 1 && R.a_inline) {   // the queue was empty: launch it here if the pipeline is idle
+            std::unique_lock<std::mutex> lk(R.amu, std::try_to_lock);
+            if (lk.owns_lock() && R.a_started && !R.a_stop && !R.a_free.empty() &&
+                R.a_free.size() == R.a_slots.size() && R.q_count.load(std::memory_order_acquire) > 0) {
+                ++R.a_inline_launches;
+                launch_locked(R, lk);
+                return TM_OK;
+            }
+        }
         if (q == 1 || q == R.a_busy_min || q == R.a_max) {   // the launcher may be waiting for this
             std::lock_guard<std::mutex> lk(R.amu);
             R.a_work.notify_one();
@@ -3753,14 +3802,19 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // moves exactly `take` queued calls (at least that many are queued) into the slot
+    // moves exactly `take` queued calls into the slot: the caller reserved
+    // them (took them off q_count under amu), and a call is in its shard before
+    // it is counted, so at least that many are there beyond other drainers'
+    // reservations -- passes repeat until all are found
     void drain_queue(Replica& R, AsyncSlot* sl, size_t take) {
         constexpr uint32_t QSHARDS = Replica::QSHARDS;
         sl->calls.clear();
         sl->bytes.clear();
         sl->offs.assign(1, 0);
         static thread_local uint32_t start = 0;
-        for (uint32_t k = 0; k < QSHARDS && sl->calls.size() < take; ++k) {
+        for (uint32_t k = 0; sl->calls.size() < take; ++k) {
+            if (k && k % QSHARDS == 0) std::this_thread::yield();   // another drainer is mid-shard
+
             Replica::QShard& sh = R.qs[(start + k) % QSHARDS];
             std::lock_guard<std::mutex> g(sh.mu);
             size_t h = sh.head, hb = sh.head_bytes;
@@ -3783,7 +3837,30 @@ struct tm_engine {
             }
         }
         start = (start + 1) % QSHARDS;   // no shard is always last
-        R.q_count.fetch_sub(sl->calls.size(), std::memory_order_acq_rel);
+    }
+
+    // amu held (lk): a free slot takes up to a_max queued calls and is
+    // launched; amu is released while the batch is built and launched
+    void launch_locked(Replica& R, std::unique_lock<std::mutex>& lk) {
+        AsyncSlot* sl = R.a_free.back();
+        R.a_free.pop_back();
+        const size_t take =
+            std::min<uint64_t>(R.q_count.load(std::memory_order_acquire), std::max<uint32_t>(R.a_max, 1));
+        R.q_count.fetch_sub(take, std::memory_order_acq_rel);   // reserved: no other drainer counts on them
+        lk.unlock();
+        drain_queue(R, sl, take);
+        const auto t0 = std::chrono::steady_clock::now();
+        try {
+            sl->rc = slot_launch(sl);
+        } catch (...) {
+            sl->rc = TM_ENOMEM;
+        }
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        lk.lock();
+        R.a_max_seen = std::max<uint64_t>(R.a_max_seen, sl->calls.size());
+        R.a_us_launch += us;
+        R.a_inflight.push_back(sl);
+        R.a_done.notify_all();
     }
 
     // Forms batches from the queue: everything queued while the pipeline was
@@ -3791,34 +3868,30 @@ struct tm_engine {
     void launcher_loop(Replica& R) {
         (void)hipSetDevice(R.device);
         std::unique_lock<std::mutex> lk(R.amu);
+        auto queued = [&] { return R.q_count.load(std::memory_order_acquire); };
         for (;;) {
             R.a_work.wait(lk, [&] {
-                const uint64_t q = R.q_count.load(std::memory_order_acquire);
-                if (R.a_stop) return q == 0 || !R.a_free.empty();
-                const bool idle = R.a_free.size() == R.a_slots.size();
-                return q && !R.a_free.empty() && (idle || q >= R.a_busy_min);
+                if (R.a_stop) return queued() == 0 || !R.a_free.empty();
+                return queued() && !R.a_free.empty();
             });
-            if (R.q_count.load(std::memory_order_acquire) == 0) break;   // stopping, queue drained
-            if (R.a_linger_us && !R.a_stop && R.q_count.load() < R.a_max)
-                R.a_work.wait_for(lk, std::chrono::microseconds(R.a_linger_us),
-                                [&] { return R.a_stop || R.q_count.load() >= R.a_max; });
-            AsyncSlot* sl = R.a_free.back();
-            R.a_free.pop_back();
-            const size_t take = std::min<uint64_t>(R.q_count.load(std::memory_order_acquire), std::max<uint32_t>(R.a_max, 1));
-            lk.unlock();
-            drain_queue(R, sl, take);
-            const auto t0 = std::chrono::steady_clock::now();
-            try {
-                sl->rc = slot_launch(sl);
-            } catch (...) {
-                sl->rc = TM_ENOMEM;
+            if (queued() == 0) {
+                if (R.a_stop) break;   // stopping, queue drained
+                continue;              // an inline launch took the calls
             }
-            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-            lk.lock();
-            R.a_max_seen = std::max<uint64_t>(R.a_max_seen, sl->calls.size());
-            R.a_us_launch += us;
-            R.a_inflight.push_back(sl);
-            R.a_done.notify_all();
+            if (!R.a_stop && R.a_free.size() != R.a_slots.size() && queued() < R.a_busy_min) {
+                // batches in flight, few calls queued: gather more for a while
+                auto enough = [&] {
+                    return R.a_stop || R.a_free.size() == R.a_slots.size() || queued() >= R.a_busy_min;
+                };
+                if (R.a_busy_wait_us) R.a_work.wait_for(lk, std::chrono::microseconds(R.a_busy_wait_us), enough);
+                else R.a_work.wait(lk, enough);
+                if (R.a_free.empty() || queued() == 0) continue;
+            }
+            if (R.a_linger_us && !R.a_stop && queued() < R.a_max)
+                R.a_work.wait_for(lk, std::chrono::microseconds(R.a_linger_us),
+                                  [&] { return R.a_stop || queued() >= R.a_max; });
+            if (R.a_free.empty() || queued() == 0) continue;
+            launch_locked(R, lk);
         }
         R.a_launcher_done = true;
         R.a_done.notify_all();
@@ -3860,7 +3933,7 @@ struct tm_engine {
         x.rows = b->d_sfids;
         x.h_rows = reinterpret_cast<uint32_t*>(d_rows);
         x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
-        x.rcap = std::min<uint64_t>(b->c_sfids, MAX_RESULT) / (b->one_region ? 1 : TICKET_GROUPS);
+        x.rcap = region_cap(std::min<uint64_t>(b->c_sfids, MAX_RESULT), b->one_region);
         HIP_OK(launch_export_host(x, S));
         if (b->rep->a_spin_us) {
             if (!sl->h_flag) {
@@ -4546,6 +4619,7 @@ int tm_async_stats_get(tm_engine* e, tm_async_stats* out) {
         out->us_launch += R->a_us_launch;
         out->us_wait += R->a_us_wait;
         out->us_deliver += R->a_us_deliver;
+        out->inline_launches += R->a_inline_launches;
     }
     return TM_OK;
 }

@@ -239,7 +239,26 @@ struct FanArgs {
     uint32_t* out;            // subscriber of delivery p
     uint64_t total;
     uint64_t* tile_j;         // total / fan_fill_tile() + 2: match entry of each fill tile's first delivery
+    // Rows mode (TM_DISPATCH_ROWS): the entries are the walk's staging, read
+    // where it was written.  Staging region g holds rtop[g] entries from
+    // g * rcap; entry j of the virtual entry space [0, vb[nreg]) is region g's
+    // entry j - vb[g] (vb[g] a multiple of 16, entries past rtop[g] padding
+    // with no deliveries), so a row -- contiguous in its region -- is
+    // contiguous here too.  nreg = 0: ids is the match CSR.
+    uint32_t nreg;
+    uint64_t rcap;            // a multiple of 16 (region_cap)
+    uint64_t vb[TICKET_GROUPS + 1];
+    uint64_t rtop[TICKET_GROUPS];
+    const uint32_t* rcount;   // n: the walk's row lengths (tm_batch_rows)
+    const unsigned long long* rsrc;   // n: the rows' first staging entries
+    uint32_t* dcount;         // n: deliveries of each row (drow = its first)
 };
+
+// staging region capacity of a launch: a multiple of 16 entries per region so
+// the fan-out's rows mode reads 16-entry chunks aligned and in bounds
+__host__ __device__ inline uint64_t region_cap(uint64_t sfids_cap, bool one_region) {
+    return (one_region ? sfids_cap : sfids_cap / TICKET_GROUPS) & ~15ull;
+}
 
 // Batched emqx_topic:match/2 (tm_rules_match): names x rules -> bitmap.
 struct RulesArgs {

@@ -1253,12 +1253,21 @@ __device__ inline uint64_t fan_moff(const FanArgs& a, uint64_t j) {
     return (big ? a.moff[j] : (uint64_t)m32) + bs;
 }
 
-__device__ inline uint64_t fan_count(const FanArgs& a, uint64_t j) {
-    if (j >= a.n_matches) return 0;
-    const uint32_t f = a.ids[j];
-    if (f >= a.nnodes) return 0;
-    const uint32_t c = a.scnt[f];   // 1 B per node: the gather's footprint stays L2-sized
-    return c < 255 ? c : a.soff[f + 1] - a.soff[f];
+// Rows mode: region of virtual entry j (vb[0] = 0, vb ascending)
+__device__ __forceinline__ uint32_t fan_region(const FanArgs& a, uint64_t j) {
+    uint32_t g = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < TICKET_GROUPS; ++k) g += (k < a.nreg && j >= a.vb[k]) ? 1u : 0u;
+    return g;
+}
+
+// filter id of entry j (rows mode: the staging entry behind it; padding ->
+// nnodes, i.e. no deliveries)
+__device__ __forceinline__ uint32_t fan_fid(const FanArgs& a, uint64_t j) {
+    if (!a.nreg) return a.ids[j];
+    const uint32_t g = fan_region(a, j);
+    const uint64_t o = j - a.vb[g];
+    return o < a.rtop[g] ? a.ids[g * a.rcap + o] : a.nnodes;
 }
 
 // Exclusive scan of one u64 per thread over a 256-thread block (4 waves).
@@ -1291,16 +1300,30 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
     // block scan per chunk); ids and offsets move as 16-B vectors
     const uint64_t j0 = (uint64_t)blockIdx.x * FAN_SCAN_TILE + (uint64_t)threadIdx.x * FAN_PER;
     uint32_t f[FAN_PER];
+    // rows mode: the 16 entries lie in one region (its virtual base and the
+    // region stride are multiples of 16), so they are one aligned chunk of
+    // staging; entries past the region's top are padding
+    const uint32_t* src = a.ids + j0;
+    uint64_t valid = a.n_matches > j0 ? a.n_matches - j0 : 0;
+    if (a.nreg && valid) {
+        const uint32_t g = fan_region(a, j0);
+        const uint64_t o = j0 - a.vb[g];
+        src = a.ids + g * a.rcap + o;
+        valid = a.rtop[g] > o ? min<uint64_t>(valid, a.rtop[g] - o) : 0;
+    }
     if (j0 + FAN_PER <= a.n_matches) {
-        const uint4* q = reinterpret_cast<const uint4*>(a.ids + j0);   // j0 % 16 == 0: 64-B aligned
+        const uint4* q = reinterpret_cast<const uint4*>(src);   // 64-B aligned
 #pragma unroll
         for (uint32_t k = 0; k < FAN_PER / 4; ++k) {
             const uint4 v = q[k];
             f[4 * k] = v.x; f[4 * k + 1] = v.y; f[4 * k + 2] = v.z; f[4 * k + 3] = v.w;
         }
+#pragma unroll
+        for (uint32_t k = 0; k < FAN_PER; ++k)
+            if (k >= valid) f[k] = a.nnodes;
     } else {
 #pragma unroll
-        for (uint32_t k = 0; k < FAN_PER; ++k) f[k] = j0 + k < a.n_matches ? a.ids[j0 + k] : a.nnodes;
+        for (uint32_t k = 0; k < FAN_PER; ++k) f[k] = k < valid ? src[k] : a.nnodes;
     }
     uint64_t c[FAN_PER], mine = 0;
 #pragma unroll
@@ -1392,6 +1415,24 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_rows(FanArgs a) {
     if (i <= a.n) a.drow[i] = fan_moff(a, a.row_off[i]);
 }
 
+// rows mode: the deliveries of publish i's row, read where the walk left it
+// (count, first staging entry): first delivery and count
+__global__ __launch_bounds__(FAN_BLOCK) void tm_fan_rows_stg(FanArgs a) {
+    const uint32_t i = blockIdx.x * FAN_BLOCK + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t c = a.rcount[i];
+    uint64_t d0 = 0, dn = 0;
+    if (c) {
+        const uint64_t s = a.rsrc[i];
+        const uint32_t g = a.nreg > 1 ? (uint32_t)(s / a.rcap) : 0u;
+        const uint64_t v = a.vb[g] + (s - g * a.rcap);
+        d0 = fan_moff(a, v);
+        dn = fan_moff(a, v + c) - d0;
+    }
+    a.drow[i] = d0;
+    a.dcount[i] = (uint32_t)dn;
+}
+
 // first j in [lo, hi) with moff[j] > p (hi if none)
 __device__ inline uint64_t fan_upper(const FanArgs& a, uint64_t lo, uint64_t hi, uint64_t p) {
     while (lo < hi) {
@@ -1436,7 +1477,7 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
         uint64_t j = jlo;
         for (uint64_t p = start + t; p < end; p += FAN_BLOCK) {
             j = fan_upper(a, j, jhi + 1, p) - 1;
-            a.out[p] = a.subs[a.soff[a.ids[j]] + (p - fan_moff(a, j))];
+            a.out[p] = a.subs[a.soff[fan_fid(a, j)] + (p - fan_moff(a, j))];
         }
         return;
     }
@@ -1473,7 +1514,7 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
                 const uint64_t j = jlo + e;
                 m0[u] = moff_at(j);
                 m1[u] = moff_at(j + 1);
-                f[u] = a.ids[j];
+                f[u] = fan_fid(a, j);
             }
         }
         int64_t v[FAN_STG];
@@ -2386,7 +2427,11 @@ hipError_t launch_fan_scan(const FanArgs& a, hipStream_t s) {
     const uint32_t nb = (uint32_t)((ne + FAN_SCAN_TILE - 1) / FAN_SCAN_TILE);
     hipLaunchKernelGGL(tm_fan_scan_local, dim3(nb), dim3(FAN_BLOCK), 0, s, a);
     hipLaunchKernelGGL(tm_fan_scan_sums, dim3(1), dim3(FAN_BLOCK), 0, s, a, nb);
-    hipLaunchKernelGGL(tm_fan_rows, dim3((a.n + 1 + FAN_BLOCK - 1) / FAN_BLOCK), dim3(FAN_BLOCK), 0, s, a);
+    if (a.nreg) {
+        if (a.n) hipLaunchKernelGGL(tm_fan_rows_stg, dim3((a.n + FAN_BLOCK - 1) / FAN_BLOCK), dim3(FAN_BLOCK), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(tm_fan_rows, dim3((a.n + 1 + FAN_BLOCK - 1) / FAN_BLOCK), dim3(FAN_BLOCK), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -125,6 +125,27 @@ class Batch:
         ptr = lambda p: C.cast(p, C.c_void_p).value  # noqa: E731
         return int(d.n_deliveries), float(d.fill_ms), ptr(d.row_offsets), ptr(d.match_offsets), ptr(d.subscribers)
 
+    def dispatch_rows(self):
+        """Fan-out over the walk's rows as it left them (TM_DISPATCH_ROWS), copied
+        to the host for checking: (first delivery u64[n], deliveries u32[n],
+        subscribers u32[total]); row i's deliveries are
+        subscribers[first[i] : first[i] + count[i]]."""
+        d = self._dispatch(N.TM_DISPATCH_ROWS)
+        n, t = d.n_topics, int(d.n_deliveries)
+        first = np.zeros(n, np.uint64)
+        cnt = np.zeros(n, np.uint32)
+        subs = np.zeros(t, np.uint32)
+        ptr = lambda p: C.cast(p, C.c_void_p).value  # noqa: E731
+        _d2h(first, ptr(d.row_offsets))
+        _d2h(cnt, ptr(d.row_counts))
+        _d2h(subs, ptr(d.subscribers))
+        return first, cnt, subs
+
+    def dispatch_rows_device(self):
+        """TM_DISPATCH_ROWS kept in HBM: -> (n_deliveries, fill kernel ms)."""
+        d = self._dispatch(N.TM_DISPATCH_ROWS)
+        return int(d.n_deliveries), float(d.fill_ms)
+
     def _dispatch(self, flags: int) -> "N.Deliveries":
         d = N.Deliveries()
         N.check(self.eng.L.tm_batch_dispatch(self.eng.h, self.h, flags, C.byref(d)), "tm_batch_dispatch")

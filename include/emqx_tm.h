@@ -204,6 +204,7 @@ typedef struct {
     double   us_launch;     /* host time forming + enqueueing batches (launcher thread) */
     double   us_wait;       /* completer time blocked on device batches */
     double   us_deliver;    /* completer time running callbacks */
+    uint64_t inline_launches; /* batches a submitting caller launched itself (pipeline idle) */
 } tm_async_stats;
 TM_API int  tm_async_stats_get(tm_engine* e, tm_async_stats* out);
 
@@ -355,19 +356,27 @@ TM_API int  tm_subscriber_down(tm_engine* e, uint32_t subscriber, uint32_t node_
  * batch, valid until its next dispatch or re-prepare (match_offsets only with
  * TM_DISPATCH_MATCH_OFFSETS too: without it the engine skips making them
  * global).  Otherwise engine-owned
- * pinned memory valid likewise.  fill_ms = device time of the copy kernel. */
+ * pinned memory valid likewise.  fill_ms = device time of the copy kernel.
+ * TM_DISPATCH_ROWS (device only, implies TM_DISPATCH_DEVICE, excludes
+ * MATCH_OFFSETS): the fan-out reads the walk's rows where it wrote them
+ * (tm_batch_rows) instead of a dense CSR built first; the deliveries of row i
+ * are then subscribers[row_offsets[i] .. row_offsets[i] + row_counts[i]) --
+ * the same runs in the same order, rows no longer adjacent in publish order
+ * (row_offsets has n_topics entries). */
 typedef struct {
     uint32_t        n_topics;
     uint64_t        n_matches;
     uint64_t        n_deliveries;
-    const uint64_t* row_offsets;    /* n_topics + 1 */
+    const uint64_t* row_offsets;    /* n_topics + 1 (TM_DISPATCH_ROWS: n_topics row starts) */
     const uint64_t* match_offsets;  /* n_matches + 1, or NULL */
     const uint32_t* subscribers;    /* n_deliveries, or NULL */
     float           fill_ms;
+    const uint32_t* row_counts;     /* TM_DISPATCH_ROWS: deliveries of each row; otherwise NULL */
 } tm_deliveries;
 #define TM_DISPATCH_COUNT_ONLY    1u
 #define TM_DISPATCH_MATCH_OFFSETS 2u
 #define TM_DISPATCH_DEVICE        4u
+#define TM_DISPATCH_ROWS          8u
 TM_API int  tm_batch_dispatch(tm_engine* e, tm_batch* b, uint32_t flags, tm_deliveries* out);
 
 /* ---- bulk load + filter-sharded mode ------------------ */

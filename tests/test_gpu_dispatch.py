@@ -19,6 +19,17 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+def assert_rows_mode_equal(b, offs, out):
+    """TM_DISPATCH_ROWS (the fan-out over the walk's rows where they lie, no
+    dense CSR first) gives every publish the same deliveries, in the same
+    order, as the CSR form."""
+    first, cnt, subs = b.dispatch_rows()
+    assert len(subs) == int(offs[-1])
+    assert np.array_equal(cnt.astype(np.uint64), np.diff(offs))
+    for i in range(len(cnt)):
+        assert np.array_equal(subs[int(first[i]):int(first[i]) + int(cnt[i])], out[offs[i]:offs[i + 1]]), i
+
+
 def test_kat_broker_on_device():
     kat = load_golden("kat_broker.json")
     for case in kat["cases"]:
@@ -86,6 +97,7 @@ def test_dispatch_skewed_fanout_and_modes(big, monkeypatch):
     assert total == int(offs[-1]) and d_moff
     offs2, moff2, out2 = b.dispatch(match_offsets=True)        # re-dispatch: offsets made global once
     assert np.array_equal(moff2, moff) and np.array_equal(offs2, offs) and np.array_equal(out2, out)
+    assert_rows_mode_equal(b, offs, out)
     names = [eng.filter_bytes(int(i)) for i in ids]
     for i, t in enumerate(T):
         exp = []
@@ -155,6 +167,7 @@ def test_dispatch_sparse_subscribers_take_the_search_path():
                 assert int(moff[j]) == offs[i] + len(exp)
                 exp.extend(subs.get(names[j], []))
             assert np.array_equal(out[offs[i]:offs[i + 1]], np.asarray(exp, np.uint32)), T[i]
+        assert_rows_mode_equal(b, offs, out)
         b.free()
         return int(offs[-1]), len(ids)
     nd, nm = check()
@@ -164,3 +177,29 @@ def test_dispatch_sparse_subscribers_take_the_search_path():
         eng.subscribe(b"#", s)
     nd, nm = check()
     assert nd > nm                                   # dense: staged path
+
+
+def test_dispatch_rows_mode_with_generic_path_rows():
+    """Rows mode over staging that also holds the generic path's rows: topics
+    deeper than the fast path and rows longer than K (a topic matching every
+    literal/'+'/'#' combination of 8 levels: 511 filters)."""
+    import itertools
+    lit = [b"a", b"b", b"c", b"d", b"e", b"f", b"g", b"h"]
+    F = []
+    for k in range(len(lit) + 1):
+        for pick in itertools.product((0, 1), repeat=k):
+            ws = [lit[i] if pick[i] == 0 else b"+" for i in range(k)]
+            F.append(b"/".join(ws + ([b"#"] if k < len(lit) else [])))
+    F = sorted(set(F))
+    eng = Engine(device=0)
+    for j, f in enumerate(F):
+        for q in range(j % 3):
+            eng.subscribe(f, 100 * j + q)
+    deep = b"/".join(lit + [b"x"] * 6)
+    T = [b"a/b/c/d/e/f/g/h", deep, b"a/b", b"zz", b"a/b/c/d/e/f/g/h/i/j/k/l"] * 300
+    b = eng.prepare(T)
+    b.launch().wait()
+    assert b.stats()["slow_topics"] > 0
+    offs, _, out = b.dispatch()
+    assert_rows_mode_equal(b, offs, out)
+    b.free()
