@@ -512,6 +512,8 @@ struct tm_batch {
     size_t c_moff32 = 0, c_fbig = 0;
     uint32_t* d_dcount = nullptr;   // TM_DISPATCH_ROWS: deliveries of each row
     size_t c_dcount = 0;
+    uint64_t *d_fmeta = nullptr, *h_fmeta = nullptr;   // TM_DISPATCH_ROWS: staging regions (vb, rtop)
+    size_t c_fmeta = 0, ch_fmeta = 0;
     uint64_t *h_ftotal = nullptr, *h_drow = nullptr, *h_moff = nullptr;
     uint32_t *d_fout = nullptr, *h_fout = nullptr;
     size_t c_moff = 0, c_fbsums = 0, c_ftotal = 0, c_drow = 0, c_fout = 0, c_ftile = 0;
@@ -519,7 +521,9 @@ struct tm_batch {
     hipEvent_t fev0 = nullptr, fev1 = nullptr;
 
     void release() {
-        dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_dcount); dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
+        dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_dcount); dev_free(d_fmeta);
+        if (h_fmeta) (void)hipHostFree(h_fmeta);
+        h_fmeta = nullptr; dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
         dev_free(d_ftile);
         for (uint64_t** h : {&h_ftotal, &h_drow, &h_moff}) {
             if (*h) (void)hipHostFree(*h);
@@ -712,9 +716,11 @@ struct Replica {
     uint32_t a_spin_us = 0;   // completers poll a pinned flag this long before blocking on the event (0: off)
     // while batches are in flight and fewer than a_busy_min calls wait, the
     // launcher gathers for at most this long, then launches what it has on a
-    // free slot (0: until the pipeline idles or a_busy_min calls queue).  Keeps
-    // a closed loop of blocking callers pipelined instead of one batch at a time.
-    uint32_t a_busy_wait_us = 40;
+    // free slot (0: until the pipeline idles or a_busy_min calls queue).
+    // Measured off by default (profiles/r04/d/): 20 / 40 / 80 us left the
+    // 64-thread blocking leg at 0.24-0.26 M calls/s (p50 155 -> 108-149 us)
+    // and cost the 4,096-in-flight leg 6.2 -> 4.6-4.7 M calls/s.
+    uint32_t a_busy_wait_us = 0;
     // a call that finds the queue empty and the whole pipeline idle launches
     // its batch itself, on the calling thread (no launcher wake-up)
     bool a_inline = true;
@@ -2356,14 +2362,24 @@ struct tm_engine {
             const uint64_t cap = std::min<uint64_t>(b->c_sfids, MAX_RESULT);
             fa.nreg = b->one_region ? 1u : TICKET_GROUPS;
             fa.rcap = region_cap(cap, b->one_region);
+            // [vb: TICKET_GROUPS + 1 | rtop: TICKET_GROUPS] in pinned memory -> HBM
+            constexpr size_t FM = 2 * TICKET_GROUPS + 1;
+            if ((rc = host_reserve(b->h_fmeta, b->ch_fmeta, FM))) return rc;
+            if ((rc = dev_reserve(b->d_fmeta, b->c_fmeta, FM))) return rc;
+            uint64_t* vb = b->h_fmeta;
+            uint64_t* rtop = b->h_fmeta + TICKET_GROUPS + 1;
+            std::fill(b->h_fmeta, b->h_fmeta + FM, 0ull);
             uint64_t v = 0, staged = 0;
             for (uint32_t g = 0; g < fa.nreg; ++g) {
-                fa.vb[g] = v;
-                fa.rtop[g] = xg_top_read(b->h_ctrl, g);
-                staged += fa.rtop[g];
-                v += (fa.rtop[g] + 15) & ~15ull;
+                vb[g] = v;
+                rtop[g] = xg_top_read(b->h_ctrl, g);
+                staged += rtop[g];
+                v += (rtop[g] + 15) & ~15ull;
             }
-            fa.vb[fa.nreg] = v;
+            for (uint32_t g = fa.nreg; g <= TICKET_GROUPS; ++g) vb[g] = v;
+            HIP_OK(hipMemcpyAsync(b->d_fmeta, b->h_fmeta, FM * 8, hipMemcpyHostToDevice, stream));
+            fa.vb = b->d_fmeta;
+            fa.rtop = b->d_fmeta + TICKET_GROUPS + 1;
             if (staged != b->total) {
                 snprintf(last_error(), 512, "staging holds %llu entries, the walk matched %llu",
                          (unsigned long long)staged, (unsigned long long)b->total);

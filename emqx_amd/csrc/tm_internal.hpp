@@ -245,10 +245,13 @@ struct FanArgs {
     // entry j - vb[g] (vb[g] a multiple of 16, entries past rtop[g] padding
     // with no deliveries), so a row -- contiguous in its region -- is
     // contiguous here too.  nreg = 0: ids is the match CSR.
+    // (vb / rtop live in device memory, not in the arguments: a kernel-argument
+    // array indexed at run time is copied to scratch, and every pointer the
+    // kernel then loads becomes a flat access -- tools/isa_check.py)
     uint32_t nreg;
     uint64_t rcap;            // a multiple of 16 (region_cap)
-    uint64_t vb[TICKET_GROUPS + 1];
-    uint64_t rtop[TICKET_GROUPS];
+    const uint64_t* vb;       // TICKET_GROUPS + 1
+    const uint64_t* rtop;     // TICKET_GROUPS
     const uint32_t* rcount;   // n: the walk's row lengths (tm_batch_rows)
     const unsigned long long* rsrc;   // n: the rows' first staging entries
     uint32_t* dcount;         // n: deliveries of each row (drow = its first)
@@ -418,14 +421,19 @@ __host__ __device__ inline uint64_t le_bytes(const uint8_t* p, uint32_t n) {   /
 // table slot.  (Equality is decided by length + the inline 16 bytes + arena,
 // never by the hash.)
 __host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-__host__ __device__ inline uint32_t hw_step(uint32_t h, uint32_t d) {
+// one 4-byte chunk's mixing (seed-independent) and its accumulation: split
+// so the device tokeniser computes both cuckoo hashes in one pass
+__host__ __device__ inline uint32_t mix_chunk(uint32_t d) {
     d *= 0xCC9E2D51u;
     d = rotl32(d, 15);
-    d *= 0x1B873593u;
-    h ^= d;
+    return d * 0x1B873593u;
+}
+__host__ __device__ inline uint32_t hw_acc(uint32_t h, uint32_t mixed) {
+    h ^= mixed;
     h = rotl32(h, 13);
     return h * 5u + 0xE6546B64u;
 }
+__host__ __device__ inline uint32_t hw_step(uint32_t h, uint32_t d) { return hw_acc(h, mix_chunk(d)); }
 __host__ __device__ inline uint32_t hw_final(uint32_t h, uint32_t n) {
     h ^= n;
     h ^= h >> 16;

@@ -1496,6 +1496,15 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
         return ((hi ? big1 : big0) ? a.moff[j] : (uint64_t)a.moff32[j]) + (hi ? bs1 : bs0);
     };
     __syncthreads();
+    // rows mode: a tile's entries usually lie in one staging region, whose
+    // entries are then one offset away (padding entries have no deliveries,
+    // so whatever they read is never used); a tile across regions maps each
+    const bool one_reg = !a.nreg || fan_region(a, jlo) == fan_region(a, jhi + 1);
+    const uint32_t* fids = a.ids;
+    if (a.nreg && one_reg) {
+        const uint32_t g = fan_region(a, jlo);
+        fids = a.ids + g * a.rcap - a.vb[g];
+    }
     // staging, FAN_STG entries per thread with every load of a step in flight
     // (the offsets and filter ids, then the dependent sone / soff gathers)
 #ifndef TM_FAN_STG
@@ -1514,7 +1523,7 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
                 const uint64_t j = jlo + e;
                 m0[u] = moff_at(j);
                 m1[u] = moff_at(j + 1);
-                f[u] = fan_fid(a, j);
+                f[u] = one_reg ? fids[j] : fan_fid(a, j);
             }
         }
         int64_t v[FAN_STG];
@@ -2058,68 +2067,73 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
     const uint32_t mask = (uint32_t)a.dict_mask;
     for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
         uint64_t head[TOK_WPL];
-        uint32_t ent[TOK_WPL], len[TOK_WPL], st[TOK_WPL], pend = 0;
+        uint32_t ent[TOK_WPL], len[TOK_WPL], st[TOK_WPL], alt[TOK_WPL], pend = 0;
         uint4 e[TOK_WPL];
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
             const uint32_t w = base + lane + 64 * k;
-            ent[k] = 0;
-            head[k] = 0;
-            len[k] = 0;
-            st[k] = 0;
-            if (w >= tw) continue;
-            const uint32_t s0 = L.wst[w] & 0x7FFFu;
-            const uint32_t nx = w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u);
-            const uint32_t n = (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u);
-            const uint8_t c0 = n ? L.bytes[s0] : 0;
-            bool irr = false;
-            ent[k] = tok_class(c0, n, irr) << WID_BITS;
-            if (irr) L.tirr[L.wtop[w]] = 1;
-            if (n == 0) { ent[k] |= W_EMPTY; continue; }
-            if (n == 1 && c0 == '+') { ent[k] |= W_PLUS; continue; }
-            if (n == 1 && c0 == '#') { ent[k] |= W_HASH; continue; }
-            const uint64_t c0w = low_bytes(lds_u64(L.bytes, s0), n < 8 ? n : 8);
-            uint32_t h32 = hw_step(HW_SEED, (uint32_t)c0w);
-            if (n > 4) h32 = hw_step(h32, (uint32_t)(c0w >> 32));
-            for (uint32_t i = 8; i < n; i += 8) {   // words over 8 bytes
-                const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
-                h32 = hw_step(h32, (uint32_t)c);
-                if (n - i > 4) h32 = hw_step(h32, (uint32_t)(c >> 32));
-            }
-            const uint32_t h = hw_final(h32, n);
-            e[k] = *reinterpret_cast<const uint4*>(a.keys + (h & mask));
-            head[k] = c0w;
+            const bool live = w < tw;
+            // word bounds: start from wst, end at the next word's start (minus
+            // the '/' unless the next word starts a topic)
+            const uint32_t s0 = live ? L.wst[w] & 0x7FFFu : 0u;
+            const uint32_t nx = live ? (w + 1 < tw ? L.wst[w + 1] : (wend | 0x8000u)) : 0x8000u;
+            const uint32_t n = live ? (nx & 0x7FFFu) - s0 - ((nx & 0x8000u) ? 0u : 1u) : 0u;
+            const uint64_t c0w = live ? lds_u64(L.bytes, s0) : 0ull;
+            const uint32_t c0 = n ? (uint32_t)(c0w & 0xFF) : 0u;
+            // class and reserved atoms, branch-free (emqx_topic:words/1's '' / '+' / '#')
+            const uint32_t cls = n == 0 ? C_EMPTY : c0 < '#' ? C_BELOW : c0 < '+' ? C_BETWEEN : C_ABOVE;
+            if (live && c0 == '+' && n > 1) L.tirr[L.wtop[w]] = 1;   // "+x": irregular topic
+            const bool atom = n == 0 || (n == 1 && (c0 == '+' || c0 == '#'));
+            ent[k] = (cls << WID_BITS) | (n == 0 ? W_EMPTY : c0 == '+' ? W_PLUS : W_HASH);
             len[k] = n;
             st[k] = s0;
-            pend |= 1u << k;
+            // both cuckoo hashes in one pass over the bytes (the mixing of
+            // each 4-byte chunk is shared; only the accumulators differ)
+            const uint64_t hd = low_bytes(c0w, n < 8 ? n : 8);
+            uint32_t d = mix_chunk((uint32_t)hd);
+            uint32_t h1 = hw_acc(HW_SEED, d), h2 = hw_acc(HW_SEED2, d);
+            if (n > 4) {
+                d = mix_chunk((uint32_t)(hd >> 32));
+                h1 = hw_acc(h1, d);
+                h2 = hw_acc(h2, d);
+            }
+            for (uint32_t i = 8; i < n; i += 8) {   // words over 8 bytes
+                const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
+                d = mix_chunk((uint32_t)c);
+                h1 = hw_acc(h1, d);
+                h2 = hw_acc(h2, d);
+                if (n - i > 4) {
+                    d = mix_chunk((uint32_t)(c >> 32));
+                    h1 = hw_acc(h1, d);
+                    h2 = hw_acc(h2, d);
+                }
+            }
+            head[k] = hd;
+            alt[k] = hw_final(h2, n) & mask;
+            const bool look = live && !atom;
+            e[k] = look ? *reinterpret_cast<const uint4*>(a.keys + (hw_final(h1, n) & mask)) : make_uint4(0, 0, 0, 0);
+            pend |= look ? 1u << k : 0u;
         }
         // primary slots: a match or an empty slot settles the word
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
             if (!(pend >> k & 1u)) continue;
             if (e[k].w == 0) {
+                ent[k] = (ent[k] & ~WID_MASK) | W_UNKNOWN;
                 pend &= ~(1u << k);
             } else if (ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) {
-                ent[k] |= e[k].w;
+                ent[k] = (ent[k] & ~WID_MASK) | e[k].w;
                 pend &= ~(1u << k);
             }
         }
-        // alternate slots of the rest (second hash, from LDS), all in flight
+        // alternate slots of the rest, all in flight
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k)
-            if (pend >> k & 1u) {
-                const uint32_t n = len[k], s0 = st[k];
-                uint32_t g32 = HW_SEED2;
-                for (uint32_t i = 0; i < n; i += 8) {
-                    const uint64_t c = low_bytes(lds_u64(L.bytes, s0 + i), n - i < 8 ? n - i : 8);
-                    g32 = hw_step(g32, (uint32_t)c);
-                    if (n - i > 4) g32 = hw_step(g32, (uint32_t)(c >> 32));
-                }
-                e[k] = *reinterpret_cast<const uint4*>(a.keys + (hw_final(g32, n) & mask));
-            }
+            if (pend >> k & 1u) e[k] = *reinterpret_cast<const uint4*>(a.keys + alt[k]);
 #pragma unroll
         for (uint32_t k = 0; k < TOK_WPL; ++k) {
-            if ((pend >> k & 1u) && ck_match(a, e[k], head[k], len[k], L.bytes + st[k])) ent[k] |= e[k].w;
+            if (pend >> k & 1u)
+                ent[k] = (ent[k] & ~WID_MASK) | (ck_match(a, e[k], head[k], len[k], L.bytes + st[k]) ? e[k].w : W_UNKNOWN);
             const uint32_t w = base + lane + 64 * k;
             if (w < tw && tile_base + w < a.words_cap) a.words[tile_base + w] = ent[k];
         }

@@ -5,7 +5,7 @@ TAG=${1:-pmc_c4}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--workload c4 --steps 2 --warmup 1"
+ARGS="--workload c4 --profile --steps 2 --warmup 1"
 for pass in "fetch FETCH_SIZE" "write WRITE_SIZE"; do
     set -- $pass
     name=$1; shift
