@@ -5,14 +5,17 @@
 Workload: 1,000,000 distinct wildcard filters
 (depth <= 7, V = 1024, Zipf 1.1, p+ = 0.15, p# = 0.25, seed 2) compiled into
 the HBM trie replica; a batch of 10,000,000 synthetic publishes per GPU
-(seed 1000 + rank), tokenised + interned on the host and resident in HBM before
-timing.  One step = the whole device pipeline over the batch: frontier-walk
-kernel and generic slow path -- every topic's complete, byte-sorted,
+(seed 1000 + rank) whose bytes are resident in HBM before timing and are
+tokenised + interned there by the device tokeniser on the first launch; the
+timed steps reuse those tokens (the dictionary does not change), and a fresh
+batch (tokeniser + walk every launch) is timed beside them
+("fresh_publishes_per_s").  One step = the frontier-walk kernel and the
+generic slow path over the batch -- every topic's complete, byte-sorted,
 deduplicated match set lands in HBM as the walk's rows (tm_batch_rows: per
-topic a count and a start in the staging array; the per-publish path consumes
-them there).  The dense CSR (row offsets + ids in topic order: scan + one copy,
-built on request by tm_batch_result / routes / dispatch / export) is timed
-beside it as "dense_csr".
+topic a count and a start in the staging array; the per-publish path and the
+fan-out consume them there).  The dense CSR (row offsets + ids in topic
+order: scan + one copy, built on request by tm_batch_result / routes /
+export) is timed beside it as "dense_csr".
 
 Multi-GPU: one process per GPU (torchrun), the trie replicated on every GPU,
 each rank matching its own 10M batch (replicated mode, no data-path
@@ -21,8 +24,12 @@ collective) -> "scaling": "weak"; value = all ranks' publishes / max rank time.
 Extra fields: roofline (HBM, algorithmic bytes per launch counted by the kernel,
 over the match kernel's HIP-event time), cpu_baseline (the CPU restatement of
 emqx_router:match_routes/1 on this host, rank 0 / N = 1 only), p99 batch latency
-at B = 65,536 and the host-inclusive end-to-end rate (bytes in host RAM ->
-sorted CSR in host RAM).
+at B = 65,536 (device-resident replay) and fresh_latency_sweep (new publishes
+from host memory to sorted ids in host memory, B = 4,096 / 65,536), the
+host-inclusive end-to-end rate, C1 on the CPU port and the device, and C5
+(K = 100 and 10: skew + 10k subscribe/unsubscribe deltas per step).  At N > 1
+every rank's sampled rows are checked against rank 0's replica on device 0
+(parity_sample_ok, emqx_amd/selfcheck.py).
 """
 
 from __future__ import annotations
@@ -990,7 +997,8 @@ def main():
 
     # the first launch tokenises the resident bytes on the device (tm_tok_*);
     # the timed steps reuse the tokens (the dictionary does not change), so a
-    # step is the trie walk + CSR over a tokenised batch already in HBM
+    # step is the trie walk (+ generic path) over a tokenised batch in HBM,
+    # leaving the rows where the walk wrote them
     for _ in range(max(args.warmup, 1)):
         for x in bs:
             x.launch().wait()

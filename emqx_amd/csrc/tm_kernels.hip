@@ -221,26 +221,6 @@ __device__ __forceinline__ uint4 q_pack(uint64_t key, uint32_t meta, uint32_t pa
     return uint4{(uint32_t)key | meta, (uint32_t)(key >> 32), parent, pw};
 }
 
-// Emission row of lane tl of this wave: rows[(blockIdx.x * 64 + tl) * K + slot].
-// wrows = this wave's rows (rows + blockIdx.x * tile_topics * K), hoisted by the caller.
-template <bool CK>
-__device__ __forceinline__ void emit_row(const MatchArgs& a, unsigned long long* wrows, uint32_t tl, uint32_t slot,
-                                         uint64_t key, uint32_t fid) {
-#ifdef TM_EXPERIMENT_NO_EMIT   // timing experiments only
-    if (slot < a.row_cap && fid == 0xFFFFFFF0u) {
-#else
-    if (slot < a.row_cap) {
-#endif
-#ifdef TM_EXPERIMENT_EMIT_HOT   // timing only: same stores, 4 slots per topic (L2-resident rows)
-        const uint32_t i = tl * a.row_cap + (slot & 3);
-#else
-        const uint32_t i = tl * a.row_cap + slot;   // < tile_topics * K <= 2^16
-#endif
-        if (CK) (void)CK_((uint64_t)blockIdx.x * a.tile_topics * a.row_cap + i, (uint64_t)gridDim.x * a.tile_topics * a.row_cap, 13);
-        wrows[i] = (key & KEY_MASK) | fid;
-    }
-}
-
 static_assert(offsetof(TileLds<512>, words) + sizeof(uint32_t) * WCAP == TileLds<512>::STAGE * 8,
               "staging area must be contiguous");
 static_assert(offsetof(TileLds<384>, words) + sizeof(uint32_t) * WCAP == TileLds<384>::STAGE * 8,
@@ -352,64 +332,16 @@ __device__ __forceinline__ void sort_classes(const MatchArgs& a, LT& L, bool kee
     }
 }
 
-// c <= row_cap <= 128 for every kept row, so a chunk always holds at least one row.
-// The rows are copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: 16 B per
-// lane, no register destination), every row of a chunk in flight at once, so
-// the read-back costs one memory round trip per chunk rather than one per row
-// batch.  Staging positions are padded to even counts: each row starts on a 16-B
-// boundary, and the odd row's extra 8 B land in its pad slot, which the sort
-// never reads.
-template <bool CK, class LT>
-__device__ __forceinline__ void sort_rows(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst) {
-    constexpr uint32_t STAGE = LT::STAGE;
-    const uint32_t lane = threadIdx.x;
-    unsigned long long* stg = reinterpret_cast<unsigned long long*>(L.q);
-    const uint32_t cp = (c + 1u) & ~1u;
-    uint32_t incl = cp;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += u;
-    }
-    const uint32_t pos = incl - cp;
-    const uint64_t rbase = (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
-    const uint64_t rlim = (uint64_t)gridDim.x * a.tile_topics * a.row_cap;
-    uint32_t rs = 0;
-    while (rs < a.tile_topics) {
-        const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
-        const uint64_t beyond = __ballot(lane >= rs && pos + cp - p0 > STAGE);
-        const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : a.tile_topics;
-        for (uint32_t r = rs; r < re; ++r) {
-            const uint32_t cr = __builtin_amdgcn_readlane(c, r);
-            if (cr == 0) continue;
-            const uint32_t pr = __builtin_amdgcn_readlane(pos, r) - p0;
-            const uint64_t rb = rbase + (uint64_t)r * a.row_cap;
-            if (lane < (cr + 1) / 2) {
-                const unsigned long long* src = a.rows + CK_(rb + 2 * lane, rlim, 50);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                 (__attribute__((address_space(3))) void*)(stg + pr), 16, 0, 0);
-            }
-        }
-        __syncthreads();   // waits for the LDS-DMA (vmcnt) before any lane reads the staging area
-        sort_classes<CK, LT>(a, L, keep && lane >= rs && lane < re, c, pos - p0, dst);
-        __syncthreads();
-        rs = re;
-    }
-}
-
 #ifndef TM_LOG_U
 #define TM_LOG_U 12  // log entries per lane per read-back step, all in flight (4 / 8 / 12 / 16: 5.10 / 5.07 / 5.04 / 5.05 ms)
 #endif
-#ifndef TM_EMIT_ROWS
-// Emission log variant of the tile epilogue: the tile's matches were appended
+// Emission log epilogue: the tile's matches were appended
 // to a wave-private log in iteration order (coalesced: one store of <= 64
 // consecutive entries per emission role per iteration), each with its topic
 // lane in a parallel byte log.  The rows are rebuilt in LDS a chunk of whole
 // rows at a time -- the log is streamed (L2-resident: written moments ago)
 // and every entry of a chunk's rows goes to its row's next free place -- and
 // sorted as before.
-#ifndef TM_LOG_REM
-#define TM_LOG_REM 0   // 1: passes after the first read only the entries of rows not yet done, compacted in place (A/B: 5.037 -> 5.027 ms, WRITE_SIZE +0.8 GB: off)
-#endif
 template <bool CK, class LT>
 __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool keep, uint32_t c, uint32_t dst,
                                               unsigned long long* wlog, uint8_t* wlane, uint32_t lcount) {
@@ -423,23 +355,17 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
         if (lane >= (uint32_t)o) incl += u;
     }
     const uint32_t pos = incl - cw;
-    constexpr uint32_t REM = NONE - 1;   // a kept row of a later chunk
     uint32_t rs = 0;
     while (rs < a.tile_topics) {
         const uint32_t p0 = __builtin_amdgcn_readlane(pos, rs);
         const uint64_t beyond = __ballot(lane >= rs && pos + cw - p0 > STAGE);
         const uint32_t re = beyond ? (uint32_t)__builtin_ctzll(beyond) : a.tile_topics;
         const bool in_chunk = keep && lane >= rs && lane < re;
-        // (depth / toff are free after the frontier loop) row base in the stage,
-        // REM for rows of later chunks, NONE for rows not staged here
-        L.depth[lane] = in_chunk ? pos - p0 : ((TM_LOG_REM && keep && lane >= re) ? REM : NONE);
+        // (depth / toff are free after the frontier loop) row base in the
+        // stage, NONE for rows not staged in this pass
+        L.depth[lane] = in_chunk ? pos - p0 : NONE;
         L.toff[lane] = 0;                            // row fill cursor
         __syncthreads();
-        // With a later chunk, this pass also moves the entries of the later
-        // chunks' rows to the front of the log (positions already read: the
-        // remainder never outruns the reads), so the next pass reads only them.
-        const bool more = TM_LOG_REM && re < a.tile_topics;
-        uint32_t wr = 0;
         for (uint32_t k0 = 0; k0 < lcount; k0 += 64 * TM_LOG_U) {
             unsigned long long e[TM_LOG_U];
             uint32_t r[TM_LOG_U];
@@ -455,29 +381,17 @@ __device__ __forceinline__ void sort_rows_log(const MatchArgs& a, LT& L, bool ke
 #pragma unroll
             for (uint32_t u = 0; u < TM_LOG_U; ++u) {
                 const uint32_t base = r[u] < 64 ? L.depth[r[u]] : NONE;
-                if (more) {
-                    const bool rem = base == REM;
-                    const uint64_t m = __ballot(rem);
-                    if (rem) {
-                        const uint32_t at = wr + prefix_count(m);
-                        wlog[at] = e[u];
-                        wlane[at] = (uint8_t)r[u];
-                    }
-                    wr += (uint32_t)__popcll(m);
-                }
-                if (base >= REM) continue;
+                if (base == NONE) continue;
                 const uint32_t at = base + atomicAdd(&L.toff[r[u]], 1u);
                 stg[CK_(at, STAGE, 49)] = e[u];
             }
         }
-        __syncthreads();   // (also: the moved entries are visible to the next pass's loads)
+        __syncthreads();
         sort_classes<CK, LT>(a, L, in_chunk, c, pos - p0, dst);
         __syncthreads();
-        if (more) lcount = wr;
         rs = re;
     }
 }
-#endif
 
 template <bool CK>
 __device__ __forceinline__ void send_to_slow(const MatchArgs& a, bool mine, uint32_t t) {
@@ -509,14 +423,12 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     bool ovf = false;
     const bool active = !(fl & TF_SLOW);
     unsigned long long* const wrows = a.rows + (uint64_t)blockIdx.x * a.tile_topics * a.row_cap;
-#ifndef TM_EMIT_ROWS
-    // the wave's log: its rows region (entries) + a byte per entry (topic lane)
-    // past the whole rows array
+    // the wave's emission log: its rows region (entries) + a byte per entry
+    // (topic lane) past the whole rows array
     const uint32_t lcap = a.tile_topics * a.row_cap;
     uint8_t* const wlane =
         reinterpret_cast<uint8_t*>(a.rows + (uint64_t)a.grid * lcap) + (uint64_t)blockIdx.x * lcap;
     uint32_t lcount = 0;
-#endif
     uint32_t tV = 0, tH = 0, tW = 0, tP = 0;   // committed only if the tile does not overflow
     const uint32_t d_me = L.depth[lane];
 
@@ -539,7 +451,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         if (x.np >= 1) L.q[qn + pre] = q_pack(x.pk0, meta | x.pf0, ROOT, (x.pf0 & M_PLUS) ? W_PLUS : wid);
         if (x.np >= 2) L.q[qn + pre + 1] = q_pack(x.pk1, meta | x.pf1, ROOT, (x.pf1 & M_PLUS) ? W_PLUS : wid);
         qn += __popcll(b0) + __popcll(b1);
-#ifndef TM_EMIT_ROWS
         const uint64_t mr = __ballot(x.ne != 0);
         if (x.ne) {   // at most one emission at the root ('#')
             L.cnt[lane] = 1;
@@ -548,12 +459,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             wlane[i] = (uint8_t)lane;
         }
         lcount = (uint32_t)__popcll(mr);
-#else
-        if (x.ne) {   // at most one emission at the root ('#')
-            L.cnt[lane] = 1;
-            emit_row<CK>(a, wrows, lane, 0, x.ek0, x.ef0);
-        }
-#endif
     }
 
     // ---- frontier loop: LIFO stack, up to 64 probes per iteration
@@ -571,14 +476,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     const uint32_t qd = lane >> 2, qs = lane & 3;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<Slot*>(a.slots), 0, BIG ? 0u : a.nslots * 16u, 0x00020000);
-#ifdef TM_EXPERIMENT_PHASES   // (timing experiments only: cycles per phase into the H / W stats, iterations into V)
-    const uint64_t ph0 = __builtin_amdgcn_s_memtime();
-    uint32_t iters = 0;
-#endif
     while (qn > 0) {
-#ifdef TM_EXPERIMENT_PHASES
-        ++iters;
-#endif
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         qn -= k;
@@ -695,7 +593,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         }
         if (pP) L.q[pre + (sL ? 1u : 0u)] = q_pack(key | ((uint64_t)dig_P(cls) << sh), nmeta | M_PLUS, s.child, W_PLUS);
         qn += ptot;
-#ifndef TM_EMIT_ROWS
         {
             // row sizes; a row's entries past K are not logged (the row goes to
             // the generic path), so the log holds at most tile_topics * K
@@ -706,9 +603,6 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             eB = eB && slotB < a.row_cap;
             const uint64_t mA = __ballot(eA), mB = __ballot(eB);
             const uint32_t nA = (uint32_t)__popcll(mA), nE = nA + (uint32_t)__popcll(mB);
-#ifdef TM_EXPERIMENT_NO_LOG   // (timing experiments only: counts kept, log stores dropped)
-            eA = eB = false;
-#endif
             if (eA) {
                 const uint32_t i = lcount + prefix_count(mA);
                 wrows[CK_(i, lcap, 13)] = (kA & KEY_MASK) | fA;
@@ -721,20 +615,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
             }
             lcount += nE;
         }
-#else
-        if (eA | eB) {
-            const uint32_t slot = atomicAdd(&L.cnt[tl], (eA ? 1u : 0u) + (eB ? 1u : 0u));
-            if (eA) emit_row<CK>(a, wrows, tl, slot, kA, fA);
-            if (eB) emit_row<CK>(a, wrows, tl, slot + (eA ? 1u : 0u), key | (2ull << sh), s.hterm);
-        }
-#endif
     }
     __syncthreads();
-#ifdef TM_EXPERIMENT_PHASES
-    tW = 0;
-    tH = lane == 0 ? (uint32_t)(__builtin_amdgcn_s_memtime() - ph0) : 0u;   // frontier loop
-    tV = lane == 0 ? iters : 0u;
-#endif
 
     if (ovf) {
         // probe stack overflow: every regular topic of the tile goes to the slow path
@@ -764,17 +646,11 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     base64 += (uint64_t)g * a.rcap;
     const uint32_t base = (uint32_t)base64;
     const uint32_t dst = base + incl - c;
-#ifndef TM_EXPERIMENT_NO_EPILOGUE   // (timing experiments only: rows left unsorted and unstaged)
     if (fits) {
-#ifndef TM_EMIT_ROWS
         sort_rows_log<CK, LT>(a, L, keep, c, dst, wrows, wlane, lcount);
-#else
-        sort_rows<CK, LT>(a, L, keep, c, dst);
-#endif
     } else if (lane == 0) {
         atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);   // host grows sfids[] and reruns
     }
-#endif
     if (keep) {
         a.count[CK_(t, a.n, 16)] = c_me;
         a.src[CK_(t, a.n, 17)] = dst;
@@ -794,13 +670,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
     // static round-robin tiles, then tickets for the tail; a ticket is taken at
     // the start of a tile so its latency hides behind the tile's work
     uint32_t tile = blockIdx.x, round = 0;
-#ifdef TM_EXPERIMENT_PHASES
-    uint64_t pro = 0;
-#endif
     while (tile < ntiles) {
-#ifdef TM_EXPERIMENT_PHASES
-        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-#endif
         // the next tile: round-robin for the first static_rounds, then from a
         // ticket (a contended counter's latency would stall every in-order vmcnt
         // wait of the tile, so only the tail balances by tickets, per XCD)
@@ -822,9 +692,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
         L.depth[lane] = my_end - my_off;
         L.cnt[lane] = 0;
         __syncthreads();
-#ifdef TM_EXPERIMENT_PHASES
-        pro += __builtin_amdgcn_s_memtime() - pt0;   // prologue: ticket, offsets, words to LDS
-#endif
         if (in_lds) match_tile<CK, BIG, true>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM, sP);
         else match_tile<CK, BIG, false>(a, L, t0, tend, wbeg, fl, valid, sV, sH, sW, sM, sP);
         __syncthreads();
@@ -835,9 +702,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
                          blockIdx.x % TICKET_GROUPS;
     }
 
-#ifdef TM_EXPERIMENT_PHASES
-    sW = lane == 0 ? pro : 0;
-#endif
     for (int o = 32; o > 0; o >>= 1) {
         sV += __shfl_xor(sV, o, 64); sH += __shfl_xor(sH, o, 64);
         sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
@@ -1887,9 +1751,6 @@ __device__ __forceinline__ uint32_t tok_class(uint8_t c0, uint32_t n, bool& irre
 template <class P>
 __device__ __forceinline__ bool ck_match(const TokArgs& a, const uint4& e, uint64_t head, uint32_t n, P p) {
     if (e.z != n || e.x != (uint32_t)head || e.y != (uint32_t)(head >> 32)) return false;
-#ifdef TM_EXPERIMENT_TOK_NO_TAIL   // (timing experiments only: words over 8 bytes match on head + length)
-    return true;
-#endif
     if (n <= 8) return true;
     const DictTail t = a.tails[e.w];
     uint64_t h2 = 0;
@@ -2272,9 +2133,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
             }
             if (lane == 0) L.ttoff[cnt] = tw;
             __syncthreads();
-#ifndef TOK_NO_LOOKUP   // (experiment hook: splitting cost alone)
             tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
-#endif
             __syncthreads();
             if (valid) {
                 const uint32_t w0 = L.ttoff[lane], tn = L.ttoff[lane + 1] - w0;
