@@ -136,6 +136,7 @@ class WordDict {
     uint32_t intern(const uint8_t* p, size_t n) {
         uint32_t id = find(p, n);
         if (id != W_UNKNOWN) return id;
+        if (next_id_ > WID_MASK) throw std::bad_alloc();   // word ids fill WID_BITS (slot + topic entries)
         if ((count_ + 1) * 2 > tab_.size()) rehash(tab_.size() * 2);
         id = next_id_++;
         const uint64_t h = hash_word(p, n);
@@ -911,7 +912,23 @@ struct tm_engine {
         uint8_t live = 0, topic = 0;
         uint8_t hasbytes = 0;            // n_foff / n_flen name this id's filter (until the id is reused)
         uint8_t pad = 0;
-        uint32_t pad2 = 0;
+        // literal children per signature bit (lsig_pos of their words),
+        // saturating: a count that reached 255 keeps its bit set for good
+        uint8_t lcnt[LSIG_BITS] = {};
+        uint8_t pad2[4 - LSIG_BITS] = {};
+        uint32_t lsig() const {
+            uint32_t s = 0;
+            for (uint32_t i = 0; i < LSIG_BITS; ++i) s |= lcnt[i] ? 1u << i : 0u;
+            return s;
+        }
+        void lsig_add(uint32_t w) {
+            uint8_t& k = lcnt[lsig_pos(w)];
+            if (k < 255) ++k;
+        }
+        void lsig_del(uint32_t w) {
+            uint8_t& k = lcnt[lsig_pos(w)];
+            if (k && k < 255) --k;
+        }
     };
     static_assert(sizeof(NodeRec) == 32, "two node records per cache line");
     std::vector<NodeRec, HugeAlloc<NodeRec>> nd;
@@ -988,7 +1005,7 @@ struct tm_engine {
         for (uint32_t i = 0; i <= max_disp; ++i) {
             for (uint32_t s = 0; s < BUCKET; ++s) {
                 const Slot& e = slots[b * BUCKET + s];
-                if (e.parent == p && e.word == w) return b * BUCKET + s;
+                if (e.parent == p && (e.word & WID_MASK) == w) return b * BUCKET + s;
             }
             if (slots[b * BUCKET + BUCKET - 1].parent == SLOT_EMPTY) return NONE;
             b = (b + 1 == nb) ? 0 : b + 1;
@@ -1027,7 +1044,7 @@ struct tm_engine {
             if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) continue;
             uint32_t disp;
             bool was_empty;
-            uint32_t i = place_slot(tab, e.parent, e.word, disp, was_empty);
+            uint32_t i = place_slot(tab, e.parent, e.word & WID_MASK, disp, was_empty);
             tab[i] = e;
             nd[e.child & ID_MASK].inslot = i;
             md = std::max(md, disp);
@@ -1142,7 +1159,7 @@ struct tm_engine {
                 const uint32_t j = cb * BUCKET + k;
                 const Slot& e = slots[j];
                 if (e.parent == SLOT_EMPTY) break;
-                const uint32_t h = home_bucket(e.parent, e.word, nb);
+                const uint32_t h = home_bucket(e.parent, e.word & WID_MASK, nb);
                 // the run of e goes h .. cb; it crosses hb iff hb lies in [h, cb)
                 const uint32_t dist_e = (cb + nb - h) % nb, dist_hole = (cb + nb - hb) % nb;
                 if (dist_e >= dist_hole) {
@@ -1206,6 +1223,7 @@ struct tm_engine {
             nd[id].hasbytes = 0;
             nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
             nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
+            for (uint8_t& k : nd[id].lcnt) k = 0;
             ++M->live_nodes;
             return id;
         }
@@ -1223,6 +1241,7 @@ struct tm_engine {
         }
         nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
         nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
+        for (uint8_t& k : nd[id].lcnt) k = 0;
         ++live_nodes;
         return id;
     }
@@ -1243,6 +1262,7 @@ struct tm_engine {
         nd[id].live = 0;
         nd[id].topic = 0;
         nd[id].ec = 0;
+        for (uint8_t& k : nd[id].lcnt) k = 0;
         if (M) {
             --M->live_nodes;
             if (id != ROOT) M->pend.emplace_back(launch_seq, id);
@@ -1270,6 +1290,7 @@ struct tm_engine {
         const uint32_t i = nd[c].inslot;
         if (i == NONE) return;
         Slot& e = slots[i];
+        e.word = (e.word & WID_MASK) | (nd[c].lsig() << WID_BITS);
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
         e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
@@ -1431,6 +1452,7 @@ struct tm_engine {
                 ++nd[p].ec;
                 if (w == W_PLUS) nd[p].plus = c;
                 else if (w == W_HASH) nd[p].hash = c;
+                else nd[p].lsig_add(w);
                 insert_edge(p, w, c);
                 if (M && M->defer && k < sd) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
                 write_summary(p);
@@ -1483,6 +1505,7 @@ struct tm_engine {
             if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
             if (w == W_PLUS) nd[p].plus = NONE;
             else if (w == W_HASH) nd[p].hash = NONE;
+            else nd[p].lsig_del(w);
             if (!nd[p].live) { rc = TM_EABORT; break; }
             if (nd[p].ec == 1 && !nd[p].topic) {
                 nd[p].ec = 0;
@@ -1870,6 +1893,7 @@ struct tm_engine {
     void write_summary_at(uint32_t c, std::vector<uint32_t>& dl) {
         const uint32_t i = nd[c].inslot;
         Slot& e = slots[i];
+        e.word = (e.word & WID_MASK) | (nd[c].lsig() << WID_BITS);
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
         e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
@@ -5301,7 +5325,7 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
                 return TM_EIO;
             }
             ++live;
-            const uint32_t h = home_bucket(sl.parent, sl.word, nb);
+            const uint32_t h = home_bucket(sl.parent, sl.word & WID_MASK, nb);
             const uint32_t d = (b + nb - h) % nb;
             md = std::max<uint64_t>(md, d);
             if (d > e->max_disp) {
@@ -5313,9 +5337,25 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
                     snprintf(last_error(), 512, "run of slot %u (home %u) broken at bucket %u", b * BUCKET + k, h, x);
                     return TM_EIO;
                 }
-            if (e->find_slot(sl.parent, sl.word) != b * BUCKET + k || e->nd[sl.child & ID_MASK].inslot != b * BUCKET + k) {
+            if (e->find_slot(sl.parent, sl.word & WID_MASK) != b * BUCKET + k || e->nd[sl.child & ID_MASK].inslot != b * BUCKET + k) {
                 snprintf(last_error(), 512, "slot %u not found by its key", b * BUCKET + k);
                 return TM_EIO;
+            }
+            // the child's literal signature: the node's own, and the parent's
+            // covers this edge's word (a clear bit must prove the edge absent)
+            const uint32_t c = sl.child & ID_MASK, w = sl.word & WID_MASK;
+            if ((sl.word >> WID_BITS) != e->nd[c].lsig()) {
+                snprintf(last_error(), 512, "slot %u: literal signature %u, node %u has %u", b * BUCKET + k,
+                         sl.word >> WID_BITS, c, e->nd[c].lsig());
+                return TM_EIO;
+            }
+            if (sl.parent != ROOT && w != W_PLUS && w != W_HASH) {
+                const uint32_t pi = e->nd[sl.parent].inslot;
+                if (pi == NONE || !((e->slots[pi].word >> WID_BITS) >> lsig_pos(w) & 1u)) {
+                    snprintf(last_error(), 512, "slot %u: word %u missing from its parent's literal signature",
+                             b * BUCKET + k, w);
+                    return TM_EIO;
+                }
             }
         }
     }

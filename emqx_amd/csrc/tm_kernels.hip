@@ -50,7 +50,9 @@ constexpr uint32_t M_DSTART = 1u << 12;  // $-rooted start probe: the node was a
 static_assert(FAST_MAX_DEPTH <= (int)M_LVL_MASK, "level field too narrow");
 constexpr uint32_t M_DISP_SHIFT = 13;    // bucket displacement of a continued probe (<= max_probe <= 48)
 constexpr uint32_t M_DISP_MASK = 0x3F;
-constexpr uint32_t Q_FOUND = 0xFFFFFFFFu;   // probe-entry marks written by the quad (parent / word fields)
+// probe-entry marks written by the quad: FOUND | the child's literal signature
+// into the parent field, TAIL into the word field (never a parent / word id)
+constexpr uint32_t Q_FOUND = ~((1u << LSIG_BITS) - 1u);
 constexpr uint32_t Q_TAIL = 0xFFFFFFFFu;
 
 // digit tables indexed by class (C_BELOW, C_BETWEEN, C_ABOVE, C_EMPTY):
@@ -120,10 +122,11 @@ __device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint3
             const uint4* q = reinterpret_cast<const uint4*>(a.slots) + si;
             s0 = q[0]; s1 = q[1]; s2 = q[2]; s3 = q[3];
         }
-        const bool m0 = s0.x == parent && s0.y == word;
-        const bool m1 = s1.x == parent && s1.y == word;
-        const bool m2 = s2.x == parent && s2.y == word;
-        const bool m3 = s3.x == parent && s3.y == word;
+        // (the word's top bits are the child's literal signature)
+        const bool m0 = s0.x == parent && (s0.y & WID_MASK) == word;
+        const bool m1 = s1.x == parent && (s1.y & WID_MASK) == word;
+        const bool m2 = s2.x == parent && (s2.y & WID_MASK) == word;
+        const bool m3 = s3.x == parent && (s3.y & WID_MASK) == word;
         const uint32_t hz = m0 ? s0.z : m1 ? s1.z : m2 ? s2.z : s3.z;
         const uint32_t hw = m0 ? s0.w : m1 ? s1.w : m2 ? s2.w : s3.w;
         if (m0 | m1 | m2 | m3) {
@@ -529,17 +532,17 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         // word ids never equal the marks.
 #pragma unroll
         for (uint32_t r = 0; r < 4; ++r) {
-            const bool m = rp[r] != SLOT_EMPTY && sl[r].x == rp[r] && sl[r].y == rw[r];
+            const bool m = rp[r] != SLOT_EMPTY && sl[r].x == rp[r] && (sl[r].y & WID_MASK) == rw[r];
             if (m) {
                 L.q[qn + 16 * r + qd].x = sl[r].z;
                 L.q[qn + 16 * r + qd].y = sl[r].w;
-                L.q[qn + 16 * r + qd].z = Q_FOUND;
+                L.q[qn + 16 * r + qd].z = Q_FOUND | (sl[r].y >> WID_BITS);
             }
             if (qs == 3 && sl[r].x == SLOT_EMPTY) L.q[qn + 16 * r + qd].w = Q_TAIL;   // out-of-range loads read 0
         }
         uint4 res = uint4{0u, 0u, 0u, 0u};
         if (has) res = L.q[idx];
-        const bool found = has && res.z == Q_FOUND;
+        const bool found = has && res.z >= Q_FOUND;
         const bool cont = has && !found && res.w != Q_TAIL && disp < a.max_probe;
         Node s;
         s.child = 0; s.term = NONE; s.hterm = NONE; s.flags = 0;
@@ -576,7 +579,9 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
                 eA = s.hterm != NONE;
                 fA = s.hterm;
                 kA = key | ((uint64_t)dig_H(cls) << sh);
-                pL = id == W_HASH ? (s.flags & NF_HASH) != 0 : (id != W_UNKNOWN && id != W_PLUS);
+                // a literal word whose signature bit is clear has no edge here
+                pL = id == W_HASH ? (s.flags & NF_HASH) != 0
+                                  : (id != W_UNKNOWN && id != W_PLUS && ((res.z >> lsig_pos(id)) & 1u));
                 pP = (s.flags & NF_PLUS) != 0;
             }
         }

@@ -65,3 +65,30 @@ def test_churn_plus_chains():
     assert worst >= 2
     for seed in range(6):
         _churn(seed=300 + seed, n_words=8, pool_n=3000, live_n=1500, steps=6000, check_every=97, wild=True)
+
+
+def test_literal_signature_saturates_and_clears():
+    """The slot's literal-child signature (tm_internal.hpp Slot.word top bits):
+    2,000 literal children under one node saturate its per-bit counts (the
+    bits then stay set), a node whose last literal child goes clears its bits
+    -- tm_debug_check compares every slot's bits with the node's counts and
+    checks each literal edge's bit in its parent's signature; lookups follow."""
+    e, t = Engine(device=-1), O.Trie()
+    wide = [b"a/b/c%d" % i for i in range(2000)]
+    narrow = [b"a/n/x", b"a/n/y", b"a/n/+", b"a/n/#"]
+    for f in wide + narrow:
+        e.insert(f)
+        t.insert(f)
+    e.debug_check()
+    for f in wide[:1990] + narrow[:2]:
+        e.delete(f)
+        t.delete(f)
+    e.debug_check()
+    for f in wide[1990:]:
+        e.delete(f)
+        t.delete(f)
+    e.insert(b"a/b/z")
+    t.insert(b"a/b/z")
+    e.debug_check()
+    for g in wide + narrow + [b"a/b/z"]:
+        assert (e.lookup(g) is None) == (not t.lookup(g)), g
