@@ -469,6 +469,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
         dels, adds = churn.step(n_deltas)
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
     ms_match, ms_churn, ms_walk, ms_tok = [], [], [], []
+    ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
     t0 = time.perf_counter()
     tc = time.perf_counter()
     Churn.apply(eng, *deltas[0])
@@ -482,14 +483,20 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
             # the deltas' upload is gathered and enqueued now, behind batch i's
             # walk on the engine stream (pinned staging: no host wait), so
             # launch i + 1 has nothing left to upload
+            tc = time.perf_counter()
             eng.sync_async()
+            ms_host["sync_async"].append(1e3 * (time.perf_counter() - tc))
+        tc = time.perf_counter()
         b.wait()
+        ms_host["wait"].append(1e3 * (time.perf_counter() - tc))
         st = b.stats()
         ms_match.append(st["ms_total"])
         ms_walk.append(st["ms_match"])
         ms_tok.append(st["ms_tokenize"])
         if i + 1 < steps:
+            tc = time.perf_counter()
             b.launch()
+            ms_host["launch"].append(1e3 * (time.perf_counter() - tc))
     elapsed = time.perf_counter() - t0
     if sync is not None:
         sync.barrier()
@@ -505,6 +512,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
         "device_ms": float(np.mean(ms_match)), "device_walk_ms": float(np.mean(ms_walk)),
         "device_tokenize_ms": float(np.mean(ms_tok)),
         "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
+        "host_ms": {k: float(np.mean(v)) if v else 0.0 for k, v in ms_host.items()},
         "churn_overlapped_with_device": True,
         "matches_delivered_per_step": delivered, "generic_path_topics": int(st["slow_topics"]),
         "uploads_delta": eng.stats()["uploads_delta"],
@@ -540,6 +548,7 @@ def run_c5(args, ws, rank, local, sync):
         "device_tokenize_ms": leg["device_tokenize_ms"],
         "churn_apply_ms": leg["churn_ms"],
         "churn_overlapped_with_device": True,
+        "host_ms": leg["host_ms"],
         "matches_delivered_per_step": leg["matches_delivered_per_step"],
         "generic_path_topics": leg["generic_path_topics"],
         "uploads_delta": leg["uploads_delta"],

@@ -458,6 +458,10 @@ struct tm_batch {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     hipEvent_t evt = nullptr;   // before the device tokeniser (fresh launches)
     hipEvent_t evc0 = nullptr, evc1 = nullptr;   // around the dense-CSR pass (ensure_dense)
+    // after the launch's last read-back: wait() syncs on it, not on the stream,
+    // so work queued behind the batch (a trie delta upload) does not hold it
+    hipEvent_t ev_end = nullptr;
+    bool end_recorded = false;
     // the waited result is the walk's own: row i = sfids[src[i] .. + count[i]);
     // dense = the CSR (row_off, ids) has been built from it since the last launch
     bool dense = false;
@@ -570,7 +574,9 @@ struct tm_batch {
         if (ev_read) (void)hipEventDestroy(ev_read);
         if (evc0) (void)hipEventDestroy(evc0);
         if (evc1) (void)hipEventDestroy(evc1);
-        ev0 = ev1 = ev2 = evt = ev_read = evc0 = evc1 = nullptr;
+        if (ev_end) (void)hipEventDestroy(ev_end);
+        ev0 = ev1 = ev2 = evt = ev_read = evc0 = evc1 = ev_end = nullptr;
+        end_recorded = false;
         if (gexec) (void)hipGraphExecDestroy(gexec);
         gexec = nullptr;
         gkey.clear();
@@ -1284,7 +1290,9 @@ struct tm_engine {
     void write_summary(uint32_t c) {
         if (c == ROOT) return;   // root record is rebuilt at every launch
         if (tl_mut && tl_mut->defer) {   // phase 1 of a parallel batch: rewritten in phase 2
-            tl_mut->sum.push_back(c);
+            // (a node made by this batch has no slot yet: phase 2's insert_edge
+            // writes its summary, from the final record)
+            if (nd[c].inslot != NONE) tl_mut->sum.push_back(c);
             return;
         }
         const uint32_t i = nd[c].inslot;
@@ -1542,6 +1550,7 @@ struct tm_engine {
     std::unordered_map<uint64_t, uint32_t> shared_made[64];
     WorkPool pool;            // workers of parallel batches (started at the first one)
     std::vector<Mut> mut_w;   // their states (reset per batch, capacity kept)
+    std::vector<std::vector<uint32_t>> parts_buf;   // a parallel batch's parts (capacity kept)
     bool pool_started = false;
 
     struct PlanEnt {
@@ -1652,7 +1661,7 @@ struct tm_engine {
 
     void make_plan(const uint8_t* buf, const uint64_t* offs, uint32_t n, bool del) {
         plan.resize(n);
-        const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 512));
+        const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 256));
         if (plan_words.size() < nt) plan_words.resize(nt);
         if (plan_tw.size() < nt) plan_tw.resize(nt);
         if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
@@ -1735,7 +1744,7 @@ struct tm_engine {
     // Filter / node ids therefore differ from a serial run's (ids are the
     // engine's own), the trie and its HBM image are the same.
     static constexpr uint32_t PAR_MIN = 2048;
-    static constexpr uint32_t PAR_RANGE_MIN = 65536;   // buckets per phase-2 range at least
+    static constexpr uint32_t PAR_RANGE_MIN = 4096;    // buckets per phase-2 range at least (>> max_disp)
 
     static uint32_t mix_word(uint32_t w) {
         uint64_t k = (uint64_t)w * 0x9E3779B97F4A7C15ull;
@@ -1758,6 +1767,15 @@ struct tm_engine {
             const uint32_t s = nd[v[q + 8]].inslot;
             if (s != NONE && s < slots.size()) __builtin_prefetch(&slots[s], 1);
         }
+    }
+
+    // per-range states of the edge phase: at least k of them, fresh, their
+    // vectors' capacity kept across batches (the rest stay merged-empty)
+    std::vector<Mut> edge_w;
+    std::vector<Mut>& edge_states(size_t k) {
+        if (edge_w.size() < k) edge_w.resize(k);
+        for (size_t i = 0; i < k; ++i) edge_w[i].reset();
+        return edge_w;
     }
 
     // Phase 2: the recorded edge work of W, by bucket range (see above).
@@ -1785,8 +1803,11 @@ struct tm_engine {
         unsigned T2 = 0;
         uint32_t RS = 0, R = 0;
         // ---- deletes, bucketed by the slot recorded in phase 1 (nothing has moved since)
+        size_t ndel = 0;
+        for (Mut& m : W) ndel += m.del.size();
         ranges(T2, RS, R);
-        if (!T2) {
+        if (!ndel) {
+        } else if (!T2) {
             for (Mut& m : W)
                 for (const auto& d : m.del) delete_edge_of(d.first);
         } else {
@@ -1798,7 +1819,7 @@ struct tm_engine {
                     if (R % 2 && r == R - 1) tail.push_back(d.first);   // (R odd: the last range wraps onto range 0)
                     else per[r].push_back(d.first);
                 }
-            std::vector<Mut> X(T2);
+            std::vector<Mut>& X = edge_states(T2);
             std::vector<std::vector<uint32_t>> late(T2);
             for (uint32_t par = 0; par < 2; ++par)
                 pool.run([&](unsigned t) {
@@ -1830,7 +1851,8 @@ struct tm_engine {
         }
         const auto e2 = now();
         ranges(T2, RS, R);
-        if (!T2) {
+        if (!nins) {
+        } else if (!T2) {
             for (Mut& m : W)
                 for (const auto& e : m.ins) insert_edge(e[0], e[1], e[2]);
         } else {
@@ -1843,7 +1865,7 @@ struct tm_engine {
                     if (R % 2 && r == R - 1) tail.push_back(e);
                     else per[r].push_back(e);
                 }
-            std::vector<Mut> X(T2);
+            std::vector<Mut>& X = edge_states(T2);
             for (uint32_t par = 0; par < 2; ++par)
                 pool.run([&](unsigned t) {
                     if (t >= T2) return;
@@ -1869,7 +1891,7 @@ struct tm_engine {
         std::vector<std::vector<uint32_t>> per(TS);
         for (Mut& m : W)
             for (uint32_t c : m.sum) per[mix_word(c) % TS].push_back(c);
-        std::vector<Mut> X(TS);
+        std::vector<Mut>& X = edge_states(TS);
         pool.run([&](unsigned t) {
             if (t >= TS) return;
             std::vector<uint32_t>& v = per[t];
@@ -1926,13 +1948,14 @@ struct tm_engine {
         ensure_pool();
         const auto ts0 = std::chrono::steady_clock::now();
         if (mut_w.size() != T) mut_w.resize(T);
-        for (Mut& m : mut_w) m.reset();
-        std::vector<Mut>& W = mut_w;
+        std::vector<Mut>& W = mut_w;   // (each worker resets its own state when phase 1 starts)
         // by the first two words: one worker owns those subtrees; 8 parts per
         // worker, taken largest first by whichever worker is free (skewed
         // churn clusters under a few first words)
         const uint32_t P = 8 * T;
-        std::vector<std::vector<uint32_t>> parts(P);
+        std::vector<std::vector<uint32_t>>& parts = parts_buf;   // (capacity kept across batches)
+        parts.resize(P);
+        for (auto& v : parts) v.clear();
         for (uint32_t i = 0; i < n; ++i) {
             const PlanEnt& pe = plan[i];
             const uint32_t* w = plan_words[pe.part].data() + pe.woff;
@@ -1989,18 +2012,17 @@ struct tm_engine {
             }
             if (!full_f_dirty && dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
         }
-        for (Mut& m : W) {
+        // (shared_made was cleared at the end of the previous batch)
+        const auto tp0 = std::chrono::steady_clock::now();
+        // phase 1: node records, by first word
+        pool.run([&](unsigned t) {
+            Mut& m = W[t];
+            m.reset();
             m.ids = &ids;
             m.next_id = &next_id;
             m.n_free = ids.size();
             m.n_fresh = fresh;
             m.fresh_base = base;
-        }
-        for (auto& sm : shared_made) sm.clear();
-        const auto tp0 = std::chrono::steady_clock::now();
-        // phase 1: node records, by first word
-        pool.run([&](unsigned t) {
-            Mut& m = W[t];
             m.defer = true;
             tl_mut = &m;
             const auto tw0 = std::chrono::steady_clock::now();
@@ -2059,6 +2081,7 @@ struct tm_engine {
         pool.run([&](unsigned t) {   // filter byte offsets: distinct nodes per worker
             for (unsigned j = t; j < T; j += pool.n)
                 for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+            for (unsigned j = t; j < 64; j += pool.n) shared_made[j].clear();   // for the next batch
         });
         if (!del) {   // ids not handed out: free ones back to the list, the fresh tail cut off
             // (the rest of each worker's last chunk: free-list ids go back; fresh
@@ -3166,6 +3189,7 @@ struct tm_engine {
             HIP_OK(hipEventCreate(&b->evt));
             HIP_OK(hipEventCreate(&b->evc0));
             HIP_OK(hipEventCreate(&b->evc1));
+            HIP_OK(hipEventCreateWithFlags(&b->ev_end, hipEventDisableTiming));
         }
         return TM_OK;
     }
@@ -3455,31 +3479,26 @@ struct tm_engine {
         s.row_off = b->d_rowoff; s.ids = b->d_ids; s.block_sums = b->d_bsums;
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? R.d_dbg : nullptr;
+        b->end_recorded = false;
+        int grc = 1;
         if (graph) {
-            int rc2 = launch_graph(b, a, s, S);
-            if (rc2 != 1) {
-                if (rc2) return rc2;
-                note_launch(b);
-                b->launched = true;
-                b->done = false;
-                b->dense = false;
-                b->csr = true;
-                b->scan_args = s;
-                return TM_OK;
-            }
-            HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
+            grc = launch_graph(b, a, s, S);
+            if (grc != 1 && grc) return grc;
+            if (grc == 1) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
         }
-        HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        if (grc == 1) HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
         note_launch(b);
         b->launched = true;
         b->done = false;
         b->dense = false;
         b->csr = csr;
         if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
-        HIP_OK(enqueue_csr(b, s, S));
+        if (grc == 1) HIP_OK(enqueue_csr(b, s, S));   // (the graph holds it)
         b->scan_args = s;
         if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
+        HIP_OK(hipEventRecord(b->ev_end, S));
+        b->end_recorded = true;
         return TM_OK;
     }
 
@@ -3653,7 +3672,10 @@ struct tm_engine {
             drained = false;
         }
         for (int attempt = 0;; ++attempt) {
-            if (!drained || attempt) HIP_OK(hipStreamSynchronize(S));
+            if (!drained || attempt) {
+                if (b->end_recorded) HIP_OK(hipEventSynchronize(b->ev_end));
+                else HIP_OK(hipStreamSynchronize(S));
+            }
             if (attempt && relaunched) ++*relaunched;
             if (b->check_tokens && b->n && b->h_bad[1]) {
                 snprintf(last_error(), 512, "token batch failed the device check (word offsets or flags)");
