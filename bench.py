@@ -468,7 +468,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
     for _ in range(steps):
         dels, adds = churn.step(n_deltas)
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
-    ms_match, ms_churn, ms_walk, ms_tok = [], [], [], []
+    ms_match, ms_churn, ms_walk, ms_tok, ms_queue = [], [], [], [], []
     ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
     t0 = time.perf_counter()
     tc = time.perf_counter()
@@ -493,6 +493,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
         ms_match.append(st["ms_total"])
         ms_walk.append(st["ms_match"])
         ms_tok.append(st["ms_tokenize"])
+        ms_queue.append(st["ms_queue"])
         if i + 1 < steps:
             tc = time.perf_counter()
             b.launch()
@@ -511,6 +512,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
         "deltas_per_step": n_deltas, "filters": len(allf), "publishes": n, "distinct_topics": int(n_rows),
         "device_ms": float(np.mean(ms_match)), "device_walk_ms": float(np.mean(ms_walk)),
         "device_tokenize_ms": float(np.mean(ms_tok)),
+        "device_queue_ms": float(np.mean(ms_queue)),
         "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
         "host_ms": {k: float(np.mean(v)) if v else 0.0 for k, v in ms_host.items()},
         "churn_overlapped_with_device": True,
@@ -549,6 +551,7 @@ def run_c5(args, ws, rank, local, sync):
         "churn_apply_ms": leg["churn_ms"],
         "churn_overlapped_with_device": True,
         "host_ms": leg["host_ms"],
+        "device_queue_ms": leg["device_queue_ms"],
         "matches_delivered_per_step": leg["matches_delivered_per_step"],
         "generic_path_topics": leg["generic_path_topics"],
         "uploads_delta": leg["uploads_delta"],

@@ -462,6 +462,7 @@ struct tm_batch {
     // so work queued behind the batch (a trie delta upload) does not hold it
     hipEvent_t ev_end = nullptr;
     bool end_recorded = false;
+    hipEvent_t evq = nullptr;   // at the launch call: evq..ev0 (or evt) is the queueing ahead of it
     // the waited result is the walk's own: row i = sfids[src[i] .. + count[i]);
     // dense = the CSR (row_off, ids) has been built from it since the last launch
     bool dense = false;
@@ -575,7 +576,8 @@ struct tm_batch {
         if (evc0) (void)hipEventDestroy(evc0);
         if (evc1) (void)hipEventDestroy(evc1);
         if (ev_end) (void)hipEventDestroy(ev_end);
-        ev0 = ev1 = ev2 = evt = ev_read = evc0 = evc1 = ev_end = nullptr;
+        if (evq) (void)hipEventDestroy(evq);
+        ev0 = ev1 = ev2 = evt = ev_read = evc0 = evc1 = ev_end = evq = nullptr;
         end_recorded = false;
         if (gexec) (void)hipGraphExecDestroy(gexec);
         gexec = nullptr;
@@ -917,11 +919,9 @@ struct tm_engine {
         uint32_t inslot = NONE;          // edge-hash slot of the incoming edge
         uint8_t live = 0, topic = 0;
         uint8_t hasbytes = 0;            // n_foff / n_flen name this id's filter (until the id is reused)
-        uint8_t pad = 0;
         // literal children per signature bit (lsig_pos of their words),
         // saturating: a count that reached 255 keeps its bit set for good
         uint8_t lcnt[LSIG_BITS] = {};
-        uint8_t pad2[4 - LSIG_BITS] = {};
         uint32_t lsig() const {
             uint32_t s = 0;
             for (uint32_t i = 0; i < LSIG_BITS; ++i) s |= lcnt[i] ? 1u << i : 0u;
@@ -1011,7 +1011,7 @@ struct tm_engine {
         for (uint32_t i = 0; i <= max_disp; ++i) {
             for (uint32_t s = 0; s < BUCKET; ++s) {
                 const Slot& e = slots[b * BUCKET + s];
-                if (e.parent == p && (e.word & WID_MASK) == w) return b * BUCKET + s;
+                if ((e.parent & ID_MASK) == p && (e.word & WID_MASK) == w) return b * BUCKET + s;
             }
             if (slots[b * BUCKET + BUCKET - 1].parent == SLOT_EMPTY) return NONE;
             b = (b + 1 == nb) ? 0 : b + 1;
@@ -1047,10 +1047,10 @@ struct tm_engine {
         uint32_t md = 0;
         uint64_t used = 0;
         for (const Slot& e : slots) {
-            if (e.parent == SLOT_EMPTY || e.parent == SLOT_TOMB) continue;
+            if (e.parent == SLOT_EMPTY) continue;
             uint32_t disp;
             bool was_empty;
-            uint32_t i = place_slot(tab, e.parent, e.word & WID_MASK, disp, was_empty);
+            uint32_t i = place_slot(tab, e.parent & ID_MASK, e.word & WID_MASK, disp, was_empty);
             tab[i] = e;
             nd[e.child & ID_MASK].inslot = i;
             md = std::max(md, disp);
@@ -1165,7 +1165,7 @@ struct tm_engine {
                 const uint32_t j = cb * BUCKET + k;
                 const Slot& e = slots[j];
                 if (e.parent == SLOT_EMPTY) break;
-                const uint32_t h = home_bucket(e.parent, e.word & WID_MASK, nb);
+                const uint32_t h = home_bucket(e.parent & ID_MASK, e.word & WID_MASK, nb);
                 // the run of e goes h .. cb; it crosses hb iff hb lies in [h, cb)
                 const uint32_t dist_e = (cb + nb - h) % nb, dist_hole = (cb + nb - hb) % nb;
                 if (dist_e >= dist_hole) {
@@ -1298,7 +1298,7 @@ struct tm_engine {
         const uint32_t i = nd[c].inslot;
         if (i == NONE) return;
         Slot& e = slots[i];
-        e.word = (e.word & WID_MASK) | (nd[c].lsig() << WID_BITS);
+        slot_set_lsig(e, nd[c].lsig());
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
         e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
@@ -1915,7 +1915,7 @@ struct tm_engine {
     void write_summary_at(uint32_t c, std::vector<uint32_t>& dl) {
         const uint32_t i = nd[c].inslot;
         Slot& e = slots[i];
-        e.word = (e.word & WID_MASK) | (nd[c].lsig() << WID_BITS);
+        slot_set_lsig(e, nd[c].lsig());
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
         e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
@@ -3190,6 +3190,7 @@ struct tm_engine {
             HIP_OK(hipEventCreate(&b->evc0));
             HIP_OK(hipEventCreate(&b->evc1));
             HIP_OK(hipEventCreateWithFlags(&b->ev_end, hipEventDisableTiming));
+            HIP_OK(hipEventCreate(&b->evq));
         }
         return TM_OK;
     }
@@ -3403,6 +3404,7 @@ struct tm_engine {
             if ((rc = tokenize(b))) return rc;
             if ((rc = upload_batch(b))) return rc;
         }
+        if (csr) HIP_OK(hipEventRecord(b->evq, S));   // (before the delta upload and the waits below)
         if ((rc = sync_device(&R))) return rc;
         if (b->own && b->seen_upload != R.upload_seq) {   // trie deltas still in flight on the replica stream land first
             HIP_OK(hipStreamWaitEvent(S, R.ev_sync, 0));
@@ -3646,6 +3648,9 @@ struct tm_engine {
         (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
         if (b->tok_timed) (void)hipEventElapsedTime(&ms_tok, b->evt, b->ev0);
         b->st.ms_tokenize = ms_tok;
+        float ms_q = 0;
+        (void)hipEventElapsedTime(&ms_q, b->evq, b->tok_timed ? b->evt : b->ev0);
+        b->st.ms_queue = ms_q;
         b->st.ms_csr = 0;   // set by ensure_dense
         b->st.topics = b->n;
         b->st.visits = b->h_stats[ST_VISITS];
@@ -5342,12 +5347,13 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
         for (uint32_t k = 0; k < BUCKET; ++k) {
             const Slot& sl = e->slots[b * BUCKET + k];
             if (sl.parent == SLOT_EMPTY) { hole = true; continue; }
-            if (hole || sl.parent == SLOT_TOMB) {
+            if (hole) {
                 snprintf(last_error(), 512, "bucket %u not filled in order", b);
                 return TM_EIO;
             }
             ++live;
-            const uint32_t h = home_bucket(sl.parent, sl.word & WID_MASK, nb);
+            const uint32_t sp = sl.parent & ID_MASK;
+            const uint32_t h = home_bucket(sp, sl.word & WID_MASK, nb);
             const uint32_t d = (b + nb - h) % nb;
             md = std::max<uint64_t>(md, d);
             if (d > e->max_disp) {
@@ -5359,21 +5365,21 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
                     snprintf(last_error(), 512, "run of slot %u (home %u) broken at bucket %u", b * BUCKET + k, h, x);
                     return TM_EIO;
                 }
-            if (e->find_slot(sl.parent, sl.word & WID_MASK) != b * BUCKET + k || e->nd[sl.child & ID_MASK].inslot != b * BUCKET + k) {
+            if (e->find_slot(sp, sl.word & WID_MASK) != b * BUCKET + k || e->nd[sl.child & ID_MASK].inslot != b * BUCKET + k) {
                 snprintf(last_error(), 512, "slot %u not found by its key", b * BUCKET + k);
                 return TM_EIO;
             }
             // the child's literal signature: the node's own, and the parent's
             // covers this edge's word (a clear bit must prove the edge absent)
             const uint32_t c = sl.child & ID_MASK, w = sl.word & WID_MASK;
-            if ((sl.word >> WID_BITS) != e->nd[c].lsig()) {
+            if (slot_lsig(sl.parent, sl.word) != e->nd[c].lsig()) {
                 snprintf(last_error(), 512, "slot %u: literal signature %u, node %u has %u", b * BUCKET + k,
-                         sl.word >> WID_BITS, c, e->nd[c].lsig());
+                         slot_lsig(sl.parent, sl.word), c, e->nd[c].lsig());
                 return TM_EIO;
             }
-            if (sl.parent != ROOT && w != W_PLUS && w != W_HASH) {
-                const uint32_t pi = e->nd[sl.parent].inslot;
-                if (pi == NONE || !((e->slots[pi].word >> WID_BITS) >> lsig_pos(w) & 1u)) {
+            if (sp != ROOT && w != W_PLUS && w != W_HASH) {
+                const uint32_t pi = e->nd[sp].inslot;
+                if (pi == NONE || !(slot_lsig(e->slots[pi].parent, e->slots[pi].word) >> lsig_pos(w) & 1u)) {
                     snprintf(last_error(), 512, "slot %u: word %u missing from its parent's literal signature",
                              b * BUCKET + k, w);
                     return TM_EIO;

@@ -10,8 +10,7 @@ struct tm_batch;
 namespace etm {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t SLOT_EMPTY = 0xFFFFFFFFu;   // slot.parent of a never-used slot
-constexpr uint32_t SLOT_TOMB = 0xFFFFFFFEu;    // slot.parent of a deleted edge
+constexpr uint32_t SLOT_EMPTY = 0xFFFFFFFFu;   // slot.parent of a free slot (never a live slot's: ids < ID_MASK)
 constexpr uint32_t ROOT = 0;                   // node id of the atom `root`
 
 // Interned word ids (low 29 bits of a topic word entry).  '' is a regular word
@@ -58,20 +57,29 @@ constexpr uint32_t B_HASH = 1u << 31;            // hash word: child has a '#' c
 // carrying the CHILD's summary, so one 64-B bucket read per visited node is all
 // the walk needs.  16 B; four slots per 64-B bucket.
 //
-// The word's top 3 bits (word ids are < 2^29) carry the child's LITERAL-CHILD
+// The key's spare bits -- the word's top 3 (word ids are < 2^29) and the
+// parent's top 2 (node ids are < 2^30) -- carry the child's 5-bit LITERAL-CHILD
 // SIGNATURE: bit lsig_pos(w) is set for every literal word w under the child
 // (not '+' / '#').  A clear bit proves the literal edge absent, so the walk
 // skips that probe -- a third of the literal probes on C2 miss, and the
-// signature settles ~35% of those without a bucket read.
+// signature settles ~45% of those without a bucket read.
 struct alignas(16) Slot {
-    uint32_t parent;   // key hi; SLOT_EMPTY / SLOT_TOMB
-    uint32_t word;     // key lo (low WID_BITS) | child's literal signature << WID_BITS
+    uint32_t parent;   // key hi: parent id | signature bits 3-4 << ID_BITS; SLOT_EMPTY when free
+    uint32_t word;     // key lo: word id | signature bits 0-2 << WID_BITS
     uint32_t child;    // child id | B_TOPIC | B_PLUS
     uint32_t hash;     // id of child/'#' (or ID_MASK) | B_HTERM | B_HASH
 };
-constexpr uint32_t LSIG_BITS = 32 - WID_BITS;
+constexpr uint32_t LSIG_WBITS = 32 - WID_BITS;              // signature bits in the word field
+constexpr uint32_t LSIG_BITS = LSIG_WBITS + (32 - ID_BITS);   // 5
 __host__ __device__ inline uint32_t lsig_pos(uint32_t w) {
     return (uint32_t)(((uint64_t)(w * 0x9E3779B1u) * LSIG_BITS) >> 32);
+}
+__host__ __device__ inline uint32_t slot_lsig(uint32_t parent_field, uint32_t word_field) {
+    return (word_field >> WID_BITS) | ((parent_field >> ID_BITS) << LSIG_WBITS);
+}
+__host__ __device__ inline void slot_set_lsig(Slot& e, uint32_t sig) {
+    e.word = (e.word & WID_MASK) | ((sig & ((1u << LSIG_WBITS) - 1u)) << WID_BITS);
+    e.parent = (e.parent & ID_MASK) | ((sig >> LSIG_WBITS) << ID_BITS);
 }
 static_assert(sizeof(Slot) == 16, "slot is 16 bytes");
 constexpr uint32_t BUCKET = 4;   // slots per 64-B bucket

@@ -122,11 +122,11 @@ __device__ __forceinline__ bool probe(const MatchArgs& a, uint32_t parent, uint3
             const uint4* q = reinterpret_cast<const uint4*>(a.slots) + si;
             s0 = q[0]; s1 = q[1]; s2 = q[2]; s3 = q[3];
         }
-        // (the word's top bits are the child's literal signature)
-        const bool m0 = s0.x == parent && (s0.y & WID_MASK) == word;
-        const bool m1 = s1.x == parent && (s1.y & WID_MASK) == word;
-        const bool m2 = s2.x == parent && (s2.y & WID_MASK) == word;
-        const bool m3 = s3.x == parent && (s3.y & WID_MASK) == word;
+        // (the key's top bits are the child's literal signature)
+        const bool m0 = (s0.x & ID_MASK) == parent && (s0.y & WID_MASK) == word;
+        const bool m1 = (s1.x & ID_MASK) == parent && (s1.y & WID_MASK) == word;
+        const bool m2 = (s2.x & ID_MASK) == parent && (s2.y & WID_MASK) == word;
+        const bool m3 = (s3.x & ID_MASK) == parent && (s3.y & WID_MASK) == word;
         const uint32_t hz = m0 ? s0.z : m1 ? s1.z : m2 ? s2.z : s3.z;
         const uint32_t hw = m0 ? s0.w : m1 ? s1.w : m2 ? s2.w : s3.w;
         if (m0 | m1 | m2 | m3) {
@@ -532,11 +532,11 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         // word ids never equal the marks.
 #pragma unroll
         for (uint32_t r = 0; r < 4; ++r) {
-            const bool m = rp[r] != SLOT_EMPTY && sl[r].x == rp[r] && (sl[r].y & WID_MASK) == rw[r];
+            const bool m = rp[r] != SLOT_EMPTY && (sl[r].x & ID_MASK) == rp[r] && (sl[r].y & WID_MASK) == rw[r];
             if (m) {
                 L.q[qn + 16 * r + qd].x = sl[r].z;
                 L.q[qn + 16 * r + qd].y = sl[r].w;
-                L.q[qn + 16 * r + qd].z = Q_FOUND | (sl[r].y >> WID_BITS);
+                L.q[qn + 16 * r + qd].z = Q_FOUND | slot_lsig(sl[r].x, sl[r].y);
             }
             if (qs == 3 && sl[r].x == SLOT_EMPTY) L.q[qn + 16 * r + qd].w = Q_TAIL;   // out-of-range loads read 0
         }
@@ -999,23 +999,38 @@ __global__ __launch_bounds__(SCAN_BLOCK) void tm_scan_sums(ScanArgs a, uint32_t 
 
 // Pass 3: one wavefront per tile of 64 topics.  Finishes the CSR offsets and
 // copies the tile's sorted rows from the staging region.  A tile whose rows were
-// staged as one run (no slow-path topic in it) is one contiguous copy, four
-// coalesced dword loads in flight per lane; otherwise each topic is copied on its own.
+// staged as one run (no slow-path topic in it) is one contiguous copy, FIN_U
+// coalesced dword loads in flight per lane; otherwise each topic is copied on
+// its own.  The next tile's (count, src, offset) are loaded before this tile's
+// copy, so a tile costs the copy's round trips, not one more for its header.
 template <bool CK>
 __global__ __launch_bounds__(64) void tm_finalize(ScanArgs a) {
     const uint32_t lane = threadIdx.x;
     const uint32_t ntiles = (a.n + TILE - 1) / TILE;
+    uint32_t nc = 0, noff = 0, nbs = 0;
+    uint64_t ns = 0;
+    auto meta = [&](uint32_t tile) {
+        const uint32_t t = tile * TILE + lane;
+        if (tile < ntiles && t < a.n) {
+            nc = a.count[t];
+            ns = a.src[t];
+            noff = a.row_off[t];
+            nbs = a.block_sums[t / SCAN_TILE];
+        }
+    };
+    meta(blockIdx.x);
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint32_t t = tile * TILE + lane;
         const bool valid = t < a.n;
         uint32_t c = 0, off = 0;
         uint64_t s = 0;
         if (valid) {
-            c = a.count[t];
-            s = a.src[t];
-            off = a.row_off[t] + a.block_sums[t / SCAN_TILE];
+            c = nc;
+            s = ns;
+            off = noff + nbs;
             a.row_off[t] = off;      // finish the CSR offsets (scan pass 1 was block-local)
         }
+        meta(tile + gridDim.x);
         const bool any = c > 0;
         const uint64_t m = __ballot(any);
         if (!m) continue;

@@ -99,6 +99,7 @@ typedef struct {
     float    ms_tokenize;   /* device tokeniser time of the last launch (0: tokens reused) */
     uint64_t probes;        /* 64-B edge-hash bucket reads of the tile walk (hits + misses) */
     float    ms_csr;        /* device time of the last dense-CSR build (scan + copy; 0: not built) */
+    float    ms_queue;      /* device time from the last launch call to its pipeline's start (work queued ahead) */
 } tm_batch_stats;
 
 typedef struct {
