@@ -1075,7 +1075,10 @@ def main():
                      "alg_bytes_per_launch": alg_bytes,
                      "per_publish": {"V": st["visits"] / n, "H": st["hash_hits"] / n,
                                      "d": st["words"] / n, "M": st["matches"] / n,
-                                     "bucket_reads": st["probes"] / n}},
+                                     "bucket_reads": st["probes"] / n},
+                     # frontier iterations: each pops <= 64 probes and waits for their reads
+                     "iterations_per_tile": st["iterations"] / max(1, -(-n // 64)),
+                     "probes_per_iteration": st["probes"] / max(1, st["iterations"])},
         "pipeline_ms": float(np.mean(ms_total)),
         "pipeline_fresh_ms": float(np.median(fresh_ms)),
         "tokenize_ms": float(np.median(fresh_tok)),

@@ -81,7 +81,7 @@ class BatchStats(C.Structure):
                 ("words", C.c_uint64), ("matches", C.c_uint64), ("slow_topics", C.c_uint64),
                 ("overflow_tiles", C.c_uint64), ("ms_match", C.c_float), ("ms_total", C.c_float),
                 ("ms_tokenize", C.c_float), ("probes", C.c_uint64),
-                ("ms_csr", C.c_float), ("ms_queue", C.c_float)]
+                ("ms_csr", C.c_float), ("ms_queue", C.c_float), ("iterations", C.c_uint64)]
 
     def asdict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

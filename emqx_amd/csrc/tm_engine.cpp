@@ -940,6 +940,10 @@ struct tm_engine {
     std::vector<NodeRec, HugeAlloc<NodeRec>> nd;
     std::vector<uint32_t> n_flen;
     std::vector<uint64_t> n_foff;
+    // 30-bit Bloom filter of each node's literal children (lext_pos), carried
+    // in its slot's '#'-id field when it has no '#' child; only grows between
+    // re-packs (rebuild_lext)
+    std::vector<uint32_t> n_lext;
     std::vector<uint32_t> free_nodes;
     // A freed node id (== filter id) is not reused while a batch launched
     // before the free may still hand it out: results are read (ids mapped to
@@ -1036,6 +1040,20 @@ struct tm_engine {
             }
             b = (b + 1 == nb) ? 0 : b + 1;
         }
+    }
+
+    // the 30-bit literal signatures from the edges as they are (clears the
+    // stale bits deletes leave); the slots change: callers upload in full
+    void rebuild_lext() {
+        std::fill(n_lext.begin(), n_lext.end(), 0u);
+        for (const Slot& e : slots) {
+            if (e.parent == SLOT_EMPTY) continue;
+            const uint32_t w = e.word & WID_MASK;
+            if (w != W_PLUS && w != W_HASH) n_lext[e.parent & ID_MASK] |= 1u << lext_pos(w);
+        }
+        for (Slot& e : slots)
+            if (e.parent != SLOT_EMPTY && !(e.hash & B_HASH)) e.hash = n_lext[e.child & ID_MASK];
+        full_dirty = true;
     }
 
     // rebuild at load <= 0.6 (any bucket count: home_bucket is multiply-shift)
@@ -1230,6 +1248,7 @@ struct tm_engine {
             nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
             nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
             for (uint8_t& k : nd[id].lcnt) k = 0;
+            n_lext[id] = 0;
             ++M->live_nodes;
             return id;
         }
@@ -1244,10 +1263,12 @@ struct tm_engine {
             nd.push_back(NodeRec{});
             n_flen.push_back(0);
             n_foff.push_back(0);
+            n_lext.push_back(0);
         }
         nd[id].parent = parent; nd[id].word = word; nd[id].ec = 0; nd[id].plus = NONE; nd[id].hash = NONE;
         nd[id].inslot = NONE; nd[id].live = 1; nd[id].topic = 0;
         for (uint8_t& k : nd[id].lcnt) k = 0;
+        n_lext[id] = 0;
         ++live_nodes;
         return id;
     }
@@ -1301,7 +1322,7 @@ struct tm_engine {
         slot_set_lsig(e, nd[c].lsig());
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
-        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
+        e.hash = h != NONE ? h | (nd[h].topic ? B_HTERM : 0u) | B_HASH : n_lext[c];
         mark_dirty(i);
     }
 
@@ -1460,7 +1481,10 @@ struct tm_engine {
                 ++nd[p].ec;
                 if (w == W_PLUS) nd[p].plus = c;
                 else if (w == W_HASH) nd[p].hash = c;
-                else nd[p].lsig_add(w);
+                else {
+                    nd[p].lsig_add(w);
+                    n_lext[p] |= 1u << lext_pos(w);
+                }
                 insert_edge(p, w, c);
                 if (M && M->defer && k < sd) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
                 write_summary(p);
@@ -1918,7 +1942,7 @@ struct tm_engine {
         slot_set_lsig(e, nd[c].lsig());
         e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
         const uint32_t h = nd[c].hash;
-        e.hash = (h != NONE ? h : ID_MASK) | ((h != NONE && nd[h].topic) ? B_HTERM : 0u) | (h != NONE ? B_HASH : 0u);
+        e.hash = h != NONE ? h | (nd[h].topic ? B_HTERM : 0u) | B_HASH : n_lext[c];
         if (full_dirty) return;
         const uint64_t m = 1ull << (i & 63);
         if (!(__atomic_fetch_or(&dirty_mark[i >> 6], m, __ATOMIC_RELAXED) & m)) dl.push_back(i);
@@ -2008,6 +2032,7 @@ struct tm_engine {
             if (fresh) {
                 nd.resize(base + fresh);   // dead records until handed out; the unused tail is cut after
                 n_flen.resize(base + fresh, 0);
+                n_lext.resize(base + fresh, 0);
                 n_foff.resize(base + fresh, 0);
             }
             if (!full_f_dirty && dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
@@ -2098,6 +2123,7 @@ struct tm_engine {
             if (fresh_used < fresh) {
                 nd.resize(base + fresh_used);
                 n_flen.resize(base + fresh_used);
+                n_lext.resize(base + fresh_used);
                 n_foff.resize(base + fresh_used);
                 if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
             }
@@ -2629,7 +2655,10 @@ struct tm_engine {
         }
         // after a bulk build or heavy churn, re-pack the host table to the
         // target load so the walk's working set stays small (a full upload)
-        if (needs_repack()) rehash((size_t)(live_edges / target_load));
+        if (needs_repack()) {
+            rehash((size_t)(live_edges / target_load));
+            rebuild_lext();   // (a full upload follows the re-pack anyway)
+        }
         const size_t nn = nd.size();
         // gather the deltas once
         const bool slots_full = full_dirty || dirty.size() > slots.size() / 8;
@@ -3659,6 +3688,7 @@ struct tm_engine {
         b->st.matches = b->h_stats[ST_MATCHES];
         b->st.slow_topics = b->h_stats[ST_SLOW];
         b->st.probes = b->h_stats[ST_PROBES];
+        b->st.iterations = b->h_stats[ST_ITERS];
         b->st.overflow_tiles = b->h_ctrl[CTRL_NOVF];
         b->st.ms_match = ms_match;
         b->st.ms_total = ms_total;
@@ -4151,6 +4181,7 @@ struct tm_engine {
         nd.push_back(NodeRec{});
         n_flen.push_back(0);
         n_foff.push_back(0);
+        n_lext.push_back(0);
         slots.clear();
         slots.resize(1024);
         for (Slot& s : slots) { memset(&s, 0, sizeof(s)); s.parent = SLOT_EMPTY; }
@@ -5372,14 +5403,17 @@ int tm_debug_check(tm_engine* e, uint64_t* max_disp_out) {
             // the child's literal signature: the node's own, and the parent's
             // covers this edge's word (a clear bit must prove the edge absent)
             const uint32_t c = sl.child & ID_MASK, w = sl.word & WID_MASK;
-            if (slot_lsig(sl.parent, sl.word) != e->nd[c].lsig()) {
-                snprintf(last_error(), 512, "slot %u: literal signature %u, node %u has %u", b * BUCKET + k,
-                         slot_lsig(sl.parent, sl.word), c, e->nd[c].lsig());
+            if (slot_lsig(sl.parent, sl.word) != e->nd[c].lsig() ||
+                (!(sl.hash & B_HASH) && sl.hash != e->n_lext[c])) {
+                snprintf(last_error(), 512, "slot %u: literal signature %u / %#x, node %u has %u / %#x", b * BUCKET + k,
+                         slot_lsig(sl.parent, sl.word), sl.hash, c, e->nd[c].lsig(), e->n_lext[c]);
                 return TM_EIO;
             }
             if (sp != ROOT && w != W_PLUS && w != W_HASH) {
                 const uint32_t pi = e->nd[sp].inslot;
-                if (pi == NONE || !(slot_lsig(e->slots[pi].parent, e->slots[pi].word) >> lsig_pos(w) & 1u)) {
+                const Slot* ps = pi == NONE ? nullptr : &e->slots[pi];
+                if (!ps || !(slot_lsig(ps->parent, ps->word) >> lsig_pos(w) & 1u) ||
+                    (!(ps->hash & B_HASH) && !(ps->hash >> lext_pos(w) & 1u))) {
                     snprintf(last_error(), 512, "slot %u: word %u missing from its parent's literal signature",
                              b * BUCKET + k, w);
                     return TM_EIO;

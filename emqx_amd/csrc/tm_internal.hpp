@@ -67,12 +67,19 @@ struct alignas(16) Slot {
     uint32_t parent;   // key hi: parent id | signature bits 3-4 << ID_BITS; SLOT_EMPTY when free
     uint32_t word;     // key lo: word id | signature bits 0-2 << WID_BITS
     uint32_t child;    // child id | B_TOPIC | B_PLUS
-    uint32_t hash;     // id of child/'#' (or ID_MASK) | B_HTERM | B_HASH
+    uint32_t hash;     // B_HASH: id of child/'#' | B_HTERM | B_HASH; else the 30-bit literal signature
 };
 constexpr uint32_t LSIG_WBITS = 32 - WID_BITS;              // signature bits in the word field
 constexpr uint32_t LSIG_BITS = LSIG_WBITS + (32 - ID_BITS);   // 5
 __host__ __device__ inline uint32_t lsig_pos(uint32_t w) {
     return (uint32_t)(((uint64_t)(w * 0x9E3779B1u) * LSIG_BITS) >> 32);
+}
+// A child with no '#' child leaves the slot's '#'-id field free: it then holds
+// a 30-bit Bloom filter of the same literal words (bit lext_pos(w)), set as
+// children arrive and rebuilt exactly when the table is re-packed -- a stale
+// bit costs one probe, never a match.
+__host__ __device__ inline uint32_t lext_pos(uint32_t w) {
+    return (uint32_t)(((uint64_t)(w * 0x85EBCA6Bu) * 30u) >> 32);
 }
 __host__ __device__ inline uint32_t slot_lsig(uint32_t parent_field, uint32_t word_field) {
     return (word_field >> WID_BITS) | ((parent_field >> ID_BITS) << LSIG_WBITS);
@@ -129,7 +136,8 @@ constexpr uint32_t ERR_CSR_RANGE = 8;    // the batch's match count does not fit
 constexpr uint64_t MAX_RESULT = 0xFFFFFFF0ull;
 
 
-enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_PROBES = 5, ST_N = 8 };
+enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_PROBES = 5, ST_ITERS = 6,
+                          ST_N = 8 };
 
 // The batch header block: ctrl (CTRL_WORDS u32) | stats (ST_N u64) | one
 // 128-B line per walk group (see TICKET_GROUPS): u32 tail ticket at +0, u64

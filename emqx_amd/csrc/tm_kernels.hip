@@ -483,7 +483,7 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         const uint32_t k = min(qn, 64u);
         const bool has = lane < k;
         qn -= k;
-        tP += lane == 0 ? k : 0u;   // bucket reads (hits, misses, continuations)
+        tP += lane == 0 ? k + (1u << 20) : 0u;   // bucket reads (hits, misses, continuations) | iterations << 20
         const uint32_t idx = qn + lane;
         uint4 e = uint4{0u, 0u, 0u, 0u};
         if (has) e = L.q[idx];
@@ -580,8 +580,10 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
                 fA = s.hterm;
                 kA = key | ((uint64_t)dig_H(cls) << sh);
                 // a literal word whose signature bit is clear has no edge here
+                // (and, for a node without a '#' child, its 30-bit signature)
                 pL = id == W_HASH ? (s.flags & NF_HASH) != 0
-                                  : (id != W_UNKNOWN && id != W_PLUS && ((res.z >> lsig_pos(id)) & 1u));
+                                  : (id != W_UNKNOWN && id != W_PLUS && ((res.z >> lsig_pos(id)) & 1u) &&
+                                     ((res.y & B_HASH) || ((res.y >> lext_pos(id)) & 1u)));
                 pP = (s.flags & NF_PLUS) != 0;
             }
         }
@@ -628,7 +630,8 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         send_to_slow<CK>(a, valid && active, t);
         return;
     }
-    sV += tV; sH += tH; sW += tW; sP += tP;
+    sV += tV; sH += tH; sW += tW;
+    sP += (tP & 0xFFFFFu) | ((unsigned long long)(tP >> 20) << 40);   // probes | iterations << 40
     const uint32_t c_me = L.cnt[lane];
     const bool row_ovf = valid && active && c_me > a.row_cap;   // row longer than K
     send_to_slow<CK>(a, row_ovf, t);
@@ -715,7 +718,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
     if (lane == 0) {
         atomicAdd(&a.stats[ST_VISITS], sV); atomicAdd(&a.stats[ST_HASH], sH);
         atomicAdd(&a.stats[ST_WORDS], sW); atomicAdd(&a.stats[ST_MATCHES], sM);
-        atomicAdd(&a.stats[ST_PROBES], sP);
+        atomicAdd(&a.stats[ST_PROBES], sP & ((1ull << 40) - 1));
+        atomicAdd(&a.stats[ST_ITERS], sP >> 40);
     }
 }
 

@@ -100,6 +100,7 @@ typedef struct {
     uint64_t probes;        /* 64-B edge-hash bucket reads of the tile walk (hits + misses) */
     float    ms_csr;        /* device time of the last dense-CSR build (scan + copy; 0: not built) */
     float    ms_queue;      /* device time from the last launch call to its pipeline's start (work queued ahead) */
+    uint64_t iterations;    /* frontier iterations of the tile walk (each pops <= 64 probes) */
 } tm_batch_stats;
 
 typedef struct {
