@@ -462,6 +462,12 @@ struct tm_batch {
     // so work queued behind the batch (a trie delta upload) does not hold it
     hipEvent_t ev_end = nullptr;
     bool end_recorded = false;
+    // one-shot launch (tm_match_batch): the dense CSR is built and copied into
+    // mapped host memory behind the walk, so the batch costs one host wait
+    bool oneshot = false;
+    uint64_t x_cap = 0;             // ids the last one-shot copy could hold
+    uint8_t *h_xrow = nullptr, *h_xids = nullptr;
+    size_t c_xrow = 0, c_xids = 0;
     hipEvent_t evq = nullptr;   // at the launch call: evq..ev0 (or evt) is the queueing ahead of it
     // the waited result is the walk's own: row i = sfids[src[i] .. + count[i]);
     // dense = the CSR (row_off, ids) has been built from it since the last launch
@@ -568,6 +574,10 @@ struct tm_batch {
         if (h_rowoff) (void)hipHostFree(h_rowoff);
         if (h_ids) (void)hipHostFree(h_ids);
         h_rowoff = h_ids = nullptr;
+        if (h_xrow) (void)hipHostFree(h_xrow);
+        if (h_xids) (void)hipHostFree(h_xids);
+        h_xrow = h_xids = nullptr;
+        c_xrow = c_xids = 0;
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev2) (void)hipEventDestroy(ev2);
@@ -3528,6 +3538,7 @@ struct tm_engine {
         b->scan_args = s;
         if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
+        if (b->oneshot && (rc = enqueue_oneshot(b, S))) return rc;
         HIP_OK(hipEventRecord(b->ev_end, S));
         b->end_recorded = true;
         return TM_OK;
@@ -3550,6 +3561,46 @@ struct tm_engine {
             return e;   // ctrl + stats
         if (eager_csr) return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
         return hipSuccess;
+    }
+
+    // tm_match_batch's tail, enqueued behind the walk: scan + finalize (the
+    // dense CSR, ids up to their capacity) and its copy into mapped host
+    // memory.  wait() then finds the whole result on the host; a walk that
+    // needed a relaunch, or more ids than fit, takes result()'s path instead.
+    int enqueue_oneshot(tm_batch* b, hipStream_t S) {
+        int rc;
+        ScanArgs s = b->scan_args;
+        s.ids = b->d_ids;
+        s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
+        if ((rc = host_reserve_coherent(b->h_xrow, b->c_xrow, ((size_t)b->n + 1) * 4))) return rc;
+        if ((rc = host_reserve_coherent(b->h_xids, b->c_xids, std::max<size_t>(b->c_ids, 1) * 4))) return rc;
+        void *d_row = nullptr, *d_ids = nullptr;
+        HIP_OK(hipHostGetDevicePointer(&d_row, b->h_xrow, 0));
+        HIP_OK(hipHostGetDevicePointer(&d_ids, b->h_xids, 0));
+        b->x_cap = std::min<uint64_t>(s.ids_cap, b->c_xids / 4);
+        HIP_OK(hipEventRecord(b->evc0, S));
+        HIP_OK(launch_scan(s, S, b->d_total));
+        HIP_OK(launch_finalize(s, S, false));
+        HIP_OK(hipEventRecord(b->evc1, S));
+        HIP_OK(launch_csr_to_host(b->d_rowoff, b->d_ids, b->n, b->d_total, b->x_cap, static_cast<uint32_t*>(d_row),
+                                  static_cast<uint32_t*>(d_ids), S));
+        return TM_OK;
+    }
+
+    // the one-shot result of a waited batch, or 1 when it does not hold
+    // (staging relaunch left it stale, or more ids than the copy could hold)
+    int oneshot_result(tm_batch* b, tm_result* out) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(b->h_xrow);
+        if (!b->oneshot || !b->done || b->total > b->x_cap || row[b->n] != b->total || row[0] != 0) return 1;
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, b->evc0, b->evc1);
+        b->st.ms_csr = ms;
+        b->dense = true;
+        out->n_topics = b->n;
+        out->n_matches = b->total;
+        out->row_offsets = row;
+        out->filter_ids = reinterpret_cast<const uint32_t*>(b->h_xids);
+        return TM_OK;
     }
 
     // The dense CSR of a waited batch (row_off[n + 1], ids[total] in topic
@@ -3591,6 +3642,7 @@ struct tm_engine {
     // arguments changed (tables moved or grew, the root record, the staging
     // capacity...).  1: capture is unavailable, launch the direct way.
     static constexpr uint32_t GRAPH_MAX = 1u << 20;
+    static constexpr uint32_t ONESHOT_MAX = 1u << 20;   // tm_match_batch: one-shot result up to this many topics
     bool use_graphs = true;
     int launch_graph(tm_batch* b, const MatchArgs& a, const ScanArgs& s, hipStream_t S) {
         std::vector<uint8_t> key(sizeof(MatchArgs) + sizeof(ScanArgs));
@@ -3708,8 +3760,14 @@ struct tm_engine {
         }
         for (int attempt = 0;; ++attempt) {
             if (!drained || attempt) {
+                static const bool wtrace = getenv("TM_WAIT_TRACE") != nullptr;
+                const auto w0 = std::chrono::steady_clock::now();
+                const bool was_done = b->end_recorded && hipEventQuery(b->ev_end) == hipSuccess;
                 if (b->end_recorded) HIP_OK(hipEventSynchronize(b->ev_end));
                 else HIP_OK(hipStreamSynchronize(S));
+                if (wtrace)
+                    fprintf(stderr, "[wait] done before: %d, sync %.1f us\n", (int)was_done,
+                            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count());
             }
             if (attempt && relaunched) ++*relaunched;
             if (b->check_tokens && b->n && b->h_bad[1]) {
@@ -4593,6 +4651,7 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
         bool armed = true;
         ~Drain() {
             e->upload_nosync = false;
+            R.scratch.oneshot = false;   // (the scratch batch serves other calls too)
             if (armed) (void)hipStreamSynchronize(R.stream);
         }
     } drain{e, R};
@@ -4601,8 +4660,14 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
         rc = e->prepare(&R.scratch, topics, offsets, n);
         e->upload_nosync = false;
         if (rc) return rc;
+        // latency-sized batches: CSR and its host copy enqueued with the walk
+        R.scratch.oneshot = n <= tm_engine::ONESHOT_MAX && !e->eager_csr;
         if ((rc = e->launch(&R.scratch))) return rc;
         if ((rc = e->wait(&R.scratch))) return rc;
+        if (e->oneshot_result(&R.scratch, out) == TM_OK) {
+            drain.armed = false;   // wait() synchronised past the copy
+            return TM_OK;
+        }
         rc = e->result(&R.scratch, out);
         drain.armed = rc != TM_OK;   // result() synchronised the stream
         return rc;

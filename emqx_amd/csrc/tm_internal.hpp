@@ -523,6 +523,10 @@ struct ExportArgs {
     uint64_t rcap;            // entries per group region of the staging area
 };
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
+// the dense CSR of a batch into device-visible pinned host memory: row_off[0..n]
+// and ids[0 .. min(*d_total, cap)) (tm_match_batch: one host wait per batch)
+hipError_t launch_csr_to_host(const uint32_t* row_off, const uint32_t* ids, uint32_t n, const uint32_t* d_total,
+                              uint64_t cap, uint32_t* h_row, uint32_t* h_ids, hipStream_t s);
 // dirty cuckoo slots -> the device table
 hipError_t launch_scatter_keys(DictKey* keys, const uint32_t* idx, const DictKey* vals, uint32_t n, hipStream_t s);
 

@@ -2198,6 +2198,24 @@ __global__ __launch_bounds__(256) void tm_export_host(ExportArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256) void tm_csr_to_host(const uint32_t* row_off, const uint32_t* ids, uint32_t n,
+                                                       const uint32_t* d_total, uint64_t cap, uint32_t* h_row,
+                                                       uint32_t* h_ids) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t total = min((uint64_t)*d_total, cap);
+    for (uint64_t i = i0; i <= n; i += stride) h_row[i] = row_off[i];
+    for (uint64_t i = i0; i < total; i += stride) h_ids[i] = ids[i];
+}
+
+hipError_t launch_csr_to_host(const uint32_t* row_off, const uint32_t* ids, uint32_t n, const uint32_t* d_total,
+                              uint64_t cap, uint32_t* h_row, uint32_t* h_ids, hipStream_t s) {
+    const uint64_t work = std::max<uint64_t>(cap, (uint64_t)n + 1);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((work / 8 + 255) / 256, 1), 1024);
+    hipLaunchKernelGGL(tm_csr_to_host, dim3(grid), dim3(256), 0, s, row_off, ids, n, d_total, cap, h_row, h_ids);
+    return hipGetLastError();
+}
+
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s) {
     const uint64_t work = a.hdr_words + a.n + a.rows_cap;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((work / 4 + 255) / 256, 1), 512);
