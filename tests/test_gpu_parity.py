@@ -406,3 +406,27 @@ def test_sync_async_queues_the_upload_behind_a_walk_in_flight():
     exp_new, _ = oracle_rows(F[100:], T)
     assert_same(T, rows(), exp_new)
     b.free()
+
+
+def test_match_batch_one_shot_result_and_its_fallbacks():
+    """tm_match_batch builds the CSR and copies it into mapped host memory
+    behind the walk (one host wait).  Rows far above the initial id capacity
+    (32 per topic) make the first call take the result() path (the copy could
+    not hold them) and grow it; the next call fits and is one-shot.  Both,
+    and a batch beyond the one-shot size, equal the oracle."""
+    rng = random.Random(71)
+    words = [b"a%d" % i for i in range(3)]
+    F = set()
+    for _ in range(8000):
+        F.add(b"/".join(rng.choice(words + [b"+"]) for _ in range(6)))
+    F = sorted(F | {b"#", b"+/#", b"+/+/#"})
+    T = [b"/".join(rng.choice(words) for _ in range(6)) for _ in range(2000)]
+    eng = Engine(device=0)
+    for f in F:
+        eng.insert(f)
+    exp, _ = oracle_rows(F, T)
+    assert sum(len(r) for r in exp) > 40 * len(T)   # above the initial id capacity (32 per topic)
+    for _ in range(2):
+        assert_same(T, engine_rows(eng, T), exp)
+    st = eng.stats()
+    assert st["filters"] == len(F)
