@@ -1184,7 +1184,8 @@ def main():
     if rank == 0 and ws == 1 and not args.profile and not args.no_c5:
         # config C5 in the driver's line: K = 100 and K = 10 filters per hot
         # topic, 10k subscribe/unsubscribe deltas per step
-        out["c5"] = {f"k{k}": c5_leg(k, 5, 10_000, args.topics, device=local) for k in (100, 10)}
+        # 10 steps: the last step's walk is the one not hidden behind a churn
+        out["c5"] = {f"k{k}": c5_leg(k, 10, 10_000, args.topics, device=local) for k in (100, 10)}
 
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -4893,10 +4893,18 @@ int tm_batch_wait(tm_engine* e, tm_batch* b) {
         HIP_OK(hipSetDevice(b->rep->device));
         HIP_OK(hipStreamSynchronize(b->own));
     }
+    static const bool wtrace = getenv("TM_WAIT_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::recursive_mutex> g(e->mu);
+    const auto t1 = std::chrono::steady_clock::now();
     int rc = e->use(b->rep);
     if (rc) return rc;
-    return e->wait(b);
+    rc = e->wait(b);
+    if (wtrace) {
+        auto us = [](auto a, auto c) { return std::chrono::duration<double, std::micro>(c - a).count(); };
+        fprintf(stderr, "[tm_batch_wait] lock %.1f us, total %.1f us\n", us(t0, t1), us(t0, std::chrono::steady_clock::now()));
+    }
+    return rc;
 }
 
 int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {
