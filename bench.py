@@ -514,6 +514,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
         "device_tokenize_ms": float(np.mean(ms_tok)),
         "device_queue_ms": float(np.mean(ms_queue)),
         "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
+        "churn_ms_steps": [round(x, 3) for x in ms_churn],   # [0]: before the first launch (no walk beside it)
         "host_ms": {k: float(np.mean(v)) if v else 0.0 for k, v in ms_host.items()},
         "churn_overlapped_with_device": True,
         "matches_delivered_per_step": delivered, "generic_path_topics": int(st["slow_topics"]),
@@ -551,6 +552,7 @@ def run_c5(args, ws, rank, local, sync):
         "churn_apply_ms": leg["churn_ms"],
         "churn_overlapped_with_device": True,
         "host_ms": leg["host_ms"],
+        "churn_ms_steps": leg["churn_ms_steps"],
         "device_queue_ms": leg["device_queue_ms"],
         "matches_delivered_per_step": leg["matches_delivered_per_step"],
         "generic_path_topics": leg["generic_path_topics"],
@@ -915,7 +917,8 @@ def e2e_rate(eng, sub, reps: int = 3) -> dict:
     return {"publishes_per_s": len(sub) / best, "topics": len(sub), "ms": 1e3 * best,
             "stages_ms": {k: min(v[1:]) for k, v in stages.items()},
             "bytes_in": int(offs[-1] - offs[0]), "matches_out": int(r.n_matches),
-            "path": "tm_match_batch: H2D bytes, device tokeniser, match, D2H CSR (best of %d)" % reps}
+            "path": ("tm_match_batch: H2D bytes, device tokeniser, match, D2H CSR, chunks of 2^20 publishes "
+                     "pipelined over two streams (best of %d; stages_ms: the same steps unpipelined)" % reps)}
 
 
 def main():

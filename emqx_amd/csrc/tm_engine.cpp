@@ -465,6 +465,8 @@ struct tm_batch {
     // one-shot launch (tm_match_batch): the dense CSR is built and copied into
     // mapped host memory behind the walk, so the batch costs one host wait
     bool oneshot = false;
+    bool eager_dense = false;       // scan + finalize enqueued by launch (oneshot implies it)
+    uint64_t dense_cap = 0;         // ids the enqueued finalize could hold
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
     uint8_t *h_xrow = nullptr, *h_xids = nullptr;
     size_t c_xrow = 0, c_xids = 0;
@@ -650,6 +652,18 @@ struct Replica {
     std::vector<tm_batch*> readers;
     tm_batch scratch;   // tm_match_batch / tm_trie_match / tm_match_routes_batch slices
     tm_batch tokb;      // staging of tm_tokenize_device
+    // tm_match_batch of more than ONESHOT_MAX topics: chunks alternate over two
+    // batches on streams of their own, so chunk j's copy to the host overlaps
+    // chunk j + 1's upload and walk; the merged CSR lands in h_prow / h_pids
+    tm_batch pipe[2];
+    bool pipe_ready = false;
+    hipStream_t pipe_copy = nullptr;                      // the results' copies to the host
+    hipEvent_t pipe_h2d[2] = {nullptr, nullptr};          // staging k uploaded
+    hipEvent_t pipe_cp[2] = {nullptr, nullptr};           // pipe[k]'s last result copied out
+    uint8_t* h_stage[2] = {nullptr, nullptr};             // pinned packed chunk (offsets | bytes)
+    size_t ch_stage[2] = {0, 0};
+    uint32_t *h_prow = nullptr, *h_pids = nullptr;
+    size_t ch_prow = 0, ch_pids = 0;
 
     // trie tables
     Slot* d_slots = nullptr;
@@ -1489,15 +1503,20 @@ struct tm_engine {
                 }
                 c = new_node(p, w);
                 ++nd[p].ec;
+                // p's slot changes with a '+' / '#' child or a new signature bit
+                // (ec is not in it): only then is it rewritten (and uploaded)
+                bool resum = true;
                 if (w == W_PLUS) nd[p].plus = c;
                 else if (w == W_HASH) nd[p].hash = c;
                 else {
+                    const uint32_t s0 = nd[p].lsig(), x0 = n_lext[p];
                     nd[p].lsig_add(w);
                     n_lext[p] |= 1u << lext_pos(w);
+                    resum = nd[p].lsig() != s0 || n_lext[p] != x0;
                 }
                 insert_edge(p, w, c);
                 if (M && M->defer && k < sd) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
-                write_summary(p);
+                if (resum) write_summary(p);
             }
             p = c;
         }
@@ -1545,9 +1564,14 @@ struct tm_engine {
             // (a parallel batch: the nodes of depth < 2 are shared by workers)
             std::unique_lock<std::recursive_mutex> rl;
             if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+            bool sig_changed = true;
             if (w == W_PLUS) nd[p].plus = NONE;
             else if (w == W_HASH) nd[p].hash = NONE;
-            else nd[p].lsig_del(w);
+            else {
+                const uint32_t s0 = nd[p].lsig();
+                nd[p].lsig_del(w);
+                sig_changed = nd[p].lsig() != s0;
+            }
             if (!nd[p].live) { rc = TM_EABORT; break; }
             if (nd[p].ec == 1 && !nd[p].topic) {
                 nd[p].ec = 0;
@@ -1557,7 +1581,7 @@ struct tm_engine {
                 continue;
             }
             --nd[p].ec;
-            write_summary(p);
+            if (sig_changed) write_summary(p);   // (a '+' / '#' child, or a signature bit gone)
             break;
         }
         if (M) ++M->version;
@@ -3538,7 +3562,7 @@ struct tm_engine {
         b->scan_args = s;
         if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
-        if (b->oneshot && (rc = enqueue_oneshot(b, S))) return rc;
+        if ((b->oneshot || b->eager_dense) && (rc = enqueue_oneshot(b, S))) return rc;
         HIP_OK(hipEventRecord(b->ev_end, S));
         b->end_recorded = true;
         return TM_OK;
@@ -3572,6 +3596,14 @@ struct tm_engine {
         ScanArgs s = b->scan_args;
         s.ids = b->d_ids;
         s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
+        b->dense_cap = s.ids_cap;
+        if (!b->oneshot) {   // the dense CSR only (the pipelined tm_match_batch copies it by DMA)
+            HIP_OK(hipEventRecord(b->evc0, S));
+            HIP_OK(launch_scan(s, S, b->d_total));
+            HIP_OK(launch_finalize(s, S, false));
+            HIP_OK(hipEventRecord(b->evc1, S));
+            return TM_OK;
+        }
         if ((rc = host_reserve_coherent(b->h_xrow, b->c_xrow, ((size_t)b->n + 1) * 4))) return rc;
         if ((rc = host_reserve_coherent(b->h_xids, b->c_xids, std::max<size_t>(b->c_ids, 1) * 4))) return rc;
         void *d_row = nullptr, *d_ids = nullptr;
@@ -3807,7 +3839,12 @@ struct tm_engine {
         }
         fill_stats(b);
         b->done = true;
-        b->dense = eager_csr;
+        b->dense = eager_csr || (b->eager_dense && !b->oneshot && b->total <= b->dense_cap);
+        if (b->dense && !eager_csr) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, b->evc0, b->evc1);
+            b->st.ms_csr = ms;
+        }
         return TM_OK;
     }
 
@@ -4273,6 +4310,7 @@ struct tm_engine {
         for (Replica* R : reps) {
             (void)hipSetDevice(R->device);
             if (R->stream) (void)hipStreamSynchronize(R->stream);
+            pipe_teardown(*R);
             R->scratch.release();
             R->tokb.release();
             dev_free(R->d_slots); dev_free(R->d_foff); dev_free(R->d_flen); dev_free(R->d_fbytes);
@@ -4345,6 +4383,153 @@ struct tm_engine {
             (void)hipStreamSynchronize(R.stream);
         }
         return first;
+    }
+
+    // tm_match_batch of a large batch on one replica, pipelined: chunks of
+    // PIPE_CHUNK topics alternate over R.pipe[0/1] (own streams).  Chunk j is
+    // uploaded and walked (dense CSR enqueued behind the walk) while chunk
+    // j - 1's ids go to the host by DMA, straight to their place in the merged
+    // CSR (the host learns a chunk's total when it waits for it, so every copy
+    // knows its offset); row offsets are rebased on the host after their copy.
+    static constexpr uint32_t PIPE_CHUNK = 1u << 20;
+    int pipe_setup(Replica& R) {
+        if (R.pipe_ready) return TM_OK;
+        for (int k = 0; k < 2; ++k) {
+            tm_batch& b = R.pipe[k];
+            b.rep = &R;
+            HIP_OK(hipStreamCreateWithFlags(&b.own, hipStreamNonBlocking));
+            b.own_user = true;   // (kept out of async_stop's sweep of slot batches)
+            R.readers.push_back(&b);
+            HIP_OK(hipEventCreateWithFlags(&R.pipe_h2d[k], hipEventDisableTiming));
+            HIP_OK(hipEventCreateWithFlags(&R.pipe_cp[k], hipEventDisableTiming));
+        }
+        HIP_OK(hipStreamCreateWithFlags(&R.pipe_copy, hipStreamNonBlocking));
+        R.pipe_ready = true;
+        return TM_OK;
+    }
+    void pipe_teardown(Replica& R) {
+        if (!R.pipe_ready) return;
+        if (R.pipe_copy) (void)hipStreamSynchronize(R.pipe_copy);
+        for (int k = 0; k < 2; ++k) {
+            tm_batch& b = R.pipe[k];
+            if (b.own) (void)hipStreamSynchronize(b.own);
+            forget_launch(&b);
+            b.release();
+            drop_user_stream(&b);
+            if (R.pipe_h2d[k]) (void)hipEventDestroy(R.pipe_h2d[k]);
+            if (R.pipe_cp[k]) (void)hipEventDestroy(R.pipe_cp[k]);
+            R.pipe_h2d[k] = R.pipe_cp[k] = nullptr;
+            if (R.h_stage[k]) (void)hipHostFree(R.h_stage[k]);
+            R.h_stage[k] = nullptr;
+            R.ch_stage[k] = 0;
+        }
+        if (R.pipe_copy) (void)hipStreamDestroy(R.pipe_copy);
+        R.pipe_copy = nullptr;
+        if (R.h_prow) (void)hipHostFree(R.h_prow);
+        if (R.h_pids) (void)hipHostFree(R.h_pids);
+        R.h_prow = R.h_pids = nullptr;
+        R.ch_prow = R.ch_pids = 0;
+        R.pipe_ready = false;
+    }
+
+    // Chunk j: its offsets (rebased) and bytes are copied into pinned staging
+    // by the engine's workers, uploaded in one async copy and walked on batch
+    // j % 2's stream; once the host has waited for it (its total gives the
+    // offset of its ids in the merged CSR), a copy stream moves its ids and row
+    // offsets to the host.  So the host fills chunk j + 1 while chunk j walks
+    // and chunk j - 1's result crosses PCIe.  Row offsets are rebased at the end.
+    int match_batch_pipelined(Replica& R, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                              tm_result* out) {
+        int rc;
+        if ((rc = pipe_setup(R))) return rc;
+        const uint32_t nch = (n + PIPE_CHUNK - 1) / PIPE_CHUNK;
+        if ((rc = host_reserve(R.h_prow, R.ch_prow, (size_t)n + 1))) return rc;
+        bool h2d_pending[2] = {false, false}, cp_pending[2] = {false, false};
+        std::vector<uint64_t> cbase(nch + 1, 0);
+        // every stream is drained before returning: staging and results stay consistent
+        struct Drain {
+            Replica& R;
+            ~Drain() {
+                for (tm_batch& b : R.pipe)
+                    if (b.own) (void)hipStreamSynchronize(b.own);
+                if (R.pipe_copy) (void)hipStreamSynchronize(R.pipe_copy);
+            }
+        } drain{R};
+        for (uint32_t j = 0; j <= nch; ++j) {
+            if (j < nch) {   // chunk j: stage, upload, walk + dense CSR
+                const int k = j & 1;
+                tm_batch* X = &R.pipe[k];
+                const uint32_t lo = j * PIPE_CHUNK, cnt = std::min(n - lo, PIPE_CHUNK);
+                const uint64_t b0 = offsets[lo], nb = offsets[lo + cnt] - b0;
+                const size_t head = packed_head(cnt);
+                if (h2d_pending[k]) HIP_OK(hipEventSynchronize(R.pipe_h2d[k]));   // staging k is free again
+                if ((rc = host_reserve(R.h_stage[k], R.ch_stage[k], head + nb))) return rc;
+                uint64_t* so = reinterpret_cast<uint64_t*>(R.h_stage[k]);
+                uint8_t* sb = R.h_stage[k] + head;
+                par_chunks((size_t)cnt + 1, [&](size_t i0, size_t i1) {
+                    for (size_t i = i0; i < i1; ++i) so[i] = offsets[lo + i] - b0;
+                });
+                par_chunks(nb, [&](size_t i0, size_t i1) { memcpy(sb + i0, topics + b0 + i0, i1 - i0); });
+                if (cp_pending[k]) HIP_OK(hipStreamWaitEvent(X->own, R.pipe_cp[k], 0));   // its last ids were copied out
+                if (dev_tok) {
+                    rc = upload_packed(X, R.h_stage[k], cnt, nb);
+                } else {
+                    upload_nosync = true;
+                    rc = prepare(X, sb, so, cnt);
+                    upload_nosync = false;
+                }
+                if (rc) return rc;
+                HIP_OK(hipEventRecord(R.pipe_h2d[k], X->own));
+                h2d_pending[k] = true;
+                X->eager_dense = true;
+                rc = launch(X);
+                X->eager_dense = false;
+                if (rc) return rc;
+            }
+            if (j >= 1) {    // chunk j - 1: wait, then its result to its place in the merged CSR
+                const int k = (j - 1) & 1;
+                tm_batch* Y = &R.pipe[k];
+                const uint32_t lo = (j - 1) * PIPE_CHUNK, cnt = std::min(n - lo, PIPE_CHUNK);
+                if ((rc = wait(Y))) return rc;
+                if ((rc = ensure_dense(Y))) return rc;   // (built by the launch unless ids overflowed)
+                const uint64_t base = cbase[j - 1], total = Y->total;
+                if (base + total > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
+                if (base + total > R.ch_pids) {
+                    // grow the merged ids (earlier copies land first): room for the rest at this chunk's rate
+                    HIP_OK(hipStreamSynchronize(R.pipe_copy));
+                    const size_t want = (size_t)(base + total) +
+                                        (size_t)((double)(total + 1) / cnt * (n - lo - cnt) * 1.25) + 1024;
+                    uint32_t* np = nullptr;
+                    HIP_OK(hipHostMalloc((void**)&np, want * sizeof(uint32_t), hipHostMallocDefault));
+                    if (base) memcpy(np, R.h_pids, base * sizeof(uint32_t));
+                    if (R.h_pids) (void)hipHostFree(R.h_pids);
+                    R.h_pids = np;
+                    R.ch_pids = want;
+                }
+                HIP_OK(hipStreamWaitEvent(R.pipe_copy, Y->ev_end, 0));
+                if (total)
+                    HIP_OK(hipMemcpyAsync(R.h_pids + base, Y->d_ids, total * 4, hipMemcpyDeviceToHost, R.pipe_copy));
+                HIP_OK(hipMemcpyAsync(R.h_prow + lo, Y->d_rowoff, (size_t)cnt * 4, hipMemcpyDeviceToHost, R.pipe_copy));
+                HIP_OK(hipEventRecord(R.pipe_cp[k], R.pipe_copy));
+                cp_pending[k] = true;
+                cbase[j] = base + total;
+            }
+        }
+        HIP_OK(hipStreamSynchronize(R.pipe_copy));
+        // chunk-local row offsets -> merged
+        for (uint32_t j = 1; j < nch; ++j) {
+            const uint32_t lo = j * PIPE_CHUNK, cnt = std::min(n - lo, PIPE_CHUNK), add = (uint32_t)cbase[j];
+            par_chunks(cnt, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) R.h_prow[lo + i] += add;
+            });
+        }
+        const uint64_t total = cbase[nch];
+        R.h_prow[n] = (uint32_t)total;
+        out->n_topics = n;
+        out->n_matches = total;
+        out->row_offsets = R.h_prow;
+        out->filter_ids = total ? R.h_pids : R.h_prow;
+        return TM_OK;
     }
 
     // tm_match_batch over every replica: merged CSR in m_rowoff / m_ids
@@ -4642,6 +4827,13 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
     }
     Replica& R = e->pick();
     if ((rc = e->use(&R))) return rc;
+    if (n > tm_engine::ONESHOT_MAX && !e->eager_csr) {
+        try {
+            return e->match_batch_pipelined(R, topics, offsets, n, out);
+        } catch (...) {
+            return TM_ENOMEM;
+        }
+    }
     // prepare's H2D of the caller's buffers is not waited for (the pipeline is,
     // below); on any early exit the stream is drained before returning, so
     // the borrowed buffers are never read after the caller frees them

@@ -430,3 +430,23 @@ def test_match_batch_one_shot_result_and_its_fallbacks():
         assert_same(T, engine_rows(eng, T), exp)
     st = eng.stats()
     assert st["filters"] == len(F)
+
+
+def test_match_batch_pipelined_equals_one_batch():
+    """tm_match_batch above one chunk (2.5M publishes: chunks of 2^20 on two
+    streams, each chunk's ids copied to their place in the merged CSR while the
+    next one walks) returns exactly the CSR of the same publishes run as one
+    batch (prepare / launch / wait / result), whose parity the other tests hold."""
+    F = gen.gen_filters(gen.C2)
+    T = gen.gen_topics(gen.C2, F, 2501, 2_500_000)
+    eng = Engine(device=0)
+    eng.insert_many(F)
+    eng.sync()
+    b = eng.prepare(T)
+    b.launch().wait()
+    exp_offs, exp_ids = b.result()
+    b.free()
+    for _ in range(2):   # the second call reuses the pipeline's buffers
+        offs, ids = eng.match_batch(T)
+        assert np.array_equal(offs, exp_offs)
+        assert np.array_equal(ids, exp_ids)
