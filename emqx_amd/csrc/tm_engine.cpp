@@ -3562,7 +3562,7 @@ struct tm_engine {
         b->scan_args = s;
         if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
-        if ((b->oneshot || b->eager_dense) && (rc = enqueue_oneshot(b, S))) return rc;
+        if ((b->oneshot || b->eager_dense) && (rc = enqueue_dense_tail(b, S))) return rc;
         HIP_OK(hipEventRecord(b->ev_end, S));
         b->end_recorded = true;
         return TM_OK;
@@ -3588,10 +3588,11 @@ struct tm_engine {
     }
 
     // tm_match_batch's tail, enqueued behind the walk: scan + finalize (the
-    // dense CSR, ids up to their capacity) and its copy into mapped host
-    // memory.  wait() then finds the whole result on the host; a walk that
-    // needed a relaunch, or more ids than fit, takes result()'s path instead.
-    int enqueue_oneshot(tm_batch* b, hipStream_t S) {
+    // dense CSR, ids up to their capacity) and, for a one-shot batch, its copy
+    // into mapped host memory.  wait() then finds the whole result on the
+    // host; a walk that needed a relaunch, or more ids than fit, takes
+    // result()'s (or ensure_dense's) path instead.
+    int enqueue_dense_tail(tm_batch* b, hipStream_t S) {
         int rc;
         ScanArgs s = b->scan_args;
         s.ids = b->d_ids;
