@@ -450,3 +450,26 @@ def test_match_batch_pipelined_equals_one_batch():
         offs, ids = eng.match_batch(T)
         assert np.array_equal(offs, exp_offs)
         assert np.array_equal(ids, exp_ids)
+
+
+def test_match_batch_pipelined_grows_its_result_buffer():
+    """The pipelined tm_match_batch sizes the merged ids from the first chunk's
+    rate; a first chunk of publishes that match (almost) nothing, then dense ones,
+    makes it grow the buffer mid-batch (the earlier chunks' copies kept).
+    Equal to the one-batch result, empty rows and all."""
+    F = gen.gen_filters(gen.C2)
+    T = gen.gen_topics(gen.C2, F, 2701, 1_200_000)
+    none = gen.Strings.from_list([b"zz/%d/unknown" % i for i in range(1_100_000)])
+    A = gen.Strings.concat([none, T])
+    eng = Engine(device=0)
+    eng.insert_many(F)
+    eng.sync()
+    b = eng.prepare(A)
+    b.launch().wait()
+    exp_offs, exp_ids = b.result()
+    b.free()
+    # the first chunk's rate is far below the rest's (root wildcards still match it)
+    assert exp_offs[1 << 20] * 4 < exp_offs[-1] - exp_offs[1_100_000]
+    offs, ids = eng.match_batch(A)
+    assert np.array_equal(offs, exp_offs)
+    assert np.array_equal(ids, exp_ids)
