@@ -924,7 +924,8 @@ def e2e_rate(eng, sub, reps: int = 3) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 200 C2 steps = ~1 s timed: long enough for an outside utilisation sampler to see the GPU busy
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--topics", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
