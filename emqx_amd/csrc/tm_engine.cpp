@@ -747,13 +747,10 @@ struct Replica {
     // device works instead of trickling out as tiny batches
     uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // tools/ab_async.sh
     uint32_t a_spin_us = 0;   // completers poll a pinned flag this long before blocking on the event (0: off)
-    // while batches are in flight and fewer than a_busy_min calls wait, the
-    // launcher gathers for at most this long, then launches what it has on a
-    // free slot (0: until the pipeline idles or a_busy_min calls queue).
-    // Measured off by default (profiles/r04/d/): 20 / 40 / 80 us left the
-    // 64-thread blocking leg at 0.24-0.26 M calls/s (p50 155 -> 108-149 us)
-    // and cost the 4,096-in-flight leg 6.2 -> 4.6-4.7 M calls/s.
-    uint32_t a_busy_wait_us = 0;
+    // (while batches are in flight and fewer than a_busy_min calls wait, the
+    // launcher waits for the pipeline to idle or a_busy_min calls; a bounded
+    // gather -- launch after 20 / 40 / 80 us -- was measured, profiles/r04/d/:
+    // blocking leg unchanged, 4,096-in-flight leg 6.2 -> 4.6-4.7 M calls/s)
     // a call that finds the queue empty and the whole pipeline idle launches
     // its batch itself, on the calling thread (no launcher wake-up)
     bool a_inline = true;
@@ -1642,7 +1639,7 @@ struct tm_engine {
         std::vector<uint64_t> hs;
         const bool root_live = nd[ROOT].live != 0;
         const uint32_t nb = nbuckets();
-        static const bool ptrace = getenv("TM_PLAN_TRACE") != nullptr;
+        static const bool ptrace = getenv("TM_PAR_TRACE") != nullptr;
         std::chrono::steady_clock::duration d_split{}, d_dict{}, d_walk{};
         using clk = std::chrono::steady_clock;
         for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
@@ -3890,7 +3887,6 @@ struct tm_engine {
         if (const char* d = getenv("TM_ASYNC_BUSY_MIN")) R.a_busy_min = (uint32_t)std::max(1, atoi(d));
         if (const char* d = getenv("TM_ASYNC_COMPLETERS")) R.a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
         if (const char* d = getenv("TM_ASYNC_SPIN_US")) R.a_spin_us = (uint32_t)std::min(10000, std::max(0, atoi(d)));
-        if (const char* d = getenv("TM_ASYNC_BUSY_WAIT_US")) R.a_busy_wait_us = (uint32_t)std::min(100000, std::max(0, atoi(d)));
         if (const char* d = getenv("TM_ASYNC_INLINE")) R.a_inline = atoi(d) != 0;
         {
             std::lock_guard<std::recursive_mutex> g(mu);
@@ -4076,8 +4072,7 @@ struct tm_engine {
                 auto enough = [&] {
                     return R.a_stop || R.a_free.size() == R.a_slots.size() || queued() >= R.a_busy_min;
                 };
-                if (R.a_busy_wait_us) R.a_work.wait_for(lk, std::chrono::microseconds(R.a_busy_wait_us), enough);
-                else R.a_work.wait(lk, enough);
+                R.a_work.wait(lk, enough);
                 if (R.a_free.empty() || queued() == 0) continue;
             }
             if (R.a_linger_us && !R.a_stop && queued() < R.a_max)

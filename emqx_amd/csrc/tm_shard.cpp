@@ -232,9 +232,6 @@ struct tm_sharded {
     std::vector<uint8_t> link;               // [i * G + j]: TM_LINK_*
     std::mutex mu;                           // one step (and one mutation) at a time
     tm_sharded_batch* last = nullptr;
-    // TM_SHARD_COPY=1: sources keep their parts and the shards copy them in
-    // (DMA) instead of the scatter writing into the shards' batches (A/B)
-    const bool copy_parts = getenv("TM_SHARD_COPY") && atoi(getenv("TM_SHARD_COPY")) != 0;
 
     template <class F>
     void each(F f) {
@@ -247,16 +244,6 @@ struct tm_sharded {
     uint64_t dict_words() {
         tm_engine_stats st{};
         return tm_stats(sh[0], &st) == TM_OK ? st.words : 0;
-    }
-
-    // bytes of slice i's memory -> shard j's device, enqueued on dest stream S
-    // (device dev[j] current): same device, or a peer copy (staged links copy
-    // from their bounce buffer instead, see step)
-    int copy_in(uint32_t i, uint32_t j, void* dst, const void* src, size_t bytes, hipStream_t S) {
-        if (!bytes) return TM_OK;
-        if (link[i * G + j] == TM_LINK_PEER) SH_HIP(hipMemcpyPeerAsync(dst, dev[j], src, dev[i], bytes, S));
-        else SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S));
-        return TM_OK;
     }
 
     // a blocking copy between shards' devices (the on-request reorder)
@@ -435,7 +422,7 @@ struct tm_sharded {
                     a.tbase = S.lo;
                     for (uint32_t j = 0; j < G; ++j) {
                         a.wbase[j] = b->W[i * G + j];
-                        if (link[i * G + j] == TM_LINK_STAGED || copy_parts) continue;
+                        if (link[i * G + j] == TM_LINK_STAGED) continue;
                         // same device or a peer: the scatter writes into shard j's batch itself
                         a.dtoff[j] = b->pb[j].toff;
                         a.dflags[j] = b->pb[j].tflags;
@@ -480,12 +467,8 @@ struct tm_sharded {
                                                       P.stream));
                         if (pn) SH_HIP(hipMemcpyAsync(dflags, bb + (size_t)pn * 4 + (size_t)pw * 4, pn,
                                                       hipMemcpyHostToDevice, P.stream));
-                        continue;
                     }
-                    if (!copy_parts) continue;   // written there by the source's scatter
-                    if ((rc = copy_in(i, j, dtoff, S.ptoff.p + S.seg[j] + j, (size_t)pn * 4, P.stream))) return rc;
-                    if ((rc = copy_in(i, j, dwords, S.pwords.p + S.seg[G + 1 + j], (size_t)pw * 4, P.stream))) return rc;
-                    if ((rc = copy_in(i, j, dflags, S.ptflags.p + S.seg[j], pn, P.stream))) return rc;
+                    // (same device or a peer: written there by the source's scatter)
                 }
                 SH_HIP(hipMemcpyAsync(P.toff + b->pn[j], b->h_close + j, 4, hipMemcpyHostToDevice, P.stream));
                 SH_HIP(hipEventRecord(ev_x1[j], P.stream));
