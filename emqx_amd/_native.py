@@ -162,6 +162,8 @@ SIGNATURES = {
     "tm_match_routes_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Routes)]),
     "tm_trie_insert_many": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
     "tm_trie_delete_many": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "tm_trie_apply_many": (C.c_int, [P, P, P, C.c_uint32, P, P, C.c_uint32, C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64)]),
     "tm_dict_load": (C.c_int, [P, P, P, C.c_uint32]),
     "tm_filter_shard": (C.c_int, [P, U8P, SZ, C.c_uint32]),
     "tm_tokenize": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64)]),

@@ -1623,8 +1623,9 @@ struct tm_engine {
     // existing paths are walked level by level for the whole group, every
     // filter's next bucket prefetched before any is probed -- PLAN_G
     // independent cache misses in flight instead of one chain per filter.
-    static constexpr uint32_t PLAN_G = 16;
-    void plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part) {
+    static constexpr uint32_t PLAN_G = 64;
+    void plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part,
+                    uint32_t pbase = 0, bool append = false) {
         // the part's vectors are worked on as locals and put back at the end:
         // the per-part vector headers share cache lines, and a push_back per
         // word on them from 8-16 threads was a false-sharing storm (plan of
@@ -1632,7 +1633,7 @@ struct tm_engine {
         // thread on eight)
         std::vector<uint32_t> W;
         W.swap(plan_words[part]);
-        W.clear();
+        if (!append) W.clear();   // (append: a second range of the same part, tm_trie_apply_many)
         std::vector<TWord> all;
         all.swap(plan_tw[part]);
         std::vector<TWord> ws;
@@ -1650,7 +1651,7 @@ struct tm_engine {
             hs.clear();
             all.clear();
             for (uint32_t i = g0; i < g1; ++i) {
-                PlanEnt& pe = plan[i];
+                PlanEnt& pe = plan[pbase + i];
                 split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
                 pe.woff = wbase + (uint32_t)all.size();
                 pe.nw = (uint32_t)ws.size();
@@ -1673,7 +1674,7 @@ struct tm_engine {
             bool run[PLAN_G], known[PLAN_G];
             const uint32_t G = g1 - g0;
             for (uint32_t q = 0; q < G; ++q) {
-                const PlanEnt& pe = plan[g0 + q];
+                const PlanEnt& pe = plan[pbase + g0 + q];
                 node[q] = ROOT;
                 k[q] = 0;
                 known[q] = true;
@@ -1683,14 +1684,14 @@ struct tm_engine {
             for (bool any = root_live; any;) {
                 any = false;
                 for (uint32_t q = 0; q < G; ++q) {
-                    const PlanEnt& pe = plan[g0 + q];
+                    const PlanEnt& pe = plan[pbase + g0 + q];
                     if (!run[q]) continue;
                     if (k[q] >= pe.nw || W[pe.woff + k[q]] == W_UNKNOWN) { run[q] = false; continue; }
                     __builtin_prefetch(&slots[(size_t)home_bucket(node[q], W[pe.woff + k[q]], nb) * BUCKET]);
                 }
                 for (uint32_t q = 0; q < G; ++q) {
                     if (!run[q]) continue;
-                    const PlanEnt& pe = plan[g0 + q];
+                    const PlanEnt& pe = plan[pbase + g0 + q];
                     const uint32_t sl = find_slot(node[q], W[pe.woff + k[q]]);
                     if (sl == NONE) { run[q] = false; continue; }
                     node[q] = slots[sl].child & ID_MASK;
@@ -1699,7 +1700,7 @@ struct tm_engine {
                 }
             }
             for (uint32_t q = 0; q < G; ++q) {
-                PlanEnt& pe = plan[g0 + q];
+                PlanEnt& pe = plan[pbase + g0 + q];
                 if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
                 else { pe.node = node[q]; pe.depth = k[q]; }
             }
@@ -1728,6 +1729,76 @@ struct tm_engine {
             }
         });
     }
+
+    // One plan for a delete list and an insert list (tm_trie_apply_many):
+    // plan[0, ndel) the deletes, plan[ndel, ndel + nins) the inserts; each
+    // worker plans its share of both lists in the same pool run.
+    void make_plan_pair(const uint8_t* dbuf, const uint64_t* doffs, uint32_t ndel, const uint8_t* ibuf,
+                        const uint64_t* ioffs, uint32_t nins) {
+        plan.resize((size_t)ndel + nins);
+        const unsigned nt = std::max(1u, std::min<unsigned>(threads, (ndel + nins) / 256));
+        if (plan_words.size() < nt) plan_words.resize(nt);
+        if (plan_tw.size() < nt) plan_tw.resize(nt);
+        auto part = [&](unsigned j) {
+            plan_range(dbuf, doffs, (uint32_t)((uint64_t)ndel * j / nt), (uint32_t)((uint64_t)ndel * (j + 1) / nt), true, j);
+            plan_range(ibuf, ioffs, (uint32_t)((uint64_t)nins * j / nt), (uint32_t)((uint64_t)nins * (j + 1) / nt), false, j,
+                       ndel, true);
+        };
+        if (nt == 1) { part(0); return; }
+        ensure_pool();
+        pool.run([&](unsigned i) {
+            for (unsigned j = i; j < nt; j += pool.n) part(j);
+        });
+    }
+
+    // After the deletes of an apply: an insert planned before them keeps its
+    // (node, depth) unless that node died (a delete emptied it -- its ancestors
+    // live as long as it does, and deletes add no edge, so the walk's stop is
+    // unchanged otherwise); those walk again from the root.  Dead ids are not
+    // handed out again before the inserts start, so `live` tells.
+    // (The walks go PLAN_G at a time, level by level with every next bucket
+    // prefetched, as in plan_range.)
+    uint32_t replan_dead_inserts(uint32_t n) {
+        std::vector<uint32_t>& redo = replan_buf;
+        redo.clear();
+        for (uint32_t i = 0; i < n; ++i) {
+            if (i + 16 < n && plan[i + 16].node != ROOT) __builtin_prefetch(&nd[plan[i + 16].node]);
+            const PlanEnt& pe = plan[i];
+            if (pe.node != ROOT && !nd[pe.node].live) redo.push_back(i);
+        }
+        const bool root_live = nd[ROOT].live != 0;
+        const uint32_t nb = nbuckets();
+        for (size_t g0 = 0; g0 < redo.size(); g0 += PLAN_G) {
+            const uint32_t G = (uint32_t)std::min<size_t>(PLAN_G, redo.size() - g0);
+            bool run[PLAN_G];
+            for (uint32_t q = 0; q < G; ++q) {
+                PlanEnt& pe = plan[redo[g0 + q]];
+                pe.node = ROOT;
+                pe.depth = 0;
+                run[q] = root_live;
+            }
+            for (bool any = root_live; any;) {
+                any = false;
+                for (uint32_t q = 0; q < G; ++q) {
+                    const PlanEnt& pe = plan[redo[g0 + q]];
+                    const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+                    if (run[q] && (pe.depth >= pe.nw || w[pe.depth] == W_UNKNOWN)) run[q] = false;
+                    if (run[q]) __builtin_prefetch(&slots[(size_t)home_bucket(pe.node, w[pe.depth], nb) * BUCKET]);
+                }
+                for (uint32_t q = 0; q < G; ++q) {
+                    if (!run[q]) continue;
+                    PlanEnt& pe = plan[redo[g0 + q]];
+                    const uint32_t s = find_slot(pe.node, plan_words[pe.part][pe.woff + pe.depth]);
+                    if (s == NONE) { run[q] = false; continue; }
+                    pe.node = slots[s].child & ID_MASK;
+                    ++pe.depth;
+                    any = true;
+                }
+            }
+        }
+        return (uint32_t)redo.size();
+    }
+    std::vector<uint32_t> replan_buf;
 
     // the serial passes prefetch what filter i + PF_FAR / i + PF_NEAR will
     // touch: their node records first, then the lines those records point at
@@ -5380,6 +5451,62 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
         rc = TM_ENOMEM;
     }
     if (n_deleted) *n_deleted = done;
+    return rc;
+}
+
+int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t* del_offsets, uint32_t n_del,
+                       const uint8_t* ins_filters, const uint64_t* ins_offsets, uint32_t n_ins, uint64_t* n_deleted,
+                       uint64_t* n_inserted) {
+    if (n_deleted) *n_deleted = 0;
+    if (n_inserted) *n_inserted = 0;
+    if (!e || !del_offsets || !ins_offsets || (!del_filters && n_del) || (!ins_filters && n_ins)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    for (uint32_t i = 0; i < n_del; ++i)
+        if (del_offsets[i + 1] < del_offsets[i]) return TM_EINVAL;
+    for (uint32_t i = 0; i < n_ins; ++i)
+        if (ins_offsets[i + 1] < ins_offsets[i]) return TM_EINVAL;
+    static const bool trace = getenv("TM_PAR_TRACE") != nullptr;
+    uint64_t done = 0;
+    int rc = TM_OK;
+    try {
+        const auto tq0 = std::chrono::steady_clock::now();
+        e->make_plan_pair(del_filters, del_offsets, n_del, ins_filters, ins_offsets, n_ins);
+        if (trace)
+            fprintf(stderr, "[plan apply del=%u ins=%u] %.2f ms\n", n_del, n_ins,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+        // the deletes (plan[0, n_del)), as tm_trie_delete_many runs them
+        if (n_del < tm_engine::PAR_MIN || e->mutate_parallel(true, del_filters, del_offsets, n_del, &done, &rc)) {
+            done = 0;
+            for (uint32_t i = 0; i < n_del && rc == TM_OK; ++i) {
+                e->prefetch_delete(i, n_del);
+                rc = e->delete_planned(i);
+                if (rc == TM_OK) ++done;
+            }
+        }
+        if (n_deleted) *n_deleted = done;
+        if (rc != TM_OK) return rc;
+        // then the inserts, their plan moved to the front and checked against the deletes
+        e->plan.erase(e->plan.begin(), e->plan.begin() + n_del);
+        const uint32_t again = e->replan_dead_inserts(n_ins);
+        if (trace)
+            fprintf(stderr, "[apply: %u of %u inserts walked again after the deletes] %.2f ms in the call\n", again, n_ins,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+        done = 0;
+        if (n_ins < tm_engine::PAR_MIN || e->mutate_parallel(false, ins_filters, ins_offsets, n_ins, &done, &rc)) {
+            done = 0;
+            for (uint32_t i = 0; i < n_ins && rc == TM_OK; ++i) {
+                e->prefetch_insert(i, n_ins);
+                rc = e->insert_planned(ins_filters, ins_offsets, i);
+                if (rc == TM_OK) ++done;
+            }
+        }
+        if (n_inserted) *n_inserted = done;
+        if (trace)
+            fprintf(stderr, "[apply_many del=%u ins=%u] %.2f ms in the call\n", n_del, n_ins,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+    } catch (...) {
+        rc = TM_ENOMEM;
+    }
     return rc;
 }
 

@@ -622,6 +622,19 @@ class Engine:
                 "tm_trie_delete_many")
         return int(done.value)
 
+    def apply_many(self, dels, adds) -> tuple:
+        """One subscription delta: delete_many(dels) then insert_many(adds),
+        planned together (tm_trie_apply_many).  Returns (deleted, inserted)."""
+        d, a = _pack(dels), _pack(adds)
+        db = np.ascontiguousarray(d.buf if d.buf.size else np.zeros(1, np.uint8))
+        do = np.ascontiguousarray(d.offs.astype(np.uint64))
+        ab = np.ascontiguousarray(a.buf if a.buf.size else np.zeros(1, np.uint8))
+        ao = np.ascontiguousarray(a.offs.astype(np.uint64))
+        nd, ni = C.c_uint64(), C.c_uint64()
+        N.check(self.L.tm_trie_apply_many(self.h, db.ctypes.data, do.ctypes.data, len(d), ab.ctypes.data,
+                                          ao.ctypes.data, len(a), C.byref(nd), C.byref(ni)), "tm_trie_apply_many")
+        return int(nd.value), int(ni.value)
+
     def dict_load(self, words):
         s = _pack(words)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))

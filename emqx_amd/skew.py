@@ -62,8 +62,13 @@ class Churn:
 
     @staticmethod
     def apply(engine, dels, adds):
-        """Unsubscribes then subscribes, two bulk C calls (emqx_trie:delete/1,
-        insert/1); dels / adds are lists of binaries or packed gen.Strings."""
+        """Unsubscribes then subscribes (emqx_trie:delete/1, insert/1): one
+        tm_trie_apply_many call where the engine has it (both lists planned
+        together), else two bulk calls; dels / adds are lists of binaries or
+        packed gen.Strings."""
+        if hasattr(engine, "apply_many"):
+            engine.apply_many(dels, adds)
+            return
         if len(dels):
             engine.delete_many(dels)
         if len(adds):

@@ -398,6 +398,18 @@ TM_API int  tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint
  * for tm_trie_insert_many). */
 TM_API int  tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                 uint64_t* n_deleted);
+/* One subscription delta: tm_trie_delete_many(del...) then
+ * tm_trie_insert_many(ins..., 0, 1), with the two lists planned together (one
+ * pass of the workers over both; an insert whose planned node a delete of the
+ * same call removed walks again).  The result equals the two calls in that
+ * order, filter for filter: emqx_trie:delete/1 then insert/1
+ * (src/emqx_trie.erl:81-116) as a session's unsubscribe + subscribe batch
+ * reaches the router (src/emqx_router.erl:113-124, 163-169).  A delete error
+ * returns before any insert; *n_deleted / *n_inserted (may be NULL) count as
+ * the two calls do. */
+TM_API int  tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t* del_offsets, uint32_t n_del,
+                               const uint8_t* ins_filters, const uint64_t* ins_offsets, uint32_t n_ins,
+                               uint64_t* n_deleted, uint64_t* n_inserted);
 /* Interns n words in order (the shared dictionary of the sharded mode).  Words
  * must not contain '/'; '', "+" and "#" have fixed ids and are skipped. */
 TM_API int  tm_dict_load(tm_engine* e, const uint8_t* words, const uint64_t* offsets, uint32_t n);

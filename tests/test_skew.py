@@ -1,5 +1,7 @@
 """C5 workload tooling and TM_BATCH_DEDUP on the host (no device)."""
 
+import pytest
+
 from emqx_amd import gen
 from emqx_amd.engine import Engine
 from emqx_amd.skew import Churn, workload
@@ -123,6 +125,54 @@ def test_parallel_churn_builds_the_same_trie_as_the_serial_pass():
         for k in range(1, len(ws) + 1):
             pre = b"/".join(ws[:k])
             assert A.lookup(pre) == B.lookup(pre), pre
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_apply_many_equals_delete_many_then_insert_many(threads):
+    """tm_trie_apply_many plans the deletes and the inserts of a delta
+    together, before any delete runs.  Its result must be the two calls'
+    (delete_many, then insert_many): same nodes, edges, filters and lookups,
+    including inserts whose planned deepest node a delete of the same call
+    removes (a sibling leaf deleted: its node dies and the insert walks again)
+    and filters deleted and re-added in one delta."""
+    import random
+
+    p = gen.SkewParams(seed=23, n_hot=2500, k_per_hot=100)
+    allf, derived, hot, _ = workload(p, 60_000, 100, seed=23, background_pool=500)
+    A = Engine(device=-1, host_threads=threads)   # the two calls
+    B = Engine(device=-1, host_threads=threads)   # one apply
+    for e in (A, B):
+        e.insert_many(allf)
+    churn = Churn(hot, derived.tolist(), seed=5)
+    rng = random.Random(6)
+    touched = []
+    for step in range(3):
+        dels, adds = churn.step(10_000)
+        # deep leaves deleted while an insert extends the same path one level
+        # further (its planned node is the deleted leaf), and re-adds
+        extra_del = rng.sample([f for f in sorted(churn.live_set) if not f.endswith(b"#")], 300)
+        extra_add = [f + b"/zz%d" % step for f in extra_del[:150]] + extra_del[150:]
+        dels = dels + extra_del
+        adds = adds + extra_add
+        A.delete_many(gen.Strings.from_list(dels))
+        A.insert_many(gen.Strings.from_list(adds))
+        nd, ni = B.apply_many(gen.Strings.from_list(dels), gen.Strings.from_list(adds))
+        assert (nd, ni) == (len(dels), len(adds))
+        a, b = A.stats(), B.stats()
+        assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+        B.debug_check()
+        touched += dels[:200] + adds[:200] + extra_add
+    for f in touched:
+        ws = f.split(b"/")
+        for k in range(1, len(ws) + 1):
+            pre = b"/".join(ws[:k])
+            assert A.lookup(pre) == B.lookup(pre), pre
+    # small deltas (the serial passes) and empty lists
+    assert B.apply_many([], []) == (0, 0)
+    A.delete_many([b"a/b/c"]); A.insert_many([b"a/b/c/d", b"a/b/c"])
+    assert B.apply_many([b"a/b/c"], [b"a/b/c/d", b"a/b/c"]) == (1, 2)
+    assert B.lookup(b"a/b/c/d") == A.lookup(b"a/b/c/d") and B.lookup(b"a/b/c") == A.lookup(b"a/b/c")
+    B.debug_check()
 
 
 def test_parallel_insert_creates_a_shared_first_level_edge_once():

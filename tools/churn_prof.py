@@ -1,7 +1,8 @@
 """C5 churn apply on the host mirror alone (dev tool; TM_PAR_TRACE=1 prints
 the parallel phases): 10k deltas per step, K filters per hot topic.
 
-    python tools/churn_prof.py [K] [steps] [device]   (device -1: host-only engine)
+    python tools/churn_prof.py [K] [steps] [device] [apply|two]   (device -1: host-only engine;
+    apply: one tm_trie_apply_many per step, two: delete_many + insert_many)
 """
 import os
 import sys
@@ -15,6 +16,7 @@ from emqx_amd.skew import Churn, workload  # noqa: E402
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 device = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+mode = sys.argv[4] if len(sys.argv) > 4 else "apply"
 p = gen.SkewParams(k_per_hot=K)
 allf, derived, hot, pubs = workload(p, 100_000, 100_000, seed=5)
 eng = Engine(device=device)
@@ -26,11 +28,15 @@ for _ in range(steps):
     deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
 for d, a in deltas:
     t = time.perf_counter()
-    eng.delete_many(d)
-    t1 = time.perf_counter()
-    eng.insert_many(a)
+    if mode == "apply":
+        eng.apply_many(d, a)
+        t1 = t
+    else:
+        eng.delete_many(d)
+        t1 = time.perf_counter()
+        eng.insert_many(a)
     t2 = time.perf_counter()
     if device >= 0:
         eng.sync()   # the delta upload, as the next launch would do it
     t3 = time.perf_counter()
-    print(f"K={K} sync {1e3 * (t3 - t2):.2f} ms del {1e3 * (t1 - t):.2f} ms  ins {1e3 * (t2 - t1):.2f} ms  total {1e3 * (t2 - t):.2f}", flush=True)
+    print(f"K={K} {mode} sync {1e3 * (t3 - t2):.2f} ms del {1e3 * (t1 - t):.2f} ms  ins {1e3 * (t2 - t1):.2f} ms  total {1e3 * (t2 - t):.2f}", flush=True)
