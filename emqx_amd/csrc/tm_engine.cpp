@@ -1755,7 +1755,8 @@ struct tm_engine {
     // (node, depth) unless that node died (a delete emptied it -- its ancestors
     // live as long as it does, and deletes add no edge, so the walk's stop is
     // unchanged otherwise); those walk again from the root.  Dead ids are not
-    // handed out again before the inserts start, so `live` tells.
+    // handed out again before the inserts start, so `live` tells, and an edge
+    // to a dead child (its delete still pending) counts as absent.
     // (The walks go PLAN_G at a time, level by level with every next bucket
     // prefetched, as in plan_range.)
     uint32_t replan_dead_inserts(uint32_t n) {
@@ -1789,7 +1790,9 @@ struct tm_engine {
                     if (!run[q]) continue;
                     PlanEnt& pe = plan[redo[g0 + q]];
                     const uint32_t s = find_slot(pe.node, plan_words[pe.part][pe.woff + pe.depth]);
-                    if (s == NONE) { run[q] = false; continue; }
+                    // (an edge whose child died in this apply waits for its
+                    // delete in the shared edge phase: a miss)
+                    if (s == NONE || !nd[slots[s].child & ID_MASK].live) { run[q] = false; continue; }
                     pe.node = slots[s].child & ID_MASK;
                     ++pe.depth;
                     any = true;
@@ -1904,9 +1907,15 @@ struct tm_engine {
         return edge_w;
     }
 
-    // Phase 2: the recorded edge work of W, by bucket range (see above).
-    void edge_phase(std::vector<Mut>& W) {
-        const unsigned T = (unsigned)W.size();
+    // Phase 2: the recorded edge work of the runs' states Ws, by bucket range
+    // (see above): every run's edge deletes, then their inserts, then the
+    // summaries.
+    void edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
+        const unsigned T = std::max(1u, threads);
+        auto each = [&](auto&& fn) {
+            for (std::vector<Mut>* W : Ws)
+                for (Mut& m : *W) fn(m);
+        };
         auto merge_edges = [&](std::vector<Mut>& X) {
             for (Mut& m : X) {
                 live_edges += m.live_edges; used_slots += m.used_slots; max_disp = std::max(max_disp, m.max_disp);
@@ -1921,7 +1930,7 @@ struct tm_engine {
             RS = ((nb + 2 * T2 - 1) / (2 * T2) + 15) / 16 * 16;   // whole 16-bucket groups: dirty-mark words stay per range
             R = (nb + RS - 1) / RS;
         };
-        for (Mut& m : W) m.defer = false;
+        each([](Mut& m) { m.defer = false; });
         const bool trace = getenv("TM_PAR_TRACE") != nullptr;
         auto now = [] { return std::chrono::steady_clock::now(); };
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1930,21 +1939,23 @@ struct tm_engine {
         uint32_t RS = 0, R = 0;
         // ---- deletes, bucketed by the slot recorded in phase 1 (nothing has moved since)
         size_t ndel = 0;
-        for (Mut& m : W) ndel += m.del.size();
+        each([&](Mut& m) { ndel += m.del.size(); });
         ranges(T2, RS, R);
         if (!ndel) {
         } else if (!T2) {
-            for (Mut& m : W)
+            each([&](Mut& m) {
                 for (const auto& d : m.del) delete_edge_of(d.first);
+            });
         } else {
             std::vector<std::vector<uint32_t>> per(2 * T2);
             std::vector<uint32_t> tail;
-            for (Mut& m : W)
+            each([&](Mut& m) {
                 for (const auto& d : m.del) {
                     const uint32_t r = d.second / BUCKET / RS;
                     if (R % 2 && r == R - 1) tail.push_back(d.first);   // (R odd: the last range wraps onto range 0)
                     else per[r].push_back(d.first);
                 }
+            });
             std::vector<Mut>& X = edge_states(T2);
             std::vector<std::vector<uint32_t>> late(T2);
             for (uint32_t par = 0; par < 2; ++par)
@@ -1969,7 +1980,7 @@ struct tm_engine {
         // ---- inserts: room first (the serial insert_edge's rehash rule, for the whole batch)
         const auto e1 = now();
         size_t nins = 0;
-        for (Mut& m : W) nins += m.ins.size();
+        each([&](Mut& m) { nins += m.ins.size(); });
         bool rehashed = false;
         if ((used_slots + nins) * 4 > slots.size() * 3 || max_disp > 48) {
             rehash(std::max<size_t>((size_t)((live_edges + nins) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
@@ -1979,18 +1990,20 @@ struct tm_engine {
         ranges(T2, RS, R);
         if (!nins) {
         } else if (!T2) {
-            for (Mut& m : W)
+            each([&](Mut& m) {
                 for (const auto& e : m.ins) insert_edge(e[0], e[1], e[2]);
+            });
         } else {
             std::vector<std::vector<std::array<uint32_t, 3>>> per(2 * T2);
             std::vector<std::array<uint32_t, 3>> tail;
             const uint32_t nb = nbuckets();
-            for (Mut& m : W)
+            each([&](Mut& m) {
                 for (const auto& e : m.ins) {
                     const uint32_t r = home_bucket(e[0], e[1], nb) / RS;
                     if (R % 2 && r == R - 1) tail.push_back(e);
                     else per[r].push_back(e);
                 }
+            });
             std::vector<Mut>& X = edge_states(T2);
             for (uint32_t par = 0; par < 2; ++par)
                 pool.run([&](unsigned t) {
@@ -2015,8 +2028,9 @@ struct tm_engine {
         // records are rewritten by one worker; dirty marks set atomically)
         const unsigned TS = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));
         std::vector<std::vector<uint32_t>> per(TS);
-        for (Mut& m : W)
+        each([&](Mut& m) {
             for (uint32_t c : m.sum) per[mix_word(c) % TS].push_back(c);
+        });
         std::vector<Mut>& X = edge_states(TS);
         pool.run([&](unsigned t) {
             if (t >= TS) return;
@@ -2050,10 +2064,36 @@ struct tm_engine {
         if (!(__atomic_fetch_or(&dirty_mark[i >> 6], m, __ATOMIC_RELAXED) & m)) dl.push_back(i);
     }
 
+    // One parallel mutation in flight between par_begin and par_finish: its
+    // workers' states and the id bookkeeping of an insert.
+    struct ParRun {
+        bool del = false;
+        uint32_t n = 0;
+        std::vector<Mut>* W = nullptr;
+        std::vector<uint32_t> ids;   // node ids of an insert: free ones, then fresh ones from base
+        size_t fresh = 0, base = 0;
+        std::chrono::steady_clock::time_point ts0, tp0, tp1, tp2;
+        uint64_t done = 0;
+        int rc = TM_OK;
+    };
+    std::vector<Mut> mut_w2;   // the insert states of tm_trie_apply_many (its deletes use mut_w)
+
     // tm_trie_insert_many / delete_many of n >= PAR_MIN planned filters (make_plan ran).
     // Returns 1 when the batch must run serially instead (nothing changed then).
     int mutate_parallel(bool del, const uint8_t* buf, const uint64_t* offs, uint32_t n, uint64_t* done_out,
                         int* rc_out) {
+        ParRun R;
+        if (par_begin(del, buf, offs, n, mut_w, R)) return 1;
+        ParRun* runs[1] = {&R};
+        par_finish(runs, 1);
+        *done_out = R.done;
+        *rc_out = R.rc;
+        return 0;
+    }
+
+    // Setup and phase 1 (node records) of a parallel mutation into the states
+    // W; 1: the batch must run serially instead (nothing changed then).
+    int par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uint32_t n, std::vector<Mut>& W, ParRun& R) {
         const unsigned T = std::max(1u, threads);
         if (T < 2 || (uint64_t)n * 4 > n_filters) return 1;   // bulk builds stay serial: churn on a big trie only
         if (!del) {
@@ -2073,8 +2113,7 @@ struct tm_engine {
         }
         ensure_pool();
         const auto ts0 = std::chrono::steady_clock::now();
-        if (mut_w.size() != T) mut_w.resize(T);
-        std::vector<Mut>& W = mut_w;   // (each worker resets its own state when phase 1 starts)
+        if (W.size() != T) W.resize(T);   // (each worker resets its own state when phase 1 starts)
         // by the first two words: one worker owns those subtrees; 8 parts per
         // worker, taken largest first by whichever worker is free (skewed
         // churn clusters under a few first words)
@@ -2118,7 +2157,8 @@ struct tm_engine {
         // the filters applied are then those finished before it, see the header
         std::atomic<bool> failed{false};
         // node ids: at most the levels the batch's filters lack, the free ids first
-        std::vector<uint32_t> ids;
+        std::vector<uint32_t>& ids = R.ids;
+        ids.clear();
         std::atomic<size_t> next_id{0};
         size_t fresh = 0;
         const size_t base = nd.size();
@@ -2185,32 +2225,57 @@ struct tm_engine {
             m.t_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
             tl_mut = nullptr;
         });
-        const auto tp1 = std::chrono::steady_clock::now();
-        // phase 2: the edge hash
-        edge_phase(W);
+        R.del = del;
+        R.n = n;
+        R.W = &W;
+        R.fresh = fresh;
+        R.base = base;
+        R.ts0 = ts0;
+        R.tp0 = tp0;
+        R.tp1 = std::chrono::steady_clock::now();
+        return 0;
+    }
+
+    // Phase 2 (the edge hash) of every run at once -- their edge deletes, then
+    // their inserts, then the summaries -- and the merges.
+    void par_finish(ParRun* const* runs, size_t nr) {
+        const unsigned T = std::max(1u, threads);
+        std::vector<std::vector<Mut>*> Ws;
+        for (size_t r = 0; r < nr; ++r) Ws.push_back(runs[r]->W);
+        edge_phase(Ws);
         const auto tp2 = std::chrono::steady_clock::now();
-        // merge the rest
-        uint64_t done = 0;
-        int rc = TM_OK;
-        for (Mut& m : W) {
-            live_nodes += m.live_nodes;
-            n_filters += m.n_filters;
-            route_entries += m.route_entries;
-            routes_dirty = routes_dirty || m.routes_dirty;
-            version += m.version;
-            done += m.done;
-            if (m.rc && !rc) rc = m.rc;
-            m.fresh_base = fbytes.size();   // (reused: this worker's bytes start here)
-            fbytes.insert(fbytes.end(), m.fb.begin(), m.fb.end());
-            dirty_f.insert(dirty_f.end(), m.dirty_f.begin(), m.dirty_f.end());
-            for (const auto& q : m.pend) pending_free.push_back(q);
+        for (size_t r = 0; r < nr; ++r) {
+            ParRun& R = *runs[r];
+            R.tp2 = tp2;
+            for (Mut& m : *R.W) {
+                live_nodes += m.live_nodes;
+                n_filters += m.n_filters;
+                route_entries += m.route_entries;
+                routes_dirty = routes_dirty || m.routes_dirty;
+                version += m.version;
+                R.done += m.done;
+                if (m.rc && !R.rc) R.rc = m.rc;
+                m.fresh_base = fbytes.size();   // (reused: this worker's bytes start here)
+                fbytes.insert(fbytes.end(), m.fb.begin(), m.fb.end());
+                dirty_f.insert(dirty_f.end(), m.dirty_f.begin(), m.dirty_f.end());
+                for (const auto& q : m.pend) pending_free.push_back(q);
+            }
         }
         pool.run([&](unsigned t) {   // filter byte offsets: distinct nodes per worker
-            for (unsigned j = t; j < T; j += pool.n)
-                for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+            for (size_t r = 0; r < nr; ++r) {
+                const std::vector<Mut>& W = *runs[r]->W;
+                for (size_t j = t; j < W.size(); j += pool.n)
+                    for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+            }
             for (unsigned j = t; j < 64; j += pool.n) shared_made[j].clear();   // for the next batch
         });
-        if (!del) {   // ids not handed out: free ones back to the list, the fresh tail cut off
+        for (size_t r = 0; r < nr; ++r) {
+            ParRun& R = *runs[r];
+            if (R.del) continue;
+            std::vector<Mut>& W = *R.W;
+            const std::vector<uint32_t>& ids = R.ids;
+            const size_t fresh = R.fresh, base = R.base;
+            // ids not handed out: free ones back to the list, the fresh tail cut off
             // (the rest of each worker's last chunk: free-list ids go back; fresh
             // ids below the highest one handed out stay as free dead records)
             size_t used = 0;
@@ -2230,17 +2295,18 @@ struct tm_engine {
                 if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
             }
         }
-        *done_out = done;
-        *rc_out = rc;
         if (getenv("TM_PAR_TRACE")) {
             const auto tp3 = std::chrono::steady_clock::now();
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "[par %s n=%u T=%u] setup %.2f ms phase1 %.2f ms edges %.2f ms merge %.2f ms; workers (items, us):",
-                    del ? "del" : "ins", n, T, ms(ts0, tp0), ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
-            for (const Mut& m : W) fprintf(stderr, " (%zu, %.0f)", m.n_items, m.t_us);
-            fprintf(stderr, "\n");
+            for (size_t r = 0; r < nr; ++r) {
+                const ParRun& R = *runs[r];
+                fprintf(stderr, "[par %s n=%u T=%u] setup %.2f ms phase1 %.2f ms edges %.2f ms merge %.2f ms%s; workers (items, us):",
+                        R.del ? "del" : "ins", R.n, T, ms(R.ts0, R.tp0), ms(R.tp0, R.tp1), ms(R.tp1, R.tp2), ms(R.tp2, tp3),
+                        nr > 1 ? " (edges + merge shared)" : "");
+                for (const Mut& m : *R.W) fprintf(stderr, " (%zu, %.0f)", m.n_items, m.t_us);
+                fprintf(stderr, "\n");
+            }
         }
-        return 0;
     }
 
     // ------------------------------------------------------------ device sync
@@ -5474,8 +5540,24 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
         if (trace)
             fprintf(stderr, "[plan apply del=%u ins=%u] %.2f ms\n", n_del, n_ins,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
-        // the deletes (plan[0, n_del)), as tm_trie_delete_many runs them
-        if (n_del < tm_engine::PAR_MIN || e->mutate_parallel(true, del_filters, del_offsets, n_del, &done, &rc)) {
+        // Both lists big enough for the parallel pass: the deletes' node
+        // records (phase 1), the inserts' (their plan checked against the
+        // deletes: an edge to a node that died is a miss), then ONE edge phase
+        // and merge for both -- the deletes' edge work runs first in it, as in
+        // the two calls.  Otherwise the two passes one after the other.
+        tm_engine::ParRun RD, RI;
+        bool del_open = false;
+        if (n_del >= tm_engine::PAR_MIN && n_ins >= tm_engine::PAR_MIN &&
+            !e->par_begin(true, del_filters, del_offsets, n_del, e->mut_w, RD)) {
+            del_open = true;
+            for (const Mut& m : e->mut_w)
+                if (m.rc) {   // a delete failed: finish the deletes alone and stop
+                    tm_engine::ParRun* runs[1] = {&RD};
+                    e->par_finish(runs, 1);
+                    if (n_deleted) *n_deleted = RD.done;
+                    return RD.rc;
+                }
+        } else if (n_del < tm_engine::PAR_MIN || e->mutate_parallel(true, del_filters, del_offsets, n_del, &done, &rc)) {
             done = 0;
             for (uint32_t i = 0; i < n_del && rc == TM_OK; ++i) {
                 e->prefetch_delete(i, n_del);
@@ -5483,16 +5565,38 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
                 if (rc == TM_OK) ++done;
             }
         }
-        if (n_deleted) *n_deleted = done;
-        if (rc != TM_OK) return rc;
-        // then the inserts, their plan moved to the front and checked against the deletes
+        if (!del_open) {
+            if (n_deleted) *n_deleted = done;
+            if (rc != TM_OK) return rc;
+        }
+        // the inserts, their plan moved to the front and checked against the deletes
         e->plan.erase(e->plan.begin(), e->plan.begin() + n_del);
         const uint32_t again = e->replan_dead_inserts(n_ins);
         if (trace)
             fprintf(stderr, "[apply: %u of %u inserts walked again after the deletes] %.2f ms in the call\n", again, n_ins,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
         done = 0;
-        if (n_ins < tm_engine::PAR_MIN || e->mutate_parallel(false, ins_filters, ins_offsets, n_ins, &done, &rc)) {
+        if (del_open) {
+            if (!e->par_begin(false, ins_filters, ins_offsets, n_ins, e->mut_w2, RI)) {
+                tm_engine::ParRun* runs[2] = {&RD, &RI};
+                e->par_finish(runs, 2);
+                if (n_deleted) *n_deleted = RD.done;
+                if (n_inserted) *n_inserted = RI.done;
+                if (trace)
+                    fprintf(stderr, "[apply_many del=%u ins=%u, one edge phase] %.2f ms in the call\n", n_del, n_ins,
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+                return RD.rc ? RD.rc : RI.rc;
+            }
+            tm_engine::ParRun* runs[1] = {&RD};   // the inserts run serially: the deletes end first
+            e->par_finish(runs, 1);
+            if (n_deleted) *n_deleted = RD.done;
+            if (RD.rc) return RD.rc;
+            for (uint32_t i = 0; i < n_ins && rc == TM_OK; ++i) {
+                e->prefetch_insert(i, n_ins);
+                rc = e->insert_planned(ins_filters, ins_offsets, i);
+                if (rc == TM_OK) ++done;
+            }
+        } else if (n_ins < tm_engine::PAR_MIN || e->mutate_parallel(false, ins_filters, ins_offsets, n_ins, &done, &rc)) {
             done = 0;
             for (uint32_t i = 0; i < n_ins && rc == TM_OK; ++i) {
                 e->prefetch_insert(i, n_ins);
