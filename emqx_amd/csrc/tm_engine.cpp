@@ -1258,6 +1258,7 @@ struct tm_engine {
                     const size_t j = k < M->n_free ? (*M->ids)[k] : M->fresh_base + (k - M->n_free);
                     if (j >= nd.size()) break;
                     __builtin_prefetch(&nd[j], 1);
+                    __builtin_prefetch(&n_lext[j], 1);
                     __builtin_prefetch(&n_flen[j], 1);
                     if (j < dirty_f_mark.size()) __builtin_prefetch(&dirty_f_mark[j], 1);
                 }
@@ -1891,7 +1892,10 @@ struct tm_engine {
     // a pass over node ids v touching each node's record and its slot: the
     // record 16 nodes ahead, the slot (from the record, by then in cache) 8 ahead
     void prefetch_edge_of(const std::vector<uint32_t>& v, size_t q) const {
-        if (q + 16 < v.size()) __builtin_prefetch(&nd[v[q + 16]]);
+        if (q + 16 < v.size()) {
+            __builtin_prefetch(&nd[v[q + 16]]);
+            __builtin_prefetch(&n_lext[v[q + 16]]);
+        }
         if (q + 8 < v.size()) {
             const uint32_t s = nd[v[q + 8]].inslot;
             if (s != NONE && s < slots.size()) __builtin_prefetch(&slots[s], 1);
@@ -2204,7 +2208,10 @@ struct tm_engine {
                         const uint32_t i = items[q];
                         if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
                             const uint32_t f = plan[items[q + 8]].node;
-                            if (f != NONE) __builtin_prefetch(&nd[f]);
+                            if (f != NONE) {
+                                __builtin_prefetch(&nd[f]);
+                                __builtin_prefetch(&n_lext[f]);   // (a new literal child sets a bit there)
+                            }
                         }
                         const PlanEnt& pe = plan[i];
                         int rc;

@@ -1,9 +1,11 @@
 #!/bin/bash
-# round 4 / ag: one plan for a delta (tm_trie_apply_many) against the two calls; plan groups of 64
+# round 4 / ag: tm_trie_apply_many (one plan, one edge phase per delta) against the two calls; C5 GPU parity tests
 set -o pipefail
 O=gpurun_out/r4ag
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_skew.py tests/test_gpu_skew_full.py > $O/pytest_skew.log 2>&1 || { tail -40 $O/pytest_skew.log; exit 1; }
+tail -2 $O/pytest_skew.log
 for k in 100 10; do
 for m in two apply two apply; do
 timeout -k 10 300 python -u tools/churn_prof.py $k 10 0 $m > $O/k${k}_$m.txt 2>&1 || { tail -20 $O/k${k}_$m.txt; exit 1; }
