@@ -345,16 +345,17 @@ unsigned default_threads() {
     return std::max(1u, std::min(h ? h : 1u, 16u));
 }
 
-// With TM_POOL_PIN=1: the CPUs of the NUMA node `device` is attached to
-// (sysfs), within this process's affinity, for the churn workers -- so the
-// host mirror's pages they first-touch and their random reads stay on one
-// socket.  Opt-in: on the 2-socket box it measured within the run-to-run
-// noise of C5's churn (profiles/r03/numa_pin/).  False (no pinning) for a
+// The CPUs of the NUMA node `device` is attached to (sysfs), within this
+// process's affinity, for the churn workers -- so the host mirror's pages they
+// first-touch and their random reads stay on one socket.  On by default since
+// late round 4 (C5 K = 100 churn, three processes each on the 2-socket box:
+// unpinned 1.72 / 2.18 / 1.95 ms per step, pinned 1.40 / 1.50 / 1.77,
+// profiles/r04/aj/); TM_POOL_PIN=0 turns it off.  False (no pinning) for a
 // host-only engine, a node-less device or fewer CPUs than `need`.
 bool device_node_cpus(int device, unsigned need, cpu_set_t& out) {
     if (device < 0) return false;
     const char* pin = getenv("TM_POOL_PIN");
-    if (!pin || pin[0] != '1') return false;
+    if (pin && pin[0] == '0') return false;
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof bus - 1, device) != hipSuccess) return false;
     for (char* c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
