@@ -5577,15 +5577,25 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
             if (n_deleted) *n_deleted = done;
             if (rc != TM_OK) return rc;
         }
-        // the inserts, their plan moved to the front and checked against the deletes
-        e->plan.erase(e->plan.begin(), e->plan.begin() + n_del);
-        const uint32_t again = e->replan_dead_inserts(n_ins);
-        if (trace)
-            fprintf(stderr, "[apply: %u of %u inserts walked again after the deletes] %.2f ms in the call\n", again, n_ins,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+        // the inserts, their plan moved to the front and checked against the
+        // deletes.  With the deletes' edge work still pending, anything thrown
+        // before the inserts' phase 1 has run must not leave it undone.
+        bool ins_open = false;
+        int irc = TM_OK;
+        try {
+            e->plan.erase(e->plan.begin(), e->plan.begin() + n_del);
+            const uint32_t again = e->replan_dead_inserts(n_ins);
+            if (trace)
+                fprintf(stderr, "[apply: %u of %u inserts walked again after the deletes] %.2f ms in the call\n", again,
+                        n_ins, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+            if (del_open) ins_open = !e->par_begin(false, ins_filters, ins_offsets, n_ins, e->mut_w2, RI);
+        } catch (...) {
+            if (!del_open) throw;
+            irc = TM_ENOMEM;   // (par_begin's setup throws before its phase 1 changes anything)
+        }
         done = 0;
         if (del_open) {
-            if (!e->par_begin(false, ins_filters, ins_offsets, n_ins, e->mut_w2, RI)) {
+            if (ins_open) {
                 tm_engine::ParRun* runs[2] = {&RD, &RI};
                 e->par_finish(runs, 2);
                 if (n_deleted) *n_deleted = RD.done;
@@ -5599,6 +5609,7 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
             e->par_finish(runs, 1);
             if (n_deleted) *n_deleted = RD.done;
             if (RD.rc) return RD.rc;
+            if (irc) return irc;
             for (uint32_t i = 0; i < n_ins && rc == TM_OK; ++i) {
                 e->prefetch_insert(i, n_ins);
                 rc = e->insert_planned(ins_filters, ins_offsets, i);
