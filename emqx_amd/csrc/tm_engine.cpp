@@ -468,6 +468,7 @@ struct tm_batch {
     bool oneshot = false;
     bool eager_dense = false;       // scan + finalize enqueued by launch (oneshot implies it)
     uint64_t dense_cap = 0;         // ids the enqueued finalize could hold
+    bool dense_enq = false;         // the LAST launch enqueued scan + finalize (set by launch, read by wait)
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
     uint8_t *h_xrow = nullptr, *h_xids = nullptr;
     size_t c_xrow = 0, c_xids = 0;
@@ -2174,6 +2175,17 @@ struct tm_engine {
             const size_t take = std::min<size_t>(total, free_nodes.size());
             fresh = total - take + (size_t)T * Mut::ID_CHUNK;   // + slack: ids are taken a chunk per worker
             if (base + fresh >= MAX_NODES) return 1;
+            // Transactional: every allocation first (a bad_alloc here leaves
+            // the engine as it was: the caller may still finish other work on
+            // it), then the commit below, which allocates nothing.
+            ids.reserve(take);
+            if (fresh) {
+                nd.reserve(base + fresh);
+                n_flen.reserve(base + fresh);
+                n_lext.reserve(base + fresh);
+                n_foff.reserve(base + fresh);
+            }
+            if (!full_f_dirty) dirty_f_mark.reserve(base + fresh);
             ids.assign(free_nodes.end() - (long)take, free_nodes.end());
             free_nodes.resize(free_nodes.size() - take);
             if (fresh) {
@@ -3687,6 +3699,7 @@ struct tm_engine {
         s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
         s.dbg = checked ? R.d_dbg : nullptr;
         b->end_recorded = false;
+        b->dense_enq = false;
         int grc = 1;
         if (graph) {
             grc = launch_graph(b, a, s, S);
@@ -3704,7 +3717,10 @@ struct tm_engine {
         b->scan_args = s;
         if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
         if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
-        if ((b->oneshot || b->eager_dense) && (rc = enqueue_dense_tail(b, S))) return rc;
+        if (b->oneshot || b->eager_dense) {
+            if ((rc = enqueue_dense_tail(b, S))) return rc;
+            b->dense_enq = true;
+        }
         HIP_OK(hipEventRecord(b->ev_end, S));
         b->end_recorded = true;
         return TM_OK;
@@ -3982,7 +3998,9 @@ struct tm_engine {
         }
         fill_stats(b);
         b->done = true;
-        b->dense = eager_csr || (b->eager_dense && !b->oneshot && b->total <= b->dense_cap);
+        // (dense_enq, not eager_dense: the pipelined caller clears eager_dense
+        // right after launch, while the tail it asked for is already queued)
+        b->dense = eager_csr || (b->dense_enq && !b->oneshot && b->total <= b->dense_cap);
         if (b->dense && !eager_csr) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, b->evc0, b->evc1);
@@ -5216,15 +5234,19 @@ int tm_batch_launch(tm_engine* e, tm_batch* b) {
 int tm_batch_wait(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
     if (!b->rep) return TM_ENODEV;   // host-only engine
-    // A batch on a stream of its own is waited for without the engine lock,
-    // so other replicas' launches (async pipelines, other callers' batches)
-    // proceed meanwhile; the caller owns b, and wait() below finds its stream
-    // drained.  A batch on the replica's shared stream is waited for under the
-    // lock (in wait()): another thread may be capturing a graph on that stream,
-    // and a synchronize on a capturing stream is refused (and breaks the capture).
-    if (b->launched && !b->done && b->own) {
+    // The walk is waited for without the engine lock, so other callers
+    // (mutations, other replicas' launches, the async launcher's inline
+    // launches) proceed meanwhile; the caller owns b.  A launch that recorded
+    // its end event is waited for on that event -- an event wait does not
+    // touch the stream, which another thread may be capturing a graph on (a
+    // synchronize on a capturing stream is refused and breaks the capture).
+    // A batch on a stream of its own without an end event drains its stream.
+    // Only a shared-stream batch without an end event waits under the lock
+    // (in wait()).  wait() then finds the work done: its own sync is a check.
+    if (b->launched && !b->done && (b->end_recorded || b->own)) {
         HIP_OK(hipSetDevice(b->rep->device));
-        HIP_OK(hipStreamSynchronize(b->own));
+        if (b->end_recorded) HIP_OK(hipEventSynchronize(b->ev_end));
+        else HIP_OK(hipStreamSynchronize(b->own));
     }
     static const bool wtrace = getenv("TM_WAIT_TRACE") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
@@ -5591,7 +5613,11 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
             if (del_open) ins_open = !e->par_begin(false, ins_filters, ins_offsets, n_ins, e->mut_w2, RI);
         } catch (...) {
             if (!del_open) throw;
-            irc = TM_ENOMEM;   // (par_begin's setup throws before its phase 1 changes anything)
+            // par_begin's setup allocates everything before it commits (takes
+            // free ids, grows the node arrays); what it did before that --
+            // new words interned, pending ids released -- leaves a consistent
+            // engine, so the deletes' edge work can still be finished below
+            irc = TM_ENOMEM;
         }
         done = 0;
         if (del_open) {

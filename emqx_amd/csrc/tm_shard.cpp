@@ -377,11 +377,17 @@ struct tm_sharded {
             uint64_t rn = 0, rw = 0;
             for (uint32_t i = 0; i < G; ++i) {
                 const Slice& S = b->src[i];
-                if (rw > 0xFFFFFFF0ull) return TM_EOVERFLOW;
                 b->R[i * G + j] = (uint32_t)rn;
                 b->W[i * G + j] = (uint32_t)rw;
                 rn += S.n ? S.part_n(j) : 0;
                 rw += S.n ? S.part_w(G, j) : 0;
+                // (after every slice, the last included: shard j's part batch
+                // and the scatter's word offsets are u32)
+                if (rn > 0xFFFFFFF0ull || rw > 0xFFFFFFF0ull) {
+                    snprintf(error_buf(), 512, "shard %u's part exceeds u32 offsets: %llu publishes, %llu words", j,
+                             (unsigned long long)rn, (unsigned long long)rw);
+                    return TM_EOVERFLOW;
+                }
             }
             b->pn[j] = (uint32_t)rn;
             b->pw[j] = rw;
