@@ -787,22 +787,37 @@ def run_group(args):
         "matches_per_step": st["matches"],
     }
     # self-check: >= 3,000 sampled rows of every device's slice against one
-    # replica on device 0 (a separate engine over the same filters)
+    # replica on device 0 (a separate engine over the same filters).  The
+    # sampled rows are gathered on each slice's device (tm_group_sample):
+    # nothing else of the N x 10M-row result crosses to the host
     from emqx_amd import selfcheck as SC
     from emqx_amd.engine import Engine
-    offs, ids = b.result()
     rep = grp.engine()
     lo = [n * k // ng for k in range(ng + 1)]
+    host_bytes = [0]
+
+    def grp_rows(idx):
+        so, si = b.sample(idx)
+        host_bytes[0] += so.nbytes + si.nbytes
+        return SC.rows_from_csr(so, si, np.arange(len(idx)), SC.engine_names(rep))
     ref = Engine(device=0)
     ref.insert_many(filters)
-    sc = group_selfcheck(lambda idx: SC.rows_from_csr(offs, ids, idx, SC.engine_names(rep)), topics, lo,
-                         [f"slice {k} (device {d})" for k, d in enumerate(devs)], ref)
+    sc = group_selfcheck(grp_rows, topics, lo, [f"slice {k} (device {d})" for k, d in enumerate(devs)], ref)
     ref.close()
+    sc["host_result_bytes"] = host_bytes[0]
     out["selfcheck"] = sc
     out["parity_sample_ok"] = sc["parity_sample_ok"]
     out["devices"] = devs
     b.free()
     grp.close()
+    # per device the workload is the N = 1 line's (C2 trie, --topics publishes):
+    # the committed PMC pass of that launch gives its HBM traffic
+    out["roofline"]["traffic"] = pmc_traffic("C2", args.topics)
+    if not args.no_cpu:
+        # north_star: the CPU reference on this host's cores in the same run, at every N
+        host = host_cpu_share()
+        out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), host)
+        out["speedup_vs_cpu_allcore"] = out["value"] / out["cpu_baseline"]["value"]
     print(json.dumps(out), flush=True)
 
 
@@ -812,11 +827,10 @@ def replica_selfcheck(eng, b, topics, sync, rank, label) -> dict:
     -- one replica on device 0 -- matches every rank's sampled publishes and
     compares bit-exactly.  Rank 0 returns the verdict, every rank the same."""
     from emqx_amd import selfcheck as SC
-    offs, ids = b.result()
     idx = SC.sample_index(len(topics))
     sample = [topics[int(i)] for i in idx]
-    rows = SC.rows_from_csr(offs, ids, idx, SC.engine_names(eng))
-    del offs, ids
+    so, si = b.sample(idx)               # gathered on the device: ~3,000 rows, not the 10M-row CSR
+    rows = SC.rows_from_csr(so, si, np.arange(len(idx)), SC.engine_names(eng))
     payloads = sync.allgather(SC.payload(sample, rows, label))
     verdict = "{}"
     if rank == 0:
@@ -1180,11 +1194,14 @@ def main():
     for x in bs:
         x.free()
 
-    if rank == 0 and ws == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
+        # north_star: the CPU reference timed on this host's cores in the same
+        # run at every N (rank 0, after the timed region; the other ranks are done)
         host = host_cpu_share()
         out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), host)
         out["speedup_vs_cpu_allcore"] = value / out["cpu_baseline"]["value"]
-        out["c1"] = c1_leg(host, device=local)
+        if ws == 1:
+            out["c1"] = c1_leg(host, device=local)
     if rank == 0 and ws == 1 and not args.profile and not args.no_c5:
         # config C5 in the driver's line: K = 100 and K = 10 filters per hot
         # topic, 10k subscribe/unsubscribe deltas per step

@@ -146,6 +146,7 @@ SIGNATURES = {
     "tm_batch_launch": (C.c_int, [P, P]),
     "tm_batch_wait": (C.c_int, [P, P]),
     "tm_batch_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_batch_sample": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_rows": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
@@ -193,6 +194,7 @@ SIGNATURES = {
     "tm_group_launch": (C.c_int, [P, P]),
     "tm_group_wait": (C.c_int, [P, P]),
     "tm_group_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_group_sample": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_group_batch_stats": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_group_batch_free": (None, [P, P]),
     "tm_group_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),

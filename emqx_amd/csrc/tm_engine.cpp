@@ -469,6 +469,7 @@ struct tm_batch {
     bool eager_dense = false;       // scan + finalize enqueued by launch (oneshot implies it)
     uint64_t dense_cap = 0;         // ids the enqueued finalize could hold
     bool dense_enq = false;         // the LAST launch enqueued scan + finalize (set by launch, read by wait)
+    std::vector<uint32_t> h_smp_off, h_smp_ids;   // tm_batch_sample's last result (host CSR)
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
     uint8_t *h_xrow = nullptr, *h_xids = nullptr;
     size_t c_xrow = 0, c_xids = 0;
@@ -4039,6 +4040,55 @@ struct tm_engine {
     }
 
 
+    // tm_batch_sample: rows rows[0..k) of a waited batch as a host CSR, gathered
+    // on the device from where the walk wrote them (two small kernels and two
+    // small copies: count + start of each sampled row, then its ids).
+    int sample(tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* out) {
+        if (!b->done || !b->csr) return TM_EINVAL;
+        for (uint32_t i = 0; i < k; ++i)
+            if (rows[i] >= b->n) return TM_EINVAL;
+        const hipStream_t S = st(b);
+        b->h_smp_off.assign((size_t)k + 1, 0);
+        b->h_smp_ids.clear();
+        if (k) {
+            struct Scratch {
+                void* p = nullptr;
+                ~Scratch() { if (p) (void)hipFree(p); }
+            } meta, ids;
+            // [rows u32 k | cnt u32 k | pad | src u64 k | off u64 k + 1]
+            const size_t o_src = (((size_t)k * 8) + 15) & ~(size_t)15, o_off = o_src + (size_t)k * 8;
+            HIP_OK(hipMalloc(&meta.p, o_off + ((size_t)k + 1) * 8));
+            uint8_t* m = static_cast<uint8_t*>(meta.p);
+            uint32_t* d_rows = reinterpret_cast<uint32_t*>(m);
+            uint32_t* d_cnt = d_rows + k;
+            unsigned long long* d_src = reinterpret_cast<unsigned long long*>(m + o_src);
+            uint64_t* d_off = reinterpret_cast<uint64_t*>(m + o_off);
+            std::vector<uint32_t> cnt(k);
+            HIP_OK(hipMemcpyAsync(d_rows, rows, (size_t)k * 4, hipMemcpyHostToDevice, S));
+            HIP_OK(launch_sample_meta(b->d_count, b->d_src, d_rows, k, d_cnt, d_src, S));
+            HIP_OK(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)k * 4, hipMemcpyDeviceToHost, S));
+            HIP_OK(hipStreamSynchronize(S));
+            std::vector<uint64_t> off((size_t)k + 1, 0);
+            for (uint32_t i = 0; i < k; ++i) off[i + 1] = off[i] + cnt[i];
+            if (off[k] > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
+            for (uint32_t i = 0; i <= k; ++i) b->h_smp_off[i] = (uint32_t)off[i];
+            b->h_smp_ids.resize(off[k]);
+            if (off[k]) {
+                HIP_OK(hipMalloc(&ids.p, off[k] * 4));
+                HIP_OK(hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, S));
+                HIP_OK(launch_sample_ids(b->d_sfids, d_cnt, d_src, d_off, k, static_cast<uint32_t*>(ids.p), S));
+                HIP_OK(hipMemcpyAsync(b->h_smp_ids.data(), ids.p, off[k] * 4, hipMemcpyDeviceToHost, S));
+                HIP_OK(hipStreamSynchronize(S));
+            }
+        }
+        if (b->h_smp_ids.empty()) b->h_smp_ids.push_back(0);   // (a valid pointer for an empty result)
+        out->n_topics = k;
+        out->n_matches = b->h_smp_off[k];
+        out->row_offsets = b->h_smp_off.data();
+        out->filter_ids = b->h_smp_ids.data();
+        return TM_OK;
+    }
+
     // ------------------------------------------------------------ async pipeline
     // Every replica runs a pipeline of its own (slots, launcher, completers);
     // tm_match_async deals the calls over them.  Slots are created on first
@@ -5269,6 +5319,19 @@ int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {
     int rc = e->use(b->rep);
     if (rc) return rc;
     return e->result(b, out);
+}
+
+int tm_batch_sample(tm_engine* e, tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* out) {
+    if (!e || !b || !out || (!rows && k)) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->use(b->rep);
+    if (rc) return rc;
+    try {
+        return e->sample(b, rows, k, out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
 }
 
 int tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out) {

@@ -28,6 +28,7 @@ struct tm_group_batch {
     std::vector<uint32_t> filter_ids;
     std::vector<uint64_t> d_rows;          // merged deliveries (tm_group_dispatch)
     std::vector<uint32_t> d_subs;
+    std::vector<uint32_t> s_off, s_ids;    // tm_group_sample's last result
 };
 
 struct tm_group {
@@ -162,6 +163,46 @@ int tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out) {
     out->n_matches = total;
     out->row_offsets = b->row_offsets.data();
     out->filter_ids = b->filter_ids.data();
+    return TM_OK;
+}
+
+int tm_group_sample(tm_group* g, tm_group_batch* b, const uint32_t* publishes, uint32_t k, tm_result* out) {
+    if (!g || !b || !out || (!publishes && k) || b->parts.size() != tm_replica_count(g->e)) return TM_EINVAL;
+    const size_t np = b->parts.size();
+    // each slice samples its own publishes (local row indices), in one call
+    std::vector<std::vector<uint32_t>> local(np), where(np);
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t t = publishes[i];
+        if (t >= b->n) return TM_EINVAL;
+        const size_t s = (size_t)(std::upper_bound(b->lo.begin(), b->lo.end(), t) - b->lo.begin()) - 1;
+        local[s].push_back(t - b->lo[s]);
+        where[s].push_back(i);
+    }
+    std::vector<uint32_t> cnt(k, 0);
+    std::vector<std::vector<uint32_t>> rows(k);
+    for (size_t s = 0; s < np; ++s) {
+        if (local[s].empty()) continue;
+        tm_result r{};
+        int rc = tm_batch_sample(g->e, b->parts[s], local[s].data(), (uint32_t)local[s].size(), &r);
+        if (rc) return rc;
+        for (size_t j = 0; j < local[s].size(); ++j)
+            rows[where[s][j]].assign(r.filter_ids + r.row_offsets[j], r.filter_ids + r.row_offsets[j + 1]);
+    }
+    b->s_off.assign((size_t)k + 1, 0);
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        tot += rows[i].size();
+        if (tot > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+        b->s_off[i + 1] = (uint32_t)tot;
+    }
+    b->s_ids.clear();
+    b->s_ids.reserve(std::max<uint64_t>(tot, 1));
+    for (auto& r : rows) b->s_ids.insert(b->s_ids.end(), r.begin(), r.end());
+    if (b->s_ids.empty()) b->s_ids.push_back(0);
+    out->n_topics = k;
+    out->n_matches = tot;
+    out->row_offsets = b->s_off.data();
+    out->filter_ids = b->s_ids.data();
     return TM_OK;
 }
 

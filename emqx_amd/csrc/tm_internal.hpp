@@ -330,6 +330,11 @@ hipError_t launch_scatter_slots(Slot* slots, const uint32_t* idx, const Slot* va
 hipError_t launch_scatter_fmeta(uint64_t* foff, uint32_t* flen, const uint32_t* idx,
                                 const uint64_t* off, const uint32_t* len, uint32_t n, hipStream_t s);
 uint32_t scan_block_count(uint32_t n);
+// sampled rows of a waited batch (tm_batch_sample): per-row count + start, then the ids
+hipError_t launch_sample_meta(const uint32_t* count, const unsigned long long* src, const uint32_t* rows, uint32_t k,
+                              uint32_t* out_cnt, unsigned long long* out_src, hipStream_t s);
+hipError_t launch_sample_ids(const uint32_t* sfids, const uint32_t* cnt, const unsigned long long* src,
+                             const uint64_t* off, uint32_t k, uint32_t* out, hipStream_t s);
 // token batches (filter-sharded mode)
 hipError_t launch_token_check(const uint32_t* toff, const uint8_t* tflags, uint32_t n, uint64_t nwords,
                               uint32_t* slow_list, uint32_t* d_nslow, uint32_t* d_bad, hipStream_t s);

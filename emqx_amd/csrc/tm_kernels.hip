@@ -1520,6 +1520,32 @@ __global__ __launch_bounds__(256) void tm_rules_match(RulesArgs a) {
     }
 }
 
+// ------------------------------------------------ sampled rows (tm_batch_sample)
+
+// A few rows of a waited batch, as the walk left them (count + start into the
+// staging area), gathered into a compact CSR: the multi-device self-check
+// reads ~3,000 rows per slice this way instead of a whole 10M-row CSR.
+__global__ __launch_bounds__(256) void tm_sample_meta(const uint32_t* count, const unsigned long long* src,
+                                                       const uint32_t* rows, uint32_t k, uint32_t* out_cnt,
+                                                       unsigned long long* out_src) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= k) return;
+    const uint32_t r = rows[i];
+    out_cnt[i] = count[r];
+    out_src[i] = src[r];
+}
+
+// one wave per sampled row: its ids to out[off[i] ..)
+__global__ __launch_bounds__(64) void tm_sample_ids(const uint32_t* sfids, const uint32_t* cnt,
+                                                     const unsigned long long* src, const uint64_t* off,
+                                                     uint32_t* out) {
+    const uint32_t i = blockIdx.x;
+    const uint32_t c = cnt[i];
+    const unsigned long long s = src[i];
+    const uint64_t o = off[i];
+    for (uint32_t j = threadIdx.x; j < c; j += 64) out[o + j] = sfids[s + j];
+}
+
 // ------------------------------------------------ token batches (sharded mode)
 
 // Row gather for the sharded exchange: 16 lanes per row (rows are short: the
@@ -2378,6 +2404,18 @@ hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const
                               const int64_t* dst_off, uint32_t* dst, hipStream_t s) {
     if (n) hipLaunchKernelGGL(tm_gather_rows, dim3((uint32_t)(((uint64_t)n * 16 + 255) / 256)), dim3(256), 0, s, src,
                               src_off, idx, n, dst_off, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample_meta(const uint32_t* count, const unsigned long long* src, const uint32_t* rows, uint32_t k,
+                              uint32_t* out_cnt, unsigned long long* out_src, hipStream_t s) {
+    if (k) hipLaunchKernelGGL(tm_sample_meta, dim3((k + 255) / 256), dim3(256), 0, s, count, src, rows, k, out_cnt, out_src);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample_ids(const uint32_t* sfids, const uint32_t* cnt, const unsigned long long* src,
+                             const uint64_t* off, uint32_t k, uint32_t* out, hipStream_t s) {
+    if (k) hipLaunchKernelGGL(tm_sample_ids, dim3(k), dim3(64), 0, s, sfids, cnt, src, off, out);
     return hipGetLastError();
 }
 

@@ -97,6 +97,15 @@ class Batch:
         N.check(self.eng.L.tm_batch_result(self.eng.h, self.h, C.byref(r)), "tm_batch_result")
         return _result_arrays(r)
 
+    def sample(self, rows):
+        """tm_batch_sample: rows `rows` (row indices) of the waited batch,
+        gathered on the device -> (offsets u32[k+1], ids) in that order."""
+        idx = np.ascontiguousarray(np.asarray(rows, dtype=np.uint32))
+        r = N.Result()
+        N.check(self.eng.L.tm_batch_sample(self.eng.h, self.h, idx.ctypes.data, len(idx), C.byref(r)),
+                "tm_batch_sample")
+        return _result_arrays(r)
+
     def routes(self):
         """Device route resolution (tm_batch_routes) -> (row_offsets, filter_ids, dests)."""
         r = N.Routes()
@@ -262,6 +271,15 @@ class GroupBatch:
     def result(self):
         r = N.Result()
         N.check(self.grp.L.tm_group_result(self.grp.h, self.h, C.byref(r)), "tm_group_result")
+        return _result_arrays(r)
+
+    def sample(self, publishes):
+        """tm_group_sample: the rows of `publishes` (indices into the whole
+        batch), each gathered on its slice's device -> (offsets u32[k+1], ids)."""
+        idx = np.ascontiguousarray(np.asarray(publishes, dtype=np.uint32))
+        r = N.Result()
+        N.check(self.grp.L.tm_group_sample(self.grp.h, self.h, idx.ctypes.data, len(idx), C.byref(r)),
+                "tm_group_sample")
         return _result_arrays(r)
 
     def dispatch(self):

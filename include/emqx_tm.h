@@ -257,6 +257,14 @@ TM_API int  tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of,
 TM_API int  tm_batch_launch(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_wait(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out);
+/* Rows rows[0..k) of a waited batch (each < the batch's row count) as a host
+ * CSR: n_topics = k, row i = filter_ids[row_offsets[i] .. row_offsets[i+1]),
+ * sorted and deduplicated like tm_batch_result's.  Gathered on the device from
+ * where the walk wrote them -- no dense CSR, no whole-batch copy: a self-check
+ * of a 10M-publish batch reads ~3,000 rows this way.  Batch-owned memory,
+ * valid until the next tm_batch_sample, re-prepare or free of the batch.
+ * Replaces nothing in the reference (a diagnostic of the device result). */
+TM_API int  tm_batch_sample(tm_engine* e, tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* out);
 TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
 /* A waited batch's result is the rows as the walk wrote them to HBM: row i
  * (one per topic, or per distinct topic with TM_BATCH_DEDUP) is
@@ -538,6 +546,11 @@ TM_API int  tm_group_prepare(tm_group* g, const uint8_t* topics, const uint64_t*
 TM_API int  tm_group_launch(tm_group* g, tm_group_batch* b);
 TM_API int  tm_group_wait(tm_group* g, tm_group_batch* b);
 TM_API int  tm_group_result(tm_group* g, tm_group_batch* b, tm_result* out);
+/* tm_batch_sample over a group batch: publishes[0..k) (indices into the whole
+ * batch, any order) -> their rows as a host CSR in that order, each gathered
+ * on the device of the slice that holds it (group-owned memory, valid until
+ * the next tm_group_sample or free of the batch). */
+TM_API int  tm_group_sample(tm_group* g, tm_group_batch* b, const uint32_t* publishes, uint32_t k, tm_result* out);
 /* Counters summed over the slices; ms_match / ms_total = the slowest slice. */
 TM_API int  tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out);
 TM_API void tm_group_batch_free(tm_group* g, tm_group_batch* b);

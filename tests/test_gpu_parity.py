@@ -163,6 +163,16 @@ def test_walk_rows_are_the_result_without_a_csr_pass(rowcap):
     assert_same(T, got, exp)
     if rowcap:
         assert st["slow_topics"] > 1000
+    # tm_batch_sample: any rows, any order, gathered on the device (no CSR pass)
+    pick = np.array([len(T) - 1, 0, 5, 5] + list(range(3, len(T), 211)), dtype=np.uint32)
+    so, si = b.sample(pick)
+    assert b.stats()["ms_csr"] == 0.0
+    for j, k in enumerate(pick.tolist()):
+        assert np.array_equal(si[so[j]:so[j + 1]], stg[int(start[k]):int(start[k]) + int(cnt[k])])
+    so, si = b.sample([])
+    assert len(so) == 1 and len(si) == 0
+    with pytest.raises(RuntimeError):
+        b.sample([len(T)])          # past the last row: TM_EINVAL
     # the dense CSR, built on request, holds the same rows in topic order
     offs, ids = b.result()
     assert b.stats()["ms_csr"] > 0.0

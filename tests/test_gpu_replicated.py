@@ -148,6 +148,44 @@ def test_replicated_engine_splits_large_batches_like_one_engine(device_pair):
         assert_same(s, engine_rows(rep, s), e2)
 
 
+def test_c3_full_trie_split_over_device_pair_sampled_per_slice(device_pair):
+    """BASELINE config C3 at its own size: C2's 1M-filter trie replicated on
+    both devices of device_pair (tm_group), 1M C2 publishes split into one
+    slice per replica; every slice's 3,000-row sample -- gathered on its own
+    device (tm_group_sample) -- equals the oracle's rows (src/emqx_trie.erl
+    restated), and the merged CSR equals one single-replica engine's."""
+    from emqx_amd import selfcheck as SC
+    F = gen.gen_filters(gen.C2)
+    T = gen.gen_topics(gen.C2, F, 1000, 1_000_000)
+    grp = Group(device_pair)
+    assert grp.insert_many(F) == len(F)
+    grp.sync()
+    b = grp.prepare(T)
+    b.launch().wait()
+    n = len(T)
+    assert b.stats()["topics"] == n
+    rep = grp.engine()
+    Fl, Tl = F.tolist(), T.tolist()
+    lo = [0, n // 2, n]
+    for k in range(2):
+        idx = lo[k] + SC.sample_index(lo[k + 1] - lo[k])
+        assert len(idx) >= 3000
+        so, si = b.sample(idx)
+        sub = [Tl[int(i)] for i in idx]
+        exp, _ = oracle_rows(Fl, sub, nthreads=16)
+        got = [[rep.filter_bytes(int(x)) for x in si[so[j]:so[j + 1]]] for j in range(len(idx))]
+        assert_same(sub, got, exp)
+    # the whole split result = one engine's on device 0
+    offs, ids = b.result()
+    b.free()
+    grp.close()
+    one = Engine(device=0)
+    one.insert_many(F)
+    o1, i1 = one.match_batch(T)
+    assert np.array_equal(o1, offs) and np.array_equal(i1, ids)
+    one.close()
+
+
 def test_replicated_routes_rules_and_dispatch_equal_one_engine():
     p = replace(gen.C1, n_filters=4000)
     F = gen.gen_filters(p).tolist()

@@ -1,0 +1,54 @@
+#!/bin/bash
+# tools/gpu.sh TAG 'STEP ARGS' ... -- the steps of one gpurun call, each under a
+# time limit of its own, stopping at the first failure (no retries).  Output:
+# gpurun_out/TAG/<i>_<kind>.{json,log,err} and a one-line summary per step.
+#
+#   tests [PYTEST ARGS]      pytest -m gpu over tests/ (e.g. "tests -k 'sample or c3'")
+#   bench [BENCH ARGS]       python bench.py ARGS -> the JSON line, summarised
+#   prof [BENCH ARGS]        rocprofv3 --kernel-trace --stats of bench.py --profile ARGS
+#   pmc COUNTERS [ARGS]      one rocprofv3 --pmc pass (COUNTERS comma-free, '+'-joined)
+#   py SCRIPT [ARGS]         python SCRIPT ARGS
+# A step may start with T=<seconds> to override its time limit.
+#
+#   gpurun --timeout 900 -- tools/gpu.sh r5a 'tests -k sample' 'bench --gpus 2 --devices 0,0'
+set -o pipefail
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+i=0
+for step in "$@"; do
+    i=$((i + 1))
+    lim=""
+    if [[ $step == T=* ]]; then lim=${step%% *}; lim=${lim#T=}; step=${step#* }; fi
+    kind=${step%% *}
+    args=""
+    [[ $step == *" "* ]] && args=${step#* }
+    base=$O/${i}_$kind
+    eval "A=($args)"   # (quotes inside a step group words: "tests -k 'a or b'")
+    echo "== step $i: $kind $args" | tee -a "$O/steps.txt"
+    case $kind in
+    tests)
+        timeout -k 10 ${lim:-900} python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests "${A[@]}" \
+            > $base.log 2>&1 || { tail -40 $base.log; exit 1; }
+        tail -1 $base.log ;;
+    bench)
+        timeout -k 10 ${lim:-600} python -u bench.py "${A[@]}" > $base.json 2> $base.err || { tail -20 $base.err; exit 1; }
+        python tools/summarize.py $base.json ;;
+    prof)
+        timeout -k 10 ${lim:-300} rocprofv3 --kernel-trace --stats -d $base.d -o kt --output-format csv -- \
+            python3 bench.py --profile "${A[@]}" > $base.json 2> $base.err || { tail -20 $base.err; exit 1; }
+        find $base.d -name '*kernel_stats.csv' -exec head -6 {} \; ;;
+    pmc)
+        ctr=${A[0]}
+        timeout -s KILL ${lim:-120} rocprofv3 --pmc ${ctr//+/ } -d $base.d -o pmc --output-format csv -- \
+            python3 bench.py --profile "${A[@]:1}" > $base.json 2> $base.err || { tail -20 $base.err; exit 1; }
+        echo "pmc pass done: $ctr" ;;
+    py)
+        timeout -k 10 ${lim:-600} python -u "${A[@]}" > $base.log 2> $base.err || { tail -20 $base.err; exit 1; }
+        tail -5 $base.log ;;
+    *)
+        echo "unknown step kind: $kind"; exit 2 ;;
+    esac
+done
+echo DONE
