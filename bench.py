@@ -431,96 +431,111 @@ def run_c4_group(args):
     print(json.dumps(out), flush=True)
 
 
-def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2):
+def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, n_batches=3):
     """Config C5: 10k hot topics take 90% of the publishes, each matched by ~k
-    filters derived from it (+ 100k background C2-style filters); one step =
-    n_deltas subscribe/unsubscribe deltas applied to the trie and uploaded to
-    the device, then the deduplicated batch is matched (every distinct topic
-    once; rows longer than the fast path's K go to the generic kernel).
-    Returns the leg's measurements (publishes/s, churn and device ms)."""
+    filters derived from it (+ 100k background C2-style filters).  Every step
+    is a NEW batch of n_topics publishes (n_batches pre-generated batches,
+    their bytes resident in HBM, taken in turn) and n_deltas subscribe /
+    unsubscribe deltas:
+      host    the deltas applied to the trie (emqx_trie:delete/1, insert/1)
+              and their upload enqueued;
+      device  the batch tokenised (emqx_topic:words/1), deduplicated (equal
+              tokens walk once, TM_BATCH_DEDUP on the device), walked
+              (rows longer than K by the generic kernel), and every
+              publish's row expanded in HBM (tm_batch_publish_rows: the
+              per-publish result; its total is "delivered").
+    Pipelined: the host applies deltas i + 1 while the device runs step i
+    (the upload of deltas i + 1 is queued behind walk i, ahead of launch
+    i + 1: read-your-writes), so a step costs max(host, device)."""
     from emqx_amd import gen
     from emqx_amd.engine import Engine
     from emqx_amd.skew import Churn, workload
 
     p = gen.SkewParams(k_per_hot=k)
     t0 = time.time()
-    allf, derived, hot, pubs = workload(p, 100_000, n_topics, seed=seed)
-    log(f"[c5 k={k}] workload: {len(allf)} filters, {len(pubs)} publishes in {time.time() - t0:.1f}s")
+    allf, derived, hot, batches = workload(p, 100_000, n_topics, seed=seed, batches=n_batches)
+    log(f"[c5 k={k}] workload: {len(allf)} filters, {n_batches} x {len(batches[0])} publishes in "
+        f"{time.time() - t0:.1f}s")
     eng = Engine(device=device)
     eng.insert_many(allf)
     eng.sync()
     churn = Churn(hot, derived.tolist(), seed=seed + 6)
-    b = eng.prepare(pubs, dedup=True)
-    row_of, n_rows = b.row_map()
+    tp = time.perf_counter()
+    bs = [eng.prepare(pubs, dedup=True) for pubs in batches]    # bytes to HBM (inputs resident)
+    prepare_ms = 1e3 * (time.perf_counter() - tp) / n_batches
     for _ in range(warmup):
-        b.launch().wait()
+        for b in bs:
+            b.retokenize().launch().wait()
     if sync is not None:
         sync.barrier()
     # The deltas are drawn before timing, as packed binaries (what the NIF's
-    # route_apply hands over).  Step i applies deltas i (emqx_trie:delete/1 and
-    # insert/1 on the host mirror) and matches batch i against the result.
-    # Pipelined: the host applies deltas i + 1 while the device walks batch i
-    # -- the host mirror and the HBM replica are separate, and the upload of
-    # deltas i + 1 is queued behind walk i on the engine stream, ahead of
-    # launch i + 1 (read-your-writes) -- so the step costs max(apply, device)
-    # rather than their sum.
+    # route_apply hands over).  Step i applies deltas i and matches batch
+    # i mod n_batches against the result.
     deltas = []
     for _ in range(steps):
         dels, adds = churn.step(n_deltas)
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
-    ms_match, ms_churn, ms_walk, ms_tok, ms_queue = [], [], [], [], []
+    ms_dev, ms_walk, ms_tok, ms_dd, ms_x, ms_queue, ms_churn = [], [], [], [], [], [], []
+    rows, delivered = [], []
     ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
     t0 = time.perf_counter()
     tc = time.perf_counter()
     Churn.apply(eng, *deltas[0])
     ms_churn.append(1e3 * (time.perf_counter() - tc))
-    b.launch()
+    bs[0].retokenize().launch()
     for i in range(steps):
+        b = bs[i % n_batches]
         if i + 1 < steps:
             tc = time.perf_counter()
             Churn.apply(eng, *deltas[i + 1])
             ms_churn.append(1e3 * (time.perf_counter() - tc))
-            # the deltas' upload is gathered and enqueued now, behind batch i's
-            # walk on the engine stream (pinned staging: no host wait), so
-            # launch i + 1 has nothing left to upload
             tc = time.perf_counter()
-            eng.sync_async()
+            eng.sync_async()     # the upload, queued behind step i on the engine stream
             ms_host["sync_async"].append(1e3 * (time.perf_counter() - tc))
         tc = time.perf_counter()
         b.wait()
         ms_host["wait"].append(1e3 * (time.perf_counter() - tc))
         st = b.stats()
-        ms_match.append(st["ms_total"])
+        ms_dev.append(st["ms_tokenize"] + st["ms_dedup"] + st["ms_total"])
         ms_walk.append(st["ms_match"])
         ms_tok.append(st["ms_tokenize"])
+        ms_dd.append(st["ms_dedup"])
+        ms_x.append(st["ms_expand"])
         ms_queue.append(st["ms_queue"])
+        rows.append(st["topics"])
+        delivered.append(st["delivered"])
         if i + 1 < steps:
             tc = time.perf_counter()
-            b.launch()
+            bs[(i + 1) % n_batches].retokenize().launch()
             ms_host["launch"].append(1e3 * (time.perf_counter() - tc))
     elapsed = time.perf_counter() - t0
     if sync is not None:
         sync.barrier()
         elapsed = sync.allmax(elapsed)
-    st = b.stats()
-    offs, _ = b.result()
-    rowlen = np.diff(offs.astype(np.int64))
-    delivered = int(rowlen[row_of].sum())
-    n = len(pubs)
+    st = bs[(steps - 1) % n_batches].stats()
+    n = len(batches[0])
     out = {
         "k": k, "publishes_per_s": n * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "steps": steps,
-        "deltas_per_step": n_deltas, "filters": len(allf), "publishes": n, "distinct_topics": int(n_rows),
-        "device_ms": float(np.mean(ms_match)), "device_walk_ms": float(np.mean(ms_walk)),
-        "device_tokenize_ms": float(np.mean(ms_tok)),
+        "distinct_topics_per_s": float(np.sum(rows)) / elapsed,
+        "batches": n_batches, "fresh_batch_every_step": True,
+        "deltas_per_step": n_deltas, "filters": len(allf), "publishes": n, "distinct_topics": int(np.mean(rows)),
+        "prepare_ms": prepare_ms,
+        "device_ms": float(np.mean(ms_dev)), "device_walk_ms": float(np.mean(ms_walk)),
+        "device_tokenize_ms": float(np.mean(ms_tok)), "device_dedup_ms": float(np.mean(ms_dd)),
+        "device_expand_ms": float(np.mean(ms_x)),
         "device_queue_ms": float(np.mean(ms_queue)),
         "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
         "churn_ms_steps": [round(x, 3) for x in ms_churn],   # [0]: before the first launch (no walk beside it)
         "host_ms": {k: float(np.mean(v)) if v else 0.0 for k, v in ms_host.items()},
         "churn_overlapped_with_device": True,
-        "matches_delivered_per_step": delivered, "generic_path_topics": int(st["slow_topics"]),
+        # (publish, filter) matches per step, every publish's row materialised
+        # in HBM (tm_batch_publish_rows), summed on the device
+        "delivered_matches_per_step": int(np.mean(delivered)),
+        "generic_path_topics": int(st["slow_topics"]),
         "uploads_delta": eng.stats()["uploads_delta"],
     }
-    b.free()
+    for b in bs:
+        b.free()
     eng.close()
     return out
 
@@ -545,16 +560,21 @@ def run_c5(args, ws, rank, local, sync):
         "config": {"workload": f"C5: 10k hot topics x ~{args.c5_k} filters + 100k background, "
                                f"{leg['publishes']} publishes per GPU (90% hot, Zipf 1.0), {args.c5_deltas} deltas per step",
                    "filters": leg["filters"], "distinct_topics": leg["distinct_topics"],
-                   "mode": "replicated, dedup batches"},
+                   "mode": "replicated, a new batch every step, deduplicated on the device"},
         "device_pipeline_ms": leg["device_ms"],
         "device_walk_ms": leg["device_walk_ms"],
         "device_tokenize_ms": leg["device_tokenize_ms"],
+        "device_dedup_ms": leg["device_dedup_ms"],
+        "device_expand_ms": leg["device_expand_ms"],
         "churn_apply_ms": leg["churn_ms"],
         "churn_overlapped_with_device": True,
         "host_ms": leg["host_ms"],
         "churn_ms_steps": leg["churn_ms_steps"],
         "device_queue_ms": leg["device_queue_ms"],
-        "matches_delivered_per_step": leg["matches_delivered_per_step"],
+        "distinct_topics_per_s": ws * leg["distinct_topics_per_s"],
+        "prepare_ms": leg["prepare_ms"],
+        "fresh_batch_every_step": True,
+        "delivered_matches_per_step": leg["delivered_matches_per_step"],
         "generic_path_topics": leg["generic_path_topics"],
         "uploads_delta": leg["uploads_delta"],
     }

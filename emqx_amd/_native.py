@@ -81,7 +81,9 @@ class BatchStats(C.Structure):
                 ("words", C.c_uint64), ("matches", C.c_uint64), ("slow_topics", C.c_uint64),
                 ("overflow_tiles", C.c_uint64), ("ms_match", C.c_float), ("ms_total", C.c_float),
                 ("ms_tokenize", C.c_float), ("probes", C.c_uint64),
-                ("ms_csr", C.c_float), ("ms_queue", C.c_float), ("iterations", C.c_uint64)]
+                ("ms_csr", C.c_float), ("ms_queue", C.c_float), ("iterations", C.c_uint64),
+                ("publishes", C.c_uint64), ("delivered", C.c_uint64), ("ms_dedup", C.c_float),
+                ("ms_expand", C.c_float)]
 
     def asdict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -150,6 +152,7 @@ SIGNATURES = {
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_rows": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
+    "tm_batch_publish_rows": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),
     "tm_batch_free": (None, [P, P]),
     "tm_batch_retokenize": (C.c_int, [P, P]),
     "tm_route_add": (C.c_int, [P, U8P, SZ, C.c_uint32]),

@@ -470,6 +470,23 @@ struct tm_batch {
     uint64_t dense_cap = 0;         // ids the enqueued finalize could hold
     bool dense_enq = false;         // the LAST launch enqueued scan + finalize (set by launch, read by wait)
     std::vector<uint32_t> h_smp_off, h_smp_ids;   // tm_batch_sample's last result (host CSR)
+    // TM_BATCH_DEDUP on the device (device-tokenised batches, etm::DedupArgs):
+    // the n_pub publishes are deduplicated by their bytes, and only the rows
+    // (distinct topics) are tokenised and walked; n becomes the row count once
+    // a launch has been waited
+    bool dedup_dev = false;
+    bool dedup_stale = false;       // fresh bytes (prepare / retokenize): the next launch deduplicates
+    bool dedup_timed = false;       // the last launch deduplicated: evd.. is its time
+    bool rowof_host = false;        // row_of holds the device map of the last dedup pass
+    unsigned long long *d_dtab = nullptr, *d_psrc = nullptr;
+    uint32_t *d_drep = nullptr, *d_dflag = nullptr, *d_dblen = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
+    uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
+    uint8_t* d_cbytes = nullptr;
+    uint64_t* d_coffs = nullptr;
+    size_t c_dtab = 0, c_psrc = 0, c_drep = 0, c_dflag = 0, c_dblen = 0, c_drbs = 0, c_dbbs = 0, c_rowof = 0;
+    size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0;
+    uint64_t dtab_mask = 0, dd_bytes = 0;
+    hipEvent_t evd = nullptr, evx0 = nullptr, evx1 = nullptr;   // before the dedup pass; around the expand
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
     uint8_t *h_xrow = nullptr, *h_xids = nullptr;
     size_t c_xrow = 0, c_xids = 0;
@@ -558,6 +575,14 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
+        dev_free(d_dtab); dev_free(d_psrc); dev_free(d_drep); dev_free(d_dflag); dev_free(d_dblen); dev_free(d_drbs);
+        dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount); dev_free(d_cbytes); dev_free(d_coffs);
+        c_dtab = c_psrc = c_drep = c_dflag = c_dblen = c_drbs = c_dbbs = c_rowof = 0;
+        c_dd = c_pcount = c_cbytes = c_coffs = 0;
+        for (hipEvent_t* ev : {&evd, &evx0, &evx1}) {
+            if (*ev) (void)hipEventDestroy(*ev);
+            *ev = nullptr;
+        }
         dev_free(d_bytes); dev_free(d_boffs); dev_free(d_wcount); dev_free(d_in);
         in_bytes = nullptr;
         in_offs = nullptr;
@@ -3499,17 +3524,18 @@ struct tm_engine {
         b->n_pub = n;
         b->row_of.clear();
         b->dev_tok = false;
+        b->dedup_dev = b->dedup_stale = b->rowof_host = false;
         if (device >= 0 && dev_tok) {
             b->launched = b->done = false;
             b->tokens_only = false;
-            if (b->dedup) {
-                dedup_topics(b, topics, offsets, n);
-                return upload_bytes(b, b->bytes.data(), b->offs.data(), b->n);
-            }
             b->n = n;
             b->bytes.clear();
             b->offs.clear();
-            return upload_bytes(b, topics, offsets, n);
+            int rc = upload_bytes(b, topics, offsets, n);
+            if (rc || !b->dedup) return rc;
+            // deduplicated on the device at launch, ahead of the tokeniser
+            b->dedup_dev = b->dedup_stale = true;
+            return reserve_dedup(b, offsets[n] - offsets[0]);
         }
         if (b->dedup) {
             dedup_topics(b, topics, offsets, n);
@@ -3574,6 +3600,58 @@ struct tm_engine {
         return TM_OK;
     }
 
+    // the device dedup's buffers for b->n publishes of nbytes bytes
+    int reserve_dedup(tm_batch* b, uint64_t nbytes) {
+        int rc;
+        const size_t n = b->n;
+        uint64_t cap = 1024;
+        while (cap < (uint64_t)n + n / 2) cap <<= 1;   // load <= 2/3 when every publish is distinct
+        b->dtab_mask = cap - 1;
+        b->dd_bytes = nbytes;
+        const size_t nb = scan_block_count((uint32_t)n) + 1;
+        if ((rc = dev_reserve(b->d_dtab, b->c_dtab, cap))) return rc;
+        if ((rc = dev_reserve(b->d_drep, b->c_drep, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_dflag, b->c_dflag, n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_dblen, b->c_dblen, n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_drbs, b->c_drbs, nb))) return rc;
+        if ((rc = dev_reserve(b->d_dbbs, b->c_dbbs, nb))) return rc;
+        if ((rc = dev_reserve(b->d_rowof, b->c_rowof, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_cbytes, b->c_cbytes, nbytes + 32))) return rc;   // (the tokeniser's 16-B windows)
+        if ((rc = dev_reserve(b->d_coffs, b->c_coffs, n + 1))) return rc;
+        if ((rc = dev_reserve(b->d_dd, b->c_dd, 2))) return rc;
+        if ((rc = dev_reserve(b->d_pcount, b->c_pcount, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_psrc, b->c_psrc, std::max<size_t>(n, 1)))) return rc;
+        if (!b->evd) {
+            HIP_OK(hipEventCreate(&b->evd));
+            HIP_OK(hipEventCreate(&b->evx0));
+            HIP_OK(hipEventCreate(&b->evx1));
+        }
+        return TM_OK;
+    }
+
+    DedupArgs dedup_args(tm_batch* b) const {
+        DedupArgs d{};
+        d.bytes = b->in_bytes; d.offs = b->in_offs; d.base = b->tok_base; d.n = b->n_pub;
+        d.table = b->d_dtab; d.mask = b->dtab_mask;
+        d.rep = b->d_drep; d.rflag = b->d_dflag; d.blen = b->d_dblen; d.rbs = b->d_drbs; d.bbs = b->d_dbbs;
+        d.row_of = b->d_rowof; d.cbytes = b->d_cbytes; d.coffs = b->d_coffs; d.dd = b->d_dd;
+        d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
+        d.stats = b->d_stats;
+        return d;
+    }
+
+    // the dedup pass over the batch's resident bytes, ahead of the tokeniser
+    int enqueue_dedup(tm_batch* b, hipStream_t S) {
+        const DedupArgs d = dedup_args(b);
+        HIP_OK(hipMemsetAsync(b->d_dtab, 0, (b->dtab_mask + 1) * 8, S));
+        if (!d.n) HIP_OK(hipMemsetAsync(b->d_dd, 0, 8, S));   // (no compact kernel: zero rows)
+        ScanArgs rs{}, bs{};
+        rs.count = d.rflag; rs.row_off = d.rflag; rs.block_sums = b->d_drbs; rs.n = d.n;   // (in place)
+        bs.count = d.blen; bs.row_off = d.blen; bs.block_sums = b->d_dbbs; bs.n = d.n;
+        HIP_OK(launch_dedup(d, rs, bs, S));
+        return TM_OK;
+    }
+
     int tokens_pending(tm_batch* b) {
         b->h_words.clear(); b->h_toff.clear(); b->h_tflags.clear(); b->h_slow.clear();
         b->dev_tok = true;
@@ -3634,10 +3712,25 @@ struct tm_engine {
             if ((rc = host_reserve(R.h_dbg, R.ch_dbg, 8))) return rc;
             HIP_OK(hipMemsetAsync(R.d_dbg, 0, 8 * 4, S));
         }
-        const bool tokenize_now = b->dev_tok && b->tok_dict != dict.size();
-        const bool graph = csr && !checked && !tokenize_now && use_graphs && !b->gbad && b->n <= GRAPH_MAX;
+        // A device-deduplicated batch: fresh bytes are deduplicated first, and
+        // only the rows are tokenised (again when the dictionary grew) and
+        // walked.  The rows are counted on the device, so the tokeniser and
+        // the walk are sized for every publish (the bound) and read the count
+        // there; wait() sets n to the rows.
+        const bool dedup_now = b->dedup_dev && b->dedup_stale;
+        const bool tokenize_now = b->dev_tok && (b->tok_dict != dict.size() || dedup_now);
+        if (b->dedup_dev) b->n = b->n_pub;
+        b->dedup_timed = dedup_now && csr;
+        const bool graph = csr && !checked && !tokenize_now && use_graphs && !b->gbad && b->n <= GRAPH_MAX &&
+                           !b->dedup_dev;
         if (!tokenize_now && !graph) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
         b->tok_timed = tokenize_now && csr;
+        if (dedup_now) {
+            if (b->dedup_timed) HIP_OK(hipEventRecord(b->evd, S));
+            if ((rc = enqueue_dedup(b, S))) return rc;
+            b->dedup_stale = false;
+            b->rowof_host = false;
+        }
         if (b->tok_timed) HIP_OK(hipEventRecord(b->evt, S));
         if (tokenize_now) {
             b->tok_dict = dict.size();
@@ -3650,6 +3743,10 @@ struct tm_engine {
             t.words_cap = b->c_words;
             t.slow_list = b->d_slow; t.d_nslow = b->d_nslow;
             t.tile_topics = tok_tile_topics(b->n, b->nwords - b->n);   // nwords = bytes + topics (reserve_tokens)
+            t.d_n = nullptr;
+            if (b->dedup_dev) {   // the rows' bytes, compacted by the dedup pass
+                t.bytes = b->d_cbytes; t.offs = b->d_coffs; t.base = 0; t.d_n = b->d_dd;
+            }
             ScanArgs ts{};
             ts.block_sums = b->d_bsums;
             HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
@@ -3667,6 +3764,7 @@ struct tm_engine {
         a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
         a.slow_list = b->d_slow; a.n_slow = b->dev_slow ? 0u : (uint32_t)b->h_slow.size();
         a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
+        a.d_n = b->dedup_dev ? b->d_dd : nullptr;   // the rows, counted by the dedup pass
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
         a.grid = match_waves(b->n, R.device, qcap);
         a.tile_topics = tile_topics(b->n);
@@ -3708,6 +3806,11 @@ struct tm_engine {
             if (grc == 1) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
         }
         if (grc == 1) HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
+            HIP_OK(hipEventRecord(b->evx0, S));
+            HIP_OK(launch_dedup_expand(dedup_args(b), S));
+            HIP_OK(hipEventRecord(b->evx1, S));
+        }
         note_launch(b);
         b->launched = true;
         b->done = false;
@@ -3916,13 +4019,18 @@ struct tm_engine {
     }
 
     void fill_stats(tm_batch* b) {
-        float ms_match = 0, ms_total = 0, ms_tok = 0;
+        float ms_match = 0, ms_total = 0, ms_tok = 0, ms_dd = 0, ms_x = 0;
         (void)hipEventElapsedTime(&ms_match, b->ev0, b->ev1);
         (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
         if (b->tok_timed) (void)hipEventElapsedTime(&ms_tok, b->evt, b->ev0);
+        if (b->dedup_timed) (void)hipEventElapsedTime(&ms_dd, b->evd, b->tok_timed ? b->evt : b->ev0);
+        if (b->dedup_dev) (void)hipEventElapsedTime(&ms_x, b->evx0, b->evx1);
         b->st.ms_tokenize = ms_tok;
+        b->st.ms_dedup = ms_dd;
+        b->st.ms_expand = ms_x;
+        b->st.publishes = b->dedup ? b->n_pub : b->n;
         float ms_q = 0;
-        (void)hipEventElapsedTime(&ms_q, b->evq, b->tok_timed ? b->evt : b->ev0);
+        (void)hipEventElapsedTime(&ms_q, b->evq, b->dedup_timed ? b->evd : b->tok_timed ? b->evt : b->ev0);
         b->st.ms_queue = ms_q;
         b->st.ms_csr = 0;   // set by ensure_dense
         b->st.topics = b->n;
@@ -3937,6 +4045,7 @@ struct tm_engine {
         b->st.ms_match = ms_match;
         b->st.ms_total = ms_total;
         b->total = b->st.matches;
+        b->st.delivered = b->dedup_dev ? b->h_stats[ST_DELIVERED] : b->st.matches;
     }
 
     // drained: the caller has already waited for the batch's stream (the
@@ -3962,6 +4071,10 @@ struct tm_engine {
                             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count());
             }
             if (attempt && relaunched) ++*relaunched;
+            if (b->dedup_dev) {   // the walk's rows: the distinct publishes counted by the dedup pass
+                b->n = b->h_ctrl[CTRL_NROWS];
+                b->scan_args.n = b->n;
+            }
             if (b->check_tokens && b->n && b->h_bad[1]) {
                 snprintf(last_error(), 512, "token batch failed the device check (word offsets or flags)");
                 return TM_EINVAL;
@@ -5262,6 +5375,24 @@ uint32_t tm_batch_replica(tm_engine* e, tm_batch* b) {
 int tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_t* n_rows) {
     if (!e || !b || !row_of) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
+    if (b->dedup_dev) {   // the device's map, once per dedup pass (the rows exist after the wait)
+        if (!b->done) return TM_EINVAL;
+        if (!b->rowof_host) {
+            int rc = e->use(b->rep);
+            if (rc) return rc;
+            b->row_of.resize(b->n_pub);
+            if (b->n_pub) {
+                HIP_OK(hipMemcpyAsync(b->row_of.data(), b->d_rowof, (size_t)b->n_pub * 4, hipMemcpyDeviceToHost,
+                                      e->st(b)));
+                HIP_OK(hipStreamSynchronize(e->st(b)));
+            }
+            b->rowof_host = true;
+        }
+        static const uint32_t none = 0;
+        *row_of = b->row_of.empty() ? &none : b->row_of.data();
+        if (n_rows) *n_rows = b->n;
+        return TM_OK;
+    }
     if (!b->dedup && b->row_of.size() != b->n) {
         b->row_of.resize(b->n);
         for (uint32_t i = 0; i < b->n; ++i) b->row_of[i] = i;
@@ -5364,11 +5495,23 @@ int tm_batch_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uin
     return TM_OK;
 }
 
+int tm_batch_publish_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uint64_t** d_start,
+                          const uint32_t** d_ids, uint64_t* n_delivered) {
+    if (!e || !b || !b->done || !b->csr) return TM_EINVAL;
+    if (b->dedup && !b->dedup_dev) return TM_EINVAL;   // host-deduplicated: rows per distinct topic only
+    if (d_count) *d_count = b->dedup_dev ? b->d_pcount : b->d_count;
+    if (d_start) *d_start = reinterpret_cast<const uint64_t*>(b->dedup_dev ? b->d_psrc : b->d_src);
+    if (d_ids) *d_ids = b->d_sfids;
+    if (n_delivered) *n_delivered = b->st.delivered;
+    return TM_OK;
+}
+
 int tm_batch_retokenize(tm_engine* e, tm_batch* b) {
     if (!e || !b) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
     if (!b->dev_tok) return TM_EINVAL;
     b->tok_dict = ~0ull;
+    b->dedup_stale = b->dedup_dev;   // a fresh pass over the resident bytes: deduplicated again
     return TM_OK;
 }
 

@@ -253,6 +253,9 @@ int tm_group_batch_stats(tm_group* g, tm_group_batch* b, tm_batch_stats* out) {
         s.ms_total = std::max(s.ms_total, p.ms_total);
         s.ms_tokenize = std::max(s.ms_tokenize, p.ms_tokenize);
         s.probes += p.probes;
+        s.iterations += p.iterations;
+        s.publishes += p.publishes;
+        s.delivered += p.delivered;
     }
     *out = s;
     return TM_OK;

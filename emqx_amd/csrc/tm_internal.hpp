@@ -125,6 +125,7 @@ enum Ctrl : uint32_t {
     CTRL_ERR = 2,           // error bits
     CTRL_SLOW_DONE = 3,
     CTRL_TILE_NEXT = 4,     // (unused: tail tickets live in MatchArgs.xtickets)
+    CTRL_NROWS = 5,         // TM_BATCH_DEDUP on the device: distinct topics (rows) of the batch
     CTRL_WORDS = 16
 };
 constexpr uint32_t ERR_STAGING = 1;      // staging capacity exceeded
@@ -137,6 +138,7 @@ constexpr uint64_t MAX_RESULT = 0xFFFFFFF0ull;
 
 
 enum StatIdx : uint32_t { ST_VISITS = 0, ST_HASH = 1, ST_WORDS = 2, ST_MATCHES = 3, ST_SLOW = 4, ST_PROBES = 5, ST_ITERS = 6,
+                          ST_DELIVERED = 7,   // TM_BATCH_DEDUP: sum over the publishes of their rows' lengths
                           ST_N = 8 };
 
 // The batch header block: ctrl (CTRL_WORDS u32) | stats (ST_N u64) | one
@@ -166,6 +168,8 @@ struct MatchArgs {
     const uint32_t* toff;     // n + 1 word offsets
     const uint8_t* tflags;
     uint32_t n;
+    const uint32_t* d_n;        // or null: the topic count is *d_n (<= n) -- a device-deduplicated
+                                // batch's rows, known only on the device when the walk is enqueued
     const uint32_t* slow_list;  // host-flagged slow topics
     uint32_t n_slow;
     const uint32_t* d_nslow;    // device-resident count of slow_list (token batches), or null
@@ -509,10 +513,48 @@ struct TokArgs {
     uint32_t* zero;           // optional: zero[0 .. zero_words) cleared by pass 1 (the batch's ctrl + stats)
     uint32_t zero_words;
     uint32_t tile_topics;     // topics per tokeniser tile (tok_tile_topics)
+    const uint32_t* d_n;      // or null: the topic count is *d_n (<= n, the launch's bound): a
+                              // device-deduplicated batch's rows
 };
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
+
+// TM_BATCH_DEDUP on the device (tm_dedup_*), before the tokeniser:
+// identical publishes (equal bytes) are tokenised and walked once.  A
+// publish's representative is the FIRST publish with its bytes (a hash table
+// of u64 {tag | index}, the index lowered to the minimum with atomicMin), so
+// rows come out in first-occurrence order, deterministically -- the same
+// rows as the host's dedup.  The representatives' bytes are compacted
+// (cbytes / coffs) and only they are tokenised and walked; row_of maps every
+// publish to its row.  After the walk, tm_dedup_expand gives every publish
+// its row's (count, start): the per-publish result.
+struct DedupArgs {
+    const uint8_t* bytes;     // the batch's publishes: bytes[offs[t] - base .. offs[t + 1] - base)
+    const uint64_t* offs;
+    uint64_t base;
+    uint32_t n;
+    unsigned long long* table;   // mask + 1 slots, zeroed
+    uint64_t mask;
+    uint32_t* rep;            // n: pass 1 the publish's table slot, pass 2 its representative
+    uint32_t* rflag;          // n + 1: 1 at a representative; scanned in place -> row ids (block-local)
+    uint32_t* blen;           // n + 1: a representative's bytes; scanned in place -> byte offsets (block-local)
+    const uint32_t* rbs;      // block sums of the two scans (SCAN_TILE entries per block)
+    const uint32_t* bbs;
+    uint32_t* row_of;         // n: row of each publish
+    uint8_t* cbytes;          // the rows' bytes, the tokeniser's input (16-B aligned, + 32 bytes of slack)
+    uint64_t* coffs;          // rows + 1 offsets into cbytes
+    uint32_t* dd;             // [0] rows: the tokeniser's and the walk's topic count (TokArgs / MatchArgs d_n)
+    // after the walk
+    uint32_t* ctrl;           // CTRL_NROWS for the host (written with the expansion: every launch)
+    const uint32_t* count;    // per row
+    const unsigned long long* src;
+    uint32_t* pcount;         // n: per publish
+    unsigned long long* psrc;
+    unsigned long long* stats;
+};
+hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);
+hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s);
 
 // tm_export_host: an async batch's per-topic results and rows -> pinned host memory
 struct ExportArgs {

@@ -670,6 +670,14 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
 template <bool CK, bool BIG, int QC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_tiles(MatchArgs a) {
     __shared__ TileLds<QC> L;
+    if (a.d_n) {
+        // a device-deduplicated batch: its rows are counted on the device.
+        // The grid was sized for the bound (every publish); tiles shrink
+        // until the rows cover every wave (a C5 batch's ~186k rows would
+        // otherwise be 2,900 tiles for 4,096 waves, the hot ones long)
+        a.n = *a.d_n;
+        while (a.tile_topics > 1 && (a.n + a.tile_topics - 1) / a.tile_topics < gridDim.x) a.tile_topics >>= 1;
+    }
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;   // topics per tile: 64, or fewer for small batches
     const uint32_t ntiles = (a.n + tt - 1) / tt;
@@ -1520,6 +1528,228 @@ __global__ __launch_bounds__(256) void tm_rules_match(RulesArgs a) {
     }
 }
 
+// ------------------------------------------------ device dedup (TM_BATCH_DEDUP)
+
+// 8 bytes at byte offset s of a 4-aligned LDS array (any alignment of s)
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t* base, uint32_t s) {
+    const uint32_t a = s & ~3u, sh = (s & 3u) * 8u;
+    const uint32_t d0 = *reinterpret_cast<const uint32_t*>(base + a);
+    const uint32_t d1 = *reinterpret_cast<const uint32_t*>(base + a + 4);
+    const uint32_t d2 = *reinterpret_cast<const uint32_t*>(base + a + 8);
+    const uint64_t lo = ((uint64_t)d1 << 32) | d0;
+    return sh ? (lo >> sh) | ((uint64_t)d2 << (64u - sh)) : lo;
+}
+
+__device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // first k (< 8) bytes of v
+    return k >= 8 ? v : (v & ((1ull << (8u * k)) - 1ull));
+}
+
+
+
+// 8 bytes at any byte offset of a buffer, as a little-endian u64: two aligned
+// 8-B reads and a funnel shift (LDS windows and HBM byte arrays are 16-B
+// aligned and padded, so the second read stays inside)
+struct GBytes {
+    const uint8_t* p;
+    __device__ __forceinline__ uint64_t at(uint64_t s) const {
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(p + (s & ~7ull));
+        const uint32_t sh = (uint32_t)(s & 7u) * 8u;
+        const uint64_t lo = q[0];
+        return sh ? (lo >> sh) | (q[1] << (64u - sh)) : lo;
+    }
+};
+struct LBytes {
+    const uint8_t* p;   // 4-B aligned LDS
+    __device__ __forceinline__ uint64_t at(uint64_t s) const { return lds_u64(p, (uint32_t)s); }
+};
+
+// a byte range's two 32-bit word hashes (the dictionary's chunk mixing) with
+// its length, as one 64-bit key, 8 bytes a step
+template <class B>
+__device__ __forceinline__ uint64_t bytes_hash(B src, uint64_t s, uint32_t n) {
+    uint32_t h1 = HW_SEED, h2 = HW_SEED2;
+    for (uint32_t i = 0; i < n; i += 8) {
+        const uint64_t c = low_bytes(src.at(s + i), n - i < 8 ? n - i : 8);
+        uint32_t d = mix_chunk((uint32_t)c);
+        h1 = hw_acc(h1, d);
+        h2 = hw_acc(h2, d);
+        d = mix_chunk((uint32_t)(c >> 32));
+        h1 = hw_acc(h1, d);
+        h2 = hw_acc(h2, d);
+    }
+    return ((uint64_t)hw_final(h1, n) << 32) | hw_final(h2, n ^ 0x5BD1E995u);
+}
+
+// equal byte ranges of length n?  (8 bytes a step; the reads of a step are independent)
+template <class B, class C>
+__device__ __forceinline__ bool bytes_equal(B x, uint64_t sx, C y, uint64_t sy, uint32_t n) {
+    uint64_t diff = 0;
+    for (uint32_t i = 0; i < n; i += 8) {
+        const uint32_t k = n - i < 8 ? n - i : 8;
+        diff |= low_bytes(x.at(sx + i) ^ y.at(sy + i), k);
+    }
+    return diff == 0;
+}
+
+// the global table: find or claim the topic's slot (see tm_dedup_insert)
+__device__ __forceinline__ uint32_t dedup_global(const DedupArgs& a, uint32_t t, uint64_t b, uint32_t len, uint64_t h) {
+    const unsigned long long tag = (unsigned long long)((h >> 32) | 1u) << 32;
+    const GBytes g{a.bytes};
+    uint64_t i = h & a.mask;
+    for (;;) {
+        unsigned long long v = __hip_atomic_load(&a.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == 0) {
+            v = atomicCAS(&a.table[i], 0ull, tag | t);
+            if (v == 0) break;
+        }
+        if ((v & 0xFFFFFFFF00000000ull) == tag) {
+            const uint32_t o = (uint32_t)v;
+            const uint64_t ob = a.offs[o] - a.base;
+            if (a.offs[o + 1] - a.base - ob == len && bytes_equal(g, ob, g, b, len)) {
+                if (t < o) atomicMin(&a.table[i], tag | t);
+                break;
+            }
+        }
+        i = (i + 1) & a.mask;
+    }
+    return (uint32_t)i;
+}
+
+// Pass 1, one thread per publish, DD_BLOCK publishes per workgroup: the
+// topic's slot of the global table.  The slot holds {tag (hash hi, | 1) << 32
+// | index}; an equal topic with a lower index lowers it (atomicMin: the tag
+// bits are equal), so the slot ends at the topic's first publish.  Slot values
+// only change under device-scope atomics, so a stale read costs at most a
+// failed CAS, which returns the current value.
+//
+// Hot topics would put hundreds of thousands of threads on one slot's line
+// (C5: Zipf over 10k hot topics, the first takes ~9% of the publishes), so
+// the workgroup first collapses its own publishes in LDS, where its bytes are
+// staged: equal hashes elect the lowest publish as the workgroup's leader, a
+// follower checks its bytes against the leader's (one whose bytes differ --
+// a hash collision -- goes to the global table itself), and only leaders
+// touch the global table; followers take their leader's slot.
+constexpr uint32_t DD_BLOCK = 512;
+constexpr uint32_t DD_LT = 1024;      // LDS slots (load <= 1/2)
+constexpr uint32_t DD_BCAP = 32768;   // the workgroup's bytes staged in LDS (more: read from HBM); 3 workgroups / CU
+
+__global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
+    __shared__ unsigned long long lkey[DD_LT];
+    __shared__ uint32_t lmin[DD_LT];
+    __shared__ uint32_t lslot[DD_LT];
+    __shared__ __attribute__((aligned(16))) uint8_t lbytes[DD_BCAP + 16];
+    for (uint32_t k = threadIdx.x; k < DD_LT; k += DD_BLOCK) {
+        lkey[k] = 0;
+        lmin[k] = NONE;
+    }
+    const uint32_t t0 = blockIdx.x * DD_BLOCK;
+    const uint32_t t = t0 + threadIdx.x;
+    const bool valid = t < a.n;
+    const uint64_t wb = a.offs[t0] - a.base, we = a.offs[min(t0 + DD_BLOCK, a.n)] - a.base;
+    const uint64_t w0 = wb & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
+    const bool staged = we - w0 <= DD_BCAP;
+    if (staged)
+        for (uint64_t k = 16u * threadIdx.x; k < we - w0; k += 16u * DD_BLOCK)
+            *reinterpret_cast<uint4*>(lbytes + k) = *reinterpret_cast<const uint4*>(a.bytes + w0 + k);
+    uint64_t b = 0;
+    uint32_t len = 0, s = 0;
+    uint64_t h = 0;
+    if (valid) {
+        b = a.offs[t] - a.base;
+        len = (uint32_t)(a.offs[t + 1] - a.base - b);
+    }
+    const LBytes lw{lbytes};
+    const GBytes gw{a.bytes};
+    __syncthreads();
+    if (valid) {
+        h = (staged ? bytes_hash(lw, b - w0, len) : bytes_hash(gw, b, len)) | 1ull;   // (0: a free LDS slot)
+        s = (uint32_t)(h >> 7) & (DD_LT - 1);
+        for (;;) {
+            const unsigned long long o = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
+            if (o == 0 || o == h) break;
+            s = (s + 1) & (DD_LT - 1);
+        }
+        atomicMin(&lmin[s], threadIdx.x);
+    }
+    __syncthreads();
+    const uint32_t lead = valid ? lmin[s] : NONE;
+    bool own = valid && lead == threadIdx.x;
+    if (valid && !own) {   // a follower: equal bytes to its leader's, or on its own
+        const uint64_t lb = a.offs[t0 + lead] - a.base;
+        const uint32_t ll = (uint32_t)(a.offs[t0 + lead + 1] - a.base - lb);
+        own = ll != len || !(staged ? bytes_equal(lw, lb - w0, lw, b - w0, len) : bytes_equal(gw, lb, gw, b, len));
+    }
+    uint32_t gi = 0;
+    if (own) {
+        gi = dedup_global(a, t, b, len, h);
+        if (lead == threadIdx.x) lslot[s] = gi;
+    }
+    __syncthreads();
+    if (valid) a.rep[t] = own ? gi : lslot[s];
+}
+
+// Pass 2: the representative of every publish; scan inputs (1 per
+// representative, and its byte count)
+__global__ __launch_bounds__(256) void tm_dedup_mark(DedupArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n) return;
+    const uint32_t r = (uint32_t)a.table[a.rep[t]];
+    a.rep[t] = r;
+    const bool first = r == t;
+    a.rflag[t] = first ? 1u : 0u;
+    a.blen[t] = first ? (uint32_t)(a.offs[t + 1] - a.offs[t]) : 0u;
+}
+
+// Pass 3 (after the two scans): row of every publish; each representative
+// copies its bytes to its row of the tokeniser's input
+__global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t == 0) {   // totals: the scans left them at [n]
+        const uint32_t rows = a.rflag[a.n];
+        a.coffs[0] = 0;
+        a.coffs[rows] = a.blen[a.n];
+        a.dd[0] = rows;
+    }
+    if (t >= a.n) return;
+    const uint32_t r = a.rep[t];
+    const uint32_t row = a.rflag[r] + a.rbs[r / SCAN_TILE];
+    a.row_of[t] = row;
+    if (r != t) return;
+    const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
+    const uint64_t o = (uint64_t)a.blen[t] + a.bbs[t / SCAN_TILE];
+    if (row) a.coffs[row] = o;
+    for (uint64_t k = 0; k < e - b; ++k) a.cbytes[o + k] = a.bytes[b + k];
+}
+
+// After the walk: every publish gets its row's (count, start) -- the result
+// per publish -- and the batch's delivered matches are summed (one atomic per
+// block)
+constexpr uint32_t EXPAND_PER_THREAD = 16;
+__global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
+    __shared__ unsigned long long sh[4];
+    unsigned long long sum = 0;
+    const uint32_t base = blockIdx.x * 256 * EXPAND_PER_THREAD + threadIdx.x;
+#pragma unroll
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
+        const uint32_t t = base + u * 256;
+        if (t < a.n) {
+            const uint32_t r = a.row_of[t];
+            const uint32_t c = a.count[r];
+            a.pcount[t] = c;
+            a.psrc[t] = a.src[r];
+            sum += c;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long s4 = sh[0] + sh[1] + sh[2] + sh[3];
+        if (s4) atomicAdd(&a.stats[ST_DELIVERED], s4);
+        if (blockIdx.x == 0) a.ctrl[CTRL_NROWS] = a.dd[0];   // the rows, for the host's read-back
+    }
+}
+
 // ------------------------------------------------ sampled rows (tm_batch_sample)
 
 // A few rows of a waited batch, as the walk left them (count + start into the
@@ -1887,6 +2117,11 @@ __global__ __launch_bounds__(64) void tm_tok_count(TokArgs a) {
         for (uint32_t i = lane; i < a.zero_words; i += 64) a.zero[i] = 0;
     }
     const uint32_t tt = a.tile_topics;
+    if (a.d_n) {   // a device-counted batch: the tiles past its topics count 0 words (the scan covers the bound)
+        const uint32_t nb = (a.n + tt - 1) / tt;
+        a.n = *a.d_n;
+        for (uint32_t i = (a.n + tt - 1) / tt + blockIdx.x * 64 + lane; i < nb; i += gridDim.x * 64) a.wcount[i] = 0;
+    }
     const uint32_t ntiles = (a.n + tt - 1) / tt;
     const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
     const uint32_t first = blockIdx.x * per, last = min(first + per, ntiles);
@@ -1942,21 +2177,6 @@ struct alignas(16) TokLds {
     uint32_t ttoff[TILE + 1];           // tile-local first word of each topic; [cnt] = words
     uint32_t tirr[TILE];                // a word of the topic starts with '+' but is not '+'
 };
-
-// 8 bytes at byte offset s of a 4-aligned LDS array (any alignment of s)
-__device__ __forceinline__ uint64_t lds_u64(const uint8_t* base, uint32_t s) {
-    const uint32_t a = s & ~3u, sh = (s & 3u) * 8u;
-    const uint32_t d0 = *reinterpret_cast<const uint32_t*>(base + a);
-    const uint32_t d1 = *reinterpret_cast<const uint32_t*>(base + a + 4);
-    const uint32_t d2 = *reinterpret_cast<const uint32_t*>(base + a + 8);
-    const uint64_t lo = ((uint64_t)d1 << 32) | d0;
-    return sh ? (lo >> sh) | ((uint64_t)d2 << (64u - sh)) : lo;
-}
-
-__device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // first k (< 8) bytes of v
-    return k >= 8 ? v : (v & ((1ull << (8u * k)) - 1ull));
-}
-
 
 #ifndef TM_TOK_WPL
 #define TM_TOK_WPL 2
@@ -2081,6 +2301,7 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
     __shared__ TokLds L;
+    if (a.d_n) a.n = *a.d_n;   // a device-counted batch (its bound sized the grid and the scan)
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;
     const uint32_t ntiles = (a.n + tt - 1) / tt;
@@ -2404,6 +2625,24 @@ hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const
                               const int64_t* dst_off, uint32_t* dst, hipStream_t s) {
     if (n) hipLaunchKernelGGL(tm_gather_rows, dim3((uint32_t)(((uint64_t)n * 16 + 255) / 256)), dim3(256), 0, s, src,
                               src_off, idx, n, dst_off, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s) {
+    if (!a.n) return hipGetLastError();
+    const dim3 g((a.n + 255) / 256);
+    hipLaunchKernelGGL(tm_dedup_insert, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(tm_dedup_mark, g, dim3(256), 0, s, a);
+    hipError_t e;
+    if ((e = launch_scan(rows_scan, s, nullptr)) != hipSuccess) return e;
+    if ((e = launch_scan(bytes_scan, s, nullptr)) != hipSuccess) return e;
+    hipLaunchKernelGGL(tm_dedup_compact, g, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s) {
+    const uint32_t g = (a.n + 256 * EXPAND_PER_THREAD - 1) / (256 * EXPAND_PER_THREAD);
+    hipLaunchKernelGGL(tm_dedup_expand, dim3(g ? g : 1u), dim3(256), 0, s, a);   // (block 0 reports the rows)
     return hipGetLastError();
 }
 

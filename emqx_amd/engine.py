@@ -179,6 +179,16 @@ class Batch:
                                          C.byref(n)), "tm_batch_rows")
         return cnt.value, start.value, ids.value, n.value
 
+    def publish_rows_device(self):
+        """tm_batch_publish_rows: device pointers of every PUBLISH's row
+        (count u32[publishes], start u64[publishes], ids) and the delivered
+        (publish, filter) matches; for a device-deduplicated batch the rows
+        expanded behind the walk."""
+        cnt, start, ids, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_uint64()
+        N.check(self.eng.L.tm_batch_publish_rows(self.eng.h, self.h, C.byref(cnt), C.byref(start), C.byref(ids),
+                                                 C.byref(n)), "tm_batch_publish_rows")
+        return cnt.value, start.value, ids.value, n.value
+
     def rows(self, n_rows: int):
         """Host copy of the walk's rows (tm_batch_rows + hipMemcpy, for tests):
         (count u32[n_rows], start u64[n_rows], staging u32[max end])."""

@@ -18,14 +18,19 @@ from . import gen
 
 
 def workload(p: gen.SkewParams, n_background_filters: int, n_publishes: int, seed: int = 5,
-             background_pool: int = 200_000, p_hot: float = 0.9):
-    """-> (all filters, hot-derived filters, hot topics, publishes) as gen.Strings."""
+             background_pool: int = 200_000, p_hot: float = 0.9, batches: int = 0):
+    """-> (all filters, hot-derived filters, hot topics, publishes) as gen.Strings;
+    batches > 0: publishes is a list of that many batches, each a different
+    draw (seed + 300 + j) over the same hot set and background pool."""
     hot, derived = gen.gen_skew(p)
     bp = replace(gen.C2, seed=seed + 100, n_filters=n_background_filters)
     background = gen.gen_filters(bp)
     pool = gen.gen_topics(bp, background, seed + 200, background_pool)
-    pubs = gen.gen_pick(hot, pool, seed + 300, n_publishes, p_hot, 1.0)
     allf = gen.Strings.from_list(derived.tolist() + background.tolist())
+    if batches:
+        pubs = [gen.gen_pick(hot, pool, seed + 300 + j, n_publishes, p_hot, 1.0) for j in range(batches)]
+    else:
+        pubs = gen.gen_pick(hot, pool, seed + 300, n_publishes, p_hot, 1.0)
     return allf, derived, hot, pubs
 
 

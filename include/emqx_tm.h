@@ -101,6 +101,10 @@ typedef struct {
     float    ms_csr;        /* device time of the last dense-CSR build (scan + copy; 0: not built) */
     float    ms_queue;      /* device time from the last launch call to its pipeline's start (work queued ahead) */
     uint64_t iterations;    /* frontier iterations of the tile walk (each pops <= 64 probes) */
+    uint64_t publishes;     /* publishes of the batch (TM_BATCH_DEDUP: >= topics, the rows) */
+    uint64_t delivered;     /* sum over the publishes of their rows' lengths (= matches without dedup) */
+    float    ms_dedup;      /* device time of the last device dedup pass (0: none) */
+    float    ms_expand;     /* device time of the per-publish row expansion (TM_BATCH_DEDUP) */
 } tm_batch_stats;
 
 typedef struct {
@@ -233,8 +237,13 @@ TM_API int  tm_batch_prepare(tm_engine* e, const uint8_t* topics, const uint64_t
                       uint32_t n, tm_batch** out);
 /* tm_batch_prepare with flags.  TM_BATCH_DEDUP: identical topics of the batch
  * are matched once (hot-topic skew, BASELINE config C5); the result then has
- * one row per DISTINCT topic (tm_result.n_topics = distinct count) and
- * tm_batch_row_map gives the row of every publish. */
+ * one row per DISTINCT topic (tm_result.n_topics = distinct count, rows in
+ * first-occurrence order) and tm_batch_row_map gives the row of every
+ * publish.  With the device tokeniser (the default) the dedup runs on the
+ * device at launch, behind the tokeniser, on every fresh pass over the batch
+ * (prepare / tm_batch_retokenize): the row count and row_of exist once the
+ * batch has been waited, and tm_batch_publish_rows gives every publish its
+ * row in HBM. */
 #define TM_BATCH_DEDUP 1u
 /* TM_BATCH_STREAM: the batch runs on a HIP stream of its own, so launches of
  * different batches overlap on the device (one batch's CSR pass with the
@@ -274,6 +283,16 @@ TM_API int  tm_batch_stats_get(tm_engine* e, tm_batch* b, tm_batch_stats* out);
  * no extra pass.  *n_matches = sum of the counts. */
 TM_API int  tm_batch_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uint64_t** d_start,
                           const uint32_t** d_ids, uint64_t* n_matches);
+/* The result per PUBLISH of a waited batch, on the device: publish i's
+ * sorted, deduplicated filter ids are d_ids[d_start[i] .. d_start[i] +
+ * d_count[i]).  For a TM_BATCH_DEDUP batch deduplicated on the device this is
+ * every publish's row (expanded behind the walk: publishes of one topic share
+ * the ids), and *n_delivered = the sum of the counts -- the (publish, filter)
+ * matches delivered (emqx_broker:publish/1 matches every message,
+ * src/emqx_broker.erl:201-210); without TM_BATCH_DEDUP it is tm_batch_rows.
+ * TM_EINVAL for a batch deduplicated on the host. */
+TM_API int  tm_batch_publish_rows(tm_engine* e, tm_batch* b, const uint32_t** d_count, const uint64_t** d_start,
+                                  const uint32_t** d_ids, uint64_t* n_delivered);
 /* Device pointers of the batch's dense CSR: row_offsets[n + 1], ids[total]
  * in topic order.  Built from the rows on first request after a launch
  * (scan + one copy, on the batch's stream; tm_batch_result, routes, dispatch

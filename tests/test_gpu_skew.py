@@ -21,18 +21,19 @@ def test_skew_dedup_churn_parity():
     eng.insert_many(allf)
     churn = Churn(hot, derived.tolist(), seed=3)
     b = eng.prepare(pubs, dedup=True)
-    row_of, n_rows = b.row_map()
-    assert n_rows < len(pubs) // 3                      # the skew collapses most publishes
     T = pubs.tolist()
-    distinct = {}
-    for i, r in enumerate(row_of.tolist()):
-        distinct.setdefault(r, T[i])
-        assert distinct[r] == T[i]
     for rnd in range(3):
         if rnd:
             dels, adds = churn.step(600)
             Churn.apply(eng, dels, adds)
         b.launch().wait()
+        row_of, n_rows = b.row_map()                    # (the device dedup's, after the wait)
+        assert n_rows < len(pubs) // 3                  # the skew collapses most publishes
+        # one row per distinct topic (bytes), in first-occurrence order
+        row_of_bytes = {}
+        for i, r in enumerate(row_of.tolist()):
+            assert row_of_bytes.setdefault(T[i], r) == r
+        assert len(row_of_bytes) == n_rows and sorted(row_of_bytes.values()) == list(range(n_rows))
         offs, ids = b.result()
         assert len(offs) == n_rows + 1
         st = b.stats()
@@ -42,15 +43,17 @@ def test_skew_dedup_churn_parity():
         for f in F:
             orc.register(f)
             orc.insert(f)
-        Td = [distinct[r] for r in range(n_rows)]
-        buf, o = P.pack(Td)
+        U = sorted(row_of_bytes)                        # every distinct publish, by its own bytes
+        buf, o = P.pack(U)
         counts, idx, _ = orc.match_batch(buf, o, nthreads=8)
+        orc.close()
         cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
         cache = {}
-        for r in range(n_rows):
+        for j, tp in enumerate(U):
+            r = row_of_bytes[tp]
             got = [cache.setdefault(int(x), eng.filter_bytes(int(x))) for x in ids[offs[r]:offs[r + 1]]]
-            exp = [F[int(j)] for j in idx[cut[r]:cut[r + 1]]]
-            assert got == exp, (rnd, Td[r][:60])
+            exp = [F[int(k)] for k in idx[cut[j]:cut[j + 1]]]
+            assert got == exp, (rnd, tp[:60])
     assert eng.stats()["uploads_delta"] >= 1
 
 
@@ -66,6 +69,7 @@ def test_churn_applied_while_the_device_walks():
     eng.insert_many(allf)
     churn = Churn(hot, derived.tolist(), seed=4)
     b = eng.prepare(pubs, dedup=True)
+    b.launch().wait()          # sizes the staging area: no capacity re-run inside the pipelined rounds
     row_of, n_rows = b.row_map()
     T = pubs.tolist()
     distinct = {}
@@ -73,7 +77,6 @@ def test_churn_applied_while_the_device_walks():
         distinct.setdefault(r, T[i])
     Td = [distinct[r] for r in range(n_rows)]
     snapshot = sorted(churn.live_set) + background
-    b.launch().wait()          # sizes the staging area: no capacity re-run inside the pipelined rounds
     b.launch()
     for rnd in range(3):
         dels, adds = churn.step(800)                      # deltas of the NEXT step
