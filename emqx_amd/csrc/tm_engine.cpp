@@ -481,10 +481,11 @@ struct tm_batch {
     unsigned long long *d_dtab = nullptr, *d_psrc = nullptr;
     uint32_t *d_drep = nullptr, *d_dflag = nullptr, *d_dblen = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
     uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
+    uint16_t* d_dlead = nullptr;
     uint8_t* d_cbytes = nullptr;
     uint64_t* d_coffs = nullptr;
     size_t c_dtab = 0, c_psrc = 0, c_drep = 0, c_dflag = 0, c_dblen = 0, c_drbs = 0, c_dbbs = 0, c_rowof = 0;
-    size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0;
+    size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0, c_dlead = 0;
     uint64_t dtab_mask = 0, dd_bytes = 0;
     hipEvent_t evd = nullptr, evx0 = nullptr, evx1 = nullptr;   // before the dedup pass; around the expand
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
@@ -577,8 +578,9 @@ struct tm_batch {
         dev_free(d_nslow);
         dev_free(d_dtab); dev_free(d_psrc); dev_free(d_drep); dev_free(d_dflag); dev_free(d_dblen); dev_free(d_drbs);
         dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount); dev_free(d_cbytes); dev_free(d_coffs);
+        dev_free(d_dlead);
         c_dtab = c_psrc = c_drep = c_dflag = c_dblen = c_drbs = c_dbbs = c_rowof = 0;
-        c_dd = c_pcount = c_cbytes = c_coffs = 0;
+        c_dd = c_pcount = c_cbytes = c_coffs = c_dlead = 0;
         for (hipEvent_t* ev : {&evd, &evx0, &evx1}) {
             if (*ev) (void)hipEventDestroy(*ev);
             *ev = nullptr;
@@ -3611,6 +3613,7 @@ struct tm_engine {
         const size_t nb = scan_block_count((uint32_t)n) + 1;
         if ((rc = dev_reserve(b->d_dtab, b->c_dtab, cap))) return rc;
         if ((rc = dev_reserve(b->d_drep, b->c_drep, std::max<size_t>(n, 1)))) return rc;
+        if ((rc = dev_reserve(b->d_dlead, b->c_dlead, std::max<size_t>(n, 1)))) return rc;
         if ((rc = dev_reserve(b->d_dflag, b->c_dflag, n + 1))) return rc;
         if ((rc = dev_reserve(b->d_dblen, b->c_dblen, n + 1))) return rc;
         if ((rc = dev_reserve(b->d_drbs, b->c_drbs, nb))) return rc;
@@ -3633,12 +3636,15 @@ struct tm_engine {
         DedupArgs d{};
         d.bytes = b->in_bytes; d.offs = b->in_offs; d.base = b->tok_base; d.n = b->n_pub;
         d.table = b->d_dtab; d.mask = b->dtab_mask;
-        d.rep = b->d_drep; d.rflag = b->d_dflag; d.blen = b->d_dblen; d.rbs = b->d_drbs; d.bbs = b->d_dbbs;
+        d.rep = b->d_drep; d.lead = b->d_dlead; d.rflag = b->d_dflag; d.blen = b->d_dblen; d.rbs = b->d_drbs; d.bbs = b->d_dbbs;
         d.row_of = b->d_rowof; d.cbytes = b->d_cbytes; d.coffs = b->d_coffs; d.dd = b->d_dd;
         d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
         d.stats = b->d_stats;
+        d.weak_hash = dedup_weak_hash ? 1u : 0u;
         return d;
     }
+    // TM_DEDUP_WEAK_HASH=1 (tests): the dedup's hash degraded to the topic's length
+    const bool dedup_weak_hash = getenv("TM_DEDUP_WEAK_HASH") && atoi(getenv("TM_DEDUP_WEAK_HASH")) != 0;
 
     // the dedup pass over the batch's resident bytes, ahead of the tokeniser
     int enqueue_dedup(tm_batch* b, hipStream_t S) {

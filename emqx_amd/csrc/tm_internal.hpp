@@ -537,6 +537,7 @@ struct DedupArgs {
     unsigned long long* table;   // mask + 1 slots, zeroed
     uint64_t mask;
     uint32_t* rep;            // n: pass 1 the publish's table slot, pass 2 its representative
+    uint16_t* lead;           // n: pass 1's workgroup leader of the publish's hash (index in its workgroup)
     uint32_t* rflag;          // n + 1: 1 at a representative; scanned in place -> row ids (block-local)
     uint32_t* blen;           // n + 1: a representative's bytes; scanned in place -> byte offsets (block-local)
     const uint32_t* rbs;      // block sums of the two scans (SCAN_TILE entries per block)
@@ -552,6 +553,8 @@ struct DedupArgs {
     uint32_t* pcount;         // n: per publish
     unsigned long long* psrc;
     unsigned long long* stats;
+    uint32_t weak_hash;       // test knob (TM_DEDUP_WEAK_HASH): hash = length only, every same-length
+                              // topic collides -- exercises the byte check of tm_dedup_mark
 };
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s);

@@ -1591,10 +1591,11 @@ __device__ __forceinline__ bool bytes_equal(B x, uint64_t sx, C y, uint64_t sy, 
     return diff == 0;
 }
 
-// the global table: find or claim the topic's slot (see tm_dedup_insert)
-__device__ __forceinline__ uint32_t dedup_global(const DedupArgs& a, uint32_t t, uint64_t b, uint32_t len, uint64_t h) {
+// the global table: find or claim the slot of the topic with hash h (see
+// tm_dedup_insert); slots are told apart by the hash (tag + home slot), the
+// bytes are checked after (tm_dedup_mark)
+__device__ __forceinline__ uint32_t dedup_global(const DedupArgs& a, uint32_t t, uint64_t h) {
     const unsigned long long tag = (unsigned long long)((h >> 32) | 1u) << 32;
-    const GBytes g{a.bytes};
     uint64_t i = h & a.mask;
     for (;;) {
         unsigned long long v = __hip_atomic_load(&a.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1603,35 +1604,37 @@ __device__ __forceinline__ uint32_t dedup_global(const DedupArgs& a, uint32_t t,
             if (v == 0) break;
         }
         if ((v & 0xFFFFFFFF00000000ull) == tag) {
-            const uint32_t o = (uint32_t)v;
-            const uint64_t ob = a.offs[o] - a.base;
-            if (a.offs[o + 1] - a.base - ob == len && bytes_equal(g, ob, g, b, len)) {
-                if (t < o) atomicMin(&a.table[i], tag | t);
-                break;
-            }
+            if (t < (uint32_t)v) atomicMin(&a.table[i], tag | t);
+            break;
         }
         i = (i + 1) & a.mask;
     }
     return (uint32_t)i;
 }
 
-// Pass 1, one thread per publish, DD_BLOCK publishes per workgroup: the
-// topic's slot of the global table.  The slot holds {tag (hash hi, | 1) << 32
-// | index}; an equal topic with a lower index lowers it (atomicMin: the tag
-// bits are equal), so the slot ends at the topic's first publish.  Slot values
-// only change under device-scope atomics, so a stale read costs at most a
-// failed CAS, which returns the current value.
+// Pass 1, one thread per publish, DD_BLOCK publishes per workgroup: the slot
+// of the publish's 64-bit byte hash in the global table.  The slot holds
+// {tag (hash hi, | 1) << 32 | index}; a publish of the same hash with a lower
+// index lowers it (atomicMin: the tag bits are equal), so the slot ends at
+// the hash's first publish.  Slot values only change under device-scope
+// atomics, so a stale read costs at most a failed CAS, which returns the
+// current value.
 //
 // Hot topics would put hundreds of thousands of threads on one slot's line
 // (C5: Zipf over 10k hot topics, the first takes ~9% of the publishes), so
 // the workgroup first collapses its own publishes in LDS, where its bytes are
-// staged: equal hashes elect the lowest publish as the workgroup's leader, a
-// follower checks its bytes against the leader's (one whose bytes differ --
-// a hash collision -- goes to the global table itself), and only leaders
-// touch the global table; followers take their leader's slot.
+// staged for hashing: equal hashes elect the lowest publish as the
+// workgroup's leader, and only leaders touch the global table; followers
+// take their leader's slot.
+//
+// Exactness: a publish is a row's member only if its BYTES equal the row's
+// first publish's -- tm_dedup_mark compares every publish with its
+// representative, and one whose bytes differ (a 64-bit hash collision) is
+// made a row of its own.  Rows then stay exact; at worst a collided topic
+// gets more than one row.
 constexpr uint32_t DD_BLOCK = 512;
 constexpr uint32_t DD_LT = 1024;      // LDS slots (load <= 1/2)
-constexpr uint32_t DD_BCAP = 32768;   // the workgroup's bytes staged in LDS (more: read from HBM); 3 workgroups / CU
+constexpr uint32_t DD_BCAP = 32768;   // the workgroup's bytes staged in LDS (more: hashed from HBM); 3 workgroups / CU
 
 __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
     __shared__ unsigned long long lkey[DD_LT];
@@ -1658,11 +1661,10 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
         b = a.offs[t] - a.base;
         len = (uint32_t)(a.offs[t + 1] - a.base - b);
     }
-    const LBytes lw{lbytes};
-    const GBytes gw{a.bytes};
     __syncthreads();
     if (valid) {
-        h = (staged ? bytes_hash(lw, b - w0, len) : bytes_hash(gw, b, len)) | 1ull;   // (0: a free LDS slot)
+        h = (staged ? bytes_hash(LBytes{lbytes}, b - w0, len) : bytes_hash(GBytes{a.bytes}, b, len)) | 1ull;   // (0: free)
+        if (a.weak_hash) h = ((uint64_t)len << 40) | ((uint64_t)len << 8) | 1ull;
         s = (uint32_t)(h >> 7) & (DD_LT - 1);
         for (;;) {
             const unsigned long long o = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
@@ -1672,32 +1674,68 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
         atomicMin(&lmin[s], threadIdx.x);
     }
     __syncthreads();
-    const uint32_t lead = valid ? lmin[s] : NONE;
-    bool own = valid && lead == threadIdx.x;
-    if (valid && !own) {   // a follower: equal bytes to its leader's, or on its own
-        const uint64_t lb = a.offs[t0 + lead] - a.base;
-        const uint32_t ll = (uint32_t)(a.offs[t0 + lead + 1] - a.base - lb);
-        own = ll != len || !(staged ? bytes_equal(lw, lb - w0, lw, b - w0, len) : bytes_equal(gw, lb, gw, b, len));
-    }
-    uint32_t gi = 0;
-    if (own) {
-        gi = dedup_global(a, t, b, len, h);
-        if (lead == threadIdx.x) lslot[s] = gi;
-    }
+    const bool lead = valid && lmin[s] == threadIdx.x;
+    if (lead) lslot[s] = dedup_global(a, t, h);
     __syncthreads();
-    if (valid) a.rep[t] = own ? gi : lslot[s];
+    if (valid) {
+        a.rep[t] = lslot[s];
+        a.lead[t] = (uint16_t)lmin[s];
+    }
 }
 
-// Pass 2: the representative of every publish; scan inputs (1 per
-// representative, and its byte count)
-__global__ __launch_bounds__(256) void tm_dedup_mark(DedupArgs a) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.n) return;
-    const uint32_t r = (uint32_t)a.table[a.rep[t]];
+// Pass 2: the representative of every publish -- the first publish of its
+// hash, kept only if the bytes are equal -- and the scan inputs (1 per
+// representative, and its byte count).  Same workgroups as pass 1, bytes
+// staged in LDS: each workgroup leader checks its bytes against the
+// representative's (HBM), each follower against its leader's (LDS) and then
+// shares its leader's verdict.  A publish whose bytes differ from its
+// representative's (a 64-bit hash collision) is its own; its equal
+// followers follow it.
+__global__ __launch_bounds__(DD_BLOCK) void tm_dedup_mark(DedupArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lbytes[DD_BCAP + 16];
+    __shared__ uint32_t lb[DD_BLOCK], ll[DD_BLOCK], lrep[DD_BLOCK];
+    const uint32_t t0 = blockIdx.x * DD_BLOCK;
+    const uint32_t t = t0 + threadIdx.x;
+    const bool valid = t < a.n;
+    const uint64_t wb = a.offs[t0] - a.base, we = a.offs[min(t0 + DD_BLOCK, a.n)] - a.base;
+    const uint64_t w0 = wb & ~15ull;
+    const bool staged = we - w0 <= DD_BCAP;
+    if (staged)
+        for (uint64_t k = 16u * threadIdx.x; k < we - w0; k += 16u * DD_BLOCK)
+            *reinterpret_cast<uint4*>(lbytes + k) = *reinterpret_cast<const uint4*>(a.bytes + w0 + k);
+    uint64_t b = 0;
+    uint32_t len = 0, r = 0, lead = 0;
+    if (valid) {
+        b = a.offs[t] - a.base;
+        len = (uint32_t)(a.offs[t + 1] - a.base - b);
+        lb[threadIdx.x] = (uint32_t)(b - w0);
+        ll[threadIdx.x] = len;
+        lead = a.lead[t];
+        r = (uint32_t)a.table[a.rep[t]];
+    }
+    __syncthreads();
+    const GBytes g{a.bytes};
+    if (valid && lead == threadIdx.x) {   // a leader: its bytes against the representative's
+        if (r != t) {
+            const uint64_t rb = a.offs[r] - a.base;
+            bool eq = a.offs[r + 1] - a.base - rb == len;
+            if (eq) eq = staged ? bytes_equal(g, rb, LBytes{lbytes}, b - w0, len) : bytes_equal(g, rb, g, b, len);
+            if (!eq) r = t;
+        }
+        lrep[threadIdx.x] = r;
+    }
+    __syncthreads();
+    if (!valid) return;
+    if (lead != threadIdx.x) {   // a follower: equal to its leader, then the leader's representative
+        const uint64_t ob = w0 + lb[lead];
+        bool eq = ll[lead] == len;
+        if (eq) eq = staged ? bytes_equal(LBytes{lbytes}, lb[lead], LBytes{lbytes}, b - w0, len) : bytes_equal(g, ob, g, b, len);
+        r = eq ? lrep[lead] : t;
+    }
     a.rep[t] = r;
     const bool first = r == t;
     a.rflag[t] = first ? 1u : 0u;
-    a.blen[t] = first ? (uint32_t)(a.offs[t + 1] - a.offs[t]) : 0u;
+    a.blen[t] = first ? len : 0u;
 }
 
 // Pass 3 (after the two scans): row of every publish; each representative
@@ -1718,7 +1756,14 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
     const uint64_t o = (uint64_t)a.blen[t] + a.bbs[t / SCAN_TILE];
     if (row) a.coffs[row] = o;
-    for (uint64_t k = 0; k < e - b; ++k) a.cbytes[o + k] = a.bytes[b + k];
+    const GBytes g{a.bytes};
+    for (uint64_t k = 0; k < e - b; k += 8) {   // 8-B reads, byte stores (rows are packed, unaligned)
+        const uint64_t v = g.at(b + k);
+        const uint32_t m = e - b - k < 8 ? (uint32_t)(e - b - k) : 8u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (j < m) a.cbytes[o + k + j] = (uint8_t)(v >> (8 * j));
+    }
 }
 
 // After the walk: every publish gets its row's (count, start) -- the result
@@ -2632,7 +2677,7 @@ hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_s
     if (!a.n) return hipGetLastError();
     const dim3 g((a.n + 255) / 256);
     hipLaunchKernelGGL(tm_dedup_insert, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
-    hipLaunchKernelGGL(tm_dedup_mark, g, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tm_dedup_mark, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
     hipError_t e;
     if ((e = launch_scan(rows_scan, s, nullptr)) != hipSuccess) return e;
     if ((e = launch_scan(bytes_scan, s, nullptr)) != hipSuccess) return e;

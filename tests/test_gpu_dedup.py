@@ -88,6 +88,32 @@ def test_device_dedup_edge_topics_match_the_oracle_per_publish():
     b.free()
 
 
+def test_device_dedup_hash_collisions_stay_exact():
+    """TM_DEDUP_WEAK_HASH: the dedup's hash is the topic's length, so every
+    two topics of one length collide; the byte check of the mark pass must
+    keep each publish with a row of its own bytes (rows may then repeat a
+    topic, never mix two) -- results per publish still equal the oracle's."""
+    import os
+    os.environ["TM_DEDUP_WEAK_HASH"] = "1"
+    try:
+        eng = Engine(device=0)
+    finally:
+        del os.environ["TM_DEDUP_WEAK_HASH"]
+    for f in FILTERS:
+        eng.insert(f)
+    base = [b"a/b", b"a/c", b"x/y", b"a/b", b"q/r", b"a/c", b"$x/a", b"%x/a", b"a//b", b"a/zz1", b"a/zz2", b"a/zz1"]
+    T = [base[(i * 5) % len(base)] for i in range(2000)]
+    b = eng.prepare(T, dedup=True)
+    b.launch().wait()
+    row_of, n_rows = _check(eng, b, T)
+    # every row's publishes have equal bytes
+    first = {}
+    for i, r in enumerate(row_of.tolist()):
+        assert first.setdefault(r, T[i]) == T[i]
+    assert n_rows > len(set(base))            # collided topics got rows of their own
+    b.free()
+
+
 def test_device_dedup_large_skewed_batch_and_empty_batch():
     p = gen.SkewParams(seed=3, n_hot=300, k_per_hot=20)
     from emqx_amd.skew import workload
