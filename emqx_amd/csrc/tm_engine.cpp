@@ -3643,6 +3643,9 @@ struct tm_engine {
         d.weak_hash = dedup_weak_hash ? 1u : 0u;
         return d;
     }
+    // TM_FRESH_FUSED=1: a fresh batch's tokeniser fill inside the walk (tm_match_fresh).  Measured
+    // slower on C2 (fresh 10M batch 5.35 -> 5.64 ms, profiles/r05/fused/): off by default
+    const bool fresh_fused = getenv("TM_FRESH_FUSED") && atoi(getenv("TM_FRESH_FUSED")) != 0;
     // TM_DEDUP_WEAK_HASH=1 (tests): the dedup's hash degraded to the topic's length
     const bool dedup_weak_hash = getenv("TM_DEDUP_WEAK_HASH") && atoi(getenv("TM_DEDUP_WEAK_HASH")) != 0;
 
@@ -3738,9 +3741,12 @@ struct tm_engine {
             b->rowof_host = false;
         }
         if (b->tok_timed) HIP_OK(hipEventRecord(b->evt, S));
+        // a fresh batch's tokeniser fill runs inside the walk (tm_match_fresh)
+        const bool fuse = tokenize_now && !checked && !b->dedup_dev && fresh_fused;
+        TokArgs t{};
+        ScanArgs ts{};
         if (tokenize_now) {
             b->tok_dict = dict.size();
-            TokArgs t{};
             t.zero = reinterpret_cast<uint32_t*>(b->d_hdr);   // the tokeniser's first kernel clears ctrl + stats
             t.zero_words = tm_batch::HDR_FIXED / 4;
             t.bytes = b->in_bytes; t.offs = b->in_offs; t.base = b->tok_base; t.n = b->n;
@@ -3753,9 +3759,10 @@ struct tm_engine {
             if (b->dedup_dev) {   // the rows' bytes, compacted by the dedup pass
                 t.bytes = b->d_cbytes; t.offs = b->d_coffs; t.base = 0; t.d_n = b->d_dd;
             }
-            ScanArgs ts{};
+            // fused: one tile for both (any tile size is a valid walk tile)
+            if (fuse) t.tile_topics = std::min(t.tile_topics, tile_topics(b->n));
             ts.block_sums = b->d_bsums;
-            HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
+            if (!fuse) HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
         }
         if (b->check_tokens && b->n) {
             HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, S));
@@ -3774,6 +3781,11 @@ struct tm_engine {
         a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
         a.grid = match_waves(b->n, R.device, qcap);
         a.tile_topics = tile_topics(b->n);
+        if (fuse) {
+            a.tile_topics = t.tile_topics;
+            a.grid = (uint32_t)std::min<uint64_t>(((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics,
+                                                  match_waves(0xFFFFFFF0u, R.device, qcap));
+        }
         a.qcap = qcap;
         {   // the first static_frac of the tiles round-robin, the tail by per-XCD tickets
             const uint64_t ntiles = ((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics;
@@ -3811,7 +3823,9 @@ struct tm_engine {
             if (grc != 1 && grc) return grc;
             if (grc == 1) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
         }
-        if (grc == 1) HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
+        if (grc == 1 && fuse) HIP_OK(launch_match_fresh(a, t, ts, b->d_nslow + 1, S, csr ? b->ev0 : nullptr,
+                                                        csr ? b->ev1 : nullptr));
+        else if (grc == 1) HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
         if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
             HIP_OK(hipEventRecord(b->evx0, S));
             HIP_OK(launch_dedup_expand(dedup_args(b), S));

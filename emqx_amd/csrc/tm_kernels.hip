@@ -2226,7 +2226,7 @@ struct alignas(16) TokLds {
 #ifndef TM_TOK_WPL
 #define TM_TOK_WPL 2
 #endif
-constexpr uint32_t TOK_WPL = TM_TOK_WPL;   // words per lane per lookup round (register budget: occupancy)
+constexpr uint32_t TOK_WPL_FILL = TM_TOK_WPL;   // words per lane per lookup round (register budget: occupancy)
 
 // The tile's words w = lane + 64 k, TOK_WPL per lane at a time: start from
 // wst, length from the next word's start (the last word of a topic ends at
@@ -2237,8 +2237,9 @@ constexpr uint32_t TOK_WPL = TM_TOK_WPL;   // words per lane per lookup round (r
 // an empty primary slot means the word is absent).  Lookups are bound by L2
 // requests, not instructions: one per word is the point.
 // Entries (class << 29 | id) go straight to words[].
+template <uint32_t TOK_WPL>
 __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t tw, uint32_t wend,
-                                           uint64_t tile_base) {
+                                           uint64_t tile_base, uint32_t* lw) {
     const uint32_t lane = threadIdx.x;
     const uint32_t mask = (uint32_t)a.dict_mask;
     for (uint32_t base = 0; base < tw; base += 64 * TOK_WPL) {
@@ -2312,12 +2313,13 @@ __device__ __forceinline__ void tok_lookup(const TokArgs& a, TokLds& L, uint32_t
                 ent[k] = (ent[k] & ~WID_MASK) | (ck_match(a, e[k], head[k], len[k], L.bytes + st[k]) ? e[k].w : W_UNKNOWN);
             const uint32_t w = base + lane + 64 * k;
             if (w < tw && tile_base + w < a.words_cap) a.words[tile_base + w] = ent[k];
+            if (lw && w < tw) lw[w] = ent[k];   // (the fused walk: the tile's words stay in LDS too)
         }
     }
 }
 
 // lane-per-topic path of a tile too long for the LDS budget: bytes from HBM
-__device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t t, uint64_t o, bool& slow) {
+__device__ __forceinline__ uint8_t tok_fill_topic_global(const TokArgs& a, uint32_t t, uint64_t o, bool& slow) {
     const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
     const uint8_t* p = a.bytes;
     bool irregular = false;
@@ -2338,6 +2340,152 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
     if (irregular || nw > FAST_MAX_DEPTH) fl |= TF_SLOW;
     a.tflags[t] = fl;
     slow = (fl & TF_SLOW) != 0;
+    return fl;
+}
+
+// One tokeniser tile (tm_tok_fill, and the prologue of the fused walk
+// tm_match_fresh): words, offsets and flags to HBM, the generic-path list.
+// out: per lane, its topic's first word (tile-local), word count and flags;
+// lds = the tile went the LDS path (lw, if set, then holds its words).
+struct TokTile {
+    bool lds;
+    uint32_t w0, nw;
+    uint8_t fl;
+    uint64_t base;   // the tile's first word in words[]
+};
+// (WPL: words per lane per lookup round -- the fused walk's register budget is tighter)
+template <uint32_t WPL>
+__device__ __forceinline__ void tok_tile(const TokArgs& a, TokLds& L, uint32_t tile, uint32_t* lw, TokTile& out) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tt = a.tile_topics;
+    const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n), cnt = tend - t0;
+    const uint32_t t = t0 + lane;
+    const bool valid = lane < cnt;
+    const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
+    const uint64_t my_b = valid ? a.offs[t] - a.base : 0, my_e = valid ? a.offs[t + 1] - a.base : 0;
+    const uint64_t a0 = b0 & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
+    const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
+    bool slow = false;
+    // the LDS path: the window fits and no topic is empty (an empty topic
+    // starts where the next one does: one bit cannot mark both)
+    bool lds = b1 - a0 <= TOK_BYTES && !__any(valid && my_b == my_e);
+    uint32_t tw = 0, wend = 0, incl = 0, mine = 0;
+    uint64_t S = 0, TS = 0;
+    const uint32_t lb = lane * TOK_LANE_BYTES;   // my 48 bytes of the window
+    out.base = tile_base;
+    out.fl = (uint8_t)TF_SLOW;
+    out.w0 = out.nw = 0;
+    if (lds) {
+        wend = (uint32_t)(b1 - a0);
+        const uint32_t r0 = (uint32_t)(b0 - a0);
+        uint4 v[TOK_LANE_BYTES / 16];
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
+            v[k] = lb + 16 * k < wend ? *reinterpret_cast<const uint4*>(a.bytes + a0 + lb + 16 * k)
+                                      : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
+            *reinterpret_cast<uint4*>(L.bytes + lb + 16 * k) = v[k];
+        for (uint32_t i = lane; i < 2 * (TOK_BYTES / 64 + 1); i += 64) reinterpret_cast<uint32_t*>(L.tsb)[i] = 0u;
+        if (lane < TILE) L.tirr[lane] = 0;
+        __syncthreads();
+        if (valid) {
+            const uint32_t p = (uint32_t)(my_b - a0);
+            atomicOr(reinterpret_cast<unsigned long long*>(&L.tsb[p >> 6]), 1ull << (p & 63));
+        }
+        // '/' bytes of my 48 (inside [r0, wend)) and topic starts, as bit masks
+#pragma unroll
+        for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k) {
+            S |= (uint64_t)gather4(byte_eq(v[k].x, '/')) << (16 * k);
+            S |= (uint64_t)gather4(byte_eq(v[k].y, '/')) << (16 * k + 4);
+            S |= (uint64_t)gather4(byte_eq(v[k].z, '/')) << (16 * k + 8);
+            S |= (uint64_t)gather4(byte_eq(v[k].w, '/')) << (16 * k + 12);
+        }
+        const uint32_t lo = r0 > lb ? min(r0 - lb, TOK_LANE_BYTES) : 0u;
+        const uint32_t hi = wend > lb ? min(wend - lb, TOK_LANE_BYTES) : 0u;
+        S &= ((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull);
+        __syncthreads();
+        const uint32_t q = lb >> 6, sh = lb & 63;
+        TS = L.tsb[q] >> sh;
+        if (sh) TS |= L.tsb[q + 1] << (64 - sh);
+        TS &= (1ull << TOK_LANE_BYTES) - 1ull;
+        // word starts = topic starts + '/' bytes; one scan numbers them
+        mine = (uint32_t)(__popcll(S) + __popcll(TS)) | ((uint32_t)__popcll(TS) << 16);
+        incl = mine;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += u;
+        }
+        tw = __shfl(incl, 63, 64) & 0xFFFFu;
+        if (tw > TOK_WORDS) {
+            lds = false;
+            __syncthreads();
+        }
+    }
+    uint32_t nw = 0, tincl = 0;
+    if (!lds) {
+        // long tile: one lane per topic, bytes from HBM; in-tile offsets by
+        // a wave scan of the per-topic word counts ('/' + 1)
+        if (valid) {
+            nw = 1;
+            for (uint64_t i = my_b; i < my_e; ++i) nw += a.bytes[i] == '/';
+        }
+        tincl = nw;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(tincl, o, 64);
+            if (lane >= (uint32_t)o) tincl += u;
+        }
+        tw = __shfl(tincl, 63, 64);
+    }
+    if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
+    out.lds = lds;
+    if (lds) {
+        uint32_t wi = (incl - mine) & 0xFFFFu;            // my first word
+        int32_t tc = (int32_t)((incl - mine) >> 16) - 1;   // the topic my first byte is in
+        uint64_t m = S | TS;
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t pos = lb + b;
+            if (TS >> b & 1ull) {
+                ++tc;
+                L.ttoff[tc] = wi;
+                L.wst[wi] = (uint16_t)(pos | 0x8000u);
+                L.wtop[wi++] = (uint8_t)tc;
+            }
+            if (S >> b & 1ull) {
+                L.wst[wi] = (uint16_t)(pos + 1);
+                L.wtop[wi++] = (uint8_t)tc;
+            }
+        }
+        if (lane == 0) L.ttoff[cnt] = tw;
+        __syncthreads();
+        tok_lookup<WPL>(a, L, tw, wend, tile_base, lw);   // the tile's words, round-robin over lanes
+        __syncthreads();
+        if (valid) {
+            const uint32_t w0 = L.ttoff[lane], tn = L.ttoff[lane + 1] - w0;
+            uint8_t fl = 0;
+            if (L.bytes[my_b - a0] == '$') fl |= TF_DOLLAR;
+            if (L.tirr[lane] || tn > FAST_MAX_DEPTH) fl |= TF_SLOW;
+            a.tflags[t] = fl;
+            a.toff[t] = (uint32_t)(tile_base + w0);
+            slow = (fl & TF_SLOW) != 0;
+            out.w0 = w0;
+            out.nw = tn;
+            out.fl = fl;
+        }
+        tok_append_slow(a, slow, t);
+        __syncthreads();
+    } else {
+        const uint64_t o = tile_base + tincl - nw;
+        if (valid) {
+            a.toff[t] = (uint32_t)o;
+            out.fl = tok_fill_topic_global(a, t, o, slow);
+            out.w0 = tincl - nw;
+            out.nw = nw;
+        }
+        tok_append_slow(a, slow, t);
+    }
 }
 
 // pass 2 (after the scan of the tile counts): word entries, offsets, flags
@@ -2347,129 +2495,81 @@ __device__ __forceinline__ void tok_fill_topic_global(const TokArgs& a, uint32_t
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 8))) void tm_tok_fill(TokArgs a) {
     __shared__ TokLds L;
     if (a.d_n) a.n = *a.d_n;   // a device-counted batch (its bound sized the grid and the scan)
-    const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;
     const uint32_t ntiles = (a.n + tt - 1) / tt;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t t0 = tile * tt, tend = min(t0 + tt, a.n), cnt = tend - t0;
+    TokTile out;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) tok_tile<TOK_WPL_FILL>(a, L, tile, nullptr, out);
+}
+
+// ------------------------------------------------ fused fresh-batch walk
+// tm_match_fresh: a fresh batch's tokeniser fill folded into the walk.  Each
+// tile is tokenised in the walk's own prologue (tok_tile: the same words,
+// offsets, flags and generic-path list in HBM as tm_tok_fill), its words
+// kept in the LDS the walk then reads them from -- the byte window and the
+// tokeniser's scratch live in the probe stack's LDS, which is free until the
+// frontier loop starts.  The walk is memory-latency bound with idle VALU, so
+// the tokeniser's arithmetic runs beside other waves' probes instead of in a
+// launch of its own.  Tiles the LDS path cannot take (a window over 3 KB,
+// more than 512 words, an empty topic) are tokenised from HBM and their
+// topics sent to the generic kernel.  tm_tok_count + the scan still run
+// first: they give every tile its place in words[].
+#ifndef TM_FUSED_WPL
+#define TM_FUSED_WPL 1   // tokeniser words per lane per lookup round inside the walk (register budget)
+#endif
+template <bool BIG, int QC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_fresh(
+    MatchArgs a, TokArgs k) {
+    __shared__ TileLds<QC> L;
+    // the walk's counters, summed per tile into LDS: registers live across the
+    // whole kernel would sit beside the tokeniser's at its peak (and spill)
+    __shared__ unsigned long long acc[5];
+    static_assert(sizeof(TokLds) <= sizeof(L.q), "the tokeniser's LDS must fit in the probe stack");
+    TokLds& T = *reinterpret_cast<TokLds*>(L.q);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tt = a.tile_topics;   // == k.tile_topics (the host fuses only then)
+    const uint32_t ntiles = (a.n + tt - 1) / tt;
+    if (lane < 5) acc[lane] = 0;
+    uint32_t tile = blockIdx.x, round = 0;
+    while (tile < ntiles) {
+        uint32_t ticket = 0;
+        if (round + 1 >= a.static_rounds && lane == 0)
+            ticket = atomicAdd(&a.xg[(blockIdx.x % TICKET_GROUPS) * TICKET_STRIDE], 1u);
+        const uint32_t t0 = tile * tt;
+        const uint32_t tend = min(t0 + tt, a.n);
         const uint32_t t = t0 + lane;
-        const bool valid = lane < cnt;
-        const uint64_t b0 = a.offs[t0] - a.base, b1 = a.offs[tend] - a.base;
-        const uint64_t my_b = valid ? a.offs[t] - a.base : 0, my_e = valid ? a.offs[t + 1] - a.base : 0;
-        const uint64_t a0 = b0 & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
-        const uint64_t tile_base = (uint64_t)a.wcount[tile] + a.bsums[tile / SCAN_TILE];   // block-local scan + block offset
-        bool slow = false;
-        // the LDS path: the window fits and no topic is empty (an empty topic
-        // starts where the next one does: one bit cannot mark both)
-        bool lds = b1 - a0 <= TOK_BYTES && !__any(valid && my_b == my_e);
-        uint32_t tw = 0, wend = 0, incl = 0, mine = 0;
-        uint64_t S = 0, TS = 0;
-        const uint32_t lb = lane * TOK_LANE_BYTES;   // my 48 bytes of the window
-        if (lds) {
-            wend = (uint32_t)(b1 - a0);
-            const uint32_t r0 = (uint32_t)(b0 - a0);
-            uint4 v[TOK_LANE_BYTES / 16];
-#pragma unroll
-            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
-                v[k] = lb + 16 * k < wend ? *reinterpret_cast<const uint4*>(a.bytes + a0 + lb + 16 * k)
-                                          : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k)
-                *reinterpret_cast<uint4*>(L.bytes + lb + 16 * k) = v[k];
-            for (uint32_t i = lane; i < TOK_BYTES / 64 + 1; i += 64) L.tsb[i] = 0;
-            if (lane < TILE) L.tirr[lane] = 0;
+        const bool valid = lane < tt && t < a.n;
+        TokTile o;
+        tok_tile<TM_FUSED_WPL>(k, T, tile, L.words, o);   // (ends on a barrier: T is free for the stack)
+        if (o.lds) {
+            L.toff[lane] = o.w0;
+            L.depth[lane] = o.nw;
+            L.cnt[lane] = 0;
             __syncthreads();
-            if (valid) {
-                const uint32_t p = (uint32_t)(my_b - a0);
-                atomicOr(reinterpret_cast<unsigned long long*>(&L.tsb[p >> 6]), 1ull << (p & 63));
+            unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sP = 0;
+            match_tile<false, BIG, true>(a, L, t0, tend, 0, o.fl, valid, sV, sH, sW, sM, sP);
+            for (int x = 32; x > 0; x >>= 1) {
+                sV += __shfl_xor(sV, x, 64); sH += __shfl_xor(sH, x, 64);
+                sW += __shfl_xor(sW, x, 64); sM += __shfl_xor(sM, x, 64);
+                sP += __shfl_xor(sP, x, 64);
             }
-            // '/' bytes of my 48 (inside [r0, wend)) and topic starts, as bit masks
-#pragma unroll
-            for (uint32_t k = 0; k < TOK_LANE_BYTES / 16; ++k) {
-                S |= (uint64_t)gather4(byte_eq(v[k].x, '/')) << (16 * k);
-                S |= (uint64_t)gather4(byte_eq(v[k].y, '/')) << (16 * k + 4);
-                S |= (uint64_t)gather4(byte_eq(v[k].z, '/')) << (16 * k + 8);
-                S |= (uint64_t)gather4(byte_eq(v[k].w, '/')) << (16 * k + 12);
+            if (lane == 0) {
+                acc[0] += sV; acc[1] += sH; acc[2] += sW; acc[3] += sM; acc[4] += sP;
             }
-            const uint32_t lo = r0 > lb ? min(r0 - lb, TOK_LANE_BYTES) : 0u;
-            const uint32_t hi = wend > lb ? min(wend - lb, TOK_LANE_BYTES) : 0u;
-            S &= ((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull);
-            __syncthreads();
-            const uint32_t q = lb >> 6, sh = lb & 63;
-            TS = L.tsb[q] >> sh;
-            if (sh) TS |= L.tsb[q + 1] << (64 - sh);
-            TS &= (1ull << TOK_LANE_BYTES) - 1ull;
-            // word starts = topic starts + '/' bytes; one scan numbers them
-            mine = (uint32_t)(__popcll(S) + __popcll(TS)) | ((uint32_t)__popcll(TS) << 16);
-            incl = mine;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o, 64);
-                if (lane >= (uint32_t)o) incl += u;
-            }
-            tw = __shfl(incl, 63, 64) & 0xFFFFu;
-            if (tw > TOK_WORDS) {
-                lds = false;
-                __syncthreads();
-            }
-        }
-        uint32_t nw = 0, tincl = 0;
-        if (!lds) {
-            // long tile: one lane per topic, bytes from HBM; in-tile offsets by
-            // a wave scan of the per-topic word counts ('/' + 1)
-            if (valid) {
-                nw = 1;
-                for (uint64_t i = my_b; i < my_e; ++i) nw += a.bytes[i] == '/';
-            }
-            tincl = nw;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(tincl, o, 64);
-                if (lane >= (uint32_t)o) tincl += u;
-            }
-            tw = __shfl(tincl, 63, 64);
-        }
-        if (tend == a.n && lane == 0) a.toff[a.n] = (uint32_t)(tile_base + tw);
-        if (lds) {
-            uint32_t wi = (incl - mine) & 0xFFFFu;            // my first word
-            int32_t tc = (int32_t)((incl - mine) >> 16) - 1;   // the topic my first byte is in
-            uint64_t m = S | TS;
-            while (m) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                const uint32_t pos = lb + b;
-                if (TS >> b & 1ull) {
-                    ++tc;
-                    L.ttoff[tc] = wi;
-                    L.wst[wi] = (uint16_t)(pos | 0x8000u);
-                    L.wtop[wi++] = (uint8_t)tc;
-                }
-                if (S >> b & 1ull) {
-                    L.wst[wi] = (uint16_t)(pos + 1);
-                    L.wtop[wi++] = (uint8_t)tc;
-                }
-            }
-            if (lane == 0) L.ttoff[cnt] = tw;
-            __syncthreads();
-            tok_lookup(a, L, tw, wend, tile_base);   // the tile's words, round-robin over lanes
-            __syncthreads();
-            if (valid) {
-                const uint32_t w0 = L.ttoff[lane], tn = L.ttoff[lane + 1] - w0;
-                uint8_t fl = 0;
-                if (L.bytes[my_b - a0] == '$') fl |= TF_DOLLAR;
-                if (L.tirr[lane] || tn > FAST_MAX_DEPTH) fl |= TF_SLOW;
-                a.tflags[t] = fl;
-                a.toff[t] = (uint32_t)(tile_base + w0);
-                slow = (fl & TF_SLOW) != 0;
-            }
-            tok_append_slow(a, slow, t);
-            __syncthreads();
         } else {
-            const uint64_t o = tile_base + tincl - nw;
-            if (valid) {
-                a.toff[t] = (uint32_t)o;
-                tok_fill_topic_global(a, t, o, slow);
-            }
-            tok_append_slow(a, slow, t);
+            send_to_slow<false>(a, valid && !(o.fl & TF_SLOW), t);
         }
+        __syncthreads();
+        ++round;
+        tile = round < a.static_rounds
+                   ? blockIdx.x + round * gridDim.x
+                   : a.static_rounds * gridDim.x + __builtin_amdgcn_readfirstlane(ticket) * TICKET_GROUPS +
+                         blockIdx.x % TICKET_GROUPS;
+    }
+    if (lane == 0) {
+        atomicAdd(&a.stats[ST_VISITS], acc[0]); atomicAdd(&a.stats[ST_HASH], acc[1]);
+        atomicAdd(&a.stats[ST_WORDS], acc[2]); atomicAdd(&a.stats[ST_MATCHES], acc[3]);
+        atomicAdd(&a.stats[ST_PROBES], acc[4] & ((1ull << 40) - 1));
+        atomicAdd(&a.stats[ST_ITERS], acc[4] >> 40);
     }
 }
 
@@ -2785,20 +2885,52 @@ static uint32_t resident_blocks(K kernel, int block) {
     return (uint32_t)(cus * per);
 }
 
-hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
+// tokeniser passes 1 and 2: words per tile, their scan (f: the fill's arguments)
+static hipError_t launch_tok_count_scan(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s,
+                                        TokArgs& f) {
     static const uint32_t cap_count = resident_blocks(tm_tok_count, 64);
-    static const uint32_t cap_fill = resident_blocks(tm_tok_fill, 64);
     const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
     hipLaunchKernelGGL(tm_tok_count, dim3(ntiles ? min(ntiles, cap_count) : 1u), dim3(64), 0, s, a);   // also clears d_nslow + zero[]
+    f = a;
     if (!a.n) return hipGetLastError();
     scan.count = a.wcount;
     scan.row_off = a.wcount;   // in place: tile counts -> block-local tile offsets
     scan.n = ntiles;
     const hipError_t e = launch_scan(scan, s, d_nwords);
-    if (e != hipSuccess) return e;
-    TokArgs f = a;
     f.bsums = scan.block_sums;
+    return e;
+}
+
+hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s) {
+    static const uint32_t cap_fill = resident_blocks(tm_tok_fill, 64);
+    TokArgs f;
+    const hipError_t e = launch_tok_count_scan(a, scan, d_nwords, s, f);
+    if (e != hipSuccess || !a.n) return e != hipSuccess ? e : hipGetLastError();
+    const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
     hipLaunchKernelGGL(tm_tok_fill, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_match_fresh(const MatchArgs& a, const TokArgs& t, ScanArgs tscan, uint32_t* d_nwords, hipStream_t s,
+                              hipEvent_t ev_a, hipEvent_t ev_b) {
+    TokArgs f;
+    hipError_t e = launch_tok_count_scan(t, tscan, d_nwords, s, f);
+    if (e != hipSuccess) return e;
+    if (ev_a && (e = hipEventRecord(ev_a, s)) != hipSuccess) return e;
+    const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
+    const bool big = (uint64_t)a.nslots * sizeof(Slot) > 0xFFFFFFFFull;
+    if (ntiles) {
+        if (a.qcap <= 384) {
+            if (big) hipLaunchKernelGGL((tm_match_fresh<true, 384>), dim3(a.grid), dim3(64), 0, s, a, f);
+            else hipLaunchKernelGGL((tm_match_fresh<false, 384>), dim3(a.grid), dim3(64), 0, s, a, f);
+        } else {
+            if (big) hipLaunchKernelGGL((tm_match_fresh<true, 512>), dim3(a.grid), dim3(64), 0, s, a, f);
+            else hipLaunchKernelGGL((tm_match_fresh<false, 512>), dim3(a.grid), dim3(64), 0, s, a, f);
+        }
+    }
+    if (ev_b && (e = hipEventRecord(ev_b, s)) != hipSuccess) return e;
+    if (big) hipLaunchKernelGGL((tm_match_slow<false, true>), dim3(a.s_waves), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((tm_match_slow<false, false>), dim3(a.s_waves), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -187,6 +187,33 @@ def test_walk_rows_are_the_result_without_a_csr_pass(rowcap):
     b.free()
 
 
+def test_fused_fresh_walk_parity():
+    """TM_FRESH_FUSED=1: each tile tokenised in the walk's prologue
+    (tm_match_fresh) -- opt-in, measured slower than the separate fill, kept
+    for A/B.  C1 in full with the walk counters, plus deep / irregular /
+    empty topics (the HBM fallback and the generic path), equal the oracle."""
+    os.environ["TM_FRESH_FUSED"] = "1"
+    try:
+        eng = Engine(device=0)
+    finally:
+        del os.environ["TM_FRESH_FUSED"]
+    F = gen.gen_filters(gen.C1).tolist() + [b"", b"+/+", b"a/#", b"+x/#"]
+    Ts = gen.gen_topics(gen.C1, gen.Strings.from_list(F), 1001, gen.C1_TOPICS)
+    T = Ts.tolist() + [b"", b"", b"/", b"+x/y", b"a/" + b"/".join([b"q"] * 14), b"a" * 3000 + b"/b", b"a/b"]
+    for f in F:
+        eng.insert(f)
+    exp, st = oracle_rows(F, T)
+    b = eng.prepare(T)
+    b.launch().wait()
+    bst = b.stats()
+    offs, ids = b.result()
+    cache = {}
+    got = [[cache.setdefault(int(i), eng.filter_bytes(int(i))) for i in r] for r in rows_of(offs, ids)]
+    assert_same(T, got, exp)
+    assert bst["matches"] == st["matches"] and bst["slow_topics"] >= 3
+    b.free()
+
+
 def test_c2_parity_sample():
     F = gen.gen_filters(gen.C2).tolist()
     T = gen.gen_topics(gen.C2, gen.Strings.from_list(F), 2002, 200_000).tolist()
