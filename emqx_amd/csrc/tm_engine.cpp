@@ -658,7 +658,16 @@ struct AsyncSlot {
     uint32_t* d_flag = nullptr;
     uint32_t seq = 0;
     int rc = TM_OK;                      // launch failure (delivered to every call)
-    bool claimed = false;                // a completer is delivering it
+    bool claimed = false;                // a completer waits for it / it is being delivered
+    // Delivery in chunks: once waited and checked (ready), the batch's calls
+    // are delivered DELIVER_CHUNK at a time by whichever completers are idle
+    // (the calls are independent), so a batch's last caller does not wait for
+    // one thread to run every callback before it.  Under the replica's amu.
+    static constexpr uint32_t DELIVER_CHUNK = 512;
+    bool ready = false;
+    uint32_t nchunks = 0, next_chunk = 0, chunks_done = 0;
+    const uint32_t* d_count = nullptr;   // (ready) the per-call counts and row starts in h_out
+    const unsigned long long* d_src = nullptr;
 };
 
 // One device copy of the trie (a replica): the HBM tables, the stream the
@@ -4481,60 +4490,105 @@ struct tm_engine {
         return TM_OK;
     }
 
-    // Each completer claims the oldest in-flight slot nobody delivers yet,
-    // waits for it and runs its callbacks; several completers deliver
-    // consecutive batches concurrently.
+    // Completers: the oldest in-flight slot nobody waits for is claimed by
+    // one completer, which waits for it and checks its control words; then
+    // every idle completer takes chunks of its calls to deliver (the last
+    // chunk's completer recycles the slot).  A failed or recovered batch is
+    // delivered whole by the completer that waited for it.
     void completer_loop(Replica& R) {
         (void)hipSetDevice(R.device);
         std::unique_lock<std::mutex> lk(R.amu);
         for (;;) {
             AsyncSlot* sl = nullptr;
+            bool head = false;
             R.a_done.wait(lk, [&] {
                 for (AsyncSlot* x : R.a_inflight)
-                    if (!x->claimed) {
+                    if (x->ready && x->next_chunk < x->nchunks) {
                         sl = x;
                         return true;
                     }
-                return R.a_launcher_done;
+                for (AsyncSlot* x : R.a_inflight)
+                    if (!x->claimed) {
+                        sl = x;
+                        head = true;
+                        return true;
+                    }
+                return R.a_launcher_done && R.a_inflight.empty();
             });
             if (!sl) break;
-            sl->claimed = true;
+            if (head) {
+                sl->claimed = true;
+                lk.unlock();
+                bool whole = true, recovered = false;
+                double us_wait = 0;
+                try {
+                    whole = slot_wait(sl, us_wait, recovered);
+                } catch (...) {
+                }
+                lk.lock();
+                R.a_us_wait += us_wait;
+                R.a_recoveries += recovered ? 1 : 0;
+                if (whole) {
+                    slot_finish(R, sl);
+                } else {
+                    sl->nchunks = std::max<uint32_t>(
+                        1, (uint32_t)((sl->calls.size() + AsyncSlot::DELIVER_CHUNK - 1) / AsyncSlot::DELIVER_CHUNK));
+                    sl->next_chunk = sl->chunks_done = 0;
+                    sl->ready = true;
+                    R.a_done.notify_all();
+                }
+                continue;
+            }
+            const uint32_t c = sl->next_chunk++;
             lk.unlock();
-            bool recovered = false;
-            double us_wait = 0, us_deliver = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            const uint32_t n = (uint32_t)sl->calls.size();
+            const uint32_t lo = std::min(n, c * AsyncSlot::DELIVER_CHUNK);
+            const uint32_t hi = std::min(n, lo + AsyncSlot::DELIVER_CHUNK);
             syncwake::in_batch = true;
-            try {
-                recovered = slot_deliver(sl, us_wait, us_deliver);
-            } catch (...) {
+            for (uint32_t i = lo; i < hi; ++i) {
+                const uint32_t k = sl->d_count[i];
+                sl->calls[i].cb(sl->calls[i].ctx, TM_OK, k ? sl->h_rows + sl->d_src[i] : sl->h_rows, k);
             }
             syncwake::in_batch = false;
             syncwake::flush();
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             lk.lock();
-            R.a_inflight.erase(std::find(R.a_inflight.begin(), R.a_inflight.end(), sl));
-            R.a_us_wait += us_wait;
-            R.a_us_deliver += us_deliver;
-            ++R.a_batches;
-            R.a_recoveries += recovered ? 1 : 0;
-            R.a_requests += sl->calls.size();
-            sl->calls.clear();
-            sl->claimed = false;
-            R.a_free.push_back(sl);
-            R.a_work.notify_all();
-            R.a_done.notify_all();
+            R.a_us_deliver += us;
+            if (++sl->chunks_done == sl->nchunks) slot_finish(R, sl);
         }
     }
 
-    // Returns true when the batch had to be re-run through the CSR path.
-    bool slot_deliver(AsyncSlot* sl, double& us_wait, double& us_deliver) {
+    // amu held: the slot's calls are all delivered -- back to the free list
+    void slot_finish(Replica& R, AsyncSlot* sl) {
+        R.a_inflight.erase(std::find(R.a_inflight.begin(), R.a_inflight.end(), sl));
+        ++R.a_batches;
+        R.a_requests += sl->calls.size();
+        sl->calls.clear();
+        sl->claimed = sl->ready = false;
+        sl->nchunks = sl->next_chunk = sl->chunks_done = 0;
+        R.a_free.push_back(sl);
+        R.a_work.notify_all();
+        R.a_done.notify_all();
+    }
+
+    // Waits for a launched slot and checks its control words.  false: its
+    // rows are ready for chunked delivery (d_count / d_src set); true: it was
+    // delivered whole here (a launch failure, an error, or a capacity miss
+    // re-run through the CSR path: *recovered).
+    bool slot_wait(AsyncSlot* sl, double& us_wait, bool& recovered) {
         tm_batch* b = &sl->b;
         const uint32_t n = (uint32_t)sl->calls.size();
         auto fail_all = [&](int rc) {
+            syncwake::in_batch = true;
             for (const AsyncCall& c : sl->calls) c.cb(c.ctx, rc, nullptr, 0);
+            syncwake::in_batch = false;
+            syncwake::flush();
         };
         if (sl->rc) {
             (void)hipStreamSynchronize(b->own);   // whatever was enqueued before the failure
             fail_all(sl->rc);
-            return false;
+            return true;
         }
         const auto tw = std::chrono::steady_clock::now();
         if (sl->h_flag && b->rep->a_spin_us) {   // poll the pinned flag first (no interrupt wake-up)
@@ -4551,27 +4605,25 @@ struct tm_engine {
         }
         if (hipEventSynchronize(sl->ev_done) != hipSuccess) {
             fail_all(TM_EIO);
-            return false;
+            return true;
         }
-        const auto td = std::chrono::steady_clock::now();
-        us_wait = std::chrono::duration<double, std::micro>(td - tw).count();
+        us_wait = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
         const size_t hdr_bytes = tm_batch::HDR_FIXED + (size_t)n * 8;
         const uint32_t* ctrl = reinterpret_cast<const uint32_t*>(sl->h_out);
         const unsigned long long* stats = reinterpret_cast<const unsigned long long*>(sl->h_out + CTRL_WORDS * 4);
-        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(sl->h_out + tm_batch::HDR_FIXED);
-        const uint32_t* count = reinterpret_cast<const uint32_t*>(sl->h_out + hdr_bytes);
         uint32_t err = 0;
         uint64_t need = 0, staged = 0;
         int rc = check_ctrl(ctrl, stats, &err, &need, &staged);
         if (rc) {
             fail_all(rc);
-            return false;
+            return true;
         }
         if (b->one_region) need = staged;
         if (!err && need > sl->c_rows / 4) err = ERR_STAGING;   // (cannot happen: rows hold the staging area)
         if (err) {
             // capacity miss (staging, generic-path scratch): the CSR path grows
             // and re-runs, then the rows come from the CSR
+            recovered = true;
             tm_result r{};
             {
                 std::lock_guard<std::recursive_mutex> g(mu);
@@ -4584,16 +4636,16 @@ struct tm_engine {
                 fail_all(rc);
                 return true;
             }
+            syncwake::in_batch = true;
             for (uint32_t i = 0; i < n; ++i)
                 sl->calls[i].cb(sl->calls[i].ctx, TM_OK, r.filter_ids + r.row_offsets[i],
                                 r.row_offsets[i + 1] - r.row_offsets[i]);
+            syncwake::in_batch = false;
+            syncwake::flush();
             return true;
         }
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t c = count[i];
-            sl->calls[i].cb(sl->calls[i].ctx, TM_OK, c ? sl->h_rows + src[i] : sl->h_rows, c);
-        }
-        us_deliver = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - td).count();
+        sl->d_src = reinterpret_cast<const unsigned long long*>(sl->h_out + tm_batch::HDR_FIXED);
+        sl->d_count = reinterpret_cast<const uint32_t*>(sl->h_out + hdr_bytes);
         return false;
     }
 

@@ -62,10 +62,12 @@ struct Call {
 // A submitter that found its window full sleeps until it has drained to
 // `resume` calls in flight (a scheduler wakes for a run of replies, not one
 // futex round trip per reply).
-struct Submitter {
+// (a cache line each: completers touch the submitters of the calls they deliver)
+struct alignas(64) Submitter {
     std::atomic<int> outstanding{0};
     std::atomic<int> sleeping{0};
     std::atomic<int> resume{0};
+    std::atomic<int> active{0};   // its callbacks running: tml_run returns only once none is
 };
 
 struct Shared {
@@ -73,7 +75,6 @@ struct Shared {
     uint64_t* hashes;
     float* lat_us;
     std::atomic<uint64_t> errors{0};
-    std::atomic<int> active{0};   // callbacks running: tml_run returns only once none is
 };
 Shared* g_shared = nullptr;
 
@@ -82,7 +83,8 @@ void futex_wake(std::atomic<int>* a) { syscall(SYS_futex, reinterpret_cast<int*>
 void on_done(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
     Call* c = static_cast<Call*>(ctx);
     Shared* s = g_shared;
-    s->active.fetch_add(1, std::memory_order_acq_rel);
+    Submitter* w = c->who;
+    w->active.fetch_add(1, std::memory_order_acq_rel);
     const double us = std::chrono::duration<double, std::micro>(clk::now() - c->t0).count();
     s->lat_us[c->topic] = (float)us;
     if (rc) {
@@ -92,13 +94,12 @@ void on_done(void* ctx, int rc, const uint32_t* ids, uint32_t n) {
         s->counts[c->topic] = n;
         if (s->hashes) s->hashes[c->topic] = row_hash(ids, n);
     }
-    Submitter* w = c->who;
     const int left = w->outstanding.fetch_sub(1, std::memory_order_acq_rel) - 1;
     if (left <= w->resume && w->sleeping.load(std::memory_order_acquire)) {
         w->sleeping.store(0, std::memory_order_release);
         futex_wake(&w->sleeping);
     }
-    s->active.fetch_sub(1, std::memory_order_acq_rel);   // last touch of shared state
+    w->active.fetch_sub(1, std::memory_order_acq_rel);   // last touch of shared state
 }
 
 }  // namespace
@@ -185,7 +186,8 @@ __attribute__((visibility("default"))) int tml_run(tm_engine* e, const uint8_t* 
         });
     }
     for (auto& t : th) t.join();
-    while (sh.active.load(std::memory_order_acquire)) std::this_thread::yield();
+    for (Submitter& w : subs)
+        while (w.active.load(std::memory_order_acquire)) std::this_thread::yield();
     out->seconds = std::chrono::duration<double>(clk::now() - t0).count();
     out->calls = n;
     out->errors = sh.errors.load();

@@ -28,8 +28,8 @@ def main():
     offs, ids = eng.match_batch(T)
     exp_h = LD.row_hashes(offs, ids)
     LD.run(eng, T.slice(0, 20000), LD.ASYNC, 4, 64, hashes=False)
-    shapes = [("sync", LD.SYNC, 16, 1), ("sync", LD.SYNC, 64, 1), ("async", LD.ASYNC, 1, 4096),
-              ("async", LD.ASYNC, 4, 1024), ("async", LD.ASYNC, 16, 256), ("async", LD.ASYNC, 8, 2048)]
+    shapes = [("sync", LD.SYNC, 16, 1), ("sync", LD.SYNC, 64, 1), ("async", LD.ASYNC, 16, 32),
+              ("async", LD.ASYNC, 16, 64), ("async", LD.ASYNC, 16, 128), ("async", LD.ASYNC, 16, 256)]
     for name, mode, th, win in shapes:
         cnt = n if mode == LD.ASYNC else min(n, 300_000)
         sub = T if cnt == n else T.slice(0, cnt)
