@@ -369,11 +369,16 @@ def run_c4_group(args):
     csr_ms = b.stats()["ms_unpartition"]
     result_ms = 1e3 * (time.perf_counter() - tr)
     # a fresh batch: slices tokenised on their devices + the plan + one step
-    fresh = []
+    fresh, fresh_phases = [], []
     for _ in range(3):
         tf = time.perf_counter()
-        b.reprepare(topics).run()
-        fresh.append(1e3 * (time.perf_counter() - tf))
+        b.reprepare(topics)
+        tp = time.perf_counter()
+        b.run()
+        te = time.perf_counter()
+        fresh.append(1e3 * (te - tf))
+        s_ = b.stats()
+        fresh_phases.append((s_["ms_stage"], s_["ms_plan"], 1e3 * (tp - tf), 1e3 * (te - tp)))
     # self-check against one engine on device 0 (fresh batch's rows = the timed batch's: same publishes)
     ref = Engine(device=0, frozen_dict=True)
     ref.dict_load(vocab)
@@ -420,6 +425,10 @@ def run_c4_group(args):
                               "publishes_per_s_with_csr": n / (1e-3 * (1e3 * elapsed / args.steps + csr_ms))},
         "fresh_publishes_per_s": n / (1e-3 * float(np.median(fresh))),
         "fresh_ms": float(np.median(fresh)),
+        # a fresh batch's phases: bytes into pinned memory, the plan (uploads,
+        # device tokenisers, part counts), the whole prepare call, the step
+        "fresh_phase_ms": dict(zip(("stage", "plan", "prepare", "step"),
+                                   np.median(np.array(fresh_phases), 0).tolist())),
         "part_topics": st["part_topics"],
         "links": [[grp.link(i, j) for j in range(G)] for i in range(G)],
         "devices": devs,

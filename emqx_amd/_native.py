@@ -110,7 +110,7 @@ class AsyncStats(C.Structure):
 class ShardedStats(C.Structure):
     _fields_ = [("match", BatchStats), ("ms_partition", C.c_float), ("ms_exchange", C.c_float),
                 ("ms_step", C.c_float), ("ms_unpartition", C.c_float), ("host_waits", C.c_uint32),
-                ("part_topics", C.c_uint32 * 64)]
+                ("part_topics", C.c_uint32 * 64), ("ms_stage", C.c_float), ("ms_plan", C.c_float)]
 
 
 # void (*tm_match_cb)(void* ctx, int rc, const uint32_t* ids, uint32_t n)

@@ -44,6 +44,7 @@
 // (src/emqx_trie.erl:53-74) that every node matches in full
 // (src/emqx_router.erl:127-141); sharding it is new.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -180,8 +181,12 @@ struct Slice {
 struct tm_sharded_batch {
     uint32_t n = 0;
     uint64_t dict_words = ~0ull;          // dictionary size the plan was made with
-    std::vector<uint8_t> bytes;           // the publishes (re-planned if the dictionary grew)
-    std::vector<uint64_t> offs;
+    // the publishes, rebased (re-planned if the dictionary grew), in pinned
+    // memory: the tokenisers' uploads run at the DMA's rate, not through the
+    // runtime's staging of pageable memory
+    uint8_t* bytes = nullptr;
+    uint64_t* offs = nullptr;
+    size_t c_bytes = 0, c_offs = 0;
     std::vector<Slice> src;               // G slices (G > 1)
     std::vector<tm_batch*> part;          // shard j's part batch (its engine)
     std::vector<PartBuffers> pb;
@@ -203,6 +208,7 @@ struct tm_sharded_batch {
     size_t ch_row = 0, ch_ids = 0;
     tm_batch_stats st{};
     float ms_partition = 0, ms_exchange = 0, ms_step = 0, ms_unpartition = 0;
+    float ms_stage = 0, ms_plan = 0;      // the last prepare: bytes into pinned memory; the plan (uploads, tokenisers)
     uint32_t host_waits = 0;
 
     void release() {
@@ -218,6 +224,11 @@ struct tm_sharded_batch {
         for (uint32_t* h : {h_row, h_ids, h_close})
             if (h) (void)hipHostFree(h);
         h_row = h_ids = h_close = nullptr;
+        if (bytes) (void)hipHostFree(bytes);
+        if (offs) (void)hipHostFree(offs);
+        bytes = nullptr;
+        offs = nullptr;
+        c_bytes = c_offs = 0;
     }
 };
 
@@ -299,8 +310,7 @@ struct tm_sharded {
     int plan(tm_sharded_batch* b) {
         int rc;
         const uint32_t n = b->n;
-        static const uint8_t zero = 0;
-        const uint8_t* bytes = b->bytes.empty() ? &zero : b->bytes.data();
+        const uint8_t* bytes = b->bytes;
         b->dict_words = dict_words();
         b->done = b->ordered = false;
         if (b->part.size() != G) {
@@ -313,7 +323,7 @@ struct tm_sharded {
             const uint64_t cap = b->offs[n] + n + 1;
             if ((rc = part_batch_buffers(sh[0], &b->part[0], n, cap, &b->pb[0]))) return rc;
             uint64_t nw = 0;
-            if ((rc = tm_tokenize_device(sh[0], bytes, b->offs.data(), n, b->pb[0].words, b->pb[0].words_cap,
+            if ((rc = tm_tokenize_device(sh[0], bytes, b->offs, n, b->pb[0].words, b->pb[0].words_cap,
                                          b->pb[0].toff, b->pb[0].tflags, &nw)))
                 return rc;
             b->pn[0] = n;
@@ -343,7 +353,7 @@ struct tm_sharded {
                 return;
             }
             uint64_t nw = 0;
-            if ((r = tm_tokenize_device(sh[i], bytes, b->offs.data() + S.lo, S.n, S.words.p, S.words.cap, S.toff.p,
+            if ((r = tm_tokenize_device(sh[i], bytes, b->offs + S.lo, S.n, S.words.p, S.words.cap, S.toff.p,
                                         S.tflags.p, &nw))) {
                 rcs[i] = r;
                 return;
@@ -794,8 +804,7 @@ int tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t
 int tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                        tm_sharded_batch** out) {
     if (!s || !offsets || !out || (!topics && n)) return TM_EINVAL;
-    for (uint32_t i = 0; i < n; ++i)
-        if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > TM_MAX_TOPIC_LEN) return TM_EINVAL;
+    if (offsets[n] < offsets[0]) return TM_EINVAL;   // (each topic is checked while the offsets are staged)
     std::lock_guard<std::mutex> lk(s->mu);
     const bool fresh = *out == nullptr;
     tm_sharded_batch* b = fresh ? new (std::nothrow) tm_sharded_batch() : *out;
@@ -804,11 +813,41 @@ int tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* off
     try {
         b->n = n;
         b->done = b->ordered = false;
-        const uint64_t base = offsets[0];
-        b->offs.assign(offsets, offsets + (size_t)n + 1);
-        for (auto& o : b->offs) o -= base;
-        b->bytes.assign(topics + base, topics + base + b->offs[n]);
+        const uint64_t base = offsets[0], nbytes = offsets[n] - base;
+        const double t0 = now_ms();
+        if ((rc = host_pinned(b->offs, b->c_offs, (size_t)n + 1)) ||
+            (rc = host_pinned(b->bytes, b->c_bytes, nbytes + 16)))   // (+16: the tokenisers' 16-B windows)
+            throw std::bad_alloc();
+        // copied by several threads (one would take ~30 ms for a 10M-publish
+        // batch), which check every topic on the way: offsets that do not
+        // decrease, names of at most ?MAX_TOPIC_LEN bytes (src/emqx_topic.erl:45)
+        const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, (nbytes + n * 8) >> 22));
+        std::vector<std::thread> th;
+        std::atomic<bool> bad{false};
+        for (unsigned k = 0; k < T; ++k)
+            th.emplace_back([&, k] {
+                const size_t o0 = (size_t)((uint64_t)(n + 1) * k / T), o1 = (size_t)((uint64_t)(n + 1) * (k + 1) / T);
+                bool ok = true;
+                for (size_t i = o0; i < o1; ++i) {
+                    b->offs[i] = offsets[i] - base;
+                    if (i < n) ok &= offsets[i + 1] >= offsets[i] && offsets[i + 1] - offsets[i] <= TM_MAX_TOPIC_LEN;
+                }
+                if (!ok) bad.store(true, std::memory_order_relaxed);
+                const size_t c0 = (size_t)(nbytes * k / T), c1 = (size_t)(nbytes * (k + 1) / T);
+                if (c1 > c0) memcpy(b->bytes + c0, topics + base + c0, c1 - c0);
+            });
+        for (auto& t : th) t.join();
+        if (bad.load()) {
+            b->n = 0;                 // (a re-prepared batch keeps nothing of the refused one:
+            b->dict_words = ~0ull;    //  its next step re-plans)
+            rc = TM_EINVAL;
+            if (fresh) tm_sharded_batch_free(s, b);
+            return rc;
+        }
+        b->ms_stage = (float)(now_ms() - t0);
+        const double t1 = now_ms();
         rc = s->plan(b);
+        b->ms_plan = (float)(now_ms() - t1);
     } catch (...) {
         rc = TM_ENOMEM;
     }
@@ -885,6 +924,8 @@ int tm_sharded_batch_stats(tm_sharded* s, tm_sharded_batch* b, tm_sharded_stats*
     out->ms_step = b->ms_step;
     out->ms_unpartition = b->ms_unpartition;
     out->host_waits = b->host_waits;
+    out->ms_stage = b->ms_stage;
+    out->ms_plan = b->ms_plan;
     for (uint32_t g = 0; g < 64; ++g) out->part_topics[g] = g < s->G && g < b->pn.size() ? b->pn[g] : 0;
     return TM_OK;
 }

@@ -53,7 +53,7 @@ class Batch:
         self.n = len(s)
         buf = s.buf if s.buf.size else np.zeros(1, np.uint8)
         self._buf = np.ascontiguousarray(buf)
-        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        self._offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         h = C.c_void_p()
         flags = (N.TM_BATCH_DEDUP if dedup else 0) | (N.TM_BATCH_STREAM if stream else 0)
         if replica is None:
@@ -264,7 +264,7 @@ class GroupBatch:
         s = _pack(topics)
         self.n = len(s)
         self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        self._offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         h = C.c_void_p()
         N.check(grp.L.tm_group_prepare(grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n, C.byref(h)),
                 "tm_group_prepare")
@@ -358,7 +358,7 @@ class Group:
     def insert_many(self, filters) -> int:
         s = _pack(filters)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         done = C.c_uint64()
         N.check(self.L.tm_group_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
                 "tm_group_insert_many")
@@ -367,7 +367,7 @@ class Group:
     def route_apply(self, events) -> int:
         s = _pack([t for _, t, _ in events])
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         dests = np.ascontiguousarray(np.array([d for _, _, d in events] or [0], np.uint32))
         ops = np.ascontiguousarray(np.array([o for o, _, _ in events] or [0], np.uint8))
         done = C.c_uint64()
@@ -389,7 +389,7 @@ class Group:
     def match_batch(self, topics):
         s = _pack(topics)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         r = N.Result()
         N.check(self.L.tm_group_match_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
                 "tm_group_match_batch")
@@ -545,7 +545,7 @@ class Engine:
         """-> (row_offsets uint32[n+1], filter_ids uint32[total]); rows sorted by filter bytes."""
         s = _pack(topics)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         r = N.Result()
         N.check(self.L.tm_match_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
                 "tm_match_batch")
@@ -575,7 +575,7 @@ class Engine:
         n = len(events)
         s = _pack([t for _, t, _ in events])
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         dests = np.ascontiguousarray(np.array([d for _, _, d in events] or [0], np.uint32))
         ops = np.ascontiguousarray(np.array([o for o, _, _ in events] or [0], np.uint8))
         done = C.c_uint64()
@@ -603,7 +603,7 @@ class Engine:
         """-> (row_offsets, filter_ids, dests): aggre(match_routes(T)) per topic."""
         s = _pack(topics)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         r = N.Routes()
         N.check(self.L.tm_match_routes_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
                 "tm_match_routes_batch")
@@ -618,9 +618,9 @@ class Engine:
         if not n or not r:
             return np.zeros((n, r), bool)
         nb = np.ascontiguousarray(sn.buf if sn.buf.size else np.zeros(1, np.uint8))
-        no = np.ascontiguousarray(sn.offs.astype(np.uint64))
+        no = np.ascontiguousarray(sn.offs, dtype=np.uint64)
         rb = np.ascontiguousarray(sr.buf if sr.buf.size else np.zeros(1, np.uint8))
-        ro = np.ascontiguousarray(sr.offs.astype(np.uint64))
+        ro = np.ascontiguousarray(sr.offs, dtype=np.uint64)
         wpr = (r + 31) // 32
         bits = np.zeros(n * wpr, np.uint32)
         N.check(self.L.tm_rules_match(self.h, nb.ctypes.data, no.ctypes.data, n, rb.ctypes.data, ro.ctypes.data, r,
@@ -634,7 +634,7 @@ class Engine:
         shard's filters and the replicated ones.  Returns how many were inserted."""
         s = _pack(filters)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         done = C.c_uint64()
         N.check(self.L.tm_trie_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), shard, nshards,
                                            C.byref(done)), "tm_trie_insert_many")
@@ -644,7 +644,7 @@ class Engine:
         """emqx_trie:delete/1 over a filter list (one C call)."""
         s = _pack(filters)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         done = C.c_uint64()
         N.check(self.L.tm_trie_delete_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
                 "tm_trie_delete_many")
@@ -655,9 +655,9 @@ class Engine:
         planned together (tm_trie_apply_many).  Returns (deleted, inserted)."""
         d, a = _pack(dels), _pack(adds)
         db = np.ascontiguousarray(d.buf if d.buf.size else np.zeros(1, np.uint8))
-        do = np.ascontiguousarray(d.offs.astype(np.uint64))
+        do = np.ascontiguousarray(d.offs, dtype=np.uint64)
         ab = np.ascontiguousarray(a.buf if a.buf.size else np.zeros(1, np.uint8))
-        ao = np.ascontiguousarray(a.offs.astype(np.uint64))
+        ao = np.ascontiguousarray(a.offs, dtype=np.uint64)
         nd, ni = C.c_uint64(), C.c_uint64()
         N.check(self.L.tm_trie_apply_many(self.h, db.ctypes.data, do.ctypes.data, len(d), ab.ctypes.data,
                                           ao.ctypes.data, len(a), C.byref(nd), C.byref(ni)), "tm_trie_apply_many")
@@ -666,7 +666,7 @@ class Engine:
     def dict_load(self, words):
         s = _pack(words)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         N.check(self.L.tm_dict_load(self.h, buf.ctypes.data, offs.ctypes.data, len(s)), "tm_dict_load")
 
     def filter_shard(self, f: bytes, nshards: int) -> int:
@@ -676,7 +676,7 @@ class Engine:
         s = _pack(topics)
         n = len(s)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         cap = int(n + np.count_nonzero(s.buf == ord("/"))) if n else 0
         words = np.zeros(max(cap, 1), np.uint32)
         toff = np.zeros(n + 1, np.uint32)
@@ -693,7 +693,7 @@ class Engine:
         s = _pack(topics)
         n = len(s)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         if words_cap is None:
             words_cap = int(n + np.count_nonzero(s.buf == ord("/"))) if n else 0
         dev = torch.device("cuda", self.device)
@@ -807,7 +807,7 @@ class ShardedBatch:
         s = _pack(topics)
         self.n = len(s)
         self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        self._offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         h = C.c_void_p()
         N.check(grp.L.tm_sharded_prepare(grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n, C.byref(h)),
                 "tm_sharded_prepare")
@@ -822,7 +822,7 @@ class ShardedBatch:
         s = _pack(topics)
         self.n = len(s)
         self._buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        self._offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        self._offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         N.check(self.grp.L.tm_sharded_prepare(self.grp.h, self._buf.ctypes.data, self._offs.ctypes.data, self.n,
                                               C.byref(self.h)), "tm_sharded_prepare")
         return self
@@ -838,7 +838,7 @@ class ShardedBatch:
         out = st.match.asdict()
         out.update(ms_partition=st.ms_partition, ms_exchange=st.ms_exchange, ms_step=st.ms_step,
                    ms_unpartition=st.ms_unpartition, host_waits=st.host_waits,
-                   part_topics=list(st.part_topics)[:len(self.grp)])
+                   part_topics=list(st.part_topics)[:len(self.grp)], ms_stage=st.ms_stage, ms_plan=st.ms_plan)
         return out
 
     def free(self):
@@ -892,13 +892,13 @@ class ShardedGroup:
     def dict_load(self, words):
         s = _pack(words)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         N.check(self.L.tm_sharded_dict_load(self.h, buf.ctypes.data, offs.ctypes.data, len(s)), "tm_sharded_dict_load")
 
     def insert_many(self, filters) -> int:
         s = _pack(filters)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         done = C.c_uint64()
         N.check(self.L.tm_sharded_insert_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
                 "tm_sharded_insert_many")
@@ -907,7 +907,7 @@ class ShardedGroup:
     def delete_many(self, filters) -> int:
         s = _pack(filters)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         done = C.c_uint64()
         N.check(self.L.tm_sharded_delete_many(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(done)),
                 "tm_sharded_delete_many")
@@ -919,7 +919,7 @@ class ShardedGroup:
     def match_batch(self, topics):
         s = _pack(topics)
         buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
-        offs = np.ascontiguousarray(s.offs.astype(np.uint64))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
         r = N.Result()
         N.check(self.L.tm_sharded_match_batch(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
                 "tm_sharded_match_batch")

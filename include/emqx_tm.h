@@ -618,6 +618,8 @@ typedef struct {
     float ms_unpartition;     /* host wall time: the publish-order CSR (on request) */
     uint32_t host_waits;      /* blocking host waits in the last step: 1, + 1 per capacity relaunch */
     uint32_t part_topics[64]; /* publishes each shard matched */
+    float ms_stage;           /* host wall time of the last prepare's copy of the publishes into pinned memory */
+    float ms_plan;            /* host wall time of the last prepare's plan (uploads, device tokenisers, counts) */
 } tm_sharded_stats;
 /* how shard i's memory reaches shard j's device */
 #define TM_LINK_SAME   0      /* same device: D2D copies */
@@ -643,9 +645,9 @@ TM_API int  tm_sharded_insert_many(tm_sharded* s, const uint8_t* filters, const 
  * owner, or all G for a replicated filter), as tm_sharded_insert_many counts. */
 TM_API int  tm_sharded_delete_many(tm_sharded* s, const uint8_t* filters, const uint64_t* offsets, uint32_t n,
                                    uint64_t* n_deleted);
-/* A publish batch: bytes copied, slice i tokenised on shard i's device and
- * its parts counted (the plan of the exchange).  A non-NULL *out is
- * re-prepared in place. */
+/* A publish batch: bytes copied (into pinned memory, by several threads),
+ * slice i tokenised on shard i's device and its parts counted (the plan of
+ * the exchange).  A non-NULL *out is re-prepared in place. */
 TM_API int  tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
                                tm_sharded_batch** out);
 /* One step (returns with every shard's rows in its HBM; one host wait). */
