@@ -17,8 +17,9 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
-TM_SOURCES = ["tm_engine.cpp", "tm_group.cpp", "tm_shard.cpp", "tm_kernels.hip"]
-TM_HEADERS = ["tm_internal.hpp", os.path.join("..", "..", "include", "emqx_tm.h")]
+TM_SOURCES = ["tm_engine.cpp", "tm_churn.cpp", "tm_upload.cpp", "tm_batch.cpp", "tm_async.cpp", "tm_pipeline.cpp",
+              "tm_fanout.cpp", "tm_group.cpp", "tm_shard.cpp", "tm_kernels.hip"]
+TM_HEADERS = ["tm_internal.hpp", "tm_engine_impl.hpp", os.path.join("..", "..", "include", "emqx_tm.h")]
 
 
 def _digest(deps, extra=""):

@@ -1,0 +1,759 @@
+// tm_churn.cpp -- trie mutations (emqx_trie insert/1, delete/1 and their batched
+// parallel pass: plan, node records, edge phase, summaries).  Semantics follow
+// src/emqx_trie.erl:81-116, 145-158, 190-204.
+#include "tm_engine_impl.hpp"
+
+int tm_engine::trie_insert_ids(const uint8_t* t, size_t len, const uint32_t* ids_p, uint32_t nids, uint32_t from,
+                    uint32_t k0, uint32_t sd) {
+    struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
+    // add_path/1 for every triple (:145-158), in one walk: existing edges
+    // are followed, the missing suffix is created
+    uint32_t p = from;
+    bool created = false;
+    Mut* const M = tl_mut;
+    for (size_t k = k0; k < ids.size(); ++k) {
+        const uint32_t w = ids[k];
+        // (a parallel batch: the nodes of depth < sd are shared by workers)
+        std::unique_lock<std::recursive_mutex> rl;
+        if (M && k < sd) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+        uint32_t c = NONE;
+        if (M && M->defer) {   // an edge made earlier in this batch is not in the hash yet
+            // (levels < sd: made by any worker, held in the stripe's shared map)
+            if (k < sd) {
+                const auto& sm = shared_made[p & 63];
+                const auto it = sm.find((uint64_t)p << 32 | w);
+                if (it != sm.end()) c = it->second;
+            } else {
+                c = M->made_get((uint64_t)p << 32 | w);
+            }
+        }
+        // The edge hash is frozen during phase 1 of a parallel insert and the
+        // plan's walk stopped at level k0 on a miss, so every deeper parent
+        // is a node of this batch: only the made maps can hold its edges.
+        if (c == NONE && !(M && M->defer) && !created) {
+            const uint32_t s = nd[p].live ? find_slot(p, w) : NONE;
+            if (s != NONE) c = slots[s].child & ID_MASK;
+        }
+        if (c == NONE) {
+            if (!created) {
+                // node ids are 30-bit (two flag bits ride in the slot's id words); a
+                // parallel batch checked its whole need up front
+                const size_t need = ids.size() - k;
+                if (!M && nd.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
+                    return TM_ENOMEM;
+                created = true;
+            }
+            if (!nd[p].live) {               // only the root can be absent here
+                nd[p].live = 1; nd[p].ec = 0;
+                if (M) ++M->live_nodes;
+                else ++live_nodes;
+            }
+            c = new_node(p, w);
+            ++nd[p].ec;
+            // p's slot changes with a '+' / '#' child or a new signature bit
+            // (ec is not in it): only then is it rewritten (and uploaded)
+            bool resum = true;
+            if (w == W_PLUS) nd[p].plus = c;
+            else if (w == W_HASH) nd[p].hash = c;
+            else {
+                const uint32_t s0 = nd[p].lsig(), x0 = n_lext[p];
+                nd[p].lsig_add(w);
+                n_lext[p] |= 1u << lext_pos(w);
+                resum = nd[p].lsig() != s0 || n_lext[p] != x0;
+            }
+            insert_edge(p, w, c);
+            if (M && M->defer && k < sd) shared_made[p & 63][(uint64_t)p << 32 | w] = c;   // (stripe lock held)
+            if (resum) write_summary(p);
+        }
+        p = c;
+    }
+    std::unique_lock<std::recursive_mutex> tl;
+    if (M && ids.size() < sd) tl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+    if (!created && nd[p].topic) return TM_OK;   // inserted already: idempotent
+    set_topic(p, t, len);   // write_trie_node(#trie_node{node_id = Topic, topic = Topic})
+    if (M) ++M->version;
+    else ++version;
+    return TM_OK;
+}
+
+int tm_engine::trie_delete(const uint8_t* t, size_t len) {
+    std::vector<uint32_t> ids;
+    if (!filter_words(t, len, false, ids)) return TM_OK;
+    const uint32_t n = walk(ids);
+    if (n == NONE) return TM_OK;
+    return trie_delete_at(n, ids.data(), (uint32_t)ids.size());
+}
+
+int tm_engine::trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids) {
+    struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
+    Mut* const M = tl_mut;
+    std::unique_lock<std::recursive_mutex> nl;
+    if (M && ids.size() < 2) nl = std::unique_lock<std::recursive_mutex>(shared_mu(n));
+    if (nd[n].ec != 0) {
+        if (nd[n].topic) {
+            clear_topic(n);
+            if (M) ++M->version;
+            else ++version;
+        }
+        return TM_OK;
+    }
+    clear_topic(n);
+    uint32_t child = n;
+    int rc = TM_OK;
+    bool child_dead = false;
+    for (size_t k = ids.size(); k-- > 0;) {
+        const uint32_t p = nd[child].parent;
+        const uint32_t w = ids[k];
+        delete_edge_of(child);
+        if (!child_dead) { kill_node(child); child_dead = true; }
+        // (a parallel batch: the nodes of depth < 2 are shared by workers)
+        std::unique_lock<std::recursive_mutex> rl;
+        if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+        bool sig_changed = true;
+        if (w == W_PLUS) nd[p].plus = NONE;
+        else if (w == W_HASH) nd[p].hash = NONE;
+        else {
+            const uint32_t s0 = nd[p].lsig();
+            nd[p].lsig_del(w);
+            sig_changed = nd[p].lsig() != s0;
+        }
+        if (!nd[p].live) { rc = TM_EABORT; break; }
+        if (nd[p].ec == 1 && !nd[p].topic) {
+            nd[p].ec = 0;
+            if (p == ROOT) { kill_node(p); break; }
+            kill_node(p);
+            child = p;
+            continue;
+        }
+        --nd[p].ec;
+        if (sig_changed) write_summary(p);   // (a '+' / '#' child, or a signature bit gone)
+        break;
+    }
+    if (M) ++M->version;
+    else ++version;
+    return rc;
+}
+
+void tm_engine::plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo, uint32_t hi, bool del, uint32_t part,
+                uint32_t pbase, bool append) {
+    // the part's vectors are worked on as locals and put back at the end:
+    // the per-part vector headers share cache lines, and a push_back per
+    // word on them from 8-16 threads was a false-sharing storm (plan of
+    // 5,000 filters: 0.45 us per filter on one thread, 3-5x that per
+    // thread on eight)
+    std::vector<uint32_t> W;
+    W.swap(plan_words[part]);
+    if (!append) W.clear();   // (append: a second range of the same part, tm_trie_apply_many)
+    std::vector<TWord> all;
+    all.swap(plan_tw[part]);
+    std::vector<TWord> ws;
+    std::vector<uint64_t> hs;
+    const bool root_live = nd[ROOT].live != 0;
+    const uint32_t nb = nbuckets();
+    static const bool ptrace = getenv("TM_PAR_TRACE") != nullptr;
+    std::chrono::steady_clock::duration d_split{}, d_dict{}, d_walk{};
+    using clk = std::chrono::steady_clock;
+    for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
+        const auto c0 = ptrace ? clk::now() : clk::time_point{};
+        const uint32_t g1 = std::min(hi, g0 + PLAN_G);
+        // words and their dictionary entries
+        const uint32_t wbase = (uint32_t)W.size();
+        hs.clear();
+        all.clear();
+        for (uint32_t i = g0; i < g1; ++i) {
+            PlanEnt& pe = plan[pbase + i];
+            split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
+            pe.woff = wbase + (uint32_t)all.size();
+            pe.nw = (uint32_t)ws.size();
+            pe.part = part;
+            for (const TWord& w : ws) {
+                all.push_back(w);
+                hs.push_back(w.n == 0 || is_plus(w) || is_hash(w) ? 0 : dict.prefetch(w.p, w.n));
+            }
+        }
+        const auto c1 = ptrace ? clk::now() : clk::time_point{};
+        for (size_t j = 0; j < all.size(); ++j) {
+            const TWord& w = all[j];
+            W.push_back(w.n == 0 ? W_EMPTY : is_plus(w) ? W_PLUS : is_hash(w) ? W_HASH : dict.find_h(w.p, w.n, hs[j]));
+        }
+        const auto c2 = ptrace ? clk::now() : clk::time_point{};
+        d_split += c1 - c0;
+        d_dict += c2 - c1;
+        // the existing paths, level by level over the group
+        uint32_t node[PLAN_G], k[PLAN_G];
+        bool run[PLAN_G], known[PLAN_G];
+        const uint32_t G = g1 - g0;
+        for (uint32_t q = 0; q < G; ++q) {
+            const PlanEnt& pe = plan[pbase + g0 + q];
+            node[q] = ROOT;
+            k[q] = 0;
+            known[q] = true;
+            for (uint32_t j = 0; j < pe.nw; ++j) known[q] &= W[pe.woff + j] != W_UNKNOWN;
+            run[q] = root_live;
+        }
+        for (bool any = root_live; any;) {
+            any = false;
+            for (uint32_t q = 0; q < G; ++q) {
+                const PlanEnt& pe = plan[pbase + g0 + q];
+                if (!run[q]) continue;
+                if (k[q] >= pe.nw || W[pe.woff + k[q]] == W_UNKNOWN) { run[q] = false; continue; }
+                __builtin_prefetch(&slots[(size_t)home_bucket(node[q], W[pe.woff + k[q]], nb) * BUCKET]);
+            }
+            for (uint32_t q = 0; q < G; ++q) {
+                if (!run[q]) continue;
+                const PlanEnt& pe = plan[pbase + g0 + q];
+                const uint32_t sl = find_slot(node[q], W[pe.woff + k[q]]);
+                if (sl == NONE) { run[q] = false; continue; }
+                node[q] = slots[sl].child & ID_MASK;
+                ++k[q];
+                any = true;
+            }
+        }
+        for (uint32_t q = 0; q < G; ++q) {
+            PlanEnt& pe = plan[pbase + g0 + q];
+            if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
+            else { pe.node = node[q]; pe.depth = k[q]; }
+        }
+        if (ptrace) d_walk += clk::now() - c2;
+    }
+    plan_words[part].swap(W);
+    plan_tw[part].swap(all);
+    if (ptrace) {
+        auto us = [](auto d) { return std::chrono::duration<double, std::micro>(d).count(); };
+        fprintf(stderr, "  [plan part %u: %u filters] split+hash %.0f us, dict %.0f us, walk %.0f us\n", part, hi - lo,
+                us(d_split), us(d_dict), us(d_walk));
+    }
+}
+
+void tm_engine::make_plan(const uint8_t* buf, const uint64_t* offs, uint32_t n, bool del) {
+    plan.resize(n);
+    const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 256));
+    if (plan_words.size() < nt) plan_words.resize(nt);
+    if (plan_tw.size() < nt) plan_tw.resize(nt);
+    if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
+    ensure_pool();   // the engine's workers (no thread start-up per batch)
+    pool.run([&](unsigned i) {
+        for (unsigned j = i; j < nt; j += pool.n) {
+            const uint32_t lo = (uint32_t)((uint64_t)n * j / nt), hi = (uint32_t)((uint64_t)n * (j + 1) / nt);
+            plan_range(buf, offs, lo, hi, del, j);
+        }
+    });
+}
+
+void tm_engine::make_plan_pair(const uint8_t* dbuf, const uint64_t* doffs, uint32_t ndel, const uint8_t* ibuf,
+                    const uint64_t* ioffs, uint32_t nins) {
+    plan.resize((size_t)ndel + nins);
+    const unsigned nt = std::max(1u, std::min<unsigned>(threads, (ndel + nins) / 256));
+    if (plan_words.size() < nt) plan_words.resize(nt);
+    if (plan_tw.size() < nt) plan_tw.resize(nt);
+    auto part = [&](unsigned j) {
+        plan_range(dbuf, doffs, (uint32_t)((uint64_t)ndel * j / nt), (uint32_t)((uint64_t)ndel * (j + 1) / nt), true, j);
+        plan_range(ibuf, ioffs, (uint32_t)((uint64_t)nins * j / nt), (uint32_t)((uint64_t)nins * (j + 1) / nt), false, j,
+                   ndel, true);
+    };
+    if (nt == 1) { part(0); return; }
+    ensure_pool();
+    pool.run([&](unsigned i) {
+        for (unsigned j = i; j < nt; j += pool.n) part(j);
+    });
+}
+
+uint32_t tm_engine::replan_dead_inserts(uint32_t n) {
+    std::vector<uint32_t>& redo = replan_buf;
+    redo.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+        if (i + 16 < n && plan[i + 16].node != ROOT) __builtin_prefetch(&nd[plan[i + 16].node]);
+        const PlanEnt& pe = plan[i];
+        if (pe.node != ROOT && !nd[pe.node].live) redo.push_back(i);
+    }
+    const bool root_live = nd[ROOT].live != 0;
+    const uint32_t nb = nbuckets();
+    for (size_t g0 = 0; g0 < redo.size(); g0 += PLAN_G) {
+        const uint32_t G = (uint32_t)std::min<size_t>(PLAN_G, redo.size() - g0);
+        bool run[PLAN_G];
+        for (uint32_t q = 0; q < G; ++q) {
+            PlanEnt& pe = plan[redo[g0 + q]];
+            pe.node = ROOT;
+            pe.depth = 0;
+            run[q] = root_live;
+        }
+        for (bool any = root_live; any;) {
+            any = false;
+            for (uint32_t q = 0; q < G; ++q) {
+                const PlanEnt& pe = plan[redo[g0 + q]];
+                const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+                if (run[q] && (pe.depth >= pe.nw || w[pe.depth] == W_UNKNOWN)) run[q] = false;
+                if (run[q]) __builtin_prefetch(&slots[(size_t)home_bucket(pe.node, w[pe.depth], nb) * BUCKET]);
+            }
+            for (uint32_t q = 0; q < G; ++q) {
+                if (!run[q]) continue;
+                PlanEnt& pe = plan[redo[g0 + q]];
+                const uint32_t s = find_slot(pe.node, plan_words[pe.part][pe.woff + pe.depth]);
+                // (an edge whose child died in this apply waits for its
+                // delete in the shared edge phase: a miss)
+                if (s == NONE || !nd[slots[s].child & ID_MASK].live) { run[q] = false; continue; }
+                pe.node = slots[s].child & ID_MASK;
+                ++pe.depth;
+                any = true;
+            }
+        }
+    }
+    return (uint32_t)redo.size();
+}
+
+void tm_engine::prefetch_insert(uint32_t i, uint32_t n) {
+    if (i + PF_FAR < n) __builtin_prefetch(&nd[plan[i + PF_FAR].node]);
+    if (i + PF_NEAR < n) {
+        const PlanEnt& q = plan[i + PF_NEAR];
+        if (q.depth < q.nw) {
+            const uint32_t w = plan_words[q.part][q.woff + q.depth];
+            if (w != W_UNKNOWN) __builtin_prefetch(&slots[(size_t)home_bucket(q.node, w, nbuckets()) * BUCKET]);
+        }
+        const size_t nf = free_nodes.size();
+        if (nf > PF_NEAR) __builtin_prefetch(&nd[free_nodes[nf - 1 - PF_NEAR]]);
+    }
+}
+
+void tm_engine::prefetch_delete(uint32_t i, uint32_t n) {
+    if (i + PF_FAR < n && plan[i + PF_FAR].node != NONE) __builtin_prefetch(&nd[plan[i + PF_FAR].node]);
+    if (i + PF_NEAR < n && plan[i + PF_NEAR].node != NONE) {
+        const NodeRec& r = nd[plan[i + PF_NEAR].node];
+        __builtin_prefetch(&nd[r.parent]);
+        if (r.inslot != NONE) {
+            __builtin_prefetch(&slots[r.inslot]);
+            if ((r.inslot >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[r.inslot >> 6]);
+        }
+    }
+}
+
+int tm_engine::insert_planned(const uint8_t* buf, const uint64_t* offs, uint32_t i) {
+    PlanEnt& pe = plan[i];
+    uint32_t* ids = plan_words[pe.part].data() + pe.woff;
+    for (uint32_t k = pe.depth; k < pe.nw; ++k)
+        if (ids[k] == W_UNKNOWN) {   // new word (or interned by an earlier filter of the batch)
+            if (frozen) return TM_ENOENT;
+            const uint8_t* f = buf + offs[i];
+            static thread_local std::vector<TWord> ws;
+            split_words(f, offs[i + 1] - offs[i], ws);
+            for (uint32_t j = k; j < pe.nw; ++j)
+                if (ids[j] == W_UNKNOWN) ids[j] = dict.intern(ws[j].p, ws[j].n);
+            break;
+        }
+    // the planned prefix was walked with the root live; a root created since
+    // (empty trie at plan time) restarts at ROOT, level 0
+    return trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i], ids, pe.nw, pe.node, pe.depth);
+}
+
+void tm_engine::ensure_pool() {
+    if (!pool_started) {
+        cpu_set_t cpus;
+        pool.start(threads, device_node_cpus(device, threads, cpus) ? &cpus : nullptr);
+        pool_started = true;
+    }
+}
+
+void tm_engine::prefetch_edge_of(const std::vector<uint32_t>& v, size_t q) const {
+    if (q + 16 < v.size()) {
+        __builtin_prefetch(&nd[v[q + 16]]);
+        __builtin_prefetch(&n_lext[v[q + 16]]);
+    }
+    if (q + 8 < v.size()) {
+        const uint32_t s = nd[v[q + 8]].inslot;
+        if (s != NONE && s < slots.size()) __builtin_prefetch(&slots[s], 1);
+    }
+}
+
+void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
+    const unsigned T = std::max(1u, threads);
+    auto each = [&](auto&& fn) {
+        for (std::vector<Mut>* W : Ws)
+            for (Mut& m : *W) fn(m);
+    };
+    auto merge_edges = [&](std::vector<Mut>& X) {
+        for (Mut& m : X) {
+            live_edges += m.live_edges; used_slots += m.used_slots; max_disp = std::max(max_disp, m.max_disp);
+            dirty.insert(dirty.end(), m.dirty.begin(), m.dirty.end());
+            m.live_edges = m.used_slots = 0; m.max_disp = 0; m.dirty.clear();
+        }
+    };
+    auto ranges = [&](unsigned& T2, uint32_t& RS, uint32_t& R) {
+        const uint32_t nb = nbuckets();
+        T2 = std::min<unsigned>(T, nb / (2 * PAR_RANGE_MIN));
+        if (T2 < 2) { T2 = 0; return; }
+        RS = ((nb + 2 * T2 - 1) / (2 * T2) + 15) / 16 * 16;   // whole 16-bucket groups: dirty-mark words stay per range
+        R = (nb + RS - 1) / RS;
+    };
+    each([](Mut& m) { m.defer = false; });
+    const bool trace = getenv("TM_PAR_TRACE") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto e0 = now();
+    unsigned T2 = 0;
+    uint32_t RS = 0, R = 0;
+    // ---- deletes, bucketed by the slot recorded in phase 1 (nothing has moved since)
+    size_t ndel = 0;
+    each([&](Mut& m) { ndel += m.del.size(); });
+    ranges(T2, RS, R);
+    if (!ndel) {
+    } else if (!T2) {
+        each([&](Mut& m) {
+            for (const auto& d : m.del) delete_edge_of(d.first);
+        });
+    } else {
+        std::vector<std::vector<uint32_t>> per(2 * T2);
+        std::vector<uint32_t> tail;
+        each([&](Mut& m) {
+            for (const auto& d : m.del) {
+                const uint32_t r = d.second / BUCKET / RS;
+                if (R % 2 && r == R - 1) tail.push_back(d.first);   // (R odd: the last range wraps onto range 0)
+                else per[r].push_back(d.first);
+            }
+        });
+        std::vector<Mut>& X = edge_states(T2);
+        std::vector<std::vector<uint32_t>> late(T2);
+        for (uint32_t par = 0; par < 2; ++par)
+            pool.run([&](unsigned t) {
+                if (t >= T2) return;
+                const uint32_t r = 2 * t + par;
+                tl_mut = &X[t];
+                const std::vector<uint32_t>& v = per[r];
+                for (size_t q = 0; q < v.size(); ++q) {
+                    prefetch_edge_of(v, q);
+                    const uint32_t c = v[q];
+                    // an odd range's slot may have been pulled back into the even range before it
+                    if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
+                    delete_edge_of(c);
+                }
+                tl_mut = nullptr;
+            });
+        merge_edges(X);
+        for (auto& l : late) tail.insert(tail.end(), l.begin(), l.end());
+        for (uint32_t c : tail) delete_edge_of(c);   // serially, global counters
+    }
+    // ---- inserts: room first (the serial insert_edge's rehash rule, for the whole batch)
+    const auto e1 = now();
+    size_t nins = 0;
+    each([&](Mut& m) { nins += m.ins.size(); });
+    bool rehashed = false;
+    if ((used_slots + nins) * 4 > slots.size() * 3 || max_disp > 48) {
+        rehash(std::max<size_t>((size_t)((live_edges + nins) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
+        rehashed = true;
+    }
+    const auto e2 = now();
+    ranges(T2, RS, R);
+    if (!nins) {
+    } else if (!T2) {
+        each([&](Mut& m) {
+            for (const auto& e : m.ins) insert_edge(e[0], e[1], e[2]);
+        });
+    } else {
+        std::vector<std::vector<std::array<uint32_t, 3>>> per(2 * T2);
+        std::vector<std::array<uint32_t, 3>> tail;
+        const uint32_t nb = nbuckets();
+        each([&](Mut& m) {
+            for (const auto& e : m.ins) {
+                const uint32_t r = home_bucket(e[0], e[1], nb) / RS;
+                if (R % 2 && r == R - 1) tail.push_back(e);
+                else per[r].push_back(e);
+            }
+        });
+        std::vector<Mut>& X = edge_states(T2);
+        for (uint32_t par = 0; par < 2; ++par)
+            pool.run([&](unsigned t) {
+                if (t >= T2) return;
+                tl_mut = &X[t];
+                const auto& v = per[2 * t + par];
+                for (size_t q = 0; q < v.size(); ++q) {
+                    if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
+                        __builtin_prefetch(&slots[(size_t)home_bucket(v[q + 8][0], v[q + 8][1], nb) * BUCKET], 1);
+                        __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                    }
+                    insert_edge(v[q][0], v[q][1], v[q][2]);
+                }
+                tl_mut = nullptr;
+            });
+        merge_edges(X);
+        for (const auto& e : tail) insert_edge(e[0], e[1], e[2]);
+    }
+    if (max_disp > 48) rehash(std::max<size_t>((size_t)(live_edges / 0.55), slots.size() * 2));
+    const auto e3 = now();
+    // ---- summaries of the nodes whose record changed: by node (a node's
+    // records are rewritten by one worker; dirty marks set atomically)
+    const unsigned TS = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));
+    std::vector<std::vector<uint32_t>> per(TS);
+    each([&](Mut& m) {
+        for (uint32_t c : m.sum) per[mix_word(c) % TS].push_back(c);
+    });
+    std::vector<Mut>& X = edge_states(TS);
+    pool.run([&](unsigned t) {
+        if (t >= TS) return;
+        std::vector<uint32_t>& v = per[t];
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (size_t q = 0; q < v.size(); ++q) {
+            prefetch_edge_of(v, q);
+            const uint32_t c = v[q];
+            if (!nd[c].live || nd[c].inslot == NONE) continue;
+            write_summary_at(c, X[t].dirty);
+        }
+    });
+    merge_edges(X);
+    if (trace)
+        fprintf(stderr, "[par edges T2=%u nb=%u] del %.2f rehash %d %.2f ins %.2f sum %.2f ms\n", T2, nbuckets(),
+                ms(e0, e1), (int)rehashed, ms(e1, e2), ms(e2, e3), ms(e3, now()));
+}
+
+void tm_engine::write_summary_at(uint32_t c, std::vector<uint32_t>& dl) {
+    const uint32_t i = nd[c].inslot;
+    Slot& e = slots[i];
+    slot_set_lsig(e, nd[c].lsig());
+    e.child = c | (nd[c].topic ? B_TOPIC : 0u) | (nd[c].plus != NONE ? B_PLUS : 0u);
+    const uint32_t h = nd[c].hash;
+    e.hash = h != NONE ? h | (nd[h].topic ? B_HTERM : 0u) | B_HASH : n_lext[c];
+    if (full_dirty) return;
+    const uint64_t m = 1ull << (i & 63);
+    if (!(__atomic_fetch_or(&dirty_mark[i >> 6], m, __ATOMIC_RELAXED) & m)) dl.push_back(i);
+}
+
+std::vector<Mut> mut_w2;   // the insert states of tm_trie_apply_many (its deletes use mut_w)
+
+// tm_trie_insert_many / delete_many of n >= PAR_MIN planned filters (make_plan ran).
+// Returns 1 when the batch must run serially instead (nothing changed then).
+int tm_engine::mutate_parallel(bool del, const uint8_t* buf, const uint64_t* offs, uint32_t n, uint64_t* done_out,
+                    int* rc_out) {
+    ParRun R;
+    if (par_begin(del, buf, offs, n, mut_w, R)) return 1;
+    ParRun* runs[1] = {&R};
+    par_finish(runs, 1);
+    *done_out = R.done;
+    *rc_out = R.rc;
+    return 0;
+}
+
+int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uint32_t n, std::vector<Mut>& W, ParRun& R) {
+    const unsigned T = std::max(1u, threads);
+    if (T < 2 || (uint64_t)n * 4 > n_filters) return 1;   // bulk builds stay serial: churn on a big trie only
+    if (!del) {
+        // new words are interned first, serially (the dictionary is not thread-safe)
+        for (uint32_t i = 0; i < n; ++i) {
+            PlanEnt& pe = plan[i];
+            uint32_t* ids = plan_words[pe.part].data() + pe.woff;
+            bool unknown = false;
+            for (uint32_t k = pe.depth; k < pe.nw; ++k) unknown |= ids[k] == W_UNKNOWN;
+            if (!unknown) continue;
+            if (frozen) return 1;   // TM_ENOENT semantics of the serial pass (stop at the first)
+            static thread_local std::vector<TWord> ws;
+            split_words(buf + offs[i], offs[i + 1] - offs[i], ws);
+            for (uint32_t k = pe.depth; k < pe.nw; ++k)
+                if (ids[k] == W_UNKNOWN) ids[k] = dict.intern(ws[k].p, ws[k].n);
+        }
+    }
+    ensure_pool();
+    const auto ts0 = std::chrono::steady_clock::now();
+    if (W.size() != T) W.resize(T);   // (each worker resets its own state when phase 1 starts)
+    // by the first two words: one worker owns those subtrees; 8 parts per
+    // worker, taken largest first by whichever worker is free (skewed
+    // churn clusters under a few first words)
+    const uint32_t P = 8 * T;
+    std::vector<std::vector<uint32_t>>& parts = parts_buf;   // (capacity kept across batches)
+    parts.resize(P);
+    for (auto& v : parts) v.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+        const PlanEnt& pe = plan[i];
+        const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+        const uint32_t key = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
+        parts[mix_word(key) % P].push_back(i);
+    }
+    // An insert part far above a worker's share (a hot first-two-words
+    // prefix, e.g. 10% of C5's churn under "+/+") is split by its third
+    // word: its filters then share the depth-2 nodes too, under the same
+    // striped locks and shared made map (parts split_from.. are those).
+    const uint32_t split_from = P;
+    if (!del) {
+        const size_t big = std::max<size_t>(64, n / (2 * T));
+        constexpr uint32_t SPLIT = 8;
+        for (uint32_t q = 0; q < split_from; ++q) {
+            if (parts[q].size() <= big) continue;
+            std::vector<uint32_t> whole;
+            whole.swap(parts[q]);
+            const size_t first = parts.size();
+            parts.resize(first + SPLIT);
+            for (uint32_t i : whole) {
+                const PlanEnt& pe = plan[i];
+                const uint32_t* w = plan_words[pe.part].data() + pe.woff;
+                parts[first + (pe.nw > 2 ? mix_word(w[2] * 0xC2B2AE35u + 7) % SPLIT : 0)].push_back(i);
+            }
+        }
+    }
+    const uint32_t NP = (uint32_t)parts.size();
+    std::vector<uint32_t> porder(NP);
+    for (uint32_t q = 0; q < NP; ++q) porder[q] = q;
+    std::sort(porder.begin(), porder.end(), [&](uint32_t a, uint32_t b) { return parts[a].size() > parts[b].size(); });
+    std::atomic<uint32_t> next_part{0};
+    // the first error stops every worker (not just the one that hit it):
+    // the filters applied are then those finished before it, see the header
+    std::atomic<bool> failed{false};
+    // node ids: at most the levels the batch's filters lack, the free ids first
+    std::vector<uint32_t>& ids = R.ids;
+    ids.clear();
+    std::atomic<size_t> next_id{0};
+    size_t fresh = 0;
+    const size_t base = nd.size();
+    if (!del) {
+        release_pending_ids();
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < n; ++i) total += plan[i].nw - plan[i].depth;
+        const size_t take = std::min<size_t>(total, free_nodes.size());
+        fresh = total - take + (size_t)T * Mut::ID_CHUNK;   // + slack: ids are taken a chunk per worker
+        if (base + fresh >= MAX_NODES) return 1;
+        // Transactional: every allocation first (a bad_alloc here leaves
+        // the engine as it was: the caller may still finish other work on
+        // it), then the commit below, which allocates nothing.
+        ids.reserve(take);
+        if (fresh) {
+            nd.reserve(base + fresh);
+            n_flen.reserve(base + fresh);
+            n_lext.reserve(base + fresh);
+            n_foff.reserve(base + fresh);
+        }
+        if (!full_f_dirty) dirty_f_mark.reserve(base + fresh);
+        ids.assign(free_nodes.end() - (long)take, free_nodes.end());
+        free_nodes.resize(free_nodes.size() - take);
+        if (fresh) {
+            nd.resize(base + fresh);   // dead records until handed out; the unused tail is cut after
+            n_flen.resize(base + fresh, 0);
+            n_lext.resize(base + fresh, 0);
+            n_foff.resize(base + fresh, 0);
+        }
+        if (!full_f_dirty && dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
+    }
+    // (shared_made was cleared at the end of the previous batch)
+    const auto tp0 = std::chrono::steady_clock::now();
+    // phase 1: node records, by first word
+    pool.run([&](unsigned t) {
+        Mut& m = W[t];
+        m.reset();
+        m.ids = &ids;
+        m.next_id = &next_id;
+        m.n_free = ids.size();
+        m.n_fresh = fresh;
+        m.fresh_base = base;
+        m.defer = true;
+        tl_mut = &m;
+        const auto tw0 = std::chrono::steady_clock::now();
+        try {
+            for (uint32_t pi; !m.rc && !failed.load(std::memory_order_relaxed) && (pi = next_part.fetch_add(1)) < NP;) {
+                const std::vector<uint32_t>& items = parts[porder[pi]];
+                const uint32_t sd = porder[pi] >= split_from ? 3 : 2;
+                const size_t ni = items.size();
+                m.n_items += ni;
+                for (size_t q = 0; q < ni; ++q) {
+                    if ((q & 63) == 63 && failed.load(std::memory_order_relaxed)) break;
+                    const uint32_t i = items[q];
+                    if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
+                        const uint32_t f = plan[items[q + 8]].node;
+                        if (f != NONE) {
+                            __builtin_prefetch(&nd[f]);
+                            __builtin_prefetch(&n_lext[f]);   // (a new literal child sets a bit there)
+                        }
+                    }
+                    const PlanEnt& pe = plan[i];
+                    int rc;
+                    if (del) {
+                        rc = delete_planned(i);
+                    } else {
+                        rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
+                                             plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth, sd);
+                    }
+                    if (rc) { m.rc = rc; failed.store(true, std::memory_order_relaxed); break; }
+                    ++m.done;
+                }
+            }
+        } catch (...) {
+            m.rc = TM_ENOMEM;
+            failed.store(true, std::memory_order_relaxed);
+        }
+        m.t_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
+        tl_mut = nullptr;
+    });
+    R.del = del;
+    R.n = n;
+    R.W = &W;
+    R.fresh = fresh;
+    R.base = base;
+    R.ts0 = ts0;
+    R.tp0 = tp0;
+    R.tp1 = std::chrono::steady_clock::now();
+    return 0;
+}
+
+void tm_engine::par_finish(ParRun* const* runs, size_t nr) {
+    const unsigned T = std::max(1u, threads);
+    std::vector<std::vector<Mut>*> Ws;
+    for (size_t r = 0; r < nr; ++r) Ws.push_back(runs[r]->W);
+    edge_phase(Ws);
+    const auto tp2 = std::chrono::steady_clock::now();
+    for (size_t r = 0; r < nr; ++r) {
+        ParRun& R = *runs[r];
+        R.tp2 = tp2;
+        for (Mut& m : *R.W) {
+            live_nodes += m.live_nodes;
+            n_filters += m.n_filters;
+            route_entries += m.route_entries;
+            routes_dirty = routes_dirty || m.routes_dirty;
+            version += m.version;
+            R.done += m.done;
+            if (m.rc && !R.rc) R.rc = m.rc;
+            m.fresh_base = fbytes.size();   // (reused: this worker's bytes start here)
+            fbytes.insert(fbytes.end(), m.fb.begin(), m.fb.end());
+            dirty_f.insert(dirty_f.end(), m.dirty_f.begin(), m.dirty_f.end());
+            for (const auto& q : m.pend) pending_free.push_back(q);
+        }
+    }
+    pool.run([&](unsigned t) {   // filter byte offsets: distinct nodes per worker
+        for (size_t r = 0; r < nr; ++r) {
+            const std::vector<Mut>& W = *runs[r]->W;
+            for (size_t j = t; j < W.size(); j += pool.n)
+                for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+        }
+        for (unsigned j = t; j < 64; j += pool.n) shared_made[j].clear();   // for the next batch
+    });
+    for (size_t r = 0; r < nr; ++r) {
+        ParRun& R = *runs[r];
+        if (R.del) continue;
+        std::vector<Mut>& W = *R.W;
+        const std::vector<uint32_t>& ids = R.ids;
+        const size_t fresh = R.fresh, base = R.base;
+        // ids not handed out: free ones back to the list, the fresh tail cut off
+        // (the rest of each worker's last chunk: free-list ids go back; fresh
+        // ids below the highest one handed out stay as free dead records)
+        size_t used = 0;
+        for (const Mut& m : W) used = std::max(used, m.id_lo);   // highest id index handed out + 1
+        const size_t avail = ids.size() + fresh;
+        if (used > avail) used = avail;
+        for (const Mut& m : W)
+            for (size_t k = m.id_lo; k < std::min(m.id_hi, used); ++k)
+                free_nodes.push_back(k < ids.size() ? ids[k] : (uint32_t)(base + (k - ids.size())));
+        for (size_t k = used; k < ids.size(); ++k) free_nodes.push_back(ids[k]);
+        const size_t fresh_used = used > ids.size() ? used - ids.size() : 0;
+        if (fresh_used < fresh) {
+            nd.resize(base + fresh_used);
+            n_flen.resize(base + fresh_used);
+            n_lext.resize(base + fresh_used);
+            n_foff.resize(base + fresh_used);
+            if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
+        }
+    }
+    if (getenv("TM_PAR_TRACE")) {
+        const auto tp3 = std::chrono::steady_clock::now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        for (size_t r = 0; r < nr; ++r) {
+            const ParRun& R = *runs[r];
+            fprintf(stderr, "[par %s n=%u T=%u] setup %.2f ms phase1 %.2f ms edges %.2f ms merge %.2f ms%s; workers (items, us):",
+                    R.del ? "del" : "ins", R.n, T, ms(R.ts0, R.tp0), ms(R.tp0, R.tp1), ms(R.tp1, R.tp2), ms(R.tp2, tp3),
+                    nr > 1 ? " (edges + merge shared)" : "");
+            for (const Mut& m : *R.W) fprintf(stderr, " (%zu, %.0f)", m.n_items, m.t_us);
+            fprintf(stderr, "\n");
+        }
+    }
+}

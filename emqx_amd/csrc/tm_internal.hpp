@@ -1,10 +1,10 @@
-// tm_internal.hpp -- layout shared by the host engine (tm_engine.cpp) and the
+// tm_internal.hpp -- layout shared by the host engine (tm_engine_impl.hpp and its modules) and the
 // gfx950 kernels (tm_kernels.hip).  See DESIGN.md "Data layout in HBM".
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-struct tm_engine;   // include/emqx_tm.h (opaque handles, defined in tm_engine.cpp)
+struct tm_engine;   // include/emqx_tm.h (opaque handles, defined in tm_engine_impl.hpp)
 struct tm_batch;
 
 namespace etm {
@@ -285,6 +285,12 @@ struct FanArgs {
     const uint32_t* rcount;   // n: the walk's row lengths (tm_batch_rows)
     const unsigned long long* rsrc;   // n: the rows' first staging entries
     uint32_t* dcount;         // n: deliveries of each row (drow = its first)
+    // Per entry j, written by the scan for the fill (null: the fill gathers it
+    // itself): INT64_MIN + the subscriber of a one-subscriber run, else the
+    // subs[] index of the run's start minus the entry's block-relative first
+    // delivery -- so the fill's staging reads it with the entry's offsets
+    // instead of a gather by filter id behind them
+    int64_t* ebase;
 };
 
 // staging region capacity of a launch: a multiple of 16 entries per region so
@@ -401,6 +407,25 @@ struct PartBuffers {
 // each with its own wait)
 int part_batch_buffers(tm_engine* e, tm_batch** io, uint32_t n, uint64_t nwords, PartBuffers* out);
 int part_batch_finish(tm_engine* e, tm_batch* b, uint32_t* relaunched);
+// Host arrays still being staged by other threads (tm_sharded_prepare): the
+// topic bytes in chunks of chunk_bytes (items [0, nbyte_items)), the rebased
+// offsets in chunks of chunk_offs (items after); ready[item] turns 1 once the
+// item is in place (release), bad turns true first when a staged topic fails
+// its check.  The tokeniser uploads each chunk it needs as soon as it is ready
+// (the DMA of one overlaps the copying of the next) and refuses to launch on a
+// bad batch.
+struct TokStaged {
+    const uint8_t* ready;   // (read with __atomic_load_n, acquire)
+    const bool* bad;
+    uint64_t chunk_bytes, chunk_offs;
+    uint32_t nbyte_items;
+};
+// tm_tokenize_device with the topic bytes [base, base + nbytes) of topics and
+// the n + 1 offsets at offsets (absolute, offsets[0] == base once staged)
+// taken from a staging in progress
+int tokenize_device_staged(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, uint64_t base,
+                           uint64_t nbytes, uint64_t off_item0, const TokStaged& st, uint32_t* d_words,
+                           uint64_t words_cap, uint32_t* d_toff, uint8_t* d_tflags, uint64_t* nwords_out);
 // un-partition: counts_o[order[p]] = counts_p[p]
 hipError_t launch_unpart_counts(const uint32_t* order, const uint32_t* counts_p, uint32_t n, uint32_t* counts_o,
                                 hipStream_t s);
@@ -430,7 +455,7 @@ static_assert(sizeof(DictEnt) == 48, "dictionary entry is 48 bytes (three 16-B l
 // and HW_SEED2), so a
 // lookup is two independent 16-B loads and no probe chain; head + len are the
 // whole word up to 8 bytes, longer words also compare their DictTail (by id).
-// Mirrored from the host interner (tm_engine.cpp WordDict).
+// Mirrored from the host interner (tm_engine_impl.hpp WordDict).
 struct DictKey {
     uint64_t head;   // bytes 0..7, little-endian, zero-padded
     uint32_t len;
@@ -485,7 +510,7 @@ constexpr uint32_t HW_SEED = 0x9E3779B9u;
 constexpr uint32_t HW_SEED2 = 0x7F4A7C15u;
 
 // Device tokenisation of a topic batch (bytes[offs[t] - base .. offs[t+1] - base)):
-// the same words, classes, flags and ids as the host tokeniser (tm_engine.cpp
+// the same words, classes, flags and ids as the host tokeniser (tm_batch.cpp
 // tokenize_range), against the uploaded dictionary.
 // One wavefront per tile of 64 topics: a tile's bytes are contiguous, so
 // pass 1 counts the tile's words ('/' + 1 per topic) with coalesced loads,

@@ -307,10 +307,26 @@ struct tm_sharded {
     // counted (the plan: how many publishes and words of slice i shard j
     // walks, and where they land in shard j's batch), every shard's part batch
     // sized.  One shard: the slice is tokenised straight into the part batch.
-    int plan(tm_sharded_batch* b) {
+    //
+    // uoffs / st: called by tm_sharded_prepare while the staging threads are
+    // still copying the batch into b->bytes / b->offs (TokStaged); the slice
+    // bounds then come from the caller's own offsets uoffs.
+    int plan(tm_sharded_batch* b, const uint64_t* uoffs = nullptr, const TokStaged* st = nullptr) {
         int rc;
         const uint32_t n = b->n;
         const uint8_t* bytes = b->bytes;
+        // the bytes of topics [lo, hi) and where they start in b->bytes
+        auto span = [&](uint32_t lo, uint32_t hi, uint64_t& at) -> uint64_t {
+            at = st ? uoffs[lo] - uoffs[0] : b->offs[lo];
+            return (st ? uoffs[hi] - uoffs[0] : b->offs[hi]) - at;
+        };
+        auto tokenize = [&](uint32_t i, uint32_t lo, uint32_t cnt, uint32_t* w, uint64_t wcap, uint32_t* toff,
+                            uint8_t* tfl, uint64_t* nw) {
+            if (!st) return tm_tokenize_device(sh[i], bytes, b->offs + lo, cnt, w, wcap, toff, tfl, nw);
+            uint64_t at;
+            const uint64_t nb = span(lo, lo + cnt, at);
+            return tokenize_device_staged(sh[i], bytes, b->offs + lo, cnt, at, nb, lo, *st, w, wcap, toff, tfl, nw);
+        };
         b->dict_words = dict_words();
         b->done = b->ordered = false;
         if (b->part.size() != G) {
@@ -320,11 +336,11 @@ struct tm_sharded {
         b->pn.assign(G, 0);
         b->pw.assign(G, 0);
         if (G == 1) {
-            const uint64_t cap = b->offs[n] + n + 1;
+            uint64_t at;
+            const uint64_t cap = span(0, n, at) + n + 1;
             if ((rc = part_batch_buffers(sh[0], &b->part[0], n, cap, &b->pb[0]))) return rc;
             uint64_t nw = 0;
-            if ((rc = tm_tokenize_device(sh[0], bytes, b->offs, n, b->pb[0].words, b->pb[0].words_cap,
-                                         b->pb[0].toff, b->pb[0].tflags, &nw)))
+            if ((rc = tokenize(0, 0, n, b->pb[0].words, b->pb[0].words_cap, b->pb[0].toff, b->pb[0].tflags, &nw)))
                 return rc;
             b->pn[0] = n;
             b->pw[0] = nw;
@@ -338,7 +354,8 @@ struct tm_sharded {
             S.n = (uint32_t)((uint64_t)n * (i + 1) / G) - S.lo;
             S.on(dev[i]);
             S.seg.assign(2 * ((size_t)G + 1), 0);
-            const uint64_t nbytes = b->offs[S.lo + S.n] - b->offs[S.lo];
+            uint64_t at;
+            const uint64_t nbytes = span(S.lo, S.lo + S.n, at);
             int r;
             const uint32_t nb = std::max<uint32_t>(1, (S.n + PART_BLOCK - 1) / PART_BLOCK), gb = G * nb;
             if ((r = S.words.reserve(nbytes + S.n + 1)) || (r = S.toff.reserve((size_t)S.n + 1)) ||
@@ -353,8 +370,7 @@ struct tm_sharded {
                 return;
             }
             uint64_t nw = 0;
-            if ((r = tm_tokenize_device(sh[i], bytes, b->offs + S.lo, S.n, S.words.p, S.words.cap, S.toff.p,
-                                        S.tflags.p, &nw))) {
+            if ((r = tokenize(i, S.lo, S.n, S.words.p, S.words.cap, S.toff.p, S.tflags.p, &nw))) {
                 rcs[i] = r;
                 return;
             }
@@ -820,34 +836,52 @@ int tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* off
             throw std::bad_alloc();
         // copied by several threads (one would take ~30 ms for a 10M-publish
         // batch), which check every topic on the way: offsets that do not
-        // decrease, names of at most ?MAX_TOPIC_LEN bytes (src/emqx_topic.erl:45)
+        // decrease, names of at most ?MAX_TOPIC_LEN bytes (src/emqx_topic.erl:45).
+        // The copy is cut into items taken in order (the bytes, then the
+        // offsets), and the plan's tokenisers upload each item as soon as it is
+        // in place: the DMA runs behind the copy instead of after it.
+        constexpr uint64_t CB = 4ull << 20, CO = 512ull << 10;
+        const uint64_t nbi = (nbytes + CB - 1) / CB, noi = ((uint64_t)n + 1 + CO - 1) / CO;
+        std::vector<uint8_t> ready(nbi + noi, 0);
+        bool bad = false;
+        std::atomic<uint64_t> next{0};
+        std::mutex staged_mu;
+        float staged_ms = 0;   // when the last staging thread ran out of items
+        auto stage = [&] {
+            for (uint64_t it; (it = next.fetch_add(1, std::memory_order_relaxed)) < nbi + noi;) {
+                if (it < nbi) {
+                    const uint64_t c0 = it * CB, c1 = std::min(nbytes, c0 + CB);
+                    memcpy(b->bytes + c0, topics + base + c0, c1 - c0);
+                } else {
+                    const uint64_t o0 = (it - nbi) * CO, o1 = std::min<uint64_t>((uint64_t)n + 1, o0 + CO);
+                    bool ok = true;
+                    for (uint64_t i = o0; i < o1; ++i) {
+                        b->offs[i] = offsets[i] - base;
+                        if (i < n) ok &= offsets[i + 1] >= offsets[i] && offsets[i + 1] - offsets[i] <= TM_MAX_TOPIC_LEN;
+                    }
+                    if (!ok) __atomic_store_n(&bad, true, __ATOMIC_RELEASE);
+                }
+                __atomic_store_n(&ready[it], (uint8_t)1, __ATOMIC_RELEASE);
+            }
+            const float t = (float)(now_ms() - t0);
+            std::lock_guard<std::mutex> g(staged_mu);
+            staged_ms = std::max(staged_ms, t);
+        };
         const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, (nbytes + n * 8) >> 22));
         std::vector<std::thread> th;
-        std::atomic<bool> bad{false};
-        for (unsigned k = 0; k < T; ++k)
-            th.emplace_back([&, k] {
-                const size_t o0 = (size_t)((uint64_t)(n + 1) * k / T), o1 = (size_t)((uint64_t)(n + 1) * (k + 1) / T);
-                bool ok = true;
-                for (size_t i = o0; i < o1; ++i) {
-                    b->offs[i] = offsets[i] - base;
-                    if (i < n) ok &= offsets[i + 1] >= offsets[i] && offsets[i + 1] - offsets[i] <= TM_MAX_TOPIC_LEN;
-                }
-                if (!ok) bad.store(true, std::memory_order_relaxed);
-                const size_t c0 = (size_t)(nbytes * k / T), c1 = (size_t)(nbytes * (k + 1) / T);
-                if (c1 > c0) memcpy(b->bytes + c0, topics + base + c0, c1 - c0);
-            });
+        for (unsigned k = 0; k < T; ++k) th.emplace_back(stage);
+        b->dict_words = ~0ull;
+        const TokStaged st{ready.data(), &bad, CB, CO, (uint32_t)nbi};
+        const double t1 = now_ms();
+        rc = s->plan(b, offsets, &st);
+        b->ms_plan = (float)(now_ms() - t1);
         for (auto& t : th) t.join();
-        if (bad.load()) {
+        b->ms_stage = staged_ms;
+        if (bad) {
             b->n = 0;                 // (a re-prepared batch keeps nothing of the refused one:
             b->dict_words = ~0ull;    //  its next step re-plans)
             rc = TM_EINVAL;
-            if (fresh) tm_sharded_batch_free(s, b);
-            return rc;
         }
-        b->ms_stage = (float)(now_ms() - t0);
-        const double t1 = now_ms();
-        rc = s->plan(b);
-        b->ms_plan = (float)(now_ms() - t1);
     } catch (...) {
         rc = TM_ENOMEM;
     }

@@ -619,7 +619,8 @@ typedef struct {
     uint32_t host_waits;      /* blocking host waits in the last step: 1, + 1 per capacity relaunch */
     uint32_t part_topics[64]; /* publishes each shard matched */
     float ms_stage;           /* host wall time of the last prepare's copy of the publishes into pinned memory */
-    float ms_plan;            /* host wall time of the last prepare's plan (uploads, device tokenisers, counts) */
+    float ms_plan;            /* host wall time of the last prepare's plan (uploads, device tokenisers, counts);
+                                 the uploads start while the copy runs, so the two overlap */
 } tm_sharded_stats;
 /* how shard i's memory reaches shard j's device */
 #define TM_LINK_SAME   0      /* same device: D2D copies */

@@ -1,4 +1,4 @@
-"""The host edge hash under heavy churn at high load (tm_engine.cpp
+"""The host edge hash under heavy churn at high load (tm_engine_impl.hpp
 delete_edge_of: backward-shift deletion at bucket granularity, no tombstones).
 tm_debug_check verifies the table invariants the kernels' probes rely on
 (buckets filled in order, every key's probe run unbroken and within

@@ -8,7 +8,8 @@
 #   prof [BENCH ARGS]        rocprofv3 --kernel-trace --stats of bench.py --profile ARGS
 #   pmc COUNTERS [ARGS]      one rocprofv3 --pmc pass (COUNTERS comma-free, '+'-joined)
 #   py SCRIPT [ARGS]         python SCRIPT ARGS
-# A step may start with T=<seconds> to override its time limit.
+# A step may start with T=<seconds> (its time limit) and E=NAME=VALUE (an
+# environment variable for that step only).
 #
 #   gpurun --timeout 900 -- tools/gpu.sh r5a 'tests -k sample' 'bench --gpus 2 --devices 0,0'
 set -o pipefail
@@ -20,7 +21,12 @@ i=0
 for step in "$@"; do
     i=$((i + 1))
     lim=""
-    if [[ $step == T=* ]]; then lim=${step%% *}; lim=${lim#T=}; step=${step#* }; fi
+    envs=()
+    while [[ $step == T=* || $step == E=* ]]; do
+        w=${step%% *}; step=${step#* }
+        if [[ $w == T=* ]]; then lim=${w#T=}; else envs+=("${w#E=}"); fi
+    done
+    for e in "${envs[@]}"; do export "$e"; done
     kind=${step%% *}
     args=""
     [[ $step == *" "* ]] && args=${step#* }
@@ -50,5 +56,6 @@ for step in "$@"; do
     *)
         echo "unknown step kind: $kind"; exit 2 ;;
     esac
+    for e in "${envs[@]}"; do unset "${e%%=*}"; done
 done
 echo DONE
