@@ -176,8 +176,8 @@ def c1_leg(host, device=0):
 
 def pmc_traffic(workload, topics, filters=None):
     """HBM bytes per walk launch from the committed PMC pass of this workload
-    (tools/pmc_traffic.sh -> profiles/pmc_latest.json for C2,
-    tools/pmc_traffic_c4.sh -> profiles/pmc_c4.json for C4), or None."""
+    (`tools/gpu.sh TAG 'traffic c2'` -> profiles/pmc_latest.json for C2,
+    `'traffic c4'` -> profiles/pmc_c4.json for C4), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json" if workload == "C2" else "pmc_c4.json")
     try:
         with open(path) as f:

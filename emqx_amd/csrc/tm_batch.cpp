@@ -10,7 +10,6 @@ int tm_engine::ensure_slow_scratch(tm_batch* b) {
         // skewed batch (C5: ~28k rows of ~1,000 matches) needs several
         // waves per CU; idle waves exit at once (scratch ~350 KB each)
         uint32_t w = b->n < 65536 ? 64u : std::min<uint32_t>(TM_SLOW_WAVES_MAX, b->n / 32);
-        if (const char* v = getenv("TM_SLOW_WAVES")) w = std::max(1, atoi(v));
         b->s_waves = w;
     }
     const size_t q = (size_t)b->s_waves * b->s_qcap, o = (size_t)b->s_waves * b->s_ocap;
@@ -703,15 +702,11 @@ int tm_engine::launch(tm_batch* b, bool csr) {
 }
 
 hipError_t tm_engine::enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S, unsigned ev_flags) {
+    (void)s;
     hipError_t e;
-    if (eager_csr) {
-        if ((e = launch_scan(s, S, b->d_total)) != hipSuccess) return e;
-        if ((e = launch_finalize(s, S, false)) != hipSuccess) return e;
-    }
     if ((e = hipEventRecordWithFlags(b->ev2, S, ev_flags)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S)) != hipSuccess)
         return e;   // ctrl + stats
-    if (eager_csr) return hipMemcpyAsync(b->h_total, b->d_total, 4, hipMemcpyDeviceToHost, S);
     return hipSuccess;
 }
 
@@ -901,14 +896,8 @@ int tm_engine::wait(tm_batch* b, bool drained, uint32_t* relaunched) {
     }
     for (int attempt = 0;; ++attempt) {
         if (!drained || attempt) {
-            static const bool wtrace = getenv("TM_WAIT_TRACE") != nullptr;
-            const auto w0 = std::chrono::steady_clock::now();
-            const bool was_done = b->end_recorded && hipEventQuery(b->ev_end) == hipSuccess;
             if (b->end_recorded) HIP_OK(hipEventSynchronize(b->ev_end));
             else HIP_OK(hipStreamSynchronize(S));
-            if (wtrace)
-                fprintf(stderr, "[wait] done before: %d, sync %.1f us\n", (int)was_done,
-                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count());
         }
         if (attempt && relaunched) ++*relaunched;
         if (b->dedup_dev) {   // the walk's rows: the distinct publishes counted by the dedup pass
@@ -938,24 +927,12 @@ int tm_engine::wait(tm_batch* b, bool drained, uint32_t* relaunched) {
         if ((rc = grow_for(b, err, need, staged))) return rc;
         if ((rc = launch(b))) return rc;
     }
-    // eager CSR (TM_EAGER_CSR): the finalize pass is rerun alone when ids[] was too small
-    if (eager_csr && b->h_total[0] > b->c_ids) {
-        int rc = dev_reserve(b->d_ids, b->c_ids, (size_t)b->h_total[0] + b->h_total[0] / 4);
-        if (rc) return rc;
-        b->scan_args.ids = b->d_ids;
-        b->scan_args.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull);
-        // scan + finalize again (finalize turns the block-local offsets into global ones)
-        HIP_OK(launch_scan(b->scan_args, S, b->d_total));
-        HIP_OK(launch_finalize(b->scan_args, S, checked));
-        HIP_OK(hipEventRecord(b->ev2, S));
-        HIP_OK(hipStreamSynchronize(S));
-    }
     fill_stats(b);
     b->done = true;
     // (dense_enq, not eager_dense: the pipelined caller clears eager_dense
     // right after launch, while the tail it asked for is already queued)
-    b->dense = eager_csr || (b->dense_enq && !b->oneshot && b->total <= b->dense_cap);
-    if (b->dense && !eager_csr) {
+    b->dense = b->dense_enq && !b->oneshot && b->total <= b->dense_cap;
+    if (b->dense) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, b->evc0, b->evc1);
         b->st.ms_csr = ms;

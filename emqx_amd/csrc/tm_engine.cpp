@@ -201,7 +201,7 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
     }
     Replica& R = e->pick();
     if ((rc = e->use(&R))) return rc;
-    if (n > tm_engine::ONESHOT_MAX && !e->eager_csr) {
+    if (n > tm_engine::ONESHOT_MAX) {
         try {
             return e->match_batch_pipelined(R, topics, offsets, n, out);
         } catch (...) {
@@ -227,7 +227,7 @@ int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
         e->upload_nosync = false;
         if (rc) return rc;
         // latency-sized batches: CSR and its host copy enqueued with the walk
-        R.scratch.oneshot = n <= tm_engine::ONESHOT_MAX && !e->eager_csr;
+        R.scratch.oneshot = n <= tm_engine::ONESHOT_MAX;
         if ((rc = e->launch(&R.scratch))) return rc;
         if ((rc = e->wait(&R.scratch))) return rc;
         if (e->oneshot_result(&R.scratch, out) == TM_OK) {
@@ -481,18 +481,10 @@ int tm_batch_wait(tm_engine* e, tm_batch* b) {
         if (b->end_recorded) HIP_OK(hipEventSynchronize(b->ev_end));
         else HIP_OK(hipStreamSynchronize(b->own));
     }
-    static const bool wtrace = getenv("TM_WAIT_TRACE") != nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::recursive_mutex> g(e->mu);
-    const auto t1 = std::chrono::steady_clock::now();
     int rc = e->use(b->rep);
     if (rc) return rc;
-    rc = e->wait(b);
-    if (wtrace) {
-        auto us = [](auto a, auto c) { return std::chrono::duration<double, std::micro>(c - a).count(); };
-        fprintf(stderr, "[tm_batch_wait] lock %.1f us, total %.1f us\n", us(t0, t1), us(t0, std::chrono::steady_clock::now()));
-    }
-    return rc;
+    return e->wait(b);
 }
 
 int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {

@@ -800,7 +800,7 @@ struct Replica {
     // a batch launches when a slot is free and either nothing is in flight or
     // at least a_busy_min calls queued: under load, calls accumulate while the
     // device works instead of trickling out as tiny batches
-    uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // tools/ab_async.sh
+    uint32_t a_max = 16384, a_linger_us = 0, a_depth = 4, a_busy_min = 128, a_ncompleters = 6;   // (depth / completers: TM_ASYNC_DEPTH / TM_ASYNC_COMPLETERS)
     uint32_t a_spin_us = 0;   // completers poll a pinned flag this long before blocking on the event (0: off)
     // (while batches are in flight and fewer than a_busy_min calls wait, the
     // launcher waits for the pipeline to idle or a_busy_min calls; a bounded
@@ -808,7 +808,7 @@ struct Replica {
     // blocking leg unchanged, 4,096-in-flight leg 6.2 -> 4.6-4.7 M calls/s)
     // a call that finds the queue empty and the whole pipeline idle launches
     // its batch itself, on the calling thread (no launcher wake-up)
-    bool a_inline = true;
+    const bool a_inline = true;
     uint64_t a_batches = 0, a_requests = 0, a_recoveries = 0, a_max_seen = 0, a_inline_launches = 0;
     // where the pipeline's time goes (host microseconds, summed over batches)
     double a_us_launch = 0, a_us_wait = 0, a_us_deliver = 0;
@@ -1064,10 +1064,10 @@ struct tm_engine {
     bool frozen = false;           // TM_CFG_FROZEN_DICT: words only via tm_dict_load
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
-    uint32_t qcap = 384;           // LDS probe stack per wave, 384 or 512 (TM_QCAP); C2 tiles peak at ~340
-    double static_frac = 0.5;       // share of tiles scheduled round-robin before tickets (TM_STATIC_FRAC)
+    uint32_t qcap = 384;           // LDS probe stack per wave (C2 tiles peak at ~340; 512 measured no faster)
+    double static_frac = 0.5;       // share of tiles scheduled round-robin before per-XCD tickets
     uint64_t fan_big_limit = 0xFFFFFFFFull;   // fan-out scan blocks above this use u64 offsets (TM_FAN_BIG: tests)
-    double target_load = 0.35;     // edge-hash load after a re-pack (TM_LOAD)
+    double target_load = 0.35;     // edge-hash load after a re-pack
     uint64_t result_limit = MAX_RESULT;   // matches per batch (TM_RESULT_LIMIT: test-only knob to lower it)
     uint64_t staging_min = 1u << 16;      // initial staging entries of a batch (TM_STAGING_MIN: test-only)
 
@@ -1941,8 +1941,6 @@ struct tm_engine {
     // then what the walk left in HBM -- row i = sfids[src[i] .. + count[i]),
     // sorted and deduplicated -- and the dense CSR (scan + finalize copy) is
     // built only for a consumer that asks for offsets (ensure_dense).
-    // TM_EAGER_CSR=1 builds it in every launch (round-2 behaviour, for A/B).
-    bool eager_csr = getenv("TM_EAGER_CSR") && atoi(getenv("TM_EAGER_CSR")) != 0;
     hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S, unsigned ev_flags = 0);
 
     // tm_match_batch's tail, enqueued behind the walk: scan + finalize (the

@@ -7,16 +7,12 @@ int tm_engine::init(const tm_config* cfg, const int32_t* devices, uint32_t ndev)
     const char* ck = getenv("TM_CHECKED");
     checked = ck && ck[0] == '1';
     if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
-    if (const char* qc = getenv("TM_QCAP")) qcap = atoi(qc) <= 384 ? 384u : 512u;
-    if (const char* sf = getenv("TM_STATIC_FRAC")) static_frac = std::min(1.0, std::max(0.0, atof(sf)));
     if (const char* fb = getenv("TM_FAN_BIG")) fan_big_limit = std::min<uint64_t>(0xFFFFFFFFull, strtoull(fb, nullptr, 10));
-    if (const char* ld = getenv("TM_LOAD")) target_load = std::min(0.75, std::max(0.1, atof(ld)));
     if (const char* rl = getenv("TM_RESULT_LIMIT"))
         result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));
     if (const char* sm = getenv("TM_STAGING_MIN")) staging_min = std::max<uint64_t>(64, strtoull(sm, nullptr, 10));
     threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
     dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
-    if (const char* ht = getenv("TM_HOST_TOKENIZE")) dev_tok = dev_tok && !(ht[0] == '1');
     if (const char* ng = getenv("TM_NO_GRAPH")) use_graphs = ng[0] != '1';
     // root node id 0 (absent until the first add_path, like the reference)
     nd.push_back(NodeRec{});

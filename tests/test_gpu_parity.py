@@ -197,7 +197,8 @@ def test_fused_fresh_walk_parity():
         eng = Engine(device=0)
     finally:
         del os.environ["TM_FRESH_FUSED"]
-    F = gen.gen_filters(gen.C1).tolist() + [b"", b"+/+", b"a/#", b"+x/#"]
+    # (C1 already holds b"" and b"+/+": oracle ids are positions in a duplicate-free list)
+    F = list(dict.fromkeys(gen.gen_filters(gen.C1).tolist() + [b"", b"+/+", b"a/#", b"+x/#"]))
     Ts = gen.gen_topics(gen.C1, gen.Strings.from_list(F), 1001, gen.C1_TOPICS)
     T = Ts.tolist() + [b"", b"", b"/", b"+x/y", b"a/" + b"/".join([b"q"] * 14), b"a" * 3000 + b"/b", b"a/b"]
     for f in F:

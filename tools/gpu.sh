@@ -7,6 +7,7 @@
 #   bench [BENCH ARGS]       python bench.py ARGS -> the JSON line, summarised
 #   prof [BENCH ARGS]        rocprofv3 --kernel-trace --stats of bench.py --profile ARGS
 #   pmc COUNTERS [ARGS]      one rocprofv3 --pmc pass (COUNTERS comma-free, '+'-joined)
+#   traffic c2|c4 [ARGS]     FETCH_SIZE + WRITE_SIZE passes -> $O/pmc_<workload>.json
 #   py SCRIPT [ARGS]         python SCRIPT ARGS
 # A step may start with T=<seconds> (its time limit) and E=NAME=VALUE (an
 # environment variable for that step only).
@@ -50,6 +51,18 @@ for step in "$@"; do
         timeout -s KILL ${lim:-120} rocprofv3 --pmc ${ctr//+/ } -d $base.d -o pmc --output-format csv -- \
             python3 bench.py --profile "${A[@]:1}" > $base.json 2> $base.err || { tail -20 $base.err; exit 1; }
         echo "pmc pass done: $ctr" ;;
+    traffic)
+        # HBM bytes per walk launch (roofline.traffic): FETCH_SIZE and WRITE_SIZE
+        # in passes of their own, folded by pmc_summary.py into
+        # $O/pmc_<workload>.json (copy to profiles/pmc_latest.json / pmc_c4.json)
+        wl=${A[0]}; extra=("${A[@]:1}")
+        sargs=(); [[ $wl == c4 ]] && sargs=(--workload C4 --filters 100000000)
+        for pass in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL ${lim:-300} rocprofv3 --pmc $pass -d $base.d/$pass -o p --output-format csv -- \
+                python3 bench.py --workload $wl --profile --steps 2 --warmup 1 "${extra[@]}" \
+                > $base.$pass.json 2> $base.$pass.err || { tail -20 $base.$pass.err; exit 1; }
+        done
+        python3 tools/pmc_summary.py $base.d "${sargs[@]}" --write $O/pmc_$wl.json | tail -12 ;;
     py)
         timeout -k 10 ${lim:-600} python -u "${A[@]}" > $base.log 2> $base.err || { tail -20 $base.err; exit 1; }
         tail -5 $base.log ;;
