@@ -558,8 +558,6 @@ struct tm_batch {
     uint32_t* d_moff32 = nullptr;
     uint8_t* d_fbig = nullptr;
     size_t c_moff32 = 0, c_fbig = 0;
-    int64_t* d_febase = nullptr;    // the fill's per-entry subscriber bases (FanArgs.ebase)
-    size_t c_febase = 0;
     uint32_t* d_dcount = nullptr;   // TM_DISPATCH_ROWS: deliveries of each row
     size_t c_dcount = 0;
     uint64_t *d_fmeta = nullptr, *h_fmeta = nullptr;   // TM_DISPATCH_ROWS: staging regions (vb, rtop)
@@ -572,7 +570,6 @@ struct tm_batch {
 
     void release() {
         dev_free(d_moff); dev_free(d_moff32); dev_free(d_fbig); dev_free(d_dcount); dev_free(d_fmeta);
-        dev_free(d_febase);
         if (h_fmeta) (void)hipHostFree(h_fmeta);
         h_fmeta = nullptr; dev_free(d_fbsums); dev_free(d_ftotal); dev_free(d_drow); dev_free(d_fout);
         dev_free(d_ftile);
@@ -1910,8 +1907,6 @@ struct tm_engine {
     int reserve_dedup(tm_batch* b, uint64_t nbytes);
 
     DedupArgs dedup_args(tm_batch* b) const;
-    // TM_FAN_EBASE=0: the fan-out fill gathers its subscriber bases itself (A/B; default: the scan writes them)
-    const bool fan_ebase = !getenv("TM_FAN_EBASE") || atoi(getenv("TM_FAN_EBASE")) != 0;
     // TM_FRESH_FUSED=1: a fresh batch's tokeniser fill inside the walk (tm_match_fresh).  Measured
     // slower on C2 (fresh 10M batch 5.35 -> 5.64 ms, profiles/r05/fused/): off by default
     const bool fresh_fused = getenv("TM_FRESH_FUSED") && atoi(getenv("TM_FRESH_FUSED")) != 0;

@@ -289,7 +289,6 @@ int tm_engine::batch_dispatch(tm_batch* b, uint32_t flags, tm_deliveries* out) {
     if ((rc = dev_reserve(b->d_drow, b->c_drow, (size_t)n + 1))) return rc;
     if ((rc = host_reserve(b->h_ftotal, b->ch_ftotal, 1))) return rc;
     const bool counts_only = flags & TM_DISPATCH_COUNT_ONLY;
-    if (!counts_only && fan_ebase && (rc = dev_reserve(b->d_febase, b->c_febase, nm + 1))) return rc;
     if (!b->fev0) {
         HIP_OK(hipEventCreate(&b->fev0));
         HIP_OK(hipEventCreate(&b->fev1));
@@ -298,7 +297,6 @@ int tm_engine::batch_dispatch(tm_batch* b, uint32_t flags, tm_deliveries* out) {
     fa.soff = R.d_soff; fa.scnt = R.d_scnt; fa.sone = R.d_sone; fa.subs = R.d_subs; fa.nnodes = subs_nn;
     fa.moff = b->d_moff; fa.moff32 = b->d_moff32; fa.bbig = b->d_fbig; fa.bsums = b->d_fbsums;
     fa.big_limit = fan_big_limit; fa.d_total = b->d_ftotal; fa.drow = b->d_drow;
-    fa.ebase = (!counts_only && fan_ebase) ? b->d_febase : nullptr;
     HIP_OK(launch_fan_scan(fa, stream));
     HIP_OK(hipMemcpyAsync(b->h_ftotal, b->d_ftotal, 8, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));

@@ -285,12 +285,6 @@ struct FanArgs {
     const uint32_t* rcount;   // n: the walk's row lengths (tm_batch_rows)
     const unsigned long long* rsrc;   // n: the rows' first staging entries
     uint32_t* dcount;         // n: deliveries of each row (drow = its first)
-    // Per entry j, written by the scan for the fill (null: the fill gathers it
-    // itself): INT64_MIN + the subscriber of a one-subscriber run, else the
-    // subs[] index of the run's start minus the entry's block-relative first
-    // delivery -- so the fill's staging reads it with the entry's offsets
-    // instead of a gather by filter id behind them
-    int64_t* ebase;
 };
 
 // staging region capacity of a launch: a multiple of 16 entries per region so

@@ -1231,38 +1231,8 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_scan_local(FanArgs a) {
         }
         mine += c[k];
     }
-    // the fill's per-entry base: the one subscriber, or where the run starts
-    // in subs[] (all gathers of the thread in flight before any is used)
-    int64_t eb[FAN_PER];
-    if (a.ebase) {
-#pragma unroll
-        for (uint32_t k = 0; k < FAN_PER; ++k) {
-            eb[k] = 0;
-            if (c[k] == 1) eb[k] = INT64_MIN + (int64_t)a.sone[f[k]];
-            else if (c[k] > 1) eb[k] = (int64_t)a.soff[f[k]];
-        }
-    }
     uint64_t total;
     uint64_t run = fan_block_scan(mine, lds, total);
-    if (a.ebase && j0 <= a.n_matches) {
-        uint64_t r = run;
-#pragma unroll
-        for (uint32_t k = 0; k < FAN_PER; ++k) {
-            if (c[k] > 1) eb[k] -= (int64_t)r;   // block-relative: the fill subtracts the block's offset
-            r += c[k];
-        }
-        if (j0 + FAN_PER <= a.n_matches + 1) {
-            uint4* q = reinterpret_cast<uint4*>(a.ebase + j0);   // 128-B aligned (j0 % 16 == 0)
-#pragma unroll
-            for (uint32_t k = 0; k < FAN_PER / 2; ++k)
-                q[k] = make_uint4((uint32_t)eb[2 * k], (uint32_t)((uint64_t)eb[2 * k] >> 32), (uint32_t)eb[2 * k + 1],
-                                  (uint32_t)((uint64_t)eb[2 * k + 1] >> 32));
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < FAN_PER; ++k)
-                if (j0 + k <= a.n_matches) a.ebase[j0 + k] = eb[k];
-        }
-    }
     const bool big = total > a.big_limit;
     if (!big && j0 + FAN_PER <= a.n_matches + 1) {
         uint4* q = reinterpret_cast<uint4*>(a.moff32 + j0);
@@ -1440,18 +1410,16 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     for (uint32_t e0 = t; e0 < (uint32_t)ne; e0 += FAN_BLOCK * FAN_STG) {
         uint64_t m0[FAN_STG], m1[FAN_STG];
         uint32_t f[FAN_STG];
-        int64_t eb[FAN_STG];
         bool act[FAN_STG];
 #pragma unroll
         for (uint32_t u = 0; u < FAN_STG; ++u) {
             const uint32_t e = e0 + u * FAN_BLOCK;
-            m0[u] = 0; m1[u] = 0; f[u] = 0; eb[u] = 0;
+            m0[u] = 0; m1[u] = 0; f[u] = 0;
             if (e < (uint32_t)ne) {
                 const uint64_t j = jlo + e;
                 m0[u] = moff_at(j);
                 m1[u] = moff_at(j + 1);
-                if (a.ebase) eb[u] = a.ebase[j];   // (written by the scan: no gather by filter id)
-                else f[u] = one_reg ? fids[j] : fan_fid(a, j);
+                f[u] = one_reg ? fids[j] : fan_fid(a, j);
             }
         }
         int64_t v[FAN_STG];
@@ -1461,13 +1429,8 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
             v[u] = 0;
             // a one-delivery run keeps its subscriber inline (one 4-B gather,
             // no dependent read of subs[]): INT64_MIN + id marks it
-            if (act[u] && a.ebase) {
-                const uint64_t j = jlo + e0 + u * FAN_BLOCK;
-                v[u] = eb[u] < INT64_MIN + (1ll << 33) ? eb[u]
-                                                       : eb[u] - (int64_t)(j / FAN_SCAN_TILE != sb0 ? bs1 : bs0);
-            } else if (act[u]) {
-                v[u] = m1[u] - m0[u] == 1 ? INT64_MIN + (int64_t)a.sone[f[u]] : (int64_t)a.soff[f[u]] - (int64_t)m0[u];
-            }
+            if (act[u]) v[u] = m1[u] - m0[u] == 1 ? INT64_MIN + (int64_t)a.sone[f[u]]
+                                                  : (int64_t)a.soff[f[u]] - (int64_t)m0[u];
         }
 #pragma unroll
         for (uint32_t u = 0; u < FAN_STG; ++u) {
