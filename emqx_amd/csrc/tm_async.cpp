@@ -102,7 +102,7 @@ int tm_engine::match_async(Replica& R, const uint8_t* t, size_t len, tm_match_cb
             return TM_OK;
         }
     }
-    if (q == 1 || q == R.a_busy_min || q == R.a_max) {   // the launcher may be waiting for this
+    if (q == 1 || q == R.a_gather_at.load() || q == R.a_max) {   // the launcher may be waiting for this
         std::lock_guard<std::mutex> lk(R.amu);
         R.a_work.notify_one();
     }
@@ -148,6 +148,7 @@ void tm_engine::launch_locked(Replica& R, std::unique_lock<std::mutex>& lk) {
     const size_t take =
         std::min<uint64_t>(R.q_count.load(std::memory_order_acquire), std::max<uint32_t>(R.a_max, 1));
     R.q_count.fetch_sub(take, std::memory_order_acq_rel);   // reserved: no other drainer counts on them
+    R.a_inflight_calls += take;
     lk.unlock();
     drain_queue(R, sl, take);
     const auto t0 = std::chrono::steady_clock::now();
@@ -177,12 +178,25 @@ void tm_engine::launcher_loop(Replica& R) {
             if (R.a_stop) break;   // stopping, queue drained
             continue;              // an inline launch took the calls
         }
-        if (!R.a_stop && R.a_free.size() != R.a_slots.size() && queued() < R.a_busy_min) {
-            // batches in flight, few calls queued: gather more for a while
+        // Batches in flight and few calls queued: gather more for a while.
+        // "Few" scales with the calls the pipeline holds: a share of them per
+        // slot, at most a_busy_min.  Under load (thousands of calls in flight)
+        // batches stay large; with a few dozen blocking callers their calls
+        // spread over the slots instead of queueing behind one batch, so the
+        // device runs several small batches at once.
+        // (A/B, 64 blocking callers: 0.47 M calls/s with a fixed 128, 0.62 M
+        // calls/s scaled; the 2,048 / 4,096-in-flight legs unchanged)
+        auto need = [&] {
+            return std::min<uint64_t>(R.a_busy_min, std::max<uint64_t>(1, (R.a_inflight_calls + queued()) / R.a_depth));
+        };
+        if (!R.a_stop && R.a_free.size() != R.a_slots.size() && queued() < need()) {
             auto enough = [&] {
-                return R.a_stop || R.a_free.size() == R.a_slots.size() || queued() >= R.a_busy_min;
+                const uint64_t k = need();
+                R.a_gather_at.store(k);   // (seq_cst: a caller that reaches k after this sees it)
+                return R.a_stop || R.a_free.size() == R.a_slots.size() || queued() >= k;
             };
             R.a_work.wait(lk, enough);
+            R.a_gather_at.store(~0ull);
             if (R.a_free.empty() || queued() == 0) continue;
         }
         if (R.a_linger_us && !R.a_stop && queued() < R.a_max)
@@ -308,6 +322,7 @@ void tm_engine::completer_loop(Replica& R) {
 
 void tm_engine::slot_finish(Replica& R, AsyncSlot* sl) {
     R.a_inflight.erase(std::find(R.a_inflight.begin(), R.a_inflight.end(), sl));
+    R.a_inflight_calls -= sl->calls.size();
     ++R.a_batches;
     R.a_requests += sl->calls.size();
     sl->calls.clear();

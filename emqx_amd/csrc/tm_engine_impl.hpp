@@ -791,6 +791,10 @@ struct Replica {
     std::atomic<bool> a_live{false};     // pipeline threads running and accepting calls
     std::vector<AsyncSlot*> a_slots, a_free;
     std::deque<AsyncSlot*> a_inflight;
+    uint64_t a_inflight_calls = 0;   // calls of the batches in a_inflight (under amu)
+    // the queue length the gathering launcher waits for (callers reaching it
+    // wake it; ~0: not gathering)
+    std::atomic<uint64_t> a_gather_at{~0ull};
     std::thread a_launcher;
     std::vector<std::thread> a_completers;
     bool a_started = false, a_stop = false, a_launcher_done = false;

@@ -29,7 +29,8 @@ def main():
     exp_h = LD.row_hashes(offs, ids)
     LD.run(eng, T.slice(0, 20000), LD.ASYNC, 4, 64, hashes=False)
     shapes = [("sync", LD.SYNC, 16, 1), ("sync", LD.SYNC, 64, 1), ("async", LD.ASYNC, 16, 32),
-              ("async", LD.ASYNC, 16, 64), ("async", LD.ASYNC, 16, 128), ("async", LD.ASYNC, 16, 256)]
+              ("async", LD.ASYNC, 16, 64), ("async", LD.ASYNC, 16, 128), ("async", LD.ASYNC, 16, 256),
+              ("async", LD.ASYNC, 8, 128), ("async", LD.ASYNC, 8, 256)]
     for name, mode, th, win in shapes:
         cnt = n if mode == LD.ASYNC else min(n, 300_000)
         sub = T if cnt == n else T.slice(0, cnt)
@@ -39,7 +40,7 @@ def main():
         b1 = eng.async_stats()
         nb = max(b1["batches"] - b0["batches"], 1)
         print(json.dumps({"mode": name, "threads": th, "window": win, "calls_per_s": cnt / st["seconds"],
-                          "p50_us": st["p50_us"], "p99_us": st["p99_us"], "ok": bool(np.array_equal(hs, exp_h[:cnt])),
+                          "p50_us": st["p50_us"], "p99_us": st["p99_us"], "mean_us": st["mean_us"], "max_us": st["max_us"], "ok": bool(np.array_equal(hs, exp_h[:cnt])),
                           "mean_batch": (b1["requests"] - b0["requests"]) / nb,
                           "us_per_batch": {k: (b1[k] - b0[k]) / nb for k in ("us_launch", "us_wait", "us_deliver")},
                           "wall": time.time() - t0}), flush=True)
