@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
     if (lead) lslot[s] = dedup_global(a, t, h);
     __syncthreads();
     if (valid) {
-        a.rep[t] = lslot[s];
+        if (lead) a.rep[t] = lslot[s];   // (followers take their leader's verdict in pass 2)
         a.lead[t] = (uint16_t)lmin[s];
     }
 }
@@ -1711,7 +1711,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_mark(DedupArgs a) {
         lb[threadIdx.x] = (uint32_t)(b - w0);
         ll[threadIdx.x] = len;
         lead = a.lead[t];
-        r = (uint32_t)a.table[a.rep[t]];
+        if (lead == threadIdx.x) r = (uint32_t)a.table[a.rep[t]];   // (only leaders read the table)
     }
     __syncthreads();
     const GBytes g{a.bytes};
