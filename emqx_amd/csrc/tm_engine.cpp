@@ -995,8 +995,12 @@ int tokenize_device_staged(tm_engine* e, const uint8_t* topics, const uint64_t* 
     int rc = e->set_device();
     if (rc) return rc;
     try {
-        return e->tokenize_device(topics, offsets, n, d_words, words_cap, d_toff, d_tflags, nwords_out, &st, base,
-                                  nbytes, off_item0);
+        rc = e->tokenize_device(topics, offsets, n, d_words, words_cap, d_toff, d_tflags, nwords_out, &st, base,
+                                nbytes, off_item0);
+        // a failure may leave copies from the caller's staging in flight: they
+        // finish before the caller can free it
+        if (rc && !e->reps.empty()) (void)hipStreamSynchronize(e->reps[0]->stream);
+        return rc;
     } catch (...) {
         return TM_ENOMEM;
     }
