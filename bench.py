@@ -448,14 +448,16 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     unsubscribe deltas:
       host    the deltas applied to the trie (emqx_trie:delete/1, insert/1)
               and their upload enqueued;
-      device  the batch tokenised (emqx_topic:words/1), deduplicated (equal
-              tokens walk once, TM_BATCH_DEDUP on the device), walked
-              (rows longer than K by the generic kernel), and every
-              publish's row expanded in HBM (tm_batch_publish_rows: the
-              per-publish result; its total is "delivered").
-    Pipelined: the host applies deltas i + 1 while the device runs step i
-    (the upload of deltas i + 1 is queued behind walk i, ahead of launch
-    i + 1: read-your-writes), so a step costs max(host, device)."""
+      device  the batch deduplicated (equal bytes walk once, TM_BATCH_DEDUP
+              on the device), its distinct topics tokenised
+              (emqx_topic:words/1) and walked (rows longer than K by the
+              generic kernel), and every publish's row expanded in HBM
+              (tm_batch_publish_rows: the per-publish result; its total is
+              "delivered").
+    Pipelined: the host applies deltas i + 1 while the device runs step i;
+    their upload is queued behind walk i and batch i + 1 behind the upload
+    (read-your-writes) before batch i is waited for, so a step costs about
+    max(host, device)."""
     from emqx_amd import gen
     from emqx_amd.engine import Engine
     from emqx_amd.skew import Churn, workload
@@ -501,6 +503,13 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
             tc = time.perf_counter()
             eng.sync_async()     # the upload, queued behind step i on the engine stream
             ms_host["sync_async"].append(1e3 * (time.perf_counter() - tc))
+            # batch i + 1 is queued behind the upload before batch i is waited
+            # for: the device goes from walk i to upload i + 1 to batch i + 1
+            # without waiting for the host (the batches rotate, so i's rows
+            # stay intact until it is read below)
+            tc = time.perf_counter()
+            bs[(i + 1) % n_batches].retokenize().launch()
+            ms_host["launch"].append(1e3 * (time.perf_counter() - tc))
         tc = time.perf_counter()
         b.wait()
         ms_host["wait"].append(1e3 * (time.perf_counter() - tc))
@@ -513,10 +522,6 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         ms_queue.append(st["ms_queue"])
         rows.append(st["topics"])
         delivered.append(st["delivered"])
-        if i + 1 < steps:
-            tc = time.perf_counter()
-            bs[(i + 1) % n_batches].retokenize().launch()
-            ms_host["launch"].append(1e3 * (time.perf_counter() - tc))
     elapsed = time.perf_counter() - t0
     if sync is not None:
         sync.barrier()
