@@ -112,5 +112,21 @@ def build_all(force=False):
     return [build_tm(force), build_gen(force), build_load(force), build_nif_mock(force)]
 
 
+def build_variant(name, defines):
+    """A/B builds (dev): libemqx_tm with extra -D defines into
+    emqx_amd/variants/libemqx_tm_<name>.so, loaded with EMQX_TM_LIB=<path>."""
+    out_dir = os.path.join(HERE, "variants")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"libemqx_tm_{name}.so")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall",
+          "-Wl,-soname,libemqx_tm.so", *defines, "-o", out]
+         + [os.path.join(CSRC, f) for f in TM_SOURCES] + ["-lpthread"])
+    return out
+
+
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if "--variant" in sys.argv:   # python -m emqx_amd.build --variant NAME -DFOO=1 ...
+        i = sys.argv.index("--variant")
+        build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")])
+    else:
+        build_all(force="--force" in sys.argv)
