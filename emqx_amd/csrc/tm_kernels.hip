@@ -1703,7 +1703,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_mark(DedupArgs a) {
     if (staged)
         for (uint64_t k = 16u * threadIdx.x; k < we - w0; k += 16u * DD_BLOCK)
             *reinterpret_cast<uint4*>(lbytes + k) = *reinterpret_cast<const uint4*>(a.bytes + w0 + k);
-    uint64_t b = 0;
+    uint64_t b = 0, rb = 0, re = 0;
     uint32_t len = 0, r = 0, lead = 0;
     if (valid) {
         b = a.offs[t] - a.base;
@@ -1711,14 +1711,19 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_mark(DedupArgs a) {
         lb[threadIdx.x] = (uint32_t)(b - w0);
         ll[threadIdx.x] = len;
         lead = a.lead[t];
-        if (lead == threadIdx.x) r = (uint32_t)a.table[a.rep[t]];   // (only leaders read the table)
+        if (lead == threadIdx.x) {   // (only leaders read the table)
+            r = (uint32_t)a.table[a.rep[t]];
+            if (r != t) {   // the representative's bounds, in flight with the staging loads
+                rb = a.offs[r] - a.base;
+                re = a.offs[r + 1] - a.base;
+            }
+        }
     }
     __syncthreads();
     const GBytes g{a.bytes};
     if (valid && lead == threadIdx.x) {   // a leader: its bytes against the representative's
         if (r != t) {
-            const uint64_t rb = a.offs[r] - a.base;
-            bool eq = a.offs[r + 1] - a.base - rb == len;
+            bool eq = re - rb == len;
             if (eq) eq = staged ? bytes_equal(g, rb, LBytes{lbytes}, b - w0, len) : bytes_equal(g, rb, g, b, len);
             if (!eq) r = t;
         }

@@ -25,14 +25,15 @@ int tm_engine::ensure_delta_idle() {
 
 int tm_engine::sync_device(const Replica* back) {
     if (reps.empty()) return TM_ENODEV;
-    int rc = ensure_delta_idle();
-    if (rc) return rc;
     bool any = false;
     for (Replica* R : reps) any = any || upload_pending(*R);
-    if (!any) {
+    if (!any) {   // (an upload in flight is ordered before later work on the device: no host wait)
         HIP_OK(hipSetDevice(back ? back->device : device));
         return TM_OK;
     }
+    // the last async upload still reads the pinned staging this one rewrites
+    int rc = ensure_delta_idle();
+    if (rc) return rc;
     // after a bulk build or heavy churn, re-pack the host table to the
     // target load so the walk's working set stays small (a full upload)
     if (needs_repack()) {
