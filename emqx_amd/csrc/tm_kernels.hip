@@ -667,6 +667,12 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
     (void)tend;
 }
 
+#ifndef TM_DN_TILES_PER_WAVE
+#define TM_DN_TILES_PER_WAVE 4
+#endif
+// device-counted batches: tiles shrink until each wave has this many to take
+constexpr uint32_t DN_TILES_PER_WAVE = TM_DN_TILES_PER_WAVE;
+
 template <bool CK, bool BIG, int QC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_tiles(MatchArgs a) {
     __shared__ TileLds<QC> L;
@@ -676,7 +682,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
         // until the rows cover every wave (a C5 batch's ~186k rows would
         // otherwise be 2,900 tiles for 4,096 waves, the hot ones long)
         a.n = *a.d_n;
-        while (a.tile_topics > 1 && (a.n + a.tile_topics - 1) / a.tile_topics < gridDim.x) a.tile_topics >>= 1;
+        while (a.tile_topics > 1 && (a.n + a.tile_topics - 1) / a.tile_topics < DN_TILES_PER_WAVE * gridDim.x)
+            a.tile_topics >>= 1;
+        // the host sized the static share for every publish: the rows take
+        // half of their own tiles round-robin, the rest by tickets (a skewed
+        // batch's hot rows come first, in the first tiles)
+        const uint32_t nt = (a.n + a.tile_topics - 1) / a.tile_topics;
+        a.static_rounds = max(1u, nt / (2u * gridDim.x));
     }
     const uint32_t lane = threadIdx.x;
     const uint32_t tt = a.tile_topics;   // topics per tile: 64, or fewer for small batches
