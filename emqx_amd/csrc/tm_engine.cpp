@@ -728,6 +728,7 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     if (!e || !offsets || (!filters && n)) return TM_EINVAL;
     if (nshards > 1 && shard >= nshards) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
+    WorkPool::Linger linger(e->pool);   // (the workers spin between this call's phases)
     uint64_t done = 0;
     int rc = TM_OK;
     for (uint32_t i = 0; i < n; ++i)
@@ -776,6 +777,7 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
                         uint64_t* n_deleted) {
     if (!e || !offsets || (!filters && n)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
+    WorkPool::Linger linger(e->pool);   // (the workers spin between this call's phases)
     uint64_t done = 0;
     int rc = TM_OK;
     for (uint32_t i = 0; i < n; ++i)
@@ -812,6 +814,7 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
     if (n_inserted) *n_inserted = 0;
     if (!e || !del_offsets || !ins_offsets || (!del_filters && n_del) || (!ins_filters && n_ins)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
+    WorkPool::Linger linger(e->pool);   // (the workers spin between this call's phases)
     for (uint32_t i = 0; i < n_del; ++i)
         if (del_offsets[i + 1] < del_offsets[i]) return TM_EINVAL;
     for (uint32_t i = 0; i < n_ins; ++i)

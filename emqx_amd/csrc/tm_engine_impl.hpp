@@ -836,13 +836,27 @@ struct WorkPool {
     static long futex(std::atomic<uint32_t>* a, int op, uint32_t v) {
         return syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), op | FUTEX_PRIVATE_FLAG, v, nullptr, nullptr, 0);
     }
-    static bool spin_until_changed(const std::atomic<uint32_t>& a, uint32_t v) {
-        for (int i = 0; i < 2048; ++i) {
+    // How long an idle worker (or the caller waiting for them) spins before
+    // it sleeps on the futex.  Short by default: the box runs under a CFS CPU
+    // quota, where spinning threads would burn it.  A bulk mutation raises it
+    // for its duration (Linger): its phases follow each other within tens of
+    // µs, and a futex wake-up per phase and worker cost ~25 µs each (C5 K = 10
+    // churn 2.6 -> 1.8 ms on the box); the limit is re-read while spinning,
+    // so the workers sleep soon after the mutation ends.
+    static constexpr int SPIN_IDLE = 2048, SPIN_LINGER = 1 << 16;
+    std::atomic<int> spin_limit{SPIN_IDLE};
+    bool spin_until_changed(const std::atomic<uint32_t>& a, uint32_t v) const {
+        for (int i = 0;; ++i) {
             if (a.load(std::memory_order_acquire) != v) return true;
+            if ((i & 255) == 0 && i >= spin_limit.load(std::memory_order_relaxed)) return false;
             __builtin_ia32_pause();
         }
-        return false;
     }
+    struct Linger {   // scope of a bulk mutation
+        WorkPool& p;
+        explicit Linger(WorkPool& q) : p(q) { p.spin_limit.store(SPIN_LINGER, std::memory_order_relaxed); }
+        ~Linger() { p.spin_limit.store(SPIN_IDLE, std::memory_order_relaxed); }
+    };
     // `cpus` (may be null): the CPUs the workers run on
     void start(unsigned k, const cpu_set_t* cpus) {
         n = std::max(1u, k);

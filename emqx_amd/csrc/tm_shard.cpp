@@ -649,6 +649,12 @@ int tm_sharded_create(const int32_t* devices, uint32_t n, const tm_config* cfg, 
     for (uint32_t i = 0; i < n; ++i) {
         tm_config c = cfg ? *cfg : tm_config{0, 0, 0, 0};
         c.device = devices[i];
+        // the shards mutate in parallel (each()): their host workers share the
+        // process's CPUs instead of 16 per shard
+        if (!c.host_threads && n > 1) {
+            const unsigned hw = std::thread::hardware_concurrency();
+            c.host_threads = std::max(1u, std::min(hw ? hw : 1u, 16u) / n);
+        }
         c.flags = (c.flags | TM_CFG_FROZEN_DICT) & ~TM_CFG_HOST_TOKENIZE;   // ids agree across shards
         tm_engine* e = nullptr;
         int rc = tm_create(&c, &e);
