@@ -1368,6 +1368,9 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_tiles(FanArgs a, uint64_t nt
 // copy is then one LDS read + one subscriber load + one coalesced store per
 // delivery.  A tile covering more than FAN_LDS_ENTRIES entries (long stretches
 // of filters without local subscribers) searches moff per delivery instead.
+// WIDE: the batch delivers more than big_limit (some scan block may hold u64
+// offsets); otherwise only the 32-bit staging path is compiled in
+template <bool WIDE>
 __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
     __shared__ int64_t base[FAN_LDS_ENTRIES];
     __shared__ __attribute__((aligned(16))) uint16_t own[FAN_FILL_TILE];
@@ -1419,6 +1422,43 @@ __global__ __launch_bounds__(FAN_BLOCK) void tm_fan_fill(FanArgs a) {
 #define TM_FAN_STG 8
 #endif
     constexpr uint32_t FAN_STG = TM_FAN_STG;
+    if (!WIDE || (!big0 && !big1)) {
+        // both scan blocks of the tile's entries hold u32 offsets (the common
+        // case): the loads stay 32-bit until the gathers are issued
+        for (uint32_t e0 = t; e0 < (uint32_t)ne; e0 += FAN_BLOCK * FAN_STG) {
+            uint32_t r0[FAN_STG], r1[FAN_STG], f[FAN_STG];
+#pragma unroll
+            for (uint32_t u = 0; u < FAN_STG; ++u) {
+                const uint32_t e = e0 + u * FAN_BLOCK;
+                r0[u] = 0; r1[u] = 0; f[u] = 0;
+                if (e < (uint32_t)ne) {
+                    const uint64_t j = jlo + e;
+                    r0[u] = a.moff32[j];
+                    r1[u] = a.moff32[j + 1];
+                    f[u] = one_reg ? fids[j] : fan_fid(a, j);
+                }
+            }
+            int64_t v[FAN_STG];
+            uint32_t at[FAN_STG];   // my mark's place in own[], NONE: inactive
+#pragma unroll
+            for (uint32_t u = 0; u < FAN_STG; ++u) {
+                const uint64_t j = jlo + e0 + u * FAN_BLOCK;
+                const uint64_t m0 = r0[u] + (j / FAN_SCAN_TILE != sb0 ? bs1 : bs0);
+                const uint64_t m1 = r1[u] + ((j + 1) / FAN_SCAN_TILE != sb0 ? bs1 : bs0);
+                const bool act = e0 + u * FAN_BLOCK < (uint32_t)ne && m1 > m0 && m1 > start && m0 < end;
+                v[u] = 0;
+                at[u] = act ? (m0 > start ? (uint32_t)(m0 - start) : 0u) : NONE;
+                if (act) v[u] = m1 - m0 == 1 ? INT64_MIN + (int64_t)a.sone[f[u]] : (int64_t)a.soff[f[u]] - (int64_t)m0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < FAN_STG; ++u) {
+                if (at[u] == NONE) continue;
+                const uint32_t e = e0 + u * FAN_BLOCK;
+                base[e] = v[u];
+                own[at[u]] = (uint16_t)(e + 1);
+            }
+        }
+    } else
     for (uint32_t e0 = t; e0 < (uint32_t)ne; e0 += FAN_BLOCK * FAN_STG) {
         uint64_t m0[FAN_STG], m1[FAN_STG];
         uint32_t f[FAN_STG];
@@ -2770,7 +2810,8 @@ hipError_t launch_fan_fill(const FanArgs& a, hipStream_t s) {
         const uint64_t nt = (a.total + FAN_FILL_TILE - 1) / FAN_FILL_TILE;
         hipLaunchKernelGGL(tm_fan_tiles, dim3((uint32_t)((nt + 1 + FAN_BLOCK - 1) / FAN_BLOCK)), dim3(FAN_BLOCK), 0, s,
                            a, nt);
-        hipLaunchKernelGGL(tm_fan_fill, dim3((uint32_t)nt), dim3(FAN_BLOCK), 0, s, a);
+        if (a.total > a.big_limit) hipLaunchKernelGGL(tm_fan_fill<true>, dim3((uint32_t)nt), dim3(FAN_BLOCK), 0, s, a);
+        else hipLaunchKernelGGL(tm_fan_fill<false>, dim3((uint32_t)nt), dim3(FAN_BLOCK), 0, s, a);
     }
     return hipGetLastError();
 }
