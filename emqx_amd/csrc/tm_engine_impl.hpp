@@ -726,13 +726,8 @@ struct Replica {
     uint8_t* d_fbytes = nullptr;
     size_t c_fbytes = 0;
     uint64_t fbytes_uploaded = 0;
-    uint32_t* d_didx = nullptr;
-    Slot* d_dval = nullptr;
-    size_t cd_didx = 0, cd_dval = 0;
-    uint32_t* d_fidx = nullptr;
-    uint64_t* d_foffv = nullptr;
-    uint32_t* d_flenv = nullptr;
-    size_t cd_fidx = 0, cd_foffv = 0, cd_flenv = 0;
+    uint8_t* d_dblob = nullptr;   // the engine's delta blob (h_dblob), uploaded in one copy
+    size_t cd_dblob = 0;
     // word dictionary mirror (device tokeniser): cuckoo key table, tails, arena
     DictKey* d_dkey = nullptr;
     size_t d_dict_n = 0;            // cuckoo slots on the device
@@ -838,24 +833,33 @@ struct WorkPool {
     }
     // How long an idle worker (or the caller waiting for them) spins before
     // it sleeps on the futex.  Short by default: the box runs under a CFS CPU
-    // quota, where spinning threads would burn it.  A bulk mutation raises it
-    // for its duration (Linger): its phases follow each other within tens of
-    // µs, and a futex wake-up per phase and worker cost ~25 µs each (C5 K = 10
-    // churn 2.6 -> 1.8 ms on the box); the limit is re-read while spinning,
-    // so the workers sleep soon after the mutation ends.
-    static constexpr int SPIN_IDLE = 2048, SPIN_LINGER = 1 << 16;
-    std::atomic<int> spin_limit{SPIN_IDLE};
+    // quota, where spinning threads would burn it.  A bulk mutation keeps
+    // them spinning for its duration and a short grace after (Linger): its
+    // phases follow each other within tens of µs, and a futex wake-up per
+    // phase and worker cost ~25 µs each (host-only K = 10 churn 1.97 -> 1.71
+    // ms on the box); the deadline is re-read while spinning, so the workers
+    // sleep soon after the grace.
+    // (the grace after a mutation covers the delta gather that usually
+    // follows it, tm_sync_async: its fork-joins find the workers awake)
+    static constexpr int SPIN_IDLE = 2048;
+    static constexpr int64_t GRACE_NS = 150000;
+    std::atomic<int64_t> linger_until{0};   // steady-clock ns; INT64_MAX inside a mutation
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     bool spin_until_changed(const std::atomic<uint32_t>& a, uint32_t v) const {
         for (int i = 0;; ++i) {
             if (a.load(std::memory_order_acquire) != v) return true;
-            if ((i & 255) == 0 && i >= spin_limit.load(std::memory_order_relaxed)) return false;
+            if ((i & 255) == 0 && i >= SPIN_IDLE && now_ns() > linger_until.load(std::memory_order_relaxed))
+                return false;
             __builtin_ia32_pause();
         }
     }
     struct Linger {   // scope of a bulk mutation
         WorkPool& p;
-        explicit Linger(WorkPool& q) : p(q) { p.spin_limit.store(SPIN_LINGER, std::memory_order_relaxed); }
-        ~Linger() { p.spin_limit.store(SPIN_IDLE, std::memory_order_relaxed); }
+        explicit Linger(WorkPool& q) : p(q) { p.linger_until.store(INT64_MAX, std::memory_order_relaxed); }
+        ~Linger() { p.linger_until.store(now_ns() + GRACE_NS, std::memory_order_relaxed); }
     };
     // `cpus` (may be null): the CPUs the workers run on
     void start(unsigned k, const cpu_set_t* cpus) {
@@ -1061,13 +1065,17 @@ struct tm_engine {
     bool full_dirty = true;
     bool full_f_dirty = true;
     // delta staging in pinned host memory, filled once per upload and copied to every replica
+    // the gathered slot and filter-metadata deltas: one pinned blob, so a
+    // replica's delta upload is one copy (six used to cost ~0.1 ms of device
+    // time per upload in H2D setup gaps); the arrays point into it
+    uint8_t* h_dblob = nullptr;
+    size_t ch_dblob = 0, blob_bytes = 0;
+    size_t blob_off[5] = {0, 0, 0, 0, 0};   // didx | dval | fidx | foffv | flenv
     uint32_t* h_didx = nullptr;
     Slot* h_dval = nullptr;
-    size_t ch_didx = 0, ch_dval = 0;
     uint32_t* h_fidx = nullptr;
     uint64_t* h_foffv = nullptr;
     uint32_t* h_flenv = nullptr;
-    size_t ch_fidx = 0, ch_foffv = 0, ch_flenv = 0;
     uint32_t* h_dxidx = nullptr;
     DictKey* h_dxval = nullptr;
     size_t ch_dxidx = 0, ch_dxval = 0;

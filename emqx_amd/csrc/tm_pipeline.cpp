@@ -57,7 +57,7 @@ void tm_engine::destroy() {
         R->tokb.release();
         dev_free(R->d_slots); dev_free(R->d_foff); dev_free(R->d_flen); dev_free(R->d_fbytes);
         dev_free(R->d_dkey); dev_free(R->d_tail); dev_free(R->d_arena); dev_free(R->d_dxidx); dev_free(R->d_dxval);
-        dev_free(R->d_didx); dev_free(R->d_dval); dev_free(R->d_fidx); dev_free(R->d_foffv); dev_free(R->d_flenv);
+        dev_free(R->d_dblob);
         dev_free(R->d_dbg); dev_free(R->d_roff); dev_free(R->d_rdest); dev_free(R->d_rl);
         dev_free(R->d_soff); dev_free(R->d_subs); dev_free(R->d_scnt); dev_free(R->d_sone);
         if (R->h_dbg) (void)hipHostFree(R->h_dbg);
@@ -68,11 +68,10 @@ void tm_engine::destroy() {
         delete R;
     }
     reps.clear();
-    for (void* h : {(void*)h_dxidx, (void*)h_dxval, (void*)h_didx, (void*)h_dval, (void*)h_fidx, (void*)h_foffv,
-                    (void*)h_flenv})
+    for (void* h : {(void*)h_dxidx, (void*)h_dxval, (void*)h_dblob})
         if (h) (void)hipHostFree(h);
-    h_dxidx = nullptr; h_dxval = nullptr; h_didx = nullptr; h_dval = nullptr;
-    h_fidx = nullptr; h_foffv = nullptr; h_flenv = nullptr;
+    h_dxidx = nullptr; h_dxval = nullptr; h_dblob = nullptr;
+    h_didx = nullptr; h_dval = nullptr; h_fidx = nullptr; h_foffv = nullptr; h_flenv = nullptr;
 }
 
 int tm_engine::run_slices(const uint8_t* topics, const uint64_t* offsets, uint32_t n) {

@@ -43,27 +43,44 @@ int tm_engine::sync_device(const Replica* back) {
     const size_t nn = nd.size();
     // gather the deltas once
     const bool slots_full = full_dirty || dirty.size() > slots.size() / 8;
+    {   // the blob's layout: the slot deltas, then the filter-metadata deltas
+        const size_t k1 = (!slots_full && !dirty.empty()) ? dirty.size() : 0;
+        const size_t k2 = (!full_f_dirty && !dirty_f.empty()) ? dirty_f.size() : 0;
+        auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+        blob_off[0] = 0;
+        blob_off[1] = al(k1 * sizeof(uint32_t));
+        blob_off[2] = blob_off[1] + al(k1 * sizeof(Slot));
+        blob_off[3] = blob_off[2] + al(k2 * sizeof(uint32_t));
+        blob_off[4] = blob_off[3] + al(k2 * sizeof(uint64_t));
+        blob_bytes = blob_off[4] + al(k2 * sizeof(uint32_t));
+        if (blob_bytes && (rc = host_reserve(h_dblob, ch_dblob, blob_bytes))) return rc;
+        h_didx = reinterpret_cast<uint32_t*>(h_dblob + blob_off[0]);
+        h_dval = reinterpret_cast<Slot*>(h_dblob + blob_off[1]);
+        h_fidx = reinterpret_cast<uint32_t*>(h_dblob + blob_off[2]);
+        h_foffv = reinterpret_cast<uint64_t*>(h_dblob + blob_off[3]);
+        h_flenv = reinterpret_cast<uint32_t*>(h_dblob + blob_off[4]);
+    }
     if (!slots_full && !dirty.empty()) {
         const size_t k = dirty.size();
-        if ((rc = host_reserve(h_didx, ch_didx, k))) return rc;
-        if ((rc = host_reserve(h_dval, ch_dval, k))) return rc;
         par_chunks(k, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; ++i) {
                 if (i + 16 < i1) __builtin_prefetch(&slots[dirty[i + 16]]);
-                h_didx[i] = dirty[i];
-                h_dval[i] = slots[dirty[i]];
+                const uint32_t d = dirty[i];
+                h_didx[i] = d;
+                h_dval[i] = slots[d];
+                // the set is consumed here (every set bit is in `dirty`; words
+                // shared by two entries are cleared twice, to the same 0)
+                __atomic_store_n(&dirty_mark[d >> 6], 0ull, __ATOMIC_RELAXED);
             }
         });
     }
     if (!full_f_dirty && !dirty_f.empty()) {
         const size_t k = dirty_f.size();
-        if ((rc = host_reserve(h_fidx, ch_fidx, k))) return rc;
-        if ((rc = host_reserve(h_foffv, ch_foffv, k))) return rc;
-        if ((rc = host_reserve(h_flenv, ch_flenv, k))) return rc;
         par_chunks(k, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; ++i) {
                 const uint32_t c = dirty_f[i];
                 h_fidx[i] = c; h_foffv[i] = n_foff[c]; h_flenv[i] = n_flen[c];
+                dirty_f_mark[c] = 0;   // (each node is listed once)
             }
         });
     }
@@ -90,19 +107,16 @@ int tm_engine::sync_device(const Replica* back) {
         async[r] = as;
     }
     // the dirty sets are consumed: every replica has them now
+    // (the delta gathers above cleared their marks on the workers)
     if (slots_full) {
         full_dirty = false;
         for (uint32_t i : dirty) dirty_mark[i >> 6] = 0;   // every set bit is in `dirty`
         if (dirty_mark.size() != (slots.size() + 63) / 64) dirty_mark.assign((slots.size() + 63) / 64, 0);
-    } else {
-        for (uint32_t i : dirty) dirty_mark[i >> 6] = 0;
     }
     dirty.clear();
     if (full_f_dirty) {
         full_f_dirty = false;
         dirty_f_mark.assign(nn, 0);
-    } else {
-        for (uint32_t c : dirty_f) dirty_f_mark[c] = 0;
     }
     dirty_f.clear();
     if (dev_tok) dx.clear();
@@ -146,6 +160,12 @@ int tm_engine::upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn,
             HIP_OK(hipEventRecord(r->ev_read, r->own));
             HIP_OK(hipStreamWaitEvent(stream, r->ev_read, 0));
         }
+    // the delta blob, in one copy (the scatters below read their parts)
+    if (blob_bytes) {
+        if ((rc = dev_reserve(R.d_dblob, R.cd_dblob, blob_bytes))) return rc;
+        HIP_OK(hipMemcpyAsync(R.d_dblob, h_dblob, blob_bytes, hipMemcpyHostToDevice, stream));
+        async_used = true;
+    }
     // edge hash
     bool full = slots_full;
     if (R.d_nslots != slots.size()) {
@@ -160,11 +180,8 @@ int tm_engine::upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn,
         ++uploads_full;
     } else if (!dirty.empty()) {
         const size_t k = dirty.size();
-        if ((rc = dev_reserve(R.d_didx, R.cd_didx, k))) return rc;
-        if ((rc = dev_reserve(R.d_dval, R.cd_dval, k))) return rc;
-        HIP_OK(hipMemcpyAsync(R.d_didx, h_didx, k * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(R.d_dval, h_dval, k * sizeof(Slot), hipMemcpyHostToDevice, stream));
-        HIP_OK(launch_scatter_slots(R.d_slots, R.d_didx, R.d_dval, (uint32_t)k, stream));
+        HIP_OK(launch_scatter_slots(R.d_slots, reinterpret_cast<const uint32_t*>(R.d_dblob + blob_off[0]),
+                                    reinterpret_cast<const Slot*>(R.d_dblob + blob_off[1]), (uint32_t)k, stream));
         ++uploads_delta;
         delta_slots += k;
         async_used = true;
@@ -220,13 +237,9 @@ int tm_engine::upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn,
         HIP_OK(hipMemcpyAsync(R.d_flen, n_flen.data(), nn * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
     } else if (!dirty_f.empty()) {
         const size_t k = dirty_f.size();
-        if ((rc = dev_reserve(R.d_fidx, R.cd_fidx, k))) return rc;
-        if ((rc = dev_reserve(R.d_foffv, R.cd_foffv, k))) return rc;
-        if ((rc = dev_reserve(R.d_flenv, R.cd_flenv, k))) return rc;
-        HIP_OK(hipMemcpyAsync(R.d_fidx, h_fidx, k * 4, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(R.d_foffv, h_foffv, k * 8, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(R.d_flenv, h_flenv, k * 4, hipMemcpyHostToDevice, stream));
-        HIP_OK(launch_scatter_fmeta(R.d_foff, R.d_flen, R.d_fidx, R.d_foffv, R.d_flenv, (uint32_t)k, stream));
+        HIP_OK(launch_scatter_fmeta(R.d_foff, R.d_flen, reinterpret_cast<const uint32_t*>(R.d_dblob + blob_off[2]),
+                                    reinterpret_cast<const uint64_t*>(R.d_dblob + blob_off[3]),
+                                    reinterpret_cast<const uint32_t*>(R.d_dblob + blob_off[4]), (uint32_t)k, stream));
         async_used = true;
     }
     if (dev_tok && (rc = sync_dict(R, keys_full, pageable_used, async_used, h2d_tail))) return rc;
