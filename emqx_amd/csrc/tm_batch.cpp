@@ -583,17 +583,18 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     b->dedup_timed = dedup_now && csr;
     const bool graph = csr && !checked && !tokenize_now && use_graphs && !b->gbad && b->n <= GRAPH_MAX &&
                        !b->dedup_dev;
-    if (!tokenize_now && !graph) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // ctrl + stats
+    // a fresh device-deduplicated batch (C5: every launch) replays its whole
+    // sequence -- dedup, tokeniser, walk, expand, read-back -- as one captured
+    // graph: ~25 enqueues cost ~0.2 ms of host time per launch otherwise
+    const bool fuse = tokenize_now && !checked && !b->dedup_dev && fresh_fused;
+    const bool dgraph = csr && !checked && use_graphs && !b->gbad && b->dedup_dev && dedup_now && tokenize_now &&
+                        !b->check_tokens;
     b->tok_timed = tokenize_now && csr;
     if (dedup_now) {
-        if (b->dedup_timed) HIP_OK(hipEventRecord(b->evd, S));
-        if ((rc = enqueue_dedup(b, S))) return rc;
         b->dedup_stale = false;
         b->rowof_host = false;
     }
-    if (b->tok_timed) HIP_OK(hipEventRecord(b->evt, S));
-    // a fresh batch's tokeniser fill runs inside the walk (tm_match_fresh)
-    const bool fuse = tokenize_now && !checked && !b->dedup_dev && fresh_fused;
+    // (a fresh batch's tokeniser fill runs inside the walk when fused: tm_match_fresh)
     TokArgs t{};
     ScanArgs ts{};
     if (tokenize_now) {
@@ -613,11 +614,6 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         // fused: one tile for both (any tile size is a valid walk tile)
         if (fuse) t.tile_topics = std::min(t.tile_topics, tile_topics(b->n));
         ts.block_sums = b->d_bsums;
-        if (!fuse) HIP_OK(launch_tokenize(t, ts, b->d_nslow + 1, S));
-    }
-    if (b->check_tokens && b->n) {
-        HIP_OK(hipMemsetAsync(b->d_nslow, 0, 2 * 4, S));
-        HIP_OK(launch_token_check(b->d_toff, b->d_tflags, b->n, b->nwords, b->d_slow, b->d_nslow, b->d_nslow + 1, S));
     }
     MatchArgs a{};
     a.slots = R.d_slots;
@@ -657,8 +653,10 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;
     a.nwords = (uint32_t)std::max<uint64_t>(b->nwords, 1);
     a.nslots = (uint32_t)slots.size();
-    a.nnodes = (uint32_t)nd.size();
-    a.nfbytes = fbytes.size();
+    // (bounds of the checked build only: left 0 otherwise, so churn does not
+    // change the launch's arguments and a captured graph stays valid)
+    a.nnodes = checked ? (uint32_t)nd.size() : 0u;
+    a.nfbytes = checked ? fbytes.size() : 0u;
     a.dbg = checked ? R.d_dbg : nullptr;
     ScanArgs s{};
     s.count = b->d_count; s.src = b->d_src;
@@ -668,19 +666,88 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     s.dbg = checked ? R.d_dbg : nullptr;
     b->end_recorded = false;
     b->dense_enq = false;
+    // Everything the launch puts on the stream (xf: hipEventRecordExternal
+    // while a graph is captured, so that replays re-record the timing events;
+    // csr_too: the read-back of ctrl + stats as well)
+    auto enqueue = [&](unsigned xf, bool csr_too) -> hipError_t {
+        hipError_t e;
+        if (!tokenize_now && (e = hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S)) != hipSuccess) return e;
+        if (dedup_now) {
+            if (b->dedup_timed && (e = hipEventRecordWithFlags(b->evd, S, xf)) != hipSuccess) return e;
+            if (enqueue_dedup(b, S) != TM_OK) return hipErrorUnknown;
+        }
+        if (b->tok_timed && (e = hipEventRecordWithFlags(b->evt, S, xf)) != hipSuccess) return e;
+        if (tokenize_now && !fuse && (e = launch_tokenize(t, ts, b->d_nslow + 1, S)) != hipSuccess) return e;
+        if (b->check_tokens && b->n) {
+            if ((e = hipMemsetAsync(b->d_nslow, 0, 2 * 4, S)) != hipSuccess) return e;
+            if ((e = launch_token_check(b->d_toff, b->d_tflags, b->n, b->nwords, b->d_slow, b->d_nslow,
+                                        b->d_nslow + 1, S)) != hipSuccess)
+                return e;
+        }
+        if (fuse)
+            e = launch_match_fresh(a, t, ts, b->d_nslow + 1, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr);
+        else
+            e = launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked, xf);
+        if (e != hipSuccess) return e;
+        if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
+            if ((e = hipEventRecordWithFlags(b->evx0, S, xf)) != hipSuccess) return e;
+            if ((e = launch_dedup_expand(dedup_args(b), S)) != hipSuccess) return e;
+            if ((e = hipEventRecordWithFlags(b->evx1, S, xf)) != hipSuccess) return e;
+        }
+        return csr_too ? enqueue_csr(b, s, S, xf) : hipSuccess;
+    };
     int grc = 1;
-    if (graph) {
+    if (graph) {   // a repeated tokenised batch: memset + walk + read-back replayed
         grc = launch_graph(b, a, s, S);
         if (grc != 1 && grc) return grc;
-        if (grc == 1) HIP_OK(hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S));   // capture refused: the direct way
     }
-    if (grc == 1 && fuse) HIP_OK(launch_match_fresh(a, t, ts, b->d_nslow + 1, S, csr ? b->ev0 : nullptr,
-                                                    csr ? b->ev1 : nullptr));
-    else if (grc == 1) HIP_OK(launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked));
-    if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
-        HIP_OK(hipEventRecord(b->evx0, S));
-        HIP_OK(launch_dedup_expand(dedup_args(b), S));
-        HIP_OK(hipEventRecord(b->evx1, S));
+    bool csr_done = false;
+    if (dgraph) {
+        const DedupArgs d = dedup_args(b);
+        std::vector<uint8_t> key(sizeof t + sizeof ts + sizeof a + sizeof s + sizeof d);
+        uint8_t* k = key.data();
+        memcpy(k, &t, sizeof t); k += sizeof t;
+        memcpy(k, &ts, sizeof ts); k += sizeof ts;
+        memcpy(k, &a, sizeof a); k += sizeof a;
+        memcpy(k, &s, sizeof s); k += sizeof s;
+        memcpy(k, &d, sizeof d);
+        if (b->gexec && b->gkey == key) {
+            HIP_OK(hipGraphLaunch(b->gexec, S));
+            grc = 0;
+        } else {
+            if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
+            b->gexec = nullptr;
+            if (b->gkey == key) {   // the second launch with these arguments: capture them
+                hipGraph_t g = nullptr;
+                if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) == hipSuccess) {
+                    const hipError_t e = enqueue(hipEventRecordExternal, true);
+                    const hipError_t e2 = hipStreamEndCapture(S, &g);
+                    if (e == hipSuccess && e2 == hipSuccess && g &&
+                        hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
+                        (void)hipGraphDestroy(g);
+                        HIP_OK(hipGraphLaunch(b->gexec, S));
+                        grc = 0;
+                    } else {
+                        if (g) (void)hipGraphDestroy(g);
+                        (void)hipGetLastError();
+                        b->gexec = nullptr;
+                        b->gbad = true;   // the direct way from now on
+                    }
+                } else {
+                    (void)hipGetLastError();
+                    b->gbad = true;
+                }
+            }
+            b->gkey.swap(key);
+        }
+        csr_done = grc == 0;
+    }
+    if (grc == 1) {
+        const hipError_t e = enqueue(0u, false);
+        if (e != hipSuccess) {
+            snprintf(last_error(), 512, "%s at launch (%s)", hipGetErrorString(e), __FILE_NAME__);
+            return TM_EIO;
+        }
     }
     note_launch(b);
     b->launched = true;
@@ -688,7 +755,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     b->dense = false;
     b->csr = csr;
     if (!csr) return TM_OK;   // the async slot enqueues its read-back and event
-    if (grc == 1) HIP_OK(enqueue_csr(b, s, S));   // (the graph holds it)
+    if (grc == 1 && !csr_done) HIP_OK(enqueue_csr(b, s, S));   // (a graph holds it)
     b->scan_args = s;
     if (b->check_tokens) HIP_OK(hipMemcpyAsync(b->h_bad, b->d_nslow, 2 * 4, hipMemcpyDeviceToHost, S));
     if (checked) HIP_OK(hipMemcpyAsync(R.h_dbg, R.d_dbg, 8 * 4, hipMemcpyDeviceToHost, S));
