@@ -590,10 +590,6 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     const bool dgraph = csr && !checked && use_graphs && !b->gbad && b->dedup_dev && dedup_now && tokenize_now &&
                         !b->check_tokens;
     b->tok_timed = tokenize_now && csr;
-    if (dedup_now) {
-        b->dedup_stale = false;
-        b->rowof_host = false;
-    }
     // (a fresh batch's tokeniser fill runs inside the walk when fused: tm_match_fresh)
     TokArgs t{};
     ScanArgs ts{};
@@ -748,6 +744,10 @@ int tm_engine::launch(tm_batch* b, bool csr) {
             snprintf(last_error(), 512, "%s at launch (%s)", hipGetErrorString(e), __FILE_NAME__);
             return TM_EIO;
         }
+    }
+    if (dedup_now) {   // (enqueued: a failed launch dedups again next time)
+        b->dedup_stale = false;
+        b->rowof_host = false;
     }
     note_launch(b);
     b->launched = true;
