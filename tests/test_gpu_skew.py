@@ -97,3 +97,44 @@ def test_churn_applied_while_the_device_walks():
         b.launch()                                         # sees the deltas applied above
     b.wait()
     b.free()
+
+
+def test_fresh_dedup_batches_replay_through_churn():
+    """A fresh deduplicated batch every step (the C5 leg: retokenize().launch()):
+    from the third launch on, the launch replays a captured graph (dedup,
+    tokeniser, walk, expand).  The trie changes between launches, and every
+    launch must equal the oracle on its own snapshot -- the replay must not keep
+    stale trie arguments."""
+    p = gen.SkewParams(seed=11, n_hot=100, k_per_hot=40)
+    allf, derived, hot, pubs = workload(p, 2000, 30_000, seed=11, background_pool=4000)
+    background = allf.tolist()[len(derived):]
+    eng = Engine(device=0)
+    eng.insert_many(allf)
+    churn = Churn(hot, derived.tolist(), seed=5)
+    b = eng.prepare(pubs, dedup=True)
+    T = pubs.tolist()
+    for rnd in range(6):
+        dels, adds = churn.step(500)
+        Churn.apply(eng, gen.Strings.from_list(dels), gen.Strings.from_list(adds))
+        snapshot = sorted(churn.live_set) + background
+        b.retokenize().launch().wait()
+        st = b.stats()
+        assert st["publishes"] == len(T) and st["ms_dedup"] > 0.0
+        row_of, n_rows = b.row_map()
+        distinct = {}
+        for i, r in enumerate(row_of.tolist()):
+            distinct.setdefault(r, T[i])
+        Td = [distinct[r] for r in range(n_rows)]
+        offs, ids = b.result()
+        got = [[eng.filter_bytes(int(x)) for x in ids[offs[r]:offs[r + 1]]] for r in range(n_rows)]
+        orc = P.Oracle()
+        for f in snapshot:
+            orc.register(f)
+            orc.insert(f)
+        buf, o = P.pack(Td)
+        counts, idx, _ = orc.match_batch(buf, o, nthreads=8)
+        cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+        for r in range(n_rows):
+            assert got[r] == [snapshot[int(j)] for j in idx[cut[r]:cut[r + 1]]], (rnd, Td[r][:60])
+        orc.close()
+    b.free()
