@@ -548,6 +548,10 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         "delivered_matches_per_step": int(np.mean(delivered)),
         "generic_path_topics": int(st["slow_topics"]),
         "uploads_delta": eng.stats()["uploads_delta"],
+        # launches replayed as a captured HIP graph (from each batch's second
+        # launch on): a replay times only its whole span, reported as its walk,
+        # so the phase means above mix the direct launches' split with that
+        "graph_launches": eng.stats()["graph_launches"],
     }
     for b in bs:
         b.free()
@@ -592,6 +596,7 @@ def run_c5(args, ws, rank, local, sync):
         "delivered_matches_per_step": leg["delivered_matches_per_step"],
         "generic_path_topics": leg["generic_path_topics"],
         "uploads_delta": leg["uploads_delta"],
+        "graph_launches": leg["graph_launches"],
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -91,7 +91,8 @@ class BatchStats(C.Structure):
 
 class EngineStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("version", "nodes", "edges", "filters", "words", "slots",
-                                          "device_bytes", "uploads_full", "uploads_delta", "delta_slots")]
+                                          "device_bytes", "uploads_full", "uploads_delta", "delta_slots",
+                                          "graph_launches")]
 
     def asdict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

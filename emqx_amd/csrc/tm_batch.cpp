@@ -551,6 +551,20 @@ int tm_engine::upload_packed(tm_batch* b, const uint8_t* blk, uint32_t n, uint64
     return tokens_pending(b);
 }
 
+// A captured deduplicated batch replayed: its timing events are recorded on
+// the stream around the graph (an event record inside that capture is refused
+// by the runtime), so the replay's whole span is its walk time.
+hipError_t tm_engine::graph_replay(tm_batch* b, hipStream_t S) {
+    hipError_t e;
+    if (b->dedup_timed && (e = hipEventRecord(b->evd, S)) != hipSuccess) return e;
+    if ((e = hipEventRecord(b->ev0, S)) != hipSuccess) return e;
+    if ((e = hipGraphLaunch(b->gexec, S)) != hipSuccess) return e;
+    if ((e = hipEventRecord(b->ev1, S)) != hipSuccess) return e;
+    if ((e = hipEventRecord(b->ev2, S)) != hipSuccess) return e;
+    ++graph_launches;
+    return hipSuccess;
+}
+
 int tm_engine::launch(tm_batch* b, bool csr) {
     if (reps.empty()) return TM_ENODEV;
     int rc;
@@ -661,18 +675,20 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     s.n = b->n; s.ids_cap = (uint32_t)std::min<size_t>(b->c_ids, 0xFFFFFFF0ull); s.ctrl = b->d_ctrl;
     s.dbg = checked ? R.d_dbg : nullptr;
     b->end_recorded = false;
+    b->graphed = false;
     b->dense_enq = false;
-    // Everything the launch puts on the stream (xf: hipEventRecordExternal
-    // while a graph is captured, so that replays re-record the timing events;
-    // csr_too: the read-back of ctrl + stats as well)
-    auto enqueue = [&](unsigned xf, bool csr_too) -> hipError_t {
+    // Everything the launch puts on the stream (cap: captured into a graph,
+    // without the timing events -- the runtime refuses event records inside this
+    // capture, so graph_replay records them around the whole graph; csr_too:
+    // the read-back of ctrl + stats as well)
+    auto enqueue = [&](bool cap, bool csr_too) -> hipError_t {
         hipError_t e;
         if (!tokenize_now && (e = hipMemsetAsync(b->d_hdr, 0, tm_batch::HDR_FIXED, S)) != hipSuccess) return e;
         if (dedup_now) {
-            if (b->dedup_timed && (e = hipEventRecordWithFlags(b->evd, S, xf)) != hipSuccess) return e;
+            if (b->dedup_timed && !cap && (e = hipEventRecord(b->evd, S)) != hipSuccess) return e;
             if (enqueue_dedup(b, S) != TM_OK) return hipErrorUnknown;
         }
-        if (b->tok_timed && (e = hipEventRecordWithFlags(b->evt, S, xf)) != hipSuccess) return e;
+        if (b->tok_timed && !cap && (e = hipEventRecord(b->evt, S)) != hipSuccess) return e;
         if (tokenize_now && !fuse && (e = launch_tokenize(t, ts, b->d_nslow + 1, S)) != hipSuccess) return e;
         if (b->check_tokens && b->n) {
             if ((e = hipMemsetAsync(b->d_nslow, 0, 2 * 4, S)) != hipSuccess) return e;
@@ -683,14 +699,16 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         if (fuse)
             e = launch_match_fresh(a, t, ts, b->d_nslow + 1, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr);
         else
-            e = launch_match(a, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr, checked, xf);
+            e = launch_match(a, S, csr && !cap ? b->ev0 : nullptr, csr && !cap ? b->ev1 : nullptr, checked, 0u);
         if (e != hipSuccess) return e;
         if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
-            if ((e = hipEventRecordWithFlags(b->evx0, S, xf)) != hipSuccess) return e;
+            if (!cap && (e = hipEventRecord(b->evx0, S)) != hipSuccess) return e;
             if ((e = launch_dedup_expand(dedup_args(b), S)) != hipSuccess) return e;
-            if ((e = hipEventRecordWithFlags(b->evx1, S, xf)) != hipSuccess) return e;
+            if (!cap && (e = hipEventRecord(b->evx1, S)) != hipSuccess) return e;
         }
-        return csr_too ? enqueue_csr(b, s, S, xf) : hipSuccess;
+        if (cap && csr_too)   // (ev2 is recorded after the graph's launch)
+            return hipMemcpyAsync(b->h_hdr, b->d_hdr, tm_batch::HDR_FIXED, hipMemcpyDeviceToHost, S);
+        return csr_too ? enqueue_csr(b, s, S) : hipSuccess;
     };
     int grc = 1;
     if (graph) {   // a repeated tokenised batch: memset + walk + read-back replayed
@@ -708,7 +726,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         memcpy(k, &s, sizeof s); k += sizeof s;
         memcpy(k, &d, sizeof d);
         if (b->gexec && b->gkey == key) {
-            HIP_OK(hipGraphLaunch(b->gexec, S));
+            HIP_OK(graph_replay(b, S));
             grc = 0;
         } else {
             if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
@@ -716,12 +734,12 @@ int tm_engine::launch(tm_batch* b, bool csr) {
             if (b->gkey == key) {   // the second launch with these arguments: capture them
                 hipGraph_t g = nullptr;
                 if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) == hipSuccess) {
-                    const hipError_t e = enqueue(hipEventRecordExternal, true);
+                    const hipError_t e = enqueue(true, true);
                     const hipError_t e2 = hipStreamEndCapture(S, &g);
                     if (e == hipSuccess && e2 == hipSuccess && g &&
                         hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
                         (void)hipGraphDestroy(g);
-                        HIP_OK(hipGraphLaunch(b->gexec, S));
+                        HIP_OK(graph_replay(b, S));
                         grc = 0;
                     } else {
                         if (g) (void)hipGraphDestroy(g);
@@ -737,9 +755,10 @@ int tm_engine::launch(tm_batch* b, bool csr) {
             b->gkey.swap(key);
         }
         csr_done = grc == 0;
+        if (csr_done) { b->tok_timed = false; b->graphed = true; }   // (replayed: see the enqueue above)
     }
     if (grc == 1) {
-        const hipError_t e = enqueue(0u, false);
+        const hipError_t e = enqueue(false, false);
         if (e != hipSuccess) {
             snprintf(last_error(), 512, "%s at launch (%s)", hipGetErrorString(e), __FILE_NAME__);
             return TM_EIO;
@@ -881,6 +900,7 @@ int tm_engine::launch_graph(tm_batch* b, const MatchArgs& a, const ScanArgs& s, 
         b->gkey.swap(key);
     }
     HIP_OK(hipGraphLaunch(b->gexec, S));
+    ++graph_launches;
     return TM_OK;
 }
 
@@ -929,7 +949,7 @@ void tm_engine::fill_stats(tm_batch* b) {
     (void)hipEventElapsedTime(&ms_total, b->ev0, b->ev2);
     if (b->tok_timed) (void)hipEventElapsedTime(&ms_tok, b->evt, b->ev0);
     if (b->dedup_timed) (void)hipEventElapsedTime(&ms_dd, b->evd, b->tok_timed ? b->evt : b->ev0);
-    if (b->dedup_dev) (void)hipEventElapsedTime(&ms_x, b->evx0, b->evx1);
+    if (b->dedup_dev && !b->graphed) (void)hipEventElapsedTime(&ms_x, b->evx0, b->evx1);
     b->st.ms_tokenize = ms_tok;
     b->st.ms_dedup = ms_dd;
     b->st.ms_expand = ms_x;

@@ -116,6 +116,7 @@ int tm_stats(tm_engine* e, tm_engine_stats* o) {
     o->uploads_full = e->uploads_full;
     o->uploads_delta = e->uploads_delta;
     o->delta_slots = e->delta_slots;
+    o->graph_launches = e->graph_launches;
     return TM_OK;
 }
 

@@ -509,6 +509,7 @@ struct tm_batch {
     // dense = the CSR (row_off, ids) has been built from it since the last launch
     bool dense = false;
     bool tok_timed = false;     // the last launch tokenised: evt..ev0 is its time
+    bool graphed = false;       // the last launch replayed a captured dedup graph (expand untimed)
     bool launched = false, done = false;
     // staging as one region shared by every walk group (set when one group's
     // reservation alone would need more than the staging limit / TICKET_GROUPS)
@@ -1083,7 +1084,7 @@ struct tm_engine {
 
 
     uint64_t version = 1;
-    uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0;
+    uint64_t uploads_full = 0, uploads_delta = 0, delta_slots = 0, graph_launches = 0;
     bool frozen = false;           // TM_CFG_FROZEN_DICT: words only via tm_dict_load
     bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variant
     uint32_t row_cap = 128;        // K: fast-path row slots per topic (TM_ROWCAP)
@@ -1963,6 +1964,7 @@ struct tm_engine {
     // sorted and deduplicated -- and the dense CSR (scan + finalize copy) is
     // built only for a consumer that asks for offsets (ensure_dense).
     hipError_t enqueue_csr(tm_batch* b, const ScanArgs& s, hipStream_t S, unsigned ev_flags = 0);
+    hipError_t graph_replay(tm_batch* b, hipStream_t S);
 
     // tm_match_batch's tail, enqueued behind the walk: scan + finalize (the
     // dense CSR, ids up to their capacity) and, for a one-shot batch, its copy

@@ -118,6 +118,7 @@ typedef struct {
     uint64_t uploads_full;  /* full trie uploads */
     uint64_t uploads_delta; /* incremental delta uploads */
     uint64_t delta_slots;   /* slots written by delta uploads */
+    uint64_t graph_launches;   /* batch launches replayed as a captured HIP graph (repeated or fresh deduplicated batches) */
 } tm_engine_stats;
 
 /* ---- engine ---------------------------------------------------------- */

@@ -137,4 +137,5 @@ def test_fresh_dedup_batches_replay_through_churn():
         for r in range(n_rows):
             assert got[r] == [snapshot[int(j)] for j in idx[cut[r]:cut[r + 1]]], (rnd, Td[r][:60])
         orc.close()
+    assert eng.stats()["graph_launches"] >= 3   # (launches 3..6 replayed the graph captured at launch 2)
     b.free()
