@@ -24,12 +24,19 @@ collective) -> "scaling": "weak"; value = all ranks' publishes / max rank time.
 Extra fields: roofline (HBM, algorithmic bytes per launch counted by the kernel,
 over the match kernel's HIP-event time), cpu_baseline (the CPU restatement of
 emqx_router:match_routes/1 on this host, rank 0 / N = 1 only), p99 batch latency
-at B = 65,536 (device-resident replay) and fresh_latency_sweep (new publishes
-from host memory to sorted ids in host memory, B = 4,096 / 65,536), the
-host-inclusive end-to-end rate, C1 on the CPU port and the device, and C5
-(K = 100 and 10: skew + 10k subscribe/unsubscribe deltas per step).  At N > 1
-every rank's sampled rows are checked against rank 0's replica on device 0
-(parity_sample_ok, emqx_amd/selfcheck.py).
+at B = 65,536 as §8d defines it (submit -> results ready: new publishes from
+host memory to sorted ids in host memory; the device-resident replay beside it
+as p99_resident_ms), the per-publish drop-in path (coalesce: async and
+blocking calls, the CPU port beside them), the host-inclusive end-to-end rate,
+C1 on the CPU port and the device, and C5 (K = 100, 10 and 1000: skew + 10k
+subscribe/unsubscribe deltas per step).
+
+Self-checks, after the timed regions (the oracle only as the checker): at
+N = 1 3,000 evenly spaced rows of the timed C2 launch against the CPU
+restatement, and 3,000 distinct rows of every C5 leg's last (graph-replayed)
+batch against the oracle on that step's snapshot; at N > 1 every rank's
+sampled rows against rank 0's replica on device 0 (emqx_amd/selfcheck.py).
+All of them -> parity_sample_ok.
 """
 
 from __future__ import annotations
@@ -177,7 +184,9 @@ def c1_leg(host, device=0):
 def pmc_traffic(workload, topics, filters=None):
     """HBM bytes per walk launch from the committed PMC pass of this workload
     (`tools/gpu.sh TAG 'traffic c2'` -> profiles/pmc_latest.json for C2,
-    `'traffic c4'` -> profiles/pmc_c4.json for C4), or None."""
+    `'traffic c4'` -> profiles/pmc_c4.json for C4), or None.  The counters are
+    NOT collected in this run (a --pmc pass is a rocprofv3 run of its own):
+    roofline.traffic_source names the file they come from."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json" if workload == "C2" else "pmc_c4.json")
     try:
         with open(path) as f:
@@ -189,6 +198,82 @@ def pmc_traffic(workload, topics, filters=None):
     if filters is not None and pmc.get("filters") not in (None, filters):
         return None
     return pmc.get("hbm_bytes_per_launch")
+
+
+def traffic_source(workload):
+    return ("profiles/" + ("pmc_latest.json" if workload == "C2" else "pmc_c4.json")
+            + " (rocprofv3 FETCH_SIZE and WRITE_SIZE passes of this workload, committed; not counted in this run)")
+
+
+def c2_selfcheck(eng, b, filters, topics) -> dict:
+    """THE CHECKER, after the timed region (oracle/ is used here only as the
+    checker, like cpu_baseline): >= 3,000 evenly spaced rows of the timed
+    launch, gathered on the device (tm_batch_sample), as filter bytes against
+    the CPU restatement of emqx_trie:match/1 (oracle/tm_oracle.c, ETS layout,
+    src/emqx_trie.erl:96-99,162-186) over the same 1M filters."""
+    from emqx_amd import selfcheck as SC
+    from oracle import pyoracle
+    t0 = time.time()
+    idx = SC.sample_index(len(topics))
+    so, si = b.sample(idx)
+    got = SC.rows_from_csr(so, si, np.arange(len(idx)), SC.engine_names(eng))
+    orc = pyoracle.Oracle()
+    for f in filters.tolist():
+        orc.register(f)
+        orc.insert(f)
+    ts = [topics[int(i)] for i in idx]
+    buf, offs = pyoracle.pack(ts)
+    counts, oidx, _ = orc.match_batch(buf, offs, nthreads=8)
+    cut = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    names = {}
+
+    def name(j):
+        if j not in names:
+            names[j] = orc.filter_bytes(j)
+        return names[j]
+    exp = [[name(int(j)) for j in oidx[cut[i]:cut[i + 1]]] for i in range(len(ts))]
+    orc.close()
+    bad = [i for i in range(len(ts)) if got[i] != exp[i]]
+    return {"parity_sample_ok": not bad and len(ts) > 0, "sampled_rows": len(ts),
+            "matches_checked": int(cut[-1]), "mismatches": [ts[i].decode("latin-1") for i in bad[:3]],
+            "checker": "oracle/tm_oracle.c trie restatement over the same filters (rows as filter bytes)",
+            "seconds": round(time.time() - t0, 2)}
+
+
+def c5_selfcheck(eng, b, pubs, derived, allf, live, added) -> dict:
+    """THE CHECKER, after the timed region (oracle/ only as the checker): the
+    last step's batch -- a fresh deduplicated launch replayed from its captured
+    graph and matched after every delta of the run -- against the CPU
+    restatement on that snapshot (the trie's state now; oracle/c5_checker.py
+    FinalSnapshot: inverted index + live set for the derived filters, trie
+    oracle for the background ones, brute-force emqx_topic:match/2 for the
+    churned-in ones).  3,000 evenly spaced distinct rows (by their first
+    publish's bytes, gathered on the device) and the publish -> row map at
+    3,000 evenly spaced publishes (equal bytes <=> equal row)."""
+    from emqx_amd import selfcheck as SC
+    from oracle.c5_checker import FinalSnapshot, _word_id
+    t0 = time.time()
+    row_of, n_rows = b.row_map()
+    u, first = np.unique(row_of, return_index=True)
+    rows_ok = len(u) == n_rows and (u == np.arange(n_rows)).all() and (np.diff(first) > 0).all()
+    ridx = SC.sample_index(n_rows)
+    ts = [pubs[int(first[r])] for r in ridx]
+    distinct_ok = len(set(ts)) == len(ts)
+    pidx = SC.sample_index(len(row_of))
+    map_ok = all(pubs[int(i)] == pubs[int(first[row_of[i]])] for i in pidx)
+    so, si = b.sample(ridx)
+    got = SC.rows_from_csr(so, si, np.arange(len(ridx)), SC.engine_names(eng))
+    chk = FinalSnapshot(derived, allf.slice(len(derived), len(allf)).tolist(), live, added)
+    exp = chk.rows(ts)
+    chk.close()
+    bad = [i for i in range(len(ts)) if got[i] != exp[i]]
+    hot = sum(1 for t in ts if all(_word_id(w) >= 0 for w in t.split(b"/")))
+    return {"parity_sample_ok": bool(not bad and rows_ok and distinct_ok and map_ok and ts),
+            "sampled_rows": len(ts), "sampled_hot_rows": hot, "sampled_publishes": len(pidx),
+            "matches_checked": int(sum(len(e) for e in exp)), "row_map_ok": bool(rows_ok and map_ok and distinct_ok),
+            "mismatches": [ts[i].decode("latin-1")[:80] for i in bad[:3]],
+            "checker": "oracle/c5_checker.py FinalSnapshot on the last step's snapshot",
+            "seconds": round(time.time() - t0, 2)}
 
 
 def timed_steps(bs, steps, ms_match=None, ms_total=None):
@@ -440,7 +525,7 @@ def run_c4_group(args):
     print(json.dumps(out), flush=True)
 
 
-def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, n_batches=3):
+def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, n_batches=3, selfcheck=True):
     """Config C5: 10k hot topics take 90% of the publishes, each matched by ~k
     filters derived from it (+ 100k background C2-style filters).  Every step
     is a NEW batch of n_topics publishes (n_batches pre-generated batches,
@@ -457,7 +542,10 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     Pipelined: the host applies deltas i + 1 while the device runs step i;
     their upload is queued behind walk i and batch i + 1 behind the upload
     (read-your-writes) before batch i is waited for, so a step costs about
-    max(host, device)."""
+    max(host, device).  From a batch's second launch on, the launch replays a
+    captured HIP graph; the device phase split comes from the direct launches
+    (each batch's first, in the warm-up).  After the timed region the last
+    step's batch is checked against the oracle on its snapshot (c5_selfcheck)."""
     from emqx_amd import gen
     from emqx_amd.engine import Engine
     from emqx_amd.skew import Churn, workload
@@ -474,21 +562,28 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     tp = time.perf_counter()
     bs = [eng.prepare(pubs, dedup=True) for pubs in batches]    # bytes to HBM (inputs resident)
     prepare_ms = 1e3 * (time.perf_counter() - tp) / n_batches
-    for _ in range(warmup):
+    split = []
+    for w in range(warmup):
         for b in bs:
             b.retokenize().launch().wait()
+            if w == 0:       # each batch's first launch is direct: its events time every phase
+                st = b.stats()
+                split.append((st["ms_dedup"], st["ms_tokenize"], st["ms_match"], st["ms_expand"],
+                              st["ms_dedup"] + st["ms_tokenize"] + st["ms_total"]))
     if sync is not None:
         sync.barrier()
     # The deltas are drawn before timing, as packed binaries (what the NIF's
     # route_apply hands over).  Step i applies deltas i and matches batch
     # i mod n_batches against the result.
-    deltas = []
+    deltas, added = [], []
     for _ in range(steps):
         dels, adds = churn.step(n_deltas)
+        added += adds
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
-    ms_dev, ms_walk, ms_tok, ms_dd, ms_x, ms_queue, ms_churn = [], [], [], [], [], [], []
+    ms_dev, ms_queue, ms_churn = [], [], []
     rows, delivered = [], []
     ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
+    g0 = eng.stats()["graph_launches"]
     t0 = time.perf_counter()
     tc = time.perf_counter()
     Churn.apply(eng, *deltas[0])
@@ -515,11 +610,9 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         if i + 1 < steps:   # (the last step's wait is the device's tail, no churn beside it)
             ms_host["wait"].append(1e3 * (time.perf_counter() - tc))
         st = b.stats()
+        # a graph replay times its whole span (reported as its walk), a direct
+        # launch each phase: their sum is the launch's device time either way
         ms_dev.append(st["ms_tokenize"] + st["ms_dedup"] + st["ms_total"])
-        ms_walk.append(st["ms_match"])
-        ms_tok.append(st["ms_tokenize"])
-        ms_dd.append(st["ms_dedup"])
-        ms_x.append(st["ms_expand"])
         ms_queue.append(st["ms_queue"])
         rows.append(st["topics"])
         delivered.append(st["delivered"])
@@ -527,17 +620,24 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     if sync is not None:
         sync.barrier()
         elapsed = sync.allmax(elapsed)
-    st = bs[(steps - 1) % n_batches].stats()
+    graph_launches = eng.stats()["graph_launches"] - g0
+    last = (steps - 1) % n_batches
+    st = bs[last].stats()
     n = len(batches[0])
+    sp = np.median(np.array(split), 0).tolist() if split else [0.0] * 5
     out = {
         "k": k, "publishes_per_s": n * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "steps": steps,
         "distinct_topics_per_s": float(np.sum(rows)) / elapsed,
-        "batches": n_batches, "fresh_batch_every_step": True,
+        "batches": n_batches, "dedup_tokenise_walk_expand_every_step": True,
+        # the rotated batches' bytes were uploaded before timing (prepare_ms
+        # per batch, host copy + H2D): the timed rate is HBM-resident input
+        "inputs_resident_in_hbm": True,
+        "publishes_per_s_with_prepare": n / (1e-3 * (1e3 * elapsed / steps + prepare_ms)),
         "deltas_per_step": n_deltas, "filters": len(allf), "publishes": n, "distinct_topics": int(np.mean(rows)),
         "prepare_ms": prepare_ms,
-        "device_ms": float(np.mean(ms_dev)), "device_walk_ms": float(np.mean(ms_walk)),
-        "device_tokenize_ms": float(np.mean(ms_tok)), "device_dedup_ms": float(np.mean(ms_dd)),
-        "device_expand_ms": float(np.mean(ms_x)),
+        "device_ms": float(np.mean(ms_dev)),
+        # per-phase device times of a direct (non-graph) launch of each batch
+        "device_split_direct_ms": dict(zip(("dedup", "tokenize", "walk", "expand", "total"), sp)),
         "device_queue_ms": float(np.mean(ms_queue)),
         "churn_ms": float(np.mean(ms_churn)), "churn_ms_max": float(np.max(ms_churn)),
         "churn_ms_steps": [round(x, 3) for x in ms_churn],   # [0]: before the first launch (no walk beside it)
@@ -548,11 +648,14 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         "delivered_matches_per_step": int(np.mean(delivered)),
         "generic_path_topics": int(st["slow_topics"]),
         "uploads_delta": eng.stats()["uploads_delta"],
-        # launches replayed as a captured HIP graph (from each batch's second
-        # launch on): a replay times only its whole span, reported as its walk,
-        # so the phase means above mix the direct launches' split with that
-        "graph_launches": eng.stats()["graph_launches"],
+        # timed launches replayed as a captured HIP graph
+        "graph_launches": graph_launches,
     }
+    if selfcheck:
+        out["selfcheck"] = c5_selfcheck(eng, bs[last], batches[last], derived, allf, churn.live_set, added)
+        out["parity_sample_ok"] = out["selfcheck"]["parity_sample_ok"]
+        if not out["parity_sample_ok"]:
+            log(f"[c5 k={k}] PARITY SAMPLE FAILED: {out['selfcheck']}")
     for b in bs:
         b.free()
     eng.close()
@@ -562,7 +665,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
 def run_c5(args, ws, rank, local, sync):
     """--workload c5: the C5 leg alone as the bench line (K = --c5-k)."""
     leg = c5_leg(args.c5_k, args.steps, args.c5_deltas, args.topics, device=local, seed=5 + rank, sync=sync,
-                 warmup=args.warmup)
+                 warmup=args.warmup, selfcheck=not args.profile)
     out = {
         "metric": "publishes matched/sec (node), hot-topic skew + churn (C5)",
         "value": ws * leg["publishes_per_s"],
@@ -581,27 +684,68 @@ def run_c5(args, ws, rank, local, sync):
                    "filters": leg["filters"], "distinct_topics": leg["distinct_topics"],
                    "mode": "replicated, a new batch every step, deduplicated on the device"},
         "device_pipeline_ms": leg["device_ms"],
-        "device_walk_ms": leg["device_walk_ms"],
-        "device_tokenize_ms": leg["device_tokenize_ms"],
-        "device_dedup_ms": leg["device_dedup_ms"],
-        "device_expand_ms": leg["device_expand_ms"],
         "churn_apply_ms": leg["churn_ms"],
-        "churn_overlapped_with_device": True,
-        "host_ms": leg["host_ms"],
-        "churn_ms_steps": leg["churn_ms_steps"],
-        "device_queue_ms": leg["device_queue_ms"],
         "distinct_topics_per_s": ws * leg["distinct_topics_per_s"],
-        "prepare_ms": leg["prepare_ms"],
-        "fresh_batch_every_step": True,
-        "delivered_matches_per_step": leg["delivered_matches_per_step"],
-        "generic_path_topics": leg["generic_path_topics"],
-        "uploads_delta": leg["uploads_delta"],
-        "graph_launches": leg["graph_launches"],
+        "leg": leg,
     }
+    if not args.profile:
+        out["parity_sample_ok"] = leg.get("parity_sample_ok")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if sync is not None:
         sync.close()
+
+
+COALESCE_LEGS = (("async", 1, 8, 256), ("async_4096", 1, 16, 256), ("sync", 0, 64, 1))
+
+
+def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
+    """Per-publish emqx_trie:match/1 calls through the drop-in boundary, driven
+    by the native load generator (emqx_amd/csrc/tm_load.cpp): legs = (name,
+    mode, threads, calls in flight per thread, calls).  Every call's row is
+    checked against the batch path (length + hash)."""
+    from emqx_amd import load as LD
+    if exp_c is None:
+        offs, ids = eng.match_batch(topics)
+        exp_c = np.diff(offs.astype(np.int64))
+        exp_h = LD.row_hashes(offs, ids)
+    LD.run(eng, topics.slice(0, min(20_000, len(topics))), LD.ASYNC, 4, 64, hashes=False)    # warm the slots
+    out = {}
+    for name, mode, th, win, cnt in legs:
+        sub = topics if cnt == len(topics) else topics.slice(0, cnt)
+        b0 = eng.async_stats()
+        st, counts, hashes = LD.run(eng, sub, mode, th, win)
+        b1 = eng.async_stats()
+        ok = (st["errors"] == 0 and np.array_equal(counts.astype(np.int64), exp_c[:cnt])
+              and np.array_equal(hashes, exp_h[:cnt]))
+        nb = max(b1["batches"] - b0["batches"], 1)
+        out[name] = {"calls_per_s": cnt / st["seconds"], "calls": cnt, "threads": th, "outstanding_per_thread": win,
+                     "in_flight": th * win, "p50_us": st["p50_us"], "p99_us": st["p99_us"], "mean_us": st["mean_us"],
+                     "max_us": st["max_us"], "rows_equal_batch_path": bool(ok),
+                     "batches": b1["batches"] - b0["batches"],
+                     "mean_batch": (b1["requests"] - b0["requests"]) / nb,
+                     "recoveries": b1["recoveries"] - b0["recoveries"],
+                     "host_us_per_batch": {k: (b1[k] - b0[k]) / nb for k in ("us_launch", "us_wait", "us_deliver")},
+                     "inline_launches": b1["inline_launches"] - b0["inline_launches"]}
+        log(f"[coalesce] {name}: {out[name]}")
+    return out
+
+
+def coalesce_brief(eng, topics) -> dict:
+    """The default line's per-publish sub-object (~2 s): async with 2,048
+    calls in flight (8 threads x 256) and 64 blocking threads, on the C2 trie
+    of the headline; the CPU port's rate is added beside it by the caller."""
+    n = min(len(topics), 1_000_000)
+    sub = topics.slice(0, n)
+    legs = coalesce_legs(eng, sub, (("async", 1, 8, 256, n), ("sync", 0, 64, 1, min(n, 300_000))))
+    return {"workload": f"C2 1M filters, {n} single-topic tm_match_async / tm_match_coalesced calls",
+            "async_calls_per_s": legs["async"]["calls_per_s"], "async_p50_us": legs["async"]["p50_us"],
+            "async_p99_us": legs["async"]["p99_us"], "async_max_us": legs["async"]["max_us"],
+            "async_in_flight": legs["async"]["in_flight"],
+            "sync_calls_per_s": legs["sync"]["calls_per_s"], "sync_threads": 64,
+            "sync_p99_us": legs["sync"]["p99_us"],
+            "rows_equal_batch_path": legs["async"]["rows_equal_batch_path"] and legs["sync"]["rows_equal_batch_path"],
+            "legs": legs}
 
 
 def run_coalesce(args, ws, rank, local, sync):
@@ -618,7 +762,6 @@ def run_coalesce(args, ws, rank, local, sync):
     (length + hash).  The CPU baseline is the oracle restatement of
     match_routes/1 on the lease's cores over the same topics."""
     from emqx_amd import gen
-    from emqx_amd import load as LD
     from emqx_amd.engine import Engine
 
     p = gen.C2
@@ -629,29 +772,8 @@ def run_coalesce(args, ws, rank, local, sync):
     eng.insert_many(filters)
     eng.sync()
     eng.coalesce_config(max_batch=args.coalesce_max_batch, linger_us=args.coalesce_linger_us)
-    offs, ids = eng.match_batch(topics)
-    exp_c = np.diff(offs.astype(np.int64))
-    exp_h = LD.row_hashes(offs, ids)
-    LD.run(eng, topics.slice(0, 20_000), LD.ASYNC, 4, 64, hashes=False)    # warm the slots
-    legs = {}
-    for name, mode, th, win, cnt in (("async", LD.ASYNC, 8, 256, n), ("async_4096", LD.ASYNC, 16, 256, n),
-                                     ("sync", LD.SYNC, 64, 1, min(n, 400_000))):
-        sub = topics if cnt == n else topics.slice(0, cnt)
-        b0 = eng.async_stats()
-        st, counts, hashes = LD.run(eng, sub, mode, th, win)
-        b1 = eng.async_stats()
-        ok = (st["errors"] == 0 and np.array_equal(counts.astype(np.int64), exp_c[:cnt])
-              and np.array_equal(hashes, exp_h[:cnt]))
-        legs[name] = {"calls_per_s": cnt / st["seconds"], "calls": cnt, "threads": th, "outstanding_per_thread": win,
-                      "p50_us": st["p50_us"], "p99_us": st["p99_us"], "mean_us": st["mean_us"],
-                      "max_us": st["max_us"], "rows_equal_batch_path": bool(ok),
-                      "batches": b1["batches"] - b0["batches"],
-                      "mean_batch": (b1["requests"] - b0["requests"]) / max(b1["batches"] - b0["batches"], 1),
-                      "recoveries": b1["recoveries"] - b0["recoveries"],
-                      "host_us_per_batch": {k: (b1[k] - b0[k]) / max(b1["batches"] - b0["batches"], 1)
-                                            for k in ("us_launch", "us_wait", "us_deliver")},
-                      "inline_launches": b1["inline_launches"] - b0["inline_launches"]}
-        log(f"[coalesce] {name}: {legs[name]}")
+    legs = coalesce_legs(eng, topics, [(name, mode, th, win, n if mode else min(n, 400_000))
+                                       for name, mode, th, win in COALESCE_LEGS])
     out = {"metric": "emqx_trie:match/1 calls/sec, one call per publish (tm_match_async, 2048 in flight)",
            "value": legs["async"]["calls_per_s"], "unit": "calls/s", "n_gpus": 1, "steps": 1, "warmup": 1,
            "ms_per_step": 1e3 * n / legs["async"]["calls_per_s"], "higher_is_better": True, "scaling": "weak",
@@ -1096,6 +1218,14 @@ def main():
     n = len(topics)
     value = ws * n * args.steps / elapsed
     ms_step = 1e3 * elapsed / args.steps
+    # the timed launch checks itself (oracle as the checker, outside the timed
+    # region): N = 1 against the CPU restatement; N > 1 below against rank 0's
+    # replica on device 0
+    c2_check = None
+    if ws == 1 and not args.profile:
+        c2_check = c2_selfcheck(eng, b, filters, topics)
+        if not c2_check["parity_sample_ok"]:
+            log(f"[rank 0] C2 PARITY SAMPLE FAILED: {c2_check}")
 
     # fresh batches: the same resident bytes tokenised again every launch, so a
     # step is the whole device pipeline of a never-seen batch (tokenise + walk
@@ -1133,6 +1263,7 @@ def main():
                    "batches_in_flight": nb},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_source("C2") if traffic else None,
                      "kernel": "tm_match_tiles", "kernel_ms": k_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "per_publish": {"V": st["visits"] / n, "H": st["hash_hits"] / n,
@@ -1148,6 +1279,9 @@ def main():
         "matches_per_step": st["matches"],
         "slow_path_topics": st["slow_topics"],
     }
+    if c2_check is not None:
+        out["selfcheck"] = c2_check
+        out["parity_sample_ok"] = c2_check["parity_sample_ok"]
 
     # the same steps with the dense CSR built after every wait (scan + copy
     # of every row into topic order, tm_batch_device_csr): what a consumer
@@ -1218,17 +1352,24 @@ def main():
             except Exception as e:  # report, don't hide
                 sweep[str(bsz)] = {"error": str(e)}
         main_lat = sweep.get("65536", {})
-        out["p99_batch_ms"] = main_lat.get("p99_ms")
-        out["p50_batch_ms"] = main_lat.get("p50_ms")
-        out["latency_batch"] = 65536
+        out["p99_resident_ms"] = main_lat.get("p99_ms")
+        out["p50_resident_ms"] = main_lat.get("p50_ms")
         out["latency_sweep"] = sweep
         if "error" in main_lat:
             out["latency_error"] = main_lat["error"]
-        # fresh-batch latency (submit -> results ready): new
-        # topic bytes in host memory -> tm_match_batch (H2D, device tokeniser,
-        # walk, CSR, D2H) -> sorted ids in host memory, a different slice of
-        # publishes every batch
+        # the headline latency, SURVEY.md §8d's "batch submit -> results
+        # ready": new topic bytes in host memory -> tm_match_batch (H2D,
+        # device tokeniser, walk, CSR, D2H) -> sorted ids in host memory, a
+        # different slice of publishes every batch, B = 65,536
         out["fresh_latency_sweep"] = fresh_latency(eng, filters, topics, args.latency_batches)
+        fl = out["fresh_latency_sweep"]["65536"]
+        out["p99_batch_ms"] = fl["p99_ms"]
+        out["p50_batch_ms"] = fl["p50_ms"]
+        out["latency_batch"] = 65536
+        out["latency_path"] = "submit -> results ready: " + fl["path"] + " (fresh publishes every batch)"
+        # the drop-in per-publish path: emqx_trie:match/1 once per publish
+        # (the NIF's match/2), async and blocking, on this C2 trie
+        out["coalesce"] = coalesce_brief(eng, topics)
         # host-inclusive end to end, timed at the C ABI (tm_match_batch): topic
         # bytes in host RAM -> H2D -> device tokenise -> match -> sorted CSR in
         # the engine's pinned host buffers (what a NIF hands to the broker)
@@ -1244,13 +1385,21 @@ def main():
         host = host_cpu_share()
         out["cpu_baseline"] = cpu_baseline(filters, topics, min(200_000, n), min(args.cpu_sample, n), host)
         out["speedup_vs_cpu_allcore"] = value / out["cpu_baseline"]["value"]
+        if "coalesce" in out:
+            cv = out["cpu_baseline"]["value"]
+            out["coalesce"]["cpu_port_publishes_per_s"] = cv
+            out["coalesce"]["async_vs_cpu_port"] = out["coalesce"]["async_calls_per_s"] / cv
+            out["coalesce"]["sync_vs_cpu_port"] = out["coalesce"]["sync_calls_per_s"] / cv
         if ws == 1:
             out["c1"] = c1_leg(host, device=local)
     if rank == 0 and ws == 1 and not args.profile and not args.no_c5:
-        # config C5 in the driver's line: K = 100 and K = 10 filters per hot
-        # topic, 10k subscribe/unsubscribe deltas per step
+        # config C5 in the driver's line: K = 100, 10 and 1000 filters per hot
+        # topic, 10k subscribe/unsubscribe deltas per step; each leg checks
+        # its last step's batch against the oracle on that step's snapshot
         # 10 steps: the last step's walk is the one not hidden behind a churn
-        out["c5"] = {f"k{k}": c5_leg(k, 10, 10_000, args.topics, device=local) for k in (100, 10)}
+        out["c5"] = {f"k{k}": c5_leg(k, 10, 10_000, args.topics, device=local) for k in (100, 10, 1000)}
+        out["parity_sample_ok"] = bool(out.get("parity_sample_ok", True)
+                                       and all(v.get("parity_sample_ok") for v in out["c5"].values()))
 
     if rank == 0:
         print(json.dumps(out), flush=True)

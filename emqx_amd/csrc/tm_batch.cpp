@@ -1064,14 +1064,11 @@ int tm_engine::sample(tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* 
     b->h_smp_off.assign((size_t)k + 1, 0);
     b->h_smp_ids.clear();
     if (k) {
-        struct Scratch {
-            void* p = nullptr;
-            ~Scratch() { if (p) (void)hipFree(p); }
-        } meta, ids;
-        // [rows u32 k | cnt u32 k | pad | src u64 k | off u64 k + 1]
+        int rc;
+        // [rows u32 k | cnt u32 k | pad | src u64 k | off u64 k + 1], batch-owned
         const size_t o_src = (((size_t)k * 8) + 15) & ~(size_t)15, o_off = o_src + (size_t)k * 8;
-        HIP_OK(hipMalloc(&meta.p, o_off + ((size_t)k + 1) * 8));
-        uint8_t* m = static_cast<uint8_t*>(meta.p);
+        if ((rc = dev_reserve(b->d_smp_meta, b->c_smp_meta, o_off + ((size_t)k + 1) * 8))) return rc;
+        uint8_t* m = b->d_smp_meta;
         uint32_t* d_rows = reinterpret_cast<uint32_t*>(m);
         uint32_t* d_cnt = d_rows + k;
         unsigned long long* d_src = reinterpret_cast<unsigned long long*>(m + o_src);
@@ -1087,10 +1084,10 @@ int tm_engine::sample(tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* 
         for (uint32_t i = 0; i <= k; ++i) b->h_smp_off[i] = (uint32_t)off[i];
         b->h_smp_ids.resize(off[k]);
         if (off[k]) {
-            HIP_OK(hipMalloc(&ids.p, off[k] * 4));
+            if ((rc = dev_reserve(b->d_smp_ids, b->c_smp_ids, off[k]))) return rc;
             HIP_OK(hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, S));
-            HIP_OK(launch_sample_ids(b->d_sfids, d_cnt, d_src, d_off, k, static_cast<uint32_t*>(ids.p), S));
-            HIP_OK(hipMemcpyAsync(b->h_smp_ids.data(), ids.p, off[k] * 4, hipMemcpyDeviceToHost, S));
+            HIP_OK(launch_sample_ids(b->d_sfids, d_cnt, d_src, d_off, k, b->d_smp_ids, S));
+            HIP_OK(hipMemcpyAsync(b->h_smp_ids.data(), b->d_smp_ids, off[k] * 4, hipMemcpyDeviceToHost, S));
             HIP_OK(hipStreamSynchronize(S));
         }
     }

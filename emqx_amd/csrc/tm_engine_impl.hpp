@@ -483,6 +483,9 @@ struct tm_batch {
     uint64_t dense_cap = 0;         // ids the enqueued finalize could hold
     bool dense_enq = false;         // the LAST launch enqueued scan + finalize (set by launch, read by wait)
     std::vector<uint32_t> h_smp_off, h_smp_ids;   // tm_batch_sample's last result (host CSR)
+    uint8_t* d_smp_meta = nullptr;   // tm_batch_sample's device scratch, kept (a hipFree per call
+    uint32_t* d_smp_ids = nullptr;   //  would synchronise the device under the other streams)
+    size_t c_smp_meta = 0, c_smp_ids = 0;
     // TM_BATCH_DEDUP on the device (device-tokenised batches, etm::DedupArgs):
     // the n_pub publishes are deduplicated by their bytes, and only the rows
     // (distinct topics) are tokenised and walked; n becomes the row count once
@@ -593,6 +596,8 @@ struct tm_batch {
         dev_free(d_dtab); dev_free(d_psrc); dev_free(d_drep); dev_free(d_dflag); dev_free(d_dblen); dev_free(d_drbs);
         dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount); dev_free(d_cbytes); dev_free(d_coffs);
         dev_free(d_dlead);
+        dev_free(d_smp_meta); dev_free(d_smp_ids);
+        c_smp_meta = c_smp_ids = 0;
         c_dtab = c_psrc = c_drep = c_dflag = c_dblen = c_drbs = c_dbbs = c_rowof = 0;
         c_dd = c_pcount = c_cbytes = c_coffs = c_dlead = 0;
         for (hipEvent_t* ev : {&evd, &evx0, &evx1}) {
@@ -842,9 +847,15 @@ struct WorkPool {
     // sleep soon after the grace.
     // (the grace after a mutation covers the delta gather that usually
     // follows it, tm_sync_async: its fork-joins find the workers awake)
+    // Inside a mutation the deadline is pushed to now + PHASE_GAP_NS at the
+    // start and the end of every run(): the workers spin across the short
+    // gaps between phases but sleep through a long serial stretch of the
+    // calling thread (a bulk build's merge of 10^8 filters, say).
     static constexpr int SPIN_IDLE = 2048;
     static constexpr int64_t GRACE_NS = 150000;
-    std::atomic<int64_t> linger_until{0};   // steady-clock ns; INT64_MAX inside a mutation
+    static constexpr int64_t PHASE_GAP_NS = 300000;
+    std::atomic<int64_t> linger_until{0};   // steady-clock ns
+    std::atomic<int> lingering{0};          // mutations in progress (Linger scopes)
     static int64_t now_ns() {
         return std::chrono::duration_cast<std::chrono::nanoseconds>(
                    std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -859,9 +870,19 @@ struct WorkPool {
     }
     struct Linger {   // scope of a bulk mutation
         WorkPool& p;
-        explicit Linger(WorkPool& q) : p(q) { p.linger_until.store(INT64_MAX, std::memory_order_relaxed); }
-        ~Linger() { p.linger_until.store(now_ns() + GRACE_NS, std::memory_order_relaxed); }
+        explicit Linger(WorkPool& q) : p(q) {
+            p.lingering.fetch_add(1, std::memory_order_relaxed);
+            p.linger_until.store(now_ns() + PHASE_GAP_NS, std::memory_order_relaxed);
+        }
+        ~Linger() {
+            p.lingering.fetch_sub(1, std::memory_order_relaxed);
+            p.linger_until.store(now_ns() + GRACE_NS, std::memory_order_relaxed);
+        }
     };
+    void refresh_linger() {
+        if (lingering.load(std::memory_order_relaxed))
+            linger_until.store(now_ns() + PHASE_GAP_NS, std::memory_order_relaxed);
+    }
     // `cpus` (may be null): the CPUs the workers run on
     void start(unsigned k, const cpu_set_t* cpus) {
         n = std::max(1u, k);
@@ -883,6 +904,7 @@ struct WorkPool {
     }
     void run(const std::function<void(unsigned)>& f) {
         if (n <= 1) { f(0); return; }
+        refresh_linger();
         job = &f;
         busy.store(n - 1, std::memory_order_release);
         gen.fetch_add(1, std::memory_order_acq_rel);
@@ -890,6 +912,7 @@ struct WorkPool {
         f(0);
         for (uint32_t b; (b = busy.load(std::memory_order_acquire)) != 0;)
             if (!spin_until_changed(busy, b)) futex(&busy, FUTEX_WAIT, b);
+        refresh_linger();
     }
     ~WorkPool() {
         stop.store(true, std::memory_order_release);

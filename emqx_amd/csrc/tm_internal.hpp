@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 struct tm_engine;   // include/emqx_tm.h (opaque handles, defined in tm_engine_impl.hpp)
 struct tm_batch;
 
@@ -168,10 +170,12 @@ struct MatchArgs {
     const uint32_t* toff;     // n + 1 word offsets
     const uint8_t* tflags;
     uint32_t n;
+    uint32_t pad0_;             // (explicit padding: the struct's bytes are a graph cache key, tm_batch.cpp)
     const uint32_t* d_n;        // or null: the topic count is *d_n (<= n) -- a device-deduplicated
                                 // batch's rows, known only on the device when the walk is enqueued
     const uint32_t* slow_list;  // host-flagged slow topics
     uint32_t n_slow;
+    uint32_t pad1_;
     const uint32_t* d_nslow;    // device-resident count of slow_list (token batches), or null
     // outputs
     uint32_t* count;          // per topic |M(t)|
@@ -183,15 +187,18 @@ struct MatchArgs {
     uint32_t grid;            // tm_match_tiles workgroups (= match_waves(n)); rows[] is sized for it
     uint32_t qcap;            // LDS probe-stack entries per wave (384 or 512)
     uint32_t static_rounds;   // round-robin tiles per wave before tickets (>= 1)
+    uint32_t pad2_;
     uint32_t* xg;             // the header's group lines (header + XG_WORD)
     uint64_t rcap;            // staging entries per group region (sfids_cap / TICKET_GROUPS)
     uint32_t sgmask;          // staging group of a wave = (blockIdx % TICKET_GROUPS) & sgmask
                               // (TICKET_GROUPS - 1; 0 = one region for all: a skewed batch)
+    uint32_t pad3_;
     uint32_t* sfids;          // staging: sorted filter ids, one contiguous run per tile
     uint64_t sfids_cap;
     uint32_t* ctrl;
     uint32_t* ovf_list;       // topics redone by the slow path (row > K or stack overflow)
     uint32_t ovf_cap;
+    uint32_t pad4_;
     unsigned long long* stats;
     // slow-path scratch
     uint32_t* s_qparent;
@@ -517,6 +524,7 @@ struct TokArgs {
     const uint64_t* offs;     // n + 1 absolute offsets (caller's), minus base
     uint64_t base;
     uint32_t n;
+    uint32_t pad0_;           // (explicit padding: the struct's bytes are a graph cache key)
     const DictKey* keys;      // cuckoo table of probe keys (DictKey)
     const DictTail* tails;    // by word id
     uint64_t dict_mask;       // cuckoo table size - 1 (power of two)
@@ -558,6 +566,7 @@ struct DedupArgs {
     const uint64_t* offs;
     uint64_t base;
     uint32_t n;
+    uint32_t pad0_;           // (explicit padding: the struct's bytes are a graph cache key)
     unsigned long long* table;   // mask + 1 slots, zeroed
     uint64_t mask;
     uint32_t* rep;            // n: pass 1 the publish's table slot, pass 2 its representative
@@ -579,9 +588,17 @@ struct DedupArgs {
     unsigned long long* stats;
     uint32_t weak_hash;       // test knob (TM_DEDUP_WEAK_HASH): hash = length only, every same-length
                               // topic collides -- exercises the byte check of tm_dedup_mark
+    uint32_t pad1_;
 };
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s);
+// A captured launch is keyed by the bytes of its argument structs
+// (tm_batch.cpp launch / launch_graph): no implicit padding, so equal
+// arguments always give equal keys (the pads are members, zeroed by `{}`)
+static_assert(std::has_unique_object_representations_v<MatchArgs>, "MatchArgs has implicit padding");
+static_assert(std::has_unique_object_representations_v<ScanArgs>, "ScanArgs has implicit padding");
+static_assert(std::has_unique_object_representations_v<TokArgs>, "TokArgs has implicit padding");
+static_assert(std::has_unique_object_representations_v<DedupArgs>, "DedupArgs has implicit padding");
 
 // tm_export_host: an async batch's per-topic results and rows -> pinned host memory
 struct ExportArgs {

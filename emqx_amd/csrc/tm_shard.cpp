@@ -875,6 +875,17 @@ int tm_sharded_prepare(tm_sharded* s, const uint8_t* topics, const uint64_t* off
         };
         const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, (nbytes + n * 8) >> 22));
         std::vector<std::thread> th;
+        // joins the staging threads on every way out of this scope (a throw
+        // from plan() or from a thread's creation included): a joinable
+        // std::thread destroyed by the unwind would std::terminate, and the
+        // threads use the locals above, which outlive this guard
+        struct Joiner {
+            std::vector<std::thread>& th;
+            ~Joiner() {
+                for (auto& t : th)
+                    if (t.joinable()) t.join();
+            }
+        } joiner{th};
         for (unsigned k = 0; k < T; ++k) th.emplace_back(stage);
         b->dict_words = ~0ull;
         const TokStaged st{ready.data(), &bad, CB, CO, (uint32_t)nbi};

@@ -3,13 +3,13 @@ derived filters (10M) + 100k background filters, a 10M-publish batch with
 TM_BATCH_DEDUP, 10,000 subscribe/unsubscribe deltas between two launches.
 Every row of both batches is checked for CSR consistency and duplicate-free
 ids; 3,000 rows per batch (300 hot, 2,700 background) are checked exactly
-against the oracle on that batch's snapshot (tests/c5_checker.py: inverted
+against the oracle on that batch's snapshot (oracle/c5_checker.py: inverted
 index for the derived filters, trie oracle for the background ones, brute
 force for the churned-in ones)."""
 
 import numpy as np
 import pytest
-from c5_checker import SnapshotOracle
+from oracle.c5_checker import SnapshotOracle
 
 from emqx_amd import gen
 from emqx_amd.engine import Engine

@@ -51,11 +51,11 @@ def test_churn_keeps_live_set_consistent():
 
 
 def test_c5_checker_equals_the_trie_oracle_under_churn():
-    """tests/c5_checker.py (the full-scale C5 test's expected rows) against the
+    """oracle/c5_checker.py (the full-scale C5 test's expected rows) against the
     trie oracle over the whole snapshot, on a small C5 workload with churn."""
     import random
 
-    from c5_checker import SnapshotOracle
+    from oracle.c5_checker import FinalSnapshot, SnapshotOracle
     from oracle import pyoracle as P
 
     p = gen.SkewParams(seed=12, n_hot=60, k_per_hot=80, vocab=8)   # small vocab: many cross-family matches
@@ -65,15 +65,23 @@ def test_c5_checker_equals_the_trie_oracle_under_churn():
     live = set(derived.tolist())
     churn = Churn(hot, derived.tolist(), seed=5)
     T = sorted(set(pubs.tolist()))[:400] + hot.tolist()
+    added = []
     for rnd in range(3):
         if rnd:
             dels, adds = churn.step(400)
+            # a base filter deleted and subscribed again: listed once by FinalSnapshot
+            adds += [f for f in dels[:5] if f not in churn.live_set]
+            churn.live_set.update(adds)
+            added += adds
             for f in dels:
                 chk.delete(f)
                 live.discard(f)
             for f in adds:
                 chk.insert(f)
                 live.add(f)
+        fin = FinalSnapshot(derived, background, churn.live_set, added)
+        assert fin.rows(T) == chk.rows(T), rnd
+        fin.close()
         orc = P.Oracle()
         F = sorted(live) + background
         for f in F:
