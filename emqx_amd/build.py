@@ -112,6 +112,73 @@ def build_all(force=False):
     return [build_tm(force), build_gen(force), build_load(force), build_nif_mock(force)]
 
 
+SAN_FLAGS = {
+    # host code only: every -fsanitize= right after -Xarch_host (no GPU sanitizer on this pool)
+    "asan": ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-Xarch_host", "-fsanitize=thread"],
+}
+SAN_LINK = {"asan": ["-fsanitize=address,undefined"], "tsan": ["-fsanitize=thread"]}
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def san_runtime(kind):
+    """The clang sanitizer runtime a process must preload to load a sanitized
+    library from an uninstrumented interpreter (LD_PRELOAD)."""
+    import glob
+    name = {"asan": "libclang_rt.asan-x86_64.so", "tsan": "libclang_rt.tsan-x86_64.so"}[kind]
+    hits = sorted(glob.glob(f"/opt/rocm/lib/llvm/lib/clang/*/lib/linux/{name}"))
+    return hits[-1] if hits else None
+
+
+def build_sanitized(kind, force=False, jobs=8):
+    """Host-sanitized builds for the CPU sanitizer tests:
+    emqx_amd/variants/<kind>/libemqx_tm.so (the engine's host C++ under
+    ASan + UBSan, or TSan) and libemqx_nif_mock.so (the erl_nif shim + the
+    runtime stand-in, same sanitizer, linked to it).  The kernels' object is
+    built once, unsanitized (device code is not instrumented either way).
+    -> the directory."""
+    from concurrent.futures import ThreadPoolExecutor
+    out_dir = os.path.join(HERE, "variants", kind)
+    obj_dir = os.path.join(HERE, "variants", "obj")
+    os.makedirs(out_dir, exist_ok=True)
+    os.makedirs(obj_dir, exist_ok=True)
+    hdrs = [os.path.join(CSRC, f) for f in TM_HEADERS]
+    flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-g",
+             "-fno-omit-frame-pointer"]
+    lib = os.path.join(out_dir, "libemqx_tm.so")
+    deps = [os.path.join(CSRC, f) for f in TM_SOURCES] + hdrs
+    if force or _stale(lib, deps, kind + ARCH):
+        def obj(src, san):
+            base = os.path.splitext(os.path.basename(src))[0]
+            o = os.path.join(obj_dir if not san else out_dir, base + ".o")
+            key = (kind if san else "") + ARCH
+            if force or _stale(o, [src] + hdrs, key):
+                _run([HIPCC, *flags, "-O1" if san else "-O3", *(SAN_FLAGS[kind] if san else []),
+                      f'-DTM_SRC_HASH="{_digest(deps, ARCH)}"', "-c", "-o", o, src])
+                _stamp(o, [src] + hdrs, key)
+            return o
+        srcs = [os.path.join(CSRC, f) for f in TM_SOURCES]
+        with ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(lambda s: obj(s, not s.endswith(".hip")), srcs))
+        tmp = lib + ".tmp"
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-fno-gpu-sanitize", "-shared-libsan",
+              *SAN_LINK[kind], "-Wl,-soname,libemqx_tm.so", "-o", tmp, *objs, "-lpthread"])
+        os.replace(tmp, lib)
+        _stamp(lib, deps, kind + ARCH)
+    mock = os.path.join(ROOT, "tests", "nif_mock")
+    nsrcs = [os.path.join(CSRC, "nif", "emqx_tm_nif.c"), os.path.join(mock, "mock_erts.c")]
+    nif = os.path.join(out_dir, "libemqx_nif_mock.so")
+    ndeps = nsrcs + [os.path.join(mock, "erl_nif.h"), lib, os.path.join(ROOT, "include", "emqx_tm.h")]
+    if force or _stale(nif, ndeps, kind):
+        _run([os.path.join(LLVM_BIN, "clang"), "-O1", "-g", "-fno-omit-frame-pointer", "-std=gnu11", "-fPIC",
+              "-shared", "-Wall", "-Wextra", "-Werror", *SAN_LINK[kind], "-shared-libsan",
+              "-I" + mock, "-I" + os.path.join(ROOT, "include"), "-o", nif, *nsrcs,
+              "-L" + out_dir, "-lemqx_tm", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+        _stamp(nif, ndeps, kind)
+    return out_dir
+
+
 def build_variant(name, defines):
     """A/B builds (dev): libemqx_tm with extra -D defines into
     emqx_amd/variants/libemqx_tm_<name>.so, loaded with EMQX_TM_LIB=<path>."""

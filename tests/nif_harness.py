@@ -12,7 +12,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "..", "emqx_amd", "libemqx_nif_mock.so")
+LIB = os.environ.get("EMQX_NIF_MOCK_LIB") or os.path.join(HERE, "..", "emqx_amd", "libemqx_nif_mock.so")
 
 TERM = C.c_size_t
 
