@@ -121,12 +121,20 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 
 // Peer access between two devices, both ways: LINK_PEER when the runtime
 // grants it (xGMI on an MI355X node), LINK_STAGED otherwise (copies bounce
-// through pinned host memory).  TM_SHARD_STAGED=1 forces the staged path,
-// even on one device (tests exercise it on a one-GPU box).
+// through pinned host memory).  Test knob TM_SHARD_LINK (so that a one-GPU
+// box runs every link kind's code): "staged" forces the staged path (alias
+// TM_SHARD_STAGED=1); "peer" takes the peer path for a pair on one device
+// (a peer store / hipMemcpyPeer into the same HBM); "probe" runs the
+// runtime's peer probe even for a device paired with itself, where peer
+// access is refused -- the denied branch, which must fall back to staged.
 uint8_t open_link(int a, int b) {
     const char* f = getenv("TM_SHARD_STAGED");
     if (f && atoi(f) != 0) return TM_LINK_STAGED;
-    if (a == b) return TM_LINK_SAME;
+    const char* m = getenv("TM_SHARD_LINK");
+    const std::string mode = m ? m : "";
+    if (mode == "staged") return TM_LINK_STAGED;
+    if (a == b && mode == "peer") return TM_LINK_PEER;
+    if (a == b && mode != "probe") return TM_LINK_SAME;
     int ab = 0, ba = 0;
     if (hipDeviceCanAccessPeer(&ab, a, b) != hipSuccess || hipDeviceCanAccessPeer(&ba, b, a) != hipSuccess || !ab ||
         !ba) {

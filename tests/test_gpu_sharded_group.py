@@ -152,20 +152,28 @@ def test_c4_20m_iot_filters_two_shards_properties_and_oracle_sample():
     grp.close()
 
 
-def test_staged_links_and_three_shards(monkeypatch):
-    """Parts copied through pinned host memory (the path taken when two
-    devices cannot reach each other's memory), forced on one device by
-    TM_SHARD_STAGED; and three shards: every row equals the oracle's, one host
+def test_link_kinds_and_three_shards(monkeypatch):
+    """Every link kind's code on one device, three shards: parts copied
+    through pinned host memory (the path taken when two devices cannot reach
+    each other's memory, TM_SHARD_LINK=staged), the peer path (peer stores
+    and hipMemcpyPeer, TM_SHARD_LINK=peer: here into the same HBM), and the
+    runtime's peer probe run for a device paired with itself
+    (TM_SHARD_LINK=probe), where peer access is refused: the denied branch
+    must fall back to a working link.  Every row equals the oracle's, one host
     wait per step, the result identical to the same-device links'."""
     F, T, vocab = workload(43)
     exp, _ = oracle_rows(F, T)
     res = {}
-    for mode in ("same", "staged"):
-        if mode == "staged":
-            monkeypatch.setenv("TM_SHARD_STAGED", "1")
+    for mode in ("same", "staged", "peer", "probe"):
+        if mode != "same":
+            monkeypatch.setenv("TM_SHARD_LINK", mode)
         grp = ShardedGroup([0, 0, 0])
-        monkeypatch.delenv("TM_SHARD_STAGED", raising=False)
-        assert grp.link(0, 1) == mode and grp.link(2, 2) == mode
+        monkeypatch.delenv("TM_SHARD_LINK", raising=False)
+        links = {grp.link(i, j) for i in range(3) for j in range(3)}
+        if mode == "probe":     # refused peer access to itself -> staged (or peer, should the runtime grant it)
+            assert len(links) == 1 and links <= {"staged", "peer"}, links
+        else:
+            assert links == {mode}, links
         grp.dict_load(vocab)
         grp.insert_many(F)
         b = grp.prepare(T)
@@ -178,7 +186,7 @@ def test_staged_links_and_three_shards(monkeypatch):
         res[mode] = got
         b.free()
         grp.close()
-    assert res["same"] == res["staged"]
+    assert res["same"] == res["staged"] == res["peer"] == res["probe"]
 
 
 def test_c4_100m_iot_filters_one_shard_properties_and_oracle_sample():
