@@ -473,16 +473,25 @@ int tm_engine::reserve_tokens(tm_batch* b, uint32_t n, uint64_t nbytes) {
 int tm_engine::reserve_dedup(tm_batch* b, uint64_t nbytes) {
     int rc;
     const size_t n = b->n;
+    if (nbytes >> DD_OFF_BITS) {   // (a table slot holds a 40-bit byte offset)
+        snprintf(last_error(), 512, "device dedup: batch of %llu bytes over 2^40", (unsigned long long)nbytes);
+        return TM_EINVAL;
+    }
     uint64_t cap = 1024;
     while (cap < (uint64_t)n + n / 2) cap <<= 1;   // load <= 2/3 when every publish is distinct
+    const uint64_t old_mask = b->dtab_mask;
     b->dtab_mask = cap - 1;
     b->dd_bytes = nbytes;
-    const size_t nb = scan_block_count((uint32_t)n) + 1;
+    const size_t nblk = dedup_blocks((uint32_t)n);
+    const size_t nb = scan_block_count((uint32_t)nblk) + 1;
+    void* old_tab = b->d_dtab;
     if ((rc = dev_reserve(b->d_dtab, b->c_dtab, cap))) return rc;
-    if ((rc = dev_reserve(b->d_drep, b->c_drep, std::max<size_t>(n, 1)))) return rc;
-    if ((rc = dev_reserve(b->d_dlead, b->c_dlead, std::max<size_t>(n, 1)))) return rc;
-    if ((rc = dev_reserve(b->d_dflag, b->c_dflag, n + 1))) return rc;
-    if ((rc = dev_reserve(b->d_dblen, b->c_dblen, n + 1))) return rc;
+    if (b->d_dtab != old_tab || old_mask != b->dtab_mask) b->dtab_dirty = true;
+    if ((rc = dev_reserve(b->d_dsrow, b->c_dsrow, cap))) return rc;
+    if ((rc = dev_reserve(b->d_dslot, b->c_dslot, std::max<size_t>(n, 1)))) return rc;
+    if ((rc = dev_reserve(b->d_dbits, b->c_dbits, std::max<size_t>(nblk, 1) * (DD_TILE / 64)))) return rc;
+    if ((rc = dev_reserve(b->d_dbc, b->c_dbc, nblk + 1))) return rc;
+    if ((rc = dev_reserve(b->d_dbb, b->c_dbb, nblk + 1))) return rc;
     if ((rc = dev_reserve(b->d_drbs, b->c_drbs, nb))) return rc;
     if ((rc = dev_reserve(b->d_dbbs, b->c_dbbs, nb))) return rc;
     if ((rc = dev_reserve(b->d_rowof, b->c_rowof, std::max<size_t>(n, 1)))) return rc;
@@ -503,7 +512,8 @@ DedupArgs tm_engine::dedup_args(tm_batch* b) const {
     DedupArgs d{};
     d.bytes = b->in_bytes; d.offs = b->in_offs; d.base = b->tok_base; d.n = b->n_pub;
     d.table = b->d_dtab; d.mask = b->dtab_mask;
-    d.rep = b->d_drep; d.lead = b->d_dlead; d.rflag = b->d_dflag; d.blen = b->d_dblen; d.rbs = b->d_drbs; d.bbs = b->d_dbbs;
+    d.slot = b->d_dslot; d.repbits = b->d_dbits; d.bcount = b->d_dbc; d.bbytes = b->d_dbb;
+    d.rbs = b->d_drbs; d.bbs = b->d_dbbs; d.srow = b->d_dsrow;
     d.row_of = b->d_rowof; d.cbytes = b->d_cbytes; d.coffs = b->d_coffs; d.dd = b->d_dd;
     d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
     d.stats = b->d_stats;
@@ -511,14 +521,23 @@ DedupArgs tm_engine::dedup_args(tm_batch* b) const {
     return d;
 }
 
+// the dedup passes (no table clear: clear_dedup_table, outside any capture)
 int tm_engine::enqueue_dedup(tm_batch* b, hipStream_t S) {
     const DedupArgs d = dedup_args(b);
-    HIP_OK(hipMemsetAsync(b->d_dtab, 0, (b->dtab_mask + 1) * 8, S));
     if (!d.n) HIP_OK(hipMemsetAsync(b->d_dd, 0, 8, S));   // (no compact kernel: zero rows)
+    const uint32_t nblk = dedup_blocks(d.n);
     ScanArgs rs{}, bs{};
-    rs.count = d.rflag; rs.row_off = d.rflag; rs.block_sums = b->d_drbs; rs.n = d.n;   // (in place)
-    bs.count = d.blen; bs.row_off = d.blen; bs.block_sums = b->d_dbbs; bs.n = d.n;
+    rs.count = d.bcount; rs.row_off = d.bcount; rs.block_sums = b->d_drbs; rs.n = nblk;   // (in place)
+    bs.count = d.bbytes; bs.row_off = d.bbytes; bs.block_sums = b->d_dbbs; bs.n = nblk;
     HIP_OK(launch_dedup(d, rs, bs, S));
+    return TM_OK;
+}
+
+// a dirty table (new, or a pass whose expansion was not waited for) is
+// cleared before the next pass; a clean one is zero already
+int tm_engine::clear_dedup_table(tm_batch* b, hipStream_t S) {
+    if (b->dtab_dirty) HIP_OK(hipMemsetAsync(b->d_dtab, 0, (b->dtab_mask + 1) * 8, S));
+    b->dtab_dirty = true;   // until this pass's expansion has been waited for
     return TM_OK;
 }
 
@@ -716,6 +735,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         if (grc != 1 && grc) return grc;
     }
     bool csr_done = false;
+    if (dedup_now && (rc = clear_dedup_table(b, S))) return rc;   // (outside the capture below)
     if (dgraph) {
         const DedupArgs d = dedup_args(b);
         std::vector<uint8_t> key(sizeof t + sizeof ts + sizeof a + sizeof s + sizeof d);
@@ -1016,6 +1036,7 @@ int tm_engine::wait(tm_batch* b, bool drained, uint32_t* relaunched) {
     }
     fill_stats(b);
     b->done = true;
+    if (b->dedup_dev) b->dtab_dirty = false;   // (its expansion cleared the claimed slots)
     // (dense_enq, not eager_dense: the pipelined caller clears eager_dense
     // right after launch, while the tail it asked for is already queued)
     b->dense = b->dense_enq && !b->oneshot && b->total <= b->dense_cap;

@@ -494,15 +494,19 @@ struct tm_batch {
     bool dedup_stale = false;       // fresh bytes (prepare / retokenize): the next launch deduplicates
     bool dedup_timed = false;       // the last launch deduplicated: evd.. is its time
     bool rowof_host = false;        // row_of holds the device map of the last dedup pass
-    unsigned long long *d_dtab = nullptr, *d_psrc = nullptr;
-    uint32_t *d_drep = nullptr, *d_dflag = nullptr, *d_dblen = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
+    unsigned long long *d_dtab = nullptr, *d_psrc = nullptr, *d_dsrow = nullptr, *d_dbits = nullptr;
+    uint32_t *d_dslot = nullptr, *d_dbc = nullptr, *d_dbb = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
     uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
-    uint16_t* d_dlead = nullptr;
     uint8_t* d_cbytes = nullptr;
     uint64_t* d_coffs = nullptr;
-    size_t c_dtab = 0, c_psrc = 0, c_drep = 0, c_dflag = 0, c_dblen = 0, c_drbs = 0, c_dbbs = 0, c_rowof = 0;
-    size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0, c_dlead = 0;
+    size_t c_dtab = 0, c_psrc = 0, c_dsrow = 0, c_dbits = 0, c_dslot = 0, c_dbc = 0, c_dbb = 0, c_drbs = 0,
+           c_dbbs = 0, c_rowof = 0;
+    size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0;
     uint64_t dtab_mask = 0, dd_bytes = 0;
+    // the table is zero between passes (the expansion clears the claimed
+    // slots); dirty: a pass was enqueued and its expansion not yet waited
+    // for, or the table is new -- the next pass clears it first
+    bool dtab_dirty = true;
     hipEvent_t evd = nullptr, evx0 = nullptr, evx1 = nullptr;   // before the dedup pass; around the expand
     uint64_t x_cap = 0;             // ids the last one-shot copy could hold
     uint8_t *h_xrow = nullptr, *h_xids = nullptr;
@@ -593,13 +597,14 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_dtab); dev_free(d_psrc); dev_free(d_drep); dev_free(d_dflag); dev_free(d_dblen); dev_free(d_drbs);
-        dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount); dev_free(d_cbytes); dev_free(d_coffs);
-        dev_free(d_dlead);
+        dev_free(d_dtab); dev_free(d_psrc); dev_free(d_dsrow); dev_free(d_dbits); dev_free(d_dslot); dev_free(d_dbc);
+        dev_free(d_dbb); dev_free(d_drbs); dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount);
+        dev_free(d_cbytes); dev_free(d_coffs);
+        dtab_dirty = true;
         dev_free(d_smp_meta); dev_free(d_smp_ids);
         c_smp_meta = c_smp_ids = 0;
-        c_dtab = c_psrc = c_drep = c_dflag = c_dblen = c_drbs = c_dbbs = c_rowof = 0;
-        c_dd = c_pcount = c_cbytes = c_coffs = c_dlead = 0;
+        c_dtab = c_psrc = c_dsrow = c_dbits = c_dslot = c_dbc = c_dbb = c_drbs = c_dbbs = c_rowof = 0;
+        c_dd = c_pcount = c_cbytes = c_coffs = 0;
         for (hipEvent_t* ev : {&evd, &evx0, &evx1}) {
             if (*ev) (void)hipEventDestroy(*ev);
             *ev = nullptr;
@@ -1965,6 +1970,7 @@ struct tm_engine {
 
     // the dedup pass over the batch's resident bytes, ahead of the tokeniser
     int enqueue_dedup(tm_batch* b, hipStream_t S);
+    int clear_dedup_table(tm_batch* b, hipStream_t S);
 
     int tokens_pending(tm_batch* b);
 

@@ -554,28 +554,40 @@ uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 
 // TM_BATCH_DEDUP on the device (tm_dedup_*), before the tokeniser:
 // identical publishes (equal bytes) are tokenised and walked once.  A
-// publish's representative is the FIRST publish with its bytes (a hash table
-// of u64 {tag | index}, the index lowered to the minimum with atomicMin), so
-// rows come out in first-occurrence order, deterministically -- the same
-// rows as the host's dedup.  The representatives' bytes are compacted
-// (cbytes / coffs) and only they are tokenised and walked; row_of maps every
-// publish to its row.  After the walk, tm_dedup_expand gives every publish
-// its row's (count, start): the per-publish result.
+// publish's representative is the FIRST publish with its bytes, so rows come
+// out in first-occurrence order, deterministically -- the same rows as the
+// host's dedup.  The representatives' bytes are compacted (cbytes / coffs) and
+// only they are tokenised and walked; after the walk, tm_dedup_expand gives
+// every publish its row (row_of) and its row's (count, start): the
+// per-publish result.  Passes (tm_kernels.hip):
+//   claim    every distinct topic of a workgroup claims one slot of the global
+//            table {1 | tag | len | byte offset}, checking the bytes of any
+//            occupant with its tag and length (exact: a slot holds one topic);
+//            equal topics lower the offset to the first occurrence (offsets
+//            grow with the publish index) -> slot[t]
+//   count    representative bits (offset == the slot's) -> repbits, and
+//            per 4,096-publish block the representatives and their bytes
+//   (two scans of the block sums)
+//   compact  each representative: its row, its bytes into cbytes, coffs, and
+//            srow[slot] = {publish << 32 | row}
+//   expand   (after the walk) row_of[t] = srow[slot[t]]; the representative
+//            clears its table slot, so the table is zero for the next pass
 struct DedupArgs {
     const uint8_t* bytes;     // the batch's publishes: bytes[offs[t] - base .. offs[t + 1] - base)
     const uint64_t* offs;
     uint64_t base;
     uint32_t n;
     uint32_t pad0_;           // (explicit padding: the struct's bytes are a graph cache key)
-    unsigned long long* table;   // mask + 1 slots, zeroed
+    unsigned long long* table;   // mask + 1 slots, zero between passes
     uint64_t mask;
-    uint32_t* rep;            // n: pass 1 the publish's table slot, pass 2 its representative
-    uint16_t* lead;           // n: pass 1's workgroup leader of the publish's hash (index in its workgroup)
-    uint32_t* rflag;          // n + 1: 1 at a representative; scanned in place -> row ids (block-local)
-    uint32_t* blen;           // n + 1: a representative's bytes; scanned in place -> byte offsets (block-local)
+    uint32_t* slot;           // n: the table slot of each publish's topic
+    unsigned long long* repbits;  // ceil(n / 64): bit t = publish t is its topic's representative
+    uint32_t* bcount;         // nblk + 1: representatives per DD_TILE block; scanned in place -> row bases
+    uint32_t* bbytes;         // nblk + 1: their bytes; scanned in place -> byte bases
     const uint32_t* rbs;      // block sums of the two scans (SCAN_TILE entries per block)
     const uint32_t* bbs;
-    uint32_t* row_of;         // n: row of each publish
+    unsigned long long* srow; // mask + 1: per claimed slot {representative << 32 | row}
+    uint32_t* row_of;         // n: row of each publish (written by the expansion)
     uint8_t* cbytes;          // the rows' bytes, the tokeniser's input (16-B aligned, + 32 bytes of slack)
     uint64_t* coffs;          // rows + 1 offsets into cbytes
     uint32_t* dd;             // [0] rows: the tokeniser's and the walk's topic count (TokArgs / MatchArgs d_n)
@@ -587,9 +599,12 @@ struct DedupArgs {
     unsigned long long* psrc;
     unsigned long long* stats;
     uint32_t weak_hash;       // test knob (TM_DEDUP_WEAK_HASH): hash = length only, every same-length
-                              // topic collides -- exercises the byte check of tm_dedup_mark
+                              // topic collides -- exercises the claim's byte check and probing
     uint32_t pad1_;
 };
+constexpr uint32_t DD_TILE = 4096;   // publishes per count / compact block
+constexpr uint32_t DD_OFF_BITS = 40; // byte offset bits of a table slot (a batch's bytes < 2^40)
+__host__ __device__ inline uint32_t dedup_blocks(uint32_t n) { return (n + DD_TILE - 1) / DD_TILE; }
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s);
 // A captured launch is keyed by the bytes of its argument structs

@@ -1598,234 +1598,288 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // fir
 
 
 
-// 8 bytes at any byte offset of a buffer, as a little-endian u64: two aligned
-// 8-B reads and a funnel shift (LDS windows and HBM byte arrays are 16-B
-// aligned and padded, so the second read stays inside)
-struct GBytes {
-    const uint8_t* p;
-    __device__ __forceinline__ uint64_t at(uint64_t s) const {
-        const uint64_t* q = reinterpret_cast<const uint64_t*>(p + (s & ~7ull));
-        const uint32_t sh = (uint32_t)(s & 7u) * 8u;
-        const uint64_t lo = q[0];
-        return sh ? (lo >> sh) | (q[1] << (64u - sh)) : lo;
+// A topic's first 64 bytes as 8 little-endian u64 chunks, zero past len:
+// the 16-B aligned loads that cover them (the batch bytes are 16-B aligned
+// and padded by 16), all issued before any is used, and a funnel shift by the
+// topic's offset within the first load.  Lanes of a wave read neighbouring
+// topics, so a load instruction's lines are mostly the wave's next ones.
+__device__ __forceinline__ void dd_load64(const uint8_t* bytes, uint64_t b, uint32_t len, uint64_t (&c)[8]) {
+    const uint64_t a0 = b & ~15ull;
+    const uint32_t sh = (uint32_t)(b & 15u);
+    const uint32_t need = sh + (len < 64u ? len : 64u);
+    uint64_t w[10];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (16u * k < need) v = *reinterpret_cast<const uint4*>(bytes + a0 + 16u * k);
+        w[2 * k] = ((uint64_t)v.y << 32) | v.x;
+        w[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
     }
-};
-struct LBytes {
-    const uint8_t* p;   // 4-B aligned LDS
-    __device__ __forceinline__ uint64_t at(uint64_t s) const { return lds_u64(p, (uint32_t)s); }
-};
-
-// a byte range's two 32-bit word hashes (the dictionary's chunk mixing) with
-// its length, as one 64-bit key, 8 bytes a step
-template <class B>
-__device__ __forceinline__ uint64_t bytes_hash(B src, uint64_t s, uint32_t n) {
-    uint32_t h1 = HW_SEED, h2 = HW_SEED2;
-    for (uint32_t i = 0; i < n; i += 8) {
-        const uint64_t c = low_bytes(src.at(s + i), n - i < 8 ? n - i : 8);
-        uint32_t d = mix_chunk((uint32_t)c);
-        h1 = hw_acc(h1, d);
-        h2 = hw_acc(h2, d);
-        d = mix_chunk((uint32_t)(c >> 32));
-        h1 = hw_acc(h1, d);
-        h2 = hw_acc(h2, d);
+    const bool odd = sh >= 8u;
+    const uint32_t bs = (sh & 7u) * 8u;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint64_t lo = odd ? w[j + 1] : w[j];
+        const uint64_t hi = odd ? w[j + 2] : w[j + 1];
+        const uint64_t v = bs ? (lo >> bs) | (hi << (64u - bs)) : lo;
+        const uint32_t k = 8u * j;
+        c[j] = k >= len ? 0ull : low_bytes(v, len - k < 8u ? len - k : 8u);
     }
-    return ((uint64_t)hw_final(h1, n) << 32) | hw_final(h2, n ^ 0x5BD1E995u);
 }
 
-// equal byte ranges of length n?  (8 bytes a step; the reads of a step are independent)
-template <class B, class C>
-__device__ __forceinline__ bool bytes_equal(B x, uint64_t sx, C y, uint64_t sy, uint32_t n) {
+__device__ __forceinline__ uint64_t dd_mix(uint64_t h, uint64_t c) {
+    c *= 0x87C37B91114253D5ull;
+    c = (c << 31) | (c >> 33);
+    c *= 0x4CF5AD432745937Full;
+    h ^= c;
+    h = (h << 27) | (h >> 37);
+    return h * 5u + 0x52DCE729ull;
+}
+
+// 64-bit hash of a topic: its 8-B chunks mixed in order, then its length
+__device__ __forceinline__ uint64_t dd_hash(const uint8_t* bytes, uint64_t b, uint32_t len, const uint64_t (&c)[8]) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) h = dd_mix(h, c[j]);
+    for (uint32_t k = 64; k < len; k += 64) {   // (topics over 64 bytes: the next 64 at a time)
+        uint64_t x[8];
+        dd_load64(bytes, b + k, len - k, x);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) h = dd_mix(h, x[j]);
+    }
+    h ^= (uint64_t)len * 0xC2B2AE3D27D4EB4Full;
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ull;
+    return h ^ (h >> 33);
+}
+
+// the len bytes at b (first 64 in c) equal to the len bytes at ob?
+__device__ __forceinline__ bool dd_equal(const uint8_t* bytes, const uint64_t (&c)[8], uint64_t b, uint64_t ob,
+                                         uint32_t len) {
+    uint64_t o[8];
+    dd_load64(bytes, ob, len, o);
     uint64_t diff = 0;
-    for (uint32_t i = 0; i < n; i += 8) {
-        const uint32_t k = n - i < 8 ? n - i : 8;
-        diff |= low_bytes(x.at(sx + i) ^ y.at(sy + i), k);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) diff |= c[j] ^ o[j];
+    for (uint32_t k = 64; diff == 0 && k < len; k += 64) {
+        uint64_t x[8], y[8];
+        dd_load64(bytes, b + k, len - k, x);
+        dd_load64(bytes, ob + k, len - k, y);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) diff |= x[j] ^ y[j];
     }
     return diff == 0;
 }
 
-// the global table: find or claim the slot of the topic with hash h (see
-// tm_dedup_insert); slots are told apart by the hash (tag + home slot), the
-// bytes are checked after (tm_dedup_mark)
-__device__ __forceinline__ uint32_t dedup_global(const DedupArgs& a, uint32_t t, uint64_t h) {
-    const unsigned long long tag = (unsigned long long)((h >> 32) | 1u) << 32;
+// The global table: a slot holds ONE topic, {1 | 10 hash bits | length (13
+// bits) | byte offset (40 bits)}.  A claim probes from the hash's home; an
+// occupant with the same hash bits and length has its bytes compared, and
+// only equal bytes join it (lowering the offset with atomicMin: the topic's
+// first occurrence has the lowest offset -- offsets grow with the publish
+// index, strictly for non-empty topics); anything else probes on.  So a
+// slot's topic never changes once claimed, and a hash collision costs a
+// probe, never a wrong row.
+constexpr uint64_t DD_OFF_MASK = (1ull << DD_OFF_BITS) - 1ull;
+
+__device__ __forceinline__ uint32_t dd_claim(const DedupArgs& a, uint64_t h, uint64_t b, uint32_t len,
+                                             const uint64_t (&c)[8]) {
+    const unsigned long long want =
+        (1ull << 63) | (((h >> 54) & 0x3FFull) << 53) | ((uint64_t)len << DD_OFF_BITS) | b;
     uint64_t i = h & a.mask;
     for (;;) {
         unsigned long long v = __hip_atomic_load(&a.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v == 0) {
-            v = atomicCAS(&a.table[i], 0ull, tag | t);
-            if (v == 0) break;
+            v = atomicCAS(&a.table[i], 0ull, want);
+            if (v == 0) return (uint32_t)i;
         }
-        if ((v & 0xFFFFFFFF00000000ull) == tag) {
-            if (t < (uint32_t)v) atomicMin(&a.table[i], tag | t);
-            break;
+        if ((v >> DD_OFF_BITS) == (want >> DD_OFF_BITS) && dd_equal(a.bytes, c, b, v & DD_OFF_MASK, len)) {
+            if (b < (v & DD_OFF_MASK)) atomicMin(&a.table[i], want);
+            return (uint32_t)i;
         }
         i = (i + 1) & a.mask;
     }
-    return (uint32_t)i;
 }
 
-// Pass 1, one thread per publish, DD_BLOCK publishes per workgroup: the slot
-// of the publish's 64-bit byte hash in the global table.  The slot holds
-// {tag (hash hi, | 1) << 32 | index}; a publish of the same hash with a lower
-// index lowers it (atomicMin: the tag bits are equal), so the slot ends at
-// the hash's first publish.  Slot values only change under device-scope
-// atomics, so a stale read costs at most a failed CAS, which returns the
-// current value.
-//
-// Hot topics would put hundreds of thousands of threads on one slot's line
-// (C5: Zipf over 10k hot topics, the first takes ~9% of the publishes), so
-// the workgroup first collapses its own publishes in LDS, where its bytes are
-// staged for hashing: equal hashes elect the lowest publish as the
-// workgroup's leader, and only leaders touch the global table; followers
-// take their leader's slot.
-//
-// Exactness: a publish is a row's member only if its BYTES equal the row's
-// first publish's -- tm_dedup_mark compares every publish with its
-// representative, and one whose bytes differ (a 64-bit hash collision) is
-// made a row of its own.  Rows then stay exact; at worst a collided topic
-// gets more than one row.
-constexpr uint32_t DD_BLOCK = 512;
-constexpr uint32_t DD_LT = 1024;      // LDS slots (load <= 1/2)
-constexpr uint32_t DD_BCAP = 32768;   // the workgroup's bytes staged in LDS (more: hashed from HBM); 3 workgroups / CU
+// Pass 1 (claim), one thread per publish, its bytes in registers.  C5's hot
+// topics would put hundreds of thousands of claims on one slot's line (Zipf
+// over 10k hot topics, the first ~9% of the publishes), so the workgroup first
+// collapses its own publishes in LDS: equal hashes elect the lowest thread,
+// whose bytes each follower compares with its own (a follower whose bytes
+// differ -- a 64-bit collision -- takes part in the next round's election), and
+// only the leaders claim global slots; followers take their leader's.
+constexpr uint32_t DD_BLOCK = 256;
+constexpr uint32_t DD_LT = 512;       // LDS election slots (load <= 1/2)
 
-__global__ __launch_bounds__(DD_BLOCK) void tm_dedup_insert(DedupArgs a) {
+__global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
     __shared__ unsigned long long lkey[DD_LT];
     __shared__ uint32_t lmin[DD_LT];
-    __shared__ uint32_t lslot[DD_LT];
-    __shared__ __attribute__((aligned(16))) uint8_t lbytes[DD_BCAP + 16];
-    for (uint32_t k = threadIdx.x; k < DD_LT; k += DD_BLOCK) {
-        lkey[k] = 0;
-        lmin[k] = NONE;
-    }
-    const uint32_t t0 = blockIdx.x * DD_BLOCK;
-    const uint32_t t = t0 + threadIdx.x;
+    __shared__ uint32_t lslot[DD_BLOCK];
+    __shared__ uint64_t lb[DD_BLOCK];
+    __shared__ uint32_t ll[DD_BLOCK];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t = blockIdx.x * DD_BLOCK + tid;
     const bool valid = t < a.n;
-    const uint64_t wb = a.offs[t0] - a.base, we = a.offs[min(t0 + DD_BLOCK, a.n)] - a.base;
-    const uint64_t w0 = wb & ~15ull;   // bytes[] is 16-B aligned: so are the window's loads
-    const bool staged = we - w0 <= DD_BCAP;
-    if (staged)
-        for (uint64_t k = 16u * threadIdx.x; k < we - w0; k += 16u * DD_BLOCK)
-            *reinterpret_cast<uint4*>(lbytes + k) = *reinterpret_cast<const uint4*>(a.bytes + w0 + k);
-    uint64_t b = 0;
-    uint32_t len = 0, s = 0;
-    uint64_t h = 0;
+    uint64_t b = 0, h = 0;
+    uint32_t len = 0;
     if (valid) {
         b = a.offs[t] - a.base;
         len = (uint32_t)(a.offs[t + 1] - a.base - b);
     }
-    __syncthreads();
+    uint64_t c[8];
+    dd_load64(a.bytes, b, len, c);
     if (valid) {
-        h = (staged ? bytes_hash(LBytes{lbytes}, b - w0, len) : bytes_hash(GBytes{a.bytes}, b, len)) | 1ull;   // (0: free)
+        h = dd_hash(a.bytes, b, len, c);
         if (a.weak_hash) h = ((uint64_t)len << 40) | ((uint64_t)len << 8) | 1ull;
-        s = (uint32_t)(h >> 7) & (DD_LT - 1);
-        for (;;) {
-            const unsigned long long o = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
-            if (o == 0 || o == h) break;
-            s = (s + 1) & (DD_LT - 1);
+    }
+    lb[tid] = b;
+    ll[tid] = len;
+    bool pend = valid, leader = false;
+    uint32_t lead = tid, s = 0;
+    while (__syncthreads_or(pend)) {
+        for (uint32_t k = tid; k < DD_LT; k += DD_BLOCK) {
+            lkey[k] = 0;
+            lmin[k] = NONE;
         }
-        atomicMin(&lmin[s], threadIdx.x);
-    }
-    __syncthreads();
-    const bool lead = valid && lmin[s] == threadIdx.x;
-    if (lead) lslot[s] = dedup_global(a, t, h);
-    __syncthreads();
-    if (valid) {
-        if (lead) a.rep[t] = lslot[s];   // (followers take their leader's verdict in pass 2)
-        a.lead[t] = (uint16_t)lmin[s];
-    }
-}
-
-// Pass 2: the representative of every publish -- the first publish of its
-// hash, kept only if the bytes are equal -- and the scan inputs (1 per
-// representative, and its byte count).  Same workgroups as pass 1, bytes
-// staged in LDS: each workgroup leader checks its bytes against the
-// representative's (HBM), each follower against its leader's (LDS) and then
-// shares its leader's verdict.  A publish whose bytes differ from its
-// representative's (a 64-bit hash collision) is its own; its equal
-// followers follow it.
-__global__ __launch_bounds__(DD_BLOCK) void tm_dedup_mark(DedupArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lbytes[DD_BCAP + 16];
-    __shared__ uint32_t lb[DD_BLOCK], ll[DD_BLOCK], lrep[DD_BLOCK];
-    const uint32_t t0 = blockIdx.x * DD_BLOCK;
-    const uint32_t t = t0 + threadIdx.x;
-    const bool valid = t < a.n;
-    const uint64_t wb = a.offs[t0] - a.base, we = a.offs[min(t0 + DD_BLOCK, a.n)] - a.base;
-    const uint64_t w0 = wb & ~15ull;
-    const bool staged = we - w0 <= DD_BCAP;
-    if (staged)
-        for (uint64_t k = 16u * threadIdx.x; k < we - w0; k += 16u * DD_BLOCK)
-            *reinterpret_cast<uint4*>(lbytes + k) = *reinterpret_cast<const uint4*>(a.bytes + w0 + k);
-    uint64_t b = 0, rb = 0, re = 0;
-    uint32_t len = 0, r = 0, lead = 0;
-    if (valid) {
-        b = a.offs[t] - a.base;
-        len = (uint32_t)(a.offs[t + 1] - a.base - b);
-        lb[threadIdx.x] = (uint32_t)(b - w0);
-        ll[threadIdx.x] = len;
-        lead = a.lead[t];
-        if (lead == threadIdx.x) {   // (only leaders read the table)
-            r = (uint32_t)a.table[a.rep[t]];
-            if (r != t) {   // the representative's bounds, in flight with the staging loads
-                rb = a.offs[r] - a.base;
-                re = a.offs[r + 1] - a.base;
+        __syncthreads();
+        if (pend) {
+            s = (uint32_t)(h >> 7) & (DD_LT - 1);
+            for (;;) {
+                const unsigned long long o = atomicCAS(&lkey[s], 0ull, (unsigned long long)(h | 1ull));
+                if (o == 0 || o == (h | 1ull)) break;
+                s = (s + 1) & (DD_LT - 1);
+            }
+            atomicMin(&lmin[s], tid);
+        }
+        __syncthreads();
+        if (pend) {
+            const uint32_t L = lmin[s];
+            if (L == tid) {
+                leader = true;
+                pend = false;
+            } else if (ll[L] == len && dd_equal(a.bytes, c, b, lb[L], len)) {
+                lead = L;
+                pend = false;
             }
         }
     }
+    if (leader) lslot[tid] = dd_claim(a, h, b, len, c);
     __syncthreads();
-    const GBytes g{a.bytes};
-    if (valid && lead == threadIdx.x) {   // a leader: its bytes against the representative's
-        if (r != t) {
-            bool eq = re - rb == len;
-            if (eq) eq = staged ? bytes_equal(g, rb, LBytes{lbytes}, b - w0, len) : bytes_equal(g, rb, g, b, len);
-            if (!eq) r = t;
-        }
-        lrep[threadIdx.x] = r;
-    }
-    __syncthreads();
-    if (!valid) return;
-    if (lead != threadIdx.x) {   // a follower: equal to its leader, then the leader's representative
-        const uint64_t ob = w0 + lb[lead];
-        bool eq = ll[lead] == len;
-        if (eq) eq = staged ? bytes_equal(LBytes{lbytes}, lb[lead], LBytes{lbytes}, b - w0, len) : bytes_equal(g, ob, g, b, len);
-        r = eq ? lrep[lead] : t;
-    }
-    a.rep[t] = r;
-    const bool first = r == t;
-    a.rflag[t] = first ? 1u : 0u;
-    a.blen[t] = first ? len : 0u;
+    if (valid) a.slot[t] = lslot[lead];
 }
 
-// Pass 3 (after the two scans): row of every publish; each representative
-// copies its bytes to its row of the tokeniser's input
-__global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t == 0) {   // totals: the scans left them at [n]
-        const uint32_t rows = a.rflag[a.n];
-        a.coffs[0] = 0;
-        a.coffs[rows] = a.blen[a.n];
-        a.dd[0] = rows;
-    }
-    if (t >= a.n) return;
-    const uint32_t r = a.rep[t];
-    const uint32_t row = a.rflag[r] + a.rbs[r / SCAN_TILE];
-    a.row_of[t] = row;
-    if (r != t) return;
-    const uint64_t b = a.offs[t] - a.base, e = a.offs[t + 1] - a.base;
-    const uint64_t o = (uint64_t)a.blen[t] + a.bbs[t / SCAN_TILE];
-    if (row) a.coffs[row] = o;
-    const GBytes g{a.bytes};
-    for (uint64_t k = 0; k < e - b; k += 8) {   // 8-B reads, byte stores (rows are packed, unaligned)
-        const uint64_t v = g.at(b + k);
-        const uint32_t m = e - b - k < 8 ? (uint32_t)(e - b - k) : 8u;
+// Pass 2 (count): publish t is its topic's representative when its offset is
+// the slot's (an empty topic: the first of the empty publishes at that
+// offset).  Ballots -> repbits; per DD_TILE block the representatives and
+// their bytes -> bcount / bbytes (scanned next).  16 independent slot ->
+// table chains per thread in flight.
+constexpr uint32_t DD_PT = DD_TILE / 256;
+
+__global__ __launch_bounds__(256) void tm_dedup_count(DedupArgs a) {
+    __shared__ uint32_t sc[4], sb[4];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t0 = blockIdx.x * DD_TILE;
+    uint32_t cnt = 0, byt = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            if (j < m) a.cbytes[o + k + j] = (uint8_t)(v >> (8 * j));
+    for (uint32_t u = 0; u < DD_PT; ++u) {
+        const uint32_t t = t0 + u * 256 + tid;
+        bool rep = false;
+        uint32_t len = 0;
+        if (t < a.n) {
+            const unsigned long long v = a.table[a.slot[t]];
+            const uint64_t o0 = a.offs[t], o1 = a.offs[t + 1];
+            const uint64_t b = o0 - a.base;
+            len = (uint32_t)(o1 - o0);
+            rep = (v & DD_OFF_MASK) == b && (len || t == 0 || a.offs[t - 1] != o0);
+        }
+        const uint64_t bits = __ballot(rep);
+        if ((tid & 63) == 0) a.repbits[(t0 + u * 256 + tid) / 64] = bits;
+        cnt += rep ? 1u : 0u;
+        byt += rep ? len : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        byt += __shfl_xor(byt, o, 64);
+    }
+    if ((tid & 63) == 0) {
+        sc[tid >> 6] = cnt;
+        sb[tid >> 6] = byt;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.bcount[blockIdx.x] = sc[0] + sc[1] + sc[2] + sc[3];
+        a.bbytes[blockIdx.x] = sb[0] + sb[1] + sb[2] + sb[3];
     }
 }
 
-// After the walk: every publish gets its row's (count, start) -- the result
-// per publish -- and the batch's delivered matches are summed (one atomic per
-// block)
+// exclusive scan of one u64 per thread over a 256-thread block (-> the block total)
+__device__ __forceinline__ uint64_t block256_excl_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t incl = v;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) sh[wid] = incl;
+    __syncthreads();
+    uint64_t base = 0;
+    for (uint32_t w = 0; w < wid; ++w) base += sh[w];
+    total = sh[0] + sh[1] + sh[2] + sh[3];
+    return base + incl - v;
+}
+
+// Pass 3 (compact), same blocks, 16 consecutive publishes per thread: every
+// representative's row and byte offset (block base from the scans + its rank
+// in the block), its bytes copied into the tokeniser's input, and
+// srow[slot] = {publish << 32 | row} for the expansion.
+__global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
+    __shared__ uint64_t sh[4];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nblk = dedup_blocks(a.n);
+    const uint32_t first = blockIdx.x * DD_TILE + tid * DD_PT;
+    const uint32_t mine = (uint32_t)(a.repbits[first / 64] >> (first & 63)) & ((1u << DD_PT) - 1u);
+    uint32_t my_bytes = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < DD_PT; ++j) {
+        if ((mine >> j) & 1u) {
+            const uint32_t t = first + j;
+            my_bytes += (uint32_t)(a.offs[t + 1] - a.offs[t]);
+        }
+    }
+    uint64_t tot;
+    const uint64_t ex = block256_excl_scan(((uint64_t)my_bytes << 16) | (uint64_t)__popc(mine), sh, tot);
+    uint32_t row = a.bcount[blockIdx.x] + a.rbs[blockIdx.x / SCAN_TILE] + (uint32_t)(ex & 0xFFFFu);
+    uint64_t off = (uint64_t)a.bbytes[blockIdx.x] + a.bbs[blockIdx.x / SCAN_TILE] + (ex >> 16);
+    if (blockIdx.x == 0 && tid == 0) {   // totals: the scans left them at [nblk]
+        a.dd[0] = a.bcount[nblk];
+        a.coffs[a.bcount[nblk]] = a.bbytes[nblk];
+    }
+    for (uint32_t rest = mine; rest; rest &= rest - 1) {   // (representatives are few: not unrolled)
+        const uint32_t t = first + (uint32_t)__ffs(rest) - 1u;
+        a.srow[a.slot[t]] = ((unsigned long long)t << 32) | row;
+        a.coffs[row] = off;
+        const uint64_t b = a.offs[t] - a.base;
+        const uint32_t n = (uint32_t)(a.offs[t + 1] - a.offs[t]);
+        for (uint32_t k = 0; k < n; k += 64) {   // 16-B loads, byte stores (rows are packed, unaligned)
+            uint64_t x[8];
+            dd_load64(a.bytes, b + k, n - k, x);
+            const uint32_t m = n - k < 64u ? n - k : 64u;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+                for (uint32_t q = 8 * j; q < m && q < 8 * j + 8; ++q)
+                    a.cbytes[off + k + q] = (uint8_t)(x[j] >> (8 * (q & 7)));
+        }
+        ++row;
+        off += n;
+    }
+}
+
+// After the walk: every publish gets its row (row_of) and its row's (count,
+// start) -- the result per publish -- and the batch's delivered matches are
+// summed (one atomic per block).  A representative clears its table slot
+// (nothing reads the table after the compaction): the next dedup pass finds
+// it zero without a memset.
 constexpr uint32_t EXPAND_PER_THREAD = 16;
 __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     __shared__ unsigned long long sh[4];
@@ -1835,7 +1889,11 @@ __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const uint32_t t = base + u * 256;
         if (t < a.n) {
-            const uint32_t r = a.row_of[t];
+            const uint32_t s = a.slot[t];
+            const unsigned long long v = a.srow[s];
+            const uint32_t r = (uint32_t)v;
+            if ((uint32_t)(v >> 32) == t) a.table[s] = 0;
+            a.row_of[t] = r;
             const uint32_t c = a.count[r];
             a.pcount[t] = c;
             a.psrc[t] = a.src[r];
@@ -2833,13 +2891,13 @@ hipError_t launch_gather_rows(const uint32_t* src, const int64_t* src_off, const
 
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s) {
     if (!a.n) return hipGetLastError();
-    const dim3 g((a.n + 255) / 256);
-    hipLaunchKernelGGL(tm_dedup_insert, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
-    hipLaunchKernelGGL(tm_dedup_mark, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
+    const uint32_t nblk = dedup_blocks(a.n);
+    hipLaunchKernelGGL(tm_dedup_claim, dim3((a.n + DD_BLOCK - 1) / DD_BLOCK), dim3(DD_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(tm_dedup_count, dim3(nblk), dim3(256), 0, s, a);
     hipError_t e;
     if ((e = launch_scan(rows_scan, s, nullptr)) != hipSuccess) return e;
     if ((e = launch_scan(bytes_scan, s, nullptr)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tm_dedup_compact, g, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tm_dedup_compact, dim3(nblk), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

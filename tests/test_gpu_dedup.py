@@ -90,9 +90,12 @@ def test_device_dedup_edge_topics_match_the_oracle_per_publish():
 
 def test_device_dedup_hash_collisions_stay_exact():
     """TM_DEDUP_WEAK_HASH: the dedup's hash is the topic's length, so every
-    two topics of one length collide; the byte check of the mark pass must
-    keep each publish with a row of its own bytes (rows may then repeat a
-    topic, never mix two) -- results per publish still equal the oracle's."""
+    two topics of one length collide -- in the workgroup's election and in the
+    global table.  The claim compares bytes before joining a slot (a follower
+    whose bytes differ from its leader's runs in the next election, a claim
+    probes past an occupant with other bytes), so rows never mix two topics
+    and collisions cost no extra rows: one row per distinct topic, in
+    first-occurrence order, and every publish's result equals the oracle's."""
     import os
     os.environ["TM_DEDUP_WEAK_HASH"] = "1"
     try:
@@ -110,7 +113,7 @@ def test_device_dedup_hash_collisions_stay_exact():
     first = {}
     for i, r in enumerate(row_of.tolist()):
         assert first.setdefault(r, T[i]) == T[i]
-    assert n_rows > len(set(base))            # collided topics got rows of their own
+    assert n_rows == len(set(base))           # collisions resolved by the bytes, not by extra rows
     b.free()
 
 
