@@ -1627,6 +1627,14 @@ __device__ __forceinline__ void dd_load64(const uint8_t* bytes, uint64_t b, uint
     }
 }
 
+// 8 bytes at any offset of the padded batch bytes: two aligned 8-B loads and a funnel shift
+__device__ __forceinline__ uint64_t dd_u64(const uint8_t* bytes, uint64_t s) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(bytes + (s & ~7ull));
+    const uint32_t sh = (uint32_t)(s & 7u) * 8u;
+    const uint64_t lo = q[0];
+    return sh ? (lo >> sh) | (q[1] << (64u - sh)) : lo;
+}
+
 __device__ __forceinline__ uint64_t dd_mix(uint64_t h, uint64_t c) {
     c *= 0x87C37B91114253D5ull;
     c = (c << 31) | (c >> 33);
@@ -1641,12 +1649,8 @@ __device__ __forceinline__ uint64_t dd_hash(const uint8_t* bytes, uint64_t b, ui
     uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) h = dd_mix(h, c[j]);
-    for (uint32_t k = 64; k < len; k += 64) {   // (topics over 64 bytes: the next 64 at a time)
-        uint64_t x[8];
-        dd_load64(bytes, b + k, len - k, x);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) h = dd_mix(h, x[j]);
-    }
+    for (uint32_t k = 64; k < len; k += 8)   // (topics over 64 bytes: rare, kept narrow)
+        h = dd_mix(h, low_bytes(dd_u64(bytes, b + k), len - k < 8u ? len - k : 8u));
     h ^= (uint64_t)len * 0xC2B2AE3D27D4EB4Full;
     h ^= h >> 33;
     h *= 0xFF51AFD7ED558CCDull;
@@ -1663,13 +1667,8 @@ __device__ __forceinline__ bool dd_equal(const uint8_t* bytes, const uint64_t (&
     uint64_t diff = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) diff |= c[j] ^ o[j];
-    for (uint32_t k = 64; diff == 0 && k < len; k += 64) {
-        uint64_t x[8], y[8];
-        dd_load64(bytes, b + k, len - k, x);
-        dd_load64(bytes, ob + k, len - k, y);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) diff |= x[j] ^ y[j];
-    }
+    for (uint32_t k = 64; diff == 0 && k < len; k += 8)   // (topics over 64 bytes: rare, kept narrow)
+        diff |= low_bytes(dd_u64(bytes, b + k) ^ dd_u64(bytes, ob + k), len - k < 8u ? len - k : 8u);
     return diff == 0;
 }
 
@@ -1718,6 +1717,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
     __shared__ uint32_t lslot[DD_BLOCK];
     __shared__ uint64_t lb[DD_BLOCK];
     __shared__ uint32_t ll[DD_BLOCK];
+    __shared__ uint64_t lc[8][DD_BLOCK];   // every publish's first 64 bytes: a follower checks its leader's here
     const uint32_t tid = threadIdx.x;
     const uint32_t t = blockIdx.x * DD_BLOCK + tid;
     const bool valid = t < a.n;
@@ -1727,11 +1727,15 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
         b = a.offs[t] - a.base;
         len = (uint32_t)(a.offs[t + 1] - a.base - b);
     }
-    uint64_t c[8];
-    dd_load64(a.bytes, b, len, c);
-    if (valid) {
-        h = dd_hash(a.bytes, b, len, c);
-        if (a.weak_hash) h = ((uint64_t)len << 40) | ((uint64_t)len << 8) | 1ull;
+    {
+        uint64_t c[8];
+        dd_load64(a.bytes, b, len, c);
+        if (valid) {
+            h = dd_hash(a.bytes, b, len, c);
+            if (a.weak_hash) h = ((uint64_t)len << 40) | ((uint64_t)len << 8) | 1ull;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) lc[q][tid] = c[q];
     }
     lb[tid] = b;
     ll[tid] = len;
@@ -1758,13 +1762,30 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
             if (L == tid) {
                 leader = true;
                 pend = false;
-            } else if (ll[L] == len && dd_equal(a.bytes, c, b, lb[L], len)) {
-                lead = L;
-                pend = false;
+            } else if (ll[L] == len) {   // the leader's first 64 bytes from LDS, the rest (long topics) from HBM
+                uint64_t diff = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) diff |= lc[q][L] ^ lc[q][tid];
+                bool eq = diff == 0;
+                if (eq && len > 64u) {
+                    uint64_t c[8];
+#pragma unroll
+                    for (uint32_t q = 0; q < 8; ++q) c[q] = lc[q][tid];
+                    eq = dd_equal(a.bytes, c, b, lb[L], len);
+                }
+                if (eq) {
+                    lead = L;
+                    pend = false;
+                }
             }
         }
     }
-    if (leader) lslot[tid] = dd_claim(a, h, b, len, c);
+    if (leader) {
+        uint64_t c[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) c[q] = lc[q][tid];
+        lslot[tid] = dd_claim(a, h, b, len, c);
+    }
     __syncthreads();
     if (valid) a.slot[t] = lslot[lead];
 }
@@ -1780,19 +1801,28 @@ __global__ __launch_bounds__(256) void tm_dedup_count(DedupArgs a) {
     __shared__ uint32_t sc[4], sb[4];
     const uint32_t tid = threadIdx.x;
     const uint32_t t0 = blockIdx.x * DD_TILE;
+    // every load of a stage issued before the next stage's: slot + offsets,
+    // then the table (16 independent chains per thread)
+    uint32_t sl[DD_PT];
+    uint64_t o0[DD_PT], o1[DD_PT];
+#pragma unroll
+    for (uint32_t u = 0; u < DD_PT; ++u) {
+        const uint32_t t = t0 + u * 256 + tid;
+        const bool in = t < a.n;
+        sl[u] = in ? a.slot[t] : 0u;
+        o0[u] = in ? a.offs[t] : 0ull;
+        o1[u] = in ? a.offs[t + 1] : 0ull;
+    }
+    unsigned long long v[DD_PT];
+#pragma unroll
+    for (uint32_t u = 0; u < DD_PT; ++u) v[u] = (t0 + u * 256 + tid < a.n) ? a.table[sl[u]] : 0ull;
     uint32_t cnt = 0, byt = 0;
 #pragma unroll
     for (uint32_t u = 0; u < DD_PT; ++u) {
         const uint32_t t = t0 + u * 256 + tid;
-        bool rep = false;
-        uint32_t len = 0;
-        if (t < a.n) {
-            const unsigned long long v = a.table[a.slot[t]];
-            const uint64_t o0 = a.offs[t], o1 = a.offs[t + 1];
-            const uint64_t b = o0 - a.base;
-            len = (uint32_t)(o1 - o0);
-            rep = (v & DD_OFF_MASK) == b && (len || t == 0 || a.offs[t - 1] != o0);
-        }
+        const uint32_t len = (uint32_t)(o1[u] - o0[u]);
+        bool rep = t < a.n && (v[u] & DD_OFF_MASK) == o0[u] - a.base;
+        if (rep && !len && t) rep = a.offs[t - 1] != o0[u];   // (empty topics: the first at that offset)
         const uint64_t bits = __ballot(rep);
         if ((tid & 63) == 0) a.repbits[(t0 + u * 256 + tid) / 64] = bits;
         cnt += rep ? 1u : 0u;
@@ -1832,12 +1862,39 @@ __device__ __forceinline__ uint64_t block256_excl_scan(uint64_t v, uint64_t* sh,
 // Pass 3 (compact), same blocks, 16 consecutive publishes per thread: every
 // representative's row and byte offset (block base from the scans + its rank
 // in the block), its bytes copied into the tokeniser's input, and
-// srow[slot] = {publish << 32 | row} for the expansion.
+// srow[slot] = {publish << 32 | row} for the expansion.  A thread's
+// representatives get consecutive rows and one contiguous byte range, which it
+// writes as aligned dwords assembled in a shift register (byte stores only
+// for the partial dwords at its two ends, shared with its neighbours): the
+// first blocks hold most first occurrences (C5: ~1,900 of block 0's 4,096
+// publishes), and byte stores made them the kernel's tail.
+__device__ __forceinline__ void dd_put(uint8_t* dst, uint64_t lo, uint64_t hi, uint64_t& acc, uint32_t& bits,
+                                       uint64_t& w, uint32_t v, uint32_t nb) {
+    // append nb (<= 4) bytes of v at dword w's bit `bits`; full dwords inside
+    // [lo, hi) are stored whole, a dword reaching outside byte by byte
+    acc |= (uint64_t)v << bits;
+    bits += 8u * nb;
+    if (bits >= 32u) {
+        const uint64_t d0 = w * 4;
+        if (d0 >= lo && d0 + 4 <= hi) {
+            *reinterpret_cast<uint32_t*>(dst + d0) = (uint32_t)acc;
+        } else {
+            for (uint32_t q = 0; q < 4; ++q)
+                if (d0 + q >= lo && d0 + q < hi) dst[d0 + q] = (uint8_t)(acc >> (8 * q));
+        }
+        acc >>= 32;
+        bits -= 32u;
+        ++w;
+    }
+}
+
 __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     __shared__ uint64_t sh[4];
     const uint32_t tid = threadIdx.x;
     const uint32_t nblk = dedup_blocks(a.n);
     const uint32_t first = blockIdx.x * DD_TILE + tid * DD_PT;
+    const uint32_t row0 = a.bcount[blockIdx.x] + a.rbs[blockIdx.x / SCAN_TILE];
+    const uint64_t off0 = (uint64_t)a.bbytes[blockIdx.x] + a.bbs[blockIdx.x / SCAN_TILE];
     const uint32_t mine = (uint32_t)(a.repbits[first / 64] >> (first & 63)) & ((1u << DD_PT) - 1u);
     uint32_t my_bytes = 0;
 #pragma unroll
@@ -1849,29 +1906,40 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     }
     uint64_t tot;
     const uint64_t ex = block256_excl_scan(((uint64_t)my_bytes << 16) | (uint64_t)__popc(mine), sh, tot);
-    uint32_t row = a.bcount[blockIdx.x] + a.rbs[blockIdx.x / SCAN_TILE] + (uint32_t)(ex & 0xFFFFu);
-    uint64_t off = (uint64_t)a.bbytes[blockIdx.x] + a.bbs[blockIdx.x / SCAN_TILE] + (ex >> 16);
+    uint32_t row = row0 + (uint32_t)(ex & 0xFFFFu);
+    const uint64_t lo = off0 + (ex >> 16), hi = lo + my_bytes;   // this thread's bytes in cbytes
+    uint64_t off = lo;
     if (blockIdx.x == 0 && tid == 0) {   // totals: the scans left them at [nblk]
         a.dd[0] = a.bcount[nblk];
         a.coffs[a.bcount[nblk]] = a.bbytes[nblk];
     }
+    uint64_t acc = 0, w = lo >> 2;
+    uint32_t bits = 8u * (uint32_t)(lo & 3u);
     for (uint32_t rest = mine; rest; rest &= rest - 1) {   // (representatives are few: not unrolled)
         const uint32_t t = first + (uint32_t)__ffs(rest) - 1u;
         a.srow[a.slot[t]] = ((unsigned long long)t << 32) | row;
         a.coffs[row] = off;
         const uint64_t b = a.offs[t] - a.base;
         const uint32_t n = (uint32_t)(a.offs[t + 1] - a.offs[t]);
-        for (uint32_t k = 0; k < n; k += 64) {   // 16-B loads, byte stores (rows are packed, unaligned)
+        for (uint32_t k = 0; k < n; k += 64) {
             uint64_t x[8];
             dd_load64(a.bytes, b + k, n - k, x);
             const uint32_t m = n - k < 64u ? n - k : 64u;
 #pragma unroll
-            for (uint32_t j = 0; j < 8; ++j)
-                for (uint32_t q = 8 * j; q < m && q < 8 * j + 8; ++q)
-                    a.cbytes[off + k + q] = (uint8_t)(x[j] >> (8 * (q & 7)));
+            for (uint32_t q = 0; q < 16; ++q) {
+                if (4u * q >= m) break;
+                const uint32_t nb = m - 4u * q < 4u ? m - 4u * q : 4u;
+                const uint32_t v = (uint32_t)(x[q >> 1] >> (32 * (q & 1)));
+                dd_put(a.cbytes, lo, hi, acc, bits, w, nb == 4u ? v : (v & ((1u << (8 * nb)) - 1u)), nb);
+            }
         }
         ++row;
         off += n;
+    }
+    if (bits && hi > lo) {   // the last partial dword
+        const uint64_t d0 = w * 4;
+        for (uint32_t q = 0; q < 4; ++q)
+            if (d0 + q >= lo && d0 + q < hi) a.cbytes[d0 + q] = (uint8_t)(acc >> (8 * q));
     }
 }
 
@@ -1880,24 +1948,41 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
 // summed (one atomic per block).  A representative clears its table slot
 // (nothing reads the table after the compaction): the next dedup pass finds
 // it zero without a memset.
-constexpr uint32_t EXPAND_PER_THREAD = 16;
+constexpr uint32_t EXPAND_PER_THREAD = 8;
 __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     __shared__ unsigned long long sh[4];
-    unsigned long long sum = 0;
     const uint32_t base = blockIdx.x * 256 * EXPAND_PER_THREAD + threadIdx.x;
+    // staged: every slot, then every srow entry, then every row's count and
+    // start -- each stage's loads in flight together (three dependent levels)
+    uint32_t sl[EXPAND_PER_THREAD];
+#pragma unroll
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
+        const uint32_t t = base + u * 256;
+        sl[u] = t < a.n ? a.slot[t] : 0u;
+    }
+    unsigned long long v[EXPAND_PER_THREAD];
+#pragma unroll
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) v[u] = base + u * 256 < a.n ? a.srow[sl[u]] : 0ull;
+    uint32_t c[EXPAND_PER_THREAD];
+    unsigned long long sr[EXPAND_PER_THREAD];
+#pragma unroll
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
+        const bool in = base + u * 256 < a.n;
+        c[u] = in ? a.count[(uint32_t)v[u]] : 0u;
+        sr[u] = in ? a.src[(uint32_t)v[u]] : 0ull;
+    }
+    unsigned long long sum = 0;
 #pragma unroll
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const uint32_t t = base + u * 256;
         if (t < a.n) {
-            const uint32_t s = a.slot[t];
-            const unsigned long long v = a.srow[s];
-            const uint32_t r = (uint32_t)v;
-            if ((uint32_t)(v >> 32) == t) a.table[s] = 0;
-            a.row_of[t] = r;
-            const uint32_t c = a.count[r];
-            a.pcount[t] = c;
-            a.psrc[t] = a.src[r];
-            sum += c;
+            // the representative clears its slot (nothing reads the table
+            // after the compaction): the next pass finds it zero
+            if ((uint32_t)(v[u] >> 32) == t) a.table[sl[u]] = 0;
+            a.row_of[t] = (uint32_t)v[u];
+            a.pcount[t] = c[u];
+            a.psrc[t] = sr[u];
+            sum += c[u];
         }
     }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);

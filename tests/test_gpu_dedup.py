@@ -60,7 +60,11 @@ def test_device_dedup_edge_topics_match_the_oracle_per_publish():
         eng.insert(f)
     base = [b"a/b", b"a/b", b"$x/a", b"%x/a", b"$x/a", b"", b"", b"/", b"a//b", b"a//b", b"+x/y", b"+x/y",
             b"a/zz1", b"a/zz2", b"x/y", b"x/y/", b"a/b/c/d/e/f/g/h/i/j/k/l/m", b"a/b/c/d/e/f/g/h/i/j/k/l/m",
-            b"$SYS/x", b"$SYS/x", b"a/1/2/3/4/5/6/7/8/9/10/11/12", b"q"]
+            b"$SYS/x", b"$SYS/x", b"a/1/2/3/4/5/6/7/8/9/10/11/12", b"q",
+            # long topics (over the 64 bytes the dedup keeps in registers): equal
+            # heads, different tails at bytes 65, 130 and 4,000
+            b"L/" + b"x" * 62 + b"/1", b"L/" + b"x" * 62 + b"/2", b"L/" + b"y" * 126 + b"/1",
+            b"L/" + b"y" * 126 + b"/2", b"L/" + b"z" * 3996 + b"/1", b"L/" + b"z" * 3996 + b"/2"]
     T = [base[(i * 7) % len(base)] for i in range(3000)]
     b = eng.prepare(T, dedup=True)
     b.launch().wait()
