@@ -494,11 +494,13 @@ struct tm_batch {
     bool dedup_stale = false;       // fresh bytes (prepare / retokenize): the next launch deduplicates
     bool dedup_timed = false;       // the last launch deduplicated: evd.. is its time
     bool rowof_host = false;        // row_of holds the device map of the last dedup pass
-    unsigned long long *d_dtab = nullptr, *d_psrc = nullptr, *d_dsrow = nullptr, *d_dbits = nullptr;
+    unsigned long long *d_dtab = nullptr, *d_psrc = nullptr, *d_dbits = nullptr;
     uint32_t *d_dslot = nullptr, *d_dbc = nullptr, *d_dbb = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
+    uint32_t *d_dsrow = nullptr, *d_drrep = nullptr;
     uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
     uint8_t* d_cbytes = nullptr;
     uint64_t* d_coffs = nullptr;
+    size_t c_drrep = 0;
     size_t c_dtab = 0, c_psrc = 0, c_dsrow = 0, c_dbits = 0, c_dslot = 0, c_dbc = 0, c_dbb = 0, c_drbs = 0,
            c_dbbs = 0, c_rowof = 0;
     size_t c_dd = 0, c_pcount = 0, c_cbytes = 0, c_coffs = 0;
@@ -597,6 +599,8 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
+        dev_free(d_drrep);
+        c_drrep = 0;
         dev_free(d_dtab); dev_free(d_psrc); dev_free(d_dsrow); dev_free(d_dbits); dev_free(d_dslot); dev_free(d_dbc);
         dev_free(d_dbb); dev_free(d_drbs); dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount);
         dev_free(d_cbytes); dev_free(d_coffs);

@@ -568,8 +568,8 @@ uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 //   count    representative bits (offset == the slot's) -> repbits, and
 //            per 4,096-publish block the representatives and their bytes
 //   (two scans of the block sums)
-//   compact  each representative: its row, its bytes into cbytes, coffs, and
-//            srow[slot] = {publish << 32 | row}
+//   compact  each representative: its row, its bytes into cbytes, coffs,
+//            srow[slot] = row and rrep[row] = the representative
 //   expand   (after the walk) row_of[t] = srow[slot[t]]; the representative
 //            clears its table slot, so the table is zero for the next pass
 struct DedupArgs {
@@ -586,7 +586,8 @@ struct DedupArgs {
     uint32_t* bbytes;         // nblk + 1: their bytes; scanned in place -> byte bases
     const uint32_t* rbs;      // block sums of the two scans (SCAN_TILE entries per block)
     const uint32_t* bbs;
-    unsigned long long* srow; // mask + 1: per claimed slot {representative << 32 | row}
+    uint32_t* srow;           // mask + 1: per claimed slot, its row
+    uint32_t* rrep;           // n: per row, its representative publish
     uint32_t* row_of;         // n: row of each publish (written by the expansion)
     uint8_t* cbytes;          // the rows' bytes, the tokeniser's input (16-B aligned, + 32 bytes of slack)
     uint64_t* coffs;          // rows + 1 offsets into cbytes
@@ -602,7 +603,7 @@ struct DedupArgs {
                               // topic collides -- exercises the claim's byte check and probing
     uint32_t pad1_;
 };
-constexpr uint32_t DD_TILE = 4096;   // publishes per count / compact block
+constexpr uint32_t DD_TILE = 1024;   // publishes per count / compact block
 constexpr uint32_t DD_OFF_BITS = 40; // byte offset bits of a table slot (a batch's bytes < 2^40)
 __host__ __device__ inline uint32_t dedup_blocks(uint32_t n) { return (n + DD_TILE - 1) / DD_TILE; }
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);

@@ -1862,12 +1862,13 @@ __device__ __forceinline__ uint64_t block256_excl_scan(uint64_t v, uint64_t* sh,
 // Pass 3 (compact), same blocks, 16 consecutive publishes per thread: every
 // representative's row and byte offset (block base from the scans + its rank
 // in the block), its bytes copied into the tokeniser's input, and
-// srow[slot] = {publish << 32 | row} for the expansion.  A thread's
+// srow[slot] = row, rrep[row] = publish for the expansion.  A thread's
 // representatives get consecutive rows and one contiguous byte range, which it
 // writes as aligned dwords assembled in a shift register (byte stores only
 // for the partial dwords at its two ends, shared with its neighbours): the
-// first blocks hold most first occurrences (C5: ~1,900 of block 0's 4,096
-// publishes), and byte stores made them the kernel's tail.
+// first blocks hold most first occurrences (C5: ~1,900 of the first 4,096
+// publishes), and byte stores made them the kernel's tail; 4 publishes per
+// thread keep a thread's serial representatives few.
 __device__ __forceinline__ void dd_put(uint8_t* dst, uint64_t lo, uint64_t hi, uint64_t& acc, uint32_t& bits,
                                        uint64_t& w, uint32_t v, uint32_t nb) {
     // append nb (<= 4) bytes of v at dword w's bit `bits`; full dwords inside
@@ -1917,7 +1918,8 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     uint32_t bits = 8u * (uint32_t)(lo & 3u);
     for (uint32_t rest = mine; rest; rest &= rest - 1) {   // (representatives are few: not unrolled)
         const uint32_t t = first + (uint32_t)__ffs(rest) - 1u;
-        a.srow[a.slot[t]] = ((unsigned long long)t << 32) | row;
+        a.srow[a.slot[t]] = row;
+        a.rrep[row] = t;
         a.coffs[row] = off;
         const uint64_t b = a.offs[t] - a.base;
         const uint32_t n = (uint32_t)(a.offs[t + 1] - a.offs[t]);
@@ -1952,24 +1954,24 @@ constexpr uint32_t EXPAND_PER_THREAD = 8;
 __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     __shared__ unsigned long long sh[4];
     const uint32_t base = blockIdx.x * 256 * EXPAND_PER_THREAD + threadIdx.x;
-    // staged: every slot, then every srow entry, then every row's count and
-    // start -- each stage's loads in flight together (three dependent levels)
-    uint32_t sl[EXPAND_PER_THREAD];
+    // staged: every slot, then every slot's row, then every row's count,
+    // start and representative -- each stage's loads in flight together
+    uint32_t sl[EXPAND_PER_THREAD], r[EXPAND_PER_THREAD];
 #pragma unroll
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const uint32_t t = base + u * 256;
         sl[u] = t < a.n ? a.slot[t] : 0u;
     }
-    unsigned long long v[EXPAND_PER_THREAD];
 #pragma unroll
-    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) v[u] = base + u * 256 < a.n ? a.srow[sl[u]] : 0ull;
-    uint32_t c[EXPAND_PER_THREAD];
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) r[u] = base + u * 256 < a.n ? a.srow[sl[u]] : 0u;
+    uint32_t c[EXPAND_PER_THREAD], rep[EXPAND_PER_THREAD];
     unsigned long long sr[EXPAND_PER_THREAD];
 #pragma unroll
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const bool in = base + u * 256 < a.n;
-        c[u] = in ? a.count[(uint32_t)v[u]] : 0u;
-        sr[u] = in ? a.src[(uint32_t)v[u]] : 0ull;
+        c[u] = in ? a.count[r[u]] : 0u;
+        sr[u] = in ? a.src[r[u]] : 0ull;
+        rep[u] = in ? a.rrep[r[u]] : NONE;
     }
     unsigned long long sum = 0;
 #pragma unroll
@@ -1978,8 +1980,8 @@ __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
         if (t < a.n) {
             // the representative clears its slot (nothing reads the table
             // after the compaction): the next pass finds it zero
-            if ((uint32_t)(v[u] >> 32) == t) a.table[sl[u]] = 0;
-            a.row_of[t] = (uint32_t)v[u];
+            if (rep[u] == t) a.table[sl[u]] = 0;
+            a.row_of[t] = r[u];
             a.pcount[t] = c[u];
             a.psrc[t] = sr[u];
             sum += c[u];

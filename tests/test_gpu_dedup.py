@@ -65,7 +65,7 @@ def test_device_dedup_edge_topics_match_the_oracle_per_publish():
             # heads, different tails at bytes 65, 130 and 4,000
             b"L/" + b"x" * 62 + b"/1", b"L/" + b"x" * 62 + b"/2", b"L/" + b"y" * 126 + b"/1",
             b"L/" + b"y" * 126 + b"/2", b"L/" + b"z" * 3996 + b"/1", b"L/" + b"z" * 3996 + b"/2"]
-    T = [base[(i * 7) % len(base)] for i in range(3000)]
+    T = [base[(i * 11) % len(base)] for i in range(3000)]   # (11: coprime with len(base), every topic occurs)
     b = eng.prepare(T, dedup=True)
     b.launch().wait()
     row_of, n_rows = _check(eng, b, T)
