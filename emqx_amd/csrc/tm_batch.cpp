@@ -489,6 +489,7 @@ int tm_engine::reserve_dedup(tm_batch* b, uint64_t nbytes) {
     if (b->d_dtab != old_tab || old_mask != b->dtab_mask) b->dtab_dirty = true;
     if ((rc = dev_reserve(b->d_dsrow, b->c_dsrow, cap))) return rc;
     if ((rc = dev_reserve(b->d_drrep, b->c_drrep, std::max<size_t>(n, 1)))) return rc;
+    if ((rc = dev_reserve(b->d_dbsum, b->c_dbsum, n / DD_EXPAND_TILE + 2))) return rc;   // (expansion blocks)
     if ((rc = dev_reserve(b->d_dslot, b->c_dslot, std::max<size_t>(n, 1)))) return rc;
     if ((rc = dev_reserve(b->d_dbits, b->c_dbits, std::max<size_t>(nblk, 1) * (DD_TILE / 64)))) return rc;
     if ((rc = dev_reserve(b->d_dbc, b->c_dbc, nblk + 1))) return rc;
@@ -518,6 +519,7 @@ DedupArgs tm_engine::dedup_args(tm_batch* b) const {
     d.row_of = b->d_rowof; d.cbytes = b->d_cbytes; d.coffs = b->d_coffs; d.dd = b->d_dd;
     d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
     d.stats = b->d_stats;
+    d.bsum = b->d_dbsum;
     d.weak_hash = dedup_weak_hash ? 1u : 0u;
     return d;
 }
@@ -678,6 +680,8 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     a.xg = b->d_ctrl + XG_WORD;
     a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
     a.stats = b->d_stats;
+    if ((rc = dev_reserve(b->d_wstats, b->c_wstats, (size_t)a.grid * WSTATS))) return rc;
+    a.wstats = b->d_wstats;
     a.s_qparent = b->d_sqpar; a.s_qpw = b->d_sqpw; a.s_qmeta = b->d_sqmeta; a.s_qkey = b->d_sqkey;
     a.s_ofid = b->d_sofid; a.s_okey = b->d_sokey;
     a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;

@@ -432,6 +432,8 @@ struct tm_batch {
     // device outputs
     uint32_t *d_sfids = nullptr, *d_rowoff = nullptr, *d_ids = nullptr;
     unsigned long long* d_rows = nullptr;
+    unsigned long long* d_wstats = nullptr;   // the walk waves' partial stats
+    size_t c_wstats = 0;
     uint32_t *d_bsums = nullptr, *d_ovf = nullptr, *d_total = nullptr;
     size_t c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
     uint32_t* h_total = nullptr;
@@ -497,6 +499,8 @@ struct tm_batch {
     unsigned long long *d_dtab = nullptr, *d_psrc = nullptr, *d_dbits = nullptr;
     uint32_t *d_dslot = nullptr, *d_dbc = nullptr, *d_dbb = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
     uint32_t *d_dsrow = nullptr, *d_drrep = nullptr;
+    unsigned long long* d_dbsum = nullptr;
+    size_t c_dbsum = 0;
     uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
     uint8_t* d_cbytes = nullptr;
     uint64_t* d_coffs = nullptr;
@@ -599,8 +603,8 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_drrep);
-        c_drrep = 0;
+        dev_free(d_drrep); dev_free(d_dbsum);
+        c_drrep = c_dbsum = 0;
         dev_free(d_dtab); dev_free(d_psrc); dev_free(d_dsrow); dev_free(d_dbits); dev_free(d_dslot); dev_free(d_dbc);
         dev_free(d_dbb); dev_free(d_drbs); dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount);
         dev_free(d_cbytes); dev_free(d_coffs);
@@ -620,6 +624,8 @@ struct tm_batch {
         h_bad = nullptr;
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
         dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
+        dev_free(d_wstats);
+        c_wstats = 0;
         if (h_total) (void)hipHostFree(h_total);
         h_total = nullptr;
         dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total);

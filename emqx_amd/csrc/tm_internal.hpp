@@ -156,6 +156,7 @@ __host__ __device__ __forceinline__ uint64_t xg_top_read(const uint32_t* hdr, ui
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
 }
 
+constexpr uint32_t WSTATS = 8;   // u64 partial sums per walk wave (MatchArgs.wstats)
 struct MatchArgs {
     // trie replica
     const Slot* slots;
@@ -200,6 +201,7 @@ struct MatchArgs {
     uint32_t ovf_cap;
     uint32_t pad4_;
     unsigned long long* stats;
+    unsigned long long* wstats;   // or null: per walk wave WSTATS partial sums (tm_stats_reduce adds them up)
     // slow-path scratch
     uint32_t* s_qparent;
     uint32_t* s_qpw;
@@ -598,12 +600,14 @@ struct DedupArgs {
     const unsigned long long* src;
     uint32_t* pcount;         // n: per publish
     unsigned long long* psrc;
+    unsigned long long* bsum;  // the expansion's per-block sums of delivered matches
     unsigned long long* stats;
     uint32_t weak_hash;       // test knob (TM_DEDUP_WEAK_HASH): hash = length only, every same-length
                               // topic collides -- exercises the claim's byte check and probing
     uint32_t pad1_;
 };
 constexpr uint32_t DD_TILE = 1024;   // publishes per count / compact block
+constexpr uint32_t DD_EXPAND_TILE = 2048;   // publishes per expansion block (one partial sum each)
 constexpr uint32_t DD_OFF_BITS = 40; // byte offset bits of a table slot (a batch's bytes < 2^40)
 __host__ __device__ inline uint32_t dedup_blocks(uint32_t n) { return (n + DD_TILE - 1) / DD_TILE; }
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);

@@ -735,11 +735,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? 
         sW += __shfl_xor(sW, o, 64); sM += __shfl_xor(sM, o, 64);
         sP += __shfl_xor(sP, o, 64);
     }
-    if (lane == 0) {
+    if (lane == 0 && a.wstats) {
+        // the wave's sums, added up by tm_stats_reduce: ~4,000 waves ending
+        // together would queue 6 same-line device atomics each (~30 ns apiece)
+        unsigned long long* w = a.wstats + (uint64_t)blockIdx.x * WSTATS;
+        w[0] = sV; w[1] = sH; w[2] = sW; w[3] = sM;
+        w[4] = sP & ((1ull << 40) - 1); w[5] = sP >> 40;
+    } else if (lane == 0) {
         atomicAdd(&a.stats[ST_VISITS], sV); atomicAdd(&a.stats[ST_HASH], sH);
         atomicAdd(&a.stats[ST_WORDS], sW); atomicAdd(&a.stats[ST_MATCHES], sM);
         atomicAdd(&a.stats[ST_PROBES], sP & ((1ull << 40) - 1));
         atomicAdd(&a.stats[ST_ITERS], sP >> 40);
+    }
+}
+
+// the walk waves' sums -> the batch's stats (one block; after the walk)
+__global__ __launch_bounds__(256) void tm_stats_reduce(const unsigned long long* w, uint32_t waves,
+                                                       unsigned long long* stats) {
+    __shared__ unsigned long long sh[4][6];
+    unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < waves; i += 256)
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) v[k] += w[(uint64_t)i * WSTATS + k];
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const uint32_t k = threadIdx.x;
+        const unsigned long long t = sh[0][k] + sh[1][k] + sh[2][k] + sh[3][k];
+        const uint32_t idx[6] = {ST_VISITS, ST_HASH, ST_WORDS, ST_MATCHES, ST_PROBES, ST_ITERS};
+        if (t) atomicAdd(&stats[idx[k]], t);
     }
 }
 
@@ -1950,7 +1978,7 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
 // summed (one atomic per block).  A representative clears its table slot
 // (nothing reads the table after the compaction): the next dedup pass finds
 // it zero without a memset.
-constexpr uint32_t EXPAND_PER_THREAD = 8;
+constexpr uint32_t EXPAND_PER_THREAD = DD_EXPAND_TILE / 256;
 __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     __shared__ unsigned long long sh[4];
     const uint32_t base = blockIdx.x * 256 * EXPAND_PER_THREAD + threadIdx.x;
@@ -1990,10 +2018,25 @@ __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sum;
     __syncthreads();
+    // a partial sum per block, added up by tm_dedup_sum: one same-address
+    // atomic per block serialised at ~30 ns each (4,883 blocks: ~0.15 ms)
+    if (threadIdx.x == 0) a.bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// the expansion's block sums -> the batch's delivered matches; the rows for
+// the host's read-back
+__global__ __launch_bounds__(1024) void tm_dedup_sum(DedupArgs a, uint32_t nb) {
+    __shared__ unsigned long long sh[16];
+    unsigned long long s = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += 1024) s += a.bsum[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long s4 = sh[0] + sh[1] + sh[2] + sh[3];
-        if (s4) atomicAdd(&a.stats[ST_DELIVERED], s4);
-        if (blockIdx.x == 0) a.ctrl[CTRL_NROWS] = a.dd[0];   // the rows, for the host's read-back
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < 16; ++w) t += sh[w];
+        if (t) atomicAdd(&a.stats[ST_DELIVERED], t);
+        a.ctrl[CTRL_NROWS] = a.dd[0];
     }
 }
 
@@ -2875,6 +2918,7 @@ static hipError_t launch_match_t(const MatchArgs& a, hipStream_t s, hipEvent_t e
         else hipLaunchKernelGGL((tm_match_tiles<CK, BIG, 512>), dim3(grid), dim3(64), 0, s, a);
     }
     if (ev_b && (e = hipEventRecordWithFlags(ev_b, s, ev_flags)) != hipSuccess) return e;
+    if (ntiles && a.wstats) hipLaunchKernelGGL(tm_stats_reduce, dim3(1), dim3(256), 0, s, a.wstats, a.grid, a.stats);
     hipLaunchKernelGGL((tm_match_slow<CK, BIG>), dim3(a.s_waves), dim3(64), 0, s, a);
     return hipSuccess;
 }
@@ -2990,7 +3034,8 @@ hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_s
 
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s) {
     const uint32_t g = (a.n + 256 * EXPAND_PER_THREAD - 1) / (256 * EXPAND_PER_THREAD);
-    hipLaunchKernelGGL(tm_dedup_expand, dim3(g ? g : 1u), dim3(256), 0, s, a);   // (block 0 reports the rows)
+    if (g) hipLaunchKernelGGL(tm_dedup_expand, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tm_dedup_sum, dim3(1), dim3(1024), 0, s, a, g);   // (also reports the rows)
     return hipGetLastError();
 }
 
