@@ -622,11 +622,9 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     // a fresh device-deduplicated batch (C5: every launch) replays its whole
     // sequence -- dedup, tokeniser, walk, expand, read-back -- as one captured
     // graph: ~25 enqueues cost ~0.2 ms of host time per launch otherwise
-    const bool fuse = tokenize_now && !checked && !b->dedup_dev && fresh_fused;
     const bool dgraph = csr && !checked && use_graphs && !b->gbad && b->dedup_dev && dedup_now && tokenize_now &&
                         !b->check_tokens;
     b->tok_timed = tokenize_now && csr;
-    // (a fresh batch's tokeniser fill runs inside the walk when fused: tm_match_fresh)
     TokArgs t{};
     ScanArgs ts{};
     if (tokenize_now) {
@@ -643,8 +641,6 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         if (b->dedup_dev) {   // the rows' bytes, compacted by the dedup pass
             t.bytes = b->d_cbytes; t.offs = b->d_coffs; t.base = 0; t.d_n = b->d_dd;
         }
-        // fused: one tile for both (any tile size is a valid walk tile)
-        if (fuse) t.tile_topics = std::min(t.tile_topics, tile_topics(b->n));
         ts.block_sums = b->d_bsums;
     }
     MatchArgs a{};
@@ -660,11 +656,6 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
     a.grid = match_waves(b->n, R.device, qcap);
     a.tile_topics = tile_topics(b->n);
-    if (fuse) {
-        a.tile_topics = t.tile_topics;
-        a.grid = (uint32_t)std::min<uint64_t>(((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics,
-                                              match_waves(0xFFFFFFF0u, R.device, qcap));
-    }
     a.qcap = qcap;
     {   // the first static_frac of the tiles round-robin, the tail by per-XCD tickets
         const uint64_t ntiles = ((uint64_t)b->n + a.tile_topics - 1) / a.tile_topics;
@@ -713,17 +704,14 @@ int tm_engine::launch(tm_batch* b, bool csr) {
             if (enqueue_dedup(b, S) != TM_OK) return hipErrorUnknown;
         }
         if (b->tok_timed && !cap && (e = hipEventRecord(b->evt, S)) != hipSuccess) return e;
-        if (tokenize_now && !fuse && (e = launch_tokenize(t, ts, b->d_nslow + 1, S)) != hipSuccess) return e;
+        if (tokenize_now && (e = launch_tokenize(t, ts, b->d_nslow + 1, S)) != hipSuccess) return e;
         if (b->check_tokens && b->n) {
             if ((e = hipMemsetAsync(b->d_nslow, 0, 2 * 4, S)) != hipSuccess) return e;
             if ((e = launch_token_check(b->d_toff, b->d_tflags, b->n, b->nwords, b->d_slow, b->d_nslow,
                                         b->d_nslow + 1, S)) != hipSuccess)
                 return e;
         }
-        if (fuse)
-            e = launch_match_fresh(a, t, ts, b->d_nslow + 1, S, csr ? b->ev0 : nullptr, csr ? b->ev1 : nullptr);
-        else
-            e = launch_match(a, S, csr && !cap ? b->ev0 : nullptr, csr && !cap ? b->ev1 : nullptr, checked, 0u);
+        e = launch_match(a, S, csr && !cap ? b->ev0 : nullptr, csr && !cap ? b->ev1 : nullptr, checked, 0u);
         if (e != hipSuccess) return e;
         if (b->dedup_dev) {   // every publish's row (count, start) + the delivered matches
             if (!cap && (e = hipEventRecord(b->evx0, S)) != hipSuccess) return e;

@@ -1972,9 +1972,6 @@ struct tm_engine {
     int reserve_dedup(tm_batch* b, uint64_t nbytes);
 
     DedupArgs dedup_args(tm_batch* b) const;
-    // TM_FRESH_FUSED=1: a fresh batch's tokeniser fill inside the walk (tm_match_fresh).  Measured
-    // slower on C2 (fresh 10M batch 5.35 -> 5.64 ms, profiles/r05/fused/): off by default
-    const bool fresh_fused = getenv("TM_FRESH_FUSED") && atoi(getenv("TM_FRESH_FUSED")) != 0;
     // TM_DEDUP_WEAK_HASH=1 (tests): the dedup's hash degraded to the topic's length
     const bool dedup_weak_hash = getenv("TM_DEDUP_WEAK_HASH") && atoi(getenv("TM_DEDUP_WEAK_HASH")) != 0;
 

@@ -546,11 +546,6 @@ struct TokArgs {
                               // device-deduplicated batch's rows
 };
 hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, hipStream_t s);
-// a fresh batch in one walk (tm_match_fresh): tokeniser count + scan, then the
-// walk with each tile's fill in its prologue (t.tile_topics == a.tile_topics),
-// then the generic kernel; ev_a / ev_b around the fused walk
-hipError_t launch_match_fresh(const MatchArgs& a, const TokArgs& t, ScanArgs tscan, uint32_t* d_nwords, hipStream_t s,
-                              hipEvent_t ev_a, hipEvent_t ev_b);
 // topics per tokeniser tile for n topics of nbytes (64 unless topics are long)
 uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 

@@ -2588,8 +2588,8 @@ __device__ __forceinline__ uint8_t tok_fill_topic_global(const TokArgs& a, uint3
     return fl;
 }
 
-// One tokeniser tile (tm_tok_fill, and the prologue of the fused walk
-// tm_match_fresh): words, offsets and flags to HBM, the generic-path list.
+// One tokeniser tile (tm_tok_fill): words, offsets and flags to HBM, the
+// generic-path list.
 // out: per lane, its topic's first word (tile-local), word count and flags;
 // lds = the tile went the LDS path (lw, if set, then holds its words).
 struct TokTile {
@@ -2746,77 +2746,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) tok_tile<TOK_WPL_FILL>(a, L, tile, nullptr, out);
 }
 
-// ------------------------------------------------ fused fresh-batch walk
-// tm_match_fresh: a fresh batch's tokeniser fill folded into the walk.  Each
-// tile is tokenised in the walk's own prologue (tok_tile: the same words,
-// offsets, flags and generic-path list in HBM as tm_tok_fill), its words
-// kept in the LDS the walk then reads them from -- the byte window and the
-// tokeniser's scratch live in the probe stack's LDS, which is free until the
-// frontier loop starts.  The walk is memory-latency bound with idle VALU, so
-// the tokeniser's arithmetic runs beside other waves' probes instead of in a
-// launch of its own.  Tiles the LDS path cannot take (a window over 3 KB,
-// more than 512 words, an empty topic) are tokenised from HBM and their
-// topics sent to the generic kernel.  tm_tok_count + the scan still run
-// first: they give every tile its place in words[].
-#ifndef TM_FUSED_WPL
-#define TM_FUSED_WPL 1   // tokeniser words per lane per lookup round inside the walk (register budget)
-#endif
-template <bool BIG, int QC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QC == 384 ? TM_WPE384 : 3, 8))) void tm_match_fresh(
-    MatchArgs a, TokArgs k) {
-    __shared__ TileLds<QC> L;
-    // the walk's counters, summed per tile into LDS: registers live across the
-    // whole kernel would sit beside the tokeniser's at its peak (and spill)
-    __shared__ unsigned long long acc[5];
-    static_assert(sizeof(TokLds) <= sizeof(L.q), "the tokeniser's LDS must fit in the probe stack");
-    TokLds& T = *reinterpret_cast<TokLds*>(L.q);
-    const uint32_t lane = threadIdx.x;
-    const uint32_t tt = a.tile_topics;   // == k.tile_topics (the host fuses only then)
-    const uint32_t ntiles = (a.n + tt - 1) / tt;
-    if (lane < 5) acc[lane] = 0;
-    uint32_t tile = blockIdx.x, round = 0;
-    while (tile < ntiles) {
-        uint32_t ticket = 0;
-        if (round + 1 >= a.static_rounds && lane == 0)
-            ticket = atomicAdd(&a.xg[(blockIdx.x % TICKET_GROUPS) * TICKET_STRIDE], 1u);
-        const uint32_t t0 = tile * tt;
-        const uint32_t tend = min(t0 + tt, a.n);
-        const uint32_t t = t0 + lane;
-        const bool valid = lane < tt && t < a.n;
-        TokTile o;
-        tok_tile<TM_FUSED_WPL>(k, T, tile, L.words, o);   // (ends on a barrier: T is free for the stack)
-        if (o.lds) {
-            L.toff[lane] = o.w0;
-            L.depth[lane] = o.nw;
-            L.cnt[lane] = 0;
-            __syncthreads();
-            unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sP = 0;
-            match_tile<false, BIG, true>(a, L, t0, tend, 0, o.fl, valid, sV, sH, sW, sM, sP);
-            for (int x = 32; x > 0; x >>= 1) {
-                sV += __shfl_xor(sV, x, 64); sH += __shfl_xor(sH, x, 64);
-                sW += __shfl_xor(sW, x, 64); sM += __shfl_xor(sM, x, 64);
-                sP += __shfl_xor(sP, x, 64);
-            }
-            if (lane == 0) {
-                acc[0] += sV; acc[1] += sH; acc[2] += sW; acc[3] += sM; acc[4] += sP;
-            }
-        } else {
-            send_to_slow<false>(a, valid && !(o.fl & TF_SLOW), t);
-        }
-        __syncthreads();
-        ++round;
-        tile = round < a.static_rounds
-                   ? blockIdx.x + round * gridDim.x
-                   : a.static_rounds * gridDim.x + __builtin_amdgcn_readfirstlane(ticket) * TICKET_GROUPS +
-                         blockIdx.x % TICKET_GROUPS;
-    }
-    if (lane == 0) {
-        atomicAdd(&a.stats[ST_VISITS], acc[0]); atomicAdd(&a.stats[ST_HASH], acc[1]);
-        atomicAdd(&a.stats[ST_WORDS], acc[2]); atomicAdd(&a.stats[ST_MATCHES], acc[3]);
-        atomicAdd(&a.stats[ST_PROBES], acc[4] & ((1ull << 40) - 1));
-        atomicAdd(&a.stats[ST_ITERS], acc[4] >> 40);
-    }
-}
 
 // Read-back of an async batch in ONE kernel, written straight into pinned host
 // memory: the header block's first hdr_words (ctrl + stats + src), the counts,
@@ -3156,29 +3085,6 @@ hipError_t launch_tokenize(const TokArgs& a, ScanArgs scan, uint32_t* d_nwords, 
     if (e != hipSuccess || !a.n) return e != hipSuccess ? e : hipGetLastError();
     const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
     hipLaunchKernelGGL(tm_tok_fill, dim3(min(ntiles, cap_fill)), dim3(64), 0, s, f);
-    return hipGetLastError();
-}
-
-hipError_t launch_match_fresh(const MatchArgs& a, const TokArgs& t, ScanArgs tscan, uint32_t* d_nwords, hipStream_t s,
-                              hipEvent_t ev_a, hipEvent_t ev_b) {
-    TokArgs f;
-    hipError_t e = launch_tok_count_scan(t, tscan, d_nwords, s, f);
-    if (e != hipSuccess) return e;
-    if (ev_a && (e = hipEventRecord(ev_a, s)) != hipSuccess) return e;
-    const uint32_t ntiles = (a.n + a.tile_topics - 1) / a.tile_topics;
-    const bool big = (uint64_t)a.nslots * sizeof(Slot) > 0xFFFFFFFFull;
-    if (ntiles) {
-        if (a.qcap <= 384) {
-            if (big) hipLaunchKernelGGL((tm_match_fresh<true, 384>), dim3(a.grid), dim3(64), 0, s, a, f);
-            else hipLaunchKernelGGL((tm_match_fresh<false, 384>), dim3(a.grid), dim3(64), 0, s, a, f);
-        } else {
-            if (big) hipLaunchKernelGGL((tm_match_fresh<true, 512>), dim3(a.grid), dim3(64), 0, s, a, f);
-            else hipLaunchKernelGGL((tm_match_fresh<false, 512>), dim3(a.grid), dim3(64), 0, s, a, f);
-        }
-    }
-    if (ev_b && (e = hipEventRecord(ev_b, s)) != hipSuccess) return e;
-    if (big) hipLaunchKernelGGL((tm_match_slow<false, true>), dim3(a.s_waves), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((tm_match_slow<false, false>), dim3(a.s_waves), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -187,16 +187,11 @@ def test_walk_rows_are_the_result_without_a_csr_pass(rowcap):
     b.free()
 
 
-def test_fused_fresh_walk_parity():
-    """TM_FRESH_FUSED=1: each tile tokenised in the walk's prologue
-    (tm_match_fresh) -- opt-in, measured slower than the separate fill, kept
-    for A/B.  C1 in full with the walk counters, plus deep / irregular /
-    empty topics (the HBM fallback and the generic path), equal the oracle."""
-    os.environ["TM_FRESH_FUSED"] = "1"
-    try:
-        eng = Engine(device=0)
-    finally:
-        del os.environ["TM_FRESH_FUSED"]
+def test_fresh_batch_edge_topics_parity():
+    """A fresh batch (device tokeniser + walk) of C1 in full with the walk
+    counters, plus deep / irregular / empty topics and a 3,000-byte word (the
+    tokeniser's HBM fallback and the generic path), equal the oracle."""
+    eng = Engine(device=0)
     # (C1 already holds b"" and b"+/+": oracle ids are positions in a duplicate-free list)
     F = list(dict.fromkeys(gen.gen_filters(gen.C1).tolist() + [b"", b"+/+", b"a/#", b"+x/#"]))
     Ts = gen.gen_topics(gen.C1, gen.Strings.from_list(F), 1001, gen.C1_TOPICS)
