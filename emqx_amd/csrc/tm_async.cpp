@@ -6,9 +6,9 @@
 int tm_engine::async_start(Replica& R) {
     if (R.a_started) return TM_OK;
     if (reps.empty()) return TM_ENODEV;
-    if (const char* d = getenv("TM_ASYNC_DEPTH")) R.a_depth = (uint32_t)std::min(16, std::max(1, atoi(d)));
-    if (const char* d = getenv("TM_ASYNC_COMPLETERS")) R.a_ncompleters = (uint32_t)std::min(8, std::max(1, atoi(d)));
-    if (const char* d = getenv("TM_ASYNC_SPIN_US")) R.a_spin_us = (uint32_t)std::min(10000, std::max(0, atoi(d)));
+    if (kn.async_depth) R.a_depth = (uint32_t)kn.async_depth;
+    if (kn.async_completers) R.a_ncompleters = (uint32_t)kn.async_completers;
+    if (kn.async_spin_us >= 0) R.a_spin_us = (uint32_t)kn.async_spin_us;
     {
         std::lock_guard<std::recursive_mutex> g(mu);
         HIP_OK(hipSetDevice(R.device));

@@ -520,7 +520,7 @@ DedupArgs tm_engine::dedup_args(tm_batch* b) const {
     d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
     d.stats = b->d_stats;
     d.bsum = b->d_dbsum;
-    d.weak_hash = dedup_weak_hash ? 1u : 0u;
+    d.weak_hash = kn.dedup_weak_hash ? 1u : 0u;
     return d;
 }
 

@@ -150,7 +150,7 @@ void tm_engine::plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo
     std::vector<uint64_t> hs;
     const bool root_live = nd[ROOT].live != 0;
     const uint32_t nb = nbuckets();
-    static const bool ptrace = getenv("TM_PAR_TRACE") != nullptr;
+    const bool ptrace = kn.par_trace;
     std::chrono::steady_clock::duration d_split{}, d_dict{}, d_walk{};
     using clk = std::chrono::steady_clock;
     for (uint32_t g0 = lo; g0 < hi; g0 += PLAN_G) {
@@ -347,7 +347,7 @@ int tm_engine::insert_planned(const uint8_t* buf, const uint64_t* offs, uint32_t
 void tm_engine::ensure_pool() {
     if (!pool_started) {
         cpu_set_t cpus;
-        pool.start(threads, device_node_cpus(device, threads, cpus) ? &cpus : nullptr);
+        pool.start(threads, device_node_cpus(device, threads, kn.pool_pin, cpus) ? &cpus : nullptr);
         pool_started = true;
     }
 }
@@ -384,7 +384,7 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
         R = (nb + RS - 1) / RS;
     };
     each([](Mut& m) { m.defer = false; });
-    const bool trace = getenv("TM_PAR_TRACE") != nullptr;
+    const bool trace = kn.par_trace;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto e0 = now();
@@ -744,7 +744,7 @@ void tm_engine::par_finish(ParRun* const* runs, size_t nr) {
             if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
         }
     }
-    if (getenv("TM_PAR_TRACE")) {
+    if (kn.par_trace) {
         const auto tp3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         for (size_t r = 0; r < nr; ++r) {

@@ -738,12 +738,12 @@ int tm_trie_insert_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
         if (nshards <= 1) {
             const auto tq0 = std::chrono::steady_clock::now();
             e->make_plan(filters, offsets, n, false);
-            if (getenv("TM_PAR_TRACE"))
+            if (e->kn.par_trace)
                 fprintf(stderr, "[plan ins n=%u] %.2f ms\n", n,
                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
             if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(false, filters, offsets, n, &done, &rc)) {
                 if (n_inserted) *n_inserted = done;
-                if (getenv("TM_PAR_TRACE"))
+                if (e->kn.par_trace)
                     fprintf(stderr, "[insert_many n=%u] %.2f ms in the call\n", n,
                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
                 return rc;
@@ -786,12 +786,12 @@ int tm_trie_delete_many(tm_engine* e, const uint8_t* filters, const uint64_t* of
     try {
         const auto tq0 = std::chrono::steady_clock::now();
         e->make_plan(filters, offsets, n, true);
-        if (getenv("TM_PAR_TRACE"))
+        if (e->kn.par_trace)
             fprintf(stderr, "[plan del n=%u] %.2f ms\n", n,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
         if (n >= tm_engine::PAR_MIN && !e->mutate_parallel(true, filters, offsets, n, &done, &rc)) {
             if (n_deleted) *n_deleted = done;
-            if (getenv("TM_PAR_TRACE"))
+            if (e->kn.par_trace)
                 fprintf(stderr, "[delete_many n=%u] %.2f ms in the call\n", n,
                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
             return rc;
@@ -820,7 +820,7 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
         if (del_offsets[i + 1] < del_offsets[i]) return TM_EINVAL;
     for (uint32_t i = 0; i < n_ins; ++i)
         if (ins_offsets[i + 1] < ins_offsets[i]) return TM_EINVAL;
-    static const bool trace = getenv("TM_PAR_TRACE") != nullptr;
+    const bool trace = e->kn.par_trace;
     uint64_t done = 0;
     int rc = TM_OK;
     try {

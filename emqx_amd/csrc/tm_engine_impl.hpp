@@ -348,11 +348,8 @@ struct HugeAlloc {
 // host worker threads when tm_config.host_threads is 0: TM_HOST_THREADS, else
 // min(hardware threads, 16) -- the GPU box leases 16 CPUs of cgroup bandwidth
 // out of 256 hardware threads, so hardware_concurrency() alone overcounts.
-inline unsigned default_threads() {
-    if (const char* v = getenv("TM_HOST_THREADS")) {
-        const int t = atoi(v);
-        if (t > 0) return (unsigned)std::min(t, 64);
-    }
+inline unsigned default_threads(const Knobs& k) {
+    if (k.host_threads) return k.host_threads;
     unsigned h = std::thread::hardware_concurrency();
     return std::max(1u, std::min(h ? h : 1u, 16u));
 }
@@ -364,10 +361,8 @@ inline unsigned default_threads() {
 // unpinned 1.72 / 2.18 / 1.95 ms per step, pinned 1.40 / 1.50 / 1.77,
 // profiles/r04/aj/); TM_POOL_PIN=0 turns it off.  False (no pinning) for a
 // host-only engine, a node-less device or fewer CPUs than `need`.
-inline bool device_node_cpus(int device, unsigned need, cpu_set_t& out) {
-    if (device < 0) return false;
-    const char* pin = getenv("TM_POOL_PIN");
-    if (pin && pin[0] == '0') return false;
+inline bool device_node_cpus(int device, unsigned need, bool pin, cpu_set_t& out) {
+    if (device < 0 || !pin) return false;
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof bus - 1, device) != hipSuccess) return false;
     for (char* c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
@@ -1973,7 +1968,7 @@ struct tm_engine {
 
     DedupArgs dedup_args(tm_batch* b) const;
     // TM_DEDUP_WEAK_HASH=1 (tests): the dedup's hash degraded to the topic's length
-    const bool dedup_weak_hash = getenv("TM_DEDUP_WEAK_HASH") && atoi(getenv("TM_DEDUP_WEAK_HASH")) != 0;
+    Knobs kn;   // the environment knobs, read at init
 
     // the dedup pass over the batch's resident bytes, ahead of the tokeniser
     int enqueue_dedup(tm_batch* b, hipStream_t S);

@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <type_traits>
 
 struct tm_engine;   // include/emqx_tm.h (opaque handles, defined in tm_engine_impl.hpp)
@@ -644,5 +647,47 @@ __host__ __device__ inline uint32_t prefix_shard(uint32_t id0, uint32_t id1, uin
 // min(tiles, resident capacity), so that every wave is resident from the start
 uint32_t match_waves(uint32_t n, int device, uint32_t qcap);
 uint32_t tile_topics(uint32_t n);
+
+// Every environment knob the engine reads, in one place (INTEGRATION.md lists
+// them).  Read once per engine at tm_create (tests set them around an
+// engine's creation) and per sharded group at tm_sharded_create.
+struct Knobs {
+    // test / debug knobs
+    bool checked = false;          // TM_CHECKED=1: bounds-checked kernel variants
+    bool no_graph = false;         // TM_NO_GRAPH=1: no captured HIP graphs
+    bool par_trace = false;        // TM_PAR_TRACE: per-phase churn timings on stderr
+    bool dedup_weak_hash = false;  // TM_DEDUP_WEAK_HASH=1: the dedup's hash degraded to the length
+    int row_cap = 0;               // TM_ROWCAP: fast-path row slots per topic (1..128)
+    uint64_t fan_big = 0;          // TM_FAN_BIG: fan-out scan blocks above this use u64 offsets
+    uint64_t result_limit = 0;     // TM_RESULT_LIMIT: matches per batch
+    uint64_t staging_min = 0;      // TM_STAGING_MIN: initial staging entries of a batch
+    std::string shard_link;        // TM_SHARD_LINK (staged | peer | probe), TM_SHARD_STAGED=1
+    // deployment knobs
+    unsigned host_threads = 0;     // TM_HOST_THREADS: host workers when tm_config.host_threads is 0
+    bool pool_pin = true;          // TM_POOL_PIN=0: workers not pinned to the GPU's NUMA node
+    int async_depth = 0, async_completers = 0, async_spin_us = -1;   // TM_ASYNC_DEPTH / _COMPLETERS / _SPIN_US
+
+    static Knobs read() {
+        Knobs k;
+        auto env = [](const char* n) { return getenv(n); };
+        auto on = [&](const char* n) { const char* v = env(n); return v && atoi(v) != 0; };
+        k.checked = on("TM_CHECKED");
+        k.no_graph = on("TM_NO_GRAPH");
+        k.par_trace = env("TM_PAR_TRACE") != nullptr;
+        k.dedup_weak_hash = on("TM_DEDUP_WEAK_HASH");
+        if (const char* v = env("TM_ROWCAP")) k.row_cap = std::min(128, std::max(1, atoi(v)));
+        if (const char* v = env("TM_FAN_BIG")) k.fan_big = std::min<uint64_t>(0xFFFFFFFFull, strtoull(v, nullptr, 10));
+        if (const char* v = env("TM_RESULT_LIMIT")) k.result_limit = strtoull(v, nullptr, 10);
+        if (const char* v = env("TM_STAGING_MIN")) k.staging_min = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
+        if (on("TM_SHARD_STAGED")) k.shard_link = "staged";
+        else if (const char* v = env("TM_SHARD_LINK")) k.shard_link = v;
+        if (const char* v = env("TM_HOST_THREADS")) k.host_threads = (unsigned)std::min(std::max(atoi(v), 0), 64);
+        if (const char* v = env("TM_POOL_PIN")) k.pool_pin = v[0] != '0';
+        if (const char* v = env("TM_ASYNC_DEPTH")) k.async_depth = std::min(16, std::max(1, atoi(v)));
+        if (const char* v = env("TM_ASYNC_COMPLETERS")) k.async_completers = std::min(8, std::max(1, atoi(v)));
+        if (const char* v = env("TM_ASYNC_SPIN_US")) k.async_spin_us = std::min(10000, std::max(0, atoi(v)));
+        return k;
+    }
+};
 
 }  // namespace etm

@@ -4,16 +4,15 @@
 
 int tm_engine::init(const tm_config* cfg, const int32_t* devices, uint32_t ndev) {
     frozen = cfg && (cfg->flags & TM_CFG_FROZEN_DICT);
-    const char* ck = getenv("TM_CHECKED");
-    checked = ck && ck[0] == '1';
-    if (const char* rcap = getenv("TM_ROWCAP")) row_cap = std::min(128, std::max(1, atoi(rcap)));
-    if (const char* fb = getenv("TM_FAN_BIG")) fan_big_limit = std::min<uint64_t>(0xFFFFFFFFull, strtoull(fb, nullptr, 10));
-    if (const char* rl = getenv("TM_RESULT_LIMIT"))
-        result_limit = std::min<uint64_t>(MAX_RESULT, strtoull(rl, nullptr, 10));
-    if (const char* sm = getenv("TM_STAGING_MIN")) staging_min = std::max<uint64_t>(64, strtoull(sm, nullptr, 10));
-    threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads();
+    kn = Knobs::read();
+    checked = kn.checked;
+    if (kn.row_cap) row_cap = (uint32_t)kn.row_cap;
+    if (kn.fan_big) fan_big_limit = kn.fan_big;
+    if (kn.result_limit) result_limit = std::min<uint64_t>(MAX_RESULT, kn.result_limit);
+    if (kn.staging_min) staging_min = kn.staging_min;
+    threads = (cfg && cfg->host_threads) ? cfg->host_threads : default_threads(kn);
     dev_tok = !(cfg && (cfg->flags & TM_CFG_HOST_TOKENIZE));
-    if (const char* ng = getenv("TM_NO_GRAPH")) use_graphs = ng[0] != '1';
+    use_graphs = !kn.no_graph;
     // root node id 0 (absent until the first add_path, like the reference)
     nd.push_back(NodeRec{});
     n_flen.push_back(0);

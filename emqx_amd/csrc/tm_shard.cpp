@@ -127,11 +127,7 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 // (a peer store / hipMemcpyPeer into the same HBM); "probe" runs the
 // runtime's peer probe even for a device paired with itself, where peer
 // access is refused -- the denied branch, which must fall back to staged.
-uint8_t open_link(int a, int b) {
-    const char* f = getenv("TM_SHARD_STAGED");
-    if (f && atoi(f) != 0) return TM_LINK_STAGED;
-    const char* m = getenv("TM_SHARD_LINK");
-    const std::string mode = m ? m : "";
+uint8_t open_link(int a, int b, const std::string& mode) {
     if (mode == "staged") return TM_LINK_STAGED;
     if (a == b && mode == "peer") return TM_LINK_PEER;
     if (a == b && mode != "probe") return TM_LINK_SAME;
@@ -675,8 +671,10 @@ int tm_sharded_create(const int32_t* devices, uint32_t n, const tm_config* cfg, 
     }
     // every shard copies parts to every other: open the links both ways
     s->link.assign((size_t)n * n, TM_LINK_SAME);
+    const Knobs kn = Knobs::read();
     for (uint32_t i = 0; i < n; ++i)
-        for (uint32_t j = i; j < n; ++j) s->link[i * n + j] = s->link[j * n + i] = open_link(devices[i], devices[j]);
+        for (uint32_t j = i; j < n; ++j)
+            s->link[i * n + j] = s->link[j * n + i] = open_link(devices[i], devices[j], kn.shard_link);
     bool ok = hipSetDevice(s->home) == hipSuccess && hipStreamCreateWithFlags(&s->s, hipStreamNonBlocking) == hipSuccess;
     for (uint32_t g = 0; ok && g < n; ++g) {
         ok = hipSetDevice(devices[g]) == hipSuccess &&
