@@ -440,6 +440,7 @@ int tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of, uint32_
             if (rc) return rc;
             b->row_of.resize(b->n_pub);
             if (b->n_pub) {
+                HIP_OK(launch_dedup_rowof(e->dedup_args(b), e->st(b)));
                 HIP_OK(hipMemcpyAsync(b->row_of.data(), b->d_rowof, (size_t)b->n_pub * 4, hipMemcpyDeviceToHost,
                                       e->st(b)));
                 HIP_OK(hipStreamSynchronize(e->st(b)));

@@ -570,8 +570,10 @@ uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 //   (two scans of the block sums)
 //   compact  each representative: its row, its bytes into cbytes, coffs,
 //            srow[slot] = row and rrep[row] = the representative
-//   expand   (after the walk) row_of[t] = srow[slot[t]]; the representative
-//            clears its table slot, so the table is zero for the next pass
+//   expand   (after the walk) every publish's (count, start) through
+//            srow[slot[t]]; the representative clears its table slot, so the
+//            table is zero for the next pass (row_of[t] = srow[slot[t]] is
+//            built only when the host asks for it)
 struct DedupArgs {
     const uint8_t* bytes;     // the batch's publishes: bytes[offs[t] - base .. offs[t + 1] - base)
     const uint64_t* offs;
@@ -588,7 +590,7 @@ struct DedupArgs {
     const uint32_t* bbs;
     uint32_t* srow;           // mask + 1: per claimed slot, its row
     uint32_t* rrep;           // n: per row, its representative publish
-    uint32_t* row_of;         // n: row of each publish (written by the expansion)
+    uint32_t* row_of;         // n: row of each publish (tm_dedup_rowof, when the host asks)
     uint8_t* cbytes;          // the rows' bytes, the tokeniser's input (16-B aligned, + 32 bytes of slack)
     uint64_t* coffs;          // rows + 1 offsets into cbytes
     uint32_t* dd;             // [0] rows: the tokeniser's and the walk's topic count (TokArgs / MatchArgs d_n)
@@ -610,6 +612,7 @@ constexpr uint32_t DD_OFF_BITS = 40; // byte offset bits of a table slot (a batc
 __host__ __device__ inline uint32_t dedup_blocks(uint32_t n) { return (n + DD_TILE - 1) / DD_TILE; }
 hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_scan, hipStream_t s);
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s);
+hipError_t launch_dedup_rowof(const DedupArgs& a, hipStream_t s);
 // A captured launch is keyed by the bytes of its argument structs
 // (tm_batch.cpp launch / launch_graph): no implicit padding, so equal
 // arguments always give equal keys (the pads are members, zeroed by `{}`)

@@ -1710,13 +1710,20 @@ __device__ __forceinline__ bool dd_equal(const uint8_t* bytes, const uint64_t (&
 // probe, never a wrong row.
 constexpr uint64_t DD_OFF_MASK = (1ull << DD_OFF_BITS) - 1ull;
 
+// Slots are read with PLAIN loads (this XCD's L2, not the device-coherent
+// path): a stale copy can only be 0 (then the CAS returns the slot's value)
+// or an older offset of the slot's own topic (equal bytes all the same) --
+// a slot's topic never changes.
+__device__ __forceinline__ unsigned long long dd_want(uint64_t h, uint64_t b, uint32_t len) {
+    return (1ull << 63) | (((h >> 54) & 0x3FFull) << 53) | ((uint64_t)len << DD_OFF_BITS) | b;
+}
+
 __device__ __forceinline__ uint32_t dd_claim(const DedupArgs& a, uint64_t h, uint64_t b, uint32_t len,
                                              const uint64_t (&c)[8]) {
-    const unsigned long long want =
-        (1ull << 63) | (((h >> 54) & 0x3FFull) << 53) | ((uint64_t)len << DD_OFF_BITS) | b;
+    const unsigned long long want = dd_want(h, b, len);
     uint64_t i = h & a.mask;
     for (;;) {
-        unsigned long long v = __hip_atomic_load(&a.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long v = a.table[i];
         if (v == 0) {
             v = atomicCAS(&a.table[i], 0ull, want);
             if (v == 0) return (uint32_t)i;
@@ -1729,10 +1736,11 @@ __device__ __forceinline__ uint32_t dd_claim(const DedupArgs& a, uint64_t h, uin
     }
 }
 
-// Pass 1 (claim), one thread per publish, its bytes in registers.  C5's hot
-// topics would put hundreds of thousands of claims on one slot's line (Zipf
-// over 10k hot topics, the first ~9% of the publishes), so the workgroup first
-// collapses its own publishes in LDS: equal hashes elect the lowest thread,
+// Pass 1 (claim), one thread per publish, its bytes in registers.  A
+// publish whose topic already holds its home slot joins it at once.  C5's
+// hot topics would put hundreds of thousands of claims on one slot's line
+// (Zipf over 10k hot topics, the first ~9% of the publishes), so the others
+// first collapse in the workgroup's LDS: equal hashes elect the lowest thread,
 // whose bytes each follower compares with its own (a follower whose bytes
 // differ -- a 64-bit collision -- takes part in the next round's election), and
 // only the leaders claim global slots; followers take their leader's.
@@ -1755,19 +1763,31 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
         b = a.offs[t] - a.base;
         len = (uint32_t)(a.offs[t + 1] - a.base - b);
     }
+    bool resolved = false;
+    uint32_t rslot = 0;
     {
         uint64_t c[8];
         dd_load64(a.bytes, b, len, c);
         if (valid) {
             h = dd_hash(a.bytes, b, len, c);
             if (a.weak_hash) h = ((uint64_t)len << 40) | ((uint64_t)len << 8) | 1ull;
+            // a topic already in its home slot (the common case once a hot
+            // topic has been claimed: C5's 90% hot publishes) joins it here,
+            // two L2 reads, no election and no atomic
+            const uint64_t i = h & a.mask;
+            const unsigned long long want = dd_want(h, b, len), v = a.table[i];
+            if (v && (v >> DD_OFF_BITS) == (want >> DD_OFF_BITS) && dd_equal(a.bytes, c, b, v & DD_OFF_MASK, len)) {
+                if (b < (v & DD_OFF_MASK)) atomicMin(&a.table[i], want);
+                resolved = true;
+                rslot = (uint32_t)i;
+            }
         }
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) lc[q][tid] = c[q];
     }
     lb[tid] = b;
     ll[tid] = len;
-    bool pend = valid, leader = false;
+    bool pend = valid && !resolved, leader = false;
     uint32_t lead = tid, s = 0;
     while (__syncthreads_or(pend)) {
         for (uint32_t k = tid; k < DD_LT; k += DD_BLOCK) {
@@ -1815,7 +1835,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
         lslot[tid] = dd_claim(a, h, b, len, c);
     }
     __syncthreads();
-    if (valid) a.slot[t] = lslot[lead];
+    if (valid) a.slot[t] = resolved ? rslot : lslot[lead];
 }
 
 // Pass 2 (count): publish t is its topic's representative when its offset is
@@ -1973,9 +1993,8 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     }
 }
 
-// After the walk: every publish gets its row (row_of) and its row's (count,
-// start) -- the result per publish -- and the batch's delivered matches are
-// summed (one atomic per block).  A representative clears its table slot
+// After the walk: every publish gets its row's (count, start) -- the result
+// per publish -- and the batch's delivered matches are summed per block.  A representative clears its table slot
 // (nothing reads the table after the compaction): the next dedup pass finds
 // it zero without a memset.
 constexpr uint32_t EXPAND_PER_THREAD = DD_EXPAND_TILE / 256;
@@ -2009,7 +2028,6 @@ __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
             // the representative clears its slot (nothing reads the table
             // after the compaction): the next pass finds it zero
             if (rep[u] == t) a.table[sl[u]] = 0;
-            a.row_of[t] = r[u];
             a.pcount[t] = c[u];
             a.psrc[t] = sr[u];
             sum += c[u];
@@ -2021,6 +2039,13 @@ __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     // a partial sum per block, added up by tm_dedup_sum: one same-address
     // atomic per block serialised at ~30 ns each (4,883 blocks: ~0.15 ms)
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// row_of[t] = srow[slot[t]]: the publish -> row map, built only when the host
+// asks for it (tm_batch_row_map) -- the per-launch expansion skips the 40 MB
+__global__ __launch_bounds__(256) void tm_dedup_rowof(DedupArgs a) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t < a.n) a.row_of[t] = a.srow[a.slot[t]];
 }
 
 // the expansion's block sums -> the batch's delivered matches; the rows for
@@ -2958,6 +2983,11 @@ hipError_t launch_dedup(const DedupArgs& a, ScanArgs rows_scan, ScanArgs bytes_s
     if ((e = launch_scan(rows_scan, s, nullptr)) != hipSuccess) return e;
     if ((e = launch_scan(bytes_scan, s, nullptr)) != hipSuccess) return e;
     hipLaunchKernelGGL(tm_dedup_compact, dim3(nblk), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dedup_rowof(const DedupArgs& a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(tm_dedup_rowof, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
