@@ -671,8 +671,13 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     a.xg = b->d_ctrl + XG_WORD;
     a.ctrl = b->d_ctrl; a.ovf_list = b->d_ovf; a.ovf_cap = (uint32_t)std::min<size_t>(b->c_ovf, 0xFFFFFFF0ull);
     a.stats = b->d_stats;
-    if ((rc = dev_reserve(b->d_wstats, b->c_wstats, (size_t)a.grid * WSTATS))) return rc;
-    a.wstats = b->d_wstats;
+    // a walk of many waves writes per-wave sums (one reduce kernel after it);
+    // a small one adds them atomically -- a few dozen same-line atomics cost
+    // less than one more launch on the per-publish path
+    if (a.grid >= WSTATS_MIN_WAVES) {
+        if ((rc = dev_reserve(b->d_wstats, b->c_wstats, (size_t)a.grid * WSTATS))) return rc;
+        a.wstats = b->d_wstats;
+    }
     a.s_qparent = b->d_sqpar; a.s_qpw = b->d_sqpw; a.s_qmeta = b->d_sqmeta; a.s_qkey = b->d_sqkey;
     a.s_ofid = b->d_sofid; a.s_okey = b->d_sokey;
     a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;

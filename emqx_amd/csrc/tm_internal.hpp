@@ -160,6 +160,10 @@ __host__ __device__ __forceinline__ uint64_t xg_top_read(const uint32_t* hdr, ui
 }
 
 constexpr uint32_t WSTATS = 8;   // u64 partial sums per walk wave (MatchArgs.wstats)
+// walks of at least this many waves sum their stats by tm_stats_reduce: ~4,000
+// waves ending together queued ~24k same-line device atomics (C5 K = 100 walk
+// 0.48 -> 0.23 ms without them, C2 4.75 -> 4.62 ms)
+constexpr uint32_t WSTATS_MIN_WAVES = 256;
 struct MatchArgs {
     // trie replica
     const Slot* slots;
