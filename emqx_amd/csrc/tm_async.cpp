@@ -53,6 +53,7 @@ void tm_engine::async_stop(Replica& R) {
         if (sl->b.own) (void)hipStreamDestroy(sl->b.own);
         if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
         if (sl->h_in) (void)hipHostFree(sl->h_in);
+        if (sl->h_bin) (void)hipHostFree(sl->h_bin);
         if (sl->h_rows) (void)hipHostFree(sl->h_rows);
         if (sl->h_out) (void)hipHostFree(sl->h_out);
         if (sl->h_flag) (void)hipHostFree(sl->h_flag);
@@ -213,17 +214,69 @@ int tm_engine::slot_launch(AsyncSlot* sl) {
     const uint32_t n = (uint32_t)sl->calls.size();
     const size_t nb = sl->bytes.size(), head = packed_head(n);
     int rc;
+    Replica& R = *sl->b.rep;
+    // The bounded form (tm_batch::bounded): the batch is sized for max_batch
+    // calls once, its input written into mapped pinned memory, and from the
+    // second launch on the device work and the export replay one captured
+    // graph.  Topics the size doesn't fit (more bytes than the slot holds)
+    // take the packed H2D form below.
+    const bool bounded = dev_tok && use_graphs && !checked && n <= R.a_max;
+    if (bounded) {
+        if (sl->bound != R.a_max || nb > sl->bytes_cap) {
+            sl->bound = R.a_max;
+            sl->bytes_cap = std::max<uint64_t>({sl->bytes_cap, (uint64_t)sl->bound * 64, (uint64_t)nb + nb / 2});
+        }
+        const size_t o_offs = 64, o_bytes = (o_offs + ((size_t)sl->bound + 1) * 8 + 15) & ~(size_t)15;
+        if ((rc = host_reserve_coherent(sl->h_bin, sl->c_bin, o_bytes + sl->bytes_cap + 32))) return rc;
+        *reinterpret_cast<volatile uint32_t*>(sl->h_bin) = n;
+        memcpy(sl->h_bin + o_offs, sl->offs.data(), ((size_t)n + 1) * 8);
+        if (nb) memcpy(sl->h_bin + o_bytes, sl->bytes.data(), nb);
+        std::lock_guard<std::recursive_mutex> g(mu);
+        HIP_OK(hipSetDevice(R.device));
+        tm_batch* b = &sl->b;
+        const hipStream_t S = b->own;
+        uint8_t* d_bin = nullptr;
+        HIP_OK(hipHostGetDevicePointer((void**)&d_bin, sl->h_bin, 0));
+        if ((rc = prepare_bounded(b, sl->bound, sl->bytes_cap, reinterpret_cast<const uint64_t*>(d_bin + o_offs),
+                                  d_bin + o_bytes, reinterpret_cast<uint32_t*>(d_bin))))
+            return rc;
+        ExportArgs x{};
+        if ((rc = slot_export_args(sl, x, sl->bound))) return rc;
+        x.d_n = reinterpret_cast<const uint32_t*>(d_bin);
+        x.fixed_words = tm_batch::HDR_FIXED / 4;
+        b->tail_key.assign(sizeof x + sizeof(uint32_t*), 0);
+        memcpy(b->tail_key.data(), &x, sizeof x);
+        memcpy(b->tail_key.data() + sizeof x, &sl->d_flag, sizeof(uint32_t*));
+        b->tail = [this, sl, x](hipStream_t st) { return slot_tail(sl, x, st); };
+        if ((rc = launch(b, false))) return rc;
+        if (!b->tail_done) HIP_OK(slot_tail(sl, x, S));
+        HIP_OK(hipEventRecord(sl->ev_done, S));
+        return TM_OK;
+    }
     if ((rc = host_reserve(sl->h_in, sl->c_in, head + nb))) return rc;
     memcpy(sl->h_in, sl->offs.data(), ((size_t)n + 1) * 8);
     if (nb) memcpy(sl->h_in + head, sl->bytes.data(), nb);
     std::lock_guard<std::recursive_mutex> g(mu);
-    HIP_OK(hipSetDevice(sl->b.rep->device));
+    HIP_OK(hipSetDevice(R.device));
     tm_batch* b = &sl->b;
     const hipStream_t S = b->own;
     rc = dev_tok ? upload_packed(b, sl->h_in, n, nb)
                  : prepare(b, sl->h_in + head, reinterpret_cast<const uint64_t*>(sl->h_in), n);
     if (rc) return rc;
+    b->tail = nullptr;
     if ((rc = launch(b, false))) return rc;
+    ExportArgs x{};
+    if ((rc = slot_export_args(sl, x, n))) return rc;
+    HIP_OK(slot_tail(sl, x, S));
+    HIP_OK(hipEventRecord(sl->ev_done, S));
+    return TM_OK;
+}
+
+// the export of a slot's batch of n (or, bounded, at most n) calls into its
+// pinned buffers: [ctrl | stats | src n u64 | count n u32] and the rows
+int tm_engine::slot_export_args(AsyncSlot* sl, ExportArgs& x, uint32_t n) {
+    int rc;
+    tm_batch* b = &sl->b;
     const size_t hdr_bytes = tm_batch::HDR_FIXED + (size_t)n * 8;
     if ((rc = host_reserve_coherent(sl->h_out, sl->c_out, hdr_bytes + (size_t)n * 4 + 8))) return rc;
     uint8_t* rows8 = reinterpret_cast<uint8_t*>(sl->h_rows);
@@ -232,7 +285,6 @@ int tm_engine::slot_launch(AsyncSlot* sl) {
     void *d_out = nullptr, *d_rows = nullptr;
     HIP_OK(hipHostGetDevicePointer(&d_out, sl->h_out, 0));
     HIP_OK(hipHostGetDevicePointer(&d_rows, sl->h_rows, 0));
-    ExportArgs x{};
     x.hdr = reinterpret_cast<const uint32_t*>(b->d_hdr);
     x.hdr_words = hdr_bytes / 4;
     x.h_hdr = reinterpret_cast<uint32_t*>(d_out);
@@ -243,17 +295,19 @@ int tm_engine::slot_launch(AsyncSlot* sl) {
     x.h_rows = reinterpret_cast<uint32_t*>(d_rows);
     x.rows_cap = std::min<uint64_t>(b->c_sfids, sl->c_rows / 4);
     x.rcap = region_cap(std::min<uint64_t>(b->c_sfids, MAX_RESULT), b->one_region);
-    HIP_OK(launch_export_host(x, S));
-    if (b->rep->a_spin_us) {
-        if (!sl->h_flag) {
-            HIP_OK(hipHostMalloc((void**)&sl->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
-            *sl->h_flag = 0;
-            HIP_OK(hipHostGetDevicePointer((void**)&sl->d_flag, sl->h_flag, 0));
-        }
-        HIP_OK(hipStreamWriteValue32(S, sl->d_flag, ++sl->seq, 0));
+    if (b->rep->a_spin_us && !sl->h_flag) {
+        HIP_OK(hipHostMalloc((void**)&sl->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+        *sl->h_flag = 0;
+        HIP_OK(hipHostGetDevicePointer((void**)&sl->d_flag, sl->h_flag, 0));
     }
-    HIP_OK(hipEventRecord(sl->ev_done, S));
     return TM_OK;
+}
+
+// the export kernel, and the completion flag when completers poll it
+hipError_t tm_engine::slot_tail(AsyncSlot* sl, const ExportArgs& x, hipStream_t S) {
+    hipError_t e = launch_export_host(x, S);
+    if (e == hipSuccess && sl->b.rep->a_spin_us && sl->d_flag) e = hipStreamWriteValue32(S, sl->d_flag, ++sl->seq, 0);
+    return e;
 }
 
 void tm_engine::completer_loop(Replica& R) {
@@ -385,7 +439,19 @@ bool tm_engine::slot_wait(AsyncSlot* sl, double& us_wait, bool& recovered) {
         {
             std::lock_guard<std::recursive_mutex> g(mu);
             (void)hipSetDevice(b->rep->device);
-            rc = grow_for(b, err, need, staged);
+            if (b->bounded) {   // sized for its bound: re-run as a packed batch of exactly these calls
+                const size_t nb = sl->bytes.size(), head = packed_head(n);
+                rc = host_reserve(sl->h_in, sl->c_in, head + nb);
+                if (!rc) {
+                    memcpy(sl->h_in, sl->offs.data(), ((size_t)n + 1) * 8);
+                    if (nb) memcpy(sl->h_in + head, sl->bytes.data(), nb);
+                    rc = upload_packed(b, sl->h_in, n, nb);
+                }
+                if (!rc) rc = grow_for(b, err, need, staged);
+                if (!rc) rc = launch(b);
+            } else {
+                rc = grow_for(b, err, need, staged);
+            }
             if (!rc) rc = wait(b);
             if (!rc) rc = result(b, &r);
         }

@@ -557,6 +557,7 @@ int tm_engine::upload_packed(tm_batch* b, const uint8_t* blk, uint32_t n, uint64
     const size_t head = packed_head(n);
     if (nbytes + n + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
     b->dedup = false;
+    b->bounded = false;
     b->n_pub = n;
     b->row_of.clear();
     b->launched = b->done = false;
@@ -570,6 +571,32 @@ int tm_engine::upload_packed(tm_batch* b, const uint8_t* blk, uint32_t n, uint64
     HIP_OK(hipMemcpyAsync(b->d_in, blk, head + nbytes, hipMemcpyHostToDevice, b->own));
     b->in_offs = reinterpret_cast<const uint64_t*>(b->d_in);
     b->in_bytes = b->d_in + head;
+    return tokens_pending(b);
+}
+
+// An async slot's bounded batch (see tm_batch::bounded): sized for `bound`
+// topics and `bytes_cap` bytes; its offsets, bytes and count live in mapped
+// pinned memory (d_offs / d_bytes / d_n, device pointers), written by the
+// slot before every launch.  Called before every launch (cheap once sized):
+// the tokens are made fresh each time.
+int tm_engine::prepare_bounded(tm_batch* b, uint32_t bound, uint64_t bytes_cap, const uint64_t* d_offs,
+                               const uint8_t* d_bytes, uint32_t* d_n) {
+    int rc;
+    if (bytes_cap + bound + 1 > 0xFFFFFFF0ull) return TM_EOVERFLOW;
+    b->dedup = b->dedup_dev = false;
+    b->n_pub = bound;
+    b->n = bound;
+    b->row_of.clear();
+    b->launched = b->done = false;
+    b->tokens_only = false;
+    b->bytes.clear();
+    b->offs.clear();
+    b->tok_base = 0;
+    if ((rc = reserve_tokens(b, bound, bytes_cap))) return rc;
+    b->in_offs = d_offs;
+    b->in_bytes = d_bytes;
+    b->d_nb = d_n;
+    b->bounded = true;
     return tokens_pending(b);
 }
 
@@ -641,6 +668,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         if (b->dedup_dev) {   // the rows' bytes, compacted by the dedup pass
             t.bytes = b->d_cbytes; t.offs = b->d_coffs; t.base = 0; t.d_n = b->d_dd;
         }
+        if (b->bounded) t.d_n = b->d_nb;   // (sized for the bound, counted in pinned memory)
         ts.block_sums = b->d_bsums;
     }
     MatchArgs a{};
@@ -652,7 +680,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
     a.slow_list = b->d_slow; a.n_slow = b->dev_slow ? 0u : (uint32_t)b->h_slow.size();
     a.d_nslow = b->dev_slow ? b->d_nslow : nullptr;
-    a.d_n = b->dedup_dev ? b->d_dd : nullptr;   // the rows, counted by the dedup pass
+    a.d_n = b->dedup_dev ? b->d_dd : b->bounded ? b->d_nb : nullptr;   // the rows, counted by the dedup pass
     a.count = b->d_count; a.src = b->d_src; a.rows = b->d_rows; a.row_cap = row_cap;
     a.grid = match_waves(b->n, R.device, qcap);
     a.tile_topics = tile_topics(b->n);
@@ -774,6 +802,53 @@ int tm_engine::launch(tm_batch* b, bool csr) {
         }
         csr_done = grc == 0;
         if (csr_done) { b->tok_timed = false; b->graphed = true; }   // (replayed: see the enqueue above)
+    }
+    // A bounded batch (an async slot's): the same arguments every launch, so
+    // from its second launch on the tokeniser, the walk, the generic path and
+    // the slot's tail (export + flag) replay as one captured graph: ~10
+    // enqueues of ~3 us host time each become one
+    b->tail_done = false;
+    if (!csr && b->bounded && b->tail && tokenize_now && use_graphs && !checked && !b->gbad && grc == 1) {
+        std::vector<uint8_t> key(sizeof t + sizeof ts + sizeof a + sizeof s + b->tail_key.size());
+        uint8_t* k = key.data();
+        memcpy(k, &t, sizeof t); k += sizeof t;
+        memcpy(k, &ts, sizeof ts); k += sizeof ts;
+        memcpy(k, &a, sizeof a); k += sizeof a;
+        memcpy(k, &s, sizeof s); k += sizeof s;
+        if (!b->tail_key.empty()) memcpy(k, b->tail_key.data(), b->tail_key.size());
+        if (b->gexec && b->gkey == key) {
+            HIP_OK(hipGraphLaunch(b->gexec, S));
+            ++graph_launches;
+            grc = 0;
+        } else {
+            if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
+            b->gexec = nullptr;
+            if (b->gkey == key) {   // the second launch with these arguments: capture them
+                hipGraph_t g = nullptr;
+                if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) == hipSuccess) {
+                    hipError_t e = enqueue(true, false);
+                    if (e == hipSuccess) e = b->tail(S);
+                    const hipError_t e2 = hipStreamEndCapture(S, &g);
+                    if (e == hipSuccess && e2 == hipSuccess && g &&
+                        hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
+                        (void)hipGraphDestroy(g);
+                        HIP_OK(hipGraphLaunch(b->gexec, S));
+                        ++graph_launches;
+                        grc = 0;
+                    } else {
+                        if (g) (void)hipGraphDestroy(g);
+                        (void)hipGetLastError();
+                        b->gexec = nullptr;
+                        b->gbad = true;   // the direct way from now on
+                    }
+                } else {
+                    (void)hipGetLastError();
+                    b->gbad = true;
+                }
+            }
+            b->gkey.swap(key);
+        }
+        b->tail_done = grc == 0;
     }
     if (grc == 1) {
         const hipError_t e = enqueue(false, false);

@@ -460,6 +460,16 @@ struct tm_batch {
     hipGraphExec_t gexec = nullptr;
     std::vector<uint8_t> gkey;      // the arguments gexec was captured with, or of the last direct launch
     bool gbad = false;              // capture failed once: this batch launches directly
+    // A bounded batch (the async slots' fresh batches, tm_async.cpp): sized
+    // for n topics and bytes_cap bytes once, its input read by the tokeniser
+    // straight from mapped pinned memory and its count from *d_nb (pinned
+    // too), so every launch has the same arguments and replays one captured
+    // graph: tokeniser, walk, generic path and `tail` (the slot's export).
+    bool bounded = false;
+    uint32_t* d_nb = nullptr;
+    std::function<hipError_t(hipStream_t)> tail;
+    std::vector<uint8_t> tail_key;  // the tail's arguments (part of the graph key)
+    bool tail_done = false;         // the last launch enqueued the tail (in the graph)
     bool own_user = false;   // TM_BATCH_STREAM: a caller's batch on a stream of its own (async slots: false)
     // generic-path scratch, per batch (batches on different streams run concurrently)
     uint32_t s_waves = 0, s_qcap = 1u << 13, s_ocap = 1u << 14;
@@ -674,6 +684,11 @@ struct AsyncSlot {
     std::vector<AsyncCall> calls;
     uint8_t* h_in = nullptr;             // pinned [offs (n+1) u64 | bytes] (H2D source)
     size_t c_in = 0;
+    // the bounded batch's input, mapped and coherent: [n | pad | offs (bound + 1) u64 | bytes]
+    uint8_t* h_bin = nullptr;
+    size_t c_bin = 0;
+    uint32_t bound = 0;                  // topics the bounded batch is sized for (0: not set up)
+    uint64_t bytes_cap = 0;
     // written by tm_export_host: [ctrl | stats | src n u64 | count n u32] and the rows
     uint8_t* h_out = nullptr;
     size_t c_out = 0;
@@ -1973,6 +1988,10 @@ struct tm_engine {
     // the dedup pass over the batch's resident bytes, ahead of the tokeniser
     int enqueue_dedup(tm_batch* b, hipStream_t S);
     int clear_dedup_table(tm_batch* b, hipStream_t S);
+    int prepare_bounded(tm_batch* b, uint32_t bound, uint64_t bytes_cap, const uint64_t* d_offs,
+                        const uint8_t* d_bytes, uint32_t* d_n);
+    int slot_export_args(AsyncSlot* sl, ExportArgs& x, uint32_t n);
+    hipError_t slot_tail(AsyncSlot* sl, const ExportArgs& x, hipStream_t S);
 
     int tokens_pending(tm_batch* b);
 

@@ -637,7 +637,12 @@ struct ExportArgs {
     uint32_t* h_rows;
     uint64_t rows_cap;        // entries h_rows holds
     uint64_t rcap;            // entries per group region of the staging area
+    // or null: the batch's topic count is *d_n (a bounded batch, n above is
+    // its bound): hdr_words = fixed_words + 2 * n and the counts follow it
+    const uint32_t* d_n;
+    uint64_t fixed_words;
 };
+static_assert(std::has_unique_object_representations_v<ExportArgs>, "ExportArgs has implicit padding");
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
 // the dense CSR of a batch into device-visible pinned host memory: row_off[0..n]
 // and ids[0 .. min(*d_total, cap)) (tm_match_batch: one host wait per batch)

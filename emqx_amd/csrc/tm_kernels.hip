@@ -2780,6 +2780,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TM_TOK_WPE, 
 __global__ __launch_bounds__(256) void tm_export_host(ExportArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a.d_n) {   // a bounded batch: the layout follows its count
+        a.n = *a.d_n;
+        a.hdr_words = a.fixed_words + 2 * a.n;
+        a.h_count = a.h_hdr + a.hdr_words;
+    }
     for (uint64_t i = i0; i < a.hdr_words; i += stride) a.h_hdr[i] = a.hdr[i];
     for (uint64_t i = i0; i < a.n; i += stride) a.h_count[i] = a.count[i];
     for (uint32_t g = 0; g < TICKET_GROUPS; ++g) {   // each group region's reserved entries
