@@ -54,6 +54,8 @@ void tm_engine::async_stop(Replica& R) {
         if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
         if (sl->h_in) (void)hipHostFree(sl->h_in);
         if (sl->h_bin) (void)hipHostFree(sl->h_bin);
+        for (AsyncSlot::GraphCache& gc : sl->gc)
+            if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
         if (sl->h_rows) (void)hipHostFree(sl->h_rows);
         if (sl->h_out) (void)hipHostFree(sl->h_out);
         if (sl->h_flag) (void)hipHostFree(sl->h_flag);
@@ -222,10 +224,15 @@ int tm_engine::slot_launch(AsyncSlot* sl) {
     // take the packed H2D form below.
     const bool bounded = dev_tok && use_graphs && !checked && n <= R.a_max;
     if (bounded) {
-        if (sl->bound != R.a_max || nb > sl->bytes_cap) {
-            sl->bound = R.a_max;
-            sl->bytes_cap = std::max<uint64_t>({sl->bytes_cap, (uint64_t)sl->bound * 64, (uint64_t)nb + nb / 2});
+        // size class: 1/512, 1/64, 1/8 of max_batch (at least 32 calls), or all of it
+        uint32_t cls = 0, bound = R.a_max;
+        for (; cls + 1 < AsyncSlot::NCLASS; ++cls) {
+            const uint32_t c = std::max<uint32_t>(32, R.a_max >> (9 - 3 * cls));
+            if (n <= c && c < R.a_max) { bound = c; break; }
         }
+        sl->bound = bound;
+        if (nb > sl->bytes_cap || sl->bytes_cap < (uint64_t)R.a_max * 64)
+            sl->bytes_cap = std::max<uint64_t>({sl->bytes_cap, (uint64_t)R.a_max * 64, (uint64_t)nb + nb / 2});
         const size_t o_offs = 64, o_bytes = (o_offs + ((size_t)sl->bound + 1) * 8 + 15) & ~(size_t)15;
         if ((rc = host_reserve_coherent(sl->h_bin, sl->c_bin, o_bytes + sl->bytes_cap + 32))) return rc;
         *reinterpret_cast<volatile uint32_t*>(sl->h_bin) = n;
@@ -248,7 +255,13 @@ int tm_engine::slot_launch(AsyncSlot* sl) {
         memcpy(b->tail_key.data(), &x, sizeof x);
         memcpy(b->tail_key.data() + sizeof x, &sl->d_flag, sizeof(uint32_t*));
         b->tail = [this, sl, x](hipStream_t st) { return slot_tail(sl, x, st); };
-        if ((rc = launch(b, false))) return rc;
+        AsyncSlot::GraphCache& gc = sl->gc[cls];
+        std::swap(b->gexec, gc.exec);
+        std::swap(b->gkey, gc.key);
+        rc = launch(b, false);
+        std::swap(b->gexec, gc.exec);
+        std::swap(b->gkey, gc.key);
+        if (rc) return rc;
         if (!b->tail_done) HIP_OK(slot_tail(sl, x, S));
         HIP_OK(hipEventRecord(sl->ev_done, S));
         return TM_OK;

@@ -689,6 +689,15 @@ struct AsyncSlot {
     size_t c_bin = 0;
     uint32_t bound = 0;                  // topics the bounded batch is sized for (0: not set up)
     uint64_t bytes_cap = 0;
+    // the bounded batch's captured graphs, one per size class (a batch of n
+    // calls runs in the smallest class >= n: a 20-call batch would otherwise
+    // launch the grids of a 16,384-call one); swapped into b.gexec / b.gkey
+    // around each launch
+    static constexpr uint32_t NCLASS = 4;
+    struct GraphCache {
+        hipGraphExec_t exec = nullptr;
+        std::vector<uint8_t> key;
+    } gc[NCLASS];
     // written by tm_export_host: [ctrl | stats | src n u64 | count n u32] and the rows
     uint8_t* h_out = nullptr;
     size_t c_out = 0;
