@@ -58,6 +58,11 @@ class Result(C.Structure):
                 ("row_offsets", C.POINTER(C.c_uint32)), ("filter_ids", C.POINTER(C.c_uint32))]
 
 
+class ResultPacked(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("id_bytes", C.c_uint32), ("n_matches", C.c_uint64),
+                ("row_offsets", C.POINTER(C.c_uint32)), ("ids", C.POINTER(C.c_uint8))]
+
+
 class Routes(C.Structure):
     _fields_ = [("n_topics", C.c_uint32), ("n_routes", C.c_uint64), ("row_offsets", C.POINTER(C.c_uint32)),
                 ("filter_ids", C.POINTER(C.c_uint32)), ("dests", C.POINTER(C.c_uint32))]
@@ -137,6 +142,7 @@ SIGNATURES = {
     "tm_trie_empty": (C.c_int, [P]),
     "tm_trie_match": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_match_batch": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
+    "tm_match_batch_packed": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(ResultPacked)]),
     "tm_match_coalesced": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "tm_coalesce_config": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "tm_match_async": (C.c_int, [P, U8P, SZ, MATCH_CB, P]),
@@ -181,6 +187,8 @@ SIGNATURES = {
     "tm_filter_id": (C.c_int, [P, U8P, SZ, C.POINTER(C.c_uint32)]),
     "tm_filter_copy": (C.c_int, [P, C.c_uint32, P, SZ, C.POINTER(SZ)]),
     "tm_filters_copy": (C.c_int, [P, P, C.c_uint32, P, SZ, P, P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "tm_filters_copy_packed": (C.c_int, [P, P, C.c_uint32, C.c_uint32, P, SZ, P, P, C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint64)]),
     "tm_topic_match": (C.c_int, [U8P, SZ, U8P, SZ]),
     "tm_topic_wildcard": (C.c_int, [U8P, SZ]),
     "tm_topic_validate": (C.c_int, [C.c_int, U8P, SZ, C.POINTER(C.c_char_p)]),

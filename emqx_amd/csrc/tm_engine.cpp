@@ -186,6 +186,31 @@ int tm_trie_empty(tm_engine* e) {
     return e->live_edges == 0;
 }
 
+int tm_match_batch_packed(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
+                          tm_result_packed* out) {
+    if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->set_device();
+    if (rc) return rc;
+    Replica& R = e->pick();
+    if ((rc = e->use(&R))) return rc;
+    // 3 bytes while every node id fits 24 bits (the ids a result can hold)
+    const uint32_t pack = e->nd.size() <= (1u << 24) ? 3u : 4u;
+    tm_result r{};
+    try {
+        rc = e->match_batch_pipelined(R, topics, offsets, n, &r, pack);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+    if (rc) return rc;
+    out->n_topics = r.n_topics;
+    out->id_bytes = pack;
+    out->n_matches = r.n_matches;
+    out->row_offsets = r.row_offsets;
+    out->ids = pack == 3 ? R.h_pids8 : reinterpret_cast<const uint8_t*>(r.filter_ids);
+    return TM_OK;
+}
+
 int tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_result* out) {
     if (!e || !offsets || !out || (!topics && n)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(e->mu);
@@ -1098,20 +1123,25 @@ int tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, size_t* 
     return TM_OK;
 }
 
-int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, size_t cap, uint64_t* offs,
-                    uint32_t* keep, uint32_t* n_out, uint64_t* need) {
-    if (!e || !offs || !n_out || !need || (n && !ids) || (cap && !buf)) return TM_EINVAL;
+extern "C++" {
+namespace {
+// ids read in place: u32 ids, or packed little-endian ids of 3 / 4 bytes
+template <class Id>
+int filters_copy(tm_engine* e, Id id_at, uint32_t n, uint8_t* buf, size_t cap, uint64_t* offs, uint32_t* keep,
+                 uint32_t* n_out, uint64_t* need) {
     std::lock_guard<std::recursive_mutex> g(e->mu);
     uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i)
-        if (ids[i] < e->nd.size() && e->nd[ids[i]].hasbytes) total += e->n_flen[ids[i]];
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t id = id_at(i);
+        if (id < e->nd.size() && e->nd[id].hasbytes) total += e->n_flen[id];
+    }
     *need = total;
     if (total > cap) return TM_OK;   // nothing copied: the caller grows buf and asks again
     uint32_t k = 0;
     uint64_t at = 0;
     offs[0] = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t id = ids[i];
+        const uint32_t id = id_at(i);
         if (id >= e->nd.size() || !e->nd[id].hasbytes) continue;
         const uint32_t len = e->n_flen[id];
         if (len) memcpy(buf + at, e->fbytes.data() + e->n_foff[id], len);
@@ -1121,6 +1151,29 @@ int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf,
     }
     *n_out = k;
     return TM_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, size_t cap, uint64_t* offs,
+                    uint32_t* keep, uint32_t* n_out, uint64_t* need) {
+    if (!e || !offs || !n_out || !need || (n && !ids) || (cap && !buf)) return TM_EINVAL;
+    return filters_copy(e, [ids](uint32_t i) { return ids[i]; }, n, buf, cap, offs, keep, n_out, need);
+}
+
+int tm_filters_copy_packed(tm_engine* e, const uint8_t* ids, uint32_t id_bytes, uint32_t n, uint8_t* buf, size_t cap,
+                           uint64_t* offs, uint32_t* keep, uint32_t* n_out, uint64_t* need) {
+    if (!e || !offs || !n_out || !need || (n && !ids) || (cap && !buf) || (id_bytes != 3 && id_bytes != 4))
+        return TM_EINVAL;
+    if (id_bytes == 4)
+        return filters_copy(e, [ids](uint32_t i) { uint32_t v; memcpy(&v, ids + 4ull * i, 4); return v; }, n, buf,
+                            cap, offs, keep, n_out, need);
+    return filters_copy(
+        e, [ids](uint32_t i) {
+            const uint8_t* p = ids + 3ull * i;
+            return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16;
+        },
+        n, buf, cap, offs, keep, n_out, need);
 }
 
 int tm_filter_id(tm_engine* e, const uint8_t* f, size_t len, uint32_t* id) {

@@ -429,6 +429,8 @@ struct tm_batch {
     unsigned long long* d_rows = nullptr;
     unsigned long long* d_wstats = nullptr;   // the walk waves' partial stats
     size_t c_wstats = 0;
+    uint8_t* d_pack = nullptr;                // the dense ids packed 3 bytes each (tm_match_batch_packed)
+    size_t c_pack = 0;
     uint32_t *d_bsums = nullptr, *d_ovf = nullptr, *d_total = nullptr;
     size_t c_sfids = 0, c_rows = 0, c_rowoff = 0, c_ids = 0, c_bsums = 0, c_ovf = 0;
     uint32_t* h_total = nullptr;
@@ -629,8 +631,8 @@ struct tm_batch {
         h_bad = nullptr;
         dev_free(d_words); dev_free(d_toff); dev_free(d_slow); dev_free(d_tflags);
         dev_free(d_sfids); dev_free(d_rows); dev_free(d_rowoff); dev_free(d_ids);
-        dev_free(d_wstats);
-        c_wstats = 0;
+        dev_free(d_wstats); dev_free(d_pack);
+        c_wstats = c_pack = 0;
         if (h_total) (void)hipHostFree(h_total);
         h_total = nullptr;
         dev_free(d_bsums); dev_free(d_ovf); dev_free(d_total);
@@ -752,9 +754,12 @@ struct Replica {
     hipStream_t pipe_copy = nullptr;                      // the results' copies to the host
     hipEvent_t pipe_h2d[2] = {nullptr, nullptr};          // staging k uploaded
     hipEvent_t pipe_cp[2] = {nullptr, nullptr};           // pipe[k]'s last result copied out
+    hipEvent_t pipe_pk[2] = {nullptr, nullptr};           // pipe[k]'s ids packed (tm_match_batch_packed)
     uint8_t* h_stage[2] = {nullptr, nullptr};             // pinned packed chunk (offsets | bytes)
     size_t ch_stage[2] = {0, 0};
     uint32_t *h_prow = nullptr, *h_pids = nullptr;
+    uint8_t* h_pids8 = nullptr;                             // the merged ids packed 3 bytes each
+    size_t ch_pids8 = 0;
     size_t ch_prow = 0, ch_pids = 0;
 
     // trie tables
@@ -2179,7 +2184,7 @@ struct tm_engine {
     // offsets to the host.  So the host fills chunk j + 1 while chunk j walks
     // and chunk j - 1's result crosses PCIe.  Row offsets are rebased at the end.
     int match_batch_pipelined(Replica& R, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
-                              tm_result* out);
+                              tm_result* out, uint32_t pack = 0);
 
     // tm_match_batch over every replica: merged CSR in m_rowoff / m_ids
     int match_batch_split(const uint8_t* topics, const uint64_t* offsets, uint32_t n, tm_result* out);

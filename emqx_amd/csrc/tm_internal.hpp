@@ -644,6 +644,8 @@ struct ExportArgs {
 };
 static_assert(std::has_unique_object_representations_v<ExportArgs>, "ExportArgs has implicit padding");
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s);
+// ids[0..n) (each < 2^24) packed little-endian 3 bytes each into out (3n bytes)
+hipError_t launch_pack_ids(const uint32_t* ids, uint64_t n, uint8_t* out, hipStream_t s);
 // the dense CSR of a batch into device-visible pinned host memory: row_off[0..n]
 // and ids[0 .. min(*d_total, cap)) (tm_match_batch: one host wait per batch)
 hipError_t launch_csr_to_host(const uint32_t* row_off, const uint32_t* ids, uint32_t n, const uint32_t* d_total,

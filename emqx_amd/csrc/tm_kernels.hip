@@ -2812,6 +2812,29 @@ hipError_t launch_csr_to_host(const uint32_t* row_off, const uint32_t* ids, uint
     return hipGetLastError();
 }
 
+// 4 ids -> 12 bytes (three aligned dword stores) per thread; the last
+// partial group byte by byte
+__global__ __launch_bounds__(256) void tm_pack_ids(const uint32_t* ids, uint64_t n, uint8_t* out) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x, j = 4 * g;
+    if (j >= n) return;
+    if (j + 4 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(ids + j);
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + 12 * g);
+        o[0] = (v.x & 0xFFFFFFu) | (v.y << 24);
+        o[1] = ((v.y >> 8) & 0xFFFFu) | (v.z << 16);
+        o[2] = ((v.z >> 16) & 0xFFu) | (v.w << 8);
+        return;
+    }
+    for (uint64_t q = j; q < n; ++q)
+        for (uint32_t b = 0; b < 3; ++b) out[3 * q + b] = (uint8_t)(ids[q] >> (8 * b));
+}
+
+hipError_t launch_pack_ids(const uint32_t* ids, uint64_t n, uint8_t* out, hipStream_t s) {
+    const uint64_t groups = (n + 3) / 4;
+    if (groups) hipLaunchKernelGGL(tm_pack_ids, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, ids, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_export_host(const ExportArgs& a, hipStream_t s) {
     const uint64_t work = a.hdr_words + a.n + a.rows_cap;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((work / 4 + 255) / 256, 1), 512);

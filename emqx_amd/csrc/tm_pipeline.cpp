@@ -106,6 +106,7 @@ int tm_engine::pipe_setup(Replica& R) {
         R.readers.push_back(&b);
         HIP_OK(hipEventCreateWithFlags(&R.pipe_h2d[k], hipEventDisableTiming));
         HIP_OK(hipEventCreateWithFlags(&R.pipe_cp[k], hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&R.pipe_pk[k], hipEventDisableTiming));
     }
     HIP_OK(hipStreamCreateWithFlags(&R.pipe_copy, hipStreamNonBlocking));
     R.pipe_ready = true;
@@ -123,7 +124,8 @@ void tm_engine::pipe_teardown(Replica& R) {
         drop_user_stream(&b);
         if (R.pipe_h2d[k]) (void)hipEventDestroy(R.pipe_h2d[k]);
         if (R.pipe_cp[k]) (void)hipEventDestroy(R.pipe_cp[k]);
-        R.pipe_h2d[k] = R.pipe_cp[k] = nullptr;
+        if (R.pipe_pk[k]) (void)hipEventDestroy(R.pipe_pk[k]);
+        R.pipe_h2d[k] = R.pipe_cp[k] = R.pipe_pk[k] = nullptr;
         if (R.h_stage[k]) (void)hipHostFree(R.h_stage[k]);
         R.h_stage[k] = nullptr;
         R.ch_stage[k] = 0;
@@ -132,13 +134,15 @@ void tm_engine::pipe_teardown(Replica& R) {
     R.pipe_copy = nullptr;
     if (R.h_prow) (void)hipHostFree(R.h_prow);
     if (R.h_pids) (void)hipHostFree(R.h_pids);
+    if (R.h_pids8) (void)hipHostFree(R.h_pids8);
     R.h_prow = R.h_pids = nullptr;
-    R.ch_prow = R.ch_pids = 0;
+    R.h_pids8 = nullptr;
+    R.ch_prow = R.ch_pids = R.ch_pids8 = 0;
     R.pipe_ready = false;
 }
 
 int tm_engine::match_batch_pipelined(Replica& R, const uint8_t* topics, const uint64_t* offsets, uint32_t n,
-                          tm_result* out) {
+                          tm_result* out, uint32_t pack) {
     int rc;
     if ((rc = pipe_setup(R))) return rc;
     const uint32_t nch = (n + PIPE_CHUNK - 1) / PIPE_CHUNK;
@@ -193,6 +197,34 @@ int tm_engine::match_batch_pipelined(Replica& R, const uint8_t* topics, const ui
             if ((rc = ensure_dense(Y))) return rc;   // (built by the launch unless ids overflowed)
             const uint64_t base = cbase[j - 1], total = Y->total;
             if (base + total > MAX_RESULT) return TM_EOVERFLOW;   // u32 CSR offsets
+            if (pack == 3) {   // ids packed to 3 bytes on the device, copied packed (h_pids8)
+                if (base + total > R.ch_pids8 / 3) {
+                    HIP_OK(hipStreamSynchronize(R.pipe_copy));
+                    const size_t want = (size_t)(base + total) +
+                                        (size_t)((double)(total + 1) / cnt * (n - lo - cnt) * 1.25) + 1024;
+                    uint8_t* np = nullptr;
+                    HIP_OK(hipHostMalloc((void**)&np, want * 3 + 16, hipHostMallocDefault));
+                    if (base) memcpy(np, R.h_pids8, base * 3);
+                    if (R.h_pids8) (void)hipHostFree(R.h_pids8);
+                    R.h_pids8 = np;
+                    R.ch_pids8 = want * 3 + 16;
+                }
+                if (total) {
+                    if ((rc = dev_reserve(Y->d_pack, Y->c_pack, total * 3 + 16))) return rc;
+                    HIP_OK(launch_pack_ids(Y->d_ids, total, Y->d_pack, Y->own));
+                }
+                HIP_OK(hipEventRecord(R.pipe_pk[k], Y->own));
+                HIP_OK(hipStreamWaitEvent(R.pipe_copy, R.pipe_pk[k], 0));
+                if (total)
+                    HIP_OK(hipMemcpyAsync(R.h_pids8 + base * 3, Y->d_pack, total * 3, hipMemcpyDeviceToHost,
+                                          R.pipe_copy));
+                HIP_OK(hipMemcpyAsync(R.h_prow + lo, Y->d_rowoff, (size_t)cnt * 4, hipMemcpyDeviceToHost,
+                                      R.pipe_copy));
+                HIP_OK(hipEventRecord(R.pipe_cp[k], R.pipe_copy));
+                cp_pending[k] = true;
+                cbase[j] = base + total;
+                continue;
+            }
             if (base + total > R.ch_pids) {
                 // grow the merged ids (earlier copies land first): room for the rest at this chunk's rate
                 HIP_OK(hipStreamSynchronize(R.pipe_copy));

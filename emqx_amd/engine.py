@@ -551,6 +551,39 @@ class Engine:
                 "tm_match_batch")
         return _result_arrays(r)
 
+    def match_batch_packed(self, topics):
+        """tm_match_batch_packed -> (row_offsets uint32[n+1], packed ids uint8[total * id_bytes],
+        id_bytes); id j = ids[j*id_bytes ...] little-endian."""
+        s = _pack(topics)
+        buf = np.ascontiguousarray(s.buf if s.buf.size else np.zeros(1, np.uint8))
+        offs = np.ascontiguousarray(s.offs, dtype=np.uint64)
+        r = N.ResultPacked()
+        N.check(self.L.tm_match_batch_packed(self.h, buf.ctypes.data, offs.ctypes.data, len(s), C.byref(r)),
+                "tm_match_batch_packed")
+        n, m, ib = r.n_topics, int(r.n_matches), int(r.id_bytes)
+        ro = np.ctypeslib.as_array(r.row_offsets, shape=(n + 1,)).copy()
+        ids = np.ctypeslib.as_array(r.ids, shape=(max(m * ib, 1),))[:m * ib].copy() if m else np.zeros(0, np.uint8)
+        return ro, ids, ib
+
+    def filters_copy_packed(self, ids, id_bytes: int) -> list:
+        """tm_filters_copy_packed over packed ids: [(index, filter bytes)]."""
+        a = np.ascontiguousarray(ids, dtype=np.uint8)
+        n = len(a) // id_bytes
+        offs = np.zeros(n + 1, np.uint64)
+        keep = np.zeros(max(n, 1), np.uint32)
+        k, need = C.c_uint32(), C.c_uint64()
+        cap = 64 * max(n, 1)
+        while True:
+            buf = np.zeros(max(cap, 1), np.uint8)
+            N.check(self.L.tm_filters_copy_packed(self.h, a.ctypes.data if n else None, id_bytes, n, buf.ctypes.data,
+                                                  cap, offs.ctypes.data, keep.ctypes.data, C.byref(k),
+                                                  C.byref(need)), "tm_filters_copy_packed")
+            if need.value <= cap:
+                break
+            cap = need.value
+        raw = buf.tobytes()
+        return [(int(keep[j]), raw[int(offs[j]):int(offs[j + 1])]) for j in range(k.value)]
+
     def prepare(self, topics, dedup: bool = False, stream: bool = False, replica=None) -> Batch:
         """Device-resident batch; dedup=True matches identical topics once (TM_BATCH_DEDUP);
         stream=True gives it a HIP stream of its own, so launches of several

@@ -222,6 +222,22 @@ TM_API int  tm_async_stats_get(tm_engine* e, tm_async_stats* out);
 TM_API int  tm_match_batch(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
                     uint32_t n, tm_result* out);
 
+/* tm_match_batch for consumers that read the ids in place (the NIF turning
+ * them into filter binaries through tm_filters_copy_packed): filter id j of
+ * the result is ids[j * id_bytes ..] little-endian, id_bytes = 3 while every
+ * node id of the engine fits 24 bits (~16.7M trie nodes), else 4.  The ids
+ * cross PCIe packed -- 3/4 of the bytes -- and nobody unpacks them.  Rows
+ * (row_offsets, u32) as in tm_result; the buffers live until the next call. */
+typedef struct {
+    uint32_t        n_topics;
+    uint32_t        id_bytes;
+    uint64_t        n_matches;
+    const uint32_t* row_offsets;
+    const uint8_t*  ids;
+} tm_result_packed;
+TM_API int  tm_match_batch_packed(tm_engine* e, const uint8_t* topics, const uint64_t* offsets,
+                    uint32_t n, tm_result_packed* out);
+
 /* Split form for pipelining / device-resident benchmarking:
  * prepare = H2D of the topic bytes and offsets (default), or host tokenise +
  *           intern + H2D of the word ids with TM_CFG_HOST_TOKENIZE
@@ -510,6 +526,10 @@ TM_API int  tm_filter_copy(tm_engine* e, uint32_t id, uint8_t* buf, size_t cap, 
  * in ids of filter k. */
 TM_API int  tm_filters_copy(tm_engine* e, const uint32_t* ids, uint32_t n, uint8_t* buf, size_t cap,
                             uint64_t* offs, uint32_t* keep, uint32_t* n_out, uint64_t* need);
+/* tm_filters_copy over ids packed id_bytes (3 or 4) bytes each, as
+ * tm_match_batch_packed returns them (no unpack pass). */
+TM_API int  tm_filters_copy_packed(tm_engine* e, const uint8_t* ids, uint32_t id_bytes, uint32_t n, uint8_t* buf,
+                            size_t cap, uint64_t* offs, uint32_t* keep, uint32_t* n_out, uint64_t* need);
 /* Id of an inserted filter, TM_ENOENT if absent. */
 TM_API int  tm_filter_id(tm_engine* e, const uint8_t* filter, size_t len, uint32_t* id);
 

@@ -15,6 +15,7 @@ from emqx_amd import _native as N
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PAIRS = [("tm_config", N.Config), ("tm_trie_node", N.TrieNode), ("tm_result", N.Result),
+         ("tm_result_packed", N.ResultPacked),
          ("tm_routes", N.Routes), ("tm_deliveries", N.Deliveries), ("tm_batch_stats", N.BatchStats),
          ("tm_engine_stats", N.EngineStats), ("tm_async_stats", N.AsyncStats),
          ("tm_sharded_stats", N.ShardedStats)]

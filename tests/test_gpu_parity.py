@@ -506,3 +506,43 @@ def test_match_batch_pipelined_grows_its_result_buffer():
     offs, ids = eng.match_batch(A)
     assert np.array_equal(offs, exp_offs)
     assert np.array_equal(ids, exp_ids)
+
+
+def _widen(ids8, ib):
+    raw = np.asarray(ids8, np.uint8).reshape(-1, ib).astype(np.uint32)
+    out = np.zeros(len(raw), np.uint32)
+    for b in range(ib):
+        out |= raw[:, b] << np.uint32(8 * b)
+    return out
+
+
+def test_match_batch_packed_equals_u32_ids():
+    """tm_match_batch_packed: the ids of tm_match_batch, 3 bytes each (little
+    endian) while the trie holds < 2^24 nodes, packed on the device before the
+    copy.  Same row offsets and, widened, the same ids: for a one-chunk batch,
+    a pipelined 2.5M-publish batch, one whose buffer grows mid-batch and an
+    empty one; tm_filters_copy_packed names the same filters as tm_filters_copy."""
+    F = gen.gen_filters(gen.C2)
+    T = gen.gen_topics(gen.C2, F, 2501, 2_500_000)
+    none = gen.Strings.from_list([b"zz/%d/unknown" % i for i in range(1_100_000)])
+    eng = Engine(device=0)
+    eng.insert_many(F)
+    eng.sync()
+    for batch in (T.slice(0, 70_000), T, gen.Strings.concat([none, T.slice(0, 1_200_000)]),
+                  gen.Strings.from_list([])):
+        offs, ids = eng.match_batch(batch)
+        offs, ids = offs.copy(), ids.copy()
+        po, pids, ib = eng.match_batch_packed(batch)
+        assert ib == 3
+        assert np.array_equal(po, offs)
+        assert len(pids) == 3 * len(ids)
+        assert np.array_equal(_widen(pids, ib), ids)
+    offs, ids = eng.match_batch(T.slice(0, 5000))
+    ids = ids.copy()
+    _, pids, ib = eng.match_batch_packed(T.slice(0, 5000))
+    assert eng.filters_copy_packed(pids, ib) == eng.filters_copy(ids)
+    # a removed filter drops out of both copies alike
+    gone = eng.filters_copy(ids[:1])[0][1]
+    eng.delete(gone)
+    eng.sync()
+    assert eng.filters_copy_packed(pids, ib) == eng.filters_copy(ids)
