@@ -155,6 +155,7 @@ SIGNATURES = {
     "tm_batch_launch": (C.c_int, [P, P]),
     "tm_batch_wait": (C.c_int, [P, P]),
     "tm_batch_result": (C.c_int, [P, P, C.POINTER(Result)]),
+    "tm_batch_result_packed": (C.c_int, [P, P, C.POINTER(ResultPacked)]),
     "tm_batch_sample": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Result)]),
     "tm_batch_stats_get": (C.c_int, [P, P, C.POINTER(BatchStats)]),
     "tm_batch_device_csr": (C.c_int, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_uint64)]),

@@ -227,7 +227,8 @@ static void packed_free(packed* p) {
     p->buf = NULL; p->offs = NULL; p->keep = NULL;
 }
 
-static int pack_filters(tm_engine* e, const uint32_t* ids, uint64_t n, packed* p) {
+/* ids are uint32 (id_bytes 0) or packed id_bytes each (tm_batch_result_packed) */
+static int pack_filters_w(tm_engine* e, const void* ids, uint32_t id_bytes, uint64_t n, packed* p) {
     if (n > 0xFFFFFFF0ull) return TM_EOVERFLOW;
     size_t cap = 32 * (size_t)n + 64;
     uint64_t need = 0;
@@ -237,12 +238,20 @@ static int pack_filters(tm_engine* e, const uint32_t* ids, uint64_t n, packed* p
     for (;;) {
         p->buf = enif_alloc(cap);
         if (!p->offs || !p->keep || !p->buf) { packed_free(p); return TM_ENOMEM; }
-        int rc = tm_filters_copy(e, ids, (uint32_t)n, p->buf, cap, p->offs, p->keep, &p->n, &need);
+        int rc = id_bytes
+                     ? tm_filters_copy_packed(e, (const uint8_t*)ids, id_bytes, (uint32_t)n, p->buf, cap, p->offs,
+                                              p->keep, &p->n, &need)
+                     : tm_filters_copy(e, (const uint32_t*)ids, (uint32_t)n, p->buf, cap, p->offs, p->keep, &p->n,
+                                       &need);
         if (rc) { packed_free(p); return rc; }
         if (need <= cap) return TM_OK;
         enif_free(p->buf);
         cap = (size_t)need;
     }
+}
+
+static int pack_filters(tm_engine* e, const uint32_t* ids, uint64_t n, packed* p) {
+    return pack_filters_w(e, ids, 0, n, p);
 }
 
 /* The list of the packed filters k with lo <= keep[k] < hi, for *k counting
@@ -358,12 +367,13 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
     (void)argc;
     if (!get_engine(env, argv[0], &r) || !pack_binaries(env, argv[1], &n, &buf, &offs)) return enif_make_badarg(env);
     tm_batch* b;
-    tm_result res;
+    tm_result_packed res;
     packed p;
     int rc = run_batch(r->e, buf, offs, n, &b);
     enif_free(buf); enif_free(offs);
-    if (!rc) rc = tm_batch_result(r->e, b, &res);
-    if (!rc) rc = pack_filters(r->e, res.filter_ids, res.n_matches, &p);
+    /* ids 3 bytes each off the device, read in place by the filter copy */
+    if (!rc) rc = tm_batch_result_packed(r->e, b, &res);
+    if (!rc) rc = pack_filters_w(r->e, res.ids, res.id_bytes, res.n_matches, &p);
     if (rc) {
         if (b) tm_batch_free(r->e, b);
         return err(env, rc);

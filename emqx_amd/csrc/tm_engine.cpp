@@ -528,6 +528,19 @@ int tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out) {
     return e->result(b, out);
 }
 
+int tm_batch_result_packed(tm_engine* e, tm_batch* b, tm_result_packed* out) {
+    if (!e || !b || !out) return TM_EINVAL;
+    if (!b->rep) return TM_ENODEV;   // host-only engine
+    std::lock_guard<std::recursive_mutex> g(e->mu);
+    int rc = e->use(b->rep);
+    if (rc) return rc;
+    try {
+        return e->result_packed(b, out);
+    } catch (...) {
+        return TM_ENOMEM;
+    }
+}
+
 int tm_batch_sample(tm_engine* e, tm_batch* b, const uint32_t* rows, uint32_t k, tm_result* out) {
     if (!e || !b || !out || (!rows && k)) return TM_EINVAL;
     if (!b->rep) return TM_ENODEV;   // host-only engine

@@ -449,6 +449,8 @@ struct tm_batch {
     uint32_t* h_rowoff = nullptr;
     uint32_t* h_ids = nullptr;
     size_t ch_rowoff = 0, ch_ids = 0;
+    uint8_t* h_ids8 = nullptr;                // the ids 3 bytes each (tm_batch_result_packed)
+    size_t ch_ids8 = 0;
     // the replica (device copy of the trie) the batch runs on; fixed for the
     // batch's life: its buffers live on that replica's device
     struct Replica* rep = nullptr;
@@ -647,6 +649,9 @@ struct tm_batch {
         if (h_rowoff) (void)hipHostFree(h_rowoff);
         if (h_ids) (void)hipHostFree(h_ids);
         h_rowoff = h_ids = nullptr;
+        if (h_ids8) (void)hipHostFree(h_ids8);
+        h_ids8 = nullptr;
+        ch_ids8 = 0;
         if (h_xrow) (void)hipHostFree(h_xrow);
         if (h_xids) (void)hipHostFree(h_xids);
         h_xrow = h_xids = nullptr;
@@ -2074,6 +2079,7 @@ struct tm_engine {
     int wait(tm_batch* b, bool drained = false, uint32_t* relaunched = nullptr);
 
     int result(tm_batch* b, tm_result* out);
+    int result_packed(tm_batch* b, tm_result_packed* out);
 
 
     // tm_batch_sample: rows rows[0..k) of a waited batch as a host CSR, gathered

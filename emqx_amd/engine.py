@@ -97,6 +97,15 @@ class Batch:
         N.check(self.eng.L.tm_batch_result(self.eng.h, self.h, C.byref(r)), "tm_batch_result")
         return _result_arrays(r)
 
+    def result_packed(self):
+        """tm_batch_result_packed -> (row_offsets u32[n+1], packed ids u8, id_bytes)."""
+        r = N.ResultPacked()
+        N.check(self.eng.L.tm_batch_result_packed(self.eng.h, self.h, C.byref(r)), "tm_batch_result_packed")
+        n, m, ib = r.n_topics, int(r.n_matches), int(r.id_bytes)
+        ro = np.ctypeslib.as_array(r.row_offsets, shape=(n + 1,)).copy()
+        ids = np.ctypeslib.as_array(r.ids, shape=(m * ib,)).copy() if m else np.zeros(0, np.uint8)
+        return ro, ids, ib
+
     def sample(self, rows):
         """tm_batch_sample: rows `rows` (row indices) of the waited batch,
         gathered on the device -> (offsets u32[k+1], ids) in that order."""

@@ -283,6 +283,11 @@ TM_API int  tm_batch_row_map(tm_engine* e, tm_batch* b, const uint32_t** row_of,
 TM_API int  tm_batch_launch(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_wait(tm_engine* e, tm_batch* b);
 TM_API int  tm_batch_result(tm_engine* e, tm_batch* b, tm_result* out);
+/* tm_batch_result with the ids packed on the device as in tm_match_batch_packed
+ * (3 bytes while node ids fit 24 bits, else 4), into the batch's own pinned
+ * buffers: valid until the batch is re-prepared or freed, so concurrent
+ * callers on their own batches (the NIF's match_batch) do not share them. */
+TM_API int  tm_batch_result_packed(tm_engine* e, tm_batch* b, tm_result_packed* out);
 /* Rows rows[0..k) of a waited batch (each < the batch's row count) as a host
  * CSR: n_topics = k, row i = filter_ids[row_offsets[i] .. row_offsets[i+1]),
  * sorted and deduplicated like tm_batch_result's.  Gathered on the device from

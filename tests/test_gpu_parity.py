@@ -537,6 +537,13 @@ def test_match_batch_packed_equals_u32_ids():
         assert np.array_equal(po, offs)
         assert len(pids) == 3 * len(ids)
         assert np.array_equal(_widen(pids, ib), ids)
+    b = eng.prepare(T.slice(0, 300_000))   # the batch-owned form (the NIF's match_batch)
+    b.launch().wait()
+    offs, ids = b.result()
+    offs, ids = offs.copy(), ids.copy()
+    po, pids, ib = b.result_packed()
+    b.free()
+    assert ib == 3 and np.array_equal(po, offs) and np.array_equal(_widen(pids, ib), ids)
     offs, ids = eng.match_batch(T.slice(0, 5000))
     ids = ids.copy()
     _, pids, ib = eng.match_batch_packed(T.slice(0, 5000))
