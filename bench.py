@@ -709,10 +709,13 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
         offs, ids = eng.match_batch(topics)
         exp_c = np.diff(offs.astype(np.int64))
         exp_h = LD.row_hashes(offs, ids)
-    LD.run(eng, topics.slice(0, min(20_000, len(topics))), LD.ASYNC, 4, 64, hashes=False)    # warm the slots
     out = {}
     for name, mode, th, win, cnt in legs:
         sub = topics if cnt == len(topics) else topics.slice(0, cnt)
+        # untimed warm-up at the leg's own concurrency: the batch sizes it
+        # forms get their slot graphs captured here (a one-time setup cost
+        # per size class, milliseconds each), not inside the timed calls
+        LD.run(eng, topics.slice(0, min(max(20_000, 8 * th * win), len(topics))), mode, th, win, hashes=False)
         b0 = eng.async_stats()
         st, counts, hashes = LD.run(eng, sub, mode, th, win)
         b1 = eng.async_stats()

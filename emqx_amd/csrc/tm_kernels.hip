@@ -1626,32 +1626,42 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) {   // fir
 
 
 
-// A topic's first 64 bytes as 8 little-endian u64 chunks, zero past len:
+// A topic's first 64 bytes as 16 little-endian u32 words, zero past len:
 // the 16-B aligned loads that cover them (the batch bytes are 16-B aligned
-// and padded by 16), all issued before any is used, and a funnel shift by the
-// topic's offset within the first load.  Lanes of a wave read neighbouring
-// topics, so a load instruction's lines are mostly the wave's next ones.
-__device__ __forceinline__ void dd_load64(const uint8_t* bytes, uint64_t b, uint32_t len, uint64_t (&c)[8]) {
+// and padded by 16), all issued before any is used, then the topic's offset
+// within the first load taken out in 32-bit ops only -- two word selects and
+// one v_alignbyte per word (64-bit variable shifts cost 3-4 VALU each).
+// Lanes of a wave read neighbouring topics, so a load instruction's lines are
+// mostly the wave's next ones.
+__device__ __forceinline__ void dd_load64(const uint8_t* bytes, uint64_t b, uint32_t len, uint32_t (&c)[16]) {
     const uint64_t a0 = b & ~15ull;
     const uint32_t sh = (uint32_t)(b & 15u);
     const uint32_t need = sh + (len < 64u ? len : 64u);
-    uint64_t w[10];
+    uint32_t w[20];
 #pragma unroll
     for (uint32_t k = 0; k < 5; ++k) {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (16u * k < need) v = *reinterpret_cast<const uint4*>(bytes + a0 + 16u * k);
-        w[2 * k] = ((uint64_t)v.y << 32) | v.x;
-        w[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
     }
-    const bool odd = sh >= 8u;
-    const uint32_t bs = (sh & 7u) * 8u;
+    // (selects as masks: written as `q ? w[i + 1] : w[i]` the compiler turns
+    // them into one dynamically indexed array -- scratch memory)
+    const uint32_t m1 = 0u - ((sh >> 2) & 1u), m2 = 0u - ((sh >> 3) & 1u);
+    uint32_t s1[19];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint64_t lo = odd ? w[j + 1] : w[j];
-        const uint64_t hi = odd ? w[j + 2] : w[j + 1];
-        const uint64_t v = bs ? (lo >> bs) | (hi << (64u - bs)) : lo;
-        const uint32_t k = 8u * j;
-        c[j] = k >= len ? 0ull : low_bytes(v, len - k < 8u ? len - k : 8u);
+    for (uint32_t i = 0; i < 19; ++i) s1[i] = w[i] ^ ((w[i] ^ w[i + 1]) & m1);
+    uint32_t s2[17];
+#pragma unroll
+    for (uint32_t i = 0; i < 17; ++i) s2[i] = s1[i] ^ ((s1[i] ^ s1[i + 2]) & m2);
+    const uint32_t r = sh & 3u;
+    const uint32_t pm = (1u << ((len & 3u) * 8u)) - 1u;   // the partial last word's bytes
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(s2[j + 1], s2[j], r);
+        c[j] = 4u * j + 4u <= len ? x : (4u * j < len ? (x & pm) : 0u);
     }
 }
 
@@ -1672,11 +1682,19 @@ __device__ __forceinline__ uint64_t dd_mix(uint64_t h, uint64_t c) {
     return h * 5u + 0x52DCE729ull;
 }
 
-// 64-bit hash of a topic: its 8-B chunks mixed in order, then its length
-__device__ __forceinline__ uint64_t dd_hash(const uint8_t* bytes, uint64_t b, uint32_t len, const uint64_t (&c)[8]) {
-    uint64_t h = 0x9E3779B97F4A7C15ull;
+// 64-bit hash of a topic.  The first 64 bytes: NH (sum over word pairs of
+// (w[2i] + k[2i]) * (w[2i+1] + k[2i+1]), exact 32x32 -> 64-bit products: one
+// v_mad_u64_u32 per 8 bytes, where a 64x64 multiply chain took three 64-bit
+// multiplies of ~4 quarter-rate ops each); the bytes past 64 (rare) chained
+// through dd_mix; then the length and a 64-bit finaliser.  Only the table's
+// spread depends on it: a collision costs a probe and a byte compare.
+__device__ __forceinline__ uint64_t dd_hash(const uint8_t* bytes, uint64_t b, uint32_t len, const uint32_t (&c)[16]) {
+    constexpr uint32_t K[16] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu, 0x165667B1u, 0xD3A2646Du,
+                                0xFD7046C5u, 0xB55A4F09u, 0x6C8E9CF5u, 0x7FEB352Du, 0x846CA68Bu, 0x94D049BBu,
+                                0xBF58476Du, 0x1CE4E5B9u, 0x2545F491u, 0x9FB21C65u};
+    uint64_t h = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) h = dd_mix(h, c[j]);
+    for (uint32_t j = 0; j < 8; ++j) h += (uint64_t)(c[2 * j] + K[2 * j]) * (uint64_t)(c[2 * j + 1] + K[2 * j + 1]);
     for (uint32_t k = 64; k < len; k += 8)   // (topics over 64 bytes: rare, kept narrow)
         h = dd_mix(h, low_bytes(dd_u64(bytes, b + k), len - k < 8u ? len - k : 8u));
     h ^= (uint64_t)len * 0xC2B2AE3D27D4EB4Full;
@@ -1688,15 +1706,15 @@ __device__ __forceinline__ uint64_t dd_hash(const uint8_t* bytes, uint64_t b, ui
 }
 
 // the len bytes at b (first 64 in c) equal to the len bytes at ob?
-__device__ __forceinline__ bool dd_equal(const uint8_t* bytes, const uint64_t (&c)[8], uint64_t b, uint64_t ob,
+__device__ __forceinline__ bool dd_equal(const uint8_t* bytes, const uint32_t (&c)[16], uint64_t b, uint64_t ob,
                                          uint32_t len) {
-    uint64_t o[8];
+    uint32_t o[16];
     dd_load64(bytes, ob, len, o);
-    uint64_t diff = 0;
+    uint32_t diff = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) diff |= c[j] ^ o[j];
+    for (uint32_t j = 0; j < 16; ++j) diff |= c[j] ^ o[j];
     for (uint32_t k = 64; diff == 0 && k < len; k += 8)   // (topics over 64 bytes: rare, kept narrow)
-        diff |= low_bytes(dd_u64(bytes, b + k) ^ dd_u64(bytes, ob + k), len - k < 8u ? len - k : 8u);
+        diff |= low_bytes(dd_u64(bytes, b + k) ^ dd_u64(bytes, ob + k), len - k < 8u ? len - k : 8u) != 0;
     return diff == 0;
 }
 
@@ -1719,7 +1737,7 @@ __device__ __forceinline__ unsigned long long dd_want(uint64_t h, uint64_t b, ui
 }
 
 __device__ __forceinline__ uint32_t dd_claim(const DedupArgs& a, uint64_t h, uint64_t b, uint32_t len,
-                                             const uint64_t (&c)[8]) {
+                                             const uint32_t (&c)[16]) {
     const unsigned long long want = dd_want(h, b, len);
     uint64_t i = h & a.mask;
     for (;;) {
@@ -1753,7 +1771,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
     __shared__ uint32_t lslot[DD_BLOCK];
     __shared__ uint64_t lb[DD_BLOCK];
     __shared__ uint32_t ll[DD_BLOCK];
-    __shared__ uint64_t lc[8][DD_BLOCK];   // every publish's first 64 bytes: a follower checks its leader's here
+    __shared__ uint32_t lc[16][DD_BLOCK];   // every publish's first 64 bytes: a follower checks its leader's here
     const uint32_t tid = threadIdx.x;
     const uint32_t t = blockIdx.x * DD_BLOCK + tid;
     const bool valid = t < a.n;
@@ -1766,7 +1784,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
     bool resolved = false;
     uint32_t rslot = 0;
     {
-        uint64_t c[8];
+        uint32_t c[16];
         dd_load64(a.bytes, b, len, c);
         if (valid) {
             h = dd_hash(a.bytes, b, len, c);
@@ -1783,7 +1801,7 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
             }
         }
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) lc[q][tid] = c[q];
+        for (uint32_t q = 0; q < 16; ++q) lc[q][tid] = c[q];
     }
     lb[tid] = b;
     ll[tid] = len;
@@ -1811,14 +1829,14 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
                 leader = true;
                 pend = false;
             } else if (ll[L] == len) {   // the leader's first 64 bytes from LDS, the rest (long topics) from HBM
-                uint64_t diff = 0;
+                uint32_t diff = 0;
 #pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) diff |= lc[q][L] ^ lc[q][tid];
+                for (uint32_t q = 0; q < 16; ++q) diff |= lc[q][L] ^ lc[q][tid];
                 bool eq = diff == 0;
                 if (eq && len > 64u) {
-                    uint64_t c[8];
+                    uint32_t c[16];
 #pragma unroll
-                    for (uint32_t q = 0; q < 8; ++q) c[q] = lc[q][tid];
+                    for (uint32_t q = 0; q < 16; ++q) c[q] = lc[q][tid];
                     eq = dd_equal(a.bytes, c, b, lb[L], len);
                 }
                 if (eq) {
@@ -1829,9 +1847,9 @@ __global__ __launch_bounds__(DD_BLOCK) void tm_dedup_claim(DedupArgs a) {
         }
     }
     if (leader) {
-        uint64_t c[8];
+        uint32_t c[16];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) c[q] = lc[q][tid];
+        for (uint32_t q = 0; q < 16; ++q) c[q] = lc[q][tid];
         lslot[tid] = dd_claim(a, h, b, len, c);
     }
     __syncthreads();
@@ -1972,15 +1990,14 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
         const uint64_t b = a.offs[t] - a.base;
         const uint32_t n = (uint32_t)(a.offs[t + 1] - a.offs[t]);
         for (uint32_t k = 0; k < n; k += 64) {
-            uint64_t x[8];
+            uint32_t x[16];
             dd_load64(a.bytes, b + k, n - k, x);
             const uint32_t m = n - k < 64u ? n - k : 64u;
 #pragma unroll
             for (uint32_t q = 0; q < 16; ++q) {
                 if (4u * q >= m) break;
                 const uint32_t nb = m - 4u * q < 4u ? m - 4u * q : 4u;
-                const uint32_t v = (uint32_t)(x[q >> 1] >> (32 * (q & 1)));
-                dd_put(a.cbytes, lo, hi, acc, bits, w, nb == 4u ? v : (v & ((1u << (8 * nb)) - 1u)), nb);
+                dd_put(a.cbytes, lo, hi, acc, bits, w, x[q], nb);   // (x is zero past the topic)
             }
         }
         ++row;
