@@ -708,7 +708,7 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     }
     a.s_qparent = b->d_sqpar; a.s_qpw = b->d_sqpw; a.s_qmeta = b->d_sqmeta; a.s_qkey = b->d_sqkey;
     a.s_ofid = b->d_sofid; a.s_okey = b->d_sokey;
-    a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves;
+    a.s_qcap = b->s_qcap; a.s_ocap = b->s_ocap; a.s_waves = b->s_waves; a.s_lcap = kn.slow_lds;
     a.nwords = (uint32_t)std::max<uint64_t>(b->nwords, 1);
     a.nslots = (uint32_t)slots.size();
     // (bounds of the checked build only: left 0 otherwise, so churn does not

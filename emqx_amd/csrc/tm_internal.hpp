@@ -183,7 +183,7 @@ struct MatchArgs {
                                 // batch's rows, known only on the device when the walk is enqueued
     const uint32_t* slow_list;  // host-flagged slow topics
     uint32_t n_slow;
-    uint32_t pad1_;
+    uint32_t s_lcap;            // generic path: LDS probe-stack entries to use (0 = all; TM_SLOW_LDS)
     const uint32_t* d_nslow;    // device-resident count of slow_list (token batches), or null
     // outputs
     uint32_t* count;          // per topic |M(t)|
@@ -672,6 +672,7 @@ struct Knobs {
     bool par_trace = false;        // TM_PAR_TRACE: per-phase churn timings on stderr
     bool dedup_weak_hash = false;  // TM_DEDUP_WEAK_HASH=1: the dedup's hash degraded to the length
     int row_cap = 0;               // TM_ROWCAP: fast-path row slots per topic (1..128)
+    uint32_t slow_lds = 0;         // TM_SLOW_LDS: generic-path LDS stack entries (small: forces the global restart)
     uint64_t fan_big = 0;          // TM_FAN_BIG: fan-out scan blocks above this use u64 offsets
     uint64_t result_limit = 0;     // TM_RESULT_LIMIT: matches per batch
     uint64_t staging_min = 0;      // TM_STAGING_MIN: initial staging entries of a batch
@@ -690,6 +691,7 @@ struct Knobs {
         k.par_trace = env("TM_PAR_TRACE") != nullptr;
         k.dedup_weak_hash = on("TM_DEDUP_WEAK_HASH");
         if (const char* v = env("TM_ROWCAP")) k.row_cap = std::min(128, std::max(1, atoi(v)));
+        if (const char* v = env("TM_SLOW_LDS")) k.slow_lds = (uint32_t)std::max(1, atoi(v));
         if (const char* v = env("TM_FAN_BIG")) k.fan_big = std::min<uint64_t>(0xFFFFFFFFull, strtoull(v, nullptr, 10));
         if (const char* v = env("TM_RESULT_LIMIT")) k.result_limit = strtoull(v, nullptr, 10);
         if (const char* v = env("TM_STAGING_MIN")) k.staging_min = std::max<uint64_t>(64, strtoull(v, nullptr, 10));

@@ -811,10 +811,17 @@ __device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp
     }
 }
 
-#ifndef TM_SORT_LDS
-#define TM_SORT_LDS 1024   // generic path: rows up to this many are sorted in LDS (12 B each: it bounds waves per CU; C5 K=1000 device 3.54 -> 2.95 ms vs 2048)
+// Generic path LDS: the probe stack while a topic is walked (SLOW_SQ 16-B
+// entries {parent, meta, key lo, key hi}), then the same 16 KB as the row's
+// sort area: 2,048 u64 (path code | filter id) or 4,096 u32 filter ids (rows
+// ordered by bytes).  A LIFO stack popped 64 at a time grows by at most 64
+// entries per level, so 1,024 holds a 10-level topic's whole frontier; a
+// deeper or wider one restarts in global scratch.
+#ifndef TM_SLOW_SQ
+#define TM_SLOW_SQ 1024
 #endif
-constexpr uint32_t SORT_LDS = TM_SORT_LDS;
+constexpr uint32_t SLOW_SQ = TM_SLOW_SQ;
+constexpr uint32_t SORT_LDS = SLOW_SQ * 2;    // u64 entries of the sort area
 constexpr uint32_t SM_PLUS = 1u << 29;
 constexpr uint32_t SM_SKIPE = 1u << 30;
 constexpr uint32_t SM_DSTART = 1u << 31;
@@ -824,10 +831,46 @@ __device__ __forceinline__ uint32_t slow_flags(uint32_t pf) {
     return ((pf & M_PLUS) ? SM_PLUS : 0u) | ((pf & M_SKIPE) ? SM_SKIPE : 0u) | ((pf & M_DSTART) ? SM_DSTART : 0u);
 }
 
+// bitonic sort of n (power of two) u64 in LDS, ascending
+__device__ void bitonic_lds64(unsigned long long* k, uint32_t n) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t kk = 2; kk <= n; kk <<= 1) {
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = k[i], y = k[ixj];
+                    if ((x > y) == ((i & kk) == 0)) { k[i] = y; k[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// bitonic sort of n (power of two) filter ids in LDS by filter bytes
+template <bool CK>
+__device__ void bitonic_lds_bytes(const MatchArgs& a, uint32_t* f, uint32_t n) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t kk = 2; kk <= n; kk <<= 1) {
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t x = f[i], y = f[ixj];
+                    if (filter_less<CK>(a, y, x) == ((i & kk) == 0)) { f[i] = y; f[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <bool CK, bool BIG>
 __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
-    __shared__ unsigned long long sk[SORT_LDS];
-    __shared__ uint32_t sf[SORT_LDS];
+    __shared__ uint4 sq[SLOW_SQ];
+    unsigned long long* const sk = reinterpret_cast<unsigned long long*>(sq);   // (after the walk)
+    uint32_t* const sfi = reinterpret_cast<uint32_t*>(sq);
     const uint32_t lane = threadIdx.x;
     const uint32_t wave = blockIdx.x;
     uint32_t* qpar = a.s_qparent + (size_t)wave * a.s_qcap;
@@ -838,6 +881,7 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
     const uint32_t novf = min(a.ctrl[CTRL_NOVF], a.ovf_cap);
     const uint32_t n_slow = a.d_nslow ? min(*a.d_nslow, a.n) : a.n_slow;
     const uint32_t total_items = n_slow + novf;
+    const uint32_t lcap = a.s_lcap && a.s_lcap < SLOW_SQ ? a.s_lcap : SLOW_SQ;
     unsigned long long sV = 0, sH = 0, sW = 0, sM = 0, sS = 0;
 
     for (uint32_t item = wave; item < total_items; item += gridDim.x) {
@@ -853,79 +897,119 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
         sS += 1;
         uint32_t qn = 0, on = 0;
         bool err = false;
-        if (d > 0) {
-            Expand x; x.ne = 0; x.np = 0;
-            if (lane == 0) {
-                sV += 1; sW += d;
-                if (!dollar && (a.root.flags & NF_HASH)) sH += 1;
-                expand_root(a.root, dollar, d, w[0], x);
-                if (x.np >= 1) { qpar[0] = ROOT; qkey[0] = x.pk0; qmeta[0] = 1u | slow_flags(x.pf0); }
-                if (x.np >= 2) { qpar[1] = ROOT; qkey[1] = x.pk1; qmeta[1] = 1u | slow_flags(x.pf1); }
-                if (x.ne >= 1) { ofid[0] = x.ef0; okey[0] = x.ek0; }
+        // the stack in LDS; a topic whose frontier outgrows it walks again
+        // with the stack in its wave's global scratch (the counters of the
+        // abandoned attempt are dropped)
+        for (bool in_lds = true;;) {
+            unsigned long long tV = 0, tH = 0, tW = 0;
+            bool spill = false;
+            qn = 0; on = 0;
+            if (d > 0) {
+                Expand x; x.ne = 0; x.np = 0;
+                if (lane == 0) {
+                    tV += 1; tW += d;
+                    if (!dollar && (a.root.flags & NF_HASH)) tH += 1;
+                    expand_root(a.root, dollar, d, w[0], x);
+                    if (in_lds) {
+                        if (x.np >= 1) sq[0] = uint4{ROOT, 1u | slow_flags(x.pf0), (uint32_t)x.pk0, (uint32_t)(x.pk0 >> 32)};
+                        if (x.np >= 2) sq[1] = uint4{ROOT, 1u | slow_flags(x.pf1), (uint32_t)x.pk1, (uint32_t)(x.pk1 >> 32)};
+                    } else {
+                        if (x.np >= 1) { qpar[0] = ROOT; qkey[0] = x.pk0; qmeta[0] = 1u | slow_flags(x.pf0); }
+                        if (x.np >= 2) { qpar[1] = ROOT; qkey[1] = x.pk1; qmeta[1] = 1u | slow_flags(x.pf1); }
+                    }
+                    if (x.ne >= 1) { ofid[0] = x.ef0; okey[0] = x.ek0; }
+                }
+                qn = __shfl(x.np, 0, 64);
+                on = __shfl(x.ne, 0, 64);
+                if (!in_lds) __threadfence_block();
+                __syncthreads();
             }
-            qn = __shfl(x.np, 0, 64);
-            on = __shfl(x.ne, 0, 64);
-            __threadfence_block();
-            __syncthreads();
-        }
-        while (qn > 0 && !err) {
-            const uint32_t k = min(qn, 64u);
-            const bool has = lane < k;
-            const uint32_t idx = qn - k + lane;
-            uint32_t parent = 0, meta = 0;
-            unsigned long long key = 0;
-            if (has) {
-                const uint32_t ci = CK_(idx, a.s_qcap, 27);
-                parent = qpar[ci]; meta = qmeta[ci]; key = qkey[ci];
+            while (qn > 0) {
+                const uint32_t k = min(qn, 64u);
+                const bool has = lane < k;
+                const uint32_t idx = qn - k + lane;
+                uint32_t parent = 0, meta = 0;
+                unsigned long long key = 0;
+                if (has) {
+                    if (in_lds) {
+                        const uint4 e = sq[CK_(idx, SLOW_SQ, 27)];
+                        parent = e.x; meta = e.y; key = ((unsigned long long)e.w << 32) | e.z;
+                    } else {
+                        const uint32_t ci = CK_(idx, a.s_qcap, 27);
+                        parent = qpar[ci]; meta = qmeta[ci]; key = qkey[ci];
+                    }
+                }
+                if (!in_lds) __threadfence_block();
+                __syncthreads();   // every entry popped before the pushes reuse their places
+                qn -= k;
+                const uint32_t lc = meta & SM_LVL;
+                uint32_t pw = W_PLUS;
+                if (has && !(meta & SM_PLUS)) pw = w[CK_(lc - 1, d, 28)] & WID_MASK;
+                Node s;
+                const bool found = has && probe<CK, BIG>(a, parent, pw, s);
+                Expand x; x.ne = 0; x.np = 0;
+                if (found) {
+                    if (!(meta & SM_DSTART)) tV += 1;
+                    if (s.flags & NF_HASH) tH += 1;
+                    const uint32_t fl2 = (meta & SM_SKIPE) ? M_SKIPE : 0u;
+                    expand(s, lc, d, fl2, key, lc < d ? w[CK_(lc, d, 29)] : 0u, w[CK_(lc - 1, d, 28)], x);
+                }
+                const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
+                const uint64_t e0 = __ballot(x.ne >= 1), e1 = __ballot(x.ne >= 2);
+                const uint32_t ptot = __popcll(b0) + __popcll(b1);
+                const uint32_t etot = __popcll(e0) + __popcll(e1);
+                if (in_lds && qn + ptot > lcap) { spill = true; break; }
+                if (qn + ptot > a.s_qcap || on + etot > a.s_ocap) { err = true; break; }
+                const uint32_t pre = prefix_count(b0) + prefix_count(b1);
+                const uint32_t m0 = (lc + 1) | slow_flags(x.pf0), m1 = (lc + 1) | slow_flags(x.pf1);
+                if (in_lds) {
+                    if (x.np >= 1) sq[qn + pre] = uint4{s.child, m0, (uint32_t)x.pk0, (uint32_t)(x.pk0 >> 32)};
+                    if (x.np >= 2) sq[qn + pre + 1] = uint4{s.child, m1, (uint32_t)x.pk1, (uint32_t)(x.pk1 >> 32)};
+                } else {
+                    if (x.np >= 1) { const uint32_t p = qn + pre; qpar[p] = s.child; qkey[p] = x.pk0; qmeta[p] = m0; }
+                    if (x.np >= 2) { const uint32_t p = qn + pre + 1; qpar[p] = s.child; qkey[p] = x.pk1; qmeta[p] = m1; }
+                }
+                qn += ptot;
+                const uint32_t epre = prefix_count(e0) + prefix_count(e1);
+                if (x.ne >= 1) { ofid[on + epre] = x.ef0; okey[on + epre] = x.ek0; }
+                if (x.ne >= 2) { ofid[on + epre + 1] = x.ef1; okey[on + epre + 1] = x.ek1; }
+                on += etot;
+                if (!in_lds) __threadfence_block();
+                __syncthreads();
             }
-            __threadfence_block();
-            __syncthreads();
-            qn -= k;
-            const uint32_t lc = meta & SM_LVL;
-            uint32_t pw = W_PLUS;
-            if (has && !(meta & SM_PLUS)) pw = w[CK_(lc - 1, d, 28)] & WID_MASK;
-            Node s;
-            const bool found = has && probe<CK, BIG>(a, parent, pw, s);
-            Expand x; x.ne = 0; x.np = 0;
-            if (found) {
-                if (!(meta & SM_DSTART)) sV += 1;
-                if (s.flags & NF_HASH) sH += 1;
-                const uint32_t fl2 = (meta & SM_SKIPE) ? M_SKIPE : 0u;
-                expand(s, lc, d, fl2, key, lc < d ? w[CK_(lc, d, 29)] : 0u, w[CK_(lc - 1, d, 28)], x);
+            if (spill) {
+                in_lds = false;
+                __syncthreads();
+                continue;
             }
-            const uint64_t b0 = __ballot(x.np >= 1), b1 = __ballot(x.np >= 2);
-            const uint64_t e0 = __ballot(x.ne >= 1), e1 = __ballot(x.ne >= 2);
-            const uint32_t ptot = __popcll(b0) + __popcll(b1);
-            const uint32_t etot = __popcll(e0) + __popcll(e1);
-            if (qn + ptot > a.s_qcap || on + etot > a.s_ocap) { err = true; break; }
-            const uint32_t pre = prefix_count(b0) + prefix_count(b1);
-            if (x.np >= 1) { const uint32_t p = qn + pre; qpar[p] = s.child; qkey[p] = x.pk0; qmeta[p] = (lc + 1) | slow_flags(x.pf0); }
-            if (x.np >= 2) { const uint32_t p = qn + pre + 1; qpar[p] = s.child; qkey[p] = x.pk1; qmeta[p] = (lc + 1) | slow_flags(x.pf1); }
-            qn += ptot;
-            const uint32_t epre = prefix_count(e0) + prefix_count(e1);
-            if (x.ne >= 1) { ofid[on + epre] = x.ef0; okey[on + epre] = x.ek0; }
-            if (x.ne >= 2) { ofid[on + epre + 1] = x.ef1; okey[on + epre + 1] = x.ek1; }
-            on += etot;
-            __threadfence_block();
-            __syncthreads();
+            sV += tV; sH += tH; sW += tW;
+            break;
         }
         if (err) {
             if (lane == 0) atomicOr(&a.ctrl[CTRL_ERR], ERR_SLOW_SCRATCH);
             __syncthreads();
             continue;
         }
-        // sort the row (path code, or filter bytes for deep/irregular topics)
+        __threadfence_block();   // this wave's emissions, read back below
+        __syncthreads();
+        // sort the row (path code | filter id, or filter bytes for deep /
+        // irregular topics), in LDS when it fits
         uint32_t np2 = 1;
         while (np2 < on) np2 <<= 1;
+        bool sorted_in_lds = false;
         if (on > 1) {
-            if (np2 <= SORT_LDS) {
-                for (uint32_t i = lane; i < np2; i += 64) {
-                    sk[i] = i < on ? okey[i] : ~0ull;
-                    sf[i] = i < on ? ofid[i] : NONE;
-                }
+            if (!by_bytes && np2 <= SORT_LDS) {
+                // (path codes use bits 31..63, filter ids < 2^30: one u64
+                // orders by code, then id)
+                for (uint32_t i = lane; i < np2; i += 64) sk[i] = i < on ? (okey[i] | ofid[i]) : ~0ull;
                 __syncthreads();
-                bitonic<CK>(a, sk, sf, np2, by_bytes);
-                for (uint32_t i = lane; i < on; i += 64) ofid[i] = sf[i];
+                bitonic_lds64(sk, np2);
+                sorted_in_lds = true;
+            } else if (by_bytes && np2 <= 2 * SORT_LDS) {
+                for (uint32_t i = lane; i < np2; i += 64) sfi[i] = i < on ? ofid[i] : NONE;
+                __syncthreads();
+                bitonic_lds_bytes<CK>(a, sfi, np2);
+                sorted_in_lds = true;
             } else if (np2 <= a.s_ocap) {
                 for (uint32_t i = on + lane; i < np2; i += 64) { okey[i] = ~0ull; ofid[i] = NONE; }
                 __threadfence_block();
@@ -933,6 +1017,7 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
                 bitonic<CK>(a, okey, ofid, np2, by_bytes);
             } else {
                 if (lane == 0) atomicOr(&a.ctrl[CTRL_ERR], ERR_SLOW_SCRATCH);
+                __syncthreads();
                 continue;
             }
             __threadfence_block();
@@ -945,7 +1030,10 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
         const bool fits = base + on <= a.rcap;
         base += (uint64_t)g * a.rcap;
         if (fits) {
-            for (uint32_t i = lane; i < on; i += 64) a.sfids[CK_(base + i, a.sfids_cap, 30)] = ofid[i];
+            for (uint32_t i = lane; i < on; i += 64) {
+                const uint32_t f = !sorted_in_lds ? ofid[i] : by_bytes ? sfi[i] : (uint32_t)(sk[i] & ~KEY_MASK);
+                a.sfids[CK_(base + i, a.sfids_cap, 30)] = f;
+            }
         } else if (lane == 0) {
             atomicOr(&a.ctrl[CTRL_ERR], ERR_STAGING);
         }

@@ -239,6 +239,44 @@ def test_forced_slow_path_parity():
     assert_same(T, engine_rows(eng, T), exp)
 
 
+@pytest.mark.parametrize("slow_lds", [None, "2"])
+def test_long_rows_every_generic_sort(slow_lds):
+    """Rows far past the fast path's K go to the generic path, whose probe
+    stack lives in LDS (TM_SLOW_LDS=2: every topic outgrows it and walks again
+    in global scratch) and whose sort runs in LDS up to 2,048 path-coded
+    matches or 4,096 byte-ordered ones, in global scratch beyond: topics with
+    ~1,000, ~1,500, ~3,000 (depth 10) and ~6,000 (depth 11, ordered by bytes)
+    matches, beside ordinary ones."""
+    import itertools
+    F = set()
+    topics = []
+    for depth, hashes in ((10, False), (9, True), (10, True), (11, False), (12, True)):
+        ws = [b"l%d%s_%d" % (depth, b"h" if hashes else b"", i) for i in range(depth)]
+        topics.append(b"/".join(ws))
+        for mask in itertools.product((0, 1), repeat=depth):
+            lv = [b"+" if m else w for m, w in zip(mask, ws)]
+            F.add(b"/".join(lv))
+            if hashes:
+                F.add(b"/".join(lv + [b"#"]))
+                F.add(b"/".join(lv[:-1] + [b"#"]))
+    F = sorted(F | {b"#", b"+/#", b"zz/top"})
+    T = topics + [b"zz/top", b"l10_0/x", b"nothing/here"] + topics
+    env = {"TM_SLOW_LDS": slow_lds} if slow_lds else {}
+    os.environ.update(env)
+    try:
+        eng = Engine(device=0)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    eng.insert_many(F)
+    eng.sync()
+    exp, _ = oracle_rows(F, T)
+    # path-coded rows sorted in LDS (np2 2,048) and in global scratch (4,096);
+    # by bytes (deeper than 10 levels) in LDS (4,096) and in global scratch
+    assert [len(r) for r in exp[:5]] == [1029, 1282, 2563, 2054, 10245]
+    assert_same(T, engine_rows(eng, T), exp)
+
+
 def test_deep_irregular_and_edge_topics():
     rng = random.Random(9)
     W = [b"a", b"b", b"", b"!", b"%", b"$q", b"#x", b"~", b"\xc3\xa9"]
