@@ -674,7 +674,11 @@ int tm_engine::launch(tm_batch* b, bool csr) {
     MatchArgs a{};
     a.slots = R.d_slots;
     a.nbuckets = nbuckets();
-    a.max_probe = max_disp;
+    // (a bound on the probe run, not the exact max_disp: a longer run stops
+    // at its first bucket with a free last slot all the same, and a value
+    // that changes only at these steps keeps the captured launch graphs of
+    // churned batches valid)
+    a.max_probe = max_disp <= 4 ? 4 : max_disp <= 8 ? 8 : max_disp <= 16 ? 16 : max_disp <= 48 ? 48 : max_disp;
     a.root = root_rec();
     a.foff = R.d_foff; a.flen = R.d_flen; a.fbytes = R.d_fbytes;
     a.words = b->d_words; a.toff = b->d_toff; a.tflags = b->d_tflags; a.n = b->n;
@@ -775,6 +779,20 @@ int tm_engine::launch(tm_batch* b, bool csr) {
             HIP_OK(graph_replay(b, S));
             grc = 0;
         } else {
+            if (kn.par_trace && b->gkey.size() == key.size()) {   // which arguments changed (offsets per struct)
+                const size_t ends[5] = {sizeof t, sizeof t + sizeof ts, sizeof t + sizeof ts + sizeof a,
+                                        sizeof t + sizeof ts + sizeof a + sizeof s, key.size()};
+                const char* names[5] = {"tok", "tscan", "match", "scan", "dedup"};
+                fprintf(stderr, "[graph key miss]");
+                size_t st = 0;
+                for (int q = 0; q < 5; ++q) {
+                    for (size_t i = st; i < ends[q]; i += 4)
+                        if (memcmp(&key[i], &b->gkey[i], std::min<size_t>(4, ends[q] - i)))
+                            fprintf(stderr, " %s+%zu", names[q], i - st);
+                    st = ends[q];
+                }
+                fprintf(stderr, "\n");
+            }
             if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
             b->gexec = nullptr;
             if (b->gkey == key) {   // the second launch with these arguments: capture them

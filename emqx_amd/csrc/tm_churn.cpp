@@ -39,7 +39,7 @@ int tm_engine::trie_insert_ids(const uint8_t* t, size_t len, const uint32_t* ids
                 // node ids are 30-bit (two flag bits ride in the slot's id words); a
                 // parallel batch checked its whole need up front
                 const size_t need = ids.size() - k;
-                if (!M && nd.size() + need >= MAX_NODES && free_nodes.size() + pending_free.size() < need)
+                if (!M && nd.size() + need >= MAX_NODES && free_nodes.size() + pending_n < need)
                     return TM_ENOMEM;
                 created = true;
             }
@@ -84,11 +84,11 @@ int tm_engine::trie_delete(const uint8_t* t, size_t len) {
     return trie_delete_at(n, ids.data(), (uint32_t)ids.size());
 }
 
-int tm_engine::trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids) {
+int tm_engine::trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids, uint32_t sd) {
     struct { const uint32_t* d; uint32_t n; size_t size() const { return n; } uint32_t operator[](size_t i) const { return d[i]; } } ids{ids_p, nids};
     Mut* const M = tl_mut;
     std::unique_lock<std::recursive_mutex> nl;
-    if (M && ids.size() < 2) nl = std::unique_lock<std::recursive_mutex>(shared_mu(n));
+    if (M && ids.size() < sd) nl = std::unique_lock<std::recursive_mutex>(shared_mu(n));
     if (nd[n].ec != 0) {
         if (nd[n].topic) {
             clear_topic(n);
@@ -106,9 +106,9 @@ int tm_engine::trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids) 
         const uint32_t w = ids[k];
         delete_edge_of(child);
         if (!child_dead) { kill_node(child); child_dead = true; }
-        // (a parallel batch: the nodes of depth < 2 are shared by workers)
+        // (a parallel batch: the nodes of depth < sd are shared by workers)
         std::unique_lock<std::recursive_mutex> rl;
-        if (M && k < 2) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
+        if (M && k < sd) rl = std::unique_lock<std::recursive_mutex>(shared_mu(p));
         bool sig_changed = true;
         if (w == W_PLUS) nd[p].plus = NONE;
         else if (w == W_HASH) nd[p].hash = NONE;
@@ -213,6 +213,10 @@ void tm_engine::plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo
             PlanEnt& pe = plan[pbase + g0 + q];
             if (del) pe.node = (root_live && known[q] && k[q] == pe.nw) ? node[q] : NONE;
             else { pe.node = node[q]; pe.depth = k[q]; }
+            const uint32_t* w = W.data() + pe.woff;
+            pe.pkey = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
+            pe.sub = (uint8_t)(pe.nw > 2 ? mix_word(w[2] * 0xC2B2AE35u + 7) % PART_SPLIT : 0);
+            pe.unk = !known[q];
         }
         if (ptrace) d_walk += clk::now() - c2;
     }
@@ -259,10 +263,27 @@ void tm_engine::make_plan_pair(const uint8_t* dbuf, const uint64_t* doffs, uint3
 }
 
 uint32_t tm_engine::replan_dead_inserts(uint32_t n) {
-    std::vector<uint32_t>& redo = replan_buf;
+    const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 1024));
+    if (replan_buf.size() < nt) replan_buf.resize(nt);
+    if (nt == 1) {
+        replan_range(0, n, replan_buf[0]);
+        return (uint32_t)replan_buf[0].size();
+    }
+    ensure_pool();
+    std::atomic<uint32_t> total{0};
+    pool.run([&](unsigned i) {   // (read-only on the trie; each worker's own plan entries)
+        for (unsigned j = i; j < nt; j += pool.n) {
+            replan_range((uint32_t)((uint64_t)n * j / nt), (uint32_t)((uint64_t)n * (j + 1) / nt), replan_buf[j]);
+            total.fetch_add((uint32_t)replan_buf[j].size(), std::memory_order_relaxed);
+        }
+    });
+    return total.load();
+}
+
+void tm_engine::replan_range(uint32_t lo, uint32_t hi, std::vector<uint32_t>& redo) {
     redo.clear();
-    for (uint32_t i = 0; i < n; ++i) {
-        if (i + 16 < n && plan[i + 16].node != ROOT) __builtin_prefetch(&nd[plan[i + 16].node]);
+    for (uint32_t i = lo; i < hi; ++i) {
+        if (i + 16 < hi && plan[i + 16].node != ROOT) __builtin_prefetch(&nd[plan[i + 16].node]);
         const PlanEnt& pe = plan[i];
         if (pe.node != ROOT && !nd[pe.node].live) redo.push_back(i);
     }
@@ -298,7 +319,6 @@ uint32_t tm_engine::replan_dead_inserts(uint32_t n) {
             }
         }
     }
-    return (uint32_t)redo.size();
 }
 
 void tm_engine::prefetch_insert(uint32_t i, uint32_t n) {
@@ -347,6 +367,7 @@ int tm_engine::insert_planned(const uint8_t* buf, const uint64_t* offs, uint32_t
 void tm_engine::ensure_pool() {
     if (!pool_started) {
         cpu_set_t cpus;
+        pool.trace = kn.par_trace;
         pool.start(threads, device_node_cpus(device, threads, kn.pool_pin, cpus) ? &cpus : nullptr);
         pool_started = true;
     }
@@ -365,10 +386,12 @@ void tm_engine::prefetch_edge_of(const std::vector<uint32_t>& v, size_t q) const
 
 void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
     const unsigned T = std::max(1u, threads);
-    auto each = [&](auto&& fn) {
-        for (std::vector<Mut>* W : Ws)
-            for (Mut& m : *W) fn(m);
-    };
+    std::vector<Mut*> ms;   // every phase-1 state
+    for (std::vector<Mut>* W : Ws)
+        for (Mut& m : *W) {
+            m.defer = false;
+            ms.push_back(&m);
+        }
     auto merge_edges = [&](std::vector<Mut>& X) {
         for (Mut& m : X) {
             live_edges += m.live_edges; used_slots += m.used_slots; max_disp = std::max(max_disp, m.max_disp);
@@ -383,32 +406,52 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
         RS = ((nb + 2 * T2 - 1) / (2 * T2) + 15) / 16 * 16;   // whole 16-bucket groups: dirty-mark words stay per range
         R = (nb + RS - 1) / RS;
     };
-    each([](Mut& m) { m.defer = false; });
     const bool trace = kn.par_trace;
     auto now = [] { return std::chrono::steady_clock::now(); };
-    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    auto msd = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto e0 = now();
+    size_t ndel = 0, nins = 0;
+    for (Mut* m : ms) {
+        ndel += m->del.size();
+        nins += m->ins.size();
+    }
+    // Whether the inserts need a rehash first (the serial insert_edge's rule,
+    // for the whole batch) is known now: the deletes free exactly ndel slots
+    // and leave max_disp as it is.  Without one, the inserts' ranges are the
+    // deletes' and everything is bucketed in one run below.
+    const auto need_rehash = [&](uint64_t used) { return (used + nins) * 4 > slots.size() * 3 || max_disp > 48; };
+    const bool rehash_ahead = need_rehash(used_slots - ndel);
     unsigned T2 = 0;
     uint32_t RS = 0, R = 0;
-    // ---- deletes, bucketed by the slot recorded in phase 1 (nothing has moved since)
-    size_t ndel = 0;
-    each([&](Mut& m) { ndel += m.del.size(); });
     ranges(T2, RS, R);
-    if (!ndel) {
-    } else if (!T2) {
-        each([&](Mut& m) {
-            for (const auto& d : m.del) delete_edge_of(d.first);
-        });
-    } else {
-        std::vector<std::vector<uint32_t>> per(2 * T2);
-        std::vector<uint32_t> tail;
-        each([&](Mut& m) {
-            for (const auto& d : m.del) {
-                const uint32_t r = d.second / BUCKET / RS;
-                if (R % 2 && r == R - 1) tail.push_back(d.first);   // (R odd: the last range wraps onto range 0)
-                else per[r].push_back(d.first);
-            }
-        });
+    const unsigned TS = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));   // summary workers
+    // ---- bucketing, each worker over the phase-1 states it owns: deletes
+    // by the slot recorded in phase 1 (nothing has moved since), inserts by
+    // home bucket, summaries by node.  Range tail = the last range when R is
+    // odd (it wraps onto range 0: run serially), or everything without T2.
+    const uint32_t nb = nbuckets(), tail = 2 * T2;
+    const unsigned NB = pool.n;
+    if (edge_bins.size() < NB) edge_bins.resize(NB);
+    auto bin_of = [&](uint32_t bucket) { const uint32_t r = bucket / RS; return (R % 2 && r == R - 1) ? tail : r; };
+    pool.run([&](unsigned t) {
+        EdgeBins& B = edge_bins[t];
+        B.del.resize(tail + 1);
+        B.ins.resize(tail + 1);
+        B.sum.resize(TS);
+        for (auto& v : B.del) v.clear();
+        for (auto& v : B.ins) v.clear();
+        for (auto& v : B.sum) v.clear();
+        for (size_t j = t; j < ms.size(); j += NB) {
+            const Mut& m = *ms[j];
+            for (const auto& d : m.del) B.del[T2 ? bin_of(d.second / BUCKET) : tail].push_back(d);
+            if (!rehash_ahead)
+                for (const auto& e : m.ins) B.ins[T2 ? bin_of(home_bucket(e[0], e[1], nb)) : tail].push_back(e);
+            for (uint32_t c : m.sum) B.sum[mix_word(c) % TS].push_back(c);
+        }
+    });
+    tr_mark("e.bucket");
+    // ---- deletes: even ranges in parallel, then odd ones
+    if (ndel && T2) {
         std::vector<Mut>& X = edge_states(T2);
         std::vector<std::vector<uint32_t>> late(T2);
         for (uint32_t par = 0; par < 2; ++par)
@@ -416,78 +459,102 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
                 if (t >= T2) return;
                 const uint32_t r = 2 * t + par;
                 tl_mut = &X[t];
-                const std::vector<uint32_t>& v = per[r];
-                for (size_t q = 0; q < v.size(); ++q) {
-                    prefetch_edge_of(v, q);
-                    const uint32_t c = v[q];
-                    // an odd range's slot may have been pulled back into the even range before it
-                    if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
-                    delete_edge_of(c);
+                for (unsigned w = 0; w < NB; ++w) {
+                    const auto& v = edge_bins[w].del[r];
+                    for (size_t q = 0; q < v.size(); ++q) {
+                        if (q + 16 < v.size()) {   // the record 16 ahead, the slot (as recorded) 8 ahead
+                            __builtin_prefetch(&nd[v[q + 16].first]);
+                            __builtin_prefetch(&n_lext[v[q + 16].first]);
+                        }
+                        if (q + 8 < v.size() && v[q + 8].second < slots.size()) __builtin_prefetch(&slots[v[q + 8].second], 1);
+                        const uint32_t c = v[q].first;
+                        // an odd range's slot may have been pulled back into the even range before it
+                        if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
+                        delete_edge_of(c);
+                    }
                 }
                 tl_mut = nullptr;
             });
+        tr_mark("e.druns");
         merge_edges(X);
-        for (auto& l : late) tail.insert(tail.end(), l.begin(), l.end());
-        for (uint32_t c : tail) delete_edge_of(c);   // serially, global counters
+        for (auto& l : late)
+            for (uint32_t c : l) delete_edge_of(c);   // serially, global counters
     }
-    // ---- inserts: room first (the serial insert_edge's rehash rule, for the whole batch)
+    for (unsigned w = 0; w < NB && ndel; ++w)
+        for (const auto& d : edge_bins[w].del[tail]) delete_edge_of(d.first);
+    tr_mark("e.dtail");
+    // ---- inserts: room first, then by range as the deletes
     const auto e1 = now();
-    size_t nins = 0;
-    each([&](Mut& m) { nins += m.ins.size(); });
     bool rehashed = false;
-    if ((used_slots + nins) * 4 > slots.size() * 3 || max_disp > 48) {
+    if (need_rehash(used_slots)) {
         rehash(std::max<size_t>((size_t)((live_edges + nins) / 0.55), slots.size() * (max_disp > 48 ? 2 : 1)));
         rehashed = true;
     }
     const auto e2 = now();
-    ranges(T2, RS, R);
-    if (!nins) {
-    } else if (!T2) {
-        each([&](Mut& m) {
-            for (const auto& e : m.ins) insert_edge(e[0], e[1], e[2]);
-        });
-    } else {
-        std::vector<std::vector<std::array<uint32_t, 3>>> per(2 * T2);
-        std::vector<std::array<uint32_t, 3>> tail;
-        const uint32_t nb = nbuckets();
-        each([&](Mut& m) {
-            for (const auto& e : m.ins) {
-                const uint32_t r = home_bucket(e[0], e[1], nb) / RS;
-                if (R % 2 && r == R - 1) tail.push_back(e);
-                else per[r].push_back(e);
+    if (rehashed || rehash_ahead) {   // (rare) inserts bucketed for the table as it is now, by one worker
+        ranges(T2, RS, R);
+        const uint32_t nb2 = nbuckets(), tail2 = 2 * T2;
+        for (unsigned w = 0; w < NB; ++w)
+            for (auto& v : edge_bins[w].ins) v.clear();
+        EdgeBins& B = edge_bins[0];
+        B.ins.resize(tail2 + 1);
+        for (const Mut* m : ms)
+            for (const auto& e : m->ins) {
+                const uint32_t r = T2 ? home_bucket(e[0], e[1], nb2) / RS : tail2;
+                B.ins[T2 && R % 2 && r == R - 1 ? tail2 : r].push_back(e);
             }
-        });
+    }
+    const uint32_t itail = 2 * T2;
+    if (nins && T2) {
+        const uint32_t nbi = nbuckets();
         std::vector<Mut>& X = edge_states(T2);
         for (uint32_t par = 0; par < 2; ++par)
             pool.run([&](unsigned t) {
                 if (t >= T2) return;
+                const uint32_t r = 2 * t + par;
                 tl_mut = &X[t];
-                const auto& v = per[2 * t + par];
-                for (size_t q = 0; q < v.size(); ++q) {
-                    if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
-                        __builtin_prefetch(&slots[(size_t)home_bucket(v[q + 8][0], v[q + 8][1], nb) * BUCKET], 1);
-                        __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                for (unsigned w = 0; w < NB; ++w) {
+                    if (r >= edge_bins[w].ins.size()) continue;
+                    const auto& v = edge_bins[w].ins[r];
+                    for (size_t q = 0; q < v.size(); ++q) {
+                        if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
+                            __builtin_prefetch(&slots[(size_t)home_bucket(v[q + 8][0], v[q + 8][1], nbi) * BUCKET], 1);
+                            __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                        }
+                        insert_edge(v[q][0], v[q][1], v[q][2]);
                     }
-                    insert_edge(v[q][0], v[q][1], v[q][2]);
                 }
                 tl_mut = nullptr;
             });
+        tr_mark("e.iruns");
         merge_edges(X);
-        for (const auto& e : tail) insert_edge(e[0], e[1], e[2]);
     }
+    for (unsigned w = 0; w < NB && nins; ++w)
+        if (itail < edge_bins[w].ins.size())
+            for (const auto& e : edge_bins[w].ins[itail]) insert_edge(e[0], e[1], e[2]);
     if (max_disp > 48) rehash(std::max<size_t>((size_t)(live_edges / 0.55), slots.size() * 2));
+    tr_mark("e.itail");
     const auto e3 = now();
     // ---- summaries of the nodes whose record changed: by node (a node's
     // records are rewritten by one worker; dirty marks set atomically)
-    const unsigned TS = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));
-    std::vector<std::vector<uint32_t>> per(TS);
-    each([&](Mut& m) {
-        for (uint32_t c : m.sum) per[mix_word(c) % TS].push_back(c);
-    });
-    std::vector<Mut>& X = edge_states(TS);
+    const unsigned TS2 = (unsigned)std::min<size_t>(T, std::max<size_t>(1, slots.size() / 4096));
+    if (TS2 != TS) {   // (the table grew: rebucketed by one worker)
+        std::vector<uint32_t> all;
+        for (unsigned w = 0; w < NB; ++w)
+            for (auto& v : edge_bins[w].sum) {
+                all.insert(all.end(), v.begin(), v.end());
+                v.clear();
+            }
+        edge_bins[0].sum.assign(TS2, {});
+        for (uint32_t c : all) edge_bins[0].sum[mix_word(c) % TS2].push_back(c);
+    }
+    std::vector<Mut>& X = edge_states(TS2);
     pool.run([&](unsigned t) {
-        if (t >= TS) return;
-        std::vector<uint32_t>& v = per[t];
+        if (t >= TS2) return;
+        std::vector<uint32_t>& v = X[t].sum;   // (a fresh state's list: scratch)
+        v.clear();
+        for (unsigned w = 0; w < NB; ++w)
+            if (t < edge_bins[w].sum.size()) v.insert(v.end(), edge_bins[w].sum[t].begin(), edge_bins[w].sum[t].end());
         std::sort(v.begin(), v.end());
         v.erase(std::unique(v.begin(), v.end()), v.end());
         for (size_t q = 0; q < v.size(); ++q) {
@@ -496,11 +563,14 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
             if (!nd[c].live || nd[c].inslot == NONE) continue;
             write_summary_at(c, X[t].dirty);
         }
+        v.clear();
     });
+    tr_mark("e.srun");
     merge_edges(X);
+    tr_mark("e.smerge");
     if (trace)
         fprintf(stderr, "[par edges T2=%u nb=%u] del %.2f rehash %d %.2f ins %.2f sum %.2f ms\n", T2, nbuckets(),
-                ms(e0, e1), (int)rehashed, ms(e1, e2), ms(e2, e3), ms(e3, now()));
+                msd(e0, e1), (int)rehashed, msd(e1, e2), msd(e2, e3), msd(e3, now()));
 }
 
 void tm_engine::write_summary_at(uint32_t c, std::vector<uint32_t>& dl) {
@@ -537,6 +607,7 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
         // new words are interned first, serially (the dictionary is not thread-safe)
         for (uint32_t i = 0; i < n; ++i) {
             PlanEnt& pe = plan[i];
+            if (!pe.unk) continue;
             uint32_t* ids = plan_words[pe.part].data() + pe.woff;
             bool unknown = false;
             for (uint32_t k = pe.depth; k < pe.nw; ++k) unknown |= ids[k] == W_UNKNOWN;
@@ -548,6 +619,7 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
                 if (ids[k] == W_UNKNOWN) ids[k] = dict.intern(ws[k].p, ws[k].n);
         }
     }
+    tr_mark(del ? "d.intern" : "i.intern");
     ensure_pool();
     const auto ts0 = std::chrono::steady_clock::now();
     if (W.size() != T) W.resize(T);   // (each worker resets its own state when phase 1 starts)
@@ -558,33 +630,26 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
     std::vector<std::vector<uint32_t>>& parts = parts_buf;   // (capacity kept across batches)
     parts.resize(P);
     for (auto& v : parts) v.clear();
-    for (uint32_t i = 0; i < n; ++i) {
-        const PlanEnt& pe = plan[i];
-        const uint32_t* w = plan_words[pe.part].data() + pe.woff;
-        const uint32_t key = mix_word(pe.nw ? w[0] : 0) ^ (pe.nw > 1 ? mix_word(w[1] * 0x85EBCA6Bu + 1) : 0u);
-        parts[mix_word(key) % P].push_back(i);
-    }
-    // An insert part far above a worker's share (a hot first-two-words
-    // prefix, e.g. 10% of C5's churn under "+/+") is split by its third
-    // word: its filters then share the depth-2 nodes too, under the same
-    // striped locks and shared made map (parts split_from.. are those).
+    // (the keys come from the plan: filters with the same first two words
+    // -- a new word counting as one word -- land in the same part)
+    for (uint32_t i = 0; i < n; ++i) parts[mix_word(plan[i].pkey) % P].push_back(i);
+    // A part far above a worker's share (a hot first-two-words prefix, e.g.
+    // 10% of C5's churn under "+/+") is split by its third word: its filters
+    // then share the depth-2 nodes too, under the same striped locks (and,
+    // for inserts, the shared made map); parts split_from.. are those.
     const uint32_t split_from = P;
-    if (!del) {
+    {
         const size_t big = std::max<size_t>(64, n / (2 * T));
-        constexpr uint32_t SPLIT = 8;
         for (uint32_t q = 0; q < split_from; ++q) {
             if (parts[q].size() <= big) continue;
             std::vector<uint32_t> whole;
             whole.swap(parts[q]);
             const size_t first = parts.size();
-            parts.resize(first + SPLIT);
-            for (uint32_t i : whole) {
-                const PlanEnt& pe = plan[i];
-                const uint32_t* w = plan_words[pe.part].data() + pe.woff;
-                parts[first + (pe.nw > 2 ? mix_word(w[2] * 0xC2B2AE35u + 7) % SPLIT : 0)].push_back(i);
-            }
+            parts.resize(first + PART_SPLIT);
+            for (uint32_t i : whole) parts[first + plan[i].sub].push_back(i);
         }
     }
+    tr_mark(del ? "d.parts" : "i.parts");
     const uint32_t NP = (uint32_t)parts.size();
     std::vector<uint32_t> porder(NP);
     for (uint32_t q = 0; q < NP; ++q) porder[q] = q;
@@ -600,27 +665,35 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
     size_t fresh = 0;
     const size_t base = nd.size();
     if (!del) {
+        tr_mark("i.sort");
         release_pending_ids();
+        tr_mark("i.release");
         uint64_t total = 0;
         for (uint32_t i = 0; i < n; ++i) total += plan[i].nw - plan[i].depth;
-        const size_t take = std::min<size_t>(total, free_nodes.size());
-        fresh = total - take + (size_t)T * Mut::ID_CHUNK;   // + slack: ids are taken a chunk per worker
+        // (+ slack: ids are taken a chunk per worker)
+        const size_t need = total + (size_t)T * Mut::ID_CHUNK;
+        const size_t take = std::min<size_t>(need, free_nodes.size());
+        fresh = need - take;
         if (base + fresh >= MAX_NODES) return 1;
         // Transactional: every allocation first (a bad_alloc here leaves
         // the engine as it was: the caller may still finish other work on
-        // it), then the commit below, which allocates nothing.
+        // it), then the commit below, which allocates nothing.  (Growth
+        // is geometric: an exact reserve would copy the arrays every batch.)
+        auto grow = [&](auto& v) {
+            if (v.capacity() < base + fresh) v.reserve(std::max(base + fresh, v.capacity() + v.capacity() / 2));
+        };
         ids.reserve(take);
         if (fresh) {
-            nd.reserve(base + fresh);
-            n_flen.reserve(base + fresh);
-            n_lext.reserve(base + fresh);
-            n_foff.reserve(base + fresh);
+            grow(nd);
+            grow(n_flen);
+            grow(n_lext);
+            grow(n_foff);
         }
-        if (!full_f_dirty) dirty_f_mark.reserve(base + fresh);
+        if (!full_f_dirty) grow(dirty_f_mark);
         ids.assign(free_nodes.end() - (long)take, free_nodes.end());
         free_nodes.resize(free_nodes.size() - take);
         if (fresh) {
-            nd.resize(base + fresh);   // dead records until handed out; the unused tail is cut after
+            nd.resize(base + fresh);   // dead records until handed out; the unused ones join the free list after
             n_flen.resize(base + fresh, 0);
             n_lext.resize(base + fresh, 0);
             n_foff.resize(base + fresh, 0);
@@ -628,6 +701,7 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
         if (!full_f_dirty && dirty_f_mark.size() < nd.size()) dirty_f_mark.resize(nd.size(), 0);
     }
     // (shared_made was cleared at the end of the previous batch)
+    tr_mark(del ? "d.alloc" : "i.alloc");
     const auto tp0 = std::chrono::steady_clock::now();
     // phase 1: node records, by first word
     pool.run([&](unsigned t) {
@@ -660,7 +734,7 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
                     const PlanEnt& pe = plan[i];
                     int rc;
                     if (del) {
-                        rc = delete_planned(i);
+                        rc = delete_planned(i, sd);
                     } else {
                         rc = trie_insert_ids(buf + offs[i], offs[i + 1] - offs[i],
                                              plan_words[pe.part].data() + pe.woff, pe.nw, pe.node, pe.depth, sd);
@@ -676,6 +750,7 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
         m.t_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
         tl_mut = nullptr;
     });
+    tr_mark(del ? "d.phase1" : "i.phase1");
     R.del = del;
     R.n = n;
     R.W = &W;
@@ -693,6 +768,10 @@ void tm_engine::par_finish(ParRun* const* runs, size_t nr) {
     for (size_t r = 0; r < nr; ++r) Ws.push_back(runs[r]->W);
     edge_phase(Ws);
     const auto tp2 = std::chrono::steady_clock::now();
+    // the workers' filter bytes and dirty filter ids go to the end of the
+    // engine's arrays: places first, copies in parallel below
+    size_t fb_end = fbytes.size(), df_end = dirty_f.size();
+    std::vector<size_t> df_at;
     for (size_t r = 0; r < nr; ++r) {
         ParRun& R = *runs[r];
         R.tp2 = tp2;
@@ -704,29 +783,40 @@ void tm_engine::par_finish(ParRun* const* runs, size_t nr) {
             version += m.version;
             R.done += m.done;
             if (m.rc && !R.rc) R.rc = m.rc;
-            m.fresh_base = fbytes.size();   // (reused: this worker's bytes start here)
-            fbytes.insert(fbytes.end(), m.fb.begin(), m.fb.end());
-            dirty_f.insert(dirty_f.end(), m.dirty_f.begin(), m.dirty_f.end());
-            for (const auto& q : m.pend) pending_free.push_back(q);
+            m.fresh_base = fb_end;   // (reused: this worker's bytes start here)
+            fb_end += m.fb.size();
+            df_at.push_back(df_end);
+            df_end += m.dirty_f.size();
+            pend_ids(launch_seq, m.pend.data(), m.pend.size());
         }
     }
-    pool.run([&](unsigned t) {   // filter byte offsets: distinct nodes per worker
+    fbytes.resize(fb_end);
+    dirty_f.resize(df_end);
+    tr_mark("f.merge");
+    pool.run([&](unsigned t) {   // bytes, dirty ids and filter byte offsets: distinct nodes per worker
+        size_t k = 0;
         for (size_t r = 0; r < nr; ++r) {
             const std::vector<Mut>& W = *runs[r]->W;
-            for (size_t j = t; j < W.size(); j += pool.n)
-                for (const auto& f : W[j].foff) n_foff[f.first] = W[j].fresh_base + f.second;
+            for (size_t j = 0; j < W.size(); ++j, ++k) {
+                if (j % pool.n != t) continue;
+                const Mut& m = W[j];
+                if (!m.fb.empty()) memcpy(fbytes.data() + m.fresh_base, m.fb.data(), m.fb.size());
+                if (!m.dirty_f.empty()) memcpy(dirty_f.data() + df_at[k], m.dirty_f.data(), m.dirty_f.size() * sizeof(uint32_t));
+                for (const auto& f : m.foff) n_foff[f.first] = m.fresh_base + f.second;
+            }
         }
         for (unsigned j = t; j < 64; j += pool.n) shared_made[j].clear();   // for the next batch
     });
+    tr_mark("f.foff");
     for (size_t r = 0; r < nr; ++r) {
         ParRun& R = *runs[r];
         if (R.del) continue;
         std::vector<Mut>& W = *R.W;
         const std::vector<uint32_t>& ids = R.ids;
         const size_t fresh = R.fresh, base = R.base;
-        // ids not handed out: free ones back to the list, the fresh tail cut off
-        // (the rest of each worker's last chunk: free-list ids go back; fresh
-        // ids below the highest one handed out stay as free dead records)
+        // ids not handed out go (back) to the free list: the rest of each
+        // worker's last chunk, the free-list ids past the highest one handed
+        // out, and the fresh records past it
         size_t used = 0;
         for (const Mut& m : W) used = std::max(used, m.id_lo);   // highest id index handed out + 1
         const size_t avail = ids.size() + fresh;
@@ -735,15 +825,12 @@ void tm_engine::par_finish(ParRun* const* runs, size_t nr) {
             for (size_t k = m.id_lo; k < std::min(m.id_hi, used); ++k)
                 free_nodes.push_back(k < ids.size() ? ids[k] : (uint32_t)(base + (k - ids.size())));
         for (size_t k = used; k < ids.size(); ++k) free_nodes.push_back(ids[k]);
+        // fresh records not handed out stay, as free dead records (cutting
+        // them re-initialised the arrays' tails every batch)
         const size_t fresh_used = used > ids.size() ? used - ids.size() : 0;
-        if (fresh_used < fresh) {
-            nd.resize(base + fresh_used);
-            n_flen.resize(base + fresh_used);
-            n_lext.resize(base + fresh_used);
-            n_foff.resize(base + fresh_used);
-            if (dirty_f_mark.size() > nd.size()) dirty_f_mark.resize(nd.size());
-        }
+        for (size_t k = fresh; k-- > fresh_used;) free_nodes.push_back((uint32_t)(base + k));
     }
+    tr_mark("f.ids");
     if (kn.par_trace) {
         const auto tp3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

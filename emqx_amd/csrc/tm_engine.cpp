@@ -864,7 +864,9 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
     int rc = TM_OK;
     try {
         const auto tq0 = std::chrono::steady_clock::now();
+        e->tr_mark(nullptr);
         e->make_plan_pair(del_filters, del_offsets, n_del, ins_filters, ins_offsets, n_ins);
+        e->tr_mark("plan");
         if (trace)
             fprintf(stderr, "[plan apply del=%u ins=%u] %.2f ms\n", n_del, n_ins,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
@@ -904,7 +906,9 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
         int irc = TM_OK;
         try {
             e->plan.erase(e->plan.begin(), e->plan.begin() + n_del);
+            e->tr_mark("erase");
             const uint32_t again = e->replan_dead_inserts(n_ins);
+            e->tr_mark("replan");
             if (trace)
                 fprintf(stderr, "[apply: %u of %u inserts walked again after the deletes] %.2f ms in the call\n", again,
                         n_ins, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
@@ -924,9 +928,15 @@ int tm_trie_apply_many(tm_engine* e, const uint8_t* del_filters, const uint64_t*
                 e->par_finish(runs, 2);
                 if (n_deleted) *n_deleted = RD.done;
                 if (n_inserted) *n_inserted = RI.done;
-                if (trace)
+                if (trace) {
                     fprintf(stderr, "[apply_many del=%u ins=%u, one edge phase] %.2f ms in the call\n", n_del, n_ins,
                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+                    fprintf(stderr, "[pool] %llu runs, %.0f us in them, %.0f us of it before the last worker started\n",
+                            (unsigned long long)e->pool.t_runs, e->pool.t_wall_us, e->pool.t_lag_us);
+                    e->pool.t_runs = 0;
+                    e->pool.t_wall_us = e->pool.t_lag_us = 0;
+                    e->tr_print();
+                }
                 return RD.rc ? RD.rc : RI.rc;
             }
             tm_engine::ParRun* runs[1] = {&RD};   // the inserts run serially: the deletes end first

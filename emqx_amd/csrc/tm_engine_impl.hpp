@@ -900,6 +900,11 @@ struct WorkPool {
     static constexpr int64_t PHASE_GAP_NS = 300000;
     std::atomic<int64_t> linger_until{0};   // steady-clock ns
     std::atomic<int> lingering{0};          // mutations in progress (Linger scopes)
+    // TM_PAR_TRACE: per run, how late the last worker started its share
+    bool trace = false;
+    std::atomic<int64_t> last_start{0};
+    uint64_t t_runs = 0;
+    double t_wall_us = 0, t_lag_us = 0;
     static int64_t now_ns() {
         return std::chrono::duration_cast<std::chrono::nanoseconds>(
                    std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -942,6 +947,12 @@ struct WorkPool {
                 if (!spin_until_changed(gen, seen)) futex(&gen, FUTEX_WAIT, seen);
             if (stop.load(std::memory_order_acquire)) return;
             seen = gen.load(std::memory_order_acquire);
+            if (trace) {
+                const int64_t t = now_ns();
+                for (int64_t o = last_start.load(std::memory_order_relaxed);
+                     o < t && !last_start.compare_exchange_weak(o, t, std::memory_order_relaxed);) {
+                }
+            }
             (*job)(i);
             if (busy.fetch_sub(1, std::memory_order_acq_rel) == 1) futex(&busy, FUTEX_WAKE, 1);
         }
@@ -949,6 +960,8 @@ struct WorkPool {
     void run(const std::function<void(unsigned)>& f) {
         if (n <= 1) { f(0); return; }
         refresh_linger();
+        const int64_t t0 = trace ? now_ns() : 0;
+        if (trace) last_start.store(t0, std::memory_order_relaxed);
         job = &f;
         busy.store(n - 1, std::memory_order_release);
         gen.fetch_add(1, std::memory_order_acq_rel);
@@ -957,6 +970,11 @@ struct WorkPool {
         for (uint32_t b; (b = busy.load(std::memory_order_acquire)) != 0;)
             if (!spin_until_changed(busy, b)) futex(&busy, FUTEX_WAIT, b);
         refresh_linger();
+        if (trace) {
+            ++t_runs;
+            t_wall_us += 1e-3 * (double)(now_ns() - t0);
+            t_lag_us += 1e-3 * (double)(last_start.load(std::memory_order_relaxed) - t0);
+        }
     }
     ~WorkPool() {
         stop.store(true, std::memory_order_release);
@@ -1012,7 +1030,7 @@ struct alignas(64) Mut {   // (one cache line boundary per worker: no false shar
     std::vector<uint8_t> fb;                            // filter bytes appended
     std::vector<std::pair<uint32_t, uint64_t>> foff;    // (node, offset into fb)
     std::vector<uint32_t> dirty, dirty_f;
-    std::vector<std::pair<uint64_t, uint32_t>> pend;    // freed ids (pending_free)
+    std::vector<uint32_t> pend;                         // freed ids (pending_free, at the call's launch_seq)
     int64_t live_nodes = 0, n_filters = 0, live_edges = 0, used_slots = 0, route_entries = 0;
     uint32_t max_disp = 0;
     uint64_t version = 0, done = 0;
@@ -1114,7 +1132,20 @@ struct tm_engine {
     // recycled id would name another filter.  Batches hold their launch
     // sequence number from launch until re-launch or free; an id freed at
     // sequence L returns to free_nodes once every live batch is newer than L.
-    std::deque<std::pair<uint64_t, uint32_t>> pending_free;
+    // (blocks of ids freed at one sequence number, oldest first)
+    struct PendBlock {
+        uint64_t seq;
+        std::vector<uint32_t> ids;
+    };
+    std::deque<PendBlock> pending_free;
+    size_t pending_n = 0;   // ids in pending_free
+    void pend_ids(uint64_t seq, const uint32_t* ids, size_t k) {
+        if (!k) return;
+        if (pending_free.empty() || pending_free.back().seq != seq) pending_free.push_back({seq, {}});
+        std::vector<uint32_t>& v = pending_free.back().ids;
+        v.insert(v.end(), ids, ids + k);
+        pending_n += k;
+    }
     std::multiset<uint64_t> live_launches;
     uint64_t launch_seq = 0;
     uint64_t live_nodes = 0, live_edges = 0, n_filters = 0;
@@ -1373,8 +1404,10 @@ struct tm_engine {
 
     void release_pending_ids() {
         const uint64_t watermark = live_launches.empty() ? ~0ull : *live_launches.begin();
-        while (!pending_free.empty() && pending_free.front().first < watermark) {
-            free_nodes.push_back(pending_free.front().second);
+        while (!pending_free.empty() && pending_free.front().seq < watermark) {
+            const std::vector<uint32_t>& v = pending_free.front().ids;
+            free_nodes.insert(free_nodes.end(), v.begin(), v.end());
+            pending_n -= v.size();
             pending_free.pop_front();
         }
     }
@@ -1460,10 +1493,10 @@ struct tm_engine {
         for (uint8_t& k : nd[id].lcnt) k = 0;
         if (M) {
             --M->live_nodes;
-            if (id != ROOT) M->pend.emplace_back(launch_seq, id);
+            if (id != ROOT) M->pend.push_back(id);
         } else {
             --live_nodes;
-            if (id != ROOT) pending_free.emplace_back(launch_seq, id);
+            if (id != ROOT) pend_ids(launch_seq, &id, 1);
         }
     }
 
@@ -1607,7 +1640,8 @@ struct tm_engine {
     int trie_delete(const uint8_t* t, size_t len);
 
     // delete/1 of the filter whose words are ids and whose node is n
-    int trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids);
+    // (sd: as for trie_insert_ids, the shared depth of a parallel batch)
+    int trie_delete_at(uint32_t n, const uint32_t* ids_p, uint32_t nids, uint32_t sd = 2);
 
     // ------------------------------------------------------------ bulk plan
     // Bulk mutations (tm_trie_insert_many / delete_many: subscribe churn, C5)
@@ -1636,6 +1670,11 @@ struct tm_engine {
         uint32_t depth;   // levels walked (insert)
         uint32_t woff, nw;
         uint32_t part;    // worker whose word vector holds the ids
+        // (for the parallel pass, from the plan's ids -- W_UNKNOWN for a new
+        // word, so filters with equal leading words still get equal values)
+        uint32_t pkey;    // the first two words' part key
+        uint8_t sub;      // the third word's sub-part (a split hot part)
+        uint8_t unk;      // a word is not in the dictionary yet
     };
     std::vector<PlanEnt> plan;
     std::vector<std::vector<uint32_t>> plan_words;
@@ -1667,7 +1706,8 @@ struct tm_engine {
     // (The walks go PLAN_G at a time, level by level with every next bucket
     // prefetched, as in plan_range.)
     uint32_t replan_dead_inserts(uint32_t n);
-    std::vector<uint32_t> replan_buf;
+    void replan_range(uint32_t lo, uint32_t hi, std::vector<uint32_t>& redo);
+    std::vector<std::vector<uint32_t>> replan_buf;   // per worker
 
     // the serial passes prefetch what filter i + PF_FAR / i + PF_NEAR will
     // touch: their node records first, then the lines those records point at
@@ -1677,10 +1717,17 @@ struct tm_engine {
 
     int insert_planned(const uint8_t* buf, const uint64_t* offs, uint32_t i);
 
-    int delete_planned(uint32_t i) {
+    int delete_planned(uint32_t i, uint32_t sd = 2) {
         const PlanEnt& pe = plan[i];
-        if (pe.node == NONE || !nd[pe.node].live) return TM_OK;   // absent, or removed earlier in the batch
-        return trie_delete_at(pe.node, plan_words[pe.part].data() + pe.woff, pe.nw);
+        if (pe.node == NONE) return TM_OK;   // absent
+        // (removed earlier in the batch: dead.  In a split part the record
+        // may be a shared depth-2 node another worker is changing: read
+        // `live` under its stripe lock)
+        std::unique_lock<std::recursive_mutex> l;
+        if (tl_mut && pe.nw < sd) l = std::unique_lock<std::recursive_mutex>(shared_mu(pe.node));
+        if (!nd[pe.node].live) return TM_OK;
+        l = {};
+        return trie_delete_at(pe.node, plan_words[pe.part].data() + pe.woff, pe.nw, sd);
     }
 
     // ------------------------------------------------------------ parallel batches
@@ -1702,6 +1749,7 @@ struct tm_engine {
     // Filter / node ids therefore differ from a serial run's (ids are the
     // engine's own), the trie and its HBM image are the same.
     static constexpr uint32_t PAR_MIN = 2048;
+    static constexpr uint32_t PART_SPLIT = 8;          // sub-parts of a hot part (by third word)
     static constexpr uint32_t PAR_RANGE_MIN = 4096;    // buckets per phase-2 range at least (>> max_disp)
 
     static uint32_t mix_word(uint32_t w) {
@@ -1732,6 +1780,34 @@ struct tm_engine {
     // write_summary for a parallel pass: the dirty mark set atomically (another
     // worker may mark a slot of the same 64-slot word)
     void write_summary_at(uint32_t c, std::vector<uint32_t>& dl);
+
+    // TM_PAR_TRACE: the named stretches of a bulk call, in order (us since
+    // the previous mark), printed at its end
+    std::vector<std::pair<const char*, double>> tr_spans;
+    std::chrono::steady_clock::time_point tr_last;
+    void tr_mark(const char* what) {
+        if (!kn.par_trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        if (what) tr_spans.emplace_back(what, std::chrono::duration<double, std::micro>(t - tr_last).count());
+        tr_last = t;
+    }
+    void tr_print() {
+        if (!kn.par_trace) return;
+        fprintf(stderr, "[spans us]");
+        for (const auto& s : tr_spans) fprintf(stderr, " %s %.0f", s.first, s.second);
+        fprintf(stderr, "\n");
+        tr_spans.clear();
+    }
+    // The edge phase's work lists, bucketed by one worker each from the
+    // phase-1 states it owns (capacity kept across batches): deletes and
+    // inserts per bucket range (+ the wrapping tail range), summaries per
+    // summary worker.
+    struct EdgeBins {
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> del;   // (child, its slot)
+        std::vector<std::vector<std::array<uint32_t, 3>>> ins;
+        std::vector<std::vector<uint32_t>> sum;
+    };
+    std::vector<EdgeBins> edge_bins;
 
     // One parallel mutation in flight between par_begin and par_finish: its
     // workers' states and the id bookkeeping of an insert.

@@ -217,13 +217,17 @@ int tm_engine::upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn,
     };
     // filter bytes (slow-path sort): arena + per-node (off, len)
     bool f_full = full_f_dirty;
+    // (grown 2x: churn appends to these every step, and a new buffer
+    // costs a full copy, a host wait for the batches reading the old one
+    // and a new capture of every batch's launch graph -- its address is an
+    // argument)
     if (R.c_foff < nn || R.c_flen < nn) {
-        if ((rc = dev_reserve(R.d_foff, R.c_foff, nn))) return rc;
-        if ((rc = dev_reserve(R.d_flen, R.c_flen, nn))) return rc;
+        if ((rc = dev_reserve(R.d_foff, R.c_foff, 2 * nn))) return rc;
+        if ((rc = dev_reserve(R.d_flen, R.c_flen, 2 * nn))) return rc;
         f_full = true;
     }
     if (R.c_fbytes < fbytes.size() + 1) {
-        if ((rc = dev_reserve(R.d_fbytes, R.c_fbytes, fbytes.size() + 1))) return rc;
+        if ((rc = dev_reserve(R.d_fbytes, R.c_fbytes, 2 * (fbytes.size() + 1)))) return rc;
         R.fbytes_uploaded = 0;
     }
     if (fbytes.size() > R.fbytes_uploaded) {

@@ -228,8 +228,41 @@ def test_parallel_insert_splits_a_hot_two_word_prefix():
     B.debug_check()
     for f in adds[::5] + [b"hp/hq", b"hp/hq/7", b"+/+/w3"]:
         assert A.lookup(f) == B.lookup(f), f
+    # the deletes split the same way (depth-2 records shared under the
+    # stripe locks): half, then the rest, which empties the hot prefix's
+    # depth-2 node from several workers at once
+    for part in (adds[::2], adds[1::2]):
+        for e in (A, B):
+            e.delete_many(gen.Strings.from_list(part))
+        a, b = A.stats(), B.stats()
+        assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+        B.debug_check()
+    for f in [b"hp/hq", b"hp/hq/7", b"+/+/w3"] + adds[1::97]:
+        assert A.lookup(f) == B.lookup(f) is None, f
+
+
+def test_parallel_inserts_that_grow_the_edge_hash():
+    """Parallel insert batches of ~20% of the trie each: the edge phase finds
+    the table too full for a batch's inserts, re-packs it after the deletes
+    and buckets the inserts for the new table.  Each batch must leave the
+    serial pass's trie (same counts, consistent hash, same lookups)."""
+    p = gen.SkewParams(seed=24, n_hot=600, k_per_hot=40)
+    allf, _, _, _ = workload(p, 12_000, 100, seed=24, background_pool=500)
+    A = Engine(device=-1, host_threads=1)
+    B = Engine(device=-1, host_threads=8)
     for e in (A, B):
-        e.delete_many(gen.Strings.from_list(adds[::2]))
-    a, b = A.stats(), B.stats()
-    assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
-    B.debug_check()
+        e.insert_many(allf)
+    grew = 0
+    for step in range(8):
+        n = max(2048, B.stats()["filters"] // 5)
+        adds = [b"g%d/%d/x%d/+/y" % (step, i % 97, i) for i in range(n)]
+        s0 = B.stats()["slots"]
+        for e in (A, B):
+            e.insert_many(gen.Strings.from_list(adds))
+        grew += B.stats()["slots"] > s0
+        a, b = A.stats(), B.stats()
+        assert all(a[k] == b[k] for k in ("nodes", "edges", "filters", "words")), (a, b)
+        B.debug_check()
+        for f in adds[::41]:
+            assert A.lookup(f) == B.lookup(f) is not None, f
+    assert grew >= 1

@@ -26,6 +26,15 @@ deltas = []
 for _ in range(steps):
     dels, adds = churn.step(10_000)
     deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
+def throttled():
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f)}
+    except OSError:
+        return {}
+
+
+th0 = throttled()
 for d, a in deltas:
     t = time.perf_counter()
     if mode == "apply":
@@ -40,3 +49,5 @@ for d, a in deltas:
         eng.sync()   # the delta upload, as the next launch would do it
     t3 = time.perf_counter()
     print(f"K={K} {mode} sync {1e3 * (t3 - t2):.2f} ms del {1e3 * (t1 - t):.2f} ms  ins {1e3 * (t2 - t1):.2f} ms  total {1e3 * (t2 - t):.2f}", flush=True)
+th1 = throttled()
+print("cgroup cpu.stat deltas:", {k: th1[k] - th0.get(k, 0) for k in th1}, flush=True)
