@@ -380,7 +380,10 @@ void tm_engine::prefetch_edge_of(const std::vector<uint32_t>& v, size_t q) const
     }
     if (q + 8 < v.size()) {
         const uint32_t s = nd[v[q + 8]].inslot;
-        if (s != NONE && s < slots.size()) __builtin_prefetch(&slots[s], 1);
+        if (s != NONE && s < slots.size()) {
+            __builtin_prefetch(&slots[s], 1);
+            if ((s >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[s >> 6], 1);
+        }
     }
 }
 
@@ -466,7 +469,10 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
                             __builtin_prefetch(&nd[v[q + 16].first]);
                             __builtin_prefetch(&n_lext[v[q + 16].first]);
                         }
-                        if (q + 8 < v.size() && v[q + 8].second < slots.size()) __builtin_prefetch(&slots[v[q + 8].second], 1);
+                        if (q + 8 < v.size() && v[q + 8].second < slots.size()) {   // (and its dirty-mark word)
+                            __builtin_prefetch(&slots[v[q + 8].second], 1);
+                            if ((v[q + 8].second >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[v[q + 8].second >> 6], 1);
+                        }
                         const uint32_t c = v[q].first;
                         // an odd range's slot may have been pulled back into the even range before it
                         if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
@@ -518,8 +524,11 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
                     const auto& v = edge_bins[w].ins[r];
                     for (size_t q = 0; q < v.size(); ++q) {
                         if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
-                            __builtin_prefetch(&slots[(size_t)home_bucket(v[q + 8][0], v[q + 8][1], nbi) * BUCKET], 1);
+                            const size_t hs = (size_t)home_bucket(v[q + 8][0], v[q + 8][1], nbi) * BUCKET;
+                            __builtin_prefetch(&slots[hs], 1);
+                            if ((hs >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[hs >> 6], 1);
                             __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                            __builtin_prefetch(&n_lext[v[q + 8][2]]);   // (its summary is written)
                         }
                         insert_edge(v[q][0], v[q][1], v[q][2]);
                     }
@@ -724,12 +733,22 @@ int tm_engine::par_begin(bool del, const uint8_t* buf, const uint64_t* offs, uin
                 for (size_t q = 0; q < ni; ++q) {
                     if ((q & 63) == 63 && failed.load(std::memory_order_relaxed)) break;
                     const uint32_t i = items[q];
-                    if (q + 8 < ni) {   // the record the walk starts from, a few filters ahead
-                        const uint32_t f = plan[items[q + 8]].node;
-                        if (f != NONE) {
-                            __builtin_prefetch(&nd[f]);
-                            __builtin_prefetch(&n_lext[f]);   // (a new literal child sets a bit there)
+                    // a few filters ahead: their plan entries and byte offsets
+                    // first (written by other workers' plans: other cores'
+                    // caches), then from those the record the walk starts
+                    // from, the filter's word ids and its bytes
+                    if (q + 16 < ni) {
+                        __builtin_prefetch(&plan[items[q + 16]]);
+                        if (!del) __builtin_prefetch(&offs[items[q + 16]]);
+                    }
+                    if (q + 8 < ni) {
+                        const PlanEnt& pf = plan[items[q + 8]];
+                        if (pf.node != NONE) {
+                            __builtin_prefetch(&nd[pf.node]);
+                            __builtin_prefetch(&n_lext[pf.node]);   // (a new literal child sets a bit there)
                         }
+                        __builtin_prefetch(plan_words[pf.part].data() + pf.woff + (del ? 0 : pf.depth));
+                        if (!del) __builtin_prefetch(buf + offs[items[q + 8]]);
                     }
                     const PlanEnt& pe = plan[i];
                     int rc;
