@@ -231,13 +231,16 @@ void tm_engine::plan_range(const uint8_t* buf, const uint64_t* offs, uint32_t lo
 
 void tm_engine::make_plan(const uint8_t* buf, const uint64_t* offs, uint32_t n, bool del) {
     plan.resize(n);
-    const unsigned nt = std::max(1u, std::min<unsigned>(threads, n / 256));
+    // (PLAN_PARTS parts per worker, taken by whichever worker is free: a
+    // worker the box's scheduler preempts holds up a part, not the run)
+    const unsigned nt = std::max(1u, std::min<unsigned>(PLAN_PARTS * threads, n / 256));
     if (plan_words.size() < nt) plan_words.resize(nt);
     if (plan_tw.size() < nt) plan_tw.resize(nt);
     if (nt == 1) { plan_range(buf, offs, 0, n, del, 0); return; }
     ensure_pool();   // the engine's workers (no thread start-up per batch)
-    pool.run([&](unsigned i) {
-        for (unsigned j = i; j < nt; j += pool.n) {
+    std::atomic<unsigned> next{0};
+    pool.run([&](unsigned) {
+        for (unsigned j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nt;) {
             const uint32_t lo = (uint32_t)((uint64_t)n * j / nt), hi = (uint32_t)((uint64_t)n * (j + 1) / nt);
             plan_range(buf, offs, lo, hi, del, j);
         }
@@ -247,7 +250,7 @@ void tm_engine::make_plan(const uint8_t* buf, const uint64_t* offs, uint32_t n, 
 void tm_engine::make_plan_pair(const uint8_t* dbuf, const uint64_t* doffs, uint32_t ndel, const uint8_t* ibuf,
                     const uint64_t* ioffs, uint32_t nins) {
     plan.resize((size_t)ndel + nins);
-    const unsigned nt = std::max(1u, std::min<unsigned>(threads, (ndel + nins) / 256));
+    const unsigned nt = std::max(1u, std::min<unsigned>(PLAN_PARTS * threads, (ndel + nins) / 256));
     if (plan_words.size() < nt) plan_words.resize(nt);
     if (plan_tw.size() < nt) plan_tw.resize(nt);
     auto part = [&](unsigned j) {
@@ -257,8 +260,9 @@ void tm_engine::make_plan_pair(const uint8_t* dbuf, const uint64_t* doffs, uint3
     };
     if (nt == 1) { part(0); return; }
     ensure_pool();
-    pool.run([&](unsigned i) {
-        for (unsigned j = i; j < nt; j += pool.n) part(j);
+    std::atomic<unsigned> next{0};
+    pool.run([&](unsigned) {
+        for (unsigned j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nt;) part(j);
     });
 }
 
@@ -402,9 +406,11 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
             m.live_edges = m.used_slots = 0; m.max_disp = 0; m.dirty.clear();
         }
     };
+    // T2 range pairs (EDGE_PAIRS per worker, each pass's ranges taken by
+    // whichever worker is free)
     auto ranges = [&](unsigned& T2, uint32_t& RS, uint32_t& R) {
         const uint32_t nb = nbuckets();
-        T2 = std::min<unsigned>(T, nb / (2 * PAR_RANGE_MIN));
+        T2 = std::min<unsigned>(EDGE_PAIRS * T, nb / (2 * PAR_RANGE_MIN));
         if (T2 < 2) { T2 = 0; return; }
         RS = ((nb + 2 * T2 - 1) / (2 * T2) + 15) / 16 * 16;   // whole 16-bucket groups: dirty-mark words stay per range
         R = (nb + RS - 1) / RS;
@@ -455,32 +461,35 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
     tr_mark("e.bucket");
     // ---- deletes: even ranges in parallel, then odd ones
     if (ndel && T2) {
-        std::vector<Mut>& X = edge_states(T2);
-        std::vector<std::vector<uint32_t>> late(T2);
-        for (uint32_t par = 0; par < 2; ++par)
+        std::vector<Mut>& X = edge_states(NB);
+        std::vector<std::vector<uint32_t>> late(NB);
+        for (uint32_t par = 0; par < 2; ++par) {
+            std::atomic<unsigned> next{0};
             pool.run([&](unsigned t) {
-                if (t >= T2) return;
-                const uint32_t r = 2 * t + par;
                 tl_mut = &X[t];
-                for (unsigned w = 0; w < NB; ++w) {
-                    const auto& v = edge_bins[w].del[r];
-                    for (size_t q = 0; q < v.size(); ++q) {
-                        if (q + 16 < v.size()) {   // the record 16 ahead, the slot (as recorded) 8 ahead
-                            __builtin_prefetch(&nd[v[q + 16].first]);
-                            __builtin_prefetch(&n_lext[v[q + 16].first]);
+                for (unsigned pr; (pr = next.fetch_add(1, std::memory_order_relaxed)) < T2;) {
+                    const uint32_t r = 2 * pr + par;
+                    for (unsigned w = 0; w < NB; ++w) {
+                        const auto& v = edge_bins[w].del[r];
+                        for (size_t q = 0; q < v.size(); ++q) {
+                            if (q + 16 < v.size()) {   // the record 16 ahead, the slot (as recorded) 8 ahead
+                                __builtin_prefetch(&nd[v[q + 16].first]);
+                                __builtin_prefetch(&n_lext[v[q + 16].first]);
+                            }
+                            if (q + 8 < v.size() && v[q + 8].second < slots.size()) {   // (and its dirty-mark word)
+                                __builtin_prefetch(&slots[v[q + 8].second], 1);
+                                if ((v[q + 8].second >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[v[q + 8].second >> 6], 1);
+                            }
+                            const uint32_t c = v[q].first;
+                            // an odd range's slot may have been pulled back into the even range before it
+                            if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
+                            delete_edge_of(c);
                         }
-                        if (q + 8 < v.size() && v[q + 8].second < slots.size()) {   // (and its dirty-mark word)
-                            __builtin_prefetch(&slots[v[q + 8].second], 1);
-                            if ((v[q + 8].second >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[v[q + 8].second >> 6], 1);
-                        }
-                        const uint32_t c = v[q].first;
-                        // an odd range's slot may have been pulled back into the even range before it
-                        if (nd[c].inslot / BUCKET / RS != r) { late[t].push_back(c); continue; }
-                        delete_edge_of(c);
                     }
                 }
                 tl_mut = nullptr;
             });
+        }
         tr_mark("e.druns");
         merge_edges(X);
         for (auto& l : late)
@@ -513,28 +522,31 @@ void tm_engine::edge_phase(const std::vector<std::vector<Mut>*>& Ws) {
     const uint32_t itail = 2 * T2;
     if (nins && T2) {
         const uint32_t nbi = nbuckets();
-        std::vector<Mut>& X = edge_states(T2);
-        for (uint32_t par = 0; par < 2; ++par)
+        std::vector<Mut>& X = edge_states(NB);
+        for (uint32_t par = 0; par < 2; ++par) {
+            std::atomic<unsigned> next{0};
             pool.run([&](unsigned t) {
-                if (t >= T2) return;
-                const uint32_t r = 2 * t + par;
                 tl_mut = &X[t];
-                for (unsigned w = 0; w < NB; ++w) {
-                    if (r >= edge_bins[w].ins.size()) continue;
-                    const auto& v = edge_bins[w].ins[r];
-                    for (size_t q = 0; q < v.size(); ++q) {
-                        if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
-                            const size_t hs = (size_t)home_bucket(v[q + 8][0], v[q + 8][1], nbi) * BUCKET;
-                            __builtin_prefetch(&slots[hs], 1);
-                            if ((hs >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[hs >> 6], 1);
-                            __builtin_prefetch(&nd[v[q + 8][2]], 1);
-                            __builtin_prefetch(&n_lext[v[q + 8][2]]);   // (its summary is written)
+                for (unsigned pr; (pr = next.fetch_add(1, std::memory_order_relaxed)) < T2;) {
+                    const uint32_t r = 2 * pr + par;
+                    for (unsigned w = 0; w < NB; ++w) {
+                        if (r >= edge_bins[w].ins.size()) continue;
+                        const auto& v = edge_bins[w].ins[r];
+                        for (size_t q = 0; q < v.size(); ++q) {
+                            if (q + 8 < v.size()) {   // the home bucket and the child's record, a few edges ahead
+                                const size_t hs = (size_t)home_bucket(v[q + 8][0], v[q + 8][1], nbi) * BUCKET;
+                                __builtin_prefetch(&slots[hs], 1);
+                                if ((hs >> 6) < dirty_mark.size()) __builtin_prefetch(&dirty_mark[hs >> 6], 1);
+                                __builtin_prefetch(&nd[v[q + 8][2]], 1);
+                                __builtin_prefetch(&n_lext[v[q + 8][2]]);   // (its summary is written)
+                            }
+                            insert_edge(v[q][0], v[q][1], v[q][2]);
                         }
-                        insert_edge(v[q][0], v[q][1], v[q][2]);
                     }
                 }
                 tl_mut = nullptr;
             });
+        }
         tr_mark("e.iruns");
         merge_edges(X);
     }

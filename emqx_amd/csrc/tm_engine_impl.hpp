@@ -1149,7 +1149,7 @@ struct tm_engine {
     std::multiset<uint64_t> live_launches;
     uint64_t launch_seq = 0;
     uint64_t live_nodes = 0, live_edges = 0, n_filters = 0;
-    std::vector<uint8_t> fbytes;
+    std::vector<uint8_t, HugeAlloc<uint8_t>> fbytes;   // (2-MB pages: a growth step faults ~512x fewer pages)
 
     // edge hash (host mirror of the HBM replica)
     std::vector<Slot, HugeAlloc<Slot>> slots;
@@ -1750,6 +1750,11 @@ struct tm_engine {
     // engine's own), the trie and its HBM image are the same.
     static constexpr uint32_t PAR_MIN = 2048;
     static constexpr uint32_t PART_SPLIT = 8;          // sub-parts of a hot part (by third word)
+    // plan parts / edge-phase range pairs per worker, taken by whichever
+    // worker is free.  (4 of each measured slower on the box: shorter
+    // prefetch runs and plan groups; profiles/r06/s3/ab_parts.txt)
+    static constexpr uint32_t PLAN_PARTS = 1;
+    static constexpr uint32_t EDGE_PAIRS = 1;
     static constexpr uint32_t PAR_RANGE_MIN = 4096;    // buckets per phase-2 range at least (>> max_disp)
 
     static uint32_t mix_word(uint32_t w) {
