@@ -1447,8 +1447,12 @@ def main():
         # config C5 in the driver's line: K = 100, 10 and 1000 filters per hot
         # topic, 10k subscribe/unsubscribe deltas per step; each leg checks
         # its last step's batch against the oracle on that step's snapshot
-        # 10 steps: the last step's walk is the one not hidden behind a churn
-        out["c5"] = {f"k{k}": c5_leg(k, 10, 10_000, args.topics, device=local) for k in (100, 10, 1000)}
+        # 30 steps: the timed region holds the first delta's churn (nothing
+        # on the device beside it) and the last batch's walk (no churn beside
+        # it) -- ~2-4 ms of fill and drain, 0.2-0.4 ms per step over 10
+        # steps, ~0.1 over 30 (the device runs back to back in between:
+        # profiles/r06/s3/c5_k1000_timeline.txt)
+        out["c5"] = {f"k{k}": c5_leg(k, 30, 10_000, args.topics, device=local) for k in (100, 10, 1000)}
         out["parity_sample_ok"] = bool(out.get("parity_sample_ok", True)
                                        and all(v.get("parity_sample_ok") for v in out["c5"].values()))
 
