@@ -584,6 +584,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     rows, delivered = [], []
     ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
     g0 = eng.stats()["graph_launches"]
+    cg0 = cgroup_cpu_stat()
     t0 = time.perf_counter()
     tc = time.perf_counter()
     Churn.apply(eng, *deltas[0])
@@ -617,6 +618,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         rows.append(st["topics"])
         delivered.append(st["delivered"])
     elapsed = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
     if sync is not None:
         sync.barrier()
         elapsed = sync.allmax(elapsed)
@@ -650,6 +652,10 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         "uploads_delta": eng.stats()["uploads_delta"],
         # timed launches replayed as a captured HIP graph
         "graph_launches": graph_launches,
+        # CFS quota throttling of the process over the timed steps, and the
+        # CPU time it used (cgroup cpu.stat): the churn runs on the box's
+        # 16-CPU share
+        "cgroup": {k: cg1[k] - cg0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "usage_usec") if k in cg1},
     }
     if selfcheck:
         out["selfcheck"] = c5_selfcheck(eng, bs[last], batches[last], derived, allf, churn.live_set, added)
@@ -699,6 +705,17 @@ def run_c5(args, ws, rank, local, sync):
 COALESCE_LEGS = (("async", 1, 8, 256), ("async_4096", 1, 16, 256), ("sync", 0, 64, 1))
 
 
+def cgroup_cpu_stat() -> dict:
+    """The process's cgroup CPU accounting (cgroup v2 cpu.stat; {} if absent):
+    nr_throttled / throttled_usec tell whether the box's CFS quota paused the
+    whole process during a leg (a multi-ms stall every thread sees)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if len(ln.split()) == 2)}
+    except (OSError, ValueError):
+        return {}
+
+
 def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
     """Per-publish emqx_trie:match/1 calls through the drop-in boundary, driven
     by the native load generator (emqx_amd/csrc/tm_load.cpp): legs = (name,
@@ -717,7 +734,9 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
         # per size class, milliseconds each), not inside the timed calls
         LD.run(eng, topics.slice(0, min(max(20_000, 8 * th * win), len(topics))), mode, th, win, hashes=False)
         b0 = eng.async_stats()
+        c0 = cgroup_cpu_stat()
         st, counts, hashes = LD.run(eng, sub, mode, th, win)
+        c1 = cgroup_cpu_stat()
         b1 = eng.async_stats()
         ok = (st["errors"] == 0 and np.array_equal(counts.astype(np.int64), exp_c[:cnt])
               and np.array_equal(hashes, exp_h[:cnt]))
@@ -729,7 +748,10 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
                      "mean_batch": (b1["requests"] - b0["requests"]) / nb,
                      "recoveries": b1["recoveries"] - b0["recoveries"],
                      "host_us_per_batch": {k: (b1[k] - b0[k]) / nb for k in ("us_launch", "us_wait", "us_deliver")},
-                     "inline_launches": b1["inline_launches"] - b0["inline_launches"]}
+                     "inline_launches": b1["inline_launches"] - b0["inline_launches"],
+                     # CFS quota throttling of the process during the leg (cgroup cpu.stat)
+                     "cgroup_throttled": {k: c1[k] - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec")
+                                          if k in c1}}
         log(f"[coalesce] {name}: {out[name]}")
     return out
 
