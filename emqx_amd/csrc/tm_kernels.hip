@@ -542,8 +542,12 @@ __device__ __forceinline__ void match_tile(const MatchArgs& a, LT& L, uint32_t t
         }
         uint4 res = uint4{0u, 0u, 0u, 0u};
         if (has) res = L.q[idx];
-        const bool found = has && res.z >= Q_FOUND;
-        const bool cont = has && !found && res.w != Q_TAIL && disp < a.max_probe;
+        // a row already longer than K goes to the generic path whole: its
+        // entries are not expanded further (C5 K = 1000: ~10k rows of ~1,000
+        // matches each stopped at K + 1 instead of walked to the end)
+        const bool gone = has && L.cnt[tl] > a.row_cap;
+        const bool found = has && !gone && res.z >= Q_FOUND;
+        const bool cont = has && !gone && !found && res.w != Q_TAIL && disp < a.max_probe;
         Node s;
         s.child = 0; s.term = NONE; s.hterm = NONE; s.flags = 0;
         if (found) {
