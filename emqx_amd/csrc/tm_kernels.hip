@@ -816,13 +816,15 @@ __device__ void bitonic(const MatchArgs& a, unsigned long long* kp, uint32_t* fp
 }
 
 // Generic path LDS: the probe stack while a topic is walked (SLOW_SQ 16-B
-// entries {parent, meta, key lo, key hi}), then the same 16 KB as the row's
-// sort area: 2,048 u64 (path code | filter id) or 4,096 u32 filter ids (rows
-// ordered by bytes).  A LIFO stack popped 64 at a time grows by at most 64
-// entries per level, so 1,024 holds a 10-level topic's whole frontier; a
-// deeper or wider one restarts in global scratch.
+// entries {parent, meta, key lo, key hi}), then the same 8 KB as the row's
+// sort area: 1,024 u64 (path code | filter id) or 2,048 u32 filter ids (rows
+// ordered by bytes); a path-coded row of up to 2,048 sorts as two LDS runs
+// merged on the way out (merge_runs_out).  A topic whose frontier outgrows the
+// stack restarts in global scratch.  The walk is a chain of dependent probes
+// per row, so the waves per CU set its pace: 8 KB of LDS per wave allows 20
+// (16 KB: 10).
 #ifndef TM_SLOW_SQ
-#define TM_SLOW_SQ 1024
+#define TM_SLOW_SQ 512
 #endif
 constexpr uint32_t SLOW_SQ = TM_SLOW_SQ;
 constexpr uint32_t SORT_LDS = SLOW_SQ * 2;    // u64 entries of the sort area
@@ -867,6 +869,34 @@ __device__ void bitonic_lds_bytes(const MatchArgs& a, uint32_t* f, uint32_t n) {
             }
             __syncthreads();
         }
+    }
+}
+
+// A row of on (SORT_LDS < on <= 2 * SORT_LDS) path-coded entries whose first
+// SORT_LDS, sorted, are back in okey[] (global scratch, as code | id) and the
+// rest, sorted, in sk[0, nb) (LDS): every entry's place in the merged row is
+// its index in its own run plus its rank in the other (a binary search: the
+// keys are distinct, as a row's filter ids are), and its id goes there.
+__device__ __forceinline__ void merge_runs_out(const unsigned long long* A, const unsigned long long* sk, uint32_t nb,
+                                               uint32_t* out) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < SORT_LDS; i += 64) {   // run A: rank in B (LDS)
+        const unsigned long long x = A[i];
+        uint32_t lo = 0, hi = nb;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (sk[m] < x) lo = m + 1; else hi = m;
+        }
+        out[i + lo] = (uint32_t)(x & ~KEY_MASK);
+    }
+    for (uint32_t j = lane; j < nb; j += 64) {         // run B: rank in A (global)
+        const unsigned long long x = sk[j];
+        uint32_t lo = 0, hi = SORT_LDS;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (A[m] < x) lo = m + 1; else hi = m;
+        }
+        out[j + lo] = (uint32_t)(x & ~KEY_MASK);
     }
 }
 
@@ -1001,8 +1031,26 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
         uint32_t np2 = 1;
         while (np2 < on) np2 <<= 1;
         bool sorted_in_lds = false;
+        uint32_t two_runs = 0;   // > 0: sorted as two runs, the second this long (merge_runs_out)
         if (on > 1) {
-            if (!by_bytes && np2 <= SORT_LDS) {
+            if (!by_bytes && np2 > SORT_LDS && on <= 2 * SORT_LDS) {
+                // run A: the first SORT_LDS entries, sorted in LDS, back to okey[]
+                for (uint32_t i = lane; i < SORT_LDS; i += 64) sk[i] = okey[i] | ofid[i];
+                __syncthreads();
+                bitonic_lds64(sk, SORT_LDS);
+                for (uint32_t i = lane; i < SORT_LDS; i += 64) okey[i] = sk[i];
+                __threadfence_block();
+                __syncthreads();
+                // run B: the rest, sorted in LDS where it stays
+                const uint32_t nb = on - SORT_LDS;
+                uint32_t nb2 = 1;
+                while (nb2 < nb) nb2 <<= 1;
+                for (uint32_t i = lane; i < nb2; i += 64)
+                    sk[i] = i < nb ? (okey[SORT_LDS + i] | ofid[SORT_LDS + i]) : ~0ull;
+                __syncthreads();
+                if (nb2 > 1) bitonic_lds64(sk, nb2);
+                two_runs = nb;
+            } else if (!by_bytes && np2 <= SORT_LDS) {
                 // (path codes use bits 31..63, filter ids < 2^30: one u64
                 // orders by code, then id)
                 for (uint32_t i = lane; i < np2; i += 64) sk[i] = i < on ? (okey[i] | ofid[i]) : ~0ull;
@@ -1033,7 +1081,10 @@ __global__ __launch_bounds__(64) void tm_match_slow(MatchArgs a) {
         base = __shfl(base, 0, 64);
         const bool fits = base + on <= a.rcap;
         base += (uint64_t)g * a.rcap;
-        if (fits) {
+        if (fits && two_runs) {
+            (void)CK_(base + on - 1, a.sfids_cap, 30);
+            merge_runs_out(okey, sk, two_runs, a.sfids + base);
+        } else if (fits) {
             for (uint32_t i = lane; i < on; i += 64) {
                 const uint32_t f = !sorted_in_lds ? ofid[i] : by_bytes ? sfi[i] : (uint32_t)(sk[i] & ~KEY_MASK);
                 a.sfids[CK_(base + i, a.sfids_cap, 30)] = f;

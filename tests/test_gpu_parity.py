@@ -243,9 +243,10 @@ def test_forced_slow_path_parity():
 def test_long_rows_every_generic_sort(slow_lds):
     """Rows far past the fast path's K go to the generic path, whose probe
     stack lives in LDS (TM_SLOW_LDS=2: every topic outgrows it and walks again
-    in global scratch) and whose sort runs in LDS up to 2,048 path-coded
-    matches or 4,096 byte-ordered ones, in global scratch beyond: topics with
-    ~1,000, ~1,500, ~3,000 (depth 10) and ~6,000 (depth 11, ordered by bytes)
+    in global scratch) and whose sort runs in LDS up to 1,024 path-coded
+    matches (as two LDS runs merged on the way out up to 2,048) or 2,048
+    byte-ordered ones, in global scratch beyond: topics with ~1,000, ~1,300,
+    ~2,600 (depth 10), ~2,000 (depth 11, ordered by bytes) and ~10,000
     matches, beside ordinary ones."""
     import itertools
     F = set()
@@ -271,8 +272,9 @@ def test_long_rows_every_generic_sort(slow_lds):
     eng.insert_many(F)
     eng.sync()
     exp, _ = oracle_rows(F, T)
-    # path-coded rows sorted in LDS (np2 2,048) and in global scratch (4,096);
-    # by bytes (deeper than 10 levels) in LDS (4,096) and in global scratch
+    # path-coded rows sorted as two LDS runs (1,029 and 1,282 entries) and
+    # in global scratch (2,563); by bytes (deeper than 10 levels) in global
+    # scratch (2,054 and 10,245)
     assert [len(r) for r in exp[:5]] == [1029, 1282, 2563, 2054, 10245]
     assert_same(T, engine_rows(eng, T), exp)
 
