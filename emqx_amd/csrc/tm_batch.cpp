@@ -488,6 +488,7 @@ int tm_engine::reserve_dedup(tm_batch* b, uint64_t nbytes) {
     if ((rc = dev_reserve(b->d_dtab, b->c_dtab, cap))) return rc;
     if (b->d_dtab != old_tab || old_mask != b->dtab_mask) b->dtab_dirty = true;
     if ((rc = dev_reserve(b->d_dsrow, b->c_dsrow, cap))) return rc;
+    if ((rc = dev_reserve(b->d_dsmeta, b->c_dsmeta, cap))) return rc;
     if ((rc = dev_reserve(b->d_drrep, b->c_drrep, std::max<size_t>(n, 1)))) return rc;
     if ((rc = dev_reserve(b->d_dbsum, b->c_dbsum, n / DD_EXPAND_TILE + 2))) return rc;   // (expansion blocks)
     if ((rc = dev_reserve(b->d_dslot, b->c_dslot, std::max<size_t>(n, 1)))) return rc;
@@ -516,6 +517,7 @@ DedupArgs tm_engine::dedup_args(tm_batch* b) const {
     d.table = b->d_dtab; d.mask = b->dtab_mask;
     d.slot = b->d_dslot; d.repbits = b->d_dbits; d.bcount = b->d_dbc; d.bbytes = b->d_dbb;
     d.rbs = b->d_drbs; d.bbs = b->d_dbbs; d.srow = b->d_dsrow; d.rrep = b->d_drrep;
+    d.smeta = b->d_dsmeta;
     d.row_of = b->d_rowof; d.cbytes = b->d_cbytes; d.coffs = b->d_coffs; d.dd = b->d_dd;
     d.ctrl = b->d_ctrl; d.count = b->d_count; d.src = b->d_src; d.pcount = b->d_pcount; d.psrc = b->d_psrc;
     d.stats = b->d_stats;

@@ -508,6 +508,8 @@ struct tm_batch {
     unsigned long long *d_dtab = nullptr, *d_psrc = nullptr, *d_dbits = nullptr;
     uint32_t *d_dslot = nullptr, *d_dbc = nullptr, *d_dbb = nullptr, *d_drbs = nullptr, *d_dbbs = nullptr;
     uint32_t *d_dsrow = nullptr, *d_drrep = nullptr;
+    uint4* d_dsmeta = nullptr;
+    size_t c_dsmeta = 0;
     unsigned long long* d_dbsum = nullptr;
     size_t c_dbsum = 0;
     uint32_t *d_rowof = nullptr, *d_dd = nullptr, *d_pcount = nullptr;
@@ -612,8 +614,8 @@ struct tm_batch {
             *h = nullptr;
         }
         dev_free(d_nslow);
-        dev_free(d_drrep); dev_free(d_dbsum);
-        c_drrep = c_dbsum = 0;
+        dev_free(d_drrep); dev_free(d_dbsum); dev_free(d_dsmeta);
+        c_drrep = c_dbsum = c_dsmeta = 0;
         dev_free(d_dtab); dev_free(d_psrc); dev_free(d_dsrow); dev_free(d_dbits); dev_free(d_dslot); dev_free(d_dbc);
         dev_free(d_dbb); dev_free(d_drbs); dev_free(d_dbbs); dev_free(d_rowof); dev_free(d_dd); dev_free(d_pcount);
         dev_free(d_cbytes); dev_free(d_coffs);

@@ -574,9 +574,11 @@ uint32_t tok_tile_topics(uint32_t n, uint64_t nbytes);
 //   (two scans of the block sums)
 //   compact  each representative: its row, its bytes into cbytes, coffs,
 //            srow[slot] = row and rrep[row] = the representative
-//   expand   (after the walk) every publish's (count, start) through
-//            srow[slot[t]]; the representative clears its table slot, so the
-//            table is zero for the next pass (row_of[t] = srow[slot[t]] is
+//   rowmeta  (after the walk) each row's (count, start) into smeta at its
+//            slot, and the slot cleared, so the table is zero for the next
+//            pass
+//   expand   every publish's (count, start) from smeta[slot[t]]: two
+//            dependent reads instead of three (row_of[t] = srow[slot[t]] is
 //            built only when the host asks for it)
 struct DedupArgs {
     const uint8_t* bytes;     // the batch's publishes: bytes[offs[t] - base .. offs[t + 1] - base)
@@ -595,6 +597,7 @@ struct DedupArgs {
     uint32_t* srow;           // mask + 1: per claimed slot, its row
     uint32_t* rrep;           // n: per row, its representative publish
     uint32_t* row_of;         // n: row of each publish (tm_dedup_rowof, when the host asks)
+    uint4* smeta;             // mask + 1: per claimed slot, its row's (count, 0, start lo, start hi)
     uint8_t* cbytes;          // the rows' bytes, the tokeniser's input (16-B aligned, + 32 bytes of slack)
     uint64_t* coffs;          // rows + 1 offsets into cbytes
     uint32_t* dd;             // [0] rows: the tokeniser's and the walk's topic count (TokArgs / MatchArgs d_n)

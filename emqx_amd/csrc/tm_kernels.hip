@@ -2153,44 +2153,46 @@ __global__ __launch_bounds__(256) void tm_dedup_compact(DedupArgs a) {
     }
 }
 
-// After the walk: every publish gets its row's (count, start) -- the result
-// per publish -- and the batch's delivered matches are summed per block.  A representative clears its table slot
-// (nothing reads the table after the compaction): the next dedup pass finds
-// it zero without a memset.
+// After the walk, per row (a grid-stride loop over the device-counted rows):
+// its (count, start) go to smeta at its table slot, and the slot is cleared
+// (nothing reads the table after the compaction): the next dedup pass finds it
+// zero without a memset.
+__global__ __launch_bounds__(256) void tm_dedup_rowmeta(DedupArgs a) {
+    const uint32_t rows = *a.dd;
+    for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < rows; r += gridDim.x * 256) {
+        const uint32_t s = a.slot[a.rrep[r]];
+        const unsigned long long sr = a.src[r];
+        a.smeta[s] = uint4{a.count[r], 0u, (uint32_t)sr, (uint32_t)(sr >> 32)};
+        a.table[s] = 0;
+    }
+}
+
+// Then every publish gets its row's (count, start) -- the result per publish
+// -- through its slot: slot[t], then smeta[slot] (the hot topics' entries
+// stay in L2), and the batch's delivered matches are summed per block.
 constexpr uint32_t EXPAND_PER_THREAD = DD_EXPAND_TILE / 256;
 __global__ __launch_bounds__(256) void tm_dedup_expand(DedupArgs a) {
     __shared__ unsigned long long sh[4];
     const uint32_t base = blockIdx.x * 256 * EXPAND_PER_THREAD + threadIdx.x;
-    // staged: every slot, then every slot's row, then every row's count,
-    // start and representative -- each stage's loads in flight together
-    uint32_t sl[EXPAND_PER_THREAD], r[EXPAND_PER_THREAD];
+    // staged: every slot, then every slot's (count, start) -- each stage's
+    // loads in flight together
+    uint32_t sl[EXPAND_PER_THREAD];
 #pragma unroll
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const uint32_t t = base + u * 256;
         sl[u] = t < a.n ? a.slot[t] : 0u;
     }
+    uint4 m[EXPAND_PER_THREAD];
 #pragma unroll
-    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) r[u] = base + u * 256 < a.n ? a.srow[sl[u]] : 0u;
-    uint32_t c[EXPAND_PER_THREAD], rep[EXPAND_PER_THREAD];
-    unsigned long long sr[EXPAND_PER_THREAD];
-#pragma unroll
-    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
-        const bool in = base + u * 256 < a.n;
-        c[u] = in ? a.count[r[u]] : 0u;
-        sr[u] = in ? a.src[r[u]] : 0ull;
-        rep[u] = in ? a.rrep[r[u]] : NONE;
-    }
+    for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) m[u] = base + u * 256 < a.n ? a.smeta[sl[u]] : uint4{0u, 0u, 0u, 0u};
     unsigned long long sum = 0;
 #pragma unroll
     for (uint32_t u = 0; u < EXPAND_PER_THREAD; ++u) {
         const uint32_t t = base + u * 256;
         if (t < a.n) {
-            // the representative clears its slot (nothing reads the table
-            // after the compaction): the next pass finds it zero
-            if (rep[u] == t) a.table[sl[u]] = 0;
-            a.pcount[t] = c[u];
-            a.psrc[t] = sr[u];
-            sum += c[u];
+            a.pcount[t] = m[u].x;
+            a.psrc[t] = ((unsigned long long)m[u].w << 32) | m[u].z;
+            sum += m[u].x;
         }
     }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
@@ -3181,6 +3183,9 @@ hipError_t launch_dedup_rowof(const DedupArgs& a, hipStream_t s) {
 
 hipError_t launch_dedup_expand(const DedupArgs& a, hipStream_t s) {
     const uint32_t g = (a.n + 256 * EXPAND_PER_THREAD - 1) / (256 * EXPAND_PER_THREAD);
+    // (the rows are counted on the device: a grid for the bound, strided)
+    const uint32_t gr = std::min<uint32_t>(2048, (a.n + 255) / 256);
+    if (gr) hipLaunchKernelGGL(tm_dedup_rowmeta, dim3(gr), dim3(256), 0, s, a);
     if (g) hipLaunchKernelGGL(tm_dedup_expand, dim3(g), dim3(256), 0, s, a);
     hipLaunchKernelGGL(tm_dedup_sum, dim3(1), dim3(1024), 0, s, a, g);   // (also reports the rows)
     return hipGetLastError();
