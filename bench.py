@@ -731,8 +731,10 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
         sub = topics if cnt == len(topics) else topics.slice(0, cnt)
         # untimed warm-up at the leg's own concurrency: the batch sizes it
         # forms get their slot graphs captured here (a one-time setup cost
-        # per size class, milliseconds each), not inside the timed calls
-        LD.run(eng, topics.slice(0, min(max(20_000, 8 * th * win), len(topics))), mode, th, win, hashes=False)
+        # per size class and slot, milliseconds each), not inside the timed
+        # calls.  (20k calls left some slot / size-class pairs to the timed
+        # run: 9-29 ms max latencies with no CPU throttling, round 6)
+        LD.run(eng, topics.slice(0, min(max(200_000, 8 * th * win), len(topics))), mode, th, win, hashes=False)
         b0 = eng.async_stats()
         c0 = cgroup_cpu_stat()
         st, counts, hashes = LD.run(eng, sub, mode, th, win)
