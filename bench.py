@@ -582,6 +582,16 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         deltas.append((gen.Strings.from_list(dels), gen.Strings.from_list(adds)))
     ms_dev, ms_queue, ms_churn = [], [], []
     rows, delivered = [], []
+
+    def collect(bb):
+        st = bb.stats()
+        # a graph replay times its whole span (reported as its walk), a direct
+        # launch each phase: their sum is the launch's device time either way
+        ms_dev.append(st["ms_tokenize"] + st["ms_dedup"] + st["ms_total"])
+        ms_queue.append(st["ms_queue"])
+        rows.append(st["topics"])
+        delivered.append(st["delivered"])
+
     ms_host = {"sync_async": [], "wait": [], "launch": []}   # the step's host time beside the churn
     g0 = eng.stats()["graph_launches"]
     cg0 = cgroup_cpu_stat()
@@ -610,14 +620,13 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
         b.wait()
         if i + 1 < steps:   # (the last step's wait is the device's tail, no churn beside it)
             ms_host["wait"].append(1e3 * (time.perf_counter() - tc))
-        st = b.stats()
-        # a graph replay times its whole span (reported as its walk), a direct
-        # launch each phase: their sum is the launch's device time either way
-        ms_dev.append(st["ms_tokenize"] + st["ms_dedup"] + st["ms_total"])
-        ms_queue.append(st["ms_queue"])
-        rows.append(st["topics"])
-        delivered.append(st["delivered"])
     elapsed = time.perf_counter() - t0
+    # the device times, rows and deliveries of the rotated batches' last
+    # launches, read after the timed region: a batch's stats (event times)
+    # read after every wait sat on the churn's critical path (~0.1 ms of host
+    # time per step), and a relaunch overwrites them
+    for j in range(max(0, steps - n_batches), steps):
+        collect(bs[j % n_batches])
     cg1 = cgroup_cpu_stat()
     if sync is not None:
         sync.barrier()
@@ -629,7 +638,7 @@ def c5_leg(k, steps, n_deltas, n_topics, device=0, seed=5, sync=None, warmup=2, 
     sp = np.median(np.array(split), 0).tolist() if split else [0.0] * 5
     out = {
         "k": k, "publishes_per_s": n * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "steps": steps,
-        "distinct_topics_per_s": float(np.sum(rows)) / elapsed,
+        "distinct_topics_per_s": float(np.mean(rows)) * steps / elapsed,
         "batches": n_batches, "dedup_tokenise_walk_expand_every_step": True,
         # the rotated batches' bytes were uploaded before timing (prepare_ms
         # per batch, host copy + H2D): the timed rate is HBM-resident input
