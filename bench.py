@@ -743,6 +743,8 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
         # per size class and slot, milliseconds each), not inside the timed
         # calls.  (20k calls left some slot / size-class pairs to the timed
         # run: 9-29 ms max latencies with no CPU throttling, round 6)
+        if mode == 1:   # (and a burst of large batches first: every slot's largest size class)
+            LD.run(eng, topics.slice(0, min(200_000, len(topics))), mode, 8, 2048, hashes=False)
         LD.run(eng, topics.slice(0, min(max(200_000, 8 * th * win), len(topics))), mode, th, win, hashes=False)
         b0 = eng.async_stats()
         c0 = cgroup_cpu_stat()
@@ -754,7 +756,8 @@ def coalesce_legs(eng, topics, legs, exp_c=None, exp_h=None) -> dict:
         nb = max(b1["batches"] - b0["batches"], 1)
         out[name] = {"calls_per_s": cnt / st["seconds"], "calls": cnt, "threads": th, "outstanding_per_thread": win,
                      "in_flight": th * win, "p50_us": st["p50_us"], "p99_us": st["p99_us"], "mean_us": st["mean_us"],
-                     "max_us": st["max_us"], "rows_equal_batch_path": bool(ok),
+                     "max_us": st["max_us"], "max_at_s": st["max_at_s"], "seconds": st["seconds"],
+                     "rows_equal_batch_path": bool(ok),
                      "batches": b1["batches"] - b0["batches"],
                      "mean_batch": (b1["requests"] - b0["requests"]) / nb,
                      "recoveries": b1["recoveries"] - b0["recoveries"],

@@ -32,6 +32,7 @@ typedef struct {
     uint64_t calls;       // calls completed
     uint64_t errors;      // calls that returned an error
     double mean_us, p50_us, p99_us, max_us;   // per-call latency
+    double max_at_s;      // when the slowest call was submitted, seconds into the run (async mode; -1 otherwise)
 } tml_result;
 }
 
@@ -191,6 +192,11 @@ __attribute__((visibility("default"))) int tml_run(tm_engine* e, const uint8_t* 
     out->seconds = std::chrono::duration<double>(clk::now() - t0).count();
     out->calls = n;
     out->errors = sh.errors.load();
+    out->max_at_s = -1;
+    if (n && mode == 1) {
+        const size_t im = (size_t)(std::max_element(lat.begin(), lat.begin() + n) - lat.begin());
+        out->max_at_s = std::chrono::duration<double>(calls[im].t0 - t0).count();
+    }
     std::vector<float> s(lat.begin(), lat.begin() + n);
     double sum = 0;
     for (float v : s) sum += v;

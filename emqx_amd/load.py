@@ -18,7 +18,8 @@ SYNC, ASYNC = 0, 1
 
 class TmlResult(C.Structure):
     _fields_ = [("seconds", C.c_double), ("calls", C.c_uint64), ("errors", C.c_uint64), ("mean_us", C.c_double),
-                ("p50_us", C.c_double), ("p99_us", C.c_double), ("max_us", C.c_double)]
+                ("p50_us", C.c_double), ("p99_us", C.c_double), ("max_us", C.c_double),
+                ("max_at_s", C.c_double)]
 
     def asdict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
