@@ -151,7 +151,7 @@ int tm_engine::upload_to(Replica& R, bool slots_full, bool keys_full, size_t nn,
                          (dev_tok && (R.d_dict_n != dict.keys().size() || R.c_tail < dict.tails().size() + 1 ||
                                       R.c_arena < dict.arena().size() + 1));
     for (tm_batch* r : R.readers)
-        if (r->launched) {
+        if (r->launched && !r->done) {   // (a waited batch has finished reading them)
             if (realloc) {
                 HIP_OK(hipStreamSynchronize(r->own));
                 continue;
