@@ -401,7 +401,7 @@ inline bool device_node_cpus(int device, unsigned need, bool pin, cpu_set_t& out
 using namespace etm_host;
 
 #ifndef TM_SLOW_WAVES_MAX
-#define TM_SLOW_WAVES_MAX 4096   // C5 K=1000 device: 512 waves 7.75 ms, 2048 4.54, 4096 4.03 (round 2, tools/ab_slow.sh); with 8 KB of LDS per wave (round 6) 4096 1.74 ms, 8192 1.90
+#define TM_SLOW_WAVES_MAX 4096   // C5 K=1000 device: 512 waves 7.75 ms, 2048 4.54, 4096 4.03 (round 2, tools/ab_slow.sh); with 8 KB of LDS per wave (round 6) 3072 1.81, 4096 1.66, 5120 1.87, 8192 1.90 (tools/ab_slow_waves.sh)
 #endif
 
 // ===================================================================== batch
